@@ -1,0 +1,155 @@
+/*
+ * ruleset_hip.h — C ABI of libruleset_hip.so, the MI355X (gfx950) hot path of
+ * ruleset-analysis: first-match classification of connection tuples against
+ * ordered access-list rules, fused with the reducer's per-rule aggregation.
+ *
+ * The reference has no native FFI (it is Python-2 Hadoop streaming); each entry
+ * point below replaces a region of the reference's Python loop, cited file:line.
+ * Plain pointers and sizes only: "d_" pointers are device (HBM) pointers owned
+ * by the caller, "h_" pointers are host pointers owned by the caller.  The
+ * library owns only the compiled rule tables and the distinct-connection hash
+ * table behind an rsa_ctx.  Every call returns an int status (RSA_OK or a
+ * negative code) and rsa_last_error(ctx) describes the last failure.  Calls on
+ * one ctx are serialised on the ctx's HIP stream (rsa_set_stream).
+ */
+#ifndef RULESET_HIP_H
+#define RULESET_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RSA_OK 0
+#define RSA_ERR_ARG (-1)      /* bad argument / shape                          */
+#define RSA_ERR_HIP (-2)      /* HIP runtime error                              */
+#define RSA_ERR_STATE (-3)    /* call out of order (e.g. no rules loaded)       */
+#define RSA_ERR_CAPACITY (-4) /* distinct-connection table overflowed           */
+
+/* Tuple flags (rsa_tuple.flags). */
+#define RSA_F_VALID 0x01u /* line parsed and an ACL resolved: classify it     (mapper.py:124-156)  */
+#define RSA_F_HIT 0x02u   /* line contains -6-302013 / -6-302015              (connlist-reducer.py:146) */
+#define RSA_F_BUILT 0x04u /* reducer's BUILT regex matched                   (connlist-reducer.py:152-153) */
+#define RSA_F_SWAP 0x08u  /* reducer key is (dst, src, sport) of the tuple, not (src, dst, dport) */
+
+#define RSA_NO_RULE (-1)
+#define RSA_NO_THRESHOLD 0xFFFFFFFFFFFFFFFFull
+
+/* One packed connection tuple, 16 B (mapper.py:26-51 Connection + the fields the
+ * reducer derives from the same line, connlist-reducer.py:152-165). */
+typedef struct rsa_tuple {
+  uint32_t src;    /* IPv4, host order                                     */
+  uint32_t dst;    /* IPv4, host order                                     */
+  uint16_t sport;  /* source port                                          */
+  uint16_t dport;  /* destination port                                     */
+  uint16_t list;   /* candidate list id = (host, acl, protocol)           */
+  uint8_t flags;   /* RSA_F_*                                              */
+  uint8_t pspell;  /* id of the protocol word as written (e.g. "TCP")      */
+} rsa_tuple;
+
+/* One compiled candidate-list entry, 32 B: an expanded permit rule reduced to
+ * the integer predicate of FirewallRule.__contains__ (firewallrule.py:128-174).
+ * Deny rules and rules whose protocol cannot match the list's protocol are
+ * dropped at compile time (they can never be a connection's first match). */
+typedef struct rsa_rule_entry {
+  uint32_t src_lo, src_span;  /* (src - src_lo) <= src_span: IPy containment, */
+  uint32_t dst_lo, dst_span;  /* net.ip <= x < net.ip + net.len()            */
+  uint32_t port_lo;           /* sport_lo | dport_lo << 16                 */
+  uint32_t port_span;         /* (sport_hi-sport_lo) | (dport_hi-dport_lo) << 16 */
+  uint32_t gid;               /* global rule id = acl base + expanded ruleindex */
+  uint32_t reserved;
+} rsa_rule_entry;
+
+/* One distinct (rule, connection) aggregate, 40 B (connlist-reducer.py:162-176). */
+typedef struct rsa_conn_record {
+  uint64_t min_order; /* smallest order key (first occurrence in sort order) */
+  uint32_t gid;
+  uint32_t for_ip;    /* reducer key FROMIP                                   */
+  uint32_t to_ip;     /* reducer key TOIP                                     */
+  uint16_t to_port;   /* reducer key TOPORT                                   */
+  uint8_t pspell;     /* reducer key PROTO (spelling id)                      */
+  uint8_t pad;
+  uint32_t count;     /* conns[conn]                                          */
+  uint32_t first;     /* connFirst[conn] as an order-isomorphic timestamp code */
+  uint32_t last;      /* connLast[conn]                                       */
+  uint32_t pad2;
+} rsa_conn_record;
+
+typedef struct rsa_ctx rsa_ctx;
+
+/* Context: one per device.  Replaces the per-process setup of mapper.py:79-117
+ * and connlist-reducer.py:32-49 (the rule DB lives in HBM instead). */
+int rsa_ctx_create(int device, rsa_ctx **out);
+int rsa_ctx_destroy(rsa_ctx *ctx);
+const char *rsa_last_error(const rsa_ctx *ctx);
+int rsa_set_stream(rsa_ctx *ctx, void *hip_stream);
+int rsa_version(void);
+
+/* Upload compiled candidate lists (host arrays).  list_offsets has n_lists+1
+ * entries; entries[list_offsets[l] .. list_offsets[l+1]) is list l in ascending
+ * gid order.  Replaces mapper.py:159-166 (candidate list per line).  n_rules is
+ * the number of global rule ids (counter length). */
+int rsa_load_rules(rsa_ctx *ctx, const rsa_rule_entry *h_entries, uint32_t n_entries,
+                   const uint32_t *h_list_offsets, uint32_t n_lists, uint32_t n_rules);
+
+/* Bind caller-owned device counters, each n_rules long (n_rules from
+ * rsa_load_rules, or rsa_set_rule_count when no rules are loaded):
+ *   d_matches  uint64  mapper-emitted lines per rule (blocks exist iff > 0)
+ *   d_hits     uint64  "Total number of hits" (connlist-reducer.py:146-148)
+ *   d_distinct uint32  distinct connections inserted per rule
+ *   d_thresh   uint64  cap threshold P per rule, RSA_NO_THRESHOLD if uncapped */
+int rsa_bind_counters(rsa_ctx *ctx, uint64_t *d_matches, uint64_t *d_hits, uint32_t *d_distinct,
+                      uint64_t *d_thresh);
+int rsa_set_rule_count(rsa_ctx *ctx, uint32_t n_rules);
+
+/* (Re)initialise the distinct-connection table with room for `capacity`
+ * distinct (rule, connection) pairs, zero the bound counters and set the
+ * per-rule cap (config.py:15 MAX_NUMBER_OF_CONNECTIONS_PER_RULE). */
+int rsa_reset(rsa_ctx *ctx, uint64_t capacity, uint32_t cap);
+
+/* Pass 1 — classify + aggregate a batch resident in HBM (mapper.py:123-189 fused
+ * with connlist-reducer.py:62-176).  d_ts: uint32 order-isomorphic timestamp
+ * codes; d_order: uint64 unique order keys isomorphic to the reducer's input
+ * order (LC_ALL=C sort of the line within its key).  d_gid_out (nullable)
+ * receives the first-match gid or RSA_NO_RULE per tuple. */
+int rsa_classify(rsa_ctx *ctx, const rsa_tuple *d_tuples, const uint32_t *d_ts, const uint64_t *d_order,
+                 uint64_t n, int32_t *d_gid_out);
+
+/* Pass 1 with the rule already known per tuple (the reducer drop-in: the key
+ * comes from the mapper's output line, connlist-reducer.py:63-75). */
+int rsa_aggregate_gids(rsa_ctx *ctx, const rsa_tuple *d_tuples, const uint32_t *d_ts, const uint64_t *d_order,
+                       const int32_t *d_gid, uint64_t n);
+
+/* Resolve the cap (connlist-reducer.py:151): for every rule with
+ * distinct >= cap, P = the order key of the line that inserted the cap-th
+ * distinct connection, written to d_thresh.  *h_n_capped receives the number
+ * of capped rules (0 means no recount pass is needed). */
+int rsa_resolve_cap(rsa_ctx *ctx, uint32_t *h_n_capped);
+
+/* Pass 2 — recount occurrences with order <= P for capped rules, per batch.
+ * d_gid may be the d_gid_out of pass 1, or NULL to re-classify. */
+int rsa_recount(rsa_ctx *ctx, const rsa_tuple *d_tuples, const uint32_t *d_ts, const uint64_t *d_order,
+                const int32_t *d_gid, uint64_t n);
+
+/* Emit the final connection tables (connlist-reducer.py:108-126 data) into
+ * d_out (caller device buffer of `max_records`), unordered.  *h_n receives the
+ * number of records; RSA_ERR_CAPACITY if it exceeds max_records. */
+int rsa_emit(rsa_ctx *ctx, rsa_conn_record *d_out, uint64_t max_records, uint64_t *h_n);
+
+/* Multi-GPU merge (replaces the Hadoop shuffle, runAnalysis.sh:42-56).
+ * rsa_export: every table entry with its pass-1 (which=0) or pass-2 (which=1)
+ * aggregates; rsa_import: merge such records into this ctx's table (which=0:
+ * insert-or-combine; which=1: combine into the pass-2 fields of existing keys). */
+int rsa_table_size(rsa_ctx *ctx, uint64_t *h_n);
+int rsa_export(rsa_ctx *ctx, int which, rsa_conn_record *d_out, uint64_t max_records, uint64_t *h_n);
+int rsa_import(rsa_ctx *ctx, int which, const rsa_conn_record *d_in, uint64_t n);
+
+/* Synchronise the ctx stream (tests, host hand-off). */
+int rsa_sync(rsa_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RULESET_HIP_H */

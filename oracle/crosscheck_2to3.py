@@ -1,0 +1,183 @@
+"""ORACLE (test infrastructure only) — pin the oracle against the reference itself.
+
+Run in the build container only (``/root/reference`` does not exist on the GPU
+box).  For each fixture case it:
+
+1. converts the reference's ``mapper.py``, ``connlist-reducer.py``,
+   ``firewallrule.py`` and ``config.py`` with ``lib2to3`` into a scratch
+   directory under /tmp (the converted code is never written into the repo);
+2. adds two shims next to them: ``IPy.py`` (this oracle's ``ipy`` restatement —
+   IPy itself is not installed) and ``libfwregex.py`` (this oracle's
+   ``get_builtconn`` — the ``lib/fw-regex`` submodule is absent);
+3. builds ``accesslists.db`` with Python 3 ``shelve`` from the converted
+   ``FirewallRule`` class, sets the cap in ``config.py``;
+4. runs ``mapred_input_dir=/x/<host>/y python3 mapper.py < log | LC_ALL=C sort |
+   python3 connlist-reducer.py`` exactly as SURVEY.md §3.1's no-Hadoop form;
+5. checks the oracle (``oracle.pipeline``) gives the same mapper text and the
+   same reducer text, and writes the case under ``tests/golden/<case>/``:
+   ``db.json`` (input), ``log.txt`` (input), ``params.json``,
+   ``mapper.sha256`` and ``report.txt`` (outputs of the converted reference).
+
+Usage: ``python3 oracle/crosscheck_2to3.py [--cases NAME ...]``.
+"""
+
+import argparse
+import hashlib
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+REF = '/root/reference'
+GOLDEN = os.path.join(REPO, 'tests', 'golden')
+
+sys.path.insert(0, REPO)
+
+
+def _convert(src, dst):
+    shutil.copy(src, dst)
+    subprocess.run([sys.executable, '-m', 'lib2to3', '-w', '-n', '--no-diffs', dst], check=True,
+                   stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+
+
+BUILD_DB = r'''
+import json, shelve, sys
+from firewallrule import FirewallRule
+dbj = json.load(open(sys.argv[1]))
+acls = {}
+for h, a in dbj['accesslists'].items():
+    acls[h] = {}
+    for name, e in a.items():
+        rules = []
+        for r in e['rules']:
+            rule = FirewallRule(r['action'], r['protocol'], r['original'], r['src'], r['dst'],
+                                list(r['sport']), list(r['dport']))
+            rule.comments = list(r['comments']); rule.rulenum = r['rulenum']; rule.ruleindex = r['ruleindex']
+            rules.append(rule)
+        acls[h][name] = {'rules': rules, 'protocols': {p: list(v) for p, v in e['protocols'].items()},
+                         'timestamp': e['timestamp']}
+db = shelve.open('accesslists.db')
+db['firewalls'] = dbj['firewalls']
+db['accesslists'] = acls
+db.close()
+'''
+
+
+def run_reference(work, db_json, log_text, host, cap):
+    os.makedirs(work, exist_ok=True)
+    for name in ('mapper.py', 'connlist-reducer.py', 'firewallrule.py', 'config.py'):
+        _convert(os.path.join(REF, name), os.path.join(work, name))
+    with open(os.path.join(work, 'config.py')) as f:
+        cfg = f.read()
+    cfg = cfg.replace('MAX_NUMBER_OF_CONNECTIONS_PER_RULE = 1000', 'MAX_NUMBER_OF_CONNECTIONS_PER_RULE = %d' % cap)
+    with open(os.path.join(work, 'config.py'), 'w') as f:
+        f.write(cfg)
+    shutil.copy(os.path.join(HERE, 'ipy.py'), os.path.join(work, 'IPy.py'))
+    shutil.copy(os.path.join(HERE, 'fwregex.py'), os.path.join(work, 'libfwregex.py'))
+    with open(os.path.join(work, 'db.json'), 'w') as f:
+        json.dump(db_json, f)
+    with open(os.path.join(work, 'build_db.py'), 'w') as f:
+        f.write(BUILD_DB)
+    env = dict(os.environ, PYTHONIOENCODING='latin-1', LC_ALL='C', PYTHONHASHSEED='0')
+    subprocess.run([sys.executable, 'build_db.py', 'db.json'], cwd=work, check=True, env=env)
+    with open(os.path.join(work, 'log.txt'), 'w', encoding='latin-1', newline='') as f:
+        f.write(log_text)
+    env['mapred_input_dir'] = '/logs/%s/part-0000' % host
+    m = subprocess.run([sys.executable, 'mapper.py'], cwd=work, env=env, stdin=open(os.path.join(work, 'log.txt'), 'rb'),
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+    if m.returncode != 0:
+        raise RuntimeError('reference mapper failed: %s' % m.stderr.decode('latin-1')[-2000:])
+    s = subprocess.run(['sort'], input=m.stdout, stdout=subprocess.PIPE, env=env, check=True)
+    r = subprocess.run([sys.executable, 'connlist-reducer.py'], cwd=work, env=env, input=s.stdout,
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+    if r.returncode != 0:
+        raise RuntimeError('reference reducer failed: %s' % r.stderr.decode('latin-1')[-2000:])
+    return m.stdout.decode('latin-1'), r.stdout.decode('latin-1')
+
+
+def oracle_db(dbj):
+    from oracle.firewallrule import FirewallRule
+    acls = {}
+    for h, a in dbj['accesslists'].items():
+        acls[h] = {}
+        for name, e in a.items():
+            rules = []
+            for r in e['rules']:
+                rule = FirewallRule(r['action'], r['protocol'], r['original'], r['src'], r['dst'], list(r['sport']),
+                                    list(r['dport']), comments=list(r['comments']), rulenum=r['rulenum'],
+                                    ruleindex=r['ruleindex'])
+                rules.append(rule)
+            acls[h][name] = {'rules': rules, 'protocols': {p: list(v) for p, v in e['protocols'].items()},
+                             'timestamp': e['timestamp']}
+    return acls, dbj['firewalls']
+
+
+def cases():
+    import rsa_pkg
+    rsa_pkg.load()
+    from ruleset_analysis_amd import synth
+
+    def synthetic(seed, n_rules, n_lines, cap, zipf=None, interfaces=('outside',), drop_last_nl=False,
+                  missing_acl=False):
+        db, info = synth.make_db(seed, n_rules, interfaces=interfaces)
+        tr = synth.make_traffic((db, info), n_lines, seed=seed + 100, zipf=zipf)
+        lines = synth.render_lines(tr)
+        if missing_acl:
+            # bind an interface to an ACL absent from the DB (mapper.py:152-156)
+            db['firewalls']['fw1']['dmz'] = {'in': 'dmz_access_in'}
+        text = ''.join(l + '\n' for l in lines)
+        if drop_last_nl:
+            text = text[:-1]
+        return db, text, cap
+
+    yield 'small_200r', lambda: synthetic(1, 200, 3000, 1000)
+    yield 'cap5_zipf', lambda: synthetic(2, 120, 4000, 5, zipf=1.3)
+    yield 'multi_acl', lambda: synthetic(3, 80, 3000, 40, interfaces=('outside', 'partner'), missing_acl=True,
+                                         drop_last_nl=True)
+    yield 'cap1', lambda: synthetic(4, 60, 1500, 1, zipf=1.5)
+    yield 'empty_log', lambda: synthetic(5, 30, 0, 1000)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--cases', nargs='*')
+    args = ap.parse_args()
+    from oracle import pipeline as op
+    if not os.path.isdir(REF):
+        sys.exit('reference not present; this script only runs in the build container')
+    for name, make in cases():
+        if args.cases and name not in args.cases:
+            continue
+        db, text, cap = make()
+        with tempfile.TemporaryDirectory(prefix='rsa_xref_') as work:
+            ref_map, ref_red = run_reference(work, db, text, 'fw1', cap)
+        acls, fws = oracle_db(db)
+        o_map, _srt, o_red, _blocks = op.run_pipeline(text, 'fw1', acls, fws, cap=cap)
+        o_red_text = ''.join(l + '\n' for l in o_red)
+        ok_map = o_map == ref_map
+        ok_red = o_red_text == ref_red
+        print('%-12s lines=%-6d mapper %s reducer %s (%d report lines)' % (
+            name, text.count('\n'), 'OK' if ok_map else 'DIFF', 'OK' if ok_red else 'DIFF', ref_red.count('\n')))
+        if not (ok_map and ok_red):
+            sys.exit('oracle disagrees with the converted reference on case %s' % name)
+        out = os.path.join(GOLDEN, name)
+        os.makedirs(out, exist_ok=True)
+        with open(os.path.join(out, 'db.json'), 'w') as f:
+            json.dump(db, f, sort_keys=True)
+        with open(os.path.join(out, 'log.txt'), 'w', encoding='latin-1', newline='') as f:
+            f.write(text)
+        with open(os.path.join(out, 'report.txt'), 'w', encoding='latin-1', newline='') as f:
+            f.write(ref_red)
+        with open(os.path.join(out, 'mapper.sha256'), 'w') as f:
+            f.write(hashlib.sha256(ref_map.encode('latin-1')).hexdigest() + '\n')
+        with open(os.path.join(out, 'params.json'), 'w') as f:
+            json.dump({'host': 'fw1', 'cap': cap, 'source': 'lib2to3-converted reference, oracle/crosscheck_2to3.py'},
+                      f, sort_keys=True)
+
+
+if __name__ == '__main__':
+    main()

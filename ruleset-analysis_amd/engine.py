@@ -1,0 +1,189 @@
+"""Device orchestration of the hot path on one MI355X.
+
+PyTorch is plumbing here: it owns HBM buffers (tuples, counters, outputs) and
+the HIP stream; every computation happens in ``libruleset_hip.so`` through the
+C ABI (``native.Ctx``).  There is no CPU path: without a GPU or without the
+library, constructing an ``Engine`` raises.
+
+One job = pass 1 (classify + aggregate) over every batch, cap resolution,
+pass 2 over every batch if any rule is capped, then emission of the connection
+tables.  ``Results`` holds the per-rule counters and the connection records.
+"""
+
+import ctypes
+
+import numpy as np
+
+from . import native
+from .compile import RECORD_DTYPE, TUPLE_DTYPE
+
+__all__ = ['Engine', 'Results', 'DeviceBatch']
+
+
+def _torch():
+    import torch
+    return torch
+
+
+class Results(object):
+    def __init__(self, matches, hits, distinct, thresh, records, cap):
+        self.matches = matches      # uint64 [R]
+        self.hits = hits            # uint64 [R]
+        self.distinct = distinct    # uint32 [R]
+        self.thresh = thresh        # uint64 [R] (0xFFFF.. = not capped)
+        self.records = records      # RECORD_DTYPE [M]
+        self.cap = cap
+
+    def capped(self, gid):
+        return int(self.thresh[gid]) != 0xFFFFFFFFFFFFFFFF or (self.cap == 0 and self.matches[gid] > 0)
+
+
+class DeviceBatch(object):
+    """Tuples/timestamps/order keys resident in HBM (torch tensors)."""
+
+    def __init__(self, tuples, ts, order, gids=None):
+        self.tuples = tuples    # uint8 [n*16] or int32 [n,4]
+        self.ts = ts            # int32 [n]  (uint32 codes)
+        self.order = order      # int64 [n]  (uint64 keys)
+        self.gids = gids        # int32 [n] or None
+        self.n = int(ts.numel())
+
+    @classmethod
+    def from_numpy(cls, tuples, ts, order, device, gids=None):
+        torch = _torch()
+        assert tuples.dtype == TUPLE_DTYPE
+        t = torch.from_numpy(np.ascontiguousarray(tuples).view(np.int32).reshape(-1, 4)).to(device)
+        s = torch.from_numpy(np.ascontiguousarray(ts, dtype=np.uint32).view(np.int32)).to(device)
+        o = torch.from_numpy(np.ascontiguousarray(order, dtype=np.uint64).view(np.int64)).to(device)
+        g = None
+        if gids is not None:
+            g = torch.from_numpy(np.ascontiguousarray(gids, dtype=np.int32)).to(device)
+        return cls(t, s, o, g)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+class Engine(object):
+    def __init__(self, device=0):
+        torch = _torch()
+        if not torch.cuda.is_available():
+            raise native.NativeUnavailable('no HIP device visible: the hot path has no CPU fallback')
+        self.torch = torch
+        self.device = torch.device('cuda', device)
+        torch.cuda.set_device(self.device)
+        self.ctx = native.Ctx(device)
+        self.stream = torch.cuda.current_stream(self.device)
+        self.ctx.call('rsa_set_stream', ctypes.c_void_p(self.stream.cuda_stream))
+        self.n_rules = 0
+        self.counters = None
+        self.last_gids = []
+
+    # ---- setup -------------------------------------------------------------------
+    def load_rules(self, entries, offsets, n_rules):
+        entries = np.ascontiguousarray(entries)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint32)
+        self.ctx.call('rsa_load_rules', entries.ctypes.data_as(ctypes.c_void_p), ctypes.c_uint32(len(entries)),
+                      offsets.ctypes.data_as(ctypes.c_void_p), ctypes.c_uint32(len(offsets) - 1),
+                      ctypes.c_uint32(n_rules))
+        self._bind(n_rules)
+
+    def set_rule_count(self, n_rules):
+        self.ctx.call('rsa_set_rule_count', ctypes.c_uint32(n_rules))
+        self._bind(n_rules)
+
+    def _bind(self, n_rules):
+        torch = self.torch
+        n = max(int(n_rules), 1)
+        self.n_rules = int(n_rules)
+        self.counters = {
+            'matches': torch.zeros(n, dtype=torch.int64, device=self.device),
+            'hits': torch.zeros(n, dtype=torch.int64, device=self.device),
+            'distinct': torch.zeros(n, dtype=torch.int32, device=self.device),
+            'thresh': torch.full((n,), -1, dtype=torch.int64, device=self.device),
+        }
+        c = self.counters
+        self.ctx.call('rsa_bind_counters', _ptr(c['matches']), _ptr(c['hits']), _ptr(c['distinct']), _ptr(c['thresh']))
+
+    # ---- the job -----------------------------------------------------------------
+    def reset(self, capacity, cap):
+        self.ctx.call('rsa_reset', ctypes.c_uint64(int(capacity)), ctypes.c_uint32(int(cap)))
+
+    def pass1(self, b, gid_out=None):
+        if b.gids is not None:
+            self.ctx.call('rsa_aggregate_gids', _ptr(b.tuples), _ptr(b.ts), _ptr(b.order), _ptr(b.gids),
+                          ctypes.c_uint64(b.n))
+        else:
+            self.ctx.call('rsa_classify', _ptr(b.tuples), _ptr(b.ts), _ptr(b.order), ctypes.c_uint64(b.n),
+                          _ptr(gid_out))
+
+    def resolve_cap(self):
+        n = ctypes.c_uint32(0)
+        self.ctx.call('rsa_resolve_cap', ctypes.byref(n))
+        return int(n.value)
+
+    def pass2(self, b, gids=None):
+        g = b.gids if b.gids is not None else gids
+        self.ctx.call('rsa_recount', _ptr(b.tuples), _ptr(b.ts), _ptr(b.order), _ptr(g), ctypes.c_uint64(b.n))
+
+    def table_size(self):
+        n = ctypes.c_uint64(0)
+        self.ctx.call('rsa_table_size', ctypes.byref(n))
+        return int(n.value)
+
+    def emit_device(self, mode='final'):
+        """Records as a torch uint8 tensor [M*40] on device."""
+        torch = self.torch
+        size = self.table_size()
+        buf = torch.empty(max(size, 1) * RECORD_DTYPE.itemsize, dtype=torch.uint8, device=self.device)
+        n = ctypes.c_uint64(0)
+        if mode == 'final':
+            self.ctx.call('rsa_emit', _ptr(buf), ctypes.c_uint64(size), ctypes.byref(n))
+        else:
+            which = 0 if mode == 'pass1' else 1
+            self.ctx.call('rsa_export', ctypes.c_int(which), _ptr(buf), ctypes.c_uint64(size), ctypes.byref(n))
+        return buf[: int(n.value) * RECORD_DTYPE.itemsize]
+
+    def import_records(self, buf, which):
+        n = buf.numel() // RECORD_DTYPE.itemsize
+        self.ctx.call('rsa_import', ctypes.c_int(which), _ptr(buf), ctypes.c_uint64(n))
+
+    def results(self, cap):
+        c = self.counters
+        recs = self.emit_device('final')
+        self.torch.cuda.synchronize(self.device)
+        host = recs.cpu().numpy().view(RECORD_DTYPE)
+        R = self.n_rules
+        return Results(c['matches'][:R].cpu().numpy().view(np.uint64), c['hits'][:R].cpu().numpy().view(np.uint64),
+                       c['distinct'][:R].cpu().numpy().view(np.uint32), c['thresh'][:R].cpu().numpy().view(np.uint64),
+                       host.copy(), cap)
+
+    def run(self, batches, cap, capacity, keep_gids=True):
+        """Full single-GPU job over device batches; returns Results."""
+        torch = self.torch
+        self.reset(capacity, cap)
+        gid_bufs = []
+        for b in batches:
+            g = None
+            if b.gids is None and keep_gids:
+                g = torch.empty(b.n, dtype=torch.int32, device=self.device)
+            self.pass1(b, g)
+            gid_bufs.append(g)
+        if self.resolve_cap():
+            for b, g in zip(batches, gid_bufs):
+                self.pass2(b, g)
+        self.last_gids = gid_bufs
+        return self.results(cap)
+
+    def classify_only(self, b):
+        """gid per tuple (mapper drop-in); counters/table are updated as a side effect."""
+        torch = self.torch
+        g = torch.empty(b.n, dtype=torch.int32, device=self.device)
+        self.pass1(b, g)
+        return g
+
+    def close(self):
+        if self.ctx is not None:
+            self.ctx.close()
+            self.ctx = None

@@ -1,0 +1,118 @@
+"""ctypes binding of ``libruleset_hip.so`` (C ABI: ``include/ruleset_hip.h``).
+
+The library is built in-tree (``csrc/Makefile`` or ``__graft_entry__.build()``)
+and loaded from ``ruleset-analysis_amd/_build/libruleset_hip.so`` only.  There
+is no fallback: if the library or a symbol is missing, ``load()`` raises
+``NativeUnavailable`` and every product entry point fails with it.
+"""
+
+import ctypes
+import os
+
+__all__ = ['load', 'lib_path', 'NativeUnavailable', 'NativeError', 'SYMBOLS', 'Ctx']
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_BUILD = os.path.join(_HERE, '_build')
+
+
+def lib_path():
+    return os.environ.get('RSA_HIP_LIB') or os.path.join(_BUILD, 'libruleset_hip.so')
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+class NativeError(RuntimeError):
+    def __init__(self, code, msg):
+        RuntimeError.__init__(self, 'libruleset_hip error %d: %s' % (code, msg))
+        self.code = code
+
+
+RSA_OK, RSA_ERR_ARG, RSA_ERR_HIP, RSA_ERR_STATE, RSA_ERR_CAPACITY = 0, -1, -2, -3, -4
+
+P = ctypes.c_void_p
+U32 = ctypes.c_uint32
+U64 = ctypes.c_uint64
+I32 = ctypes.c_int
+PU32 = ctypes.POINTER(ctypes.c_uint32)
+PU64 = ctypes.POINTER(ctypes.c_uint64)
+
+# name -> (restype, argtypes); exactly the functions declared in include/ruleset_hip.h
+SYMBOLS = {
+    'rsa_version': (I32, []),
+    'rsa_ctx_create': (I32, [I32, ctypes.POINTER(P)]),
+    'rsa_ctx_destroy': (I32, [P]),
+    'rsa_last_error': (ctypes.c_char_p, [P]),
+    'rsa_set_stream': (I32, [P, P]),
+    'rsa_load_rules': (I32, [P, P, U32, P, U32, U32]),
+    'rsa_bind_counters': (I32, [P, P, P, P, P]),
+    'rsa_set_rule_count': (I32, [P, U32]),
+    'rsa_reset': (I32, [P, U64, U32]),
+    'rsa_classify': (I32, [P, P, P, P, U64, P]),
+    'rsa_aggregate_gids': (I32, [P, P, P, P, P, U64]),
+    'rsa_resolve_cap': (I32, [P, PU32]),
+    'rsa_recount': (I32, [P, P, P, P, P, U64]),
+    'rsa_emit': (I32, [P, P, U64, PU64]),
+    'rsa_table_size': (I32, [P, PU64]),
+    'rsa_export': (I32, [P, I32, P, U64, PU64]),
+    'rsa_import': (I32, [P, I32, P, U64]),
+    'rsa_sync': (I32, [P]),
+}
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = lib_path()
+    if not os.path.exists(path):
+        raise NativeUnavailable('libruleset_hip.so not built (%s); run __graft_entry__.build() or make -C '
+                                'ruleset-analysis_amd/csrc' % path)
+    try:
+        lib = ctypes.CDLL(path)
+    except OSError as exc:
+        raise NativeUnavailable('cannot load %s: %s' % (path, exc))
+    for name, (res, args) in SYMBOLS.items():
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            raise NativeUnavailable('%s does not export %s' % (path, name))
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+class Ctx(object):
+    """Owns one rsa_ctx; raises NativeError on any non-zero status."""
+
+    def __init__(self, device=0):
+        self.lib = load()
+        h = P()
+        rc = self.lib.rsa_ctx_create(int(device), ctypes.byref(h))
+        if rc != RSA_OK:
+            raise NativeError(rc, 'rsa_ctx_create(device=%d) failed' % device)
+        self.h = h
+        self.device = device
+
+    def check(self, rc, what):
+        if rc != RSA_OK:
+            msg = self.lib.rsa_last_error(self.h)
+            raise NativeError(rc, '%s: %s' % (what, msg.decode() if msg else ''))
+
+    def call(self, name, *args):
+        self.check(getattr(self.lib, name)(self.h, *args), name)
+
+    def close(self):
+        if self.h:
+            self.lib.rsa_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass

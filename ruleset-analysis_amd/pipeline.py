@@ -1,0 +1,67 @@
+"""The fused job on one GPU: log text -> reducer report, without the
+intermediate mapper text or the sort (the reference's
+``mapper.py | LC_ALL=C sort | connlist-reducer.py``, ``runAnalysis.sh:42-56``).
+
+The output is byte-identical to what the reference pipeline prints for the
+same input (blocks in key byte order, the mapper's blank records turned into
+the reducer's "Unable to unpack" noise pairs first), with connection-table
+ties ordered by first-seen line (SURVEY.md trap 8).
+"""
+
+import numpy as np
+
+from .compile import CompiledRules, F_HIT, F_BUILT
+from .engine import Engine, DeviceBatch
+from .logparse import parse_logs, D_CLASSIFY, D_MISSING
+from .report import reducer_report
+
+__all__ = ['analyze', 'assemble_report', 'built_hit_count']
+
+
+def built_hit_count(tuples):
+    both = F_HIT | F_BUILT
+    return int(np.count_nonzero((tuples['flags'] & both) == both))
+
+
+def assemble_report(parsed, gids, results, compiled, cap):
+    """Reducer stdout lines for parsed lines, their gids and the GPU results."""
+    db = compiled.db
+    groups = []
+    for gid in np.nonzero(results.matches > 0)[0]:
+        gid = int(gid)
+        host, acl, i = compiled.locate(gid)
+        key = '%s;%s;%d' % (host, acl, i)
+        groups.append((key + '\t', gid, host, acl, db.accesslists[host][acl]['rules'][i]))
+    groups.sort(key=lambda g: g[0])
+    disp = parsed.disposition
+    nl = np.array([l.endswith('\n') for l in parsed.lines], dtype=bool) if parsed.n else np.zeros(0, bool)
+    matched = (disp == D_CLASSIFY) & (gids >= 0)
+    n_blank = int(np.count_nonzero(matched & nl))
+    noise = []
+    for i in np.nonzero(disp == D_MISSING)[0]:
+        i = int(i)
+        line = parsed.lines[i]
+        msg = ('Unable to process line because access-list {0} is missing from data structure for host {1}, '
+               'skipping line.'.format(parsed.acl_of[i], parsed.host_of[i]))
+        skipped = 'The skipped line is: ' + (line[:-1] if nl[i] else line)
+        noise.append((msg, msg))
+        noise.append((skipped, skipped))
+        if nl[i]:
+            n_blank += 1
+    return reducer_report(results, groups, noise, cap, lambda c: parsed.ts_table[c], parsed.pspell_table,
+                          n_blank=n_blank)
+
+
+def analyze(inputs, db, cap=1000, device=0, engine=None):
+    """inputs: iterable of (host, lines-with-newlines).  Returns (report lines, results)."""
+    compiled = CompiledRules(db)
+    parsed = parse_logs(inputs, db, compiled)
+    if parsed.error is not None:
+        raise parsed.error[1]
+    eng = engine if engine is not None else Engine(device)
+    ent, off = compiled.packed()
+    eng.load_rules(ent, off, compiled.n_rules)
+    batch = DeviceBatch.from_numpy(parsed.tuples, parsed.ts, parsed.order, eng.device)
+    results = eng.run([batch], cap, capacity=max(built_hit_count(parsed.tuples), 1))
+    gids = eng.last_gids[0].cpu().numpy() if parsed.n else np.zeros(0, np.int32)
+    return assemble_report(parsed, gids, results, compiled, cap), results

@@ -1,0 +1,288 @@
+"""Seeded synthetic rule databases and ASA connection logs.
+
+Nothing here comes from the reference: it ships no logs, configs or fixtures
+(``.gitignore:48-51``).  The generators follow the reference's data shapes:
+
+* ``make_db`` writes what ``preprosess_access_lists.py`` would store for
+  ASA ``access-list NAME extended ...`` lines: each line is expanded to
+  ``|dport| x |dst| x |sport| x |src|`` ``FirewallRule`` records with dport
+  outermost (``preprosess_access_lists.py:256-276``), ``rulenum`` = line number,
+  ``ruleindex`` = list position (``:466-487``), and ``protocols`` maps each
+  protocol to its rule indices (``:489-494``).  Every ACL ends with
+  ``deny ip any any`` so the ``'ip'`` list the mapper indexes unconditionally
+  for tcp/udp (``mapper.py:161,164``) exists.
+* ``make_traffic`` draws connection tuples, mostly inside some permit rule
+  (so the first match is spread over the ACL) plus unmatched noise, and a mix
+  of message forms that exercise the reducer's edge cases: non-hit message ids
+  (``connlist-reducer.py:146``), lines the BUILT regex rejects (``:152``),
+  lines the mapper ignores, interfaces without an ACL (``mapper.py:145-149``)
+  and outbound connections (reducer key swapped relative to the tuple).
+* ``render_lines`` produces the log text; ``pack`` produces the packed tuples
+  directly (what the host parser would produce from that text) for sizes where
+  text is pointless — ``tests/test_synth_pack.py`` pins the two against each
+  other.
+
+All arrays are numpy; generation is vectorised so 10^8-line workloads build in
+seconds.
+"""
+
+import numpy as np
+
+__all__ = ['make_db', 'make_traffic', 'render_lines', 'FORM_NAMES', 'COMMON_PORTS']
+
+COMMON_PORTS = np.array([80, 443, 22, 25, 53, 123, 389, 445, 636, 993, 1433, 3306, 3389, 5432, 8080, 8443],
+                        dtype=np.int64)
+PREFIX_MASKS = {8: '255.0.0.0', 16: '255.255.0.0', 20: '255.255.240.0', 24: '255.255.255.0',
+                28: '255.255.255.240', 30: '255.255.255.252'}
+
+# message forms (per line)
+F_BUILT, F_NONHIT, F_NOYEAR, F_TEARDOWN, F_NOACL, F_OUTBOUND = range(6)
+FORM_NAMES = ['built', 'nonhit', 'noyear', 'teardown', 'noacl', 'outbound']
+
+
+def _dotted(v):
+    v = int(v)
+    return '%d.%d.%d.%d' % ((v >> 24) & 255, (v >> 16) & 255, (v >> 8) & 255, v & 255)
+
+
+class _AddrSpace(object):
+    """Address pools: internal servers live in 10/8, clients in 'public' space."""
+
+    def __init__(self, rng, n_clients=4096, n_servers=2048):
+        self.clients = np.unique(rng.integers(0x0B000000, 0xDF000000, size=n_clients * 2, dtype=np.int64))
+        rng.shuffle(self.clients)
+        self.clients = self.clients[:n_clients]
+        self.servers = np.unique(rng.integers(0x0A000000, 0x0AFFFFFF, size=n_servers * 2, dtype=np.int64))
+        rng.shuffle(self.servers)
+        self.servers = self.servers[:n_servers]
+
+
+def _addr_item(rng, pool, plens):
+    """One address spec item -> (preprocessor text, net int, prefixlen)."""
+    base = int(pool[rng.integers(len(pool))])
+    plen = int(rng.choice(plens))
+    if plen == 32:
+        return _dotted(base), base, 32
+    net = base & ~((1 << (32 - plen)) - 1) & 0xFFFFFFFF
+    return '%s/%s' % (_dotted(net), PREFIX_MASKS[plen]), net, plen
+
+
+def _addr_spec(rng, pool, p_any, p_host, p_net, p_group, net_plens):
+    """Returns (acl text fragment, [(text, net, plen), ...])."""
+    u = rng.random()
+    if u < p_any:
+        return 'any', [('any', 0, 0)]
+    u -= p_any
+    if u < p_host:
+        t, n, l = _addr_item(rng, pool, [32])
+        return 'host ' + t, [(t, n, l)]
+    u -= p_host
+    if u < p_net:
+        t, n, l = _addr_item(rng, pool, net_plens)
+        return t.replace('/', ' '), [(t, n, l)]
+    k = int(rng.integers(2, 5))
+    items, seen = [], set()
+    for _ in range(k):
+        it = _addr_item(rng, pool, [32] + list(net_plens))
+        if it[0] not in seen:
+            seen.add(it[0])
+            items.append(it)
+    return 'object-group GRP%d' % int(rng.integers(1 << 30)), items
+
+
+def _acl_lines(rng, space, acl, n_rules, kind):
+    """Generate ACL lines until ~n_rules expanded rules; returns rule dicts and meta."""
+    rules, meta = [], []
+    lineno = 0
+    target = max(2, int(n_rules))
+    while len(rules) < target - 1:
+        lineno += 1
+        action = bool(rng.random() < 0.85)
+        proto = str(rng.choice(['tcp', 'udp', 'ip'], p=[0.6, 0.25, 0.15]))
+        if kind == 'inside':
+            s_txt, srcs = _addr_spec(rng, space.servers, 0.1, 0.3, 0.6, 0.0, [16, 24])
+            d_txt, dsts = _addr_spec(rng, space.clients, 0.6, 0.2, 0.2, 0.0, [16, 24])
+        else:
+            s_txt, srcs = _addr_spec(rng, space.clients, 0.40, 0.25, 0.25, 0.10, [8, 16, 24])
+            d_txt, dsts = _addr_spec(rng, space.servers, 0.12, 0.55, 0.23, 0.10, [24, 28])
+        sports, dports, sp_txt, dp_txt = [], [], '', ''
+        if proto in ('tcp', 'udp'):
+            if rng.random() < 0.04:
+                p = int(rng.choice(COMMON_PORTS))
+                sports, sp_txt = [p], ' eq %d' % p
+            u = rng.random()
+            if u < 0.70:
+                p = int(rng.choice(COMMON_PORTS)) if rng.random() < 0.7 else int(rng.integers(1, 65536))
+                dports, dp_txt = [p], ' eq %d' % p
+            elif u < 0.82:
+                lo = int(rng.integers(1024, 60000))
+                hi = lo + int(rng.integers(1, 6))
+                dports, dp_txt = list(range(lo, hi + 1)), ' range %d %d' % (lo, hi)
+        size = max(1, len(dports)) * len(dsts) * max(1, len(sports)) * len(srcs)
+        if len(rules) + size > target - 1:
+            if size > 1:
+                continue
+        text = 'access-list %s extended %s %s %s%s %s%s' % (acl, 'permit' if action else 'deny', proto, s_txt,
+                                                            sp_txt, d_txt, dp_txt)
+        for dp in (dports or [-1]):
+            for d in dsts:
+                for sp in (sports or [-1]):
+                    for s in srcs:
+                        rules.append({'action': action, 'protocol': proto, 'original': text, 'src': s[0],
+                                      'dst': d[0], 'sport': [sp], 'dport': [dp], 'comments': [],
+                                      'rulenum': lineno, 'ruleindex': len(rules)})
+                        meta.append((action, proto, s[1], s[2], d[1], d[2], sp, dp))
+    lineno += 1
+    text = 'access-list %s extended deny ip any any' % acl
+    rules.append({'action': False, 'protocol': 'ip', 'original': text, 'src': 'any', 'dst': 'any',
+                  'sport': [-1], 'dport': [-1], 'comments': [], 'rulenum': lineno, 'ruleindex': len(rules)})
+    meta.append((False, 'ip', 0, 0, 0, 0, -1, -1))
+    protocols = {}
+    for r in rules:
+        protocols.setdefault(r['protocol'], []).append(r['ruleindex'])
+    return rules, protocols, meta
+
+
+def make_db(seed, n_rules, host='fw1', interfaces=('outside',), inside_rules=16, with_inside=True):
+    """Seeded rule DB (JSON-able dict) plus per-ACL numeric rule metadata.
+
+    ``interfaces``: each gets its own ``<ifc>_access_in`` ACL of ``n_rules``
+    expanded rules bound ``in``.  ``with_inside`` adds a small
+    ``inside_access_in`` for outbound connections.
+    """
+    rng = np.random.default_rng(seed)
+    space = _AddrSpace(rng)
+    firewalls = {host: {}}
+    acls, meta = {}, {}
+    for ifc in interfaces:
+        acl = '%s_access_in' % ifc
+        rules, protos, m = _acl_lines(rng, space, acl, n_rules, 'outside')
+        acls[acl] = {'rules': rules, 'protocols': protos, 'timestamp': 1373846400.0}
+        meta[acl] = m
+        firewalls[host][ifc] = {'in': acl}
+    if with_inside:
+        acl = 'inside_access_in'
+        rules, protos, m = _acl_lines(rng, space, acl, inside_rules, 'inside')
+        acls[acl] = {'rules': rules, 'protocols': protos, 'timestamp': 1373846400.0}
+        meta[acl] = m
+        firewalls[host]['inside'] = {'in': acl}
+    db = {'firewalls': firewalls, 'accesslists': {host: acls}}
+    return db, {'space': space, 'meta': meta, 'host': host, 'interfaces': list(interfaces),
+                'with_inside': with_inside}
+
+
+def _sample_in(rng, net, plen, n, pool, cap=256):
+    """n addresses inside net/plen (plen 0 -> from pool); at most `cap` distinct."""
+    if plen == 0:
+        return pool[rng.integers(0, len(pool), size=n)]
+    size = 1 << (32 - plen)
+    return net + rng.integers(0, min(size, cap), size=n)
+
+
+def make_traffic(db_and_info, n, seed, form_probs=(0.86, 0.04, 0.04, 0.03, 0.02, 0.01), p_unmatched=0.10,
+                 t0=15 * 86400, span=3 * 3600, zipf=None):
+    """Connection tuples + message forms, as numpy arrays (one entry per line).
+
+    Returns dict with int64 arrays src, dst, sport, dport, proto (0 tcp 1 udp),
+    ifc (index into info['interfaces'] for inbound forms), form, t (seconds
+    from Jul 1 00:00:00), cid.
+    """
+    db, info = db_and_info
+    rng = np.random.default_rng(seed)
+    space = info['space']
+    ifcs = info['interfaces']
+    form = rng.choice(len(form_probs), size=n, p=np.asarray(form_probs) / np.sum(form_probs))
+    if not info['with_inside']:
+        form[form == F_OUTBOUND] = F_BUILT
+    ifc = rng.integers(0, len(ifcs), size=n)
+    src = np.zeros(n, np.int64)
+    dst = np.zeros(n, np.int64)
+    sport = rng.integers(1024, 65536, size=n)
+    dport = COMMON_PORTS[rng.integers(0, len(COMMON_PORTS), size=n)]
+    proto = (rng.random(n) < 0.3).astype(np.int64)
+    # inbound lines: draw from a permit rule of the ACL on the chosen interface
+    for k, name in enumerate(ifcs):
+        meta = info['meta']['%s_access_in' % name]
+        permits = np.array([i for i, m in enumerate(meta) if m[0]], dtype=np.int64)
+        sel = np.nonzero((ifc == k) & (form != F_OUTBOUND))[0]
+        if len(sel) == 0 or len(permits) == 0:
+            continue
+        if zipf:
+            ranks = np.minimum(rng.zipf(zipf, size=len(sel)) - 1, len(permits) - 1)
+            perm = rng.permutation(len(permits))
+            pick = permits[perm[ranks]]
+        else:
+            pick = permits[rng.integers(0, len(permits), size=len(sel))]
+        m = np.array(meta, dtype=object)
+        sn = np.array([int(x) for x in m[:, 2]], np.int64)
+        sl = np.array([int(x) for x in m[:, 3]], np.int64)
+        dn = np.array([int(x) for x in m[:, 4]], np.int64)
+        dl = np.array([int(x) for x in m[:, 5]], np.int64)
+        sp = np.array([int(x) for x in m[:, 6]], np.int64)
+        dp = np.array([int(x) for x in m[:, 7]], np.int64)
+        pr = np.array([{'tcp': 0, 'udp': 1}.get(x, -1) for x in m[:, 1]], np.int64)
+        r = pick
+        for plen in np.unique(sl[r]):
+            w = sl[r] == plen
+            src[sel[w]] = _sample_in(rng, sn[r][w], plen, int(w.sum()), space.clients)
+        for plen in np.unique(dl[r]):
+            w = dl[r] == plen
+            dst[sel[w]] = _sample_in(rng, dn[r][w], plen, int(w.sum()), space.servers)
+        has_sp = sp[r] >= 0
+        sport[sel[has_sp]] = sp[r][has_sp]
+        has_dp = dp[r] >= 0
+        dport[sel[has_dp]] = dp[r][has_dp]
+        fixed = pr[r] >= 0
+        proto[sel[fixed]] = pr[r][fixed]
+        # unmatched noise: random everything
+        un = sel[rng.random(len(sel)) < p_unmatched]
+        src[un] = space.clients[rng.integers(0, len(space.clients), size=len(un))]
+        dst[un] = rng.integers(0x0A000000, 0x0B000000, size=len(un))
+        dport[un] = rng.integers(1, 65536, size=len(un))
+    ob = np.nonzero(form == F_OUTBOUND)[0]
+    src[ob] = space.servers[rng.integers(0, len(space.servers), size=len(ob))]
+    dst[ob] = space.clients[rng.integers(0, len(space.clients), size=len(ob))]
+    t = t0 + (np.arange(n, dtype=np.int64) * span) // max(n, 1)
+    cid = 1000000 + np.arange(n, dtype=np.int64)
+    return {'src': src, 'dst': dst, 'sport': sport, 'dport': dport, 'proto': proto, 'ifc': ifc, 'form': form,
+            't': t, 'cid': cid, 'interfaces': list(ifcs), 'host': info['host']}
+
+
+def _clock(t):
+    day = t // 86400
+    s = t % 86400
+    return int(day), '%02d:%02d:%02d' % (s // 3600, (s // 60) % 60, s % 60)
+
+
+def render_lines(tr):
+    """Log text lines (without newline) for the traffic dict."""
+    out = []
+    P = ('TCP', 'UDP')
+    MID = ('302013', '302015')
+    for i in range(len(tr['form'])):
+        f = int(tr['form'][i])
+        day, hms = _clock(int(tr['t'][i]))
+        pr = int(tr['proto'][i])
+        s, d = _dotted(tr['src'][i]), _dotted(tr['dst'][i])
+        sp, dp = int(tr['sport'][i]), int(tr['dport'][i])
+        cid = '%010d' % int(tr['cid'][i])
+        ifc = tr['interfaces'][int(tr['ifc'][i])]
+        head = 'Jul %02d %s Jul %02d 2013 %s: ' % (day, hms, day, hms)
+        if f == F_BUILT or f == F_NOACL:
+            if f == F_NOACL:
+                ifc = 'dmz'
+            out.append('%s%%ASA-6-%s: Built inbound %s connection %s for %s:%s/%d (%s/%d) to inside:%s/%d (%s/%d)'
+                       % (head, MID[pr], P[pr], cid, ifc, s, sp, s, sp, d, dp, d, dp))
+        elif f == F_NONHIT:
+            out.append('%s%%ASA-5-%s: Built inbound %s connection %s for %s:%s/%d (%s/%d) to inside:%s/%d (%s/%d)'
+                       % (head, MID[pr], P[pr], cid, ifc, s, sp, s, sp, d, dp, d, dp))
+        elif f == F_NOYEAR:
+            out.append('Jul %02d %s fw1 : %%ASA-6-%s: Built inbound %s connection %s for %s:%s/%d (%s/%d) '
+                       'to inside:%s/%d (%s/%d)' % (day, hms, MID[pr], P[pr], cid, ifc, s, sp, s, sp, d, dp, d, dp))
+        elif f == F_TEARDOWN:
+            out.append('%s%%ASA-6-302014: Teardown %s connection %s for %s:%s/%d to inside:%s/%d duration 0:00:01 '
+                       'bytes 1024 TCP FINs' % (head, P[pr], cid, ifc, s, sp, d, dp))
+        else:  # outbound: initiator (src) is inside, 'for' side is the outside peer
+            out.append('%s%%ASA-6-%s: Built outbound %s connection %s for outside:%s/%d (%s/%d) to inside:%s/%d '
+                       '(%s/%d)' % (head, MID[pr], P[pr], cid, d, dp, d, dp, s, sp, s, sp))
+    return out
