@@ -1,0 +1,222 @@
+#!/usr/bin/env python3
+"""Benchmark of the ruleset-analysis hot path on MI355X.
+
+Metric (BASELINE.json): log lines/sec classified (node) at 10k rules; % of the
+HBM roofline.  Workload = BASELINE config 3 per GPU: a 10k-rule ACL
+(replicated), 125M synthetic ASA connection tuples per GPU (weak scaling:
+N GPUs process N x 125M lines of one global log, order keys global), cap 1000.
+
+One step = the whole job over the resident batch: pass 1 (first-match
+classification fused with per-rule counters and the distinct-connection
+table), cap resolution, pass 2 when any rule is capped, and emission of the
+final connection records into HBM; for N > 1 also the merge (all_reduce of
+counters, all_to_all of records to owner ranks, threshold all_reduce, pass-2
+exchange, gather of the owners' records to rank 0).
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import rsa_pkg  # noqa: E402
+
+rsa_pkg.load()
+
+from ruleset_analysis_amd import acldb, synth  # noqa: E402
+from ruleset_analysis_amd.compile import CompiledRules  # noqa: E402
+from ruleset_analysis_amd.engine import DeviceBatch, Engine  # noqa: E402
+from ruleset_analysis_amd.pipeline import built_hit_count  # noqa: E402
+
+BYTES_PER_LINE = 28          # 16 B tuple + 4 B timestamp code + 8 B order key
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
+CONFIGS = {
+    # name: (rules, lines per GPU, cap, seed, zipf, interfaces)
+    'cfg3': (10000, 125_000_000, 1000, 3, None, ('outside',)),
+    'cfg2': (1000, 100_000_000, 1000, 2, None, ('outside',)),
+    'cfg5': (2500, 100_000_000, 1000, 5, 1.1, ('outside', 'partner', 'vpn', 'extranet')),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def build_shard(dbj, info, compiled, n, rank, seed, zipf, device, chunk=8_000_000, world=1):
+    """Generate this rank's contiguous slice of the global synthetic log straight
+    into HBM, in chunks (host memory stays bounded)."""
+    import torch
+    tuples = torch.empty((n, 4), dtype=torch.int32, device=device)
+    ts = torch.empty(n, dtype=torch.int32, device=device)
+    order = torch.empty(n, dtype=torch.int64, device=device)
+    n_hb = 0
+    span_total = 3 * 3600 * world
+    for k, a in enumerate(range(0, n, chunk)):
+        m = min(chunk, n - a)
+        g0 = rank * n + a                                # global line index of the chunk
+        t0 = 15 * 86400 + (g0 * span_total) // (n * world)
+        t1 = 15 * 86400 + ((g0 + m) * span_total) // (n * world)
+        tr = synth.make_traffic((dbj, info), m, seed=seed * 1_000_003 + rank * 1009 + k, zipf=zipf, t0=t0,
+                                span=max(t1 - t0, 1), cid0=1_000_000 + g0)
+        tup, t, o = synth.pack(tr, compiled)
+        n_hb += built_hit_count(tup)
+        tuples[a:a + m].copy_(torch.from_numpy(tup.view(np.int32).reshape(-1, 4)))
+        ts[a:a + m].copy_(torch.from_numpy(t.view(np.int32)))
+        order[a:a + m].copy_(torch.from_numpy(o.view(np.int64)))
+    return DeviceBatch(tuples, ts, order), n_hb
+
+
+def cpu_baseline(dbj, info, seconds=15.0):
+    """The oracle's restatement of the reference pipeline (mapper | sort | reducer,
+    pure Python like the reference) on a bounded sample of the same workload,
+    one core."""
+    from oracle import pipeline as op
+    from oracle.crosscheck_2to3 import oracle_db
+    acls, fws = oracle_db(dbj)
+    tr = synth.make_traffic((dbj, info), 200_000, seed=99)
+    lines = synth.render_lines(tr)
+    # calibrate on a small prefix, then size the timed sample to ~`seconds`
+    probe = 200
+    t = time.perf_counter()
+    op.run_pipeline(''.join(l + '\n' for l in lines[:probe]), 'fw1', acls, fws, cap=1000)
+    per = (time.perf_counter() - t) / probe
+    n = int(min(len(lines), max(probe, seconds / max(per, 1e-7))))
+    text = ''.join(l + '\n' for l in lines[:n])
+    t = time.perf_counter()
+    op.run_pipeline(text, 'fw1', acls, fws, cap=1000)
+    dt = time.perf_counter() - t
+    return {'value': n / dt, 'unit': 'lines/s', 'cores': 1, 'kind': 'port',
+            'sample': '%d lines of the same 10k-rule workload through oracle/pipeline.py '
+                      '(mapper | LC_ALL=C sort | reducer restated in Python, 1 process), %.1f s' % (n, dt)}
+
+
+def read_traffic(name):
+    """Per-launch HBM bytes of the pass-1 kernel from a committed rocprofv3 PMC
+    summary (profiles/<name>), corrected per MI355X_MICROARCH.md §HBM, if present."""
+    path = os.path.join(ROOT, 'profiles', name)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f).get('hbm_bytes_per_launch')
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=5)
+    ap.add_argument('--warmup', type=int, default=2)
+    ap.add_argument('--config', default='cfg3', choices=sorted(CONFIGS))
+    ap.add_argument('--lines', type=int, default=0, help='override lines per GPU')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    rules, lines, cap, seed, zipf, ifcs = CONFIGS[args.config]
+    if args.lines:
+        lines = args.lines
+    t_setup = time.perf_counter()
+    dbj, info = synth.make_db(seed, rules, interfaces=ifcs)
+    compiled = CompiledRules(acldb.load_json(dbj))
+    compiled.ensure_lists()
+    eng = Engine(local)
+    ent, off = compiled.packed()
+    eng.load_rules(ent, off, compiled.n_rules)
+    batch, n_hb = build_shard(dbj, info, compiled, lines, rank, seed, zipf, eng.device, world=world)
+    owner = None
+    if world > 1:
+        owner = Engine(local)
+        owner.set_rule_count(compiled.n_rules)
+    gbuf = torch.empty(lines, dtype=torch.int32, device=eng.device)
+    torch.cuda.synchronize()
+    log('rank %d setup %.1fs: %d rules, %d lists, %d entries, %d lines, %d hit+built' % (
+        rank, time.perf_counter() - t_setup, compiled.n_rules, compiled.n_lists(), len(ent), lines, n_hb))
+
+    capacity = max(n_hb, 1)
+    ev = []
+
+    def step(timed):
+        nonlocal capacity
+        eng.reset(capacity, cap)
+        if timed:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+        eng.pass1(batch, gbuf)
+        if timed:
+            e1.record()
+            ev.append((e0, e1))
+        if world == 1:
+            if eng.resolve_cap():
+                eng.pass2(batch, gbuf)
+            recs = eng.emit_device('final')
+            return recs.numel()
+        from ruleset_analysis_amd.dist import EngineBackend, merge
+        out = merge(EngineBackend(eng, owner, [batch], [gbuf], cap), dist, world, rank)
+        return 0 if out is None else len(out[0])
+
+    for _ in range(args.warmup):
+        step(False)
+    # size the table for the observed distinct count (capacity planning from warm-up)
+    if args.warmup:
+        capacity = max(int(eng.table_size() * 1.25), 1)
+
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        n_rec = step(True)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        tt = torch.tensor([dt], dtype=torch.float64, device=eng.device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    k_ms = [a.elapsed_time(b) for a, b in ev]
+    pass1_ms = float(np.mean(k_ms))
+    if rank == 0:
+        total_lines = lines * world * args.steps
+        value = total_lines / dt
+        achieved = BYTES_PER_LINE * lines / (pass1_ms * 1e-3) / 1e9
+        traffic = read_traffic('%s_pass1_pmc.json' % args.config)
+        res = {
+            'metric': 'log lines/sec classified (node) at %d rules; %% of HBM roofline' % rules,
+            'value': value, 'unit': 'lines/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+            'ms_per_step': dt / args.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
+            'vs_baseline': None, 'dtype': 'u32', 'data': 'synthetic (seeded ASA connection tuples, pre-parsed, '
+                                                          'resident in HBM)',
+            'config': {'workload': '%s: %d-rule ACL, %d lines per GPU, cap %d' % (args.config, compiled.n_rules,
+                                                                                  lines, cap),
+                       'rules': compiled.n_rules, 'lines_per_gpu': lines, 'cap': cap, 'parallelism': 'dp%d' % world,
+                       'records': n_rec},
+            'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                         'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
+                         'kernel': 'k_pass1<false> (classify + aggregate)', 'kernel_ms': pass1_ms,
+                         'bytes_per_line': BYTES_PER_LINE},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res['cpu_baseline'] = cpu_baseline(dbj, info)
+        print(json.dumps(res), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

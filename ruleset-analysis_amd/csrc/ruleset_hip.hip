@@ -127,7 +127,7 @@ __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Ru
         const v4u b = R.e[2 * (e + j) + 1];
         const bool m = ((src - a.x) <= a.y) & ((dst - a.z) <= a.w) &
                        ((sp - (b.x & 0xFFFFu)) <= (b.y & 0xFFFFu)) & ((dp - (b.x >> 16)) <= (b.y >> 16));
-        best = min(best, m ? b.z : kNoGid);
+        best = min(best, (m & mine) ? b.z : kNoGid);
       }
       if (__ballot(mine && best == kNoGid) == 0) break;
     }
@@ -137,7 +137,7 @@ __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Ru
         const v4u b = R.e[2 * e + 1];
         const bool m = ((src - a.x) <= a.y) & ((dst - a.z) <= a.w) &
                        ((sp - (b.x & 0xFFFFu)) <= (b.y & 0xFFFFu)) & ((dp - (b.x >> 16)) <= (b.y >> 16));
-        best = min(best, m ? b.z : kNoGid);
+        best = min(best, (m & mine) ? b.z : kNoGid);
       }
     }
   }

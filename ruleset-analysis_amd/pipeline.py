@@ -23,7 +23,7 @@ def built_hit_count(tuples):
     return int(np.count_nonzero((tuples['flags'] & both) == both))
 
 
-def assemble_report(parsed, gids, results, compiled, cap):
+def assemble_report(parsed, gids, results, compiled, cap, ts_decode=None, pspell_table=None):
     """Reducer stdout lines for parsed lines, their gids and the GPU results."""
     db = compiled.db
     groups = []
@@ -48,8 +48,11 @@ def assemble_report(parsed, gids, results, compiled, cap):
         noise.append((skipped, skipped))
         if nl[i]:
             n_blank += 1
-    return reducer_report(results, groups, noise, cap, lambda c: parsed.ts_table[c], parsed.pspell_table,
-                          n_blank=n_blank)
+    if ts_decode is None:
+        ts_decode = parsed.ts_table.__getitem__
+    if pspell_table is None:
+        pspell_table = parsed.pspell_table
+    return reducer_report(results, groups, noise, cap, ts_decode, pspell_table, n_blank=n_blank)
 
 
 def analyze(inputs, db, cap=1000, device=0, engine=None):

@@ -28,7 +28,8 @@ seconds.
 
 import numpy as np
 
-__all__ = ['make_db', 'make_traffic', 'render_lines', 'FORM_NAMES', 'COMMON_PORTS']
+__all__ = ['make_db', 'make_traffic', 'render_lines', 'pack', 'order_keys', 'ts_decode', 'PSPELL', 'FORM_NAMES',
+           'COMMON_PORTS']
 
 COMMON_PORTS = np.array([80, 443, 22, 25, 53, 123, 389, 445, 636, 993, 1433, 3306, 3389, 5432, 8080, 8443],
                         dtype=np.int64)
@@ -180,7 +181,7 @@ def _sample_in(rng, net, plen, n, pool, cap=256):
 
 
 def make_traffic(db_and_info, n, seed, form_probs=(0.86, 0.04, 0.04, 0.03, 0.02, 0.01), p_unmatched=0.10,
-                 t0=15 * 86400, span=3 * 3600, zipf=None):
+                 t0=15 * 86400, span=3 * 3600, zipf=None, cid0=1000000):
     """Connection tuples + message forms, as numpy arrays (one entry per line).
 
     Returns dict with int64 arrays src, dst, sport, dport, proto (0 tcp 1 udp),
@@ -243,7 +244,7 @@ def make_traffic(db_and_info, n, seed, form_probs=(0.86, 0.04, 0.04, 0.03, 0.02,
     src[ob] = space.servers[rng.integers(0, len(space.servers), size=len(ob))]
     dst[ob] = space.clients[rng.integers(0, len(space.clients), size=len(ob))]
     t = t0 + (np.arange(n, dtype=np.int64) * span) // max(n, 1)
-    cid = 1000000 + np.arange(n, dtype=np.int64)
+    cid = cid0 + np.arange(n, dtype=np.int64)
     return {'src': src, 'dst': dst, 'sport': sport, 'dport': dport, 'proto': proto, 'ifc': ifc, 'form': form,
             't': t, 'cid': cid, 'interfaces': list(ifcs), 'host': info['host']}
 
@@ -286,3 +287,59 @@ def render_lines(tr):
             out.append('%s%%ASA-6-%s: Built outbound %s connection %s for outside:%s/%d (%s/%d) to inside:%s/%d '
                        '(%s/%d)' % (head, MID[pr], P[pr], cid, d, dp, d, dp, s, sp, s, sp))
     return out
+
+
+PSPELL = ['TCP', 'UDP']
+
+
+def order_keys(tr):
+    """uint64 keys order-isomorphic to the byte order of the rendered lines among
+    the lines that can enter a connection table (hit + BUILT forms): time,
+    then message id digit (302013 < 302015 <=> TCP < UDP), then direction
+    ('inbound' < 'outbound'), then the zero-padded connection id."""
+    t = tr['t'].astype(np.uint64)
+    x = tr['proto'].astype(np.uint64)
+    d = (tr['form'] == F_OUTBOUND).astype(np.uint64)
+    return (t << np.uint64(36)) | (x << np.uint64(35)) | (d << np.uint64(34)) | tr['cid'].astype(np.uint64)
+
+
+def ts_decode(code):
+    """Timestamp code (seconds from Jul 1 2013 00:00:00) -> reducer string."""
+    day, hms = _clock(int(code))
+    return '2013-07-%02d %s' % (day, hms)
+
+
+def pack(tr, compiled):
+    """Packed tuples/ts/order for the traffic, equal to what logparse produces
+    from ``render_lines(tr)`` (pinned by tests/test_synth_pack.py)."""
+    from .compile import TUPLE_DTYPE, F_VALID as FL_VALID, F_HIT as FL_HIT, F_BUILT as FL_BUILT, F_SWAP as FL_SWAP
+    n = len(tr['form'])
+    form = tr['form']
+    host = tr['host']
+    ifcs = tr['interfaces']
+    out = np.zeros(n, dtype=TUPLE_DTYPE)
+    out['src'] = tr['src'].astype(np.uint32)
+    out['dst'] = tr['dst'].astype(np.uint32)
+    out['sport'] = tr['sport'].astype(np.uint16)
+    out['dport'] = tr['dport'].astype(np.uint16)
+    out['pspell'] = tr['proto'].astype(np.uint8)
+    valid = np.isin(form, [F_BUILT, F_NONHIT, F_NOYEAR, F_OUTBOUND])
+    lists = np.zeros(n, dtype=np.int64)
+    names = ('tcp', 'udp')
+    for p in (0, 1):
+        for k, ifc in enumerate(ifcs):
+            w = valid & (form != F_OUTBOUND) & (tr['ifc'] == k) & (tr['proto'] == p)
+            if w.any():
+                lists[w] = compiled.list_id(host, '%s_access_in' % ifc, names[p])
+        w = (form == F_OUTBOUND) & (tr['proto'] == p)
+        if w.any():
+            lists[w] = compiled.list_id(host, 'inside_access_in', names[p])
+    out['list'] = lists.astype(np.uint16)
+    flags = np.where(valid, FL_VALID, 0)
+    flags = flags | np.where(np.isin(form, [F_BUILT, F_NOYEAR, F_OUTBOUND]), FL_HIT, 0)
+    flags = flags | np.where(np.isin(form, [F_BUILT, F_NONHIT, F_OUTBOUND]), FL_BUILT, 0)
+    flags = flags | np.where(form == F_OUTBOUND, FL_SWAP, 0)
+    out['flags'] = flags.astype(np.uint8)
+    out['pspell'][(flags & FL_BUILT) == 0] = 0
+    ts = tr['t'].astype(np.uint32)
+    return out, ts, order_keys(tr)

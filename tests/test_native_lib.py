@@ -1,0 +1,45 @@
+"""The C-ABI library builds for gfx950, loads, and exports every entry point
+declared in include/ruleset_hip.h (no compute calls: no GPU needed)."""
+import ctypes
+import os
+import re
+
+from conftest import ROOT
+from ruleset_analysis_amd import native
+
+
+def _declared():
+    with open(os.path.join(ROOT, 'include', 'ruleset_hip.h')) as f:
+        src = f.read()
+    return sorted(set(re.findall(r'^(?:int|const char \*|void)\s*\*?\s*(rsa_\w+)\s*\(', src, re.M)))
+
+
+def test_header_and_binding_agree():
+    assert _declared() == sorted(native.SYMBOLS)
+
+
+def test_library_exports_all_symbols():
+    lib = native.load()
+    for name in _declared():
+        assert hasattr(lib, name), name
+    assert lib.rsa_version() == 1
+
+
+def test_library_is_gfx950_code_object():
+    with open(native.lib_path(), 'rb') as f:
+        blob = f.read()
+    assert b'gfx950' in blob
+
+
+def test_struct_layouts():
+    from ruleset_analysis_amd.compile import RECORD_DTYPE, RULE_DTYPE, TUPLE_DTYPE
+    assert (TUPLE_DTYPE.itemsize, RULE_DTYPE.itemsize, RECORD_DTYPE.itemsize) == (16, 32, 40)
+
+
+def test_ctx_create_without_gpu_fails_cleanly():
+    import torch
+    if torch.cuda.is_available():
+        return
+    lib = native.load()
+    h = ctypes.c_void_p()
+    assert lib.rsa_ctx_create(0, ctypes.byref(h)) != 0
