@@ -116,6 +116,10 @@ int rsa_reset(rsa_ctx *ctx, uint64_t capacity, uint32_t cap);
 int rsa_classify(rsa_ctx *ctx, const rsa_tuple *d_tuples, const uint32_t *d_ts, const uint64_t *d_order,
                  uint64_t n, int32_t *d_gid_out);
 
+/* Classification only: first-match gid per tuple, no aggregation (the mapper
+ * drop-in, mapper.py:159-189).  Needs rsa_load_rules; no counters/table. */
+int rsa_classify_only(rsa_ctx *ctx, const rsa_tuple *d_tuples, uint64_t n, int32_t *d_gid_out);
+
 /* Pass 1 with the rule already known per tuple (the reducer drop-in: the key
  * comes from the mapper's output line, connlist-reducer.py:63-75). */
 int rsa_aggregate_gids(rsa_ctx *ctx, const rsa_tuple *d_tuples, const uint32_t *d_ts, const uint64_t *d_order,

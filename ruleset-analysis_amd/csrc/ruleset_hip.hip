@@ -22,6 +22,7 @@
 //           capped rules only — the exact restatement of the frozen dict.
 //   emit    compact the table to rsa_conn_record rows.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <cstdarg>
 #include <cstdio>
@@ -69,6 +70,7 @@ struct Agg {
   unsigned long long* hits;
   unsigned int* distinct;
   const unsigned long long* thresh;
+  const unsigned long long* filter;  // per rule: lines with order > filter cannot matter (cap)
   Slot* slots;
   unsigned long long mask;  // capacity - 1 (power of two)
   unsigned int* flags;      // [0] overflow, [1] bad gid/list
@@ -86,6 +88,21 @@ __device__ __forceinline__ unsigned long long mix64(unsigned long long x) {
 
 __device__ __forceinline__ unsigned long long slot_hash(unsigned long long kA, unsigned long long kB) {
   return mix64(kA ^ (kB * 0x9e3779b97f4a7c15ull));
+}
+
+// counter[key] += 1 for every lane with `ok`, one device atomic per distinct key
+// in the wave (lanes sharing a rule are counted first: hot rules would otherwise
+// serialise thousands of atomics on one address).  Wave-uniform control flow.
+template <typename T>
+__device__ __forceinline__ void wave_count_by_key(bool ok, uint32_t key, T* counter) {
+  unsigned long long pending = __ballot(ok);
+  while (pending) {
+    const int leader = __builtin_ctzll(pending);
+    const uint32_t k = __builtin_amdgcn_readlane(key, leader);
+    const unsigned long long peers = __ballot(ok && key == k);
+    pending &= ~peers;
+    if ((int)__lane_id() == leader) atomicAdd(&counter[k], (T)__popcll(peers));
+  }
 }
 
 // Reducer key of a tuple (connlist-reducer.py:162: PROTO;FROMIP;TOIP;TOPORT).
@@ -147,10 +164,13 @@ __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Ru
 // Insert-or-combine (kA, kB) into the open-addressing table.  All key reads are
 // device atomics (executed beyond the per-XCD L2s, so every XCD sees one value).
 // A slot is claimed EMPTY->BUSY, its kA published, then kB published; a lane
-// that reads BUSY retries the same slot on its next iteration.
-__device__ __forceinline__ void table_combine(const Agg& A, unsigned long long kA, unsigned long long kB,
+// that reads BUSY retries the same slot on its next iteration.  Every key word
+// is only ever accessed by device atomics, which execute beyond the per-XCD
+// L2s, so no XCD can observe a stale copy.
+__device__ __forceinline__ bool table_combine(const Agg& A, unsigned long long kA, unsigned long long kB,
                                               unsigned int cnt, unsigned int first, unsigned int last,
                                               unsigned long long order) {
+  bool fresh = false;
   unsigned long long h = slot_hash(kA, kB) & A.mask;
   unsigned long long probes = 0;
   Slot* s = nullptr;
@@ -158,10 +178,12 @@ __device__ __forceinline__ void table_combine(const Agg& A, unsigned long long k
     Slot* c = &A.slots[h];
     const unsigned long long cur = atomicCAS(&c->kB, kEmpty, kBusy);
     if (cur == kEmpty) {
+      // kA is published by a device atomic; waiting for its completion before the
+      // kB exchange orders the two at the memory side (no cache write-back fence).
       atomicExch(&c->kA, kA);
-      __threadfence();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       atomicExch(&c->kB, kB);
-      atomicAdd(&A.distinct[kB >> 32], 1u);
+      fresh = true;
       s = c;
       break;
     }
@@ -177,12 +199,13 @@ __device__ __forceinline__ void table_combine(const Agg& A, unsigned long long k
   }
   if (!s) {
     atomicOr(&A.flags[0], 1u);
-    return;
+    return false;
   }
   atomicAdd(&s->count, cnt);
   atomicMin(&s->first, first);
   atomicMax(&s->last, last);
   atomicMin(&s->min_order, order);
+  return fresh;
 }
 
 // Find an existing key (after pass 1 completed: plain loads are coherent across
@@ -199,7 +222,11 @@ __device__ __forceinline__ Slot* table_find(const Agg& A, unsigned long long kA,
   return nullptr;
 }
 
-template <bool kGiven>
+// Pass-1 modes: classify + aggregate (mapper fused with reducer), aggregate with
+// the gid given per tuple (reducer drop-in), classify only (mapper drop-in).
+enum { kClassifyAgg = 0, kGivenAgg = 1, kClassifyOnly = 2 };
+
+template <int kMode>
 __global__ __launch_bounds__(kBlock) void k_pass1(const uint4* __restrict__ T, const uint32_t* __restrict__ TS,
                                                   const unsigned long long* __restrict__ ORD, unsigned long long n,
                                                   const int32_t* __restrict__ gin, int32_t* __restrict__ gout,
@@ -211,28 +238,30 @@ __global__ __launch_bounds__(kBlock) void k_pass1(const uint4* __restrict__ T, c
     const uint4 t = in ? T[i] : make_uint4(0u, 0u, 0u, 0u);
     const uint32_t flags = (t.w >> 16) & 0xFFu;
     uint32_t gid;
-    if (kGiven) {
+    if (kMode == kGivenAgg) {
       gid = in ? (uint32_t)gin[i] : kNoGid;
     } else {
       gid = classify_wave(t, in && (flags & RSA_F_VALID), R, A.flags);
     }
-    if (!kGiven && gout && in) gout[i] = (int32_t)gid;
-    if (gid != kNoGid) {
-      if (gid >= R.n_rules) {
-        atomicOr(&A.flags[1], 2u);
-        continue;
-      }
-      atomicAdd(&A.matches[gid], 1ull);
-      if (flags & RSA_F_HIT) {
-        atomicAdd(&A.hits[gid], 1ull);
-        if ((flags & RSA_F_BUILT) && A.cap > 0) {
-          unsigned long long kA, kB;
-          conn_key(t, gid, kA, kB);
-          const uint32_t ts = TS[i];
-          table_combine(A, kA, kB, 1u, ts, ts, ORD[i]);
-        }
+    if (kMode != kGivenAgg && gout && in) gout[i] = (int32_t)gid;
+    if (kMode == kClassifyOnly) continue;
+    if (gid != kNoGid && gid >= R.n_rules) atomicOr(&A.flags[1], 2u);
+    const bool matched = gid < R.n_rules;
+    const bool hit = matched && (flags & RSA_F_HIT);
+    wave_count_by_key(matched, gid, A.matches);
+    wave_count_by_key(hit, gid, A.hits);
+    bool fresh = false;
+    if (hit && (flags & RSA_F_BUILT) && A.cap > 0) {
+      const unsigned long long o = ORD[i];
+      // exact skip: the rule is already capped with threshold <= filter < o
+      if (o <= A.filter[gid]) {
+        unsigned long long kA, kB;
+        conn_key(t, gid, kA, kB);
+        const uint32_t ts = TS[i];
+        fresh = table_combine(A, kA, kB, 1u, ts, ts, o);
       }
     }
+    wave_count_by_key(fresh, gid, A.distinct);
   }
 }
 
@@ -290,9 +319,26 @@ __global__ void k_table_init(Slot* S, unsigned long long cap) {
   }
 }
 
-// ---- cap resolution: radix select of the cap-th smallest min_order per rule ----
+// Wave-aggregated append to a global cursor: one atomic per wave.  Must be
+// called by every lane of the wave (wave-uniform control flow).
+__device__ __forceinline__ unsigned long long wave_append(bool ok, unsigned long long* cursor) {
+  const unsigned long long mask = __ballot(ok);
+  if (mask == 0) return 0;
+  const unsigned lane = __lane_id();
+  const int leader = __builtin_ctzll(mask);
+  unsigned long long base = 0;
+  if ((int)lane == leader) base = atomicAdd(cursor, (unsigned long long)__popcll(mask));
+  base = __shfl(base, leader);
+  return base + __popcll(mask & ((1ull << lane) - 1ull));
+}
+
+// ---- cap resolution (exact): P = cap-th smallest min_order among a rule's entries.
+// Capped entries are compacted to (min_order, capped index) pairs, sorted by
+// min_order then stably by capped index (two LSD radix sorts), so each capped
+// rule's entries form one ascending segment and P is the segment's cap-th element.
 __global__ void k_cap_mark(const unsigned int* distinct, uint32_t n_rules, uint32_t cap, uint32_t* cidx,
-                           uint32_t* capped_gid, unsigned int* n_capped, unsigned long long* thresh) {
+                           uint32_t* capped_gid, uint32_t* capped_cnt, unsigned int* n_capped,
+                           unsigned long long* thresh) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= n_rules) return;
   thresh[g] = RSA_NO_THRESHOLD;
@@ -300,50 +346,40 @@ __global__ void k_cap_mark(const unsigned int* distinct, uint32_t n_rules, uint3
     const unsigned int c = atomicAdd(n_capped, 1u);
     cidx[g] = c;
     capped_gid[c] = g;
+    capped_cnt[c] = distinct[g];
   } else {
     cidx[g] = 0xFFFFFFFFu;
   }
 }
 
-__global__ void k_sel_hist(const Slot* S, unsigned long long cap_slots, const uint32_t* cidx,
-                           const unsigned long long* prefix, unsigned int* hist, int pass) {
-  const int shift = 56 - 8 * pass;
-  const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
-  for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < cap_slots; i += stride) {
-    const unsigned long long kB = S[i].kB;
-    if (kB >= kBusy) continue;
-    const uint32_t c = cidx[kB >> 32];
-    if (c == 0xFFFFFFFFu) continue;
-    const unsigned long long o = S[i].min_order;
-    if (pass > 0 && (o >> (shift + 8)) != prefix[c]) continue;
-    atomicAdd(&hist[(size_t)c * 256 + ((o >> shift) & 255u)], 1u);
-  }
-}
-
-__global__ void k_sel_pick(unsigned int* hist, unsigned long long* prefix, uint32_t* rank, uint32_t n_capped) {
-  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= n_capped) return;
-  uint32_t rem = rank[c];
-  uint32_t cum = 0;
-  uint32_t digit = 255;
-  unsigned int* h = hist + (size_t)c * 256;
-  for (uint32_t d = 0; d < 256; ++d) {
-    const uint32_t v = h[d];
-    if (cum + v >= rem) {
-      digit = d;
-      break;
+__global__ __launch_bounds__(kBlock) void k_cap_collect(const Slot* S, unsigned long long cap_slots,
+                                                        const uint32_t* cidx, unsigned long long* keys,
+                                                        uint32_t* vals, unsigned long long* cursor) {
+  const unsigned long long stride = (unsigned long long)gridDim.x * kBlock;
+  for (unsigned long long base = (unsigned long long)blockIdx.x * kBlock; base < cap_slots; base += stride) {
+    const unsigned long long i = base + threadIdx.x;
+    uint32_t c = 0xFFFFFFFFu;
+    unsigned long long o = 0;
+    if (i < cap_slots) {
+      const unsigned long long kB = S[i].kB;
+      if (kB < kBusy) {
+        c = cidx[kB >> 32];
+        o = S[i].min_order;
+      }
     }
-    cum += v;
+    const bool ok = c != 0xFFFFFFFFu;
+    const unsigned long long pos = wave_append(ok, cursor);
+    if (ok) {
+      keys[pos] = o;
+      vals[pos] = c;
+    }
   }
-  rank[c] = rem - cum;
-  prefix[c] = (prefix[c] << 8) | digit;
-  for (uint32_t d = 0; d < 256; ++d) h[d] = 0;
 }
 
-__global__ void k_sel_store(const unsigned long long* prefix, const uint32_t* capped_gid, uint32_t n_capped,
-                            unsigned long long* thresh) {
+__global__ void k_cap_pick(const unsigned long long* sorted_orders, const uint32_t* start, const uint32_t* capped_gid,
+                           uint32_t n_capped, uint32_t cap, unsigned long long* thresh) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c < n_capped) thresh[capped_gid[c]] = prefix[c];
+  if (c < n_capped) thresh[capped_gid[c]] = sorted_orders[(size_t)start[c] + cap - 1];
 }
 
 __device__ __forceinline__ rsa_conn_record make_record(const Slot& s, int which) {
@@ -363,30 +399,30 @@ __device__ __forceinline__ rsa_conn_record make_record(const Slot& s, int which)
 }
 
 // mode 0: final report rows; mode 1: export pass-1 aggregates; mode 2: export pass-2.
-__global__ void k_emit(const Slot* S, unsigned long long cap_slots, const unsigned long long* thresh, int mode,
-                       rsa_conn_record* out, unsigned long long max_out, unsigned long long* cursor) {
-  const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
-  for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < cap_slots; i += stride) {
-    const Slot s = S[i];
-    if (s.kB >= kBusy) continue;
-    int which;
-    if (mode == 0) {
-      const unsigned long long P = thresh[s.kB >> 32];
-      if (P == RSA_NO_THRESHOLD) {
-        which = 0;
-      } else if (s.min_order <= P) {
-        which = 1;
-      } else {
-        continue;
+__global__ __launch_bounds__(kBlock) void k_emit(const Slot* S, unsigned long long cap_slots,
+                                                 const unsigned long long* thresh, int mode, rsa_conn_record* out,
+                                                 unsigned long long max_out, unsigned long long* cursor) {
+  const unsigned long long stride = (unsigned long long)gridDim.x * kBlock;
+  for (unsigned long long base = (unsigned long long)blockIdx.x * kBlock; base < cap_slots; base += stride) {
+    const unsigned long long i = base + threadIdx.x;
+    int which = -1;
+    Slot s;
+    if (i < cap_slots) {
+      s = S[i];
+      if (s.kB < kBusy) {
+        if (mode == 0) {
+          const unsigned long long P = thresh[s.kB >> 32];
+          if (P == RSA_NO_THRESHOLD) which = 0;
+          else if (s.min_order <= P) which = 1;
+        } else if (mode == 1) {
+          which = 0;
+        } else if (s.count2 != 0) {
+          which = 1;
+        }
       }
-    } else if (mode == 1) {
-      which = 0;
-    } else {
-      if (s.count2 == 0) continue;
-      which = 1;
     }
-    const unsigned long long k = atomicAdd(cursor, 1ull);
-    if (k < max_out) out[k] = make_record(s, which);
+    const unsigned long long k = wave_append(which >= 0, cursor);
+    if (which >= 0 && k < max_out) out[k] = make_record(s, which);
   }
 }
 
@@ -397,7 +433,8 @@ __global__ void k_import(const rsa_conn_record* __restrict__ in, unsigned long l
     const unsigned long long kA = ((unsigned long long)r.for_ip << 32) | r.to_ip;
     const unsigned long long kB = ((unsigned long long)r.gid << 32) | ((unsigned long long)r.pspell << 16) | r.to_port;
     if (which == 0) {
-      table_combine(A, kA, kB, r.count, r.first, r.last, r.min_order);
+      const bool fresh = table_combine(A, kA, kB, r.count, r.first, r.last, r.min_order);
+      if (fresh) atomicAdd(&A.distinct[r.gid], 1u);
     } else {
       Slot* s = table_find(A, kA, kB);
       if (!s) {
@@ -411,10 +448,13 @@ __global__ void k_import(const rsa_conn_record* __restrict__ in, unsigned long l
   }
 }
 
-__global__ void k_count_used(const Slot* S, unsigned long long cap_slots, unsigned long long* cursor) {
-  const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
-  for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < cap_slots; i += stride) {
-    if (S[i].kB < kBusy) atomicAdd(cursor, 1ull);
+__global__ __launch_bounds__(kBlock) void k_count_used(const Slot* S, unsigned long long cap_slots,
+                                                       unsigned long long* cursor) {
+  const unsigned long long stride = (unsigned long long)gridDim.x * kBlock;
+  for (unsigned long long base = (unsigned long long)blockIdx.x * kBlock; base < cap_slots; base += stride) {
+    const unsigned long long i = base + threadIdx.x;
+    const bool used = i < cap_slots && S[i].kB < kBusy;
+    wave_append(used, cursor);
   }
 }
 
@@ -433,6 +473,10 @@ struct rsa_ctx {
   unsigned long long* d_hits = nullptr;
   unsigned int* d_distinct = nullptr;
   unsigned long long* d_thresh = nullptr;
+  unsigned long long* d_filter = nullptr;  // library-owned, n_rules
+  uint32_t filter_len = 0;
+  bool auto_tighten = true;
+  bool tightened = false;
   Slot* d_slots = nullptr;
   unsigned long long slot_cap = 0;    // power of two
   unsigned long long slot_alloc = 0;  // allocated slots
@@ -444,10 +488,15 @@ struct rsa_ctx {
   uint32_t* d_cidx = nullptr;
   uint32_t cidx_len = 0;
   uint32_t* d_capped_gid = nullptr;
-  unsigned long long* d_prefix = nullptr;
-  uint32_t* d_rank = nullptr;
-  unsigned int* d_hist = nullptr;
+  uint32_t* d_capped_cnt = nullptr;
+  uint32_t* d_capped_start = nullptr;
   uint32_t capped_alloc = 0;
+  // sort scratch (capped entries)
+  unsigned long long* d_keys[2] = {nullptr, nullptr};
+  uint32_t* d_vals[2] = {nullptr, nullptr};
+  unsigned long long sort_alloc = 0;
+  void* d_temp = nullptr;
+  size_t temp_alloc = 0;
   int cu_count = 256;
   std::string err;
 };
@@ -485,6 +534,7 @@ Agg agg_of(const rsa_ctx* c) {
   a.hits = c->d_hits;
   a.distinct = c->d_distinct;
   a.thresh = c->d_thresh;
+  a.filter = c->d_filter;
   a.slots = c->d_slots;
   a.mask = c->slot_cap ? c->slot_cap - 1 : 0;
   a.flags = c->d_flags;
@@ -520,6 +570,9 @@ int need_agg(rsa_ctx* c) {
 }
 
 }  // namespace
+
+static int run_pass1(rsa_ctx* c, int mode, const rsa_tuple* T, const uint32_t* TS, const uint64_t* ORD,
+                     const int32_t* G, int32_t* gout, uint64_t n);
 
 extern "C" {
 
@@ -559,9 +612,14 @@ int rsa_ctx_destroy(rsa_ctx* c) {
   hipFree(c->d_cursor);
   hipFree(c->d_cidx);
   hipFree(c->d_capped_gid);
-  hipFree(c->d_prefix);
-  hipFree(c->d_rank);
-  hipFree(c->d_hist);
+  hipFree(c->d_capped_cnt);
+  hipFree(c->d_capped_start);
+  hipFree(c->d_filter);
+  hipFree(c->d_keys[0]);
+  hipFree(c->d_keys[1]);
+  hipFree(c->d_vals[0]);
+  hipFree(c->d_vals[1]);
+  hipFree(c->d_temp);
   delete c;
   return RSA_OK;
 }
@@ -654,6 +712,16 @@ int rsa_reset(rsa_ctx* c, uint64_t capacity, uint32_t cap) {
     HIPCHK(c, hipMemsetAsync(c->d_distinct, 0, nr * sizeof(unsigned int), c->stream));
     HIPCHK(c, hipMemsetAsync(c->d_thresh, 0xFF, nr * sizeof(unsigned long long), c->stream));
   }
+  if (c->filter_len < nr || !c->d_filter) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    hipFree(c->d_filter);
+    c->d_filter = nullptr;
+    c->filter_len = 0;
+    HIPCHK(c, hipMalloc(&c->d_filter, (nr ? nr : 1) * sizeof(unsigned long long)));
+    c->filter_len = nr ? (uint32_t)nr : 1;
+  }
+  HIPCHK(c, hipMemsetAsync(c->d_filter, 0xFF, (nr ? nr : 1) * sizeof(unsigned long long), c->stream));
+  c->tightened = false;
   HIPCHK(c, hipMemsetAsync(c->d_flags, 0, 4 * sizeof(unsigned int), c->stream));
   c->table_ready = true;
   return RSA_OK;
@@ -666,9 +734,17 @@ int rsa_classify(rsa_ctx* c, const rsa_tuple* T, const uint32_t* TS, const uint6
   if (rc) return rc;
   if (n == 0) return RSA_OK;
   if (!T || !TS || !ORD) return fail(c, RSA_ERR_ARG, "null tuple/ts/order pointer");
-  k_pass1<false><<<grid_for(c, n, 16), kBlock, 0, c->stream>>>(
-      reinterpret_cast<const uint4*>(T), TS, reinterpret_cast<const unsigned long long*>(ORD), n, nullptr, gout,
-      rules_of(c), agg_of(c));
+  return run_pass1(c, kClassifyAgg, T, TS, ORD, nullptr, gout, n);
+}
+
+int rsa_classify_only(rsa_ctx* c, const rsa_tuple* T, uint64_t n, int32_t* gout) {
+  if (!c) return RSA_ERR_ARG;
+  if (!c->rules_loaded) return fail(c, RSA_ERR_STATE, "no rules loaded");
+  if (n == 0) return RSA_OK;
+  if (!T || !gout) return fail(c, RSA_ERR_ARG, "null tuple/gid pointer");
+  Agg a = agg_of(c);
+  k_pass1<kClassifyOnly><<<grid_for(c, n, 16), kBlock, 0, c->stream>>>(reinterpret_cast<const uint4*>(T), nullptr,
+                                                                      nullptr, n, nullptr, gout, rules_of(c), a);
   HIPCHK(c, hipGetLastError());
   return RSA_OK;
 }
@@ -680,10 +756,96 @@ int rsa_aggregate_gids(rsa_ctx* c, const rsa_tuple* T, const uint32_t* TS, const
   if (rc) return rc;
   if (n == 0) return RSA_OK;
   if (!T || !TS || !ORD || !G) return fail(c, RSA_ERR_ARG, "null tuple/ts/order/gid pointer");
-  Rules r = rules_of(c);
-  k_pass1<true><<<grid_for(c, n, 16), kBlock, 0, c->stream>>>(
-      reinterpret_cast<const uint4*>(T), TS, reinterpret_cast<const unsigned long long*>(ORD), n, G, nullptr, r,
-      agg_of(c));
+  return run_pass1(c, kGivenAgg, T, TS, ORD, G, nullptr, n);
+}
+
+static int ensure_temp(rsa_ctx* c, size_t bytes) {
+  if (bytes <= c->temp_alloc) return RSA_OK;
+  hipFree(c->d_temp);
+  c->d_temp = nullptr;
+  c->temp_alloc = 0;
+  HIPCHK(c, hipMalloc(&c->d_temp, bytes));
+  c->temp_alloc = bytes;
+  return RSA_OK;
+}
+
+// Exact selection of P for every rule with >= cap distinct entries in the
+// current table, written to out[] (RSA_NO_THRESHOLD for the others).  On the
+// final table this is the reducer's cap threshold; on a partial table it is an
+// upper bound of it (the filter), because first-seen orders only decrease and
+// the set of connections only grows as more lines are aggregated.
+static int cap_select(rsa_ctx* c, unsigned long long* out, uint32_t* h_n_capped) {
+  int rc = check_flags(c);
+  if (rc) return rc;
+  const uint32_t nr = c->n_rules;
+  *h_n_capped = 0;
+  if (nr == 0) return RSA_OK;
+  if (c->cidx_len < nr) {
+    hipFree(c->d_cidx);
+    hipFree(c->d_capped_gid);
+    hipFree(c->d_capped_cnt);
+    hipFree(c->d_capped_start);
+    c->d_cidx = c->d_capped_gid = c->d_capped_cnt = c->d_capped_start = nullptr;
+    c->cidx_len = 0;
+    HIPCHK(c, hipMalloc(&c->d_cidx, (size_t)nr * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(&c->d_capped_gid, (size_t)nr * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(&c->d_capped_cnt, (size_t)nr * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(&c->d_capped_start, (size_t)nr * sizeof(uint32_t)));
+    c->cidx_len = nr;
+  }
+  unsigned int* d_ncap = c->d_flags + 2;
+  HIPCHK(c, hipMemsetAsync(d_ncap, 0, sizeof(unsigned int), c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_cursor, 0, sizeof(unsigned long long), c->stream));
+  k_cap_mark<<<(nr + kBlock - 1) / kBlock, kBlock, 0, c->stream>>>(c->d_distinct, nr, c->cap, c->d_cidx,
+                                                                   c->d_capped_gid, c->d_capped_cnt, d_ncap, out);
+  HIPCHK(c, hipGetLastError());
+  unsigned int ncap = 0;
+  HIPCHK(c, hipMemcpyAsync(&ncap, d_ncap, sizeof ncap, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  *h_n_capped = ncap;
+  if (ncap == 0) return RSA_OK;
+  // upper bound on capped entries: every used slot
+  unsigned long long bound = c->slot_cap;
+  if (c->sort_alloc < bound) {
+    for (int k = 0; k < 2; ++k) {
+      hipFree(c->d_keys[k]);
+      hipFree(c->d_vals[k]);
+      c->d_keys[k] = nullptr;
+      c->d_vals[k] = nullptr;
+    }
+    c->sort_alloc = 0;
+    for (int k = 0; k < 2; ++k) {
+      HIPCHK(c, hipMalloc(&c->d_keys[k], bound * sizeof(unsigned long long)));
+      HIPCHK(c, hipMalloc(&c->d_vals[k], bound * sizeof(uint32_t)));
+    }
+    c->sort_alloc = bound;
+  }
+  k_cap_collect<<<grid_for(c, c->slot_cap, 8), kBlock, 0, c->stream>>>(c->d_slots, c->slot_cap, c->d_cidx,
+                                                                       c->d_keys[0], c->d_vals[0], c->d_cursor);
+  HIPCHK(c, hipGetLastError());
+  unsigned long long m = 0;
+  HIPCHK(c, hipMemcpyAsync(&m, c->d_cursor, sizeof m, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (m > 0xFFFFFFFFull) return fail(c, RSA_ERR_CAPACITY, "more than 2^32 capped entries");
+  int cbits = 1;
+  while (cbits < 32 && (1ull << cbits) < ncap) ++cbits;
+  // sort by min_order, then stably by capped index; exclusive scan of segment sizes
+  hipcub::DoubleBuffer<unsigned long long> keys(c->d_keys[0], c->d_keys[1]);
+  hipcub::DoubleBuffer<uint32_t> vals(c->d_vals[0], c->d_vals[1]);
+  size_t t1 = 0, t2 = 0, t3 = 0;
+  HIPCHK(c, hipcub::DeviceRadixSort::SortPairs(nullptr, t1, keys, vals, (int)m, 0, 64, c->stream));
+  HIPCHK(c, hipcub::DeviceRadixSort::SortPairs(nullptr, t2, vals, keys, (int)m, 0, cbits, c->stream));
+  HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, t3, c->d_capped_cnt, c->d_capped_start, (int)ncap, c->stream));
+  size_t tb = t1 > t2 ? t1 : t2;
+  if (t3 > tb) tb = t3;
+  rc = ensure_temp(c, tb);
+  if (rc) return rc;
+  HIPCHK(c, hipcub::DeviceRadixSort::SortPairs(c->d_temp, tb, keys, vals, (int)m, 0, 64, c->stream));
+  HIPCHK(c, hipcub::DeviceRadixSort::SortPairs(c->d_temp, tb, vals, keys, (int)m, 0, cbits, c->stream));
+  HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(c->d_temp, tb, c->d_capped_cnt, c->d_capped_start, (int)ncap,
+                                             c->stream));
+  k_cap_pick<<<(ncap + kBlock - 1) / kBlock, kBlock, 0, c->stream>>>(keys.Current(), c->d_capped_start,
+                                                                     c->d_capped_gid, ncap, c->cap, out);
   HIPCHK(c, hipGetLastError());
   return RSA_OK;
 }
@@ -692,66 +854,41 @@ int rsa_resolve_cap(rsa_ctx* c, uint32_t* h_n_capped) {
   if (!c || !h_n_capped) return RSA_ERR_ARG;
   int rc = need_agg(c);
   if (rc) return rc;
-  rc = check_flags(c);
-  if (rc) return rc;
-  const uint32_t nr = c->n_rules;
-  *h_n_capped = 0;
-  if (nr == 0) return RSA_OK;
-  if (c->cidx_len < nr) {
-    hipFree(c->d_cidx);
-    hipFree(c->d_capped_gid);
-    c->d_cidx = nullptr;
-    c->d_capped_gid = nullptr;
-    c->cidx_len = 0;
-    HIPCHK(c, hipMalloc(&c->d_cidx, (size_t)nr * sizeof(uint32_t)));
-    HIPCHK(c, hipMalloc(&c->d_capped_gid, (size_t)nr * sizeof(uint32_t)));
-    c->cidx_len = nr;
-  }
-  unsigned int* d_ncap = c->d_flags + 2;
-  HIPCHK(c, hipMemsetAsync(d_ncap, 0, sizeof(unsigned int), c->stream));
-  k_cap_mark<<<(nr + kBlock - 1) / kBlock, kBlock, 0, c->stream>>>(c->d_distinct, nr, c->cap, c->d_cidx,
-                                                                   c->d_capped_gid, d_ncap, c->d_thresh);
-  HIPCHK(c, hipGetLastError());
-  unsigned int ncap = 0;
-  HIPCHK(c, hipMemcpyAsync(&ncap, d_ncap, sizeof ncap, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  *h_n_capped = ncap;
-  if (ncap == 0) return RSA_OK;
-  if (c->capped_alloc < ncap) {
-    hipFree(c->d_prefix);
-    hipFree(c->d_rank);
-    hipFree(c->d_hist);
-    c->d_prefix = nullptr;
-    c->d_rank = nullptr;
-    c->d_hist = nullptr;
-    c->capped_alloc = 0;
-    HIPCHK(c, hipMalloc(&c->d_prefix, (size_t)ncap * sizeof(unsigned long long)));
-    HIPCHK(c, hipMalloc(&c->d_rank, (size_t)ncap * sizeof(uint32_t)));
-    HIPCHK(c, hipMalloc(&c->d_hist, (size_t)ncap * 256 * sizeof(unsigned int)));
-    c->capped_alloc = ncap;
-  }
-  HIPCHK(c, hipMemsetAsync(c->d_prefix, 0, (size_t)ncap * sizeof(unsigned long long), c->stream));
-  HIPCHK(c, hipMemsetAsync(c->d_hist, 0, (size_t)ncap * 256 * sizeof(unsigned int), c->stream));
-  // rank = cap (1-based rank of the cap-th smallest min_order)
-  {
-    uint32_t* tmp = new uint32_t[ncap];
-    for (uint32_t i = 0; i < ncap; ++i) tmp[i] = c->cap;
-    hipError_t e = hipMemcpyAsync(c->d_rank, tmp, (size_t)ncap * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    delete[] tmp;
-    if (e != hipSuccess) return fail(c, RSA_ERR_HIP, "rank upload: %s", hipGetErrorString(e));
-  }
-  for (int pass = 0; pass < 8; ++pass) {
-    k_sel_hist<<<grid_for(c, c->slot_cap, 8), kBlock, 0, c->stream>>>(c->d_slots, c->slot_cap, c->d_cidx,
-                                                                       c->d_prefix, c->d_hist, pass);
+  return cap_select(c, c->d_thresh, h_n_capped);
+}
+
+// Pass 1 over one batch.  With auto-tightening, a large first batch is split:
+// the first 1/16 builds the table, then the filter (an exact upper bound of each
+// capped rule's threshold) is computed, and the rest of the batch skips the
+// table for lines that cannot change any output.
+static int run_pass1(rsa_ctx* c, int mode, const rsa_tuple* T, const uint32_t* TS, const uint64_t* ORD,
+                     const int32_t* G, int32_t* gout, uint64_t n) {
+  auto launch = [&](uint64_t a, uint64_t m) -> int {
+    const uint4* t = reinterpret_cast<const uint4*>(T) + a;
+    const unsigned long long* o = reinterpret_cast<const unsigned long long*>(ORD) + a;
+    if (mode == kClassifyAgg) {
+      k_pass1<kClassifyAgg><<<grid_for(c, m, 16), kBlock, 0, c->stream>>>(t, TS + a, o, m, nullptr,
+                                                                          gout ? gout + a : nullptr, rules_of(c),
+                                                                          agg_of(c));
+    } else {
+      k_pass1<kGivenAgg><<<grid_for(c, m, 16), kBlock, 0, c->stream>>>(t, TS + a, o, m, G + a, nullptr,
+                                                                       rules_of(c), agg_of(c));
+    }
     HIPCHK(c, hipGetLastError());
-    k_sel_pick<<<(ncap + 63) / 64, 64, 0, c->stream>>>(c->d_hist, c->d_prefix, c->d_rank, ncap);
-    HIPCHK(c, hipGetLastError());
+    return RSA_OK;
+  };
+  const uint64_t kMinSplit = 1ull << 22;
+  if (c->auto_tighten && !c->tightened && c->cap > 0 && n >= kMinSplit) {
+    const uint64_t first = n / 16;
+    int rc = launch(0, first);
+    if (rc) return rc;
+    uint32_t ncap = 0;
+    rc = cap_select(c, c->d_filter, &ncap);
+    if (rc) return rc;
+    c->tightened = true;
+    return launch(first, n - first);
   }
-  k_sel_store<<<(ncap + kBlock - 1) / kBlock, kBlock, 0, c->stream>>>(c->d_prefix, c->d_capped_gid, ncap,
-                                                                      c->d_thresh);
-  HIPCHK(c, hipGetLastError());
-  return RSA_OK;
+  return launch(0, n);
 }
 
 int rsa_recount(rsa_ctx* c, const rsa_tuple* T, const uint32_t* TS, const uint64_t* ORD, const int32_t* G,

@@ -176,11 +176,11 @@ class Engine(object):
         self.last_gids = gid_bufs
         return self.results(cap)
 
-    def classify_only(self, b):
-        """gid per tuple (mapper drop-in); counters/table are updated as a side effect."""
+    def classify_only(self, b, out=None):
+        """First-match gid per tuple (mapper drop-in); no aggregation."""
         torch = self.torch
-        g = torch.empty(b.n, dtype=torch.int32, device=self.device)
-        self.pass1(b, g)
+        g = out if out is not None else torch.empty(b.n, dtype=torch.int32, device=self.device)
+        self.ctx.call('rsa_classify_only', _ptr(b.tuples), ctypes.c_uint64(b.n), _ptr(g))
         return g
 
     def close(self):

@@ -50,6 +50,7 @@ SYMBOLS = {
     'rsa_set_rule_count': (I32, [P, U32]),
     'rsa_reset': (I32, [P, U64, U32]),
     'rsa_classify': (I32, [P, P, P, P, U64, P]),
+    'rsa_classify_only': (I32, [P, P, U64, P]),
     'rsa_aggregate_gids': (I32, [P, P, P, P, P, U64]),
     'rsa_resolve_cap': (I32, [P, PU32]),
     'rsa_recount': (I32, [P, P, P, P, P, U64]),

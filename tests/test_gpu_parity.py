@@ -47,9 +47,14 @@ def test_golden_mapper_stream(engine, case):
     assert hashlib.sha256(text_out.encode('latin-1')).hexdigest() == sha
 
 
-def _gpu_vs_oracle(engine, n_rules, n_lines, cap, seed, zipf=None, interfaces=('outside',), batches=1):
+def _gpu_vs_oracle(engine, n_rules, n_lines, cap, seed, zipf=None, interfaces=('outside',), batches=1,
+                   shuffle=False):
     dbj, info = synth.make_db(seed, n_rules, interfaces=interfaces)
     tr = synth.make_traffic((dbj, info), n_lines, seed=seed + 1, zipf=zipf)
+    if shuffle:   # input order no longer follows the sort order
+        perm = np.random.default_rng(seed).permutation(n_lines)
+        for k in ('src', 'dst', 'sport', 'dport', 'proto', 'ifc', 'form', 't', 'cid'):
+            tr[k] = tr[k][perm]
     db = acldb.load_json(dbj)
     compiled = CompiledRules(db)
     tup, ts, order = synth.pack(tr, compiled)
@@ -107,6 +112,17 @@ def test_synth_parity_cap1(engine):
 
 def test_synth_parity_10k_rules(engine):
     _gpu_vs_oracle(engine, 10000, 150000, 1000, seed=15)
+
+
+def test_synth_parity_tightened_filter(engine):
+    # > 4M lines in one batch: the library aggregates 1/16, derives the per-rule
+    # filter, and skips the table for lines beyond it
+    res, ref = _gpu_vs_oracle(engine, 800, 5_000_000, 40, seed=16, zipf=1.2)
+    assert (ref['n_conns'] >= 40).sum() > 0           # the cap is engaged
+
+
+def test_synth_parity_tightened_filter_shuffled(engine):
+    _gpu_vs_oracle(engine, 800, 5_000_000, 40, seed=17, zipf=1.2, shuffle=True)
 
 
 def test_deterministic(engine):
