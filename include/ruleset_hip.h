@@ -61,6 +61,35 @@ typedef struct rsa_rule_entry {
   uint32_t reserved;
 } rsa_rule_entry;
 
+/* Tuple-space-search index (optional).  For one candidate list, the entries
+ * whose addresses are prefixes and whose ports are "any" or one value are
+ * grouped by shape (src mask, dst mask, port mask); each shape owns an
+ * open-addressing table of 16-B slots keyed by the masked (src, dst, ports)
+ * whose value is the smallest gid with that key.  Shapes of a list are stored
+ * in ascending min_gid order; entries that fit no shape (port ranges, odd
+ * address ranges) stay in a per-list residual list scanned linearly.  The
+ * answer is identical to the linear scan: the minimum matching gid. */
+typedef struct rsa_shape {
+  uint32_t src_mask, dst_mask; /* address prefix masks                       */
+  uint32_t port_mask;          /* 0xFFFF per exact port half, 0 for "any"     */
+  uint32_t min_gid;            /* smallest gid in the shape                  */
+  uint32_t table_off;          /* first slot of this shape's table           */
+  uint32_t table_mask;         /* table size - 1 (power of two)              */
+  uint32_t salt;               /* hash salt (unique per shape)               */
+  uint32_t reserved;
+} rsa_shape;
+
+typedef struct rsa_index_slot {
+  uint32_t src, dst, ports; /* masked key; ports = sport | dport << 16 */
+  uint32_t gid;             /* 0xFFFFFFFF = empty                     */
+} rsa_index_slot;
+
+/* Options (rsa_set_option). */
+#define RSA_OPT_AUTO_FILTER 1 /* split a large first batch to derive the exact per-rule insert filter (default 1) */
+#define RSA_OPT_USE_INDEX 2   /* classify with the loaded index (1) or the linear lists (0)                  */
+#define RSA_OPT_SCAN_PREFIX 4  /* linear scan: list entries scanned before a lane is deferred (default 256) */
+#define RSA_OPT_PROFILE_SKIP 3 /* PROFILING ONLY, results invalid: bit0 skips counters, bit1 skips the table  */
+
 /* One distinct (rule, connection) aggregate, 40 B (connlist-reducer.py:162-176). */
 typedef struct rsa_conn_record {
   uint64_t min_order; /* smallest order key (first occurrence in sort order) */
@@ -84,6 +113,7 @@ int rsa_ctx_create(int device, rsa_ctx **out);
 int rsa_ctx_destroy(rsa_ctx *ctx);
 const char *rsa_last_error(const rsa_ctx *ctx);
 int rsa_set_stream(rsa_ctx *ctx, void *hip_stream);
+int rsa_set_option(rsa_ctx *ctx, int option, int64_t value);
 int rsa_version(void);
 
 /* Upload compiled candidate lists (host arrays).  list_offsets has n_lists+1
@@ -92,6 +122,13 @@ int rsa_version(void);
  * the number of global rule ids (counter length). */
 int rsa_load_rules(rsa_ctx *ctx, const rsa_rule_entry *h_entries, uint32_t n_entries,
                    const uint32_t *h_list_offsets, uint32_t n_lists, uint32_t n_rules);
+
+/* Upload a tuple-space-search index over the lists of rsa_load_rules (same
+ * list ids).  shape_off / resid_off have n_lists+1 entries.  Enables
+ * RSA_OPT_USE_INDEX. */
+int rsa_load_index(rsa_ctx *ctx, const rsa_shape *h_shapes, uint32_t n_shapes, const uint32_t *h_shape_off,
+                   const rsa_index_slot *h_slots, uint64_t n_slots, const rsa_rule_entry *h_resid, uint32_t n_resid,
+                   const uint32_t *h_resid_off);
 
 /* Bind caller-owned device counters, each n_rules long (n_rules from
  * rsa_load_rules, or rsa_set_rule_count when no rules are loaded):
@@ -124,6 +161,10 @@ int rsa_classify_only(rsa_ctx *ctx, const rsa_tuple *d_tuples, uint64_t n, int32
  * comes from the mapper's output line, connlist-reducer.py:63-75). */
 int rsa_aggregate_gids(rsa_ctx *ctx, const rsa_tuple *d_tuples, const uint32_t *d_ts, const uint64_t *d_order,
                        const int32_t *d_gid, uint64_t n);
+
+/* Device time (ms, HIP events on the ctx stream) of the pass-1 kernel launches
+ * of the last rsa_classify / rsa_aggregate_gids call (waits for them). */
+int rsa_last_pass1_ms(rsa_ctx *ctx, float *h_ms);
 
 /* Resolve the cap (connlist-reducer.py:151): for every rule with
  * distinct >= cap, P = the order key of the line that inserted the cap-th

@@ -165,6 +165,13 @@ class CompiledRules(object):
     def n_lists(self):
         return len(self._lists)
 
+    def index(self):
+        """Tuple-space-search index of the current lists (cached until a list is added)."""
+        if getattr(self, '_index', None) is None or self._index[0] is not self._packed:
+            ent, off = self.packed()
+            self._index = (self._packed, build_index(ent, off))
+        return self._index[1]
+
     def ensure_lists(self, protos=('tcp', 'udp')):
         """Pre-build the lists the traffic is expected to need, skipping any the
         mapper would fail on (they are raised lazily at the offending line)."""
@@ -174,3 +181,102 @@ class CompiledRules(object):
                     self.list_id(host, acl, p)
                 except KeyError:
                     pass
+
+
+# ---- tuple-space-search index ------------------------------------------------------
+SHAPE_DTYPE = np.dtype([('src_mask', '<u4'), ('dst_mask', '<u4'), ('port_mask', '<u4'), ('min_gid', '<u4'),
+                        ('table_off', '<u4'), ('table_mask', '<u4'), ('salt', '<u4'), ('reserved', '<u4')])
+ISLOT_DTYPE = np.dtype([('src', '<u4'), ('dst', '<u4'), ('ports', '<u4'), ('gid', '<u4')])
+assert SHAPE_DTYPE.itemsize == 32 and ISLOT_DTYPE.itemsize == 16
+M32 = 0xFFFFFFFF
+
+
+def index_hash(s, d, p, salt):
+    """Must equal index_hash() in csrc/ruleset_hip.hip (uint32 arithmetic)."""
+    s, d, p, salt = (np.asarray(x, dtype=np.uint32) for x in (s, d, p, salt))
+    with np.errstate(over='ignore'):
+        h = (s * np.uint32(0x9E3779B1)) ^ (d * np.uint32(0x85EBCA77)) ^ (p * np.uint32(0xC2B2AE3D)) ^ \
+            (salt * np.uint32(0x27D4EB2F))
+        h ^= h >> np.uint32(15)
+        h *= np.uint32(0x2C1B3C6D)
+        h ^= h >> np.uint32(12)
+        h *= np.uint32(0x297A2D39)
+        h ^= h >> np.uint32(15)
+    return h
+
+
+def _prefix_mask(lo, span):
+    """32-bit mask if [lo, lo+span] is an aligned prefix block, else None."""
+    size = int(span) + 1
+    if size & (size - 1) or int(lo) % size:
+        return None
+    return (M32 ^ (size - 1)) & M32
+
+
+def _port_mask(lo, span):
+    if lo == 0 and span == 0xFFFF:
+        return 0
+    if span == 0:
+        return 0xFFFF
+    return None
+
+
+def build_index(ent, off, probe_cost=8):
+    """Tuple-space-search index over packed lists (rsa_load_index arrays).
+
+    Returns (shapes, shape_off, slots, resid, resid_off).  Per list, the index is
+    used only when it is cheaper than scanning (n_shapes * probe_cost + residual
+    < entries); otherwise every entry of the list stays residual (a plain scan)."""
+    shapes, shape_off, slot_parts, resid_parts, resid_off = [], [0], [], [], [0]
+    n_slots = 0
+    salt = 1
+    for L in range(len(off) - 1):
+        e = ent[off[L]:off[L + 1]]
+        groups = {}
+        resid_idx = []
+        for k in range(len(e)):
+            x = e[k]
+            sm = _prefix_mask(x['src_lo'], x['src_span'])
+            dm = _prefix_mask(x['dst_lo'], x['dst_span'])
+            pl, ps = int(x['port_lo']), int(x['port_span'])
+            spm = _port_mask(pl & 0xFFFF, ps & 0xFFFF)
+            dpm = _port_mask(pl >> 16, ps >> 16)
+            if sm is None or dm is None or spm is None or dpm is None:
+                resid_idx.append(k)
+                continue
+            pm = spm | (dpm << 16)
+            key = (int(x['src_lo']), int(x['dst_lo']), pl & pm)
+            g = groups.setdefault((sm, dm, pm), {})
+            if key not in g:                 # entries are gid-ascending: first = min gid
+                g[key] = int(x['gid'])
+        use_index = len(groups) * probe_cost + len(resid_idx) < len(e)
+        if not use_index:
+            resid_parts.append(e)
+            resid_off.append(resid_off[-1] + len(e))
+            shape_off.append(shape_off[-1])
+            continue
+        resid_parts.append(e[resid_idx])
+        resid_off.append(resid_off[-1] + len(resid_idx))
+        order = sorted(groups.items(), key=lambda kv: min(kv[1].values()))
+        for (sm, dm, pm), keys in order:
+            size = 2
+            while size < 2 * len(keys):
+                size <<= 1
+            tab = np.zeros(size, dtype=ISLOT_DTYPE)
+            tab['gid'] = M32
+            ks = np.array(list(keys.keys()), dtype=np.uint64).astype(np.uint32).reshape(-1, 3)
+            gs = np.array(list(keys.values()), dtype=np.uint32)
+            hs = index_hash(ks[:, 0], ks[:, 1], ks[:, 2], salt) & np.uint32(size - 1)
+            for (a, b, c), g, h in zip(ks.tolist(), gs.tolist(), hs.tolist()):
+                while tab['gid'][h] != M32:
+                    h = (h + 1) & (size - 1)
+                tab[h] = (a, b, c, g)
+            shapes.append((sm, dm, pm, min(keys.values()), n_slots, size - 1, salt, 0))
+            slot_parts.append(tab)
+            n_slots += size
+            salt += 1
+        shape_off.append(len(shapes))
+    shp = np.array(shapes, dtype=SHAPE_DTYPE) if shapes else np.zeros(0, SHAPE_DTYPE)
+    slots = np.concatenate(slot_parts) if slot_parts else np.zeros(0, ISLOT_DTYPE)
+    resid = np.concatenate(resid_parts) if resid_parts else np.zeros(0, RULE_DTYPE)
+    return (shp, np.array(shape_off, np.uint32), slots, resid, np.array(resid_off, np.uint32))

@@ -1,26 +1,35 @@
 // ruleset_hip.hip — MI355X (gfx950, CDNA4) hot path of ruleset-analysis.
 //
 // What the reference does per log line (Python 2, one process per Hadoop split):
-//   mapper.py:159-189        build the candidate rule list, scan it with
-//                            FirewallRule.__contains__ (firewallrule.py:128-174),
-//                            emit the FIRST matching expanded rule index;
+//   mapper.py:159-189           build the candidate rule list, scan it with
+//                               FirewallRule.__contains__ (firewallrule.py:128-174),
+//                               emit the FIRST matching expanded rule index;
 //   connlist-reducer.py:62-176  per rule: count lines, count "hits"
-//                            (-6-302013/-6-302015), keep a distinct-connection
-//                            dict capped at MAX_NUMBER_OF_CONNECTIONS_PER_RULE
-//                            (config.py:15) in sorted-line order.
+//                               (-6-302013/-6-302015), keep a distinct-connection
+//                               dict capped at MAX_NUMBER_OF_CONNECTIONS_PER_RULE
+//                               (config.py:15), in sorted-line order.
 //
-// What this library does instead (integer work, HBM/VALU bound, no MFMA):
-//   pass 1  one lane per tuple; a wave "waterfalls" over the distinct candidate
-//           lists present in it, so rule entries are wave-uniform and come in
-//           through the scalar cache; the first match is the minimum matching
-//           gid (lists are gid-sorted); per-rule counters and a distinct
-//           (rule, connection) hash table are updated with device atomics.
-//   cap     per capped rule, the order key of the line that inserted the
-//           cap-th distinct connection, by an 8-pass radix select over the
-//           table's per-entry minimum order keys.
-//   pass 2  recount (count/first/last) of occurrences with order <= P for the
-//           capped rules only — the exact restatement of the frozen dict.
-//   emit    compact the table to rsa_conn_record rows.
+// What this library does instead (integer work; HBM/atomic/VALU bound; no MFMA):
+//   classify  one lane per tuple.  Either a linear scan of the (host, acl,
+//             protocol) candidate list — a wave "waterfalls" over the distinct
+//             lists present in it so the entries are wave-uniform scalar loads —
+//             or a tuple-space-search index: one exact-match hash probe per rule
+//             shape (src prefix, dst prefix, port kinds), shapes visited in
+//             ascending min-gid order and abandoned once every lane holds a
+//             smaller match, plus a scan of the few residual rules.  Both return
+//             the minimum matching gid = the reference's first match.
+//   pass 1    per-rule line/hit counters (wave-aggregated device atomics) and an
+//             open-addressing (rule, connection) table in HBM keyed by device
+//             atomics; new entries are appended to a compact used-slot list.
+//   filter    after the first slice of a large batch, each rule that already has
+//             >= cap connections gets an exact upper bound F of its threshold;
+//             later lines with order > F cannot change any output and skip the
+//             table.
+//   cap       P = cap-th smallest first-seen order of a rule (two LSD radix
+//             sorts of the capped entries), the reducer's frozen-dict point.
+//   pass 2    recount (count/first/last) of occurrences with order <= P for the
+//             capped rules only.
+//   emit      compact the used slots to rsa_conn_record rows.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -38,31 +47,40 @@ constexpr unsigned long long kBusy = 0xFFFFFFFFFFFFFFFEull;
 constexpr uint32_t kNoGid = 0xFFFFFFFFu;
 constexpr int kBlock = 256;
 
-// One distinct (rule, connection) aggregate in HBM, 64 B (one half L2 line).
+// One distinct (rule, connection) aggregate in HBM, 64 B.
 struct alignas(64) Slot {
   unsigned long long kA;         // for_ip << 32 | to_ip
   unsigned long long kB;         // gid << 32 | pspell << 16 | to_port ; kEmpty / kBusy
   unsigned long long min_order;  // first occurrence (reducer input order)
-  unsigned int count, first, last;      // pass-1 aggregates (all occurrences)
+  unsigned int count, first, last;      // pass-1 aggregates
   unsigned int count2, first2, last2;   // pass-2 aggregates (order <= P only)
   unsigned int pad[4];
 };
 static_assert(sizeof(Slot) == 64, "slot layout");
 static_assert(sizeof(rsa_tuple) == 16, "tuple layout");
 static_assert(sizeof(rsa_rule_entry) == 32, "rule layout");
+static_assert(sizeof(rsa_shape) == 32, "shape layout");
+static_assert(sizeof(rsa_index_slot) == 16, "index slot layout");
 static_assert(sizeof(rsa_conn_record) == 40, "record layout");
 
-// Rule entries are read through the constant address space so that wave-uniform
+// Rule data is read through the constant address space so that wave-uniform
 // loads become scalar (s_load) loads through the scalar cache.
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(4))) const v4u const_uint4;
+typedef __attribute__((address_space(4))) const v4u const_v4u;
 typedef __attribute__((address_space(4))) const uint32_t const_u32;
 
 struct Rules {
-  const const_uint4* e;   // 2 x uint4 per entry
-  const const_u32* off;
+  const const_v4u* e;     // linear entries, 2 x v4u each
+  const const_u32* off;   // n_lists + 1
   uint32_t n_lists;
   uint32_t n_rules;
+  // tuple-space-search index (optional)
+  const const_v4u* shapes;      // 2 x v4u each: {smask, dmask, pmask, min_gid}, {toff, tmask, salt, pad}
+  const const_u32* shape_off;   // n_lists + 1
+  const uint4* __restrict__ islots;
+  const const_v4u* resid;       // residual linear entries
+  const const_u32* resid_off;   // n_lists + 1
+  int indexed;
 };
 
 struct Agg {
@@ -70,11 +88,14 @@ struct Agg {
   unsigned long long* hits;
   unsigned int* distinct;
   const unsigned long long* thresh;
-  const unsigned long long* filter;  // per rule: lines with order > filter cannot matter (cap)
+  const unsigned long long* filter;  // per rule: lines with order > filter cannot matter
   Slot* slots;
-  unsigned long long mask;  // capacity - 1 (power of two)
-  unsigned int* flags;      // [0] overflow, [1] bad gid/list
+  unsigned long long mask;           // capacity - 1 (power of two)
+  uint32_t* used;                    // used-slot list
+  unsigned long long* used_n;
+  unsigned int* flags;               // [0] overflow, [1] bad gid/list/state
   uint32_t cap;
+  uint32_t skip;                     // profiling only (RSA_OPT_PROFILE_SKIP): 1 counters, 2 table
 };
 
 __device__ __forceinline__ unsigned long long mix64(unsigned long long x) {
@@ -88,6 +109,17 @@ __device__ __forceinline__ unsigned long long mix64(unsigned long long x) {
 
 __device__ __forceinline__ unsigned long long slot_hash(unsigned long long kA, unsigned long long kB) {
   return mix64(kA ^ (kB * 0x9e3779b97f4a7c15ull));
+}
+
+// Hash of a tuple-space-search key; must equal compile.py's index_hash.
+__host__ __device__ __forceinline__ uint32_t index_hash(uint32_t s, uint32_t d, uint32_t p, uint32_t salt) {
+  uint32_t h = s * 0x9E3779B1u ^ (d * 0x85EBCA77u) ^ (p * 0xC2B2AE3Du) ^ (salt * 0x27D4EB2Fu);
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 12;
+  h *= 0x297A2D39u;
+  h ^= h >> 15;
+  return h;
 }
 
 // counter[key] += 1 for every lane with `ok`, one device atomic per distinct key
@@ -105,6 +137,19 @@ __device__ __forceinline__ void wave_count_by_key(bool ok, uint32_t key, T* coun
   }
 }
 
+// Wave-aggregated append to a global cursor: one atomic per wave.  Wave-uniform
+// control flow.
+__device__ __forceinline__ unsigned long long wave_append(bool ok, unsigned long long* cursor) {
+  const unsigned long long mask = __ballot(ok);
+  if (mask == 0) return 0;
+  const unsigned lane = __lane_id();
+  const int leader = __builtin_ctzll(mask);
+  unsigned long long base = 0;
+  if ((int)lane == leader) base = atomicAdd(cursor, (unsigned long long)__popcll(mask));
+  base = __shfl(base, leader);
+  return base + __popcll(mask & ((1ull << lane) - 1ull));
+}
+
 // Reducer key of a tuple (connlist-reducer.py:162: PROTO;FROMIP;TOIP;TOPORT).
 __device__ __forceinline__ void conn_key(uint4 t, uint32_t gid, unsigned long long& kA, unsigned long long& kB) {
   const uint32_t flags = (t.w >> 16) & 0xFFu;
@@ -117,10 +162,73 @@ __device__ __forceinline__ void conn_key(uint4 t, uint32_t gid, unsigned long lo
   kB = ((unsigned long long)gid << 32) | ((unsigned long long)pspell << 16) | to_port;
 }
 
-// First-match classification of one wave of tuples.  Entry loads are wave-uniform
-// (list id broadcast by readlane), so they are scalar loads through the K$.
-__device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Rules& R, unsigned int* flags) {
-  uint32_t list = t.w & 0xFFFFu;
+// The integer form of FirewallRule.__contains__ for a compiled entry.
+__device__ __forceinline__ bool entry_match(v4u a, v4u b, uint32_t src, uint32_t dst, uint32_t sp, uint32_t dp) {
+  return ((src - a.x) <= a.y) & ((dst - a.z) <= a.w) & ((sp - (b.x & 0xFFFFu)) <= (b.y & 0xFFFFu)) &
+         ((dp - (b.x >> 16)) <= (b.y >> 16));
+}
+
+// Linear first-match scan of entries [beg, end) for the `mine` lanes.
+__device__ __forceinline__ uint32_t scan_list(const const_v4u* E, uint32_t beg, uint32_t end, bool mine, uint32_t best,
+                                              uint32_t src, uint32_t dst, uint32_t sp, uint32_t dp) {
+  uint32_t e = beg;
+  for (; e + 4 <= end; e += 4) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const v4u a = E[2 * (e + j)];
+      const v4u b = E[2 * (e + j) + 1];
+      best = min(best, (entry_match(a, b, src, dst, sp, dp) & mine) ? b.z : kNoGid);
+    }
+    // entries are gid-ascending: stop once no searching lane can improve
+    if (__ballot(mine && best > E[2 * (e + 3) + 1].z) == 0) return best;
+  }
+  for (; e < end; ++e) {
+    const v4u a = E[2 * e];
+    const v4u b = E[2 * e + 1];
+    best = min(best, (entry_match(a, b, src, dst, sp, dp) & mine) ? b.z : kNoGid);
+  }
+  return best;
+}
+
+// Tuple-space search for the `mine` lanes of list L.
+__device__ __forceinline__ uint32_t search_index(const Rules& R, uint32_t L, bool mine, uint32_t src, uint32_t dst,
+                                                 uint32_t ports, uint32_t sp, uint32_t dp) {
+  uint32_t best = kNoGid;
+  const uint32_t sb = R.shape_off[L], se = R.shape_off[L + 1];
+  for (uint32_t s = sb; s < se; ++s) {
+    const v4u a = R.shapes[2 * s];       // smask, dmask, pmask, min_gid
+    const v4u b = R.shapes[2 * s + 1];   // toff, tmask, salt
+    // shapes are in ascending min_gid order: once no lane can improve, stop
+    if (__ballot(mine && best > a.w) == 0) break;
+    if (mine && best > a.w) {
+      const uint32_t ks = src & a.x, kd = dst & a.y, kp = ports & a.z;
+      uint32_t h = index_hash(ks, kd, kp, b.z) & b.y;
+      for (uint32_t probe = 0; probe <= b.y; ++probe) {
+        const uint4 q = R.islots[b.x + h];
+        if (q.w == kNoGid) break;
+        if (q.x == ks && q.y == kd && q.z == kp) {
+          best = min(best, q.w);
+          break;
+        }
+        h = (h + 1) & b.y;
+      }
+    }
+  }
+  const uint32_t rb = R.resid_off[L], re = R.resid_off[L + 1];
+  if (rb < re) best = scan_list(R.resid, rb, re, mine, best, src, dst, sp, dp);
+  return best;
+}
+
+constexpr uint32_t kDefer = 0xFFFFFFFEu;
+
+// First-match classification of one wave of tuples: waterfall over the distinct
+// candidate lists present in the wave (list id broadcast by readlane).  With the
+// linear lists, only entries [from, limit) of each list are scanned; a lane with
+// no match there whose list continues past `limit` returns kDefer (the tail
+// kernel finishes it from `limit`, in dense waves).  limit = ~0: whole list.
+__device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Rules& R, unsigned int* flags,
+                                                  uint32_t from = 0, uint32_t limit = 0xFFFFFFFFu) {
+  const uint32_t list = t.w & 0xFFFFu;
   if (active && list >= R.n_lists) {
     atomicOr(&flags[1], 1u);
     active = false;
@@ -134,78 +242,64 @@ __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Ru
     const uint32_t L = __builtin_amdgcn_readlane(list, leader);
     const bool mine = active && list == L;
     pending &= ~__ballot(mine);
-    const uint32_t beg = R.off[L];
-    const uint32_t end = R.off[L + 1];
-    uint32_t e = beg;
-    for (; e + 4 <= end; e += 4) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const v4u a = R.e[2 * (e + j)];
-        const v4u b = R.e[2 * (e + j) + 1];
-        const bool m = ((src - a.x) <= a.y) & ((dst - a.z) <= a.w) &
-                       ((sp - (b.x & 0xFFFFu)) <= (b.y & 0xFFFFu)) & ((dp - (b.x >> 16)) <= (b.y >> 16));
-        best = min(best, (m & mine) ? b.z : kNoGid);
-      }
-      if (__ballot(mine && best == kNoGid) == 0) break;
+    uint32_t b;
+    if (R.indexed) {
+      b = search_index(R, L, mine, src, dst, t.z, sp, dp);
+    } else {
+      const uint32_t beg = R.off[L], end = R.off[L + 1];
+      const uint32_t lo = (end - beg > from) ? beg + from : end;
+      const uint32_t hi = (end - beg > limit) ? beg + limit : end;
+      b = scan_list(R.e, lo, hi, mine, kNoGid, src, dst, sp, dp);
+      if (b == kNoGid && hi < end) b = kDefer;
     }
-    if (e + 4 > end) {
-      for (; e < end; ++e) {
-        const v4u a = R.e[2 * e];
-        const v4u b = R.e[2 * e + 1];
-        const bool m = ((src - a.x) <= a.y) & ((dst - a.z) <= a.w) &
-                       ((sp - (b.x & 0xFFFFu)) <= (b.y & 0xFFFFu)) & ((dp - (b.x >> 16)) <= (b.y >> 16));
-        best = min(best, (m & mine) ? b.z : kNoGid);
-      }
-    }
+    if (mine) best = b;
   }
   return active ? best : kNoGid;
 }
 
-// Insert-or-combine (kA, kB) into the open-addressing table.  All key reads are
-// device atomics (executed beyond the per-XCD L2s, so every XCD sees one value).
-// A slot is claimed EMPTY->BUSY, its kA published, then kB published; a lane
-// that reads BUSY retries the same slot on its next iteration.  Every key word
-// is only ever accessed by device atomics, which execute beyond the per-XCD
-// L2s, so no XCD can observe a stale copy.
-__device__ __forceinline__ bool table_combine(const Agg& A, unsigned long long kA, unsigned long long kB,
-                                              unsigned int cnt, unsigned int first, unsigned int last,
-                                              unsigned long long order) {
-  bool fresh = false;
+// Insert-or-combine (kA, kB) into the open-addressing table.  A slot is claimed
+// EMPTY->BUSY, its kA published, then kB published; a lane that reads BUSY
+// retries the same slot on its next iteration.  Every key word is only ever
+// accessed by device atomics (executed beyond the per-XCD L2s), so no XCD can
+// observe a stale copy.  Returns the slot index (or ~0 on overflow); *fresh is
+// set when this call created the entry.
+__device__ __forceinline__ unsigned long long table_combine(const Agg& A, unsigned long long kA,
+                                                            unsigned long long kB, unsigned int cnt,
+                                                            unsigned int first, unsigned int last,
+                                                            unsigned long long order, bool* fresh) {
   unsigned long long h = slot_hash(kA, kB) & A.mask;
   unsigned long long probes = 0;
-  Slot* s = nullptr;
+  unsigned long long found = kEmpty;
   while (true) {
     Slot* c = &A.slots[h];
     const unsigned long long cur = atomicCAS(&c->kB, kEmpty, kBusy);
     if (cur == kEmpty) {
-      // kA is published by a device atomic; waiting for its completion before the
-      // kB exchange orders the two at the memory side (no cache write-back fence).
+      // publish kA before kB: wait for the kA atomic to complete at the memory side
       atomicExch(&c->kA, kA);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       atomicExch(&c->kB, kB);
-      fresh = true;
-      s = c;
+      *fresh = true;
+      found = h;
       break;
     }
     if (cur == kBusy) continue;
-    if (cur == kB) {
-      if (atomicOr(&c->kA, 0ull) == kA) {
-        s = c;
-        break;
-      }
+    if (cur == kB && atomicOr(&c->kA, 0ull) == kA) {
+      found = h;
+      break;
     }
     h = (h + 1) & A.mask;
     if (++probes > A.mask) break;
   }
-  if (!s) {
+  if (found == kEmpty) {
     atomicOr(&A.flags[0], 1u);
-    return false;
+    return kEmpty;
   }
+  Slot* s = &A.slots[found];
   atomicAdd(&s->count, cnt);
   atomicMin(&s->first, first);
   atomicMax(&s->last, last);
   atomicMin(&s->min_order, order);
-  return fresh;
+  return found;
 }
 
 // Find an existing key (after pass 1 completed: plain loads are coherent across
@@ -226,42 +320,106 @@ __device__ __forceinline__ Slot* table_find(const Agg& A, unsigned long long kA,
 // the gid given per tuple (reducer drop-in), classify only (mapper drop-in).
 enum { kClassifyAgg = 0, kGivenAgg = 1, kClassifyOnly = 2 };
 
-template <int kMode>
-__global__ __launch_bounds__(kBlock) void k_pass1(const uint4* __restrict__ T, const uint32_t* __restrict__ TS,
-                                                  const unsigned long long* __restrict__ ORD, unsigned long long n,
-                                                  const int32_t* __restrict__ gin, int32_t* __restrict__ gout,
-                                                  Rules R, Agg A) {
-  const unsigned long long stride = (unsigned long long)gridDim.x * kBlock;
-  for (unsigned long long base = (unsigned long long)blockIdx.x * kBlock; base < n; base += stride) {
-    const unsigned long long i = base + threadIdx.x;
-    const bool in = i < n;
+// matches[key] += 1 for lanes with `m`, hits[key] += 1 for lanes with `h` (h
+// implies m): one loop over the wave's distinct keys, one device atomic per
+// key and counter.  Wave-uniform control flow.
+__device__ __forceinline__ void wave_count2(bool m, bool h, uint32_t key, unsigned long long* matches,
+                                            unsigned long long* hits) {
+  unsigned long long pending = __ballot(m);
+  const unsigned long long hm = __ballot(h);
+  while (pending) {
+    const int leader = __builtin_ctzll(pending);
+    const uint32_t k = __builtin_amdgcn_readlane(key, leader);
+    const unsigned long long peers = __ballot(m && key == k);
+    pending &= ~peers;
+    if ((int)__lane_id() == leader) {
+      atomicAdd(&matches[k], (unsigned long long)__popcll(peers));
+      const unsigned long long hp = peers & hm;
+      if (hp) atomicAdd(&hits[k], (unsigned long long)__popcll(hp));
+    }
+  }
+}
+
+// Pass 1.  kLds > 0: the per-rule line/hit counters of up to kLds rules are
+// privatised in LDS for the whole (persistent) workgroup and flushed once at the
+// end; otherwise they are wave-aggregated device atomics.  kTail: process the
+// deferred lines (indices in tail[0..*tail_n)) from list position `prefix` on;
+// otherwise scan list prefixes of `prefix` entries and defer the rest.
+template <int kMode, int kThreads, int kLds, bool kTail>
+__global__ __launch_bounds__(kThreads) void k_pass1(const uint4* __restrict__ T, const uint32_t* __restrict__ TS,
+                                                    const unsigned long long* __restrict__ ORD, unsigned long long n,
+                                                    const int32_t* __restrict__ gin, int32_t* __restrict__ gout,
+                                                    Rules R, Agg A, uint32_t prefix, uint32_t* tail,
+                                                    unsigned long long* tail_n) {
+  __shared__ uint32_t lds_cnt[kLds > 0 ? 2 * kLds : 1];
+  const bool counters = kMode != kClassifyOnly && !(A.skip & 1u);
+  if (kLds > 0 && counters) {
+    for (uint32_t r = threadIdx.x; r < 2u * kLds; r += kThreads) lds_cnt[r] = 0;
+    __syncthreads();
+  }
+  if (kTail) n = *tail_n;
+  const unsigned long long stride = (unsigned long long)gridDim.x * kThreads;
+  for (unsigned long long base = (unsigned long long)blockIdx.x * kThreads; base < n; base += stride) {
+    const unsigned long long j = base + threadIdx.x;
+    const bool in = j < n;
+    const unsigned long long i = kTail ? (in ? tail[j] : 0ull) : j;
     const uint4 t = in ? T[i] : make_uint4(0u, 0u, 0u, 0u);
     const uint32_t flags = (t.w >> 16) & 0xFFu;
     uint32_t gid;
     if (kMode == kGivenAgg) {
       gid = in ? (uint32_t)gin[i] : kNoGid;
+    } else if (kTail) {
+      gid = classify_wave(t, in && (flags & RSA_F_VALID), R, A.flags, prefix);
     } else {
-      gid = classify_wave(t, in && (flags & RSA_F_VALID), R, A.flags);
+      gid = classify_wave(t, in && (flags & RSA_F_VALID), R, A.flags, 0, prefix);
     }
-    if (kMode != kGivenAgg && gout && in) gout[i] = (int32_t)gid;
+    if (kMode != kGivenAgg && !kTail) {
+      const bool defer = gid == kDefer;
+      const unsigned long long pos = wave_append(defer, tail_n);
+      if (defer) {
+        tail[pos] = (uint32_t)i;
+        gid = kNoGid;   // finished by the tail kernel: nothing else to do here
+      }
+      if (gout && in && !defer) gout[i] = (int32_t)gid;
+      if (defer) continue;
+    } else if (kMode != kGivenAgg && gout && in) {
+      gout[i] = (int32_t)gid;
+    }
     if (kMode == kClassifyOnly) continue;
     if (gid != kNoGid && gid >= R.n_rules) atomicOr(&A.flags[1], 2u);
     const bool matched = gid < R.n_rules;
     const bool hit = matched && (flags & RSA_F_HIT);
-    wave_count_by_key(matched, gid, A.matches);
-    wave_count_by_key(hit, gid, A.hits);
+    if (counters) {
+      if (kLds > 0) {
+        if (matched) atomicAdd(&lds_cnt[gid], 1u);
+        if (hit) atomicAdd(&lds_cnt[kLds + gid], 1u);
+      } else {
+        wave_count2(matched, hit, gid, A.matches, A.hits);
+      }
+    }
     bool fresh = false;
-    if (hit && (flags & RSA_F_BUILT) && A.cap > 0) {
+    unsigned long long slot = kEmpty;
+    if (hit && (flags & RSA_F_BUILT) && A.cap > 0 && !(A.skip & 2u)) {
       const unsigned long long o = ORD[i];
       // exact skip: the rule is already capped with threshold <= filter < o
       if (o <= A.filter[gid]) {
         unsigned long long kA, kB;
         conn_key(t, gid, kA, kB);
         const uint32_t ts = TS[i];
-        fresh = table_combine(A, kA, kB, 1u, ts, ts, o);
+        slot = table_combine(A, kA, kB, 1u, ts, ts, o, &fresh);
       }
     }
     wave_count_by_key(fresh, gid, A.distinct);
+    const unsigned long long pos = wave_append(fresh, A.used_n);
+    if (fresh) A.used[pos] = (uint32_t)slot;
+  }
+  if (kLds > 0 && counters) {
+    __syncthreads();
+    for (uint32_t r = threadIdx.x; r < R.n_rules; r += kThreads) {
+      const uint32_t m = lds_cnt[r], h = lds_cnt[kLds + r];
+      if (m) atomicAdd(&A.matches[r], (unsigned long long)m);
+      if (h) atomicAdd(&A.hits[r], (unsigned long long)h);
+    }
   }
 }
 
@@ -281,7 +439,7 @@ __global__ __launch_bounds__(kBlock) void k_pass2(const uint4* __restrict__ T, c
     } else {
       gid = classify_wave(t, in && (flags & RSA_F_VALID), R, A.flags);
     }
-    if (gid == kNoGid || gid >= R.n_rules) continue;
+    if (gid >= R.n_rules) continue;
     if ((flags & (RSA_F_HIT | RSA_F_BUILT)) != (RSA_F_HIT | RSA_F_BUILT)) continue;
     const unsigned long long P = A.thresh[gid];
     if (P == RSA_NO_THRESHOLD) continue;
@@ -301,47 +459,41 @@ __global__ __launch_bounds__(kBlock) void k_pass2(const uint4* __restrict__ T, c
   }
 }
 
-__global__ void k_table_init(Slot* S, unsigned long long cap) {
-  const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
-  for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += stride) {
-    Slot s;
-    s.kA = 0;
-    s.kB = kEmpty;
-    s.min_order = kEmpty;
-    s.count = 0;
-    s.first = 0xFFFFFFFFu;
-    s.last = 0;
-    s.count2 = 0;
-    s.first2 = 0xFFFFFFFFu;
-    s.last2 = 0;
-    s.pad[0] = s.pad[1] = s.pad[2] = s.pad[3] = 0;
-    S[i] = s;
-  }
+__device__ __forceinline__ void slot_clear(Slot* S, unsigned long long i) {
+  Slot s;
+  s.kA = 0;
+  s.kB = kEmpty;
+  s.min_order = kEmpty;
+  s.count = 0;
+  s.first = 0xFFFFFFFFu;
+  s.last = 0;
+  s.count2 = 0;
+  s.first2 = 0xFFFFFFFFu;
+  s.last2 = 0;
+  s.pad[0] = s.pad[1] = s.pad[2] = s.pad[3] = 0;
+  S[i] = s;
 }
 
-// Wave-aggregated append to a global cursor: one atomic per wave.  Must be
-// called by every lane of the wave (wave-uniform control flow).
-__device__ __forceinline__ unsigned long long wave_append(bool ok, unsigned long long* cursor) {
-  const unsigned long long mask = __ballot(ok);
-  if (mask == 0) return 0;
-  const unsigned lane = __lane_id();
-  const int leader = __builtin_ctzll(mask);
-  unsigned long long base = 0;
-  if ((int)lane == leader) base = atomicAdd(cursor, (unsigned long long)__popcll(mask));
-  base = __shfl(base, leader);
-  return base + __popcll(mask & ((1ull << lane) - 1ull));
+__global__ void k_table_init(Slot* S, unsigned long long cap) {
+  const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+  for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += stride)
+    slot_clear(S, i);
+}
+
+// Reset only the slots the last job used.
+__global__ void k_table_clear(Slot* S, const uint32_t* used, unsigned long long n) {
+  const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+  for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    slot_clear(S, used[i]);
 }
 
 // ---- cap resolution (exact): P = cap-th smallest min_order among a rule's entries.
-// Capped entries are compacted to (min_order, capped index) pairs, sorted by
-// min_order then stably by capped index (two LSD radix sorts), so each capped
-// rule's entries form one ascending segment and P is the segment's cap-th element.
 __global__ void k_cap_mark(const unsigned int* distinct, uint32_t n_rules, uint32_t cap, uint32_t* cidx,
                            uint32_t* capped_gid, uint32_t* capped_cnt, unsigned int* n_capped,
-                           unsigned long long* thresh) {
+                           unsigned long long* out) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= n_rules) return;
-  thresh[g] = RSA_NO_THRESHOLD;
+  out[g] = RSA_NO_THRESHOLD;
   if (cap > 0 && distinct[g] >= cap) {
     const unsigned int c = atomicAdd(n_capped, 1u);
     cidx[g] = c;
@@ -352,20 +504,18 @@ __global__ void k_cap_mark(const unsigned int* distinct, uint32_t n_rules, uint3
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_cap_collect(const Slot* S, unsigned long long cap_slots,
+__global__ __launch_bounds__(kBlock) void k_cap_collect(const Slot* S, const uint32_t* used, unsigned long long n_used,
                                                         const uint32_t* cidx, unsigned long long* keys,
                                                         uint32_t* vals, unsigned long long* cursor) {
   const unsigned long long stride = (unsigned long long)gridDim.x * kBlock;
-  for (unsigned long long base = (unsigned long long)blockIdx.x * kBlock; base < cap_slots; base += stride) {
+  for (unsigned long long base = (unsigned long long)blockIdx.x * kBlock; base < n_used; base += stride) {
     const unsigned long long i = base + threadIdx.x;
     uint32_t c = 0xFFFFFFFFu;
     unsigned long long o = 0;
-    if (i < cap_slots) {
-      const unsigned long long kB = S[i].kB;
-      if (kB < kBusy) {
-        c = cidx[kB >> 32];
-        o = S[i].min_order;
-      }
+    if (i < n_used) {
+      const Slot* s = &S[used[i]];
+      c = cidx[s->kB >> 32];
+      o = s->min_order;
     }
     const bool ok = c != 0xFFFFFFFFu;
     const unsigned long long pos = wave_append(ok, cursor);
@@ -377,9 +527,9 @@ __global__ __launch_bounds__(kBlock) void k_cap_collect(const Slot* S, unsigned 
 }
 
 __global__ void k_cap_pick(const unsigned long long* sorted_orders, const uint32_t* start, const uint32_t* capped_gid,
-                           uint32_t n_capped, uint32_t cap, unsigned long long* thresh) {
+                           uint32_t n_capped, uint32_t cap, unsigned long long* out) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c < n_capped) thresh[capped_gid[c]] = sorted_orders[(size_t)start[c] + cap - 1];
+  if (c < n_capped) out[capped_gid[c]] = sorted_orders[(size_t)start[c] + cap - 1];
 }
 
 __device__ __forceinline__ rsa_conn_record make_record(const Slot& s, int which) {
@@ -399,26 +549,24 @@ __device__ __forceinline__ rsa_conn_record make_record(const Slot& s, int which)
 }
 
 // mode 0: final report rows; mode 1: export pass-1 aggregates; mode 2: export pass-2.
-__global__ __launch_bounds__(kBlock) void k_emit(const Slot* S, unsigned long long cap_slots,
+__global__ __launch_bounds__(kBlock) void k_emit(const Slot* S, const uint32_t* used, unsigned long long n_used,
                                                  const unsigned long long* thresh, int mode, rsa_conn_record* out,
                                                  unsigned long long max_out, unsigned long long* cursor) {
   const unsigned long long stride = (unsigned long long)gridDim.x * kBlock;
-  for (unsigned long long base = (unsigned long long)blockIdx.x * kBlock; base < cap_slots; base += stride) {
+  for (unsigned long long base = (unsigned long long)blockIdx.x * kBlock; base < n_used; base += stride) {
     const unsigned long long i = base + threadIdx.x;
     int which = -1;
     Slot s;
-    if (i < cap_slots) {
-      s = S[i];
-      if (s.kB < kBusy) {
-        if (mode == 0) {
-          const unsigned long long P = thresh[s.kB >> 32];
-          if (P == RSA_NO_THRESHOLD) which = 0;
-          else if (s.min_order <= P) which = 1;
-        } else if (mode == 1) {
-          which = 0;
-        } else if (s.count2 != 0) {
-          which = 1;
-        }
+    if (i < n_used) {
+      s = S[used[i]];
+      if (mode == 0) {
+        const unsigned long long P = thresh[s.kB >> 32];
+        if (P == RSA_NO_THRESHOLD) which = 0;
+        else if (s.min_order <= P) which = 1;
+      } else if (mode == 1) {
+        which = 0;
+      } else if (s.count2 != 0) {
+        which = 1;
       }
     }
     const unsigned long long k = wave_append(which >= 0, cursor);
@@ -426,35 +574,35 @@ __global__ __launch_bounds__(kBlock) void k_emit(const Slot* S, unsigned long lo
   }
 }
 
-__global__ void k_import(const rsa_conn_record* __restrict__ in, unsigned long long n, int which, Agg A) {
-  const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
-  for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const rsa_conn_record r = in[i];
-    const unsigned long long kA = ((unsigned long long)r.for_ip << 32) | r.to_ip;
-    const unsigned long long kB = ((unsigned long long)r.gid << 32) | ((unsigned long long)r.pspell << 16) | r.to_port;
-    if (which == 0) {
-      const bool fresh = table_combine(A, kA, kB, r.count, r.first, r.last, r.min_order);
-      if (fresh) atomicAdd(&A.distinct[r.gid], 1u);
-    } else {
-      Slot* s = table_find(A, kA, kB);
-      if (!s) {
-        atomicOr(&A.flags[1], 8u);
-        continue;
-      }
-      atomicAdd(&s->count2, r.count);
-      atomicMin(&s->first2, r.first);
-      atomicMax(&s->last2, r.last);
-    }
-  }
-}
-
-__global__ __launch_bounds__(kBlock) void k_count_used(const Slot* S, unsigned long long cap_slots,
-                                                       unsigned long long* cursor) {
+__global__ __launch_bounds__(kBlock) void k_import(const rsa_conn_record* __restrict__ in, unsigned long long n,
+                                                   int which, Agg A) {
   const unsigned long long stride = (unsigned long long)gridDim.x * kBlock;
-  for (unsigned long long base = (unsigned long long)blockIdx.x * kBlock; base < cap_slots; base += stride) {
+  for (unsigned long long base = (unsigned long long)blockIdx.x * kBlock; base < n; base += stride) {
     const unsigned long long i = base + threadIdx.x;
-    const bool used = i < cap_slots && S[i].kB < kBusy;
-    wave_append(used, cursor);
+    bool fresh = false;
+    unsigned long long slot = kEmpty;
+    uint32_t gid = kNoGid;
+    if (i < n) {
+      const rsa_conn_record r = in[i];
+      gid = r.gid;
+      const unsigned long long kA = ((unsigned long long)r.for_ip << 32) | r.to_ip;
+      const unsigned long long kB = ((unsigned long long)r.gid << 32) | ((unsigned long long)r.pspell << 16) | r.to_port;
+      if (which == 0) {
+        slot = table_combine(A, kA, kB, r.count, r.first, r.last, r.min_order, &fresh);
+      } else {
+        Slot* s = table_find(A, kA, kB);
+        if (!s) {
+          atomicOr(&A.flags[1], 8u);
+        } else {
+          atomicAdd(&s->count2, r.count);
+          atomicMin(&s->first2, r.first);
+          atomicMax(&s->last2, r.last);
+        }
+      }
+    }
+    wave_count_by_key(fresh, gid, A.distinct);
+    const unsigned long long pos = wave_append(fresh, A.used_n);
+    if (fresh) A.used[pos] = (uint32_t)slot;
   }
 }
 
@@ -463,42 +611,62 @@ __global__ __launch_bounds__(kBlock) void k_count_used(const Slot* S, unsigned l
 struct rsa_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  int cu_count = 256;
+  std::string err;
+  // rules
   rsa_rule_entry* d_entries = nullptr;
   uint32_t n_entries = 0;
   uint32_t* d_off = nullptr;
   uint32_t n_lists = 0;
   uint32_t n_rules = 0;
   bool rules_loaded = false;
+  // tuple-space-search index
+  rsa_shape* d_shapes = nullptr;
+  uint32_t* d_shape_off = nullptr;
+  rsa_index_slot* d_islots = nullptr;
+  rsa_rule_entry* d_resid = nullptr;
+  uint32_t* d_resid_off = nullptr;
+  bool indexed = false;
+  // caller-owned counters
   unsigned long long* d_matches = nullptr;
   unsigned long long* d_hits = nullptr;
   unsigned int* d_distinct = nullptr;
   unsigned long long* d_thresh = nullptr;
-  unsigned long long* d_filter = nullptr;  // library-owned, n_rules
+  // library-owned table
+  Slot* d_slots = nullptr;
+  unsigned long long slot_cap = 0;    // power of two in use
+  unsigned long long slot_alloc = 0;  // allocated (and initialised) slots
+  uint32_t* d_used = nullptr;
+  unsigned long long* d_used_n = nullptr;
+  unsigned long long used_last = 0;   // used slots at the last host read (upper bound for clearing)
+  bool table_dirty = false;           // used list may be non-empty
+  uint32_t cap = 1000;
+  bool table_ready = false;
+  unsigned long long* d_filter = nullptr;
   uint32_t filter_len = 0;
   bool auto_tighten = true;
   bool tightened = false;
-  Slot* d_slots = nullptr;
-  unsigned long long slot_cap = 0;    // power of two
-  unsigned long long slot_alloc = 0;  // allocated slots
-  uint32_t cap = 1000;
-  bool table_ready = false;
+  uint32_t profile_skip = 0;
+  uint32_t scan_prefix = 256;         // linear scan: entries per list scanned before deferring a lane
+  uint32_t* d_tail = nullptr;         // deferred line indices
+  unsigned long long* d_tail_n = nullptr;
+  unsigned long long tail_alloc = 0;
   unsigned int* d_flags = nullptr;       // 4 words
   unsigned long long* d_cursor = nullptr;
   // cap-resolution scratch
   uint32_t* d_cidx = nullptr;
-  uint32_t cidx_len = 0;
   uint32_t* d_capped_gid = nullptr;
   uint32_t* d_capped_cnt = nullptr;
   uint32_t* d_capped_start = nullptr;
-  uint32_t capped_alloc = 0;
-  // sort scratch (capped entries)
+  uint32_t cidx_len = 0;
   unsigned long long* d_keys[2] = {nullptr, nullptr};
   uint32_t* d_vals[2] = {nullptr, nullptr};
   unsigned long long sort_alloc = 0;
   void* d_temp = nullptr;
   size_t temp_alloc = 0;
-  int cu_count = 256;
-  std::string err;
+  // pass-1 kernel timing (HIP events on the ctx stream)
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  int ev_used = 0;
 };
 
 namespace {
@@ -513,18 +681,24 @@ int fail(rsa_ctx* c, int code, const char* fmt, ...) {
   return code;
 }
 
-#define HIPCHK(ctx, expr)                                                                   \
-  do {                                                                                      \
-    hipError_t e_ = (expr);                                                                 \
+#define HIPCHK(ctx, expr)                                                                          \
+  do {                                                                                             \
+    hipError_t e_ = (expr);                                                                        \
     if (e_ != hipSuccess) return fail((ctx), RSA_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
   } while (0)
 
 Rules rules_of(const rsa_ctx* c) {
   Rules r;
-  r.e = (const const_uint4*)(c->d_entries);
+  r.e = (const const_v4u*)(c->d_entries);
   r.off = (const const_u32*)(c->d_off);
   r.n_lists = c->n_lists;
   r.n_rules = c->n_rules;
+  r.shapes = (const const_v4u*)(c->d_shapes);
+  r.shape_off = (const const_u32*)(c->d_shape_off);
+  r.islots = reinterpret_cast<const uint4*>(c->d_islots);
+  r.resid = (const const_v4u*)(c->d_resid);
+  r.resid_off = (const const_u32*)(c->d_resid_off);
+  r.indexed = c->indexed ? 1 : 0;
   return r;
 }
 
@@ -537,9 +711,24 @@ Agg agg_of(const rsa_ctx* c) {
   a.filter = c->d_filter;
   a.slots = c->d_slots;
   a.mask = c->slot_cap ? c->slot_cap - 1 : 0;
+  a.used = c->d_used;
+  a.used_n = c->d_used_n;
   a.flags = c->d_flags;
   a.cap = c->cap;
+  a.skip = c->profile_skip;
   return a;
+}
+
+// LDS-privatised counter capacities (rules): 2 x 4 B per rule.
+constexpr int kLdsSmall = 10240;   // 80 KiB: two 1024-thread workgroups per CU (32 waves)
+constexpr int kLdsLarge = 20480;   // 160 KiB: one workgroup per CU
+
+unsigned grid_for_threads(const rsa_ctx* c, unsigned long long n, unsigned threads, unsigned per_cu) {
+  unsigned long long g = (n + threads - 1) / threads;
+  const unsigned long long lim = (unsigned long long)c->cu_count * per_cu;
+  if (g > lim) g = lim;
+  if (g == 0) g = 1;
+  return (unsigned)g;
 }
 
 unsigned grid_for(const rsa_ctx* c, unsigned long long n, unsigned per_cu) {
@@ -569,57 +758,268 @@ int need_agg(rsa_ctx* c) {
   return RSA_OK;
 }
 
-}  // namespace
+int used_count(rsa_ctx* c, unsigned long long* n) {
+  HIPCHK(c, hipMemcpyAsync(n, c->d_used_n, sizeof *n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (*n > c->slot_cap) *n = c->slot_cap;
+  c->used_last = *n;
+  return RSA_OK;
+}
 
-static int run_pass1(rsa_ctx* c, int mode, const rsa_tuple* T, const uint32_t* TS, const uint64_t* ORD,
-                     const int32_t* G, int32_t* gout, uint64_t n);
+int ensure_temp(rsa_ctx* c, size_t bytes) {
+  if (bytes <= c->temp_alloc) return RSA_OK;
+  hipFree(c->d_temp);
+  c->d_temp = nullptr;
+  c->temp_alloc = 0;
+  HIPCHK(c, hipMalloc(&c->d_temp, bytes));
+  c->temp_alloc = bytes;
+  return RSA_OK;
+}
+
+template <typename T>
+int upload(rsa_ctx* c, T** dst, const T* src, size_t n) {
+  hipFree(*dst);
+  *dst = nullptr;
+  HIPCHK(c, hipMalloc(dst, (n ? n : 1) * sizeof(T)));
+  if (n) HIPCHK(c, hipMemcpy(*dst, src, n * sizeof(T), hipMemcpyHostToDevice));
+  return RSA_OK;
+}
+
+// Exact selection of P for every rule with >= cap distinct entries in the
+// current table, written to out[] (RSA_NO_THRESHOLD for the others).  On the
+// final table this is the reducer's cap threshold; on a partial table it is an
+// upper bound of it (the filter): first-seen orders only decrease and the set
+// of connections only grows as more lines are aggregated.
+int cap_select(rsa_ctx* c, unsigned long long* out, uint32_t* h_n_capped) {
+  int rc = check_flags(c);
+  if (rc) return rc;
+  const uint32_t nr = c->n_rules;
+  *h_n_capped = 0;
+  if (nr == 0) return RSA_OK;
+  if (c->cidx_len < nr) {
+    hipFree(c->d_cidx);
+    hipFree(c->d_capped_gid);
+    hipFree(c->d_capped_cnt);
+    hipFree(c->d_capped_start);
+    c->d_cidx = c->d_capped_gid = c->d_capped_cnt = c->d_capped_start = nullptr;
+    c->cidx_len = 0;
+    HIPCHK(c, hipMalloc(&c->d_cidx, (size_t)nr * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(&c->d_capped_gid, (size_t)nr * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(&c->d_capped_cnt, (size_t)nr * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(&c->d_capped_start, (size_t)nr * sizeof(uint32_t)));
+    c->cidx_len = nr;
+  }
+  unsigned int* d_ncap = c->d_flags + 2;
+  HIPCHK(c, hipMemsetAsync(d_ncap, 0, sizeof(unsigned int), c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_cursor, 0, sizeof(unsigned long long), c->stream));
+  k_cap_mark<<<(nr + kBlock - 1) / kBlock, kBlock, 0, c->stream>>>(c->d_distinct, nr, c->cap, c->d_cidx,
+                                                                   c->d_capped_gid, c->d_capped_cnt, d_ncap, out);
+  HIPCHK(c, hipGetLastError());
+  unsigned int ncap = 0;
+  HIPCHK(c, hipMemcpyAsync(&ncap, d_ncap, sizeof ncap, hipMemcpyDeviceToHost, c->stream));
+  unsigned long long n_used = 0;
+  rc = used_count(c, &n_used);  // synchronises
+  if (rc) return rc;
+  *h_n_capped = ncap;
+  if (ncap == 0) return RSA_OK;
+  if (c->sort_alloc < n_used) {
+    for (int k = 0; k < 2; ++k) {
+      hipFree(c->d_keys[k]);
+      hipFree(c->d_vals[k]);
+      c->d_keys[k] = nullptr;
+      c->d_vals[k] = nullptr;
+    }
+    c->sort_alloc = 0;
+    const unsigned long long want = n_used + n_used / 4 + 1024;
+    for (int k = 0; k < 2; ++k) {
+      HIPCHK(c, hipMalloc(&c->d_keys[k], want * sizeof(unsigned long long)));
+      HIPCHK(c, hipMalloc(&c->d_vals[k], want * sizeof(uint32_t)));
+    }
+    c->sort_alloc = want;
+  }
+  k_cap_collect<<<grid_for(c, n_used, 8), kBlock, 0, c->stream>>>(c->d_slots, c->d_used, n_used, c->d_cidx,
+                                                                  c->d_keys[0], c->d_vals[0], c->d_cursor);
+  HIPCHK(c, hipGetLastError());
+  unsigned long long m = 0;
+  HIPCHK(c, hipMemcpyAsync(&m, c->d_cursor, sizeof m, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (m > 0x7FFFFFFFull) return fail(c, RSA_ERR_CAPACITY, "more than 2^31 capped entries");
+  int cbits = 1;
+  while (cbits < 32 && (1ull << cbits) < ncap) ++cbits;
+  // sort by min_order, then stably by capped index; exclusive scan of segment sizes
+  hipcub::DoubleBuffer<unsigned long long> keys(c->d_keys[0], c->d_keys[1]);
+  hipcub::DoubleBuffer<uint32_t> vals(c->d_vals[0], c->d_vals[1]);
+  size_t t1 = 0, t2 = 0, t3 = 0;
+  HIPCHK(c, hipcub::DeviceRadixSort::SortPairs(nullptr, t1, keys, vals, (int)m, 0, 64, c->stream));
+  HIPCHK(c, hipcub::DeviceRadixSort::SortPairs(nullptr, t2, vals, keys, (int)m, 0, cbits, c->stream));
+  HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, t3, c->d_capped_cnt, c->d_capped_start, (int)ncap, c->stream));
+  size_t tb = t1 > t2 ? t1 : t2;
+  if (t3 > tb) tb = t3;
+  rc = ensure_temp(c, tb);
+  if (rc) return rc;
+  HIPCHK(c, hipcub::DeviceRadixSort::SortPairs(c->d_temp, tb, keys, vals, (int)m, 0, 64, c->stream));
+  HIPCHK(c, hipcub::DeviceRadixSort::SortPairs(c->d_temp, tb, vals, keys, (int)m, 0, cbits, c->stream));
+  HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(c->d_temp, tb, c->d_capped_cnt, c->d_capped_start, (int)ncap,
+                                             c->stream));
+  k_cap_pick<<<(ncap + kBlock - 1) / kBlock, kBlock, 0, c->stream>>>(keys.Current(), c->d_capped_start,
+                                                                     c->d_capped_gid, ncap, c->cap, out);
+  HIPCHK(c, hipGetLastError());
+  return RSA_OK;
+}
+
+int ensure_tail(rsa_ctx* c, unsigned long long n) {
+  if (!c->d_tail_n) HIPCHK(c, hipMalloc(&c->d_tail_n, sizeof(unsigned long long)));
+  if (n <= c->tail_alloc) return RSA_OK;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  hipFree(c->d_tail);
+  c->d_tail = nullptr;
+  c->tail_alloc = 0;
+  HIPCHK(c, hipMalloc(&c->d_tail, n * sizeof(uint32_t)));
+  c->tail_alloc = n;
+  return RSA_OK;
+}
+
+int ensure_events(rsa_ctx* c) {
+  for (int k = 0; k < 4; ++k)
+    if (!c->ev[k]) HIPCHK(c, hipEventCreate(&c->ev[k]));
+  return RSA_OK;
+}
+
+// Pass 1 over one batch.  With auto-tightening, a large first batch is split:
+// the first 1/16 builds the table, the filter is computed, and the rest of the
+// batch skips the table for lines that cannot change any output.
+int run_pass1(rsa_ctx* c, int mode, const rsa_tuple* T, const uint32_t* TS, const uint64_t* ORD, const int32_t* G,
+              int32_t* gout, uint64_t n) {
+  int rc = ensure_events(c);
+  if (rc) return rc;
+  c->ev_used = 0;
+  auto launch = [&](uint64_t a, uint64_t m) -> int {
+    const uint4* t = reinterpret_cast<const uint4*>(T) + a;
+    const unsigned long long* o = reinterpret_cast<const unsigned long long*>(ORD) + a;
+    HIPCHK(c, hipEventRecord(c->ev[c->ev_used], c->stream));
+    int32_t* go = gout ? gout + a : nullptr;
+    const int32_t* gi = G ? G + a : nullptr;
+    const Rules r = rules_of(c);
+    const Agg ag = agg_of(c);
+    const uint32_t K = c->indexed ? 0xFFFFFFFFu : c->scan_prefix;
+    int rc2 = ensure_tail(c, m);
+    if (rc2) return rc2;
+    HIPCHK(c, hipMemsetAsync(c->d_tail_n, 0, sizeof(unsigned long long), c->stream));
+    uint32_t* tl = c->d_tail;
+    unsigned long long* tn = c->d_tail_n;
+    if (c->n_rules <= kLdsSmall) {
+      // two 1024-thread workgroups (80 KiB of counters each) per CU
+      const unsigned g = grid_for_threads(c, m, 1024, 2);
+      if (mode == kClassifyAgg)
+        k_pass1<kClassifyAgg, 1024, kLdsSmall, false><<<g, 1024, 0, c->stream>>>(t, TS + a, o, m, nullptr, go, r, ag,
+                                                                                 K, tl, tn);
+      else
+        k_pass1<kGivenAgg, 1024, kLdsSmall, false><<<g, 1024, 0, c->stream>>>(t, TS + a, o, m, gi, nullptr, r, ag, K,
+                                                                              tl, tn);
+    } else if (c->n_rules <= kLdsLarge) {
+      const unsigned g = grid_for_threads(c, m, 1024, 1);
+      if (mode == kClassifyAgg)
+        k_pass1<kClassifyAgg, 1024, kLdsLarge, false><<<g, 1024, 0, c->stream>>>(t, TS + a, o, m, nullptr, go, r, ag,
+                                                                                 K, tl, tn);
+      else
+        k_pass1<kGivenAgg, 1024, kLdsLarge, false><<<g, 1024, 0, c->stream>>>(t, TS + a, o, m, gi, nullptr, r, ag, K,
+                                                                              tl, tn);
+    } else {
+      const unsigned g = grid_for(c, m, 16);
+      if (mode == kClassifyAgg)
+        k_pass1<kClassifyAgg, kBlock, 0, false><<<g, kBlock, 0, c->stream>>>(t, TS + a, o, m, nullptr, go, r, ag, K,
+                                                                             tl, tn);
+      else
+        k_pass1<kGivenAgg, kBlock, 0, false><<<g, kBlock, 0, c->stream>>>(t, TS + a, o, m, gi, nullptr, r, ag, K, tl,
+                                                                          tn);
+    }
+    HIPCHK(c, hipGetLastError());
+    if (mode == kClassifyAgg && K != 0xFFFFFFFFu) {
+      // finish the deferred lines (count read on the device: no host sync)
+      k_pass1<kClassifyAgg, kBlock, 0, true><<<c->cu_count * 4, kBlock, 0, c->stream>>>(t, TS + a, o, m, nullptr, go,
+                                                                                      r, ag, K, tl, tn);
+    }
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(c->ev[c->ev_used + 1], c->stream));
+    c->ev_used += 2;
+    return RSA_OK;
+  };
+  if (n > 0xFFFFFFFFull) return fail(c, RSA_ERR_ARG, "batch larger than 2^32 tuples: split it");
+  c->table_dirty = true;
+  const uint64_t kMinSplit = 1ull << 22;
+  if (c->auto_tighten && !c->tightened && c->cap > 0 && n >= kMinSplit) {
+    const uint64_t first = n / 16;
+    rc = launch(0, first);
+    if (rc) return rc;
+    uint32_t ncap = 0;
+    rc = cap_select(c, c->d_filter, &ncap);
+    if (rc) return rc;
+    c->tightened = true;
+    return launch(first, n - first);
+  }
+  return launch(0, n);
+}
+
+int emit_mode(rsa_ctx* c, int mode, rsa_conn_record* out, uint64_t max_out, uint64_t* h_n) {
+  if (!c || !h_n) return RSA_ERR_ARG;
+  int rc = need_agg(c);
+  if (rc) return rc;
+  if (max_out && !out) return fail(c, RSA_ERR_ARG, "null output buffer");
+  unsigned long long n_used = 0;
+  rc = used_count(c, &n_used);
+  if (rc) return rc;
+  HIPCHK(c, hipMemsetAsync(c->d_cursor, 0, sizeof(unsigned long long), c->stream));
+  if (n_used)
+    k_emit<<<grid_for(c, n_used, 8), kBlock, 0, c->stream>>>(c->d_slots, c->d_used, n_used, c->d_thresh, mode, out,
+                                                             max_out, c->d_cursor);
+  HIPCHK(c, hipGetLastError());
+  unsigned long long n = 0;
+  HIPCHK(c, hipMemcpyAsync(&n, c->d_cursor, sizeof n, hipMemcpyDeviceToHost, c->stream));
+  rc = check_flags(c);  // synchronises
+  if (rc) return rc;
+  *h_n = n;
+  if (n > max_out) return fail(c, RSA_ERR_CAPACITY, "%llu records do not fit in %llu", n, (unsigned long long)max_out);
+  return RSA_OK;
+}
+
+}  // namespace
 
 extern "C" {
 
-int rsa_version(void) { return 1; }
+int rsa_version(void) { return 2; }
 
 int rsa_ctx_create(int device, rsa_ctx** out) {
   if (!out) return RSA_ERR_ARG;
   *out = nullptr;
+  if (hipSetDevice(device) != hipSuccess) return RSA_ERR_HIP;
   rsa_ctx* c = new rsa_ctx();
   c->device = device;
-  hipError_t e = hipSetDevice(device);
-  if (e != hipSuccess) {
-    delete c;
-    return RSA_ERR_HIP;
-  }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     c->cu_count = prop.multiProcessorCount;
   if (hipMalloc(&c->d_flags, 4 * sizeof(unsigned int)) != hipSuccess ||
-      hipMalloc(&c->d_cursor, sizeof(unsigned long long)) != hipSuccess) {
-    delete c;
+      hipMalloc(&c->d_cursor, sizeof(unsigned long long)) != hipSuccess ||
+      hipMalloc(&c->d_used_n, sizeof(unsigned long long)) != hipSuccess ||
+      hipMemset(c->d_flags, 0, 4 * sizeof(unsigned int)) != hipSuccess ||
+      hipMemset(c->d_used_n, 0, sizeof(unsigned long long)) != hipSuccess) {
+    rsa_ctx_destroy(c);
     return RSA_ERR_HIP;
   }
-  hipMemset(c->d_flags, 0, 4 * sizeof(unsigned int));
   *out = c;
   return RSA_OK;
 }
 
 int rsa_ctx_destroy(rsa_ctx* c) {
   if (!c) return RSA_OK;
-  hipSetDevice(c->device);
-  if (c->stream) hipStreamSynchronize(c->stream);
-  hipFree(c->d_entries);
-  hipFree(c->d_off);
-  hipFree(c->d_slots);
-  hipFree(c->d_flags);
-  hipFree(c->d_cursor);
-  hipFree(c->d_cidx);
-  hipFree(c->d_capped_gid);
-  hipFree(c->d_capped_cnt);
-  hipFree(c->d_capped_start);
-  hipFree(c->d_filter);
-  hipFree(c->d_keys[0]);
-  hipFree(c->d_keys[1]);
-  hipFree(c->d_vals[0]);
-  hipFree(c->d_vals[1]);
-  hipFree(c->d_temp);
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  void* bufs[] = {c->d_tail, c->d_tail_n, c->d_entries, c->d_off, c->d_shapes, c->d_shape_off, c->d_islots, c->d_resid, c->d_resid_off,
+                  c->d_slots, c->d_used, c->d_used_n, c->d_filter, c->d_flags, c->d_cursor, c->d_cidx,
+                  c->d_capped_gid, c->d_capped_cnt, c->d_capped_start, c->d_keys[0], c->d_keys[1], c->d_vals[0],
+                  c->d_vals[1], c->d_temp};
+  for (void* b : bufs) (void)hipFree(b);
+  for (int k = 0; k < 4; ++k)
+    if (c->ev[k]) (void)hipEventDestroy(c->ev[k]);
   delete c;
   return RSA_OK;
 }
@@ -630,6 +1030,28 @@ int rsa_set_stream(rsa_ctx* c, void* s) {
   if (!c) return RSA_ERR_ARG;
   c->stream = reinterpret_cast<hipStream_t>(s);
   return RSA_OK;
+}
+
+int rsa_set_option(rsa_ctx* c, int option, int64_t value) {
+  if (!c) return RSA_ERR_ARG;
+  switch (option) {
+    case RSA_OPT_AUTO_FILTER:
+      c->auto_tighten = value != 0;
+      return RSA_OK;
+    case RSA_OPT_SCAN_PREFIX:
+      if (value <= 0) return fail(c, RSA_ERR_ARG, "scan prefix must be positive");
+      c->scan_prefix = value > 0xFFFFFFFELL ? 0xFFFFFFFEu : (uint32_t)value;
+      return RSA_OK;
+    case RSA_OPT_PROFILE_SKIP:
+      c->profile_skip = (uint32_t)value;
+      return RSA_OK;
+    case RSA_OPT_USE_INDEX:
+      if (value && !c->d_shapes) return fail(c, RSA_ERR_STATE, "no index loaded");
+      c->indexed = value != 0;
+      return RSA_OK;
+    default:
+      return fail(c, RSA_ERR_ARG, "unknown option %d", option);
+  }
 }
 
 int rsa_sync(rsa_ctx* c) {
@@ -654,19 +1076,50 @@ int rsa_load_rules(rsa_ctx* c, const rsa_rule_entry* h_entries, uint32_t n_entri
   }
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  hipFree(c->d_entries);
-  hipFree(c->d_off);
-  c->d_entries = nullptr;
-  c->d_off = nullptr;
-  const size_t eb = (size_t)(n_entries ? n_entries : 1) * sizeof(rsa_rule_entry);
-  HIPCHK(c, hipMalloc(&c->d_entries, eb));
-  HIPCHK(c, hipMalloc(&c->d_off, (size_t)(n_lists + 1) * sizeof(uint32_t)));
-  if (n_entries) HIPCHK(c, hipMemcpy(c->d_entries, h_entries, (size_t)n_entries * sizeof(rsa_rule_entry), hipMemcpyHostToDevice));
-  HIPCHK(c, hipMemcpy(c->d_off, h_off, (size_t)(n_lists + 1) * sizeof(uint32_t), hipMemcpyHostToDevice));
+  int rc = upload(c, &c->d_entries, h_entries, n_entries);
+  if (rc) return rc;
+  rc = upload(c, &c->d_off, h_off, (size_t)n_lists + 1);
+  if (rc) return rc;
   c->n_entries = n_entries;
   c->n_lists = n_lists;
   c->n_rules = n_rules;
   c->rules_loaded = true;
+  c->indexed = false;  // an index must be (re)loaded for these lists
+  return RSA_OK;
+}
+
+int rsa_load_index(rsa_ctx* c, const rsa_shape* h_shapes, uint32_t n_shapes, const uint32_t* h_shape_off,
+                   const rsa_index_slot* h_slots, uint64_t n_slots, const rsa_rule_entry* h_resid, uint32_t n_resid,
+                   const uint32_t* h_resid_off) {
+  if (!c || !h_shape_off || !h_resid_off) return fail(c, RSA_ERR_ARG, "null argument");
+  if (!c->rules_loaded) return fail(c, RSA_ERR_STATE, "load the candidate lists first");
+  const uint32_t nl = c->n_lists;
+  if (h_shape_off[0] != 0 || h_shape_off[nl] != n_shapes || h_resid_off[0] != 0 || h_resid_off[nl] != n_resid)
+    return fail(c, RSA_ERR_ARG, "index offsets do not span their arrays");
+  for (uint32_t s = 0; s < n_shapes; ++s) {
+    const rsa_shape& sh = h_shapes[s];
+    if ((sh.table_mask & (sh.table_mask + 1)) != 0 || (uint64_t)sh.table_off + sh.table_mask + 1 > n_slots)
+      return fail(c, RSA_ERR_ARG, "shape %u: table outside the slot array or not a power of two", s);
+  }
+  for (uint32_t l = 0; l < nl; ++l) {
+    for (uint32_t s = h_shape_off[l] + 1; s < h_shape_off[l + 1]; ++s)
+      if (h_shapes[s].min_gid < h_shapes[s - 1].min_gid)
+        return fail(c, RSA_ERR_ARG, "list %u: shapes not in ascending min_gid order", l);
+    for (uint32_t e = h_resid_off[l] + 1; e < h_resid_off[l + 1]; ++e)
+      if (h_resid[e].gid < h_resid[e - 1].gid) return fail(c, RSA_ERR_ARG, "list %u: residual not gid-ascending", l);
+  }
+  for (uint64_t k = 0; k < n_slots; ++k)
+    if (h_slots[k].gid != kNoGid && h_slots[k].gid >= c->n_rules)
+      return fail(c, RSA_ERR_ARG, "index slot %llu gid out of range", (unsigned long long)k);
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  int rc = upload(c, &c->d_shapes, h_shapes, n_shapes);
+  if (!rc) rc = upload(c, &c->d_shape_off, h_shape_off, (size_t)nl + 1);
+  if (!rc) rc = upload(c, &c->d_islots, h_slots, (size_t)n_slots);
+  if (!rc) rc = upload(c, &c->d_resid, h_resid, n_resid);
+  if (!rc) rc = upload(c, &c->d_resid_off, h_resid_off, (size_t)nl + 1);
+  if (rc) return rc;
+  c->indexed = true;
   return RSA_OK;
 }
 
@@ -689,6 +1142,8 @@ int rsa_bind_counters(rsa_ctx* c, uint64_t* m, uint64_t* h, uint32_t* d, uint64_
 int rsa_reset(rsa_ctx* c, uint64_t capacity, uint32_t cap) {
   if (!c) return RSA_ERR_ARG;
   if (!c->d_matches) return fail(c, RSA_ERR_STATE, "counters not bound (rsa_bind_counters)");
+  if (capacity > (1ull << 31)) return fail(c, RSA_ERR_ARG, "capacity %llu > 2^31 entries",
+                                           (unsigned long long)capacity);
   HIPCHK(c, hipSetDevice(c->device));
   unsigned long long want = 1024;
   const unsigned long long need = capacity + capacity / 2 + 64;
@@ -696,15 +1151,29 @@ int rsa_reset(rsa_ctx* c, uint64_t capacity, uint32_t cap) {
   if (want > c->slot_alloc) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     hipFree(c->d_slots);
+    hipFree(c->d_used);
     c->d_slots = nullptr;
+    c->d_used = nullptr;
     c->slot_alloc = 0;
     HIPCHK(c, hipMalloc(&c->d_slots, want * sizeof(Slot)));
+    HIPCHK(c, hipMalloc(&c->d_used, want * sizeof(uint32_t)));
+    k_table_init<<<grid_for(c, want, 8), kBlock, 0, c->stream>>>(c->d_slots, want);
+    HIPCHK(c, hipGetLastError());
     c->slot_alloc = want;
+    c->table_dirty = false;
+  } else if (c->table_dirty) {
+    // clear exactly the slots the previous job used (they may lie anywhere in the allocation)
+    unsigned long long n_used = 0;
+    int rc = used_count(c, &n_used);
+    if (rc) return rc;
+    if (n_used)
+      k_table_clear<<<grid_for(c, n_used, 8), kBlock, 0, c->stream>>>(c->d_slots, c->d_used, n_used);
+    HIPCHK(c, hipGetLastError());
+    c->table_dirty = false;
   }
   c->slot_cap = want;
   c->cap = cap;
-  k_table_init<<<grid_for(c, want, 8), kBlock, 0, c->stream>>>(c->d_slots, want);
-  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemsetAsync(c->d_used_n, 0, sizeof(unsigned long long), c->stream));
   const size_t nr = c->n_rules;
   if (nr) {
     HIPCHK(c, hipMemsetAsync(c->d_matches, 0, nr * sizeof(unsigned long long), c->stream));
@@ -712,7 +1181,7 @@ int rsa_reset(rsa_ctx* c, uint64_t capacity, uint32_t cap) {
     HIPCHK(c, hipMemsetAsync(c->d_distinct, 0, nr * sizeof(unsigned int), c->stream));
     HIPCHK(c, hipMemsetAsync(c->d_thresh, 0xFF, nr * sizeof(unsigned long long), c->stream));
   }
-  if (c->filter_len < nr || !c->d_filter) {
+  if (c->filter_len < (nr ? nr : 1) || !c->d_filter) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     hipFree(c->d_filter);
     c->d_filter = nullptr;
@@ -742,10 +1211,22 @@ int rsa_classify_only(rsa_ctx* c, const rsa_tuple* T, uint64_t n, int32_t* gout)
   if (!c->rules_loaded) return fail(c, RSA_ERR_STATE, "no rules loaded");
   if (n == 0) return RSA_OK;
   if (!T || !gout) return fail(c, RSA_ERR_ARG, "null tuple/gid pointer");
+  if (!c->d_flags) return fail(c, RSA_ERR_STATE, "ctx not initialised");
+  if (n > 0xFFFFFFFFull) return fail(c, RSA_ERR_ARG, "batch larger than 2^32 tuples");
   Agg a = agg_of(c);
-  k_pass1<kClassifyOnly><<<grid_for(c, n, 16), kBlock, 0, c->stream>>>(reinterpret_cast<const uint4*>(T), nullptr,
-                                                                      nullptr, n, nullptr, gout, rules_of(c), a);
+  const uint32_t K = c->indexed ? 0xFFFFFFFFu : c->scan_prefix;
+  int rc = ensure_tail(c, n);
+  if (rc) return rc;
+  HIPCHK(c, hipMemsetAsync(c->d_tail_n, 0, sizeof(unsigned long long), c->stream));
+  const uint4* t4 = reinterpret_cast<const uint4*>(T);
+  k_pass1<kClassifyOnly, kBlock, 0, false><<<grid_for(c, n, 16), kBlock, 0, c->stream>>>(
+      t4, nullptr, nullptr, n, nullptr, gout, rules_of(c), a, K, c->d_tail, c->d_tail_n);
   HIPCHK(c, hipGetLastError());
+  if (K != 0xFFFFFFFFu) {
+    k_pass1<kClassifyOnly, kBlock, 0, true><<<c->cu_count * 4, kBlock, 0, c->stream>>>(
+        t4, nullptr, nullptr, n, nullptr, gout, rules_of(c), a, K, c->d_tail, c->d_tail_n);
+    HIPCHK(c, hipGetLastError());
+  }
   return RSA_OK;
 }
 
@@ -759,94 +1240,16 @@ int rsa_aggregate_gids(rsa_ctx* c, const rsa_tuple* T, const uint32_t* TS, const
   return run_pass1(c, kGivenAgg, T, TS, ORD, G, nullptr, n);
 }
 
-static int ensure_temp(rsa_ctx* c, size_t bytes) {
-  if (bytes <= c->temp_alloc) return RSA_OK;
-  hipFree(c->d_temp);
-  c->d_temp = nullptr;
-  c->temp_alloc = 0;
-  HIPCHK(c, hipMalloc(&c->d_temp, bytes));
-  c->temp_alloc = bytes;
-  return RSA_OK;
-}
-
-// Exact selection of P for every rule with >= cap distinct entries in the
-// current table, written to out[] (RSA_NO_THRESHOLD for the others).  On the
-// final table this is the reducer's cap threshold; on a partial table it is an
-// upper bound of it (the filter), because first-seen orders only decrease and
-// the set of connections only grows as more lines are aggregated.
-static int cap_select(rsa_ctx* c, unsigned long long* out, uint32_t* h_n_capped) {
-  int rc = check_flags(c);
-  if (rc) return rc;
-  const uint32_t nr = c->n_rules;
-  *h_n_capped = 0;
-  if (nr == 0) return RSA_OK;
-  if (c->cidx_len < nr) {
-    hipFree(c->d_cidx);
-    hipFree(c->d_capped_gid);
-    hipFree(c->d_capped_cnt);
-    hipFree(c->d_capped_start);
-    c->d_cidx = c->d_capped_gid = c->d_capped_cnt = c->d_capped_start = nullptr;
-    c->cidx_len = 0;
-    HIPCHK(c, hipMalloc(&c->d_cidx, (size_t)nr * sizeof(uint32_t)));
-    HIPCHK(c, hipMalloc(&c->d_capped_gid, (size_t)nr * sizeof(uint32_t)));
-    HIPCHK(c, hipMalloc(&c->d_capped_cnt, (size_t)nr * sizeof(uint32_t)));
-    HIPCHK(c, hipMalloc(&c->d_capped_start, (size_t)nr * sizeof(uint32_t)));
-    c->cidx_len = nr;
+int rsa_last_pass1_ms(rsa_ctx* c, float* h_ms) {
+  if (!c || !h_ms) return RSA_ERR_ARG;
+  float total = 0.f;
+  for (int k = 0; k + 1 < c->ev_used; k += 2) {
+    HIPCHK(c, hipEventSynchronize(c->ev[k + 1]));
+    float ms = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&ms, c->ev[k], c->ev[k + 1]));
+    total += ms;
   }
-  unsigned int* d_ncap = c->d_flags + 2;
-  HIPCHK(c, hipMemsetAsync(d_ncap, 0, sizeof(unsigned int), c->stream));
-  HIPCHK(c, hipMemsetAsync(c->d_cursor, 0, sizeof(unsigned long long), c->stream));
-  k_cap_mark<<<(nr + kBlock - 1) / kBlock, kBlock, 0, c->stream>>>(c->d_distinct, nr, c->cap, c->d_cidx,
-                                                                   c->d_capped_gid, c->d_capped_cnt, d_ncap, out);
-  HIPCHK(c, hipGetLastError());
-  unsigned int ncap = 0;
-  HIPCHK(c, hipMemcpyAsync(&ncap, d_ncap, sizeof ncap, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  *h_n_capped = ncap;
-  if (ncap == 0) return RSA_OK;
-  // upper bound on capped entries: every used slot
-  unsigned long long bound = c->slot_cap;
-  if (c->sort_alloc < bound) {
-    for (int k = 0; k < 2; ++k) {
-      hipFree(c->d_keys[k]);
-      hipFree(c->d_vals[k]);
-      c->d_keys[k] = nullptr;
-      c->d_vals[k] = nullptr;
-    }
-    c->sort_alloc = 0;
-    for (int k = 0; k < 2; ++k) {
-      HIPCHK(c, hipMalloc(&c->d_keys[k], bound * sizeof(unsigned long long)));
-      HIPCHK(c, hipMalloc(&c->d_vals[k], bound * sizeof(uint32_t)));
-    }
-    c->sort_alloc = bound;
-  }
-  k_cap_collect<<<grid_for(c, c->slot_cap, 8), kBlock, 0, c->stream>>>(c->d_slots, c->slot_cap, c->d_cidx,
-                                                                       c->d_keys[0], c->d_vals[0], c->d_cursor);
-  HIPCHK(c, hipGetLastError());
-  unsigned long long m = 0;
-  HIPCHK(c, hipMemcpyAsync(&m, c->d_cursor, sizeof m, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  if (m > 0xFFFFFFFFull) return fail(c, RSA_ERR_CAPACITY, "more than 2^32 capped entries");
-  int cbits = 1;
-  while (cbits < 32 && (1ull << cbits) < ncap) ++cbits;
-  // sort by min_order, then stably by capped index; exclusive scan of segment sizes
-  hipcub::DoubleBuffer<unsigned long long> keys(c->d_keys[0], c->d_keys[1]);
-  hipcub::DoubleBuffer<uint32_t> vals(c->d_vals[0], c->d_vals[1]);
-  size_t t1 = 0, t2 = 0, t3 = 0;
-  HIPCHK(c, hipcub::DeviceRadixSort::SortPairs(nullptr, t1, keys, vals, (int)m, 0, 64, c->stream));
-  HIPCHK(c, hipcub::DeviceRadixSort::SortPairs(nullptr, t2, vals, keys, (int)m, 0, cbits, c->stream));
-  HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, t3, c->d_capped_cnt, c->d_capped_start, (int)ncap, c->stream));
-  size_t tb = t1 > t2 ? t1 : t2;
-  if (t3 > tb) tb = t3;
-  rc = ensure_temp(c, tb);
-  if (rc) return rc;
-  HIPCHK(c, hipcub::DeviceRadixSort::SortPairs(c->d_temp, tb, keys, vals, (int)m, 0, 64, c->stream));
-  HIPCHK(c, hipcub::DeviceRadixSort::SortPairs(c->d_temp, tb, vals, keys, (int)m, 0, cbits, c->stream));
-  HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(c->d_temp, tb, c->d_capped_cnt, c->d_capped_start, (int)ncap,
-                                             c->stream));
-  k_cap_pick<<<(ncap + kBlock - 1) / kBlock, kBlock, 0, c->stream>>>(keys.Current(), c->d_capped_start,
-                                                                     c->d_capped_gid, ncap, c->cap, out);
-  HIPCHK(c, hipGetLastError());
+  *h_ms = total;
   return RSA_OK;
 }
 
@@ -855,40 +1258,6 @@ int rsa_resolve_cap(rsa_ctx* c, uint32_t* h_n_capped) {
   int rc = need_agg(c);
   if (rc) return rc;
   return cap_select(c, c->d_thresh, h_n_capped);
-}
-
-// Pass 1 over one batch.  With auto-tightening, a large first batch is split:
-// the first 1/16 builds the table, then the filter (an exact upper bound of each
-// capped rule's threshold) is computed, and the rest of the batch skips the
-// table for lines that cannot change any output.
-static int run_pass1(rsa_ctx* c, int mode, const rsa_tuple* T, const uint32_t* TS, const uint64_t* ORD,
-                     const int32_t* G, int32_t* gout, uint64_t n) {
-  auto launch = [&](uint64_t a, uint64_t m) -> int {
-    const uint4* t = reinterpret_cast<const uint4*>(T) + a;
-    const unsigned long long* o = reinterpret_cast<const unsigned long long*>(ORD) + a;
-    if (mode == kClassifyAgg) {
-      k_pass1<kClassifyAgg><<<grid_for(c, m, 16), kBlock, 0, c->stream>>>(t, TS + a, o, m, nullptr,
-                                                                          gout ? gout + a : nullptr, rules_of(c),
-                                                                          agg_of(c));
-    } else {
-      k_pass1<kGivenAgg><<<grid_for(c, m, 16), kBlock, 0, c->stream>>>(t, TS + a, o, m, G + a, nullptr,
-                                                                       rules_of(c), agg_of(c));
-    }
-    HIPCHK(c, hipGetLastError());
-    return RSA_OK;
-  };
-  const uint64_t kMinSplit = 1ull << 22;
-  if (c->auto_tighten && !c->tightened && c->cap > 0 && n >= kMinSplit) {
-    const uint64_t first = n / 16;
-    int rc = launch(0, first);
-    if (rc) return rc;
-    uint32_t ncap = 0;
-    rc = cap_select(c, c->d_filter, &ncap);
-    if (rc) return rc;
-    c->tightened = true;
-    return launch(first, n - first);
-  }
-  return launch(0, n);
 }
 
 int rsa_recount(rsa_ctx* c, const rsa_tuple* T, const uint32_t* TS, const uint64_t* ORD, const int32_t* G,
@@ -912,24 +1281,6 @@ int rsa_recount(rsa_ctx* c, const rsa_tuple* T, const uint32_t* TS, const uint64
   return RSA_OK;
 }
 
-static int emit_mode(rsa_ctx* c, int mode, rsa_conn_record* out, uint64_t max_out, uint64_t* h_n) {
-  if (!c || !h_n) return RSA_ERR_ARG;
-  int rc = need_agg(c);
-  if (rc) return rc;
-  if (max_out && !out) return fail(c, RSA_ERR_ARG, "null output buffer");
-  HIPCHK(c, hipMemsetAsync(c->d_cursor, 0, sizeof(unsigned long long), c->stream));
-  k_emit<<<grid_for(c, c->slot_cap, 8), kBlock, 0, c->stream>>>(c->d_slots, c->slot_cap, c->d_thresh, mode, out,
-                                                                 max_out, c->d_cursor);
-  HIPCHK(c, hipGetLastError());
-  unsigned long long n = 0;
-  HIPCHK(c, hipMemcpyAsync(&n, c->d_cursor, sizeof n, hipMemcpyDeviceToHost, c->stream));
-  rc = check_flags(c);  // synchronises
-  if (rc) return rc;
-  *h_n = n;
-  if (n > max_out) return fail(c, RSA_ERR_CAPACITY, "%llu records do not fit in %llu", n, (unsigned long long)max_out);
-  return RSA_OK;
-}
-
 int rsa_emit(rsa_ctx* c, rsa_conn_record* out, uint64_t max_out, uint64_t* h_n) {
   return emit_mode(c, 0, out, max_out, h_n);
 }
@@ -946,6 +1297,7 @@ int rsa_import(rsa_ctx* c, int which, const rsa_conn_record* in, uint64_t n) {
   if (rc) return rc;
   if (n == 0) return RSA_OK;
   if (!in) return fail(c, RSA_ERR_ARG, "null input records");
+  c->table_dirty = true;
   k_import<<<grid_for(c, n, 16), kBlock, 0, c->stream>>>(in, n, which, agg_of(c));
   HIPCHK(c, hipGetLastError());
   return RSA_OK;
@@ -955,12 +1307,9 @@ int rsa_table_size(rsa_ctx* c, uint64_t* h_n) {
   if (!c || !h_n) return RSA_ERR_ARG;
   int rc = need_agg(c);
   if (rc) return rc;
-  HIPCHK(c, hipMemsetAsync(c->d_cursor, 0, sizeof(unsigned long long), c->stream));
-  k_count_used<<<grid_for(c, c->slot_cap, 8), kBlock, 0, c->stream>>>(c->d_slots, c->slot_cap, c->d_cursor);
-  HIPCHK(c, hipGetLastError());
   unsigned long long n = 0;
-  HIPCHK(c, hipMemcpyAsync(&n, c->d_cursor, sizeof n, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  rc = used_count(c, &n);
+  if (rc) return rc;
   *h_n = n;
   return RSA_OK;
 }

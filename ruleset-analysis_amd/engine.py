@@ -89,6 +89,34 @@ class Engine(object):
                       ctypes.c_uint32(n_rules))
         self._bind(n_rules)
 
+    def load_index(self, index):
+        shapes, shape_off, slots, resid, resid_off = (np.ascontiguousarray(a) for a in index)
+        self._index_hold = (shapes, shape_off, slots, resid, resid_off)
+        v = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+        self.ctx.call('rsa_load_index', v(shapes), ctypes.c_uint32(len(shapes)), v(shape_off), v(slots),
+                      ctypes.c_uint64(len(slots)), v(resid), ctypes.c_uint32(len(resid)), v(resid_off))
+
+    def set_option(self, option, value):
+        self.ctx.call('rsa_set_option', ctypes.c_int(option), ctypes.c_int64(int(value)))
+
+    def use_index(self, on):
+        self.set_option(native.RSA_OPT_USE_INDEX, 1 if on else 0)
+
+    def auto_filter(self, on):
+        self.set_option(native.RSA_OPT_AUTO_FILTER, 1 if on else 0)
+
+    def last_pass1_ms(self):
+        ms = ctypes.c_float(0)
+        self.ctx.call('rsa_last_pass1_ms', ctypes.byref(ms))
+        return float(ms.value)
+
+    def load_compiled(self, compiled, index=True):
+        """Upload a CompiledRules' lists (and its tuple-space-search index)."""
+        ent, off = compiled.packed()
+        self.load_rules(ent, off, compiled.n_rules)
+        if index:
+            self.load_index(compiled.index())
+
     def set_rule_count(self, n_rules):
         self.ctx.call('rsa_set_rule_count', ctypes.c_uint32(n_rules))
         self._bind(n_rules)

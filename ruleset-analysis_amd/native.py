@@ -30,6 +30,7 @@ class NativeError(RuntimeError):
 
 
 RSA_OK, RSA_ERR_ARG, RSA_ERR_HIP, RSA_ERR_STATE, RSA_ERR_CAPACITY = 0, -1, -2, -3, -4
+RSA_OPT_AUTO_FILTER, RSA_OPT_USE_INDEX, RSA_OPT_PROFILE_SKIP, RSA_OPT_SCAN_PREFIX = 1, 2, 3, 4
 
 P = ctypes.c_void_p
 U32 = ctypes.c_uint32
@@ -45,6 +46,9 @@ SYMBOLS = {
     'rsa_ctx_destroy': (I32, [P]),
     'rsa_last_error': (ctypes.c_char_p, [P]),
     'rsa_set_stream': (I32, [P, P]),
+    'rsa_set_option': (I32, [P, I32, ctypes.c_int64]),
+    'rsa_load_index': (I32, [P, P, U32, P, P, U64, P, U32, P]),
+    'rsa_last_pass1_ms': (I32, [P, ctypes.POINTER(ctypes.c_float)]),
     'rsa_load_rules': (I32, [P, P, U32, P, U32, U32]),
     'rsa_bind_counters': (I32, [P, P, P, P, P]),
     'rsa_set_rule_count': (I32, [P, U32]),

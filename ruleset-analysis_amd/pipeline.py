@@ -62,8 +62,7 @@ def analyze(inputs, db, cap=1000, device=0, engine=None):
     if parsed.error is not None:
         raise parsed.error[1]
     eng = engine if engine is not None else Engine(device)
-    ent, off = compiled.packed()
-    eng.load_rules(ent, off, compiled.n_rules)
+    eng.load_compiled(compiled)
     batch = DeviceBatch.from_numpy(parsed.tuples, parsed.ts, parsed.order, eng.device)
     results = eng.run([batch], cap, capacity=max(built_hit_count(parsed.tuples), 1))
     gids = eng.last_gids[0].cpu().numpy() if parsed.n else np.zeros(0, np.int32)

@@ -38,8 +38,7 @@ def test_golden_mapper_stream(engine, case):
     db = acldb.load_json(dbj)
     compiled = CompiledRules(db)
     parsed = parse_logs([(params['host'], split_lines(text))], db, compiled)
-    ent, off = compiled.packed()
-    engine.load_rules(ent, off, compiled.n_rules)
+    engine.load_compiled(compiled)
     engine.reset(max(built_hit_count(parsed.tuples), 1), params['cap'])
     b = DeviceBatch.from_numpy(parsed.tuples, parsed.ts, parsed.order, engine.device)
     gids = engine.classify_only(b).cpu().numpy() if parsed.n else np.zeros(0, np.int32)
@@ -48,7 +47,7 @@ def test_golden_mapper_stream(engine, case):
 
 
 def _gpu_vs_oracle(engine, n_rules, n_lines, cap, seed, zipf=None, interfaces=('outside',), batches=1,
-                   shuffle=False):
+                   shuffle=False, index=True):
     dbj, info = synth.make_db(seed, n_rules, interfaces=interfaces)
     tr = synth.make_traffic((dbj, info), n_lines, seed=seed + 1, zipf=zipf)
     if shuffle:   # input order no longer follows the sort order
@@ -58,8 +57,7 @@ def _gpu_vs_oracle(engine, n_rules, n_lines, cap, seed, zipf=None, interfaces=('
     db = acldb.load_json(dbj)
     compiled = CompiledRules(db)
     tup, ts, order = synth.pack(tr, compiled)
-    ent, off = compiled.packed()
-    engine.load_rules(ent, off, compiled.n_rules)
+    engine.load_compiled(compiled, index=index)
     cuts = np.linspace(0, n_lines, batches + 1).astype(int)
     bs = [DeviceBatch.from_numpy(tup[a:b], ts[a:b], order[a:b], engine.device) for a, b in zip(cuts[:-1], cuts[1:])]
     res = engine.run(bs, cap, capacity=max(built_hit_count(tup), 1))
@@ -97,6 +95,35 @@ def test_synth_parity_uncapped(engine):
     _gpu_vs_oracle(engine, 600, 200000, 1000, seed=11)
 
 
+def test_synth_parity_linear_scan(engine):
+    _gpu_vs_oracle(engine, 3000, 200000, 100, seed=18, index=False)
+
+
+def test_synth_parity_deferred_tail(engine):
+    """A tiny scan prefix defers most lines to the tail kernel: same answers."""
+    from ruleset_analysis_amd import native
+    engine.set_option(native.RSA_OPT_SCAN_PREFIX, 3)
+    try:
+        _gpu_vs_oracle(engine, 2000, 300000, 50, seed=23, index=False, zipf=1.2)
+    finally:
+        engine.set_option(native.RSA_OPT_SCAN_PREFIX, 256)
+
+
+def test_index_and_scan_agree_10k(engine):
+    """The tuple-space-search index and the linear scan classify identically."""
+    dbj, info = synth.make_db(19, 10000)
+    tr = synth.make_traffic((dbj, info), 1_000_000, seed=20, p_unmatched=0.5)
+    compiled = CompiledRules(acldb.load_json(dbj))
+    tup, _ts, _order = synth.pack(tr, compiled)
+    b = DeviceBatch.from_numpy(tup, _ts, _order, engine.device)
+    engine.load_compiled(compiled, index=True)
+    g_idx = engine.classify_only(b).cpu().numpy()
+    engine.use_index(False)
+    g_scan = engine.classify_only(b).cpu().numpy()
+    assert np.array_equal(g_idx, g_scan)
+    assert (g_idx >= 0).sum() > 0
+
+
 def test_synth_parity_capped_zipf(engine):
     res, ref = _gpu_vs_oracle(engine, 400, 300000, 25, seed=12, zipf=1.1)
     assert (ref['n_conns'] >= 25).sum() > 10          # the cap is really engaged
@@ -130,8 +157,7 @@ def test_deterministic(engine):
     tr = synth.make_traffic((dbj, info), 100000, seed=22, zipf=1.2)
     compiled = CompiledRules(acldb.load_json(dbj))
     tup, ts, order = synth.pack(tr, compiled)
-    ent, off = compiled.packed()
-    engine.load_rules(ent, off, compiled.n_rules)
+    engine.load_compiled(compiled)
     b = DeviceBatch.from_numpy(tup, ts, order, engine.device)
     outs = []
     for _ in range(2):
@@ -149,8 +175,7 @@ def test_export_import_roundtrip(engine):
     tr = synth.make_traffic((dbj, info), 80000, seed=32, zipf=1.3)
     compiled = CompiledRules(acldb.load_json(dbj))
     tup, ts, order = synth.pack(tr, compiled)
-    ent, off = compiled.packed()
-    engine.load_rules(ent, off, compiled.n_rules)
+    engine.load_compiled(compiled)
     b = DeviceBatch.from_numpy(tup, ts, order, engine.device)
     cap = 1000000
     ref = engine.run([b], cap, capacity=built_hit_count(tup))

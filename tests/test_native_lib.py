@@ -22,7 +22,7 @@ def test_library_exports_all_symbols():
     lib = native.load()
     for name in _declared():
         assert hasattr(lib, name), name
-    assert lib.rsa_version() == 1
+    assert lib.rsa_version() == 2
 
 
 def test_library_is_gfx950_code_object():

@@ -47,8 +47,8 @@ def main():
     compiled = CompiledRules(acldb.load_json(dbj))
     compiled.ensure_lists()
     eng = Engine(0)
+    eng.load_compiled(compiled)
     ent, off = compiled.packed()
-    eng.load_rules(ent, off, compiled.n_rules)
     batch, n_hb = build_shard(dbj, info, compiled, args.lines, 0, 3, args.zipf or None, eng.device)
     g = torch.empty(args.lines, dtype=torch.int32, device=eng.device)
     cap = args.cap
@@ -58,12 +58,28 @@ def main():
     res = {'lines': args.lines, 'rules': compiled.n_rules, 'entries': len(ent), 'hit_built': n_hb,
            'distinct': size}
     res['classify_only_ms'] = timed(lambda: eng.classify_only(batch, g), args.reps)
+    eng.use_index(False)
+    from ruleset_analysis_amd import native
+    for K in (64, 256, 1024, 1 << 30):
+        eng.set_option(native.RSA_OPT_SCAN_PREFIX, K)
+        res['classify_scan_K%d_ms' % K] = timed(lambda: eng.classify_only(batch, g), args.reps)
+    eng.set_option(native.RSA_OPT_SCAN_PREFIX, 256)
+    eng.use_index(True)
 
     def p1():
         eng.reset(int(size * 1.25), cap)
         eng.pass1(batch, g)
     res['reset_ms'] = timed(lambda: eng.reset(int(size * 1.25), cap), args.reps)
     res['reset_pass1_ms'] = timed(p1, args.reps)
+    eng.use_index(False)
+    res['scan_reset_pass1_ms'] = timed(p1, args.reps)
+    for mask, name in ((1, 'no_counters'), (2, 'no_table'), (3, 'no_agg')):
+        eng.set_option(native.RSA_OPT_PROFILE_SKIP, mask)
+        res['scan_pass1_%s_ms' % name] = timed(p1, args.reps)
+    eng.set_option(native.RSA_OPT_PROFILE_SKIP, 0)
+    eng.reset(int(size * 1.25), cap)
+    eng.pass1(batch, g)
+    eng.use_index(True)
     t = time.perf_counter()
     ncap = eng.resolve_cap()
     torch.cuda.synchronize()
