@@ -32,6 +32,49 @@ REC = RECORD_DTYPE.itemsize
 NO_THRESHOLD = -1   # 0xFFFF_FFFF_FFFF_FFFF viewed as int64
 
 
+def _host_staged(dist, group):
+    """gloo cannot move device tensors: stage them through host memory (tests /
+    several ranks sharing one GPU).  RCCL moves HBM to HBM directly."""
+    try:
+        return dist.get_backend(group) == 'gloo'
+    except Exception:  # noqa: BLE001
+        return False
+
+
+def _all_reduce(t, dist, group, op=None):
+    kw = {} if op is None else {'op': op}
+    if t.is_cuda and _host_staged(dist, group):
+        h = t.cpu()
+        dist.all_reduce(h, group=group, **kw)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, group=group, **kw)
+
+
+def _all_to_all(out, inp, dist, group, out_splits=None, in_splits=None):
+    if inp.is_cuda and _host_staged(dist, group):
+        h = torch_empty_like_cpu(out)
+        dist.all_to_all_single(h, inp.cpu(), out_splits, in_splits, group=group)
+        out.copy_(h)
+    else:
+        dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
+
+
+def _all_gather(parts, t, dist, group):
+    if t.is_cuda and _host_staged(dist, group):
+        hp = [p.cpu() for p in parts]
+        dist.all_gather(hp, t.cpu(), group=group)
+        for p, h in zip(parts, hp):
+            p.copy_(h)
+    else:
+        dist.all_gather(parts, t, group=group)
+
+
+def torch_empty_like_cpu(t):
+    import torch
+    return torch.empty(t.shape, dtype=t.dtype)
+
+
 def route_records(buf, world, dist, group=None):
     """all_to_all of record bytes to owner rank gid % world; returns received bytes."""
     import torch
@@ -44,11 +87,11 @@ def route_records(buf, world, dist, group=None):
     send = rows[perm].contiguous().view(-1)
     counts = torch.bincount(owner, minlength=world).to(torch.int64)
     recv_counts = torch.empty_like(counts)
-    dist.all_to_all_single(recv_counts, counts, group=group)
+    _all_to_all(recv_counts, counts, dist, group)
     sc = [int(c) * REC for c in counts.cpu().tolist()]
     rc = [int(c) * REC for c in recv_counts.cpu().tolist()]
     out = torch.empty(sum(rc), dtype=torch.uint8, device=buf.device)
-    dist.all_to_all_single(out, send, rc, sc, group=group)
+    _all_to_all(out, send, dist, group, rc, sc)
     return out
 
 
@@ -57,15 +100,15 @@ def merge(backend, dist, world, rank, group=None):
     rank 0 and None elsewhere."""
     import torch
     c = backend.local_counters()
-    dist.all_reduce(c['matches'], group=group)
-    dist.all_reduce(c['hits'], group=group)
+    _all_reduce(c['matches'], dist, group)
+    _all_reduce(c['hits'], dist, group)
     recv = route_records(backend.export(0), world, dist, group)
     backend.owner_reset(max(recv.numel() // REC, 1))
     backend.owner_import(recv, 0)
     backend.owner_resolve_cap()
     oc = backend.owner_counters()
     thresh = oc['thresh'].clone()
-    dist.all_reduce(thresh, op=dist.ReduceOp.MAX, group=group)
+    _all_reduce(thresh, dist, group, op=dist.ReduceOp.MAX)
     capped_any = bool((thresh != NO_THRESHOLD).any().item())
     if capped_any:
         backend.set_local_thresh(thresh)
@@ -75,17 +118,17 @@ def merge(backend, dist, world, rank, group=None):
         backend.set_owner_thresh(thresh)
     final = backend.owner_emit()
     distinct = oc['distinct'].clone()
-    dist.all_reduce(distinct, group=group)
+    _all_reduce(distinct, dist, group)
     # gather the owners' rows to rank 0 (padded all_gather: sizes first)
     size = torch.tensor([final.numel()], dtype=torch.int64, device=final.device)
     sizes = [torch.zeros_like(size) for _ in range(world)]
-    dist.all_gather(sizes, size, group=group)
+    _all_gather(sizes, size, dist, group)
     sizes = [int(s.item()) for s in sizes]
     pad = max(max(sizes), 1)
     padded = torch.zeros(pad, dtype=torch.uint8, device=final.device)
     padded[:final.numel()] = final
     parts = [torch.empty(pad, dtype=torch.uint8, device=final.device) for _ in range(world)]
-    dist.all_gather(parts, padded, group=group)
+    _all_gather(parts, padded, dist, group)
     if rank != 0:
         return None
     recs = np.concatenate([p[:s].cpu().numpy() for p, s in zip(parts, sizes)]).view(RECORD_DTYPE)

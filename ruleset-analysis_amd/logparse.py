@@ -25,6 +25,7 @@ import re
 import numpy as np
 
 from .compile import TUPLE_DTYPE, F_VALID, F_HIT, F_BUILT, F_SWAP
+from .firewallrule import FirewallRule
 from .ipaddr import IP
 
 __all__ = ['ParsedLog', 'parse_logs', 'get_builtconn', 'BUILT', 'PY2_WS', 'reducer_fields',
@@ -108,7 +109,7 @@ class ParsedLog(object):
         self.n = 0
 
 
-def parse_logs(inputs, db, compiled, pspell_table=None):
+def parse_logs(inputs, db, compiled, pspell_table=None, need_order=True):
     """inputs: iterable of (host, list_of_lines).  Lines keep their '\\n'.
 
     Stops at the first line where the reference mapper would raise; the
@@ -153,10 +154,13 @@ def parse_logs(inputs, db, compiled, pspell_table=None):
     P.ts_table = distinct
     P.ts = np.array([code[s] if s is not None else 0 for s in ts_str], dtype=np.uint32)
     # order key = rank of the line bytes (sort's order within one key group)
-    keys = [l[:-1] if l.endswith('\n') else l for l in P.lines]
-    perm = sorted(range(n), key=keys.__getitem__)
     P.order = np.empty(n, dtype=np.uint64)
-    P.order[np.array(perm, dtype=np.int64)] = np.arange(n, dtype=np.uint64)
+    if need_order:
+        keys = [l[:-1] if l.endswith('\n') else l for l in P.lines]
+        perm = sorted(range(n), key=keys.__getitem__)
+        P.order[np.array(perm, dtype=np.int64)] = np.arange(n, dtype=np.uint64)
+    else:
+        P.order[:] = np.arange(n, dtype=np.uint64)
     P.pspell_table = [s for s, _ in sorted(pspell.items(), key=lambda kv: kv[1])]
     return P
 
@@ -169,7 +173,8 @@ def _parse_one(line, host, fw, acls, compiled, pspell, P, i):
     proto = d['protocol'].lower()
     # Connection(...) -> FirewallRule.__init__ validation (firewallrule.py:47-93)
     sport, dport = int(d['sport']), int(d['dport'])
-    src_ip, dst_ip = IP(d['src']), IP(d['dst'])
+    src_ip = FirewallRule._address(d['src'], 'src')
+    dst_ip = FirewallRule._address(d['dst'], 'dst')
     ifc = d['interface_in']
     if ifc not in fw:
         return zero, D_NOACL, None

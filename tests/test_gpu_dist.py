@@ -1,0 +1,92 @@
+"""The multi-GPU merge with the real HIP tables: two ranks on the box's one
+GPU (gloo, tensors staged through host memory; the bench uses RCCL), each
+classifying and aggregating its half of the log; rank 0's merged result must
+equal the C oracle over the whole log."""
+import os
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+import rsa_pkg
+
+rsa_pkg.load()
+
+from oracle import coracle  # noqa: E402
+from ruleset_analysis_amd import acldb, synth  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+NO = 0xFFFFFFFFFFFFFFFF
+
+
+def _worker(rank, world, port, args, out_q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from ruleset_analysis_amd.compile import CompiledRules
+    from ruleset_analysis_amd.dist import EngineBackend, merge
+    from ruleset_analysis_amd.engine import DeviceBatch, Engine
+    from ruleset_analysis_amd.pipeline import built_hit_count
+    seed, n_rules, n_lines, cap = args
+    dbj, info = synth.make_db(seed, n_rules)
+    tr = synth.make_traffic((dbj, info), n_lines, seed=seed + 1, zipf=1.2)
+    compiled = CompiledRules(acldb.load_json(dbj))
+    compiled.ensure_lists()
+    tup, ts, order = synth.pack(tr, compiled)
+    cut = np.linspace(0, n_lines, world + 1).astype(int)
+    a, b = cut[rank], cut[rank + 1]
+    local = Engine(0)
+    local.load_compiled(compiled)
+    owner = Engine(0)
+    owner.set_rule_count(compiled.n_rules)
+    batch = DeviceBatch.from_numpy(tup[a:b], ts[a:b], order[a:b], local.device)
+    local.reset(max(built_hit_count(tup[a:b]), 1), cap)
+    g = torch.empty(batch.n, dtype=torch.int32, device=local.device)
+    local.pass1(batch, g)
+    out = merge(EngineBackend(local, owner, [batch], [g], cap), dist, world, rank)
+    if rank == 0:
+        out_q.put(out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('cap', [12, 1000])
+def test_two_ranks_one_gpu(cap):
+    from test_dist_merge import _free_port
+    import queue
+    import time
+    args = (61, 700, 120000, cap)
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, args, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out, deadline = None, time.time() + 400
+    while out is None:
+        try:
+            out = q.get(timeout=2)
+        except queue.Empty:
+            if any(p.exitcode not in (None, 0) for p in procs) or time.time() > deadline:
+                for p in procs:
+                    p.kill()
+                pytest.fail('worker died: %s' % [p.exitcode for p in procs])
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    recs, matches, hits, distinct, thresh = out
+    dbj, info = synth.make_db(61, 700)
+    tr = synth.make_traffic((dbj, info), 120000, seed=62, zipf=1.2)
+    R = coracle.OracleRules(dbj)
+    cols, ots, oorder = coracle.inputs_from_traffic(R, tr)
+    ref = coracle.run(R, cols, ots, oorder, cap)
+    assert np.array_equal(matches, ref['matches'])
+    assert np.array_equal(hits, ref['hits'])
+    assert np.array_equal(thresh != NO, (ref['n_conns'] >= cap) & (cap > 0))
+    got = sorted((int(r['gid']), int(r['pspell']), int(r['for_ip']), int(r['to_ip']), int(r['to_port']),
+                  int(r['count']), int(r['first']), int(r['last'])) for r in recs)
+    rows = ref['rows']
+    want = sorted(zip(*(rows[k].astype(int).tolist() for k in ('gid', 'pspell', 'for_ip', 'to_ip', 'to_port',
+                                                                  'count', 'first', 'last'))))
+    assert got == want
