@@ -98,13 +98,15 @@ def cpu_baseline(dbj, info, seconds=15.0):
 
 
 def read_traffic(name):
-    """Per-launch HBM bytes of the pass-1 kernel from a committed rocprofv3 PMC
-    summary (profiles/<name>), corrected per MI355X_MICROARCH.md §HBM, if present."""
+    """HBM bytes of the pass-1 kernel launches of one step (the 1/16 slice and the
+    rest, summed like `achieved`) from a committed rocprofv3 PMC summary
+    (profiles/<name>, written by tools/pmc_summary.py with the gfx950 FETCH_SIZE
+    correction of MI355X_MICROARCH.md §HBM), if present for this workload."""
     path = os.path.join(ROOT, 'profiles', name)
     if not os.path.exists(path):
         return None
     with open(path) as f:
-        return json.load(f).get('hbm_bytes_per_launch')
+        return json.load(f).get('hbm_bytes_per_step')
 
 
 def main():
@@ -115,7 +117,8 @@ def main():
     ap.add_argument('--config', default='cfg3', choices=sorted(CONFIGS))
     ap.add_argument('--lines', type=int, default=0, help='override lines per GPU')
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--scan', action='store_true', help='classify by linear scan instead of the index')
+    ap.add_argument('--index', action='store_true',
+                    help='classify with the tuple-space-search index instead of the prefix scan')
     args = ap.parse_args()
 
     import torch
@@ -135,7 +138,7 @@ def main():
     compiled = CompiledRules(acldb.load_json(dbj))
     compiled.ensure_lists()
     eng = Engine(local)
-    eng.load_compiled(compiled, index=not args.scan)
+    eng.load_compiled(compiled, index=args.index)
     ent, _off = compiled.packed()
     batch, n_hb = build_shard(dbj, info, compiled, lines, rank, seed, zipf, eng.device, world=world)
     owner = None

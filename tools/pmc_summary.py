@@ -1,0 +1,49 @@
+#!/usr/bin/env python3
+"""Turn rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE counter CSVs of a bench run into
+profiles/<config>_pass1_pmc.json: HBM bytes per step of the pass-1 kernel.
+
+Correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE is in KiB and on gfx950 reads
+1/2 of the bytes of wide coalesced streaming reads, so read bytes =
+2 * FETCH_SIZE * 1024; WRITE_SIZE * 1024 is taken as is.  The pass-1 kernel
+also issues scattered atomics whose accounting is uncalibrated, so the figure
+is a best estimate (it is reported beside, not instead of, the algorithmic
+bytes).  Usage: pmc_summary.py FETCH_CSV WRITE_CSV OUT_JSON LINES STEPS_TOTAL
+(STEPS_TOTAL = warmup + timed steps of the profiled bench run)."""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+
+def per_dispatch(path, counter):
+    vals = defaultdict(float)
+    names = {}
+    for row in csv.DictReader(open(path)):
+        if row.get('Counter_Name') != counter:
+            continue
+        d = int(row['Dispatch_Id'])
+        vals[d] += float(row['Counter_Value'])
+        names[d] = row['Kernel_Name']
+    return vals, names
+
+
+def main():
+    fetch_csv, write_csv, out, lines, steps = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), \
+        int(sys.argv[5])
+    f, fn = per_dispatch(fetch_csv, 'FETCH_SIZE')
+    w, wn = per_dispatch(write_csv, 'WRITE_SIZE')
+    # every classify+aggregate launch of pass 1 (main slices and their deferred tails)
+    fk = [v for d, v in sorted(f.items()) if 'k_pass1<0,' in fn[d]]
+    wk = [v for d, v in sorted(w.items()) if 'k_pass1<0,' in wn[d]]
+    read = 2 * 1024 * sum(fk) / steps
+    write = 1024 * sum(wk) / steps
+    res = {'hbm_bytes_per_step': read + write, 'read_bytes_per_step': read, 'write_bytes_per_step': write,
+           'lines_per_step': lines, 'steps_seen': steps, 'bytes_per_line': (read + write) / lines,
+           'method': 'rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes), k_pass1 launches, '
+                     'FETCH_SIZE x2 gfx950 correction'}
+    json.dump(res, open(out, 'w'), indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == '__main__':
+    main()

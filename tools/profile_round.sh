@@ -1,0 +1,16 @@
+#!/bin/bash
+# Profiles of the default bench workload, run on the GPU box:
+#   kernel trace + stats, then separate FETCH_SIZE / WRITE_SIZE PMC passes.
+# Usage: tools/profile_round.sh OUTDIR [extra bench args]
+set -eo pipefail
+OUT=${1:-gpurun_out/prof}
+shift || true
+export TMPDIR=/tmp
+mkdir -p "$OUT"
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
+  python3 bench.py --no-cpu-baseline --steps 5 --warmup 2 "$@" > "$OUT/bench_trace.log" 2>&1
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o pmc --output-format csv -- \
+  python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 "$@" > "$OUT/bench_fetch.log" 2>&1
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o pmc --output-format csv -- \
+  python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 "$@" > "$OUT/bench_write.log" 2>&1
+echo done
