@@ -117,6 +117,7 @@ def main():
     ap.add_argument('--config', default='cfg3', choices=sorted(CONFIGS))
     ap.add_argument('--lines', type=int, default=0, help='override lines per GPU')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--filter-slice', type=int, default=0, help='override RSA_OPT_FILTER_SLICE')
     ap.add_argument('--index', action='store_true',
                     help='classify with the tuple-space-search index instead of the prefix scan')
     args = ap.parse_args()
@@ -139,6 +140,9 @@ def main():
     compiled.ensure_lists()
     eng = Engine(local)
     eng.load_compiled(compiled, index=args.index)
+    if args.filter_slice:
+        from ruleset_analysis_amd import native
+        eng.set_option(native.RSA_OPT_FILTER_SLICE, args.filter_slice)
     ent, _off = compiled.packed()
     batch, n_hb = build_shard(dbj, info, compiled, lines, rank, seed, zipf, eng.device, world=world)
     owner = None
@@ -204,7 +208,7 @@ def main():
                        'records': n_rec},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
-                         'kernel': 'k_pass1<kClassifyAgg> (classify + aggregate; per step: 1/16 slice + rest)', 'kernel_ms': pass1_ms,
+                         'kernel': 'k_pass1<kClassifyAgg> (classify + aggregate; per step: filter slice + rest, with deferred tails)', 'kernel_ms': pass1_ms,
                          'bytes_per_line': BYTES_PER_LINE},
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -87,6 +87,7 @@ typedef struct rsa_index_slot {
 /* Options (rsa_set_option). */
 #define RSA_OPT_AUTO_FILTER 1 /* split a large first batch to derive the exact per-rule insert filter (default 1) */
 #define RSA_OPT_USE_INDEX 2   /* classify with the loaded index (1) or the linear lists (0)                  */
+#define RSA_OPT_FILTER_SLICE 5 /* auto filter: first 1/N (>= 1M lines) of a large batch builds the bound (default 256)       */
 #define RSA_OPT_SCAN_PREFIX 4  /* linear scan: list entries scanned before a lane is deferred (default 256) */
 #define RSA_OPT_PROFILE_SKIP 3 /* PROFILING ONLY, results invalid: bit0 skips counters, bit1 skips the table  */
 

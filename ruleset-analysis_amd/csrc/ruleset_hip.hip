@@ -162,37 +162,50 @@ __device__ __forceinline__ void conn_key(uint4 t, uint32_t gid, unsigned long lo
   kB = ((unsigned long long)gid << 32) | ((unsigned long long)pspell << 16) | to_port;
 }
 
-// The integer form of FirewallRule.__contains__ for a compiled entry.
-__device__ __forceinline__ bool entry_match(v4u a, v4u b, uint32_t src, uint32_t dst, uint32_t sp, uint32_t dp) {
-  return ((src - a.x) <= a.y) & ((dst - a.z) <= a.w) & ((sp - (b.x & 0xFFFFu)) <= (b.y & 0xFFFFu)) &
-         ((dp - (b.x >> 16)) <= (b.y >> 16));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// NB: bit-cast a *value*: hipcc (ROCm 7.2) miscompiles __builtin_bit_cast applied
+// directly to an ext-vector element lvalue such as b.y (it reads element 0).
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+__device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+
+// The integer form of FirewallRule.__contains__ for a compiled entry
+// (firewallrule.py:154-171; action/protocol are settled at compile time):
+// IPy containment as unsigned range tests, both port ranges at once with packed
+// 16-bit arithmetic ((p - lo) <= span per half  <=>  min(d, span) == d).
+__device__ __forceinline__ bool entry_match(v4u a, v4u b, uint32_t src, uint32_t dst, uint32_t ports) {
+  const uint32_t lo = b.x, span = b.y;
+  const u16x2 d = as_u16x2(ports) - as_u16x2(lo);
+  const u16x2 m = __builtin_elementwise_min(d, as_u16x2(span));
+  return ((src - a.x) <= a.y) & ((dst - a.z) <= a.w) & (as_u32(m) == as_u32(d));
 }
 
-// Linear first-match scan of entries [beg, end) for the `mine` lanes.
+// Linear first-match scan of entries [beg, end) for the `mine` lanes.  Entries
+// are gid-ascending, so within a block of four the first match is selected in
+// reverse order, and the wave stops once no searching lane can improve.
 __device__ __forceinline__ uint32_t scan_list(const const_v4u* E, uint32_t beg, uint32_t end, bool mine, uint32_t best,
-                                              uint32_t src, uint32_t dst, uint32_t sp, uint32_t dp) {
+                                              uint32_t src, uint32_t dst, uint32_t ports) {
   uint32_t e = beg;
-  for (; e + 4 <= end; e += 4) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const v4u a = E[2 * (e + j)];
-      const v4u b = E[2 * (e + j) + 1];
-      best = min(best, (entry_match(a, b, src, dst, sp, dp) & mine) ? b.z : kNoGid);
-    }
-    // entries are gid-ascending: stop once no searching lane can improve
-    if (__ballot(mine && best > E[2 * (e + 3) + 1].z) == 0) return best;
+  const const_v4u* p = E + 2 * (size_t)beg;
+  for (; e + 4 <= end; e += 4, p += 8) {
+    const v4u a0 = p[0], b0 = p[1], a1 = p[2], b1 = p[3], a2 = p[4], b2 = p[5], a3 = p[6], b3 = p[7];
+    uint32_t c = entry_match(a3, b3, src, dst, ports) ? b3.z : kNoGid;
+    c = entry_match(a2, b2, src, dst, ports) ? b2.z : c;
+    c = entry_match(a1, b1, src, dst, ports) ? b1.z : c;
+    c = entry_match(a0, b0, src, dst, ports) ? b0.z : c;
+    if (mine) best = min(best, c);
+    if (__ballot(mine && best > b3.z) == 0) return best;
   }
-  for (; e < end; ++e) {
-    const v4u a = E[2 * e];
-    const v4u b = E[2 * e + 1];
-    best = min(best, (entry_match(a, b, src, dst, sp, dp) & mine) ? b.z : kNoGid);
+  for (; e < end; ++e, p += 2) {
+    const v4u a = p[0], b = p[1];
+    if (mine && entry_match(a, b, src, dst, ports)) best = min(best, b.z);
   }
   return best;
 }
 
 // Tuple-space search for the `mine` lanes of list L.
 __device__ __forceinline__ uint32_t search_index(const Rules& R, uint32_t L, bool mine, uint32_t src, uint32_t dst,
-                                                 uint32_t ports, uint32_t sp, uint32_t dp) {
+                                                 uint32_t ports) {
   uint32_t best = kNoGid;
   const uint32_t sb = R.shape_off[L], se = R.shape_off[L + 1];
   for (uint32_t s = sb; s < se; ++s) {
@@ -215,7 +228,7 @@ __device__ __forceinline__ uint32_t search_index(const Rules& R, uint32_t L, boo
     }
   }
   const uint32_t rb = R.resid_off[L], re = R.resid_off[L + 1];
-  if (rb < re) best = scan_list(R.resid, rb, re, mine, best, src, dst, sp, dp);
+  if (rb < re) best = scan_list(R.resid, rb, re, mine, best, src, dst, ports);
   return best;
 }
 
@@ -236,7 +249,6 @@ __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Ru
   uint32_t best = kNoGid;
   unsigned long long pending = __ballot(active);
   const uint32_t src = t.x, dst = t.y;
-  const uint32_t sp = t.z & 0xFFFFu, dp = t.z >> 16;
   while (pending) {
     const int leader = __builtin_ctzll(pending);
     const uint32_t L = __builtin_amdgcn_readlane(list, leader);
@@ -244,12 +256,12 @@ __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Ru
     pending &= ~__ballot(mine);
     uint32_t b;
     if (R.indexed) {
-      b = search_index(R, L, mine, src, dst, t.z, sp, dp);
+      b = search_index(R, L, mine, src, dst, t.z);
     } else {
       const uint32_t beg = R.off[L], end = R.off[L + 1];
       const uint32_t lo = (end - beg > from) ? beg + from : end;
       const uint32_t hi = (end - beg > limit) ? beg + limit : end;
-      b = scan_list(R.e, lo, hi, mine, kNoGid, src, dst, sp, dp);
+      b = scan_list(R.e, lo, hi, mine, kNoGid, src, dst, t.z);
       if (b == kNoGid && hi < end) b = kDefer;
     }
     if (mine) best = b;
@@ -647,7 +659,8 @@ struct rsa_ctx {
   bool auto_tighten = true;
   bool tightened = false;
   uint32_t profile_skip = 0;
-  uint32_t scan_prefix = 256;         // linear scan: entries per list scanned before deferring a lane
+  uint32_t scan_prefix = 256;
+  uint32_t filter_slice = 256;        // auto filter: the first 1/filter_slice of a large batch builds the bound         // linear scan: entries per list scanned before deferring a lane
   uint32_t* d_tail = nullptr;         // deferred line indices
   unsigned long long* d_tail_n = nullptr;
   unsigned long long tail_alloc = 0;
@@ -886,8 +899,8 @@ int ensure_events(rsa_ctx* c) {
 }
 
 // Pass 1 over one batch.  With auto-tightening, a large first batch is split:
-// the first 1/16 builds the table, the filter is computed, and the rest of the
-// batch skips the table for lines that cannot change any output.
+// the first 1/filter_slice builds the table, the filter is computed, and the
+// rest of the batch skips the table for lines that cannot change any output.
 int run_pass1(rsa_ctx* c, int mode, const rsa_tuple* T, const uint32_t* TS, const uint64_t* ORD, const int32_t* G,
               int32_t* gout, uint64_t n) {
   int rc = ensure_events(c);
@@ -948,7 +961,8 @@ int run_pass1(rsa_ctx* c, int mode, const rsa_tuple* T, const uint32_t* TS, cons
   c->table_dirty = true;
   const uint64_t kMinSplit = 1ull << 22;
   if (c->auto_tighten && !c->tightened && c->cap > 0 && n >= kMinSplit) {
-    const uint64_t first = n / 16;
+    uint64_t first = n / c->filter_slice;
+    if (first < (1ull << 20)) first = n < (1ull << 21) ? n / 2 : (1ull << 20);
     rc = launch(0, first);
     if (rc) return rc;
     uint32_t ncap = 0;
@@ -1037,6 +1051,10 @@ int rsa_set_option(rsa_ctx* c, int option, int64_t value) {
   switch (option) {
     case RSA_OPT_AUTO_FILTER:
       c->auto_tighten = value != 0;
+      return RSA_OK;
+    case RSA_OPT_FILTER_SLICE:
+      if (value < 2 || value > 65536) return fail(c, RSA_ERR_ARG, "filter slice must be in [2, 65536]");
+      c->filter_slice = (uint32_t)value;
       return RSA_OK;
     case RSA_OPT_SCAN_PREFIX:
       if (value <= 0) return fail(c, RSA_ERR_ARG, "scan prefix must be positive");
