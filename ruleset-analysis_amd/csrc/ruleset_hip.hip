@@ -659,8 +659,8 @@ struct rsa_ctx {
   bool auto_tighten = true;
   bool tightened = false;
   uint32_t profile_skip = 0;
-  uint32_t scan_prefix = 256;
-  uint32_t filter_slice = 256;        // auto filter: the first 1/filter_slice of a large batch builds the bound         // linear scan: entries per list scanned before deferring a lane
+  uint32_t scan_prefix = 256;         // linear scan: entries per list scanned before deferring a lane
+  uint32_t filter_slice = 256;        // auto filter: the first 1/filter_slice of a large batch builds the bound
   uint32_t* d_tail = nullptr;         // deferred line indices
   unsigned long long* d_tail_n = nullptr;
   unsigned long long tail_alloc = 0;
