@@ -118,6 +118,7 @@ def main():
     ap.add_argument('--lines', type=int, default=0, help='override lines per GPU')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--filter-slice', type=int, default=0, help='override RSA_OPT_FILTER_SLICE')
+    ap.add_argument('--opt', action='append', default=[], help='NAME=VALUE library option (e.g. SINGLE_LIST=1)')
     ap.add_argument('--index', action='store_true',
                     help='classify with the tuple-space-search index instead of the prefix scan')
     args = ap.parse_args()
@@ -140,9 +141,12 @@ def main():
     compiled.ensure_lists()
     eng = Engine(local)
     eng.load_compiled(compiled, index=args.index)
+    from ruleset_analysis_amd import native
     if args.filter_slice:
-        from ruleset_analysis_amd import native
         eng.set_option(native.RSA_OPT_FILTER_SLICE, args.filter_slice)
+    for kv in args.opt:
+        k, v = kv.split('=')
+        eng.set_option(getattr(native, 'RSA_OPT_' + k), int(v))
     ent, _off = compiled.packed()
     batch, n_hb = build_shard(dbj, info, compiled, lines, rank, seed, zipf, eng.device, world=world)
     owner = None

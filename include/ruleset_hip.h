@@ -88,6 +88,7 @@ typedef struct rsa_index_slot {
 #define RSA_OPT_AUTO_FILTER 1 /* split a large first batch to derive the exact per-rule insert filter (default 1) */
 #define RSA_OPT_USE_INDEX 2   /* classify with the loaded index (1) or the linear lists (0)                  */
 #define RSA_OPT_FILTER_SLICE 5 /* auto filter: first 1/N (>= 1M lines) of a large batch builds the bound (default 256)       */
+#define RSA_OPT_SINGLE_LIST 6  /* stage 0 scans only each wave's majority list, others deferred (default 0)  */
 #define RSA_OPT_SCAN_PREFIX 4  /* linear scan: list entries scanned before a lane is deferred (default 256) */
 #define RSA_OPT_PROFILE_SKIP 3 /* PROFILING ONLY, results invalid: bit0 skips counters, bit1 skips the table  */
 

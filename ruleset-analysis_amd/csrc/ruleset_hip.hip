@@ -81,6 +81,7 @@ struct Rules {
   const const_v4u* resid;       // residual linear entries
   const const_u32* resid_off;   // n_lists + 1
   int indexed;
+  int single_list;              // stage 0 scans only the wave's majority list
 };
 
 struct Agg {
@@ -148,6 +149,35 @@ __device__ __forceinline__ unsigned long long wave_append(bool ok, unsigned long
   if ((int)lane == leader) base = atomicAdd(cursor, (unsigned long long)__popcll(mask));
   base = __shfl(base, leader);
   return base + __popcll(mask & ((1ull << lane) - 1ull));
+}
+
+// Workgroup-aggregated append of two streams (a, b) to global cursors: one
+// device atomic per stream per workgroup call (a single hot cursor would
+// otherwise take one atomic per wave).  Every thread of the workgroup must call
+// it (workgroup-uniform control flow).  sh: 4 LDS words.
+__device__ __forceinline__ void block_append2(bool a, bool b, unsigned long long* cur_a, unsigned long long* cur_b,
+                                              unsigned long long* sh, unsigned long long& pos_a,
+                                              unsigned long long& pos_b) {
+  const unsigned long long ma = __ballot(a), mb = __ballot(b);
+  const unsigned lane = __lane_id();
+  const unsigned long long below = (1ull << lane) - 1ull;
+  unsigned long long wa = 0, wb = 0;
+  if (lane == 0) {
+    if (ma) wa = atomicAdd(&sh[0], (unsigned long long)__popcll(ma));
+    if (mb) wb = atomicAdd(&sh[1], (unsigned long long)__popcll(mb));
+  }
+  wa = __shfl(wa, 0);
+  wb = __shfl(wb, 0);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    sh[2] = sh[0] ? atomicAdd(cur_a, sh[0]) : 0ull;
+    sh[3] = sh[1] ? atomicAdd(cur_b, sh[1]) : 0ull;
+    sh[0] = 0;
+    sh[1] = 0;
+  }
+  __syncthreads();
+  pos_a = sh[2] + wa + __popcll(ma & below);
+  pos_b = sh[3] + wb + __popcll(mb & below);
 }
 
 // Reducer key of a tuple (connlist-reducer.py:162: PROTO;FROMIP;TOIP;TOPORT).
@@ -232,13 +262,40 @@ __device__ __forceinline__ uint32_t search_index(const Rules& R, uint32_t L, boo
   return best;
 }
 
-constexpr uint32_t kDefer = 0xFFFFFFFEu;
+constexpr uint32_t kDefer = 0xFFFFFFFEu;       // deferred after the list prefix (tail resumes at the prefix)
+constexpr uint32_t kDeferList = 0xFFFFFFFDu;   // deferred before any scan: not the wave's list
+
+// Stage-0 classification with the linear lists: the wave scans ONE list, its
+// majority list (approximated from the leader's list), over the first `limit`
+// entries.  Lanes of other lists return kDeferList (stage 1 scans their prefix
+// in waves that are mostly single-list again) and lanes with no match in the
+// prefix return kDefer (stage 2 scans the rest of their list).
+__device__ __forceinline__ uint32_t classify_main(uint4 t, bool active, const Rules& R, unsigned int* flags,
+                                                  uint32_t limit) {
+  const uint32_t list = t.w & 0xFFFFu;
+  if (active && list >= R.n_lists) {
+    atomicOr(&flags[1], 1u);
+    active = false;
+  }
+  const unsigned long long act = __ballot(active);
+  if (act == 0) return kNoGid;
+  uint32_t L = __builtin_amdgcn_readlane(list, __builtin_ctzll(act));
+  const unsigned long long m1 = __ballot(active && list == L);
+  if (2 * __popcll(m1) < __popcll(act)) L = __builtin_amdgcn_readlane(list, __builtin_ctzll(act & ~m1));
+  const bool mine = active && list == L;
+  const uint32_t beg = R.off[L], end = R.off[L + 1];
+  const uint32_t hi = (end - beg > limit) ? beg + limit : end;
+  uint32_t b = scan_list(R.e, beg, hi, mine, kNoGid, t.x, t.y, t.z);
+  if (b == kNoGid && hi < end) b = kDefer;
+  if (!active) return kNoGid;
+  return mine ? b : kDeferList;
+}
 
 // First-match classification of one wave of tuples: waterfall over the distinct
 // candidate lists present in the wave (list id broadcast by readlane).  With the
 // linear lists, only entries [from, limit) of each list are scanned; a lane with
-// no match there whose list continues past `limit` returns kDefer (the tail
-// kernel finishes it from `limit`, in dense waves).  limit = ~0: whole list.
+// no match there whose list continues past `limit` returns kDefer.  limit = ~0:
+// whole list.  With the index, the whole list is searched.
 __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Rules& R, unsigned int* flags,
                                                   uint32_t from = 0, uint32_t limit = 0xFFFFFFFFu) {
   const uint32_t list = t.w & 0xFFFFu;
@@ -354,48 +411,61 @@ __device__ __forceinline__ void wave_count2(bool m, bool h, uint32_t key, unsign
 
 // Pass 1.  kLds > 0: the per-rule line/hit counters of up to kLds rules are
 // privatised in LDS for the whole (persistent) workgroup and flushed once at the
-// end; otherwise they are wave-aggregated device atomics.  kTail: process the
-// deferred lines (indices in tail[0..*tail_n)) from list position `prefix` on;
-// otherwise scan list prefixes of `prefix` entries and defer the rest.
-template <int kMode, int kThreads, int kLds, bool kTail>
+// end; otherwise they are wave-aggregated device atomics.
+// Linear-list classification runs in three stages so that waves stay dense and
+// single-list: stage 0 = every line, majority list of the wave, first `prefix`
+// entries; stage 1 = lines of other lists (tailA), their first `prefix`
+// entries; stage 2 = lines unmatched in their prefix (tailB), the rest of the
+// list.  A line is aggregated by the stage that classifies it.
+template <int kMode, int kThreads, int kLds, int kStage>
 __global__ __launch_bounds__(kThreads) void k_pass1(const uint4* __restrict__ T, const uint32_t* __restrict__ TS,
                                                     const unsigned long long* __restrict__ ORD, unsigned long long n,
                                                     const int32_t* __restrict__ gin, int32_t* __restrict__ gout,
-                                                    Rules R, Agg A, uint32_t prefix, uint32_t* tail,
-                                                    unsigned long long* tail_n) {
+                                                    Rules R, Agg A, uint32_t prefix, uint32_t* tailA,
+                                                    unsigned long long* tailA_n, uint32_t* tailB,
+                                                    unsigned long long* tailB_n) {
   __shared__ uint32_t lds_cnt[kLds > 0 ? 2 * kLds : 1];
+  __shared__ unsigned long long lds_app[4];
   const bool counters = kMode != kClassifyOnly && !(A.skip & 1u);
+  if (threadIdx.x < 4) lds_app[threadIdx.x] = 0;
   if (kLds > 0 && counters) {
     for (uint32_t r = threadIdx.x; r < 2u * kLds; r += kThreads) lds_cnt[r] = 0;
-    __syncthreads();
   }
-  if (kTail) n = *tail_n;
+  __syncthreads();
+  if (kStage == 1) n = *tailA_n;
+  if (kStage == 2) n = *tailB_n;
   const unsigned long long stride = (unsigned long long)gridDim.x * kThreads;
   for (unsigned long long base = (unsigned long long)blockIdx.x * kThreads; base < n; base += stride) {
     const unsigned long long j = base + threadIdx.x;
     const bool in = j < n;
-    const unsigned long long i = kTail ? (in ? tail[j] : 0ull) : j;
+    unsigned long long i = j;
+    if (kStage == 1) i = in ? tailA[j] : 0u;
+    if (kStage == 2) i = in ? tailB[j] : 0u;
     const uint4 t = in ? T[i] : make_uint4(0u, 0u, 0u, 0u);
     const uint32_t flags = (t.w >> 16) & 0xFFu;
+    const bool valid = in && (flags & RSA_F_VALID);
     uint32_t gid;
     if (kMode == kGivenAgg) {
       gid = in ? (uint32_t)gin[i] : kNoGid;
-    } else if (kTail) {
-      gid = classify_wave(t, in && (flags & RSA_F_VALID), R, A.flags, prefix);
+    } else if (R.indexed) {
+      gid = classify_wave(t, valid, R, A.flags);
+    } else if (kStage == 0) {
+      gid = R.single_list ? classify_main(t, valid, R, A.flags, prefix)
+                          : classify_wave(t, valid, R, A.flags, 0, prefix);
+    } else if (kStage == 1) {
+      gid = classify_wave(t, valid, R, A.flags, 0, prefix);
     } else {
-      gid = classify_wave(t, in && (flags & RSA_F_VALID), R, A.flags, 0, prefix);
+      gid = classify_wave(t, valid, R, A.flags, prefix);
     }
-    if (kMode != kGivenAgg && !kTail) {
-      const bool defer = gid == kDefer;
-      const unsigned long long pos = wave_append(defer, tail_n);
-      if (defer) {
-        tail[pos] = (uint32_t)i;
-        gid = kNoGid;   // finished by the tail kernel: nothing else to do here
-      }
-      if (gout && in && !defer) gout[i] = (int32_t)gid;
-      if (defer) continue;
-    } else if (kMode != kGivenAgg && gout && in) {
-      gout[i] = (int32_t)gid;
+    if (kMode != kGivenAgg) {
+      const bool to_a = gid == kDeferList;
+      const bool to_b = gid == kDefer;
+      unsigned long long pa, pb;
+      block_append2(to_a, to_b, tailA_n, tailB_n, lds_app, pa, pb);
+      if (to_a) tailA[pa] = (uint32_t)i;
+      if (to_b) tailB[pb] = (uint32_t)i;
+      if (to_a || to_b) continue;   // finished by a later stage
+      if (gout && in) gout[i] = (int32_t)gid;
     }
     if (kMode == kClassifyOnly) continue;
     if (gid != kNoGid && gid >= R.n_rules) atomicOr(&A.flags[1], 2u);
@@ -660,6 +730,7 @@ struct rsa_ctx {
   bool tightened = false;
   uint32_t profile_skip = 0;
   uint32_t scan_prefix = 256;         // linear scan: entries per list scanned before deferring a lane
+  bool single_list = false;
   uint32_t filter_slice = 256;        // auto filter: the first 1/filter_slice of a large batch builds the bound
   uint32_t* d_tail = nullptr;         // deferred line indices
   unsigned long long* d_tail_n = nullptr;
@@ -712,6 +783,7 @@ Rules rules_of(const rsa_ctx* c) {
   r.resid = (const const_v4u*)(c->d_resid);
   r.resid_off = (const const_u32*)(c->d_resid_off);
   r.indexed = c->indexed ? 1 : 0;
+  r.single_list = c->single_list ? 1 : 0;
   return r;
 }
 
@@ -734,7 +806,7 @@ Agg agg_of(const rsa_ctx* c) {
 
 // LDS-privatised counter capacities (rules): 2 x 4 B per rule.
 constexpr int kLdsSmall = 10240;   // 80 KiB: two 1024-thread workgroups per CU (32 waves)
-constexpr int kLdsLarge = 20480;   // 160 KiB: one workgroup per CU
+constexpr int kLdsLarge = 20448;   // ~160 KiB (minus the append scratch): one workgroup per CU
 
 unsigned grid_for_threads(const rsa_ctx* c, unsigned long long n, unsigned threads, unsigned per_cu) {
   unsigned long long g = (n + threads - 1) / threads;
@@ -880,14 +952,16 @@ int cap_select(rsa_ctx* c, unsigned long long* out, uint32_t* h_n_capped) {
   return RSA_OK;
 }
 
+// Two deferred-line regions of `tail_alloc` entries each (stage-1 and stage-2
+// inputs) and their two counters.
 int ensure_tail(rsa_ctx* c, unsigned long long n) {
-  if (!c->d_tail_n) HIPCHK(c, hipMalloc(&c->d_tail_n, sizeof(unsigned long long)));
+  if (!c->d_tail_n) HIPCHK(c, hipMalloc(&c->d_tail_n, 2 * sizeof(unsigned long long)));
   if (n <= c->tail_alloc) return RSA_OK;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   hipFree(c->d_tail);
   c->d_tail = nullptr;
   c->tail_alloc = 0;
-  HIPCHK(c, hipMalloc(&c->d_tail, n * sizeof(uint32_t)));
+  HIPCHK(c, hipMalloc(&c->d_tail, 2 * n * sizeof(uint32_t)));
   c->tail_alloc = n;
   return RSA_OK;
 }
@@ -917,47 +991,51 @@ int run_pass1(rsa_ctx* c, int mode, const rsa_tuple* T, const uint32_t* TS, cons
     const uint32_t K = c->indexed ? 0xFFFFFFFFu : c->scan_prefix;
     int rc2 = ensure_tail(c, m);
     if (rc2) return rc2;
-    HIPCHK(c, hipMemsetAsync(c->d_tail_n, 0, sizeof(unsigned long long), c->stream));
-    uint32_t* tl = c->d_tail;
-    unsigned long long* tn = c->d_tail_n;
+    HIPCHK(c, hipMemsetAsync(c->d_tail_n, 0, 2 * sizeof(unsigned long long), c->stream));
+    uint32_t* ta = c->d_tail;
+    uint32_t* tb = c->d_tail + c->tail_alloc;
+    unsigned long long* na = c->d_tail_n;
+    unsigned long long* nb = c->d_tail_n + 1;
     if (c->n_rules <= kLdsSmall) {
       // two 1024-thread workgroups (80 KiB of counters each) per CU
       const unsigned g = grid_for_threads(c, m, 1024, 2);
       if (mode == kClassifyAgg)
-        k_pass1<kClassifyAgg, 1024, kLdsSmall, false><<<g, 1024, 0, c->stream>>>(t, TS + a, o, m, nullptr, go, r, ag,
-                                                                                 K, tl, tn);
+        k_pass1<kClassifyAgg, 1024, kLdsSmall, 0><<<g, 1024, 0, c->stream>>>(t, TS + a, o, m, nullptr, go, r, ag, K,
+                                                                             ta, na, tb, nb);
       else
-        k_pass1<kGivenAgg, 1024, kLdsSmall, false><<<g, 1024, 0, c->stream>>>(t, TS + a, o, m, gi, nullptr, r, ag, K,
-                                                                              tl, tn);
+        k_pass1<kGivenAgg, 1024, kLdsSmall, 0><<<g, 1024, 0, c->stream>>>(t, TS + a, o, m, gi, nullptr, r, ag, K,
+                                                                          ta, na, tb, nb);
     } else if (c->n_rules <= kLdsLarge) {
       const unsigned g = grid_for_threads(c, m, 1024, 1);
       if (mode == kClassifyAgg)
-        k_pass1<kClassifyAgg, 1024, kLdsLarge, false><<<g, 1024, 0, c->stream>>>(t, TS + a, o, m, nullptr, go, r, ag,
-                                                                                 K, tl, tn);
+        k_pass1<kClassifyAgg, 1024, kLdsLarge, 0><<<g, 1024, 0, c->stream>>>(t, TS + a, o, m, nullptr, go, r, ag, K,
+                                                                             ta, na, tb, nb);
       else
-        k_pass1<kGivenAgg, 1024, kLdsLarge, false><<<g, 1024, 0, c->stream>>>(t, TS + a, o, m, gi, nullptr, r, ag, K,
-                                                                              tl, tn);
+        k_pass1<kGivenAgg, 1024, kLdsLarge, 0><<<g, 1024, 0, c->stream>>>(t, TS + a, o, m, gi, nullptr, r, ag, K,
+                                                                          ta, na, tb, nb);
     } else {
       const unsigned g = grid_for(c, m, 16);
       if (mode == kClassifyAgg)
-        k_pass1<kClassifyAgg, kBlock, 0, false><<<g, kBlock, 0, c->stream>>>(t, TS + a, o, m, nullptr, go, r, ag, K,
-                                                                             tl, tn);
+        k_pass1<kClassifyAgg, kBlock, 0, 0><<<g, kBlock, 0, c->stream>>>(t, TS + a, o, m, nullptr, go, r, ag, K, ta,
+                                                                         na, tb, nb);
       else
-        k_pass1<kGivenAgg, kBlock, 0, false><<<g, kBlock, 0, c->stream>>>(t, TS + a, o, m, gi, nullptr, r, ag, K, tl,
-                                                                          tn);
+        k_pass1<kGivenAgg, kBlock, 0, 0><<<g, kBlock, 0, c->stream>>>(t, TS + a, o, m, gi, nullptr, r, ag, K, ta, na,
+                                                                      tb, nb);
     }
     HIPCHK(c, hipGetLastError());
     if (mode == kClassifyAgg && K != 0xFFFFFFFFu) {
-      // finish the deferred lines (count read on the device: no host sync)
-      k_pass1<kClassifyAgg, kBlock, 0, true><<<c->cu_count * 4, kBlock, 0, c->stream>>>(t, TS + a, o, m, nullptr, go,
-                                                                                      r, ag, K, tl, tn);
+      // stages 1 and 2 (their sizes are read on the device: no host sync)
+      k_pass1<kClassifyAgg, kBlock, 0, 1><<<c->cu_count * 8, kBlock, 0, c->stream>>>(t, TS + a, o, m, nullptr, go, r,
+                                                                                     ag, K, ta, na, tb, nb);
+      k_pass1<kClassifyAgg, kBlock, 0, 2><<<c->cu_count * 4, kBlock, 0, c->stream>>>(t, TS + a, o, m, nullptr, go, r,
+                                                                                     ag, K, ta, na, tb, nb);
     }
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(c->ev[c->ev_used + 1], c->stream));
     c->ev_used += 2;
     return RSA_OK;
   };
-  if (n > 0xFFFFFFFFull) return fail(c, RSA_ERR_ARG, "batch larger than 2^32 tuples: split it");
+  if (n > 0x7FFFFFFFull) return fail(c, RSA_ERR_ARG, "batch larger than 2^31 tuples: split it");
   c->table_dirty = true;
   const uint64_t kMinSplit = 1ull << 22;
   if (c->auto_tighten && !c->tightened && c->cap > 0 && n >= kMinSplit) {
@@ -1055,6 +1133,9 @@ int rsa_set_option(rsa_ctx* c, int option, int64_t value) {
     case RSA_OPT_FILTER_SLICE:
       if (value < 2 || value > 65536) return fail(c, RSA_ERR_ARG, "filter slice must be in [2, 65536]");
       c->filter_slice = (uint32_t)value;
+      return RSA_OK;
+    case RSA_OPT_SINGLE_LIST:
+      c->single_list = value != 0;
       return RSA_OK;
     case RSA_OPT_SCAN_PREFIX:
       if (value <= 0) return fail(c, RSA_ERR_ARG, "scan prefix must be positive");
@@ -1230,19 +1311,25 @@ int rsa_classify_only(rsa_ctx* c, const rsa_tuple* T, uint64_t n, int32_t* gout)
   if (n == 0) return RSA_OK;
   if (!T || !gout) return fail(c, RSA_ERR_ARG, "null tuple/gid pointer");
   if (!c->d_flags) return fail(c, RSA_ERR_STATE, "ctx not initialised");
-  if (n > 0xFFFFFFFFull) return fail(c, RSA_ERR_ARG, "batch larger than 2^32 tuples");
+  if (n > 0x7FFFFFFFull) return fail(c, RSA_ERR_ARG, "batch larger than 2^31 tuples");
   Agg a = agg_of(c);
   const uint32_t K = c->indexed ? 0xFFFFFFFFu : c->scan_prefix;
   int rc = ensure_tail(c, n);
   if (rc) return rc;
-  HIPCHK(c, hipMemsetAsync(c->d_tail_n, 0, sizeof(unsigned long long), c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_tail_n, 0, 2 * sizeof(unsigned long long), c->stream));
   const uint4* t4 = reinterpret_cast<const uint4*>(T);
-  k_pass1<kClassifyOnly, kBlock, 0, false><<<grid_for(c, n, 16), kBlock, 0, c->stream>>>(
-      t4, nullptr, nullptr, n, nullptr, gout, rules_of(c), a, K, c->d_tail, c->d_tail_n);
+  uint32_t* ta = c->d_tail;
+  uint32_t* tb = c->d_tail + c->tail_alloc;
+  unsigned long long* na = c->d_tail_n;
+  unsigned long long* nb = c->d_tail_n + 1;
+  k_pass1<kClassifyOnly, kBlock, 0, 0><<<grid_for(c, n, 16), kBlock, 0, c->stream>>>(
+      t4, nullptr, nullptr, n, nullptr, gout, rules_of(c), a, K, ta, na, tb, nb);
   HIPCHK(c, hipGetLastError());
   if (K != 0xFFFFFFFFu) {
-    k_pass1<kClassifyOnly, kBlock, 0, true><<<c->cu_count * 4, kBlock, 0, c->stream>>>(
-        t4, nullptr, nullptr, n, nullptr, gout, rules_of(c), a, K, c->d_tail, c->d_tail_n);
+    k_pass1<kClassifyOnly, kBlock, 0, 1><<<c->cu_count * 8, kBlock, 0, c->stream>>>(
+        t4, nullptr, nullptr, n, nullptr, gout, rules_of(c), a, K, ta, na, tb, nb);
+    k_pass1<kClassifyOnly, kBlock, 0, 2><<<c->cu_count * 4, kBlock, 0, c->stream>>>(
+        t4, nullptr, nullptr, n, nullptr, gout, rules_of(c), a, K, ta, na, tb, nb);
     HIPCHK(c, hipGetLastError());
   }
   return RSA_OK;

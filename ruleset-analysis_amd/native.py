@@ -31,6 +31,7 @@ class NativeError(RuntimeError):
 
 RSA_OK, RSA_ERR_ARG, RSA_ERR_HIP, RSA_ERR_STATE, RSA_ERR_CAPACITY = 0, -1, -2, -3, -4
 RSA_OPT_AUTO_FILTER, RSA_OPT_USE_INDEX, RSA_OPT_PROFILE_SKIP, RSA_OPT_SCAN_PREFIX, RSA_OPT_FILTER_SLICE = 1, 2, 3, 4, 5
+RSA_OPT_SINGLE_LIST = 6
 
 P = ctypes.c_void_p
 U32 = ctypes.c_uint32

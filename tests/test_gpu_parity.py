@@ -152,6 +152,19 @@ def test_synth_parity_tightened_filter_shuffled(engine):
     _gpu_vs_oracle(engine, 800, 5_000_000, 40, seed=17, zipf=1.2, shuffle=True)
 
 
+def test_synth_parity_single_list_stages(engine):
+    """Majority-list stage 0 + both tail stages (tiny prefix): same answers."""
+    from ruleset_analysis_amd import native
+    engine.set_option(native.RSA_OPT_SINGLE_LIST, 1)
+    engine.set_option(native.RSA_OPT_SCAN_PREFIX, 5)
+    try:
+        _gpu_vs_oracle(engine, 1500, 300000, 40, seed=24, index=False, zipf=1.1,
+                       interfaces=('outside', 'partner'))
+    finally:
+        engine.set_option(native.RSA_OPT_SINGLE_LIST, 0)
+        engine.set_option(native.RSA_OPT_SCAN_PREFIX, 256)
+
+
 def test_deterministic(engine):
     dbj, info = synth.make_db(21, 800)
     tr = synth.make_traffic((dbj, info), 100000, seed=22, zipf=1.2)
