@@ -2,9 +2,10 @@
 """Benchmark of the ruleset-analysis hot path on MI355X.
 
 Metric (BASELINE.json): log lines/sec classified (node) at 10k rules; % of the
-HBM roofline.  Workload = BASELINE config 3 per GPU: a 10k-rule ACL
-(replicated), 125M synthetic ASA connection tuples per GPU (weak scaling:
-N GPUs process N x 125M lines of one global log, order keys global), cap 1000.
+HBM/VALU roofline.  Workload = BASELINE config 3 per GPU: a 10k-rule ACL
+(replicated; no catch-all permit, so first matches spread over the whole
+list), 125M synthetic ASA connection tuples per GPU (weak scaling: N GPUs
+process N x 125M lines of one global log, order keys global), cap 1000.
 
 One step = the whole job over the resident batch: pass 1 (first-match
 classification fused with per-rule counters and the distinct-connection
@@ -37,11 +38,16 @@ from ruleset_analysis_amd.pipeline import built_hit_count  # noqa: E402
 
 BYTES_PER_LINE = 28          # 16 B tuple + 4 B timestamp code + 8 B order key
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
+# int32 VALU lane-ops/s: 256 CUs x 4 SIMDs x 32 lanes/cycle x 2.4 GHz (MI355X_MICROARCH.md:
+# a wave issues one VALU instruction over 2 cycles, 32 lanes per cycle)
+VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9
+OPS_PER_EVAL = 8             # 2 per address range test x 2 + 2 per port range test x 2
 CONFIGS = {
-    # name: (rules, lines per GPU, cap, seed, zipf, interfaces)
-    'cfg3': (10000, 125_000_000, 1000, 3, None, ('outside',)),
-    'cfg2': (1000, 100_000_000, 1000, 2, None, ('outside',)),
-    'cfg5': (2500, 100_000_000, 1000, 5, 1.1, ('outside', 'partner', 'vpn', 'extranet')),
+    # name: (rules, lines per GPU, cap, seed, zipf, interfaces, broad)
+    'cfg3': (10000, 125_000_000, 1000, 3, None, ('outside',), False),
+    'cfg3_broad': (10000, 125_000_000, 1000, 3, None, ('outside',), True),
+    'cfg2': (1000, 100_000_000, 1000, 2, None, ('outside',), False),
+    'cfg5': (2500, 100_000_000, 1000, 5, 1.1, ('outside', 'partner', 'vpn', 'extranet'), False),
 }
 
 
@@ -97,6 +103,27 @@ def cpu_baseline(dbj, info, seconds=15.0):
                       '(mapper | LC_ALL=C sort | reducer restated in Python, 1 process), %.1f s' % (n, dt)}
 
 
+def scan_work(compiled, batch, gids):
+    """Sum over lines of E(t): the 1-based position of the
+    first match in the line's compiled permit-only candidate list, or the list
+    length when nothing matches; 0 for lines that are not classified.  Computed
+    on the GPU from the pass-1 gids (a searchsorted per line)."""
+    import torch
+    ent, off = compiled.packed()
+    dev = gids.device
+    lists = (batch.tuples[:, 3] & 0xFFFF).long()
+    valid = ((batch.tuples[:, 3] >> 16) & 1) == 1
+    off_t = torch.from_numpy(off.astype(np.int64)).to(dev)
+    length = (off_t[1:] - off_t[:-1])[lists]
+    key = torch.from_numpy((np.repeat(np.arange(len(off) - 1, dtype=np.int64), np.diff(off).astype(np.int64)) << 32)
+                           | ent['gid'].astype(np.int64)).to(dev)
+    q = (lists << 32) | gids.long().clamp(min=0)
+    pos = torch.searchsorted(key, q) - off_t[lists] + 1
+    e = torch.where(gids >= 0, pos, length)
+    e = torch.where(valid, e, torch.zeros_like(e))
+    return int(e.sum().item())
+
+
 def read_traffic(name):
     """HBM bytes of the pass-1 kernel launches of one step (the 1/16 slice and the
     rest, summed like `achieved`) from a committed rocprofv3 PMC summary
@@ -118,9 +145,9 @@ def main():
     ap.add_argument('--lines', type=int, default=0, help='override lines per GPU')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--filter-slice', type=int, default=0, help='override RSA_OPT_FILTER_SLICE')
-    ap.add_argument('--opt', action='append', default=[], help='NAME=VALUE library option (e.g. SINGLE_LIST=1)')
-    ap.add_argument('--index', action='store_true',
-                    help='classify with the tuple-space-search index instead of the prefix scan')
+    ap.add_argument('--opt', action='append', default=[], help='NAME=VALUE library option (e.g. FILTER_STEPS=3)')
+    ap.add_argument('--no-index', action='store_true', help='classify with the plain linear scan')
+    ap.add_argument('--prefix', type=int, default=64, help='entries per list scanned before the index')
     args = ap.parse_args()
 
     import torch
@@ -132,15 +159,15 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
-    rules, lines, cap, seed, zipf, ifcs = CONFIGS[args.config]
+    rules, lines, cap, seed, zipf, ifcs, broad = CONFIGS[args.config]
     if args.lines:
         lines = args.lines
     t_setup = time.perf_counter()
-    dbj, info = synth.make_db(seed, rules, interfaces=ifcs)
+    dbj, info = synth.make_db(seed, rules, interfaces=ifcs, broad=broad)
     compiled = CompiledRules(acldb.load_json(dbj))
     compiled.ensure_lists()
     eng = Engine(local)
-    eng.load_compiled(compiled, index=args.index)
+    eng.load_compiled(compiled, index=not args.no_index, prefix=args.prefix)
     from ruleset_analysis_amd import native
     if args.filter_slice:
         eng.set_option(native.RSA_OPT_FILTER_SLICE, args.filter_slice)
@@ -195,6 +222,7 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     pass1_ms = float(np.mean(pass1_launch_ms))
+    sum_e = scan_work(compiled, batch, gbuf) if rank == 0 else 0
     if rank == 0:
         total_lines = lines * world * args.steps
         value = total_lines / dt
@@ -205,15 +233,25 @@ def main():
             'value': value, 'unit': 'lines/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
             'ms_per_step': dt / args.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
             'vs_baseline': None, 'dtype': 'u32', 'data': 'synthetic (seeded ASA connection tuples, pre-parsed, '
-                                                          'resident in HBM)',
+                                                          'resident in HBM; seeded ACL, %s)' % (
+                                                              'catch-all permits allowed' if broad else
+                                                              'no catch-all permit'),
             'config': {'workload': '%s: %d-rule ACL, %d lines per GPU, cap %d' % (args.config, compiled.n_rules,
                                                                                   lines, cap),
                        'rules': compiled.n_rules, 'lines_per_gpu': lines, 'cap': cap, 'parallelism': 'dp%d' % world,
                        'records': n_rec},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
-                         'kernel': 'k_pass1<kClassifyAgg> (classify + aggregate; per step: filter slice + rest, with deferred tails)', 'kernel_ms': pass1_ms,
-                         'bytes_per_line': BYTES_PER_LINE},
+                         'kernel': 'pass 1 = k_classify<kClassifyAgg> + k_tail + k_count (per step: filter slice(s) + '
+                                   'rest)', 'kernel_ms': pass1_ms, 'bytes_per_line': BYTES_PER_LINE,
+                         'valu': {'achieved': OPS_PER_EVAL * sum_e / (pass1_ms * 1e-3) / 1e12,
+                                  'peak': VALU_PEAK_OPS / 1e12, 'unit': 'Tops/s',
+                                  'frac': OPS_PER_EVAL * sum_e / (pass1_ms * 1e-3) / VALU_PEAK_OPS,
+                                  'mean_scan_position': sum_e / lines,
+                                  'definition': 'SURVEY.md 8d linear-scan work: 8 int ops x E(t) per line, E = '
+                                                '1-based first-match position in the permit-only candidate list '
+                                                '(list length if unmatched); the index does less work than this, '
+                                                'so frac > 1 is possible'}},
         }
         if world == 1 and not args.no_cpu_baseline:
             res['cpu_baseline'] = cpu_baseline(dbj, info)

@@ -61,35 +61,43 @@ typedef struct rsa_rule_entry {
   uint32_t reserved;
 } rsa_rule_entry;
 
-/* Tuple-space-search index (optional).  For one candidate list, the entries
+/* Perfect-hash tuple-space index (optional; compile.py build_index).  Per
+ * candidate list: entries [0, prefix) are scanned linearly; entries >= prefix
  * whose addresses are prefixes and whose ports are "any" or one value are
- * grouped by shape (src mask, dst mask, port mask); each shape owns an
- * open-addressing table of 16-B slots keyed by the masked (src, dst, ports)
- * whose value is the smallest gid with that key.  Shapes of a list are stored
- * in ascending min_gid order; entries that fit no shape (port ranges, odd
- * address ranges) stay in a per-list residual list scanned linearly.  The
- * answer is identical to the linear scan: the minimum matching gid. */
-typedef struct rsa_shape {
-  uint32_t src_mask, dst_mask; /* address prefix masks                       */
-  uint32_t port_mask;          /* 0xFFFF per exact port half, 0 for "any"     */
-  uint32_t min_gid;            /* smallest gid in the shape                  */
-  uint32_t table_off;          /* first slot of this shape's table           */
-  uint32_t table_mask;         /* table size - 1 (power of two)              */
-  uint32_t salt;               /* hash salt (unique per shape)               */
-  uint32_t reserved;
-} rsa_shape;
+ * grouped by shape (src mask, dst mask, port mask), and each shape owns a CHD
+ * (hash-and-displace) perfect-hash table over the masked key
+ * (src & src_mask, dst & dst_mask, ports & port_mask), ports = sport | dport << 16:
+ *   H    = fmix32(ks ^ 0x9E3779B9) ^ fmix32(kd ^ 0x7F4A7C15) ^ fmix32(kp ^ 0x2545F491)
+ *   d    = disp[disp_off + ((H >> 16) & disp_mask)]            (uint16 units)
+ *   slot = hi32((H + ((d * ((H >> 16) | 1)) << 16)) * n_slots)  (32-bit wrap)
+ *   word = image[slot_off + slot] = (H & 0xFFFF) << 16 | list-local entry index,
+ *          0xFFFFFFFF = empty
+ * and holds the smallest entry index with that key.  All other entries are
+ * residual (a gid-ascending list scanned linearly).  The answer is identical to
+ * the linear scan: the minimum matching gid (the device verifies the hashed
+ * candidate against the full entry). */
+typedef struct rsa_pht_shape {
+  uint32_t src_mask, dst_mask, port_mask;
+  uint32_t min_idx;    /* smallest list-local entry index in the shape           */
+  uint32_t slot_off;   /* first slot word in the image                           */
+  uint32_t disp_off;   /* first displacement, in uint16 units of the image       */
+  uint32_t n_slots;    /* table size (slots)                                     */
+  uint32_t disp_mask;  /* displacement buckets - 1 (power of two)                */
+} rsa_pht_shape;
 
-typedef struct rsa_index_slot {
-  uint32_t src, dst, ports; /* masked key; ports = sport | dport << 16 */
-  uint32_t gid;             /* 0xFFFFFFFF = empty                     */
-} rsa_index_slot;
+typedef struct rsa_pht_list {
+  uint32_t shape_beg, shape_end; /* this list's shapes                           */
+  uint32_t resid_beg, resid_end; /* this list's residual entries                 */
+  uint32_t prefix;               /* entries scanned linearly before the index    */
+  uint32_t reserved[3];
+} rsa_pht_list;
 
 /* Options (rsa_set_option). */
 #define RSA_OPT_AUTO_FILTER 1 /* split a large first batch to derive the exact per-rule insert filter (default 1) */
 #define RSA_OPT_USE_INDEX 2   /* classify with the loaded index (1) or the linear lists (0)                  */
 #define RSA_OPT_FILTER_SLICE 5 /* auto filter: first 1/N (>= 1M lines) of a large batch builds the bound (default 256)       */
-#define RSA_OPT_SINGLE_LIST 6  /* stage 0 scans only each wave's majority list, others deferred (default 0)  */
-#define RSA_OPT_SCAN_PREFIX 4  /* linear scan: list entries scanned before a lane is deferred (default 256) */
+#define RSA_OPT_FILTER_STEPS 7 /* auto filter: bound refinements, each after 4x the previous lines (default 1)  */
+#define RSA_OPT_FORCE_DEFER 8  /* TESTING: every index candidate goes to the exact deferred-line path        */
 #define RSA_OPT_PROFILE_SKIP 3 /* PROFILING ONLY, results invalid: bit0 skips counters, bit1 skips the table  */
 
 /* One distinct (rule, connection) aggregate, 40 B (connlist-reducer.py:162-176). */
@@ -125,12 +133,11 @@ int rsa_version(void);
 int rsa_load_rules(rsa_ctx *ctx, const rsa_rule_entry *h_entries, uint32_t n_entries,
                    const uint32_t *h_list_offsets, uint32_t n_lists, uint32_t n_rules);
 
-/* Upload a tuple-space-search index over the lists of rsa_load_rules (same
- * list ids).  shape_off / resid_off have n_lists+1 entries.  Enables
- * RSA_OPT_USE_INDEX. */
-int rsa_load_index(rsa_ctx *ctx, const rsa_shape *h_shapes, uint32_t n_shapes, const uint32_t *h_shape_off,
-                   const rsa_index_slot *h_slots, uint64_t n_slots, const rsa_rule_entry *h_resid, uint32_t n_resid,
-                   const uint32_t *h_resid_off);
+/* Upload a perfect-hash tuple-space index over the lists of rsa_load_rules
+ * (h_lists has n_lists entries, same list ids).  Enables RSA_OPT_USE_INDEX.
+ * Every offset and slot is validated against the loaded lists. */
+int rsa_load_index(rsa_ctx *ctx, const rsa_pht_list *h_lists, const rsa_pht_shape *h_shapes, uint32_t n_shapes,
+                   const uint32_t *h_image, uint32_t image_words, const rsa_rule_entry *h_resid, uint32_t n_resid);
 
 /* Bind caller-owned device counters, each n_rules long (n_rules from
  * rsa_load_rules, or rsa_set_rule_count when no rules are loaded):

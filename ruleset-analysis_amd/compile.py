@@ -165,12 +165,12 @@ class CompiledRules(object):
     def n_lists(self):
         return len(self._lists)
 
-    def index(self):
-        """Tuple-space-search index of the current lists (cached until a list is added)."""
-        if getattr(self, '_index', None) is None or self._index[0] is not self._packed:
-            ent, off = self.packed()
-            self._index = (self._packed, build_index(ent, off))
-        return self._index[1]
+    def index(self, prefix=64):
+        """Perfect-hash tuple-space index of the current lists (cached until a list is added)."""
+        ent, off = self.packed()
+        if getattr(self, '_index', None) is None or self._index[0] is not self._packed or self._index[1] != prefix:
+            self._index = (self._packed, prefix, build_index(ent, off, prefix=prefix))
+        return self._index[2]
 
     def ensure_lists(self, protos=('tcp', 'udp')):
         """Pre-build the lists the traffic is expected to need, skipping any the
@@ -183,26 +183,58 @@ class CompiledRules(object):
                     pass
 
 
-# ---- tuple-space-search index ------------------------------------------------------
-SHAPE_DTYPE = np.dtype([('src_mask', '<u4'), ('dst_mask', '<u4'), ('port_mask', '<u4'), ('min_gid', '<u4'),
-                        ('table_off', '<u4'), ('table_mask', '<u4'), ('salt', '<u4'), ('reserved', '<u4')])
-ISLOT_DTYPE = np.dtype([('src', '<u4'), ('dst', '<u4'), ('ports', '<u4'), ('gid', '<u4')])
-assert SHAPE_DTYPE.itemsize == 32 and ISLOT_DTYPE.itemsize == 16
+# ---- perfect-hash tuple-space index (LDS-resident on the GPU) ----------------------
+#
+# Per candidate list: entries [0, prefix) are scanned linearly (early exit —
+# short first matches never touch the index); entries >= prefix whose address
+# ranges are prefixes and whose ports are "any" or one value are grouped by
+# shape (src mask, dst mask, port mask).  Each shape owns a CHD perfect-hash
+# table (hash-and-displace): key (src & smask, dst & dmask, ports & pmask) ->
+# one 32-bit slot word (tag16 << 16 | list-local entry index16, tag = low half of
+# the key hash) holding the
+# smallest entry index with that key.  Everything else (odd ranges, keys whose
+# 32-bit hash collides inside a shape, lists of >= 65535 entries) is residual,
+# scanned linearly.  A query takes the minimum candidate index over all shapes;
+# the GPU verifies it against the full entry (a 16-bit tag can collide) and
+# defers the line to an exact scan when it fails.  First match = min gid, so
+# the answer is the linear scan's.
+PHT_SHAPE_DTYPE = np.dtype([('src_mask', '<u4'), ('dst_mask', '<u4'), ('port_mask', '<u4'), ('min_idx', '<u4'),
+                            ('slot_off', '<u4'), ('disp_off', '<u4'), ('n_slots', '<u4'), ('disp_mask', '<u4')])
+PHT_LIST_DTYPE = np.dtype([('shape_beg', '<u4'), ('shape_end', '<u4'), ('resid_beg', '<u4'), ('resid_end', '<u4'),
+                           ('prefix', '<u4'), ('reserved0', '<u4'), ('reserved1', '<u4'), ('reserved2', '<u4')])
+assert PHT_SHAPE_DTYPE.itemsize == 32 and PHT_LIST_DTYPE.itemsize == 32
 M32 = 0xFFFFFFFF
+PHT_EMPTY = 0xFFFFFFFF
+PHT_MAX_IDX = 0xFFFE
+SALT_S, SALT_D, SALT_P = 0x9E3779B9, 0x7F4A7C15, 0x2545F491
 
 
-def index_hash(s, d, p, salt):
-    """Must equal index_hash() in csrc/ruleset_hip.hip (uint32 arithmetic)."""
-    s, d, p, salt = (np.asarray(x, dtype=np.uint32) for x in (s, d, p, salt))
+def fmix32(x):
+    """murmur3 finaliser on uint32 arrays; must equal fmix32() in csrc/ruleset_hip.hip."""
+    x = np.asarray(x, dtype=np.uint32).copy()
     with np.errstate(over='ignore'):
-        h = (s * np.uint32(0x9E3779B1)) ^ (d * np.uint32(0x85EBCA77)) ^ (p * np.uint32(0xC2B2AE3D)) ^ \
-            (salt * np.uint32(0x27D4EB2F))
-        h ^= h >> np.uint32(15)
-        h *= np.uint32(0x2C1B3C6D)
-        h ^= h >> np.uint32(12)
-        h *= np.uint32(0x297A2D39)
-        h ^= h >> np.uint32(15)
-    return h
+        x ^= x >> np.uint32(16)
+        x *= np.uint32(0x85EBCA6B)
+        x ^= x >> np.uint32(13)
+        x *= np.uint32(0xC2B2AE35)
+        x ^= x >> np.uint32(16)
+    return x
+
+
+def pht_hash(ks, kd, kp):
+    """H of masked keys (csrc: pht_hash)."""
+    return fmix32(np.asarray(ks, np.uint32) ^ np.uint32(SALT_S)) ^ fmix32(np.asarray(kd, np.uint32) ^ np.uint32(SALT_D)) \
+        ^ fmix32(np.asarray(kp, np.uint32) ^ np.uint32(SALT_P))
+
+
+def pht_slot(H, d, n_slots):
+    """slot = hi32(x * n_slots), x = (H + ((d * ((H >> 16) | 1)) << 16)) mod 2^32.
+    The slot depends on the high half of H, the tag is the low half and the
+    displacement bucket is (H >> 16) & disp_mask (csrc: pht_probe)."""
+    H = np.asarray(H, np.uint64)
+    hi = H >> np.uint64(16)
+    x = (H + ((np.asarray(d, np.uint64) * (hi | np.uint64(1))) << np.uint64(16))) & np.uint64(M32)
+    return ((x * np.uint64(n_slots)) >> np.uint64(32)).astype(np.int64)
 
 
 def _prefix_mask(lo, span):
@@ -221,21 +253,78 @@ def _port_mask(lo, span):
     return None
 
 
-def build_index(ent, off, probe_cost=8):
-    """Tuple-space-search index over packed lists (rsa_load_index arrays).
+def _pow2_at_least(x):
+    p = 1
+    while p < x:
+        p <<= 1
+    return p
 
-    Returns (shapes, shape_off, slots, resid, resid_off).  Per list, the index is
-    used only when it is cheaper than scanning (n_shapes * probe_cost + residual
-    < entries); otherwise every entry of the list stays residual (a plain scan)."""
-    shapes, shape_off, slot_parts, resid_parts, resid_off = [], [0], [], [], [0]
-    n_slots = 0
-    salt = 1
-    for L in range(len(off) - 1):
+
+def _chd(H, load=0.9, trials=4096):
+    """Hash-and-displace placement of distinct 32-bit hashes H into
+    m = ceil(n / load) slots.  Returns (m, disp_mask, disp uint16[r], slot_of_key int64[n])."""
+    n = len(H)
+    hb = (H >> np.uint32(16)).astype(np.int64)
+    m = max(1, int(np.ceil(n / load)))
+    r = _pow2_at_least(max(1, (n + 3) // 4))
+    while True:
+        b = hb & (r - 1)
+        order = np.argsort(-np.bincount(b, minlength=r), kind='stable')
+        members = [[] for _ in range(r)]
+        for k, bb in enumerate(b.tolist()):
+            members[bb].append(k)
+        used = np.zeros(m, dtype=bool)
+        disp = np.zeros(r, dtype=np.uint16)
+        slot_of = np.full(n, -1, dtype=np.int64)
+        ds = np.arange(trials, dtype=np.uint64)[:, None]
+        ok_all = True
+        for bb in order.tolist():
+            K = members[bb]
+            if not K:
+                continue
+            sl = pht_slot(H[K][None, :], ds, m)                                # trials x |K|
+            good = ~used[sl].any(axis=1)
+            if len(K) > 1:
+                srt = np.sort(sl, axis=1)
+                good &= (srt[:, 1:] != srt[:, :-1]).all(axis=1)
+            w = np.nonzero(good)[0]
+            if len(w) == 0:
+                ok_all = False
+                break
+            d = int(w[0])
+            disp[bb] = d
+            slot_of[K] = sl[d]
+            used[sl[d]] = True
+        if ok_all:
+            return m, r - 1, disp, slot_of
+        m += m // 8 + 1
+
+
+def build_index(ent, off, prefix=64, min_entries=96):
+    """Perfect-hash tuple-space index over packed lists (rsa_load_index arrays).
+
+    Returns (lists PHT_LIST_DTYPE[n_lists], shapes PHT_SHAPE_DTYPE[], image
+    uint32[], resid RULE_DTYPE[]).  A list shorter than ``min_entries`` (or of
+    >= 65535 entries) gets no shapes: everything after its prefix is residual."""
+    n_lists = len(off) - 1
+    lists = np.zeros(n_lists, dtype=PHT_LIST_DTYPE)
+    shapes, image, resid_parts = [], [], []
+    n_img = 0
+    n_resid = 0
+    for L in range(n_lists):
         e = ent[off[L]:off[L + 1]]
+        ne = len(e)
+        pre = min(prefix, ne)
+        lists[L]['prefix'] = pre
+        lists[L]['shape_beg'] = len(shapes)
         groups = {}
         resid_idx = []
-        for k in range(len(e)):
+        indexable = ne >= min_entries and ne <= PHT_MAX_IDX
+        for k in range(pre, ne):
             x = e[k]
+            if not indexable:
+                resid_idx.append(k)
+                continue
             sm = _prefix_mask(x['src_lo'], x['src_span'])
             dm = _prefix_mask(x['dst_lo'], x['dst_span'])
             pl, ps = int(x['port_lo']), int(x['port_span'])
@@ -247,36 +336,81 @@ def build_index(ent, off, probe_cost=8):
             pm = spm | (dpm << 16)
             key = (int(x['src_lo']), int(x['dst_lo']), pl & pm)
             g = groups.setdefault((sm, dm, pm), {})
-            if key not in g:                 # entries are gid-ascending: first = min gid
-                g[key] = int(x['gid'])
-        use_index = len(groups) * probe_cost + len(resid_idx) < len(e)
-        if not use_index:
-            resid_parts.append(e)
-            resid_off.append(resid_off[-1] + len(e))
-            shape_off.append(shape_off[-1])
-            continue
-        resid_parts.append(e[resid_idx])
-        resid_off.append(resid_off[-1] + len(resid_idx))
-        order = sorted(groups.items(), key=lambda kv: min(kv[1].values()))
-        for (sm, dm, pm), keys in order:
-            size = 2
-            while size < 2 * len(keys):
-                size <<= 1
-            tab = np.zeros(size, dtype=ISLOT_DTYPE)
-            tab['gid'] = M32
+            if key not in g:                 # entries are gid-ascending: first = min index
+                g[key] = k
+        for (sm, dm, pm) in sorted(groups):
+            keys = groups[(sm, dm, pm)]
             ks = np.array(list(keys.keys()), dtype=np.uint64).astype(np.uint32).reshape(-1, 3)
-            gs = np.array(list(keys.values()), dtype=np.uint32)
-            hs = index_hash(ks[:, 0], ks[:, 1], ks[:, 2], salt) & np.uint32(size - 1)
-            for (a, b, c), g, h in zip(ks.tolist(), gs.tolist(), hs.tolist()):
-                while tab['gid'][h] != M32:
-                    h = (h + 1) & (size - 1)
-                tab[h] = (a, b, c, g)
-            shapes.append((sm, dm, pm, min(keys.values()), n_slots, size - 1, salt, 0))
-            slot_parts.append(tab)
-            n_slots += size
-            salt += 1
-        shape_off.append(len(shapes))
-    shp = np.array(shapes, dtype=SHAPE_DTYPE) if shapes else np.zeros(0, SHAPE_DTYPE)
-    slots = np.concatenate(slot_parts) if slot_parts else np.zeros(0, ISLOT_DTYPE)
+            idx = np.array(list(keys.values()), dtype=np.int64)
+            H = pht_hash(ks[:, 0], ks[:, 1], ks[:, 2])
+            # a full 32-bit hash collision between two keys of one shape: keep the
+            # smaller index in the table, the other goes residual (still exact)
+            o = np.lexsort((idx, H))
+            H, idx = H[o], idx[o]
+            dup = np.zeros(len(H), dtype=bool)
+            dup[1:] = H[1:] == H[:-1]
+            resid_idx.extend(idx[dup].tolist())
+            H, idx = H[~dup], idx[~dup]
+            nslots, dmask, disp, slot_of = _chd(H)
+            nwords_disp = (dmask + 2) // 2
+            disp_off = 2 * n_img                               # in uint16 units
+            dwords = np.zeros(nwords_disp * 2, dtype=np.uint16)
+            dwords[:dmask + 1] = disp
+            image.append(dwords.view(np.uint32))
+            n_img += nwords_disp
+            slots = np.full(nslots, PHT_EMPTY, dtype=np.uint32)
+            slots[slot_of] = ((H & np.uint32(0xFFFF)).astype(np.uint32) << np.uint32(16)) | idx.astype(np.uint32)
+            shapes.append((sm, dm, pm, int(idx.min()), n_img, disp_off, nslots, dmask))
+            image.append(slots)
+            n_img += nslots
+        lists[L]['shape_end'] = len(shapes)
+        resid_idx = sorted(resid_idx)
+        lists[L]['resid_beg'] = n_resid
+        resid_parts.append(e[resid_idx])
+        n_resid += len(resid_idx)
+        lists[L]['resid_end'] = n_resid
+    shp = np.array(shapes, dtype=PHT_SHAPE_DTYPE) if shapes else np.zeros(0, PHT_SHAPE_DTYPE)
+    img = np.concatenate(image) if image else np.zeros(0, np.uint32)
     resid = np.concatenate(resid_parts) if resid_parts else np.zeros(0, RULE_DTYPE)
-    return (shp, np.array(shape_off, np.uint32), slots, resid, np.array(resid_off, np.uint32))
+    return lists, shp, img, resid
+
+
+def pht_lookup(index, ent, off, L, src, dst, ports):
+    """Host model of the GPU classifier for one tuple (tests): the first-match
+    list-local index or -1.  Follows the device order exactly: prefix scan,
+    min candidate over the shapes, verification, residual scan."""
+    lists, shp, img, resid = index
+    h = lists[L]
+    e = ent[off[L]:off[L + 1]]
+
+    def match(x):
+        pl, ps = int(x['port_lo']), int(x['port_span'])
+        return ((src - int(x['src_lo'])) & M32) <= int(x['src_span']) and \
+            ((dst - int(x['dst_lo'])) & M32) <= int(x['dst_span']) and \
+            ((ports & 0xFFFF) - (pl & 0xFFFF)) & 0xFFFF <= (ps & 0xFFFF) and \
+            ((ports >> 16) - (pl >> 16)) & 0xFFFF <= (ps >> 16)
+    for k in range(int(h['prefix'])):
+        if match(e[k]):
+            return k
+    cand = 0xFFFF
+    d16 = img.view(np.uint16)
+    for s in shp[int(h['shape_beg']):int(h['shape_end'])]:
+        H = int(pht_hash(src & int(s['src_mask']), dst & int(s['dst_mask']), ports & int(s['port_mask'])))
+        tag = H & 0xFFFF
+        d = int(d16[int(s['disp_off']) + ((H >> 16) & int(s['disp_mask']))])
+        slot = int(pht_slot(H, d, int(s['n_slots'])))
+        w = int(img[int(s['slot_off']) + slot])
+        if (w >> 16) == tag:
+            cand = min(cand, w & 0xFFFF)
+    best = None
+    if cand != 0xFFFF:
+        if not match(e[cand]):
+            return 'defer'
+        best = cand
+    gid_best = int(e[best]['gid']) if best is not None else None
+    for x in resid[int(h['resid_beg']):int(h['resid_end'])]:
+        if gid_best is not None and int(x['gid']) >= gid_best:
+            break
+        if match(x):
+            return int(np.searchsorted(e['gid'], x['gid']))
+    return -1 if best is None else best

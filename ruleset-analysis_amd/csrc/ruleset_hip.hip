@@ -10,17 +10,22 @@
 //                               (config.py:15), in sorted-line order.
 //
 // What this library does instead (integer work; HBM/atomic/VALU bound; no MFMA):
-//   classify  one lane per tuple.  Either a linear scan of the (host, acl,
-//             protocol) candidate list — a wave "waterfalls" over the distinct
-//             lists present in it so the entries are wave-uniform scalar loads —
-//             or a tuple-space-search index: one exact-match hash probe per rule
-//             shape (src prefix, dst prefix, port kinds), shapes visited in
-//             ascending min-gid order and abandoned once every lane holds a
-//             smaller match, plus a scan of the few residual rules.  Both return
-//             the minimum matching gid = the reference's first match.
-//   pass 1    per-rule line/hit counters (wave-aggregated device atomics) and an
-//             open-addressing (rule, connection) table in HBM keyed by device
-//             atomics; new entries are appended to a compact used-slot list.
+//   classify  one lane per tuple, waves "waterfall" over the distinct candidate
+//             lists present (list id broadcast by readlane, so rule data is
+//             wave-uniform: scalar loads).  Per list: a linear scan of the first
+//             `prefix` entries with wave-level early exit (short first matches
+//             never go further), then a perfect-hash tuple-space index staged in
+//             LDS: per rule shape (src mask, dst mask, port mask) one CHD
+//             (hash-and-displace) table maps the masked key to the smallest list
+//             index with that key; the lane keeps the minimum candidate, verifies
+//             it against the full entry (the 16-bit tag may collide) and scans the
+//             few residual entries.  A failed verification defers the line to an
+//             exact linear scan.  The answer is the minimum matching gid = the
+//             reference's first match.
+//   pass 1    per-line gid|hit words (then an LDS-privatised histogram gives the
+//             per-rule line/hit counters) and an open-addressing (rule,
+//             connection) table in HBM keyed by device atomics; new entries are
+//             appended to a compact used-slot list.
 //   filter    after the first slice of a large batch, each rule that already has
 //             >= cap connections gets an exact upper bound F of its threshold;
 //             later lines with order > F cannot change any output and skip the
@@ -37,6 +42,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/ruleset_hip.h"
 
@@ -59,8 +65,8 @@ struct alignas(64) Slot {
 static_assert(sizeof(Slot) == 64, "slot layout");
 static_assert(sizeof(rsa_tuple) == 16, "tuple layout");
 static_assert(sizeof(rsa_rule_entry) == 32, "rule layout");
-static_assert(sizeof(rsa_shape) == 32, "shape layout");
-static_assert(sizeof(rsa_index_slot) == 16, "index slot layout");
+static_assert(sizeof(rsa_pht_shape) == 32, "shape layout");
+static_assert(sizeof(rsa_pht_list) == 32, "list header layout");
 static_assert(sizeof(rsa_conn_record) == 40, "record layout");
 
 // Rule data is read through the constant address space so that wave-uniform
@@ -70,18 +76,19 @@ typedef __attribute__((address_space(4))) const v4u const_v4u;
 typedef __attribute__((address_space(4))) const uint32_t const_u32;
 
 struct Rules {
-  const const_v4u* e;     // linear entries, 2 x v4u each
-  const const_u32* off;   // n_lists + 1
+  const const_v4u* e;           // linear entries, 2 x v4u each (gid-ascending per list)
+  const v4u* eg;                // the same entries for per-lane (divergent) loads
+  const const_u32* off;         // n_lists + 1
   uint32_t n_lists;
   uint32_t n_rules;
-  // tuple-space-search index (optional)
-  const const_v4u* shapes;      // 2 x v4u each: {smask, dmask, pmask, min_gid}, {toff, tmask, salt, pad}
-  const const_u32* shape_off;   // n_lists + 1
-  const uint4* __restrict__ islots;
-  const const_v4u* resid;       // residual linear entries
-  const const_u32* resid_off;   // n_lists + 1
+  // perfect-hash tuple-space index (optional)
+  const const_v4u* hdr;         // per list 2 x v4u: {shape_beg, shape_end, resid_beg, resid_end}, {prefix, ...}
+  const const_v4u* shapes;      // per shape 2 x v4u: {smask, dmask, pmask, min_idx}, {slot_off, disp_off, n_slots, disp_mask}
+  const const_v4u* resid;       // residual entries (gid-ascending per list)
+  const uint32_t* img;          // slot + displacement image (global copy)
+  uint32_t img_words;
   int indexed;
-  int single_list;              // stage 0 scans only the wave's majority list
+  int force_defer;              // testing: every index candidate takes the exact deferred path
 };
 
 struct Agg {
@@ -112,17 +119,6 @@ __device__ __forceinline__ unsigned long long slot_hash(unsigned long long kA, u
   return mix64(kA ^ (kB * 0x9e3779b97f4a7c15ull));
 }
 
-// Hash of a tuple-space-search key; must equal compile.py's index_hash.
-__host__ __device__ __forceinline__ uint32_t index_hash(uint32_t s, uint32_t d, uint32_t p, uint32_t salt) {
-  uint32_t h = s * 0x9E3779B1u ^ (d * 0x85EBCA77u) ^ (p * 0xC2B2AE3Du) ^ (salt * 0x27D4EB2Fu);
-  h ^= h >> 15;
-  h *= 0x2C1B3C6Du;
-  h ^= h >> 12;
-  h *= 0x297A2D39u;
-  h ^= h >> 15;
-  return h;
-}
-
 // counter[key] += 1 for every lane with `ok`, one device atomic per distinct key
 // in the wave (lanes sharing a rule are counted first: hot rules would otherwise
 // serialise thousands of atomics on one address).  Wave-uniform control flow.
@@ -149,35 +145,6 @@ __device__ __forceinline__ unsigned long long wave_append(bool ok, unsigned long
   if ((int)lane == leader) base = atomicAdd(cursor, (unsigned long long)__popcll(mask));
   base = __shfl(base, leader);
   return base + __popcll(mask & ((1ull << lane) - 1ull));
-}
-
-// Workgroup-aggregated append of two streams (a, b) to global cursors: one
-// device atomic per stream per workgroup call (a single hot cursor would
-// otherwise take one atomic per wave).  Every thread of the workgroup must call
-// it (workgroup-uniform control flow).  sh: 4 LDS words.
-__device__ __forceinline__ void block_append2(bool a, bool b, unsigned long long* cur_a, unsigned long long* cur_b,
-                                              unsigned long long* sh, unsigned long long& pos_a,
-                                              unsigned long long& pos_b) {
-  const unsigned long long ma = __ballot(a), mb = __ballot(b);
-  const unsigned lane = __lane_id();
-  const unsigned long long below = (1ull << lane) - 1ull;
-  unsigned long long wa = 0, wb = 0;
-  if (lane == 0) {
-    if (ma) wa = atomicAdd(&sh[0], (unsigned long long)__popcll(ma));
-    if (mb) wb = atomicAdd(&sh[1], (unsigned long long)__popcll(mb));
-  }
-  wa = __shfl(wa, 0);
-  wb = __shfl(wb, 0);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    sh[2] = sh[0] ? atomicAdd(cur_a, sh[0]) : 0ull;
-    sh[3] = sh[1] ? atomicAdd(cur_b, sh[1]) : 0ull;
-    sh[0] = 0;
-    sh[1] = 0;
-  }
-  __syncthreads();
-  pos_a = sh[2] + wa + __popcll(ma & below);
-  pos_b = sh[3] + wb + __popcll(mb & below);
 }
 
 // Reducer key of a tuple (connlist-reducer.py:162: PROTO;FROMIP;TOIP;TOPORT).
@@ -233,71 +200,82 @@ __device__ __forceinline__ uint32_t scan_list(const const_v4u* E, uint32_t beg, 
   return best;
 }
 
-// Tuple-space search for the `mine` lanes of list L.
-__device__ __forceinline__ uint32_t search_index(const Rules& R, uint32_t L, bool mine, uint32_t src, uint32_t dst,
-                                                 uint32_t ports) {
-  uint32_t best = kNoGid;
-  const uint32_t sb = R.shape_off[L], se = R.shape_off[L + 1];
-  for (uint32_t s = sb; s < se; ++s) {
-    const v4u a = R.shapes[2 * s];       // smask, dmask, pmask, min_gid
-    const v4u b = R.shapes[2 * s + 1];   // toff, tmask, salt
-    // shapes are in ascending min_gid order: once no lane can improve, stop
-    if (__ballot(mine && best > a.w) == 0) break;
-    if (mine && best > a.w) {
-      const uint32_t ks = src & a.x, kd = dst & a.y, kp = ports & a.z;
-      uint32_t h = index_hash(ks, kd, kp, b.z) & b.y;
-      for (uint32_t probe = 0; probe <= b.y; ++probe) {
-        const uint4 q = R.islots[b.x + h];
-        if (q.w == kNoGid) break;
-        if (q.x == ks && q.y == kd && q.z == kp) {
-          best = min(best, q.w);
-          break;
-        }
-        h = (h + 1) & b.y;
-      }
-    }
-  }
-  const uint32_t rb = R.resid_off[L], re = R.resid_off[L + 1];
-  if (rb < re) best = scan_list(R.resid, rb, re, mine, best, src, dst, ports);
-  return best;
+constexpr uint32_t kDefer = 0xFFFFFFFEu;   // the index candidate failed verification: exact scan later
+constexpr uint32_t kNoCand = 0xFFFFu;
+
+// murmur3 finaliser; must equal compile.py fmix32.
+__device__ __forceinline__ uint32_t fmix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x85EBCA6Bu;
+  x ^= x >> 13;
+  x *= 0xC2B2AE35u;
+  x ^= x >> 16;
+  return x;
+}
+constexpr uint32_t kSaltS = 0x9E3779B9u, kSaltD = 0x7F4A7C15u, kSaltP = 0x2545F491u;
+
+// One CHD probe (compile.py pht_slot): H -> candidate list index or kNoCand.
+// img: the slot/displacement image (LDS or global).
+template <typename P32>
+__device__ __forceinline__ uint32_t pht_probe(P32 img, uint32_t H, v4u b) {
+  const uint32_t hi = H >> 16;
+  const uint32_t d = reinterpret_cast<const uint16_t*>(img)[b.y + (hi & b.w)];
+  const uint32_t x = H + (__umul24(d, hi | 1u) << 16);
+  const uint32_t slot = __umulhi(x, b.z);
+  const uint32_t w = img[b.x + slot];
+  return ((w >> 16) == (H & 0xFFFFu)) ? (w & 0xFFFFu) : kNoCand;
 }
 
-constexpr uint32_t kDefer = 0xFFFFFFFEu;       // deferred after the list prefix (tail resumes at the prefix)
-constexpr uint32_t kDeferList = 0xFFFFFFFDu;   // deferred before any scan: not the wave's list
-
-// Stage-0 classification with the linear lists: the wave scans ONE list, its
-// majority list (approximated from the leader's list), over the first `limit`
-// entries.  Lanes of other lists return kDeferList (stage 1 scans their prefix
-// in waves that are mostly single-list again) and lanes with no match in the
-// prefix return kDefer (stage 2 scans the rest of their list).
-__device__ __forceinline__ uint32_t classify_main(uint4 t, bool active, const Rules& R, unsigned int* flags,
-                                                  uint32_t limit) {
-  const uint32_t list = t.w & 0xFFFFu;
-  if (active && list >= R.n_lists) {
-    atomicOr(&flags[1], 1u);
-    active = false;
-  }
-  const unsigned long long act = __ballot(active);
-  if (act == 0) return kNoGid;
-  uint32_t L = __builtin_amdgcn_readlane(list, __builtin_ctzll(act));
-  const unsigned long long m1 = __ballot(active && list == L);
-  if (2 * __popcll(m1) < __popcll(act)) L = __builtin_amdgcn_readlane(list, __builtin_ctzll(act & ~m1));
-  const bool mine = active && list == L;
+// First match for the `mine` lanes of list L (wave-uniform).  Without the
+// index: a linear scan of the whole list.  With it: prefix scan, then (only if
+// some lane is still open) the shapes' perfect-hash probes, verification of the
+// minimum candidate and the residual scan.  Returns gid, kNoGid or kDefer.
+template <typename P32>
+__device__ __forceinline__ uint32_t classify_list(const Rules& R, P32 img, uint32_t L, bool mine, uint32_t src,
+                                                  uint32_t dst, uint32_t ports) {
   const uint32_t beg = R.off[L], end = R.off[L + 1];
-  const uint32_t hi = (end - beg > limit) ? beg + limit : end;
-  uint32_t b = scan_list(R.e, beg, hi, mine, kNoGid, t.x, t.y, t.z);
-  if (b == kNoGid && hi < end) b = kDefer;
-  if (!active) return kNoGid;
-  return mine ? b : kDeferList;
+  if (!R.indexed) return scan_list(R.e, beg, end, mine, kNoGid, src, dst, ports);
+  const v4u h0 = R.hdr[2 * L], h1 = R.hdr[2 * L + 1];
+  uint32_t best = scan_list(R.e, beg, beg + h1.x, mine, kNoGid, src, dst, ports);
+  const bool open = mine && best == kNoGid;
+  if (__ballot(open) == 0) return best;
+  uint32_t cand = kNoCand;
+  uint32_t hs = 0, hsd = 0, hp = 0;
+  uint32_t psm = 0, pdm = 0, ppm = 0;
+  for (uint32_t s = h0.x; s < h0.y; ++s) {
+    const v4u a = R.shapes[2 * s], b = R.shapes[2 * s + 1];
+    // shapes are sorted by (src mask, dst mask, port mask): each hash component
+    // is recomputed only when its mask changes (wave-uniform branches)
+    const bool first = s == h0.x;
+    const bool s_chg = first || a.x != psm;
+    if (s_chg) {
+      hs = fmix32((src & a.x) ^ kSaltS);
+      psm = a.x;
+    }
+    if (s_chg || a.y != pdm) {
+      hsd = hs ^ fmix32((dst & a.y) ^ kSaltD);
+      pdm = a.y;
+    }
+    if (first || a.z != ppm) {
+      hp = fmix32((ports & a.z) ^ kSaltP);
+      ppm = a.z;
+    }
+    cand = min(cand, pht_probe(img, hsd ^ hp, b));
+  }
+  uint32_t res = kNoGid;
+  if (open && cand != kNoCand) {
+    const v4u ea = R.eg[2 * (size_t)(beg + cand)], eb = R.eg[2 * (size_t)(beg + cand) + 1];
+    res = (entry_match(ea, eb, src, dst, ports) && !R.force_defer) ? eb.z : kDefer;
+  }
+  if (h0.z < h0.w) res = scan_list(R.resid, h0.z, h0.w, open && res != kDefer, res, src, dst, ports);
+  return open ? res : best;
 }
 
 // First-match classification of one wave of tuples: waterfall over the distinct
-// candidate lists present in the wave (list id broadcast by readlane).  With the
-// linear lists, only entries [from, limit) of each list are scanned; a lane with
-// no match there whose list continues past `limit` returns kDefer.  limit = ~0:
-// whole list.  With the index, the whole list is searched.
-__device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Rules& R, unsigned int* flags,
-                                                  uint32_t from = 0, uint32_t limit = 0xFFFFFFFFu) {
+// candidate lists present in the wave (list id broadcast by readlane).
+// kExact: ignore the index (linear scan of whole lists) — the deferred-line path.
+template <bool kExact, typename P32>
+__device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Rules& R, P32 img, unsigned int* flags) {
   const uint32_t list = t.w & 0xFFFFu;
   if (active && list >= R.n_lists) {
     atomicOr(&flags[1], 1u);
@@ -305,21 +283,16 @@ __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Ru
   }
   uint32_t best = kNoGid;
   unsigned long long pending = __ballot(active);
-  const uint32_t src = t.x, dst = t.y;
   while (pending) {
     const int leader = __builtin_ctzll(pending);
     const uint32_t L = __builtin_amdgcn_readlane(list, leader);
     const bool mine = active && list == L;
     pending &= ~__ballot(mine);
     uint32_t b;
-    if (R.indexed) {
-      b = search_index(R, L, mine, src, dst, t.z);
+    if (kExact) {
+      b = scan_list(R.e, R.off[L], R.off[L + 1], mine, kNoGid, t.x, t.y, t.z);
     } else {
-      const uint32_t beg = R.off[L], end = R.off[L + 1];
-      const uint32_t lo = (end - beg > from) ? beg + from : end;
-      const uint32_t hi = (end - beg > limit) ? beg + limit : end;
-      b = scan_list(R.e, lo, hi, mine, kNoGid, src, dst, t.z);
-      if (b == kNoGid && hi < end) b = kDefer;
+      b = classify_list(R, img, L, mine, t.x, t.y, t.z);
     }
     if (mine) best = b;
   }
@@ -389,6 +362,119 @@ __device__ __forceinline__ Slot* table_find(const Agg& A, unsigned long long kA,
 // the gid given per tuple (reducer drop-in), classify only (mapper drop-in).
 enum { kClassifyAgg = 0, kGivenAgg = 1, kClassifyOnly = 2 };
 
+constexpr uint32_t kTagHit = 0x80000000u;   // gtag word: gid | hit bit; 0xFFFFFFFF = no match
+
+// Everything pass 1 does with a classified line: the mapper output (gout), the
+// gid|hit word the per-rule histogram counts (gtag), and the reducer's
+// distinct-connection table (connlist-reducer.py:146-176) for hit lines the
+// BUILT regex matched.  Wave-uniform control flow.
+template <int kMode>
+__device__ __forceinline__ void finish_line(bool in, unsigned long long i, uint4 t, uint32_t gid,
+                                            const uint32_t* __restrict__ TS, const unsigned long long* __restrict__ ORD,
+                                            int32_t* __restrict__ gout, uint32_t* __restrict__ gtag, uint32_t n_rules,
+                                            const Agg& A) {
+  const uint32_t flags = (t.w >> 16) & 0xFFu;
+  if (kMode != kGivenAgg && gout && in) gout[i] = (int32_t)gid;
+  if (kMode == kClassifyOnly) return;
+  if (in && gid != kNoGid && gid >= n_rules) atomicOr(&A.flags[1], 2u);
+  const bool matched = in && gid < n_rules;
+  const bool hit = matched && (flags & RSA_F_HIT);
+  if (in && !(A.skip & 1u)) gtag[i] = matched ? (gid | (hit ? kTagHit : 0u)) : 0xFFFFFFFFu;
+  bool fresh = false;
+  unsigned long long slot = kEmpty;
+  if (hit && (flags & RSA_F_BUILT) && A.cap > 0 && !(A.skip & 2u)) {
+    const unsigned long long o = ORD[i];
+    // exact skip: the rule is already capped with threshold <= filter < o
+    if (o <= A.filter[gid]) {
+      unsigned long long kA, kB;
+      conn_key(t, gid, kA, kB);
+      const uint32_t ts = TS[i];
+      slot = table_combine(A, kA, kB, 1u, ts, ts, o, &fresh);
+    }
+  }
+  wave_count_by_key(fresh, gid, A.distinct);
+  const unsigned long long pos = wave_append(fresh, A.used_n);
+  if (fresh) A.used[pos] = (uint32_t)slot;
+}
+
+// Workgroup-aggregated append to one global cursor (every thread calls it).
+__device__ __forceinline__ unsigned long long block_append(bool a, unsigned long long* cur, unsigned long long* sh) {
+  const unsigned long long ma = __ballot(a);
+  const unsigned lane = __lane_id();
+  unsigned long long wa = 0;
+  if (lane == 0 && ma) wa = atomicAdd(&sh[0], (unsigned long long)__popcll(ma));
+  wa = __shfl(wa, 0);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    sh[1] = sh[0] ? atomicAdd(cur, sh[0]) : 0ull;
+    sh[0] = 0;
+  }
+  __syncthreads();
+  return sh[1] + wa + __popcll(ma & ((1ull << lane) - 1ull));
+}
+
+constexpr int kImgSmallMax = 16000;   // LDS image words that still allow two 1024-thread workgroups per CU
+
+// Pass 1, main stage: classify with the index (staged in LDS when kImg > 0),
+// lines whose index candidate fails verification go to `tail` for k_tail.
+template <int kMode, int kImg>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kImgSmallMax ? 4 : 8, 8))) void k_classify(const uint4* __restrict__ T, const uint32_t* __restrict__ TS,
+                                                   const unsigned long long* __restrict__ ORD, unsigned long long n,
+                                                   const int32_t* __restrict__ gin, int32_t* __restrict__ gout,
+                                                   uint32_t* __restrict__ gtag, Rules R, Agg A, uint32_t* tail,
+                                                   unsigned long long* tail_n) {
+  __shared__ uint32_t lds_img[kImg > 0 ? kImg : 1];
+  __shared__ unsigned long long lds_app[2];
+  if (threadIdx.x < 2) lds_app[threadIdx.x] = 0;
+  if (kImg > 0 && kMode != kGivenAgg && R.indexed) {
+    for (uint32_t w = threadIdx.x; w < R.img_words; w += blockDim.x) lds_img[w] = R.img[w];
+  }
+  __syncthreads();
+  const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+  for (unsigned long long base = (unsigned long long)blockIdx.x * blockDim.x; base < n; base += stride) {
+    const unsigned long long i = base + threadIdx.x;
+    const bool in = i < n;
+    const uint4 t = in ? T[i] : make_uint4(0u, 0u, 0u, 0u);
+    const bool valid = in && (((t.w >> 16) & 0xFFu) & RSA_F_VALID);
+    uint32_t gid;
+    if (kMode == kGivenAgg) {
+      gid = in ? (uint32_t)gin[i] : kNoGid;
+    } else {
+      if (kImg > 0) {
+        gid = classify_wave<false>(t, valid, R, (const uint32_t*)lds_img, A.flags);
+      } else {
+        gid = classify_wave<false>(t, valid, R, R.img, A.flags);
+      }
+      const bool defer = gid == kDefer;
+      const unsigned long long pos = block_append(defer, tail_n, lds_app);
+      if (defer) {
+        tail[pos] = (uint32_t)i;
+        continue;   // finished by k_tail
+      }
+    }
+    finish_line<kMode>(in, i, t, gid, TS, ORD, gout, gtag, R.n_rules, A);
+  }
+}
+
+// Pass 1, deferred lines: exact linear scan of their whole list.
+template <int kMode>
+__global__ __launch_bounds__(kBlock) void k_tail(const uint4* __restrict__ T, const uint32_t* __restrict__ TS,
+                                                 const unsigned long long* __restrict__ ORD, int32_t* __restrict__ gout,
+                                                 uint32_t* __restrict__ gtag, Rules R, Agg A,
+                                                 const uint32_t* __restrict__ tail, const unsigned long long* tail_n) {
+  const unsigned long long n = *tail_n;
+  const unsigned long long stride = (unsigned long long)gridDim.x * kBlock;
+  for (unsigned long long base = (unsigned long long)blockIdx.x * kBlock; base < n; base += stride) {
+    const unsigned long long j = base + threadIdx.x;
+    const bool in = j < n;
+    const unsigned long long i = in ? tail[j] : 0u;
+    const uint4 t = in ? T[i] : make_uint4(0u, 0u, 0u, 0u);
+    const bool valid = in && (((t.w >> 16) & 0xFFu) & RSA_F_VALID);
+    const uint32_t gid = classify_wave<true>(t, valid, R, R.img, A.flags);
+    finish_line<kMode>(in, i, t, gid, TS, ORD, gout, gtag, R.n_rules, A);
+  }
+}
+
 // matches[key] += 1 for lanes with `m`, hits[key] += 1 for lanes with `h` (h
 // implies m): one loop over the wave's distinct keys, one device atomic per
 // key and counter.  Wave-uniform control flow.
@@ -409,119 +495,63 @@ __device__ __forceinline__ void wave_count2(bool m, bool h, uint32_t key, unsign
   }
 }
 
-// Pass 1.  kLds > 0: the per-rule line/hit counters of up to kLds rules are
-// privatised in LDS for the whole (persistent) workgroup and flushed once at the
-// end; otherwise they are wave-aggregated device atomics.
-// Linear-list classification runs in three stages so that waves stay dense and
-// single-list: stage 0 = every line, majority list of the wave, first `prefix`
-// entries; stage 1 = lines of other lists (tailA), their first `prefix`
-// entries; stage 2 = lines unmatched in their prefix (tailB), the rest of the
-// list.  A line is aggregated by the stage that classifies it.
-template <int kMode, int kThreads, int kLds, int kStage>
-__global__ __launch_bounds__(kThreads) void k_pass1(const uint4* __restrict__ T, const uint32_t* __restrict__ TS,
-                                                    const unsigned long long* __restrict__ ORD, unsigned long long n,
-                                                    const int32_t* __restrict__ gin, int32_t* __restrict__ gout,
-                                                    Rules R, Agg A, uint32_t prefix, uint32_t* tailA,
-                                                    unsigned long long* tailA_n, uint32_t* tailB,
-                                                    unsigned long long* tailB_n) {
-  __shared__ uint32_t lds_cnt[kLds > 0 ? 2 * kLds : 1];
-  __shared__ unsigned long long lds_app[4];
-  const bool counters = kMode != kClassifyOnly && !(A.skip & 1u);
-  if (threadIdx.x < 4) lds_app[threadIdx.x] = 0;
-  if (kLds > 0 && counters) {
-    for (uint32_t r = threadIdx.x; r < 2u * kLds; r += kThreads) lds_cnt[r] = 0;
-  }
-  __syncthreads();
-  if (kStage == 1) n = *tailA_n;
-  if (kStage == 2) n = *tailB_n;
-  const unsigned long long stride = (unsigned long long)gridDim.x * kThreads;
-  for (unsigned long long base = (unsigned long long)blockIdx.x * kThreads; base < n; base += stride) {
-    const unsigned long long j = base + threadIdx.x;
-    const bool in = j < n;
-    unsigned long long i = j;
-    if (kStage == 1) i = in ? tailA[j] : 0u;
-    if (kStage == 2) i = in ? tailB[j] : 0u;
-    const uint4 t = in ? T[i] : make_uint4(0u, 0u, 0u, 0u);
-    const uint32_t flags = (t.w >> 16) & 0xFFu;
-    const bool valid = in && (flags & RSA_F_VALID);
-    uint32_t gid;
-    if (kMode == kGivenAgg) {
-      gid = in ? (uint32_t)gin[i] : kNoGid;
-    } else if (R.indexed) {
-      gid = classify_wave(t, valid, R, A.flags);
-    } else if (kStage == 0) {
-      gid = R.single_list ? classify_main(t, valid, R, A.flags, prefix)
-                          : classify_wave(t, valid, R, A.flags, 0, prefix);
-    } else if (kStage == 1) {
-      gid = classify_wave(t, valid, R, A.flags, 0, prefix);
-    } else {
-      gid = classify_wave(t, valid, R, A.flags, prefix);
-    }
-    if (kMode != kGivenAgg) {
-      const bool to_a = gid == kDeferList;
-      const bool to_b = gid == kDefer;
-      unsigned long long pa, pb;
-      block_append2(to_a, to_b, tailA_n, tailB_n, lds_app, pa, pb);
-      if (to_a) tailA[pa] = (uint32_t)i;
-      if (to_b) tailB[pb] = (uint32_t)i;
-      if (to_a || to_b) continue;   // finished by a later stage
-      if (gout && in) gout[i] = (int32_t)gid;
-    }
-    if (kMode == kClassifyOnly) continue;
-    if (gid != kNoGid && gid >= R.n_rules) atomicOr(&A.flags[1], 2u);
-    const bool matched = gid < R.n_rules;
-    const bool hit = matched && (flags & RSA_F_HIT);
-    if (counters) {
-      if (kLds > 0) {
-        if (matched) atomicAdd(&lds_cnt[gid], 1u);
-        if (hit) atomicAdd(&lds_cnt[kLds + gid], 1u);
-      } else {
-        wave_count2(matched, hit, gid, A.matches, A.hits);
-      }
-    }
-    bool fresh = false;
-    unsigned long long slot = kEmpty;
-    if (hit && (flags & RSA_F_BUILT) && A.cap > 0 && !(A.skip & 2u)) {
-      const unsigned long long o = ORD[i];
-      // exact skip: the rule is already capped with threshold <= filter < o
-      if (o <= A.filter[gid]) {
-        unsigned long long kA, kB;
-        conn_key(t, gid, kA, kB);
-        const uint32_t ts = TS[i];
-        slot = table_combine(A, kA, kB, 1u, ts, ts, o, &fresh);
-      }
-    }
-    wave_count_by_key(fresh, gid, A.distinct);
-    const unsigned long long pos = wave_append(fresh, A.used_n);
-    if (fresh) A.used[pos] = (uint32_t)slot;
-  }
-  if (kLds > 0 && counters) {
+// Per-rule line and hit counters from the gid|hit words of one pass-1 call:
+// privatised in LDS for up to kLds rules, flushed once per (persistent)
+// workgroup; wave-aggregated device atomics beyond that.
+template <int kLds>
+__global__ __launch_bounds__(1024) void k_count(const uint32_t* __restrict__ gtag, unsigned long long n,
+                                                uint32_t n_rules, unsigned long long* matches,
+                                                unsigned long long* hits) {
+  __shared__ uint32_t cnt[kLds > 0 ? 2 * kLds : 1];
+  if (kLds > 0) {
+    for (uint32_t r = threadIdx.x; r < 2u * kLds; r += blockDim.x) cnt[r] = 0;
     __syncthreads();
-    for (uint32_t r = threadIdx.x; r < R.n_rules; r += kThreads) {
-      const uint32_t m = lds_cnt[r], h = lds_cnt[kLds + r];
-      if (m) atomicAdd(&A.matches[r], (unsigned long long)m);
-      if (h) atomicAdd(&A.hits[r], (unsigned long long)h);
+  }
+  const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x * 4;
+  for (unsigned long long base = ((unsigned long long)blockIdx.x * blockDim.x + threadIdx.x) * 4; base < n;
+       base += stride) {
+    uint32_t w[4];
+    if (base + 4 <= n && (base & 3) == 0) {
+      const uint4 v = *reinterpret_cast<const uint4*>(gtag + base);
+      w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
+    } else {
+      for (int k = 0; k < 4; ++k) w[k] = base + k < n ? gtag[base + k] : 0xFFFFFFFFu;
+    }
+    for (int k = 0; k < 4; ++k) {
+      const bool m = w[k] != 0xFFFFFFFFu;
+      const uint32_t g = w[k] & ~kTagHit;
+      const bool h = m && (w[k] & kTagHit);
+      if (kLds > 0) {
+        if (m) atomicAdd(&cnt[g], 1u);
+        if (h) atomicAdd(&cnt[kLds + g], 1u);
+      } else {
+        wave_count2(m, h, g, matches, hits);
+      }
+    }
+  }
+  if (kLds > 0) {
+    __syncthreads();
+    for (uint32_t r = threadIdx.x; r < n_rules; r += blockDim.x) {
+      const uint32_t m = cnt[r], h = cnt[kLds + r];
+      if (m) atomicAdd(&matches[r], (unsigned long long)m);
+      if (h) atomicAdd(&hits[r], (unsigned long long)h);
     }
   }
 }
 
-template <bool kGiven>
+// Pass 2: lines with order <= P of capped rules recount count/first/last into
+// the pass-2 fields (gids from pass 1 or from a classify-only run).
 __global__ __launch_bounds__(kBlock) void k_pass2(const uint4* __restrict__ T, const uint32_t* __restrict__ TS,
                                                   const unsigned long long* __restrict__ ORD, unsigned long long n,
-                                                  const int32_t* __restrict__ gin, Rules R, Agg A) {
+                                                  const int32_t* __restrict__ gin, uint32_t n_rules, Agg A) {
   const unsigned long long stride = (unsigned long long)gridDim.x * kBlock;
   for (unsigned long long base = (unsigned long long)blockIdx.x * kBlock; base < n; base += stride) {
     const unsigned long long i = base + threadIdx.x;
-    const bool in = i < n;
-    const uint4 t = in ? T[i] : make_uint4(0u, 0u, 0u, 0u);
+    if (i >= n) continue;
+    const uint32_t gid = (uint32_t)gin[i];
+    if (gid >= n_rules) continue;
+    const uint4 t = T[i];
     const uint32_t flags = (t.w >> 16) & 0xFFu;
-    uint32_t gid;
-    if (kGiven) {
-      gid = in ? (uint32_t)gin[i] : kNoGid;
-    } else {
-      gid = classify_wave(t, in && (flags & RSA_F_VALID), R, A.flags);
-    }
-    if (gid >= R.n_rules) continue;
     if ((flags & (RSA_F_HIT | RSA_F_BUILT)) != (RSA_F_HIT | RSA_F_BUILT)) continue;
     const unsigned long long P = A.thresh[gid];
     if (P == RSA_NO_THRESHOLD) continue;
@@ -699,16 +729,19 @@ struct rsa_ctx {
   rsa_rule_entry* d_entries = nullptr;
   uint32_t n_entries = 0;
   uint32_t* d_off = nullptr;
+  std::vector<uint32_t> h_off;        // host copy of the list offsets (validation)
   uint32_t n_lists = 0;
   uint32_t n_rules = 0;
   bool rules_loaded = false;
-  // tuple-space-search index
-  rsa_shape* d_shapes = nullptr;
-  uint32_t* d_shape_off = nullptr;
-  rsa_index_slot* d_islots = nullptr;
+  // perfect-hash tuple-space index
+  rsa_pht_list* d_hdr = nullptr;
+  rsa_pht_shape* d_shapes = nullptr;
+  uint32_t* d_img = nullptr;
+  uint32_t img_words = 0;
   rsa_rule_entry* d_resid = nullptr;
-  uint32_t* d_resid_off = nullptr;
+  bool index_loaded = false;
   bool indexed = false;
+  bool force_defer = false;
   // caller-owned counters
   unsigned long long* d_matches = nullptr;
   unsigned long long* d_hits = nullptr;
@@ -729,12 +762,15 @@ struct rsa_ctx {
   bool auto_tighten = true;
   bool tightened = false;
   uint32_t profile_skip = 0;
-  uint32_t scan_prefix = 256;         // linear scan: entries per list scanned before deferring a lane
-  bool single_list = false;
-  uint32_t filter_slice = 256;        // auto filter: the first 1/filter_slice of a large batch builds the bound
+  uint32_t filter_slice = 256;
+  uint32_t filter_steps = 1;          // filter refinements (each after 4x the previous lines)        // auto filter: the first 1/filter_slice of a large batch builds the bound
   uint32_t* d_tail = nullptr;         // deferred line indices
   unsigned long long* d_tail_n = nullptr;
   unsigned long long tail_alloc = 0;
+  uint32_t* d_gtag = nullptr;         // per-line gid|hit words of the current pass-1 call
+  unsigned long long gtag_alloc = 0;
+  int32_t* d_gscratch = nullptr;      // classify-only gids for a recount without pass-1 gids
+  unsigned long long gscratch_alloc = 0;
   unsigned int* d_flags = nullptr;       // 4 words
   unsigned long long* d_cursor = nullptr;
   // cap-resolution scratch
@@ -749,7 +785,7 @@ struct rsa_ctx {
   void* d_temp = nullptr;
   size_t temp_alloc = 0;
   // pass-1 kernel timing (HIP events on the ctx stream)
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev[32] = {};
   int ev_used = 0;
 };
 
@@ -774,16 +810,17 @@ int fail(rsa_ctx* c, int code, const char* fmt, ...) {
 Rules rules_of(const rsa_ctx* c) {
   Rules r;
   r.e = (const const_v4u*)(c->d_entries);
+  r.eg = reinterpret_cast<const v4u*>(c->d_entries);
   r.off = (const const_u32*)(c->d_off);
   r.n_lists = c->n_lists;
   r.n_rules = c->n_rules;
+  r.hdr = (const const_v4u*)(c->d_hdr);
   r.shapes = (const const_v4u*)(c->d_shapes);
-  r.shape_off = (const const_u32*)(c->d_shape_off);
-  r.islots = reinterpret_cast<const uint4*>(c->d_islots);
   r.resid = (const const_v4u*)(c->d_resid);
-  r.resid_off = (const const_u32*)(c->d_resid_off);
+  r.img = c->d_img;
+  r.img_words = c->img_words;
   r.indexed = c->indexed ? 1 : 0;
-  r.single_list = c->single_list ? 1 : 0;
+  r.force_defer = c->force_defer ? 1 : 0;
   return r;
 }
 
@@ -803,10 +840,6 @@ Agg agg_of(const rsa_ctx* c) {
   a.skip = c->profile_skip;
   return a;
 }
-
-// LDS-privatised counter capacities (rules): 2 x 4 B per rule.
-constexpr int kLdsSmall = 10240;   // 80 KiB: two 1024-thread workgroups per CU (32 waves)
-constexpr int kLdsLarge = 20448;   // ~160 KiB (minus the append scratch): one workgroup per CU
 
 unsigned grid_for_threads(const rsa_ctx* c, unsigned long long n, unsigned threads, unsigned per_cu) {
   unsigned long long g = (n + threads - 1) / threads;
@@ -952,8 +985,7 @@ int cap_select(rsa_ctx* c, unsigned long long* out, uint32_t* h_n_capped) {
   return RSA_OK;
 }
 
-// Two deferred-line regions of `tail_alloc` entries each (stage-1 and stage-2
-// inputs) and their two counters.
+// Deferred-line region of `tail_alloc` entries and its counter.
 int ensure_tail(rsa_ctx* c, unsigned long long n) {
   if (!c->d_tail_n) HIPCHK(c, hipMalloc(&c->d_tail_n, 2 * sizeof(unsigned long long)));
   if (n <= c->tail_alloc) return RSA_OK;
@@ -961,93 +993,132 @@ int ensure_tail(rsa_ctx* c, unsigned long long n) {
   hipFree(c->d_tail);
   c->d_tail = nullptr;
   c->tail_alloc = 0;
-  HIPCHK(c, hipMalloc(&c->d_tail, 2 * n * sizeof(uint32_t)));
+  HIPCHK(c, hipMalloc(&c->d_tail, n * sizeof(uint32_t)));
   c->tail_alloc = n;
   return RSA_OK;
 }
 
+template <typename T>
+int ensure_buf(rsa_ctx* c, T** p, unsigned long long* have, unsigned long long n) {
+  if (n <= *have) return RSA_OK;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  hipFree(*p);
+  *p = nullptr;
+  *have = 0;
+  HIPCHK(c, hipMalloc(p, n * sizeof(T)));
+  *have = n;
+  return RSA_OK;
+}
+
+constexpr int kMaxEvents = 32;
+
 int ensure_events(rsa_ctx* c) {
-  for (int k = 0; k < 4; ++k)
+  for (int k = 0; k < kMaxEvents; ++k)
     if (!c->ev[k]) HIPCHK(c, hipEventCreate(&c->ev[k]));
+  return RSA_OK;
+}
+
+// LDS image capacities (32-bit words) of k_classify.
+constexpr int kImgSmall = 16000;   // 62.5 KiB: two 1024-thread workgroups per CU (32 waves)
+constexpr int kImgLarge = 38912;   // 152 KiB: one workgroup per CU
+
+// Main classification launch + exact tail for lines [0, m) of T (already offset).
+template <int kMode>
+int launch_classify(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsigned long long* o, uint64_t m,
+                    const int32_t* gi, int32_t* go, uint32_t* gt) {
+  const Rules r = rules_of(c);
+  const Agg ag = agg_of(c);
+  int rc = ensure_tail(c, m);
+  if (rc) return rc;
+  HIPCHK(c, hipMemsetAsync(c->d_tail_n, 0, sizeof(unsigned long long), c->stream));
+  const bool lds = kMode != kGivenAgg && c->indexed;
+  if (lds && c->img_words <= (uint32_t)kImgSmall) {
+    k_classify<kMode, kImgSmall><<<grid_for_threads(c, m, 1024, 2), 1024, 0, c->stream>>>(
+        t, ts, o, m, gi, go, gt, r, ag, c->d_tail, c->d_tail_n);
+  } else if (lds && c->img_words <= (uint32_t)kImgLarge) {
+    k_classify<kMode, kImgLarge><<<grid_for_threads(c, m, 1024, 1), 1024, 0, c->stream>>>(
+        t, ts, o, m, gi, go, gt, r, ag, c->d_tail, c->d_tail_n);
+  } else {
+    k_classify<kMode, 0><<<grid_for_threads(c, m, 1024, 2), 1024, 0, c->stream>>>(t, ts, o, m, gi, go, gt, r, ag,
+                                                                                c->d_tail, c->d_tail_n);
+  }
+  HIPCHK(c, hipGetLastError());
+  if (kMode != kGivenAgg) {
+    // deferred lines (their number is read on the device: no host sync)
+    k_tail<kMode><<<c->cu_count * 4, kBlock, 0, c->stream>>>(t, ts, o, go, gt, r, ag, c->d_tail, c->d_tail_n);
+    HIPCHK(c, hipGetLastError());
+  }
+  return RSA_OK;
+}
+
+// LDS-privatised counter capacities (rules): 2 x 4 B per rule.
+constexpr int kCntSmall = 10240;   // 80 KiB: two 1024-thread workgroups per CU
+constexpr int kCntLarge = 20480;   // 160 KiB: one workgroup per CU
+
+int launch_count(rsa_ctx* c, const uint32_t* gt, uint64_t m) {
+  if (c->profile_skip & 1u) return RSA_OK;
+  const uint64_t quads = (m + 3) / 4;
+  if (c->n_rules <= (uint32_t)kCntSmall) {
+    k_count<kCntSmall><<<grid_for_threads(c, quads, 1024, 2), 1024, 0, c->stream>>>(gt, m, c->n_rules, c->d_matches,
+                                                                                    c->d_hits);
+  } else if (c->n_rules <= (uint32_t)kCntLarge) {
+    k_count<kCntLarge><<<grid_for_threads(c, quads, 1024, 1), 1024, 0, c->stream>>>(gt, m, c->n_rules, c->d_matches,
+                                                                                    c->d_hits);
+  } else {
+    k_count<0><<<grid_for_threads(c, quads, 1024, 4), 1024, 0, c->stream>>>(gt, m, c->n_rules, c->d_matches,
+                                                                            c->d_hits);
+  }
+  HIPCHK(c, hipGetLastError());
   return RSA_OK;
 }
 
 // Pass 1 over one batch.  With auto-tightening, a large first batch is split:
 // the first 1/filter_slice builds the table, the filter is computed, and the
-// rest of the batch skips the table for lines that cannot change any output.
+// rest of the batch skips the table for lines that cannot change any output;
+// with filter_steps > 1 the filter is refined again after 4x, 16x, ... that
+// many lines.
 int run_pass1(rsa_ctx* c, int mode, const rsa_tuple* T, const uint32_t* TS, const uint64_t* ORD, const int32_t* G,
               int32_t* gout, uint64_t n) {
   int rc = ensure_events(c);
   if (rc) return rc;
   c->ev_used = 0;
+  if (n > 0x7FFFFFFFull) return fail(c, RSA_ERR_ARG, "batch larger than 2^31 tuples: split it");
+  rc = ensure_buf(c, &c->d_gtag, &c->gtag_alloc, n);
+  if (rc) return rc;
   auto launch = [&](uint64_t a, uint64_t m) -> int {
+    if (m == 0) return RSA_OK;
+    if (c->ev_used + 2 > kMaxEvents) return fail(c, RSA_ERR_STATE, "too many pass-1 launches in one call");
     const uint4* t = reinterpret_cast<const uint4*>(T) + a;
     const unsigned long long* o = reinterpret_cast<const unsigned long long*>(ORD) + a;
     HIPCHK(c, hipEventRecord(c->ev[c->ev_used], c->stream));
     int32_t* go = gout ? gout + a : nullptr;
     const int32_t* gi = G ? G + a : nullptr;
-    const Rules r = rules_of(c);
-    const Agg ag = agg_of(c);
-    const uint32_t K = c->indexed ? 0xFFFFFFFFu : c->scan_prefix;
-    int rc2 = ensure_tail(c, m);
+    int rc2 = mode == kClassifyAgg ? launch_classify<kClassifyAgg>(c, t, TS + a, o, m, nullptr, go, c->d_gtag + a)
+                                   : launch_classify<kGivenAgg>(c, t, TS + a, o, m, gi, nullptr, c->d_gtag + a);
     if (rc2) return rc2;
-    HIPCHK(c, hipMemsetAsync(c->d_tail_n, 0, 2 * sizeof(unsigned long long), c->stream));
-    uint32_t* ta = c->d_tail;
-    uint32_t* tb = c->d_tail + c->tail_alloc;
-    unsigned long long* na = c->d_tail_n;
-    unsigned long long* nb = c->d_tail_n + 1;
-    if (c->n_rules <= kLdsSmall) {
-      // two 1024-thread workgroups (80 KiB of counters each) per CU
-      const unsigned g = grid_for_threads(c, m, 1024, 2);
-      if (mode == kClassifyAgg)
-        k_pass1<kClassifyAgg, 1024, kLdsSmall, 0><<<g, 1024, 0, c->stream>>>(t, TS + a, o, m, nullptr, go, r, ag, K,
-                                                                             ta, na, tb, nb);
-      else
-        k_pass1<kGivenAgg, 1024, kLdsSmall, 0><<<g, 1024, 0, c->stream>>>(t, TS + a, o, m, gi, nullptr, r, ag, K,
-                                                                          ta, na, tb, nb);
-    } else if (c->n_rules <= kLdsLarge) {
-      const unsigned g = grid_for_threads(c, m, 1024, 1);
-      if (mode == kClassifyAgg)
-        k_pass1<kClassifyAgg, 1024, kLdsLarge, 0><<<g, 1024, 0, c->stream>>>(t, TS + a, o, m, nullptr, go, r, ag, K,
-                                                                             ta, na, tb, nb);
-      else
-        k_pass1<kGivenAgg, 1024, kLdsLarge, 0><<<g, 1024, 0, c->stream>>>(t, TS + a, o, m, gi, nullptr, r, ag, K,
-                                                                          ta, na, tb, nb);
-    } else {
-      const unsigned g = grid_for(c, m, 16);
-      if (mode == kClassifyAgg)
-        k_pass1<kClassifyAgg, kBlock, 0, 0><<<g, kBlock, 0, c->stream>>>(t, TS + a, o, m, nullptr, go, r, ag, K, ta,
-                                                                         na, tb, nb);
-      else
-        k_pass1<kGivenAgg, kBlock, 0, 0><<<g, kBlock, 0, c->stream>>>(t, TS + a, o, m, gi, nullptr, r, ag, K, ta, na,
-                                                                      tb, nb);
-    }
-    HIPCHK(c, hipGetLastError());
-    if (mode == kClassifyAgg && K != 0xFFFFFFFFu) {
-      // stages 1 and 2 (their sizes are read on the device: no host sync)
-      k_pass1<kClassifyAgg, kBlock, 0, 1><<<c->cu_count * 8, kBlock, 0, c->stream>>>(t, TS + a, o, m, nullptr, go, r,
-                                                                                     ag, K, ta, na, tb, nb);
-      k_pass1<kClassifyAgg, kBlock, 0, 2><<<c->cu_count * 4, kBlock, 0, c->stream>>>(t, TS + a, o, m, nullptr, go, r,
-                                                                                     ag, K, ta, na, tb, nb);
-    }
-    HIPCHK(c, hipGetLastError());
+    rc2 = launch_count(c, c->d_gtag + a, m);
+    if (rc2) return rc2;
     HIPCHK(c, hipEventRecord(c->ev[c->ev_used + 1], c->stream));
     c->ev_used += 2;
     return RSA_OK;
   };
-  if (n > 0x7FFFFFFFull) return fail(c, RSA_ERR_ARG, "batch larger than 2^31 tuples: split it");
   c->table_dirty = true;
   const uint64_t kMinSplit = 1ull << 22;
   if (c->auto_tighten && !c->tightened && c->cap > 0 && n >= kMinSplit) {
-    uint64_t first = n / c->filter_slice;
-    if (first < (1ull << 20)) first = n < (1ull << 21) ? n / 2 : (1ull << 20);
-    rc = launch(0, first);
-    if (rc) return rc;
-    uint32_t ncap = 0;
-    rc = cap_select(c, c->d_filter, &ncap);
-    if (rc) return rc;
+    uint64_t done = 0;
+    uint64_t next = n / c->filter_slice;
+    if (next < (1ull << 20)) next = n < (1ull << 21) ? n / 2 : (1ull << 20);
+    for (uint32_t step = 0; step < c->filter_steps && next < n; ++step) {
+      rc = launch(done, next - done);
+      if (rc) return rc;
+      uint32_t ncap = 0;
+      rc = cap_select(c, c->d_filter, &ncap);
+      if (rc) return rc;
+      done = next;
+      next = next * 4;
+    }
     c->tightened = true;
-    return launch(first, n - first);
+    return launch(done, n - done);
   }
   return launch(0, n);
 }
@@ -1105,12 +1176,13 @@ int rsa_ctx_destroy(rsa_ctx* c) {
   if (!c) return RSA_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->d_tail, c->d_tail_n, c->d_entries, c->d_off, c->d_shapes, c->d_shape_off, c->d_islots, c->d_resid, c->d_resid_off,
+  void* bufs[] = {c->d_tail, c->d_tail_n, c->d_gtag, c->d_gscratch, c->d_entries, c->d_off, c->d_hdr, c->d_shapes,
+                  c->d_img, c->d_resid,
                   c->d_slots, c->d_used, c->d_used_n, c->d_filter, c->d_flags, c->d_cursor, c->d_cidx,
                   c->d_capped_gid, c->d_capped_cnt, c->d_capped_start, c->d_keys[0], c->d_keys[1], c->d_vals[0],
                   c->d_vals[1], c->d_temp};
   for (void* b : bufs) (void)hipFree(b);
-  for (int k = 0; k < 4; ++k)
+  for (int k = 0; k < kMaxEvents; ++k)
     if (c->ev[k]) (void)hipEventDestroy(c->ev[k]);
   delete c;
   return RSA_OK;
@@ -1134,18 +1206,18 @@ int rsa_set_option(rsa_ctx* c, int option, int64_t value) {
       if (value < 2 || value > 65536) return fail(c, RSA_ERR_ARG, "filter slice must be in [2, 65536]");
       c->filter_slice = (uint32_t)value;
       return RSA_OK;
-    case RSA_OPT_SINGLE_LIST:
-      c->single_list = value != 0;
+    case RSA_OPT_FORCE_DEFER:
+      c->force_defer = value != 0;
       return RSA_OK;
-    case RSA_OPT_SCAN_PREFIX:
-      if (value <= 0) return fail(c, RSA_ERR_ARG, "scan prefix must be positive");
-      c->scan_prefix = value > 0xFFFFFFFELL ? 0xFFFFFFFEu : (uint32_t)value;
+    case RSA_OPT_FILTER_STEPS:
+      if (value < 1 || value > 8) return fail(c, RSA_ERR_ARG, "filter steps must be in [1, 8]");
+      c->filter_steps = (uint32_t)value;
       return RSA_OK;
     case RSA_OPT_PROFILE_SKIP:
       c->profile_skip = (uint32_t)value;
       return RSA_OK;
     case RSA_OPT_USE_INDEX:
-      if (value && !c->d_shapes) return fail(c, RSA_ERR_STATE, "no index loaded");
+      if (value && !c->index_loaded) return fail(c, RSA_ERR_STATE, "no index loaded");
       c->indexed = value != 0;
       return RSA_OK;
     default:
@@ -1179,45 +1251,55 @@ int rsa_load_rules(rsa_ctx* c, const rsa_rule_entry* h_entries, uint32_t n_entri
   if (rc) return rc;
   rc = upload(c, &c->d_off, h_off, (size_t)n_lists + 1);
   if (rc) return rc;
+  c->h_off.assign(h_off, h_off + n_lists + 1);
   c->n_entries = n_entries;
   c->n_lists = n_lists;
   c->n_rules = n_rules;
   c->rules_loaded = true;
   c->indexed = false;  // an index must be (re)loaded for these lists
+  c->index_loaded = false;
   return RSA_OK;
 }
 
-int rsa_load_index(rsa_ctx* c, const rsa_shape* h_shapes, uint32_t n_shapes, const uint32_t* h_shape_off,
-                   const rsa_index_slot* h_slots, uint64_t n_slots, const rsa_rule_entry* h_resid, uint32_t n_resid,
-                   const uint32_t* h_resid_off) {
-  if (!c || !h_shape_off || !h_resid_off) return fail(c, RSA_ERR_ARG, "null argument");
+int rsa_load_index(rsa_ctx* c, const rsa_pht_list* h_lists, const rsa_pht_shape* h_shapes, uint32_t n_shapes,
+                   const uint32_t* h_image, uint32_t image_words, const rsa_rule_entry* h_resid, uint32_t n_resid) {
+  if (!c || !h_lists || (n_shapes && !h_shapes) || (image_words && !h_image) || (n_resid && !h_resid))
+    return fail(c, RSA_ERR_ARG, "null argument");
   if (!c->rules_loaded) return fail(c, RSA_ERR_STATE, "load the candidate lists first");
   const uint32_t nl = c->n_lists;
-  if (h_shape_off[0] != 0 || h_shape_off[nl] != n_shapes || h_resid_off[0] != 0 || h_resid_off[nl] != n_resid)
-    return fail(c, RSA_ERR_ARG, "index offsets do not span their arrays");
-  for (uint32_t s = 0; s < n_shapes; ++s) {
-    const rsa_shape& sh = h_shapes[s];
-    if ((sh.table_mask & (sh.table_mask + 1)) != 0 || (uint64_t)sh.table_off + sh.table_mask + 1 > n_slots)
-      return fail(c, RSA_ERR_ARG, "shape %u: table outside the slot array or not a power of two", s);
-  }
+  // validate everything the kernels index with, so no launch can read out of bounds
   for (uint32_t l = 0; l < nl; ++l) {
-    for (uint32_t s = h_shape_off[l] + 1; s < h_shape_off[l + 1]; ++s)
-      if (h_shapes[s].min_gid < h_shapes[s - 1].min_gid)
-        return fail(c, RSA_ERR_ARG, "list %u: shapes not in ascending min_gid order", l);
-    for (uint32_t e = h_resid_off[l] + 1; e < h_resid_off[l + 1]; ++e)
-      if (h_resid[e].gid < h_resid[e - 1].gid) return fail(c, RSA_ERR_ARG, "list %u: residual not gid-ascending", l);
+    const rsa_pht_list& h = h_lists[l];
+    const uint32_t len = c->h_off[l + 1] - c->h_off[l];
+    if (h.shape_beg > h.shape_end || h.shape_end > n_shapes || h.resid_beg > h.resid_end || h.resid_end > n_resid)
+      return fail(c, RSA_ERR_ARG, "list %u: shape/residual range out of bounds", l);
+    if (h.prefix > len) return fail(c, RSA_ERR_ARG, "list %u: prefix %u > list length %u", l, h.prefix, len);
+    if (h.shape_beg < h.shape_end && len > 0xFFFEu) return fail(c, RSA_ERR_ARG, "list %u: indexed list too long", l);
+    for (uint32_t s = h.shape_beg; s < h.shape_end; ++s) {
+      const rsa_pht_shape& sh = h_shapes[s];
+      if (sh.n_slots == 0 || (uint64_t)sh.slot_off + sh.n_slots > image_words ||
+          (sh.disp_mask & (sh.disp_mask + 1)) != 0 || ((uint64_t)sh.disp_off + sh.disp_mask + 1) > 2ull * image_words)
+        return fail(c, RSA_ERR_ARG, "shape %u: table outside the image", s);
+      for (uint32_t k = 0; k < sh.n_slots; ++k) {
+        const uint32_t w = h_image[sh.slot_off + k];
+        if (w != 0xFFFFFFFFu && (w & 0xFFFFu) >= len) return fail(c, RSA_ERR_ARG, "shape %u: slot index out of list", s);
+      }
+    }
+    for (uint32_t e = h.resid_beg; e < h.resid_end; ++e) {
+      if (h_resid[e].gid >= c->n_rules) return fail(c, RSA_ERR_ARG, "residual entry %u gid out of range", e);
+      if (e > h.resid_beg && h_resid[e].gid < h_resid[e - 1].gid)
+        return fail(c, RSA_ERR_ARG, "list %u: residual not gid-ascending", l);
+    }
   }
-  for (uint64_t k = 0; k < n_slots; ++k)
-    if (h_slots[k].gid != kNoGid && h_slots[k].gid >= c->n_rules)
-      return fail(c, RSA_ERR_ARG, "index slot %llu gid out of range", (unsigned long long)k);
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  int rc = upload(c, &c->d_shapes, h_shapes, n_shapes);
-  if (!rc) rc = upload(c, &c->d_shape_off, h_shape_off, (size_t)nl + 1);
-  if (!rc) rc = upload(c, &c->d_islots, h_slots, (size_t)n_slots);
+  int rc = upload(c, &c->d_hdr, h_lists, nl);
+  if (!rc) rc = upload(c, &c->d_shapes, h_shapes, n_shapes);
+  if (!rc) rc = upload(c, &c->d_img, h_image, image_words);
   if (!rc) rc = upload(c, &c->d_resid, h_resid, n_resid);
-  if (!rc) rc = upload(c, &c->d_resid_off, h_resid_off, (size_t)nl + 1);
   if (rc) return rc;
+  c->img_words = image_words;
+  c->index_loaded = true;
   c->indexed = true;
   return RSA_OK;
 }
@@ -1312,27 +1394,8 @@ int rsa_classify_only(rsa_ctx* c, const rsa_tuple* T, uint64_t n, int32_t* gout)
   if (!T || !gout) return fail(c, RSA_ERR_ARG, "null tuple/gid pointer");
   if (!c->d_flags) return fail(c, RSA_ERR_STATE, "ctx not initialised");
   if (n > 0x7FFFFFFFull) return fail(c, RSA_ERR_ARG, "batch larger than 2^31 tuples");
-  Agg a = agg_of(c);
-  const uint32_t K = c->indexed ? 0xFFFFFFFFu : c->scan_prefix;
-  int rc = ensure_tail(c, n);
-  if (rc) return rc;
-  HIPCHK(c, hipMemsetAsync(c->d_tail_n, 0, 2 * sizeof(unsigned long long), c->stream));
-  const uint4* t4 = reinterpret_cast<const uint4*>(T);
-  uint32_t* ta = c->d_tail;
-  uint32_t* tb = c->d_tail + c->tail_alloc;
-  unsigned long long* na = c->d_tail_n;
-  unsigned long long* nb = c->d_tail_n + 1;
-  k_pass1<kClassifyOnly, kBlock, 0, 0><<<grid_for(c, n, 16), kBlock, 0, c->stream>>>(
-      t4, nullptr, nullptr, n, nullptr, gout, rules_of(c), a, K, ta, na, tb, nb);
-  HIPCHK(c, hipGetLastError());
-  if (K != 0xFFFFFFFFu) {
-    k_pass1<kClassifyOnly, kBlock, 0, 1><<<c->cu_count * 8, kBlock, 0, c->stream>>>(
-        t4, nullptr, nullptr, n, nullptr, gout, rules_of(c), a, K, ta, na, tb, nb);
-    k_pass1<kClassifyOnly, kBlock, 0, 2><<<c->cu_count * 4, kBlock, 0, c->stream>>>(
-        t4, nullptr, nullptr, n, nullptr, gout, rules_of(c), a, K, ta, na, tb, nb);
-    HIPCHK(c, hipGetLastError());
-  }
-  return RSA_OK;
+  return launch_classify<kClassifyOnly>(c, reinterpret_cast<const uint4*>(T), nullptr, nullptr, n, nullptr, gout,
+                                        nullptr);
 }
 
 int rsa_aggregate_gids(rsa_ctx* c, const rsa_tuple* T, const uint32_t* TS, const uint64_t* ORD, const int32_t* G,
@@ -1372,16 +1435,17 @@ int rsa_recount(rsa_ctx* c, const rsa_tuple* T, const uint32_t* TS, const uint64
   if (rc) return rc;
   if (n == 0) return RSA_OK;
   if (!T || !TS || !ORD) return fail(c, RSA_ERR_ARG, "null tuple/ts/order pointer");
-  if (G) {
-    k_pass2<true><<<grid_for(c, n, 16), kBlock, 0, c->stream>>>(
-        reinterpret_cast<const uint4*>(T), TS, reinterpret_cast<const unsigned long long*>(ORD), n, G, rules_of(c),
-        agg_of(c));
-  } else {
+  if (!G) {
+    // re-classify into scratch gids
     if (!c->rules_loaded) return fail(c, RSA_ERR_STATE, "no rules loaded (recount without gids re-classifies)");
-    k_pass2<false><<<grid_for(c, n, 16), kBlock, 0, c->stream>>>(
-        reinterpret_cast<const uint4*>(T), TS, reinterpret_cast<const unsigned long long*>(ORD), n, nullptr,
-        rules_of(c), agg_of(c));
+    rc = ensure_buf(c, &c->d_gscratch, &c->gscratch_alloc, n);
+    if (!rc) rc = rsa_classify_only(c, T, n, c->d_gscratch);
+    if (rc) return rc;
+    G = c->d_gscratch;
   }
+  k_pass2<<<grid_for(c, n, 16), kBlock, 0, c->stream>>>(reinterpret_cast<const uint4*>(T), TS,
+                                                        reinterpret_cast<const unsigned long long*>(ORD), n, G,
+                                                        c->n_rules, agg_of(c));
   HIPCHK(c, hipGetLastError());
   return RSA_OK;
 }

@@ -90,11 +90,12 @@ class Engine(object):
         self._bind(n_rules)
 
     def load_index(self, index):
-        shapes, shape_off, slots, resid, resid_off = (np.ascontiguousarray(a) for a in index)
-        self._index_hold = (shapes, shape_off, slots, resid, resid_off)
+        """Upload a compile.build_index() result (lists, shapes, image, residual)."""
+        lists, shapes, image, resid = (np.ascontiguousarray(a) for a in index)
+        self._index_hold = (lists, shapes, image, resid)
         v = lambda a: a.ctypes.data_as(ctypes.c_void_p)
-        self.ctx.call('rsa_load_index', v(shapes), ctypes.c_uint32(len(shapes)), v(shape_off), v(slots),
-                      ctypes.c_uint64(len(slots)), v(resid), ctypes.c_uint32(len(resid)), v(resid_off))
+        self.ctx.call('rsa_load_index', v(lists), v(shapes), ctypes.c_uint32(len(shapes)), v(image),
+                      ctypes.c_uint32(len(image)), v(resid), ctypes.c_uint32(len(resid)))
 
     def set_option(self, option, value):
         self.ctx.call('rsa_set_option', ctypes.c_int(option), ctypes.c_int64(int(value)))
@@ -110,12 +111,13 @@ class Engine(object):
         self.ctx.call('rsa_last_pass1_ms', ctypes.byref(ms))
         return float(ms.value)
 
-    def load_compiled(self, compiled, index=True):
-        """Upload a CompiledRules' lists (and its tuple-space-search index)."""
+    def load_compiled(self, compiled, index=True, prefix=64):
+        """Upload a CompiledRules' lists (and its perfect-hash tuple-space index,
+        whose first ``prefix`` entries per list are scanned linearly)."""
         ent, off = compiled.packed()
         self.load_rules(ent, off, compiled.n_rules)
         if index:
-            self.load_index(compiled.index())
+            self.load_index(compiled.index(prefix=prefix))
 
     def set_rule_count(self, n_rules):
         self.ctx.call('rsa_set_rule_count', ctypes.c_uint32(n_rules))

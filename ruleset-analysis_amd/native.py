@@ -30,8 +30,8 @@ class NativeError(RuntimeError):
 
 
 RSA_OK, RSA_ERR_ARG, RSA_ERR_HIP, RSA_ERR_STATE, RSA_ERR_CAPACITY = 0, -1, -2, -3, -4
-RSA_OPT_AUTO_FILTER, RSA_OPT_USE_INDEX, RSA_OPT_PROFILE_SKIP, RSA_OPT_SCAN_PREFIX, RSA_OPT_FILTER_SLICE = 1, 2, 3, 4, 5
-RSA_OPT_SINGLE_LIST = 6
+RSA_OPT_AUTO_FILTER, RSA_OPT_USE_INDEX, RSA_OPT_PROFILE_SKIP, RSA_OPT_FILTER_SLICE, RSA_OPT_FILTER_STEPS = 1, 2, 3, 5, 7
+RSA_OPT_FORCE_DEFER = 8
 
 P = ctypes.c_void_p
 U32 = ctypes.c_uint32
@@ -48,7 +48,7 @@ SYMBOLS = {
     'rsa_last_error': (ctypes.c_char_p, [P]),
     'rsa_set_stream': (I32, [P, P]),
     'rsa_set_option': (I32, [P, I32, ctypes.c_int64]),
-    'rsa_load_index': (I32, [P, P, U32, P, P, U64, P, U32, P]),
+    'rsa_load_index': (I32, [P, P, P, U32, P, U32, P, U32]),
     'rsa_last_pass1_ms': (I32, [P, ctypes.POINTER(ctypes.c_float)]),
     'rsa_load_rules': (I32, [P, P, U32, P, U32, U32]),
     'rsa_bind_counters': (I32, [P, P, P, P, P]),

@@ -91,8 +91,12 @@ def _addr_spec(rng, pool, p_any, p_host, p_net, p_group, net_plens):
     return 'object-group GRP%d' % int(rng.integers(1 << 30)), items
 
 
-def _acl_lines(rng, space, acl, n_rules, kind):
-    """Generate ACL lines until ~n_rules expanded rules; returns rule dicts and meta."""
+def _acl_lines(rng, space, acl, n_rules, kind, broad=True):
+    """Generate ACL lines until ~n_rules expanded rules; returns rule dicts and meta.
+
+    ``broad=False`` redraws the destination of any permit whose source and
+    destination are both ``any`` (so no early catch-all permit shadows the rest
+    of the list and traffic drawn from a rule first-matches at or near it)."""
     rules, meta = [], []
     lineno = 0
     target = max(2, int(n_rules))
@@ -106,6 +110,8 @@ def _acl_lines(rng, space, acl, n_rules, kind):
         else:
             s_txt, srcs = _addr_spec(rng, space.clients, 0.40, 0.25, 0.25, 0.10, [8, 16, 24])
             d_txt, dsts = _addr_spec(rng, space.servers, 0.12, 0.55, 0.23, 0.10, [24, 28])
+            while not broad and action and s_txt == 'any' and d_txt == 'any':
+                d_txt, dsts = _addr_spec(rng, space.servers, 0.12, 0.55, 0.23, 0.10, [24, 28])
         sports, dports, sp_txt, dp_txt = [], [], '', ''
         if proto in ('tcp', 'udp'):
             if rng.random() < 0.04:
@@ -144,8 +150,12 @@ def _acl_lines(rng, space, acl, n_rules, kind):
     return rules, protocols, meta
 
 
-def make_db(seed, n_rules, host='fw1', interfaces=('outside',), inside_rules=16, with_inside=True):
+def make_db(seed, n_rules, host='fw1', interfaces=('outside',), inside_rules=16, with_inside=True, broad=True):
     """Seeded rule DB (JSON-able dict) plus per-ACL numeric rule metadata.
+
+    ``broad``: allow ``permit ... any ... any`` lines anywhere in the outside
+    ACLs (they shadow everything after them: short scans).  The bench
+    workloads use ``broad=False`` — first matches spread over the whole list.
 
     ``interfaces``: each gets its own ``<ifc>_access_in`` ACL of ``n_rules``
     expanded rules bound ``in``.  ``with_inside`` adds a small
@@ -157,7 +167,7 @@ def make_db(seed, n_rules, host='fw1', interfaces=('outside',), inside_rules=16,
     acls, meta = {}, {}
     for ifc in interfaces:
         acl = '%s_access_in' % ifc
-        rules, protos, m = _acl_lines(rng, space, acl, n_rules, 'outside')
+        rules, protos, m = _acl_lines(rng, space, acl, n_rules, 'outside', broad=broad)
         acls[acl] = {'rules': rules, 'protocols': protos, 'timestamp': 1373846400.0}
         meta[acl] = m
         firewalls[host][ifc] = {'in': acl}

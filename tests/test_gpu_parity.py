@@ -47,8 +47,8 @@ def test_golden_mapper_stream(engine, case):
 
 
 def _gpu_vs_oracle(engine, n_rules, n_lines, cap, seed, zipf=None, interfaces=('outside',), batches=1,
-                   shuffle=False, index=True):
-    dbj, info = synth.make_db(seed, n_rules, interfaces=interfaces)
+                   shuffle=False, index=True, broad=True, prefix=64):
+    dbj, info = synth.make_db(seed, n_rules, interfaces=interfaces, broad=broad)
     tr = synth.make_traffic((dbj, info), n_lines, seed=seed + 1, zipf=zipf)
     if shuffle:   # input order no longer follows the sort order
         perm = np.random.default_rng(seed).permutation(n_lines)
@@ -57,7 +57,7 @@ def _gpu_vs_oracle(engine, n_rules, n_lines, cap, seed, zipf=None, interfaces=('
     db = acldb.load_json(dbj)
     compiled = CompiledRules(db)
     tup, ts, order = synth.pack(tr, compiled)
-    engine.load_compiled(compiled, index=index)
+    engine.load_compiled(compiled, index=index, prefix=prefix)
     cuts = np.linspace(0, n_lines, batches + 1).astype(int)
     bs = [DeviceBatch.from_numpy(tup[a:b], ts[a:b], order[a:b], engine.device) for a, b in zip(cuts[:-1], cuts[1:])]
     res = engine.run(bs, cap, capacity=max(built_hit_count(tup), 1))
@@ -100,28 +100,35 @@ def test_synth_parity_linear_scan(engine):
 
 
 def test_synth_parity_deferred_tail(engine):
-    """A tiny scan prefix defers most lines to the tail kernel: same answers."""
+    """Every index candidate forced through the exact deferred-line kernel."""
     from ruleset_analysis_amd import native
-    engine.set_option(native.RSA_OPT_SCAN_PREFIX, 3)
+    engine.set_option(native.RSA_OPT_FORCE_DEFER, 1)
     try:
-        _gpu_vs_oracle(engine, 2000, 300000, 50, seed=23, index=False, zipf=1.2)
+        _gpu_vs_oracle(engine, 2000, 300000, 50, seed=23, zipf=1.2, broad=False, prefix=0)
     finally:
-        engine.set_option(native.RSA_OPT_SCAN_PREFIX, 256)
+        engine.set_option(native.RSA_OPT_FORCE_DEFER, 0)
 
 
-def test_index_and_scan_agree_10k(engine):
-    """The tuple-space-search index and the linear scan classify identically."""
-    dbj, info = synth.make_db(19, 10000)
+@pytest.mark.parametrize('broad,prefix', [(True, 64), (False, 64), (False, 0), (False, 4096)])
+def test_index_and_scan_agree_10k(engine, broad, prefix):
+    """The perfect-hash index (after a linear prefix) and the plain linear scan
+    classify identically, half of the lines unmatched (full-list scans)."""
+    dbj, info = synth.make_db(19, 10000, broad=broad)
     tr = synth.make_traffic((dbj, info), 1_000_000, seed=20, p_unmatched=0.5)
     compiled = CompiledRules(acldb.load_json(dbj))
     tup, _ts, _order = synth.pack(tr, compiled)
     b = DeviceBatch.from_numpy(tup, _ts, _order, engine.device)
-    engine.load_compiled(compiled, index=True)
+    engine.load_compiled(compiled, index=True, prefix=prefix)
     g_idx = engine.classify_only(b).cpu().numpy()
     engine.use_index(False)
     g_scan = engine.classify_only(b).cpu().numpy()
     assert np.array_equal(g_idx, g_scan)
     assert (g_idx >= 0).sum() > 0
+
+
+def test_synth_parity_10k_rules_spread(engine):
+    """Realistic ACL (no catch-all permit): first matches spread over 10k rules."""
+    _gpu_vs_oracle(engine, 10000, 300000, 20, seed=25, broad=False)
 
 
 def test_synth_parity_capped_zipf(engine):
@@ -152,17 +159,15 @@ def test_synth_parity_tightened_filter_shuffled(engine):
     _gpu_vs_oracle(engine, 800, 5_000_000, 40, seed=17, zipf=1.2, shuffle=True)
 
 
-def test_synth_parity_single_list_stages(engine):
-    """Majority-list stage 0 + both tail stages (tiny prefix): same answers."""
+def test_synth_parity_filter_steps(engine):
+    """Filter refined three times (after 1/256, 1/64, 1/16 of the batch)."""
     from ruleset_analysis_amd import native
-    engine.set_option(native.RSA_OPT_SINGLE_LIST, 1)
-    engine.set_option(native.RSA_OPT_SCAN_PREFIX, 5)
+    engine.set_option(native.RSA_OPT_FILTER_STEPS, 3)
     try:
-        _gpu_vs_oracle(engine, 1500, 300000, 40, seed=24, index=False, zipf=1.1,
+        _gpu_vs_oracle(engine, 1500, 5_000_000, 40, seed=24, zipf=1.1, broad=False,
                        interfaces=('outside', 'partner'))
     finally:
-        engine.set_option(native.RSA_OPT_SINGLE_LIST, 0)
-        engine.set_option(native.RSA_OPT_SCAN_PREFIX, 256)
+        engine.set_option(native.RSA_OPT_FILTER_STEPS, 1)
 
 
 def test_deterministic(engine):

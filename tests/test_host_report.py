@@ -95,38 +95,28 @@ def test_compiled_tables_first_match(case):
 
 
 def _emulate_index(tuples, index, ent, off):
-    """Test-only evaluation of the tuple-space-search index (hash probes)."""
-    from ruleset_analysis_amd.compile import index_hash
-    shapes, shape_off, slots, resid, resid_off = index
-    out = _emulate_first_match(tuples, resid, resid_off).astype(np.int64)
-    out[out < 0] = 1 << 40
-    valid = (tuples['flags'] & 1) == 1
-    for L in np.unique(tuples['list'][valid]):
-        idx = np.nonzero(valid & (tuples['list'] == L))[0]
-        t = tuples[idx]
-        ports = t['sport'].astype(np.uint32) | (t['dport'].astype(np.uint32) << np.uint32(16))
-        for s in shapes[shape_off[L]:shape_off[L + 1]]:
-            ks = t['src'] & s['src_mask']
-            kd = t['dst'] & s['dst_mask']
-            kp = ports & s['port_mask']
-            h = index_hash(ks, kd, kp, s['salt']) & s['table_mask']
-            for j in range(len(idx)):
-                p = int(h[j])
-                while True:
-                    q = slots[int(s['table_off']) + p]
-                    if q['gid'] == 0xFFFFFFFF:
-                        break
-                    if q['src'] == ks[j] and q['dst'] == kd[j] and q['ports'] == kp[j]:
-                        out[idx[j]] = min(out[idx[j]], int(q['gid']))
-                        break
-                    p = (p + 1) & int(s['table_mask'])
-    out[out == 1 << 40] = -1
+    """Test-only evaluation of the perfect-hash index (compile.pht_lookup, the
+    host model of the device probe sequence); deferred lines are scanned."""
+    from ruleset_analysis_amd.compile import pht_lookup
+    exact = _emulate_first_match(tuples, ent, off)
+    out = np.full(len(tuples), -1, dtype=np.int64)
+    n_defer = 0
+    for i in np.nonzero((tuples['flags'] & 1) == 1)[0]:
+        t = tuples[i]
+        L = int(t['list'])
+        ports = int(t['sport']) | (int(t['dport']) << 16)
+        k = pht_lookup(index, ent, off, L, int(t['src']), int(t['dst']), ports)
+        if k == 'defer':
+            n_defer += 1
+            out[i] = exact[i]
+        elif k >= 0:
+            out[i] = int(ent[int(off[L]) + k]['gid'])
     return out
 
 
 @pytest.mark.parametrize('case', ['small_200r', 'cap5_zipf'])
 def test_index_first_match(case):
-    """The tuple-space-search index gives the oracle's first match for every line."""
+    """The perfect-hash index gives the oracle's first match for every line."""
     dbj, text, _report, _sha, params = load_case(case)
     lines = split_lines(text)
     db = acldb.load_json(dbj)
@@ -134,8 +124,8 @@ def test_index_first_match(case):
     parsed = parse_logs([(params['host'], lines)], db, compiled)
     ent, off = compiled.packed()
     from ruleset_analysis_amd.compile import build_index
-    index = build_index(ent, off, probe_cost=0)       # force the index on every list
-    assert len(index[0]) > 0
+    index = build_index(ent, off, prefix=0, min_entries=1)    # force the index on every list
+    assert len(index[1]) > 0
     got = _emulate_index(parsed.tuples, index, ent, off)
     _results, gids, _t, _s = oracle_results(dbj, params['host'], lines, params['cap'])
     assert np.array_equal(got, gids)

@@ -42,8 +42,10 @@ def main():
     ap.add_argument('--cap', type=int, default=1000)
     ap.add_argument('--reps', type=int, default=3)
     ap.add_argument('--zipf', type=float, default=0.0)
+    ap.add_argument('--broad', action='store_true', help='allow catch-all permits (short scans)')
+    ap.add_argument('--scan', action='store_true', help='also time the plain linear scan')
     args = ap.parse_args()
-    dbj, info = synth.make_db(3, args.rules)
+    dbj, info = synth.make_db(3, args.rules, broad=args.broad)
     compiled = CompiledRules(acldb.load_json(dbj))
     compiled.ensure_lists()
     eng = Engine(0)
@@ -58,28 +60,31 @@ def main():
     res = {'lines': args.lines, 'rules': compiled.n_rules, 'entries': len(ent), 'hit_built': n_hb,
            'distinct': size}
     res['classify_only_ms'] = timed(lambda: eng.classify_only(batch, g), args.reps)
-    eng.use_index(False)
     from ruleset_analysis_amd import native
-    for K in (64, 256, 1024, 1 << 30):
-        eng.set_option(native.RSA_OPT_SCAN_PREFIX, K)
-        res['classify_scan_K%d_ms' % K] = timed(lambda: eng.classify_only(batch, g), args.reps)
-    eng.set_option(native.RSA_OPT_SCAN_PREFIX, 256)
-    eng.use_index(True)
+    for pre in (0, 16, 256):
+        eng.load_compiled(compiled, prefix=pre)
+        res['classify_prefix%d_ms' % pre] = timed(lambda: eng.classify_only(batch, g), args.reps)
+    eng.load_compiled(compiled)
+    if args.scan:
+        eng.use_index(False)
+        res['classify_scan_ms'] = timed(lambda: eng.classify_only(batch, g), args.reps)
+        eng.use_index(True)
 
     def p1():
         eng.reset(int(size * 1.25), cap)
         eng.pass1(batch, g)
     res['reset_ms'] = timed(lambda: eng.reset(int(size * 1.25), cap), args.reps)
     res['reset_pass1_ms'] = timed(p1, args.reps)
-    eng.use_index(False)
-    res['scan_reset_pass1_ms'] = timed(p1, args.reps)
     for mask, name in ((1, 'no_counters'), (2, 'no_table'), (3, 'no_agg')):
         eng.set_option(native.RSA_OPT_PROFILE_SKIP, mask)
-        res['scan_pass1_%s_ms' % name] = timed(p1, args.reps)
+        res['pass1_%s_ms' % name] = timed(p1, args.reps)
     eng.set_option(native.RSA_OPT_PROFILE_SKIP, 0)
+    for steps in (2, 3, 4):
+        eng.set_option(native.RSA_OPT_FILTER_STEPS, steps)
+        res['reset_pass1_steps%d_ms' % steps] = timed(p1, args.reps)
+    eng.set_option(native.RSA_OPT_FILTER_STEPS, 1)
     eng.reset(int(size * 1.25), cap)
     eng.pass1(batch, g)
-    eng.use_index(True)
     t = time.perf_counter()
     ncap = eng.resolve_cap()
     torch.cuda.synchronize()
