@@ -64,29 +64,37 @@ typedef struct rsa_rule_entry {
 /* Perfect-hash tuple-space index (optional; compile.py build_index).  Per
  * candidate list: entries [0, prefix) are scanned linearly; entries >= prefix
  * whose addresses are prefixes and whose ports are "any" or one value are
- * grouped by shape (src mask, dst mask, port mask), and each shape owns a CHD
- * (hash-and-displace) perfect-hash table over the masked key
- * (src & src_mask, dst & dst_mask, ports & port_mask), ports = sport | dport << 16:
+ * grouped by (src mask, dst mask) and, inside a group, by port class
+ * c = 0..3 with port mask {0, 0xFFFF0000 (dport), 0x0000FFFF (sport),
+ * 0xFFFFFFFF}.  Each (group, class) owns a CHD (hash-and-displace)
+ * perfect-hash table over the masked key (src & src_mask, dst & dst_mask,
+ * ports & port_mask), ports = sport | dport << 16:
  *   H    = fmix32(ks ^ 0x9E3779B9) ^ fmix32(kd ^ 0x7F4A7C15) ^ fmix32(kp ^ 0x2545F491)
- *   d    = disp[disp_off + ((H >> 16) & disp_mask)]            (uint16 units)
+ *   d    = disp[disp_off + ((H >> 16) & disp_mask)]            (uint16 units of the image)
  *   slot = hi32((H + ((d * ((H >> 16) | 1)) << 16)) * n_slots)  (32-bit wrap)
  *   word = image[slot_off + slot] = (H & 0xFFFF) << 16 | list-local entry index,
- *          0xFFFFFFFF = empty
+ *          0xFFFFFFFF = empty (image word 0 is always empty: absent classes
+ *          point there with n_slots = 1)
  * and holds the smallest entry index with that key.  All other entries are
  * residual (a gid-ascending list scanned linearly).  The answer is identical to
  * the linear scan: the minimum matching gid (the device verifies the hashed
  * candidate against the full entry). */
-typedef struct rsa_pht_shape {
-  uint32_t src_mask, dst_mask, port_mask;
-  uint32_t min_idx;    /* smallest list-local entry index in the shape           */
+typedef struct rsa_pht_table {
   uint32_t slot_off;   /* first slot word in the image                           */
   uint32_t disp_off;   /* first displacement, in uint16 units of the image       */
-  uint32_t n_slots;    /* table size (slots)                                     */
+  uint32_t n_slots;    /* table size (slots), >= 1                               */
   uint32_t disp_mask;  /* displacement buckets - 1 (power of two)                */
-} rsa_pht_shape;
+} rsa_pht_table;
+
+typedef struct rsa_pht_group {
+  uint32_t src_mask, dst_mask;
+  uint32_t min_idx;          /* smallest list-local entry index in the group      */
+  uint32_t n_real;           /* classes with a real table                         */
+  rsa_pht_table table[4];    /* port classes any, dport, sport, sport+dport       */
+} rsa_pht_group;
 
 typedef struct rsa_pht_list {
-  uint32_t shape_beg, shape_end; /* this list's shapes                           */
+  uint32_t group_beg, group_end; /* this list's groups (sorted by src mask)       */
   uint32_t resid_beg, resid_end; /* this list's residual entries                 */
   uint32_t prefix;               /* entries scanned linearly before the index    */
   uint32_t reserved[3];
@@ -136,7 +144,7 @@ int rsa_load_rules(rsa_ctx *ctx, const rsa_rule_entry *h_entries, uint32_t n_ent
 /* Upload a perfect-hash tuple-space index over the lists of rsa_load_rules
  * (h_lists has n_lists entries, same list ids).  Enables RSA_OPT_USE_INDEX.
  * Every offset and slot is validated against the loaded lists. */
-int rsa_load_index(rsa_ctx *ctx, const rsa_pht_list *h_lists, const rsa_pht_shape *h_shapes, uint32_t n_shapes,
+int rsa_load_index(rsa_ctx *ctx, const rsa_pht_list *h_lists, const rsa_pht_group *h_groups, uint32_t n_groups,
                    const uint32_t *h_image, uint32_t image_words, const rsa_rule_entry *h_resid, uint32_t n_resid);
 
 /* Bind caller-owned device counters, each n_rules long (n_rules from

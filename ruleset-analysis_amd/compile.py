@@ -165,7 +165,7 @@ class CompiledRules(object):
     def n_lists(self):
         return len(self._lists)
 
-    def index(self, prefix=64):
+    def index(self, prefix=32):
         """Perfect-hash tuple-space index of the current lists (cached until a list is added)."""
         ent, off = self.packed()
         if getattr(self, '_index', None) is None or self._index[0] is not self._packed or self._index[1] != prefix:
@@ -198,11 +198,14 @@ class CompiledRules(object):
 # the GPU verifies it against the full entry (a 16-bit tag can collide) and
 # defers the line to an exact scan when it fails.  First match = min gid, so
 # the answer is the linear scan's.
-PHT_SHAPE_DTYPE = np.dtype([('src_mask', '<u4'), ('dst_mask', '<u4'), ('port_mask', '<u4'), ('min_idx', '<u4'),
-                            ('slot_off', '<u4'), ('disp_off', '<u4'), ('n_slots', '<u4'), ('disp_mask', '<u4')])
-PHT_LIST_DTYPE = np.dtype([('shape_beg', '<u4'), ('shape_end', '<u4'), ('resid_beg', '<u4'), ('resid_end', '<u4'),
+PHT_GROUP_DTYPE = np.dtype([('src_mask', '<u4'), ('dst_mask', '<u4'), ('min_idx', '<u4'), ('n_real', '<u4')] +
+                           [(f, '<u4') for c in range(4) for f in ('slot_off%d' % c, 'disp_off%d' % c,
+                                                                      'n_slots%d' % c, 'disp_mask%d' % c)])
+PHT_LIST_DTYPE = np.dtype([('group_beg', '<u4'), ('group_end', '<u4'), ('resid_beg', '<u4'), ('resid_end', '<u4'),
                            ('prefix', '<u4'), ('reserved0', '<u4'), ('reserved1', '<u4'), ('reserved2', '<u4')])
-assert PHT_SHAPE_DTYPE.itemsize == 32 and PHT_LIST_DTYPE.itemsize == 32
+assert PHT_GROUP_DTYPE.itemsize == 80 and PHT_LIST_DTYPE.itemsize == 32
+# the four port classes of a group, probe order: key ports & mask
+PORT_CLASSES = (0x00000000, 0xFFFF0000, 0x0000FFFF, 0xFFFFFFFF)    # any, dport, sport, both
 M32 = 0xFFFFFFFF
 PHT_EMPTY = 0xFFFFFFFF
 PHT_MAX_IDX = 0xFFFE
@@ -303,21 +306,24 @@ def _chd(H, load=0.9, trials=4096):
 def build_index(ent, off, prefix=64, min_entries=96):
     """Perfect-hash tuple-space index over packed lists (rsa_load_index arrays).
 
-    Returns (lists PHT_LIST_DTYPE[n_lists], shapes PHT_SHAPE_DTYPE[], image
-    uint32[], resid RULE_DTYPE[]).  A list shorter than ``min_entries`` (or of
-    >= 65535 entries) gets no shapes: everything after its prefix is residual."""
+    Returns (lists PHT_LIST_DTYPE[n_lists], groups PHT_GROUP_DTYPE[], image
+    uint32[], resid RULE_DTYPE[]).  A group = one (src mask, dst mask) pair of a
+    list with a table per port class (PORT_CLASSES; an absent class points at
+    image word 0, an always-empty one-slot table).  A list shorter than
+    ``min_entries`` (or of >= 65535 entries) gets no groups: everything after
+    its prefix is residual."""
     n_lists = len(off) - 1
     lists = np.zeros(n_lists, dtype=PHT_LIST_DTYPE)
-    shapes, image, resid_parts = [], [], []
-    n_img = 0
+    groups_out, image, resid_parts = [], [np.array([PHT_EMPTY], np.uint32)], []
+    n_img = 1
     n_resid = 0
     for L in range(n_lists):
         e = ent[off[L]:off[L + 1]]
         ne = len(e)
         pre = min(prefix, ne)
         lists[L]['prefix'] = pre
-        lists[L]['shape_beg'] = len(shapes)
-        groups = {}
+        lists[L]['group_beg'] = len(groups_out)
+        shapes = {}
         resid_idx = []
         indexable = ne >= min_entries and ne <= PHT_MAX_IDX
         for k in range(pre, ne):
@@ -335,51 +341,63 @@ def build_index(ent, off, prefix=64, min_entries=96):
                 continue
             pm = spm | (dpm << 16)
             key = (int(x['src_lo']), int(x['dst_lo']), pl & pm)
-            g = groups.setdefault((sm, dm, pm), {})
+            g = shapes.setdefault((sm, dm, pm), {})
             if key not in g:                 # entries are gid-ascending: first = min index
                 g[key] = k
-        for (sm, dm, pm) in sorted(groups):
-            keys = groups[(sm, dm, pm)]
-            ks = np.array(list(keys.keys()), dtype=np.uint64).astype(np.uint32).reshape(-1, 3)
-            idx = np.array(list(keys.values()), dtype=np.int64)
-            H = pht_hash(ks[:, 0], ks[:, 1], ks[:, 2])
-            # a full 32-bit hash collision between two keys of one shape: keep the
-            # smaller index in the table, the other goes residual (still exact)
-            o = np.lexsort((idx, H))
-            H, idx = H[o], idx[o]
-            dup = np.zeros(len(H), dtype=bool)
-            dup[1:] = H[1:] == H[:-1]
-            resid_idx.extend(idx[dup].tolist())
-            H, idx = H[~dup], idx[~dup]
-            nslots, dmask, disp, slot_of = _chd(H)
-            nwords_disp = (dmask + 2) // 2
-            disp_off = 2 * n_img                               # in uint16 units
-            dwords = np.zeros(nwords_disp * 2, dtype=np.uint16)
-            dwords[:dmask + 1] = disp
-            image.append(dwords.view(np.uint32))
-            n_img += nwords_disp
-            slots = np.full(nslots, PHT_EMPTY, dtype=np.uint32)
-            slots[slot_of] = ((H & np.uint32(0xFFFF)).astype(np.uint32) << np.uint32(16)) | idx.astype(np.uint32)
-            shapes.append((sm, dm, pm, int(idx.min()), n_img, disp_off, nslots, dmask))
-            image.append(slots)
-            n_img += nslots
-        lists[L]['shape_end'] = len(shapes)
+        by_sd = {}
+        for (sm, dm, pm) in shapes:
+            by_sd.setdefault((sm, dm), {})[pm] = shapes[(sm, dm, pm)]
+        for (sm, dm) in sorted(by_sd):
+            rec = [sm, dm, 0xFFFFFFFF, 0]
+            for pm in PORT_CLASSES:
+                keys = by_sd[(sm, dm)].get(pm)
+                if not keys:
+                    rec += [0, 0, 1, 0]          # dummy: image word 0 is an empty slot
+                    continue
+                ks = np.array(list(keys.keys()), dtype=np.uint64).astype(np.uint32).reshape(-1, 3)
+                idx = np.array(list(keys.values()), dtype=np.int64)
+                H = pht_hash(ks[:, 0], ks[:, 1], ks[:, 2])
+                # a full 32-bit hash collision between two keys of one shape: keep the
+                # smaller index in the table, the other goes residual (still exact)
+                o = np.lexsort((idx, H))
+                H, idx = H[o], idx[o]
+                dup = np.zeros(len(H), dtype=bool)
+                dup[1:] = H[1:] == H[:-1]
+                resid_idx.extend(idx[dup].tolist())
+                H, idx = H[~dup], idx[~dup]
+                nslots, dmask, disp, slot_of = _chd(H)
+                nwords_disp = (dmask + 2) // 2
+                disp_off = 2 * n_img                               # in uint16 units
+                dwords = np.zeros(nwords_disp * 2, dtype=np.uint16)
+                dwords[:dmask + 1] = disp
+                image.append(dwords.view(np.uint32))
+                n_img += nwords_disp
+                slots = np.full(nslots, PHT_EMPTY, dtype=np.uint32)
+                slots[slot_of] = ((H & np.uint32(0xFFFF)).astype(np.uint32) << np.uint32(16)) | idx.astype(np.uint32)
+                rec += [n_img, disp_off, nslots, dmask]
+                rec[2] = min(rec[2], int(idx.min()))
+                rec[3] += 1
+                image.append(slots)
+                n_img += nslots
+            groups_out.append(tuple(rec))
+        lists[L]['group_end'] = len(groups_out)
         resid_idx = sorted(resid_idx)
         lists[L]['resid_beg'] = n_resid
         resid_parts.append(e[resid_idx])
         n_resid += len(resid_idx)
         lists[L]['resid_end'] = n_resid
-    shp = np.array(shapes, dtype=PHT_SHAPE_DTYPE) if shapes else np.zeros(0, PHT_SHAPE_DTYPE)
-    img = np.concatenate(image) if image else np.zeros(0, np.uint32)
+    grp = np.array(groups_out, dtype=PHT_GROUP_DTYPE) if groups_out else np.zeros(0, PHT_GROUP_DTYPE)
+    img = np.concatenate(image)
     resid = np.concatenate(resid_parts) if resid_parts else np.zeros(0, RULE_DTYPE)
-    return lists, shp, img, resid
+    return lists, grp, img, resid
 
 
 def pht_lookup(index, ent, off, L, src, dst, ports):
     """Host model of the GPU classifier for one tuple (tests): the first-match
-    list-local index or -1.  Follows the device order exactly: prefix scan,
-    min candidate over the shapes, verification, residual scan."""
-    lists, shp, img, resid = index
+    list-local index, -1, or 'defer'.  Follows the device order exactly: prefix
+    scan, min candidate over the groups' port-class probes, verification,
+    residual scan."""
+    lists, grp, img, resid = index
     h = lists[L]
     e = ent[off[L]:off[L + 1]]
 
@@ -394,14 +412,15 @@ def pht_lookup(index, ent, off, L, src, dst, ports):
             return k
     cand = 0xFFFF
     d16 = img.view(np.uint16)
-    for s in shp[int(h['shape_beg']):int(h['shape_end'])]:
-        H = int(pht_hash(src & int(s['src_mask']), dst & int(s['dst_mask']), ports & int(s['port_mask'])))
-        tag = H & 0xFFFF
-        d = int(d16[int(s['disp_off']) + ((H >> 16) & int(s['disp_mask']))])
-        slot = int(pht_slot(H, d, int(s['n_slots'])))
-        w = int(img[int(s['slot_off']) + slot])
-        if (w >> 16) == tag:
-            cand = min(cand, w & 0xFFFF)
+    for g in grp[int(h['group_beg']):int(h['group_end'])]:
+        for c, pm in enumerate(PORT_CLASSES):
+            H = int(pht_hash(src & int(g['src_mask']), dst & int(g['dst_mask']), ports & pm))
+            tag = H & 0xFFFF
+            d = int(d16[int(g['disp_off%d' % c]) + ((H >> 16) & int(g['disp_mask%d' % c]))])
+            slot = int(pht_slot(H, d, int(g['n_slots%d' % c])))
+            w = int(img[int(g['slot_off%d' % c]) + slot])
+            if (w >> 16) == tag:
+                cand = min(cand, w & 0xFFFF)
     best = None
     if cand != 0xFFFF:
         if not match(e[cand]):

@@ -36,7 +36,6 @@
 //             capped rules only.
 //   emit      compact the used slots to rsa_conn_record rows.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <cstdarg>
 #include <cstdio>
@@ -65,7 +64,7 @@ struct alignas(64) Slot {
 static_assert(sizeof(Slot) == 64, "slot layout");
 static_assert(sizeof(rsa_tuple) == 16, "tuple layout");
 static_assert(sizeof(rsa_rule_entry) == 32, "rule layout");
-static_assert(sizeof(rsa_pht_shape) == 32, "shape layout");
+static_assert(sizeof(rsa_pht_group) == 80, "group layout");
 static_assert(sizeof(rsa_pht_list) == 32, "list header layout");
 static_assert(sizeof(rsa_conn_record) == 40, "record layout");
 
@@ -82,8 +81,8 @@ struct Rules {
   uint32_t n_lists;
   uint32_t n_rules;
   // perfect-hash tuple-space index (optional)
-  const const_v4u* hdr;         // per list 2 x v4u: {shape_beg, shape_end, resid_beg, resid_end}, {prefix, ...}
-  const const_v4u* shapes;      // per shape 2 x v4u: {smask, dmask, pmask, min_idx}, {slot_off, disp_off, n_slots, disp_mask}
+  const const_v4u* hdr;         // per list 2 x v4u: {group_beg, group_end, resid_beg, resid_end}, {prefix, ...}
+  const const_v4u* groups;      // per group 5 x v4u: {smask, dmask, min_idx, n_real}, 4 x {slot_off, disp_off, n_slots, disp_mask}
   const const_v4u* resid;       // residual entries (gid-ascending per list)
   const uint32_t* img;          // slot + displacement image (global copy)
   uint32_t img_words;
@@ -202,6 +201,7 @@ __device__ __forceinline__ uint32_t scan_list(const const_v4u* E, uint32_t beg, 
 
 constexpr uint32_t kDefer = 0xFFFFFFFEu;   // the index candidate failed verification: exact scan later
 constexpr uint32_t kNoCand = 0xFFFFu;
+constexpr int kImgSmallMax = 16000;   // LDS image words that still allow two 1024-thread workgroups per CU
 
 // murmur3 finaliser; must equal compile.py fmix32.
 __device__ __forceinline__ uint32_t fmix32(uint32_t x) {
@@ -226,13 +226,27 @@ __device__ __forceinline__ uint32_t pht_probe(P32 img, uint32_t H, v4u b) {
   return ((w >> 16) == (H & 0xFFFFu)) ? (w & 0xFFFFu) : kNoCand;
 }
 
+// Port-class hash components of a tuple (PORT_CLASSES order: any, dport, sport, both).
+struct PortHash {
+  uint32_t h0, h1, h2, h3;
+};
+__device__ __forceinline__ PortHash port_hashes(uint32_t ports) {
+  PortHash p;
+  p.h0 = fmix32(0u ^ kSaltP);
+  p.h1 = fmix32((ports & 0xFFFF0000u) ^ kSaltP);
+  p.h2 = fmix32((ports & 0x0000FFFFu) ^ kSaltP);
+  p.h3 = fmix32(ports ^ kSaltP);
+  return p;
+}
+
 // First match for the `mine` lanes of list L (wave-uniform).  Without the
 // index: a linear scan of the whole list.  With it: prefix scan, then (only if
-// some lane is still open) the shapes' perfect-hash probes, verification of the
-// minimum candidate and the residual scan.  Returns gid, kNoGid or kDefer.
+// some lane is still open) four independent probes per (src mask, dst mask)
+// group, verification of the minimum candidate and the residual scan.
+// Returns gid, kNoGid or kDefer.
 template <typename P32>
 __device__ __forceinline__ uint32_t classify_list(const Rules& R, P32 img, uint32_t L, bool mine, uint32_t src,
-                                                  uint32_t dst, uint32_t ports) {
+                                                  uint32_t dst, uint32_t ports, const PortHash& ph) {
   const uint32_t beg = R.off[L], end = R.off[L + 1];
   if (!R.indexed) return scan_list(R.e, beg, end, mine, kNoGid, src, dst, ports);
   const v4u h0 = R.hdr[2 * L], h1 = R.hdr[2 * L + 1];
@@ -240,27 +254,21 @@ __device__ __forceinline__ uint32_t classify_list(const Rules& R, P32 img, uint3
   const bool open = mine && best == kNoGid;
   if (__ballot(open) == 0) return best;
   uint32_t cand = kNoCand;
-  uint32_t hs = 0, hsd = 0, hp = 0;
-  uint32_t psm = 0, pdm = 0, ppm = 0;
-  for (uint32_t s = h0.x; s < h0.y; ++s) {
-    const v4u a = R.shapes[2 * s], b = R.shapes[2 * s + 1];
-    // shapes are sorted by (src mask, dst mask, port mask): each hash component
-    // is recomputed only when its mask changes (wave-uniform branches)
-    const bool first = s == h0.x;
-    const bool s_chg = first || a.x != psm;
-    if (s_chg) {
+  uint32_t hs = 0, psm = 0;
+  for (uint32_t g = h0.x; g < h0.y; ++g) {
+    const v4u a = R.groups[5 * g];
+    const v4u t0 = R.groups[5 * g + 1], t1 = R.groups[5 * g + 2], t2 = R.groups[5 * g + 3],
+              t3 = R.groups[5 * g + 4];
+    if (g == h0.x || a.x != psm) {   // groups are sorted by src mask: wave-uniform branch
       hs = fmix32((src & a.x) ^ kSaltS);
       psm = a.x;
     }
-    if (s_chg || a.y != pdm) {
-      hsd = hs ^ fmix32((dst & a.y) ^ kSaltD);
-      pdm = a.y;
-    }
-    if (first || a.z != ppm) {
-      hp = fmix32((ports & a.z) ^ kSaltP);
-      ppm = a.z;
-    }
-    cand = min(cand, pht_probe(img, hsd ^ hp, b));
+    const uint32_t hsd = hs ^ fmix32((dst & a.y) ^ kSaltD);
+    const uint32_t c0 = pht_probe(img, hsd ^ ph.h0, t0);
+    const uint32_t c1 = pht_probe(img, hsd ^ ph.h1, t1);
+    const uint32_t c2 = pht_probe(img, hsd ^ ph.h2, t2);
+    const uint32_t c3 = pht_probe(img, hsd ^ ph.h3, t3);
+    cand = min(cand, min(min(c0, c1), min(c2, c3)));
   }
   uint32_t res = kNoGid;
   if (open && cand != kNoCand) {
@@ -271,18 +279,34 @@ __device__ __forceinline__ uint32_t classify_list(const Rules& R, P32 img, uint3
   return open ? res : best;
 }
 
+constexpr uint32_t kDeferList = 0xFFFFFFFDu;   // stage 0: not the wave's majority list
+
 // First-match classification of one wave of tuples: waterfall over the distinct
 // candidate lists present in the wave (list id broadcast by readlane).
 // kExact: ignore the index (linear scan of whole lists) — the deferred-line path.
-template <bool kExact, typename P32>
+// kMajority: classify only the wave's (approximate) majority list; lanes of
+// other lists return kDeferList (a later launch over those lanes sees mostly
+// single-list waves, so a wave pays for one list's probes, not two).
+template <bool kExact, bool kMajority, typename P32>
 __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Rules& R, P32 img, unsigned int* flags) {
   const uint32_t list = t.w & 0xFFFFu;
   if (active && list >= R.n_lists) {
     atomicOr(&flags[1], 1u);
     active = false;
   }
+  PortHash ph = {0u, 0u, 0u, 0u};
+  if (!kExact && R.indexed) ph = port_hashes(t.z);
   uint32_t best = kNoGid;
   unsigned long long pending = __ballot(active);
+  if (kMajority && pending) {
+    uint32_t L = __builtin_amdgcn_readlane(list, __builtin_ctzll(pending));
+    const unsigned long long m1 = __ballot(active && list == L);
+    if (2 * __popcll(m1) < __popcll(pending)) L = __builtin_amdgcn_readlane(list, __builtin_ctzll(pending & ~m1));
+    const bool mine = active && list == L;
+    const uint32_t b = classify_list(R, img, L, mine, t.x, t.y, t.z, ph);
+    if (!active) return kNoGid;
+    return mine ? b : kDeferList;
+  }
   while (pending) {
     const int leader = __builtin_ctzll(pending);
     const uint32_t L = __builtin_amdgcn_readlane(list, leader);
@@ -292,7 +316,7 @@ __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Ru
     if (kExact) {
       b = scan_list(R.e, R.off[L], R.off[L + 1], mine, kNoGid, t.x, t.y, t.z);
     } else {
-      b = classify_list(R, img, L, mine, t.x, t.y, t.z);
+      b = classify_list(R, img, L, mine, t.x, t.y, t.z, ph);
     }
     if (mine) best = b;
   }
@@ -397,43 +421,56 @@ __device__ __forceinline__ void finish_line(bool in, unsigned long long i, uint4
   if (fresh) A.used[pos] = (uint32_t)slot;
 }
 
-// Workgroup-aggregated append to one global cursor (every thread calls it).
-__device__ __forceinline__ unsigned long long block_append(bool a, unsigned long long* cur, unsigned long long* sh) {
-  const unsigned long long ma = __ballot(a);
+// Workgroup-aggregated append of two streams (a, b) to global cursors: one
+// device atomic per stream per workgroup call.  Every thread of the workgroup
+// must call it (workgroup-uniform control flow).  sh: 4 LDS words.
+__device__ __forceinline__ void block_append2(bool a, bool b, unsigned long long* cur_a, unsigned long long* cur_b,
+                                              unsigned long long* sh, unsigned long long& pos_a,
+                                              unsigned long long& pos_b) {
+  const unsigned long long ma = __ballot(a), mb = __ballot(b);
   const unsigned lane = __lane_id();
-  unsigned long long wa = 0;
-  if (lane == 0 && ma) wa = atomicAdd(&sh[0], (unsigned long long)__popcll(ma));
+  const unsigned long long below = (1ull << lane) - 1ull;
+  unsigned long long wa = 0, wb = 0;
+  if (lane == 0) {
+    if (ma) wa = atomicAdd(&sh[0], (unsigned long long)__popcll(ma));
+    if (mb) wb = atomicAdd(&sh[1], (unsigned long long)__popcll(mb));
+  }
   wa = __shfl(wa, 0);
+  wb = __shfl(wb, 0);
   __syncthreads();
   if (threadIdx.x == 0) {
-    sh[1] = sh[0] ? atomicAdd(cur, sh[0]) : 0ull;
+    sh[2] = sh[0] ? atomicAdd(cur_a, sh[0]) : 0ull;
+    sh[3] = sh[1] ? atomicAdd(cur_b, sh[1]) : 0ull;
     sh[0] = 0;
+    sh[1] = 0;
   }
   __syncthreads();
-  return sh[1] + wa + __popcll(ma & ((1ull << lane) - 1ull));
+  pos_a = sh[2] + wa + __popcll(ma & below);
+  pos_b = sh[3] + wb + __popcll(mb & below);
 }
 
-constexpr int kImgSmallMax = 16000;   // LDS image words that still allow two 1024-thread workgroups per CU
-
-// Pass 1, main stage: classify with the index (staged in LDS when kImg > 0),
-// lines whose index candidate fails verification go to `tail` for k_tail.
-template <int kMode, int kImg>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kImgSmallMax ? 4 : 8, 8))) void k_classify(const uint4* __restrict__ T, const uint32_t* __restrict__ TS,
-                                                   const unsigned long long* __restrict__ ORD, unsigned long long n,
-                                                   const int32_t* __restrict__ gin, int32_t* __restrict__ gout,
-                                                   uint32_t* __restrict__ gtag, Rules R, Agg A, uint32_t* tail,
-                                                   unsigned long long* tail_n) {
+// Pass 1 classification with the index (staged in LDS when kImg > 0).
+// kStage 0: every line; a wave classifies its majority list and defers the
+// other lanes to tailA.  kStage 1: the lines of tailA, all lists of a wave.
+// Lines whose index candidate fails verification go to tailB (k_tail).
+template <int kMode, int kImg, int kStage>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kImgSmallMax ? 4 : 8, 8))) void k_classify(
+    const uint4* __restrict__ T, const uint32_t* __restrict__ TS, const unsigned long long* __restrict__ ORD,
+    unsigned long long n, const int32_t* __restrict__ gin, int32_t* __restrict__ gout, uint32_t* __restrict__ gtag,
+    Rules R, Agg A, uint32_t* tailA, unsigned long long* tailA_n, uint32_t* tailB, unsigned long long* tailB_n) {
   __shared__ uint32_t lds_img[kImg > 0 ? kImg : 1];
-  __shared__ unsigned long long lds_app[2];
-  if (threadIdx.x < 2) lds_app[threadIdx.x] = 0;
+  __shared__ unsigned long long lds_app[4];
+  if (threadIdx.x < 4) lds_app[threadIdx.x] = 0;
   if (kImg > 0 && kMode != kGivenAgg && R.indexed) {
     for (uint32_t w = threadIdx.x; w < R.img_words; w += blockDim.x) lds_img[w] = R.img[w];
   }
   __syncthreads();
+  if (kStage == 1) n = *tailA_n;
   const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
   for (unsigned long long base = (unsigned long long)blockIdx.x * blockDim.x; base < n; base += stride) {
-    const unsigned long long i = base + threadIdx.x;
-    const bool in = i < n;
+    const unsigned long long j = base + threadIdx.x;
+    const bool in = j < n;
+    const unsigned long long i = kStage == 1 ? (in ? tailA[j] : 0u) : j;
     const uint4 t = in ? T[i] : make_uint4(0u, 0u, 0u, 0u);
     const bool valid = in && (((t.w >> 16) & 0xFFu) & RSA_F_VALID);
     uint32_t gid;
@@ -441,16 +478,17 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kIm
       gid = in ? (uint32_t)gin[i] : kNoGid;
     } else {
       if (kImg > 0) {
-        gid = classify_wave<false>(t, valid, R, (const uint32_t*)lds_img, A.flags);
+        gid = classify_wave<false, kStage == 0>(t, valid, R, (const uint32_t*)lds_img, A.flags);
       } else {
-        gid = classify_wave<false>(t, valid, R, R.img, A.flags);
+        gid = classify_wave<false, kStage == 0>(t, valid, R, R.img, A.flags);
       }
-      const bool defer = gid == kDefer;
-      const unsigned long long pos = block_append(defer, tail_n, lds_app);
-      if (defer) {
-        tail[pos] = (uint32_t)i;
-        continue;   // finished by k_tail
-      }
+      const bool to_a = gid == kDeferList;
+      const bool to_b = gid == kDefer;
+      unsigned long long pa, pb;
+      block_append2(to_a, to_b, tailA_n, tailB_n, lds_app, pa, pb);
+      if (to_a) tailA[pa] = (uint32_t)i;
+      if (to_b) tailB[pb] = (uint32_t)i;
+      if (to_a || to_b) continue;   // finished by a later launch
     }
     finish_line<kMode>(in, i, t, gid, TS, ORD, gout, gtag, R.n_rules, A);
   }
@@ -470,7 +508,7 @@ __global__ __launch_bounds__(kBlock) void k_tail(const uint4* __restrict__ T, co
     const unsigned long long i = in ? tail[j] : 0u;
     const uint4 t = in ? T[i] : make_uint4(0u, 0u, 0u, 0u);
     const bool valid = in && (((t.w >> 16) & 0xFFu) & RSA_F_VALID);
-    const uint32_t gid = classify_wave<true>(t, valid, R, R.img, A.flags);
+    const uint32_t gid = classify_wave<true, false>(t, valid, R, R.img, A.flags);
     finish_line<kMode>(in, i, t, gid, TS, ORD, gout, gtag, R.n_rules, A);
   }
 }
@@ -600,9 +638,13 @@ __global__ void k_table_clear(Slot* S, const uint32_t* used, unsigned long long 
 }
 
 // ---- cap resolution (exact): P = cap-th smallest min_order among a rule's entries.
+// Every rule with >= cap entries gets a contiguous segment (allocated by an
+// atomic cursor, so no scan is needed); the entries' min_order keys are
+// scattered into it and one workgroup per rule radix-selects the cap-th
+// smallest key, 8 bits at a time from the top (keys are unique order keys).
 __global__ void k_cap_mark(const unsigned int* distinct, uint32_t n_rules, uint32_t cap, uint32_t* cidx,
-                           uint32_t* capped_gid, uint32_t* capped_cnt, unsigned int* n_capped,
-                           unsigned long long* out) {
+                           uint32_t* capped_gid, uint32_t* capped_start, uint32_t* capped_fill,
+                           unsigned int* n_capped, unsigned long long* total, unsigned long long* out) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= n_rules) return;
   out[g] = RSA_NO_THRESHOLD;
@@ -610,38 +652,146 @@ __global__ void k_cap_mark(const unsigned int* distinct, uint32_t n_rules, uint3
     const unsigned int c = atomicAdd(n_capped, 1u);
     cidx[g] = c;
     capped_gid[c] = g;
-    capped_cnt[c] = distinct[g];
+    capped_start[c] = (uint32_t)atomicAdd(total, (unsigned long long)distinct[g]);
+    capped_fill[c] = 0;
   } else {
     cidx[g] = 0xFFFFFFFFu;
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_cap_collect(const Slot* S, const uint32_t* used, unsigned long long n_used,
-                                                        const uint32_t* cidx, unsigned long long* keys,
-                                                        uint32_t* vals, unsigned long long* cursor) {
+// Scatter the capped rules' min_order keys into their segments.  Lanes of one
+// wave that share a rule take their positions from one atomic (hot rules would
+// otherwise serialise thousands of atomics on one counter).
+__global__ __launch_bounds__(kBlock) void k_cap_scatter(const Slot* S, const uint32_t* used, unsigned long long n_used,
+                                                        const uint32_t* cidx, const uint32_t* capped_start,
+                                                        uint32_t* capped_fill, unsigned long long* keys,
+                                                        unsigned long long max_keys, unsigned int* flags) {
   const unsigned long long stride = (unsigned long long)gridDim.x * kBlock;
   for (unsigned long long base = (unsigned long long)blockIdx.x * kBlock; base < n_used; base += stride) {
     const unsigned long long i = base + threadIdx.x;
     uint32_t c = 0xFFFFFFFFu;
-    unsigned long long o = 0;
+    unsigned long long key = 0;
     if (i < n_used) {
       const Slot* s = &S[used[i]];
       c = cidx[s->kB >> 32];
-      o = s->min_order;
+      key = s->min_order;
     }
     const bool ok = c != 0xFFFFFFFFu;
-    const unsigned long long pos = wave_append(ok, cursor);
+    unsigned long long pending = __ballot(ok);
+    const unsigned lane = __lane_id();
+    unsigned long long pos = 0;
+    while (pending) {
+      const int leader = __builtin_ctzll(pending);
+      const uint32_t k = __builtin_amdgcn_readlane(c, leader);
+      const unsigned long long peers = __ballot(ok && c == k);
+      pending &= ~peers;
+      uint32_t b = 0;
+      if ((int)lane == leader) b = atomicAdd(&capped_fill[k], (uint32_t)__popcll(peers));
+      b = __shfl(b, leader);
+      if (ok && c == k) pos = (unsigned long long)capped_start[k] + b + __popcll(peers & ((1ull << lane) - 1ull));
+    }
     if (ok) {
-      keys[pos] = o;
-      vals[pos] = c;
+      if (pos < max_keys) keys[pos] = key;
+      else atomicOr(&flags[1], 16u);
     }
   }
 }
 
-__global__ void k_cap_pick(const unsigned long long* sorted_orders, const uint32_t* start, const uint32_t* capped_gid,
-                           uint32_t n_capped, uint32_t cap, unsigned long long* out) {
-  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c < n_capped) out[capped_gid[c]] = sorted_orders[(size_t)start[c] + cap - 1];
+// One workgroup per capped rule: the cap-th smallest key of its segment.  A
+// min/max pass bounds the keys; radix select then runs on (key - min) in 8-bit
+// digits from the highest set bit of (max - min) down, so the digits of keys
+// that share their top bits (time-ordered order keys) still spread over the
+// bins.  Per-wave LDS histograms keep bin contention inside a wave.
+constexpr int kSelThreads = 1024;
+__global__ __launch_bounds__(kSelThreads) void k_cap_select(const unsigned long long* keys,
+                                                            const uint32_t* capped_start, const uint32_t* capped_fill,
+                                                            const uint32_t* capped_gid, uint32_t cap,
+                                                            unsigned long long* out) {
+  constexpr int kWaves = kSelThreads / 64;
+  __shared__ uint32_t hist[kWaves][256];
+  __shared__ unsigned long long red_min[kWaves], red_max[kWaves];
+  __shared__ unsigned long long sh_prefix;
+  __shared__ uint32_t sh_k;
+  const uint32_t c = blockIdx.x;
+  const unsigned long long* seg = keys + capped_start[c];
+  const uint32_t n = capped_fill[c];
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // min / max
+  unsigned long long mn = ~0ull, mx = 0;
+  for (uint32_t j = threadIdx.x; j < n; j += kSelThreads) {
+    const unsigned long long k = seg[j];
+    mn = k < mn ? k : mn;
+    mx = k > mx ? k : mx;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long a = __shfl_xor(mn, o), b = __shfl_xor(mx, o);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  if (lane == 0) {
+    red_min[w] = mn;
+    red_max[w] = mx;
+  }
+  if (threadIdx.x == 0) {
+    sh_prefix = 0;
+    sh_k = cap;
+  }
+  __syncthreads();
+  mn = red_min[0];
+  mx = red_max[0];
+  for (int q = 1; q < kWaves; ++q) {
+    mn = red_min[q] < mn ? red_min[q] : mn;
+    mx = red_max[q] > mx ? red_max[q] : mx;
+  }
+  const unsigned long long range = mx - mn;
+  const int top = range ? 63 - __builtin_clzll(range) : 0;     // highest set bit of the range
+  int shift = top >= 8 ? top - 7 : 0;
+  unsigned long long hi_mask = 0;                                // bits above the current digit, fixed so far
+  while (true) {
+    for (int q = threadIdx.x; q < kWaves * 256; q += kSelThreads) (&hist[0][0])[q] = 0;
+    __syncthreads();
+    const unsigned long long prefix = sh_prefix;
+    for (uint32_t j = threadIdx.x; j < n; j += kSelThreads) {
+      const unsigned long long v = seg[j] - mn;
+      if ((v & hi_mask) == prefix) atomicAdd(&hist[w][(v >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      uint32_t hv[4], sum = 0;
+      for (int q = 0; q < 4; ++q) {
+        uint32_t t = 0;
+        for (int ww = 0; ww < kWaves; ++ww) t += hist[ww][4 * lane + q];
+        hv[q] = t;
+        sum += t;
+      }
+      uint32_t incl = sum;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t v = __shfl_up(incl, o);
+        if ((int)lane >= o) incl += v;
+      }
+      const uint32_t excl = incl - sum;
+      const uint32_t k = sh_k;
+      if (k > excl && k <= incl) {
+        uint32_t acc = excl, d = 4 * lane;
+        for (int q = 0; q < 4; ++q) {
+          if (k <= acc + hv[q]) {
+            d = 4 * lane + q;
+            break;
+          }
+          acc += hv[q];
+        }
+        sh_k = k - acc;
+        sh_prefix = prefix | ((unsigned long long)d << shift);
+      }
+    }
+    hi_mask |= 0xFFull << shift;
+    __syncthreads();
+    if (shift == 0) break;
+    // the last digit may overlap bits already fixed: they are equal in every
+    // key still counted, so the selection stays exact
+    shift = shift >= 8 ? shift - 8 : 0;
+  }
+  if (threadIdx.x == 0) out[capped_gid[c]] = sh_prefix + mn;
 }
 
 __device__ __forceinline__ rsa_conn_record make_record(const Slot& s, int which) {
@@ -735,7 +885,7 @@ struct rsa_ctx {
   bool rules_loaded = false;
   // perfect-hash tuple-space index
   rsa_pht_list* d_hdr = nullptr;
-  rsa_pht_shape* d_shapes = nullptr;
+  rsa_pht_group* d_groups = nullptr;
   uint32_t* d_img = nullptr;
   uint32_t img_words = 0;
   rsa_rule_entry* d_resid = nullptr;
@@ -779,11 +929,8 @@ struct rsa_ctx {
   uint32_t* d_capped_cnt = nullptr;
   uint32_t* d_capped_start = nullptr;
   uint32_t cidx_len = 0;
-  unsigned long long* d_keys[2] = {nullptr, nullptr};
-  uint32_t* d_vals[2] = {nullptr, nullptr};
+  unsigned long long* d_keys = nullptr;   // capped rules' min_order keys, one segment per rule
   unsigned long long sort_alloc = 0;
-  void* d_temp = nullptr;
-  size_t temp_alloc = 0;
   // pass-1 kernel timing (HIP events on the ctx stream)
   hipEvent_t ev[32] = {};
   int ev_used = 0;
@@ -815,7 +962,7 @@ Rules rules_of(const rsa_ctx* c) {
   r.n_lists = c->n_lists;
   r.n_rules = c->n_rules;
   r.hdr = (const const_v4u*)(c->d_hdr);
-  r.shapes = (const const_v4u*)(c->d_shapes);
+  r.groups = (const const_v4u*)(c->d_groups);
   r.resid = (const const_v4u*)(c->d_resid);
   r.img = c->d_img;
   r.img_words = c->img_words;
@@ -866,6 +1013,7 @@ int check_flags(rsa_ctx* c) {
   if (f[1] & 2u) return fail(c, RSA_ERR_ARG, "rule id >= n_rules (%u)", c->n_rules);
   if (f[1] & 4u) return fail(c, RSA_ERR_STATE, "pass 2 found an occurrence with no pass-1 entry");
   if (f[1] & 8u) return fail(c, RSA_ERR_STATE, "pass-2 import of a key absent from the table");
+  if (f[1] & 16u) return fail(c, RSA_ERR_STATE, "cap selection: more entries than the table reported");
   return RSA_OK;
 }
 
@@ -881,16 +1029,6 @@ int used_count(rsa_ctx* c, unsigned long long* n) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (*n > c->slot_cap) *n = c->slot_cap;
   c->used_last = *n;
-  return RSA_OK;
-}
-
-int ensure_temp(rsa_ctx* c, size_t bytes) {
-  if (bytes <= c->temp_alloc) return RSA_OK;
-  hipFree(c->d_temp);
-  c->d_temp = nullptr;
-  c->temp_alloc = 0;
-  HIPCHK(c, hipMalloc(&c->d_temp, bytes));
-  c->temp_alloc = bytes;
   return RSA_OK;
 }
 
@@ -931,7 +1069,8 @@ int cap_select(rsa_ctx* c, unsigned long long* out, uint32_t* h_n_capped) {
   HIPCHK(c, hipMemsetAsync(d_ncap, 0, sizeof(unsigned int), c->stream));
   HIPCHK(c, hipMemsetAsync(c->d_cursor, 0, sizeof(unsigned long long), c->stream));
   k_cap_mark<<<(nr + kBlock - 1) / kBlock, kBlock, 0, c->stream>>>(c->d_distinct, nr, c->cap, c->d_cidx,
-                                                                   c->d_capped_gid, c->d_capped_cnt, d_ncap, out);
+                                                                   c->d_capped_gid, c->d_capped_start,
+                                                                   c->d_capped_cnt, d_ncap, c->d_cursor, out);
   HIPCHK(c, hipGetLastError());
   unsigned int ncap = 0;
   HIPCHK(c, hipMemcpyAsync(&ncap, d_ncap, sizeof ncap, hipMemcpyDeviceToHost, c->stream));
@@ -941,51 +1080,25 @@ int cap_select(rsa_ctx* c, unsigned long long* out, uint32_t* h_n_capped) {
   *h_n_capped = ncap;
   if (ncap == 0) return RSA_OK;
   if (c->sort_alloc < n_used) {
-    for (int k = 0; k < 2; ++k) {
-      hipFree(c->d_keys[k]);
-      hipFree(c->d_vals[k]);
-      c->d_keys[k] = nullptr;
-      c->d_vals[k] = nullptr;
-    }
+    hipFree(c->d_keys);
+    c->d_keys = nullptr;
     c->sort_alloc = 0;
     const unsigned long long want = n_used + n_used / 4 + 1024;
-    for (int k = 0; k < 2; ++k) {
-      HIPCHK(c, hipMalloc(&c->d_keys[k], want * sizeof(unsigned long long)));
-      HIPCHK(c, hipMalloc(&c->d_vals[k], want * sizeof(uint32_t)));
-    }
+    HIPCHK(c, hipMalloc(&c->d_keys, want * sizeof(unsigned long long)));
     c->sort_alloc = want;
   }
-  k_cap_collect<<<grid_for(c, n_used, 8), kBlock, 0, c->stream>>>(c->d_slots, c->d_used, n_used, c->d_cidx,
-                                                                  c->d_keys[0], c->d_vals[0], c->d_cursor);
+  k_cap_scatter<<<grid_for(c, n_used, 8), kBlock, 0, c->stream>>>(c->d_slots, c->d_used, n_used, c->d_cidx,
+                                                                  c->d_capped_start, c->d_capped_cnt, c->d_keys,
+                                                                  c->sort_alloc, c->d_flags);
   HIPCHK(c, hipGetLastError());
-  unsigned long long m = 0;
-  HIPCHK(c, hipMemcpyAsync(&m, c->d_cursor, sizeof m, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  if (m > 0x7FFFFFFFull) return fail(c, RSA_ERR_CAPACITY, "more than 2^31 capped entries");
-  int cbits = 1;
-  while (cbits < 32 && (1ull << cbits) < ncap) ++cbits;
-  // sort by min_order, then stably by capped index; exclusive scan of segment sizes
-  hipcub::DoubleBuffer<unsigned long long> keys(c->d_keys[0], c->d_keys[1]);
-  hipcub::DoubleBuffer<uint32_t> vals(c->d_vals[0], c->d_vals[1]);
-  size_t t1 = 0, t2 = 0, t3 = 0;
-  HIPCHK(c, hipcub::DeviceRadixSort::SortPairs(nullptr, t1, keys, vals, (int)m, 0, 64, c->stream));
-  HIPCHK(c, hipcub::DeviceRadixSort::SortPairs(nullptr, t2, vals, keys, (int)m, 0, cbits, c->stream));
-  HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, t3, c->d_capped_cnt, c->d_capped_start, (int)ncap, c->stream));
-  size_t tb = t1 > t2 ? t1 : t2;
-  if (t3 > tb) tb = t3;
-  rc = ensure_temp(c, tb);
-  if (rc) return rc;
-  HIPCHK(c, hipcub::DeviceRadixSort::SortPairs(c->d_temp, tb, keys, vals, (int)m, 0, 64, c->stream));
-  HIPCHK(c, hipcub::DeviceRadixSort::SortPairs(c->d_temp, tb, vals, keys, (int)m, 0, cbits, c->stream));
-  HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(c->d_temp, tb, c->d_capped_cnt, c->d_capped_start, (int)ncap,
-                                             c->stream));
-  k_cap_pick<<<(ncap + kBlock - 1) / kBlock, kBlock, 0, c->stream>>>(keys.Current(), c->d_capped_start,
-                                                                     c->d_capped_gid, ncap, c->cap, out);
+  k_cap_select<<<ncap, kSelThreads, 0, c->stream>>>(c->d_keys, c->d_capped_start, c->d_capped_cnt, c->d_capped_gid,
+                                                    c->cap, out);
   HIPCHK(c, hipGetLastError());
   return RSA_OK;
 }
 
-// Deferred-line region of `tail_alloc` entries and its counter.
+// Two deferred-line regions of `tail_alloc` entries each (list-deferred and
+// verification-deferred lines) and their counters.
 int ensure_tail(rsa_ctx* c, unsigned long long n) {
   if (!c->d_tail_n) HIPCHK(c, hipMalloc(&c->d_tail_n, 2 * sizeof(unsigned long long)));
   if (n <= c->tail_alloc) return RSA_OK;
@@ -993,7 +1106,7 @@ int ensure_tail(rsa_ctx* c, unsigned long long n) {
   hipFree(c->d_tail);
   c->d_tail = nullptr;
   c->tail_alloc = 0;
-  HIPCHK(c, hipMalloc(&c->d_tail, n * sizeof(uint32_t)));
+  HIPCHK(c, hipMalloc(&c->d_tail, 2 * n * sizeof(uint32_t)));
   c->tail_alloc = n;
   return RSA_OK;
 }
@@ -1019,10 +1132,24 @@ int ensure_events(rsa_ctx* c) {
 }
 
 // LDS image capacities (32-bit words) of k_classify.
-constexpr int kImgSmall = 16000;   // 62.5 KiB: two 1024-thread workgroups per CU (32 waves)
+constexpr int kImgSmall = kImgSmallMax;   // 62.5 KiB: two 1024-thread workgroups per CU (32 waves)
 constexpr int kImgLarge = 38912;   // 152 KiB: one workgroup per CU
 
-// Main classification launch + exact tail for lines [0, m) of T (already offset).
+template <int kMode, int kImg>
+void launch_stages(rsa_ctx* c, unsigned per_cu, const uint4* t, const uint32_t* ts, const unsigned long long* o,
+                   uint64_t m, const int32_t* gi, int32_t* go, uint32_t* gt, const Rules& r, const Agg& ag) {
+  uint32_t* ta = c->d_tail;
+  uint32_t* tb = c->d_tail + c->tail_alloc;
+  unsigned long long* na = c->d_tail_n;
+  unsigned long long* nb = c->d_tail_n + 1;
+  k_classify<kMode, kImg, 0><<<grid_for_threads(c, m, 1024, per_cu), 1024, 0, c->stream>>>(t, ts, o, m, gi, go, gt,
+                                                                                          r, ag, ta, na, tb, nb);
+  if (kMode != kGivenAgg)   // list-deferred lines (their number is read on the device: no host sync)
+    k_classify<kMode, kImg, 1><<<c->cu_count * per_cu, 1024, 0, c->stream>>>(t, ts, o, m, gi, go, gt, r, ag, ta, na,
+                                                                             tb, nb);
+}
+
+// Classification launches + exact tail for lines [0, m) of T (already offset).
 template <int kMode>
 int launch_classify(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsigned long long* o, uint64_t m,
                     const int32_t* gi, int32_t* go, uint32_t* gt) {
@@ -1030,22 +1157,20 @@ int launch_classify(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsign
   const Agg ag = agg_of(c);
   int rc = ensure_tail(c, m);
   if (rc) return rc;
-  HIPCHK(c, hipMemsetAsync(c->d_tail_n, 0, sizeof(unsigned long long), c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_tail_n, 0, 2 * sizeof(unsigned long long), c->stream));
   const bool lds = kMode != kGivenAgg && c->indexed;
   if (lds && c->img_words <= (uint32_t)kImgSmall) {
-    k_classify<kMode, kImgSmall><<<grid_for_threads(c, m, 1024, 2), 1024, 0, c->stream>>>(
-        t, ts, o, m, gi, go, gt, r, ag, c->d_tail, c->d_tail_n);
+    launch_stages<kMode, kImgSmall>(c, 2, t, ts, o, m, gi, go, gt, r, ag);
   } else if (lds && c->img_words <= (uint32_t)kImgLarge) {
-    k_classify<kMode, kImgLarge><<<grid_for_threads(c, m, 1024, 1), 1024, 0, c->stream>>>(
-        t, ts, o, m, gi, go, gt, r, ag, c->d_tail, c->d_tail_n);
+    launch_stages<kMode, kImgLarge>(c, 1, t, ts, o, m, gi, go, gt, r, ag);
   } else {
-    k_classify<kMode, 0><<<grid_for_threads(c, m, 1024, 2), 1024, 0, c->stream>>>(t, ts, o, m, gi, go, gt, r, ag,
-                                                                                c->d_tail, c->d_tail_n);
+    launch_stages<kMode, 0>(c, 2, t, ts, o, m, gi, go, gt, r, ag);
   }
   HIPCHK(c, hipGetLastError());
   if (kMode != kGivenAgg) {
-    // deferred lines (their number is read on the device: no host sync)
-    k_tail<kMode><<<c->cu_count * 4, kBlock, 0, c->stream>>>(t, ts, o, go, gt, r, ag, c->d_tail, c->d_tail_n);
+    // verification-deferred lines
+    k_tail<kMode><<<c->cu_count * 4, kBlock, 0, c->stream>>>(t, ts, o, go, gt, r, ag, c->d_tail + c->tail_alloc,
+                                                             c->d_tail_n + 1);
     HIPCHK(c, hipGetLastError());
   }
   return RSA_OK;
@@ -1176,11 +1301,10 @@ int rsa_ctx_destroy(rsa_ctx* c) {
   if (!c) return RSA_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->d_tail, c->d_tail_n, c->d_gtag, c->d_gscratch, c->d_entries, c->d_off, c->d_hdr, c->d_shapes,
+  void* bufs[] = {c->d_tail, c->d_tail_n, c->d_gtag, c->d_gscratch, c->d_entries, c->d_off, c->d_hdr, c->d_groups,
                   c->d_img, c->d_resid,
                   c->d_slots, c->d_used, c->d_used_n, c->d_filter, c->d_flags, c->d_cursor, c->d_cidx,
-                  c->d_capped_gid, c->d_capped_cnt, c->d_capped_start, c->d_keys[0], c->d_keys[1], c->d_vals[0],
-                  c->d_vals[1], c->d_temp};
+                  c->d_capped_gid, c->d_capped_cnt, c->d_capped_start, c->d_keys};
   for (void* b : bufs) (void)hipFree(b);
   for (int k = 0; k < kMaxEvents; ++k)
     if (c->ev[k]) (void)hipEventDestroy(c->ev[k]);
@@ -1261,28 +1385,32 @@ int rsa_load_rules(rsa_ctx* c, const rsa_rule_entry* h_entries, uint32_t n_entri
   return RSA_OK;
 }
 
-int rsa_load_index(rsa_ctx* c, const rsa_pht_list* h_lists, const rsa_pht_shape* h_shapes, uint32_t n_shapes,
+int rsa_load_index(rsa_ctx* c, const rsa_pht_list* h_lists, const rsa_pht_group* h_groups, uint32_t n_groups,
                    const uint32_t* h_image, uint32_t image_words, const rsa_rule_entry* h_resid, uint32_t n_resid) {
-  if (!c || !h_lists || (n_shapes && !h_shapes) || (image_words && !h_image) || (n_resid && !h_resid))
+  if (!c || !h_lists || (n_groups && !h_groups) || !h_image || (n_resid && !h_resid))
     return fail(c, RSA_ERR_ARG, "null argument");
   if (!c->rules_loaded) return fail(c, RSA_ERR_STATE, "load the candidate lists first");
+  if (image_words == 0 || h_image[0] != 0xFFFFFFFFu) return fail(c, RSA_ERR_ARG, "image word 0 must be an empty slot");
   const uint32_t nl = c->n_lists;
   // validate everything the kernels index with, so no launch can read out of bounds
   for (uint32_t l = 0; l < nl; ++l) {
     const rsa_pht_list& h = h_lists[l];
     const uint32_t len = c->h_off[l + 1] - c->h_off[l];
-    if (h.shape_beg > h.shape_end || h.shape_end > n_shapes || h.resid_beg > h.resid_end || h.resid_end > n_resid)
-      return fail(c, RSA_ERR_ARG, "list %u: shape/residual range out of bounds", l);
+    if (h.group_beg > h.group_end || h.group_end > n_groups || h.resid_beg > h.resid_end || h.resid_end > n_resid)
+      return fail(c, RSA_ERR_ARG, "list %u: group/residual range out of bounds", l);
     if (h.prefix > len) return fail(c, RSA_ERR_ARG, "list %u: prefix %u > list length %u", l, h.prefix, len);
-    if (h.shape_beg < h.shape_end && len > 0xFFFEu) return fail(c, RSA_ERR_ARG, "list %u: indexed list too long", l);
-    for (uint32_t s = h.shape_beg; s < h.shape_end; ++s) {
-      const rsa_pht_shape& sh = h_shapes[s];
-      if (sh.n_slots == 0 || (uint64_t)sh.slot_off + sh.n_slots > image_words ||
-          (sh.disp_mask & (sh.disp_mask + 1)) != 0 || ((uint64_t)sh.disp_off + sh.disp_mask + 1) > 2ull * image_words)
-        return fail(c, RSA_ERR_ARG, "shape %u: table outside the image", s);
-      for (uint32_t k = 0; k < sh.n_slots; ++k) {
-        const uint32_t w = h_image[sh.slot_off + k];
-        if (w != 0xFFFFFFFFu && (w & 0xFFFFu) >= len) return fail(c, RSA_ERR_ARG, "shape %u: slot index out of list", s);
+    if (h.group_beg < h.group_end && len > 0xFFFEu) return fail(c, RSA_ERR_ARG, "list %u: indexed list too long", l);
+    for (uint32_t g = h.group_beg; g < h.group_end; ++g) {
+      for (int k = 0; k < 4; ++k) {
+        const rsa_pht_table& tb = h_groups[g].table[k];
+        if (tb.n_slots == 0 || (uint64_t)tb.slot_off + tb.n_slots > image_words ||
+            (tb.disp_mask & (tb.disp_mask + 1)) != 0 || ((uint64_t)tb.disp_off + tb.disp_mask + 1) > 2ull * image_words)
+          return fail(c, RSA_ERR_ARG, "group %u class %d: table outside the image", g, k);
+        for (uint32_t q = 0; q < tb.n_slots; ++q) {
+          const uint32_t w = h_image[tb.slot_off + q];
+          if (w != 0xFFFFFFFFu && (w & 0xFFFFu) >= len)
+            return fail(c, RSA_ERR_ARG, "group %u class %d: slot index out of list", g, k);
+        }
       }
     }
     for (uint32_t e = h.resid_beg; e < h.resid_end; ++e) {
@@ -1294,7 +1422,7 @@ int rsa_load_index(rsa_ctx* c, const rsa_pht_list* h_lists, const rsa_pht_shape*
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   int rc = upload(c, &c->d_hdr, h_lists, nl);
-  if (!rc) rc = upload(c, &c->d_shapes, h_shapes, n_shapes);
+  if (!rc) rc = upload(c, &c->d_groups, h_groups, n_groups);
   if (!rc) rc = upload(c, &c->d_img, h_image, image_words);
   if (!rc) rc = upload(c, &c->d_resid, h_resid, n_resid);
   if (rc) return rc;

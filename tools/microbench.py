@@ -61,7 +61,7 @@ def main():
            'distinct': size}
     res['classify_only_ms'] = timed(lambda: eng.classify_only(batch, g), args.reps)
     from ruleset_analysis_amd import native
-    for pre in (0, 16, 256):
+    for pre in (0, 32, 256):
         eng.load_compiled(compiled, prefix=pre)
         res['classify_prefix%d_ms' % pre] = timed(lambda: eng.classify_only(batch, g), args.reps)
     eng.load_compiled(compiled)
