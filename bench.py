@@ -76,6 +76,7 @@ def build_shard(dbj, info, compiled, n, rank, seed, zipf, device, chunk=8_000_00
         tuples[a:a + m].copy_(torch.from_numpy(tup.view(np.int32).reshape(-1, 4)))
         ts[a:a + m].copy_(torch.from_numpy(t.view(np.int32)))
         order[a:a + m].copy_(torch.from_numpy(o.view(np.int64)))
+        log('shard: %d / %d lines generated' % (a + m, n))
     return DeviceBatch(tuples, ts, order), n_hb
 
 

@@ -61,24 +61,35 @@ typedef struct rsa_rule_entry {
   uint32_t reserved;
 } rsa_rule_entry;
 
-/* Perfect-hash tuple-space index (optional; compile.py build_index).  Per
- * candidate list: entries [0, prefix) are scanned linearly; entries >= prefix
+/* Pruned perfect-hash tuple-space index (optional; compile.py build_index).
+ * Per candidate list: entries [0, prefix) are scanned linearly; entries >= prefix
  * whose addresses are prefixes and whose ports are "any" or one value are
- * grouped by (src mask, dst mask) and, inside a group, by port class
- * c = 0..3 with port mask {0, 0xFFFF0000 (dport), 0x0000FFFF (sport),
- * 0xFFFFFFFF}.  Each (group, class) owns a CHD (hash-and-displace)
- * perfect-hash table over the masked key (src & src_mask, dst & dst_mask,
- * ports & port_mask), ports = sport | dport << 16:
+ * grouped by (src mask, dst mask) (<= 64 groups per list, ascending smallest
+ * entry index) and, inside a group, by port class c = 0..3 with port mask
+ * {0, 0xFFFF0000 (dport), 0x0000FFFF (sport), 0xFFFFFFFF}.  Each (group, class)
+ * owns a CHD (hash-and-displace) perfect-hash table over the masked key
+ * (src & src_mask, dst & dst_mask, ports & port_mask), ports = sport | dport << 16:
  *   H    = fmix32(ks ^ 0x9E3779B9) ^ fmix32(kd ^ 0x7F4A7C15) ^ fmix32(kp ^ 0x2545F491)
  *   d    = disp[disp_off + ((H >> 16) & disp_mask)]            (uint16 units of the image)
  *   slot = hi32((H + ((d * ((H >> 16) | 1)) << 16)) * n_slots)  (32-bit wrap)
  *   word = image[slot_off + slot] = (H & 0xFFFF) << 16 | list-local entry index,
  *          0xFFFFFFFF = empty (image word 0 is always empty: absent classes
  *          point there with n_slots = 1)
- * and holds the smallest entry index with that key.  All other entries are
- * residual (a gid-ascending list scanned linearly).  The answer is identical to
- * the linear scan: the minimum matching gid (the device verifies the hashed
- * candidate against the full entry). */
+ * holding the smallest entry index with that key.  Pruning: per non-zero src
+ * (dst) mask of a list, a CHD table over H = fmix32((src & mask) ^ 0x9E3779B9)
+ * (dst: ^ 0x7F4A7C15) whose word value indexes a uint64 bitmap of the groups
+ * holding a rule on that prefix; groups with mask 0 are in src_any (dst_any).
+ * A tuple probes only the groups in (src bitmap & dst bitmap).  All other
+ * entries are residual (a gid-ascending list scanned linearly).  The answer is
+ * identical to the linear scan: the minimum matching gid (the device verifies
+ * the hashed candidate against the full entry).
+ *
+ * Everything lives in ONE uint32 image: word 0 = 0xFFFFFFFF, word 1 =
+ * RSA_PHT_MAGIC, word 2 = n_lists, word 3 = list_off (word offset of n_lists
+ * rsa_pht_list records); records sit at 4-word aligned offsets, bitmaps at
+ * even offsets (low word first). */
+#define RSA_PHT_MAGIC 0x33415352u
+
 typedef struct rsa_pht_table {
   uint32_t slot_off;   /* first slot word in the image                           */
   uint32_t disp_off;   /* first displacement, in uint16 units of the image       */
@@ -86,25 +97,37 @@ typedef struct rsa_pht_table {
   uint32_t disp_mask;  /* displacement buckets - 1 (power of two)                */
 } rsa_pht_table;
 
-typedef struct rsa_pht_group {
+typedef struct rsa_pht_group {   /* 80 B */
   uint32_t src_mask, dst_mask;
   uint32_t min_idx;          /* smallest list-local entry index in the group      */
   uint32_t n_real;           /* classes with a real table                         */
   rsa_pht_table table[4];    /* port classes any, dport, sport, sport+dport       */
 } rsa_pht_group;
 
-typedef struct rsa_pht_list {
-  uint32_t group_beg, group_end; /* this list's groups (sorted by src mask)       */
+typedef struct rsa_pht_mask {    /* 32 B: one pruning table */
+  uint32_t mask;             /* address mask (non-zero)                           */
+  uint32_t side;             /* 0: src, 1: dst                                    */
+  uint32_t reserved[2];
+  rsa_pht_table table;       /* word value = bitmap index                         */
+} rsa_pht_mask;
+
+typedef struct rsa_pht_list {    /* 64 B */
+  uint32_t group_off, n_groups;  /* rsa_pht_group records (image word offset)     */
+  uint32_t mask_off, n_masks;    /* rsa_pht_mask records                          */
   uint32_t resid_beg, resid_end; /* this list's residual entries                 */
   uint32_t prefix;               /* entries scanned linearly before the index    */
-  uint32_t reserved[3];
+  uint32_t bm_off;               /* uint64 bitmaps (image word offset, even)     */
+  uint32_t src_any_lo, src_any_hi, dst_any_lo, dst_any_hi;
+  uint32_t entry_beg, entry_len; /* the list in rsa_load_rules' entries          */
+  uint32_t n_bitmaps;
+  uint32_t reserved;
 } rsa_pht_list;
 
 /* Options (rsa_set_option). */
 #define RSA_OPT_AUTO_FILTER 1 /* split a large first batch to derive the exact per-rule insert filter (default 1) */
 #define RSA_OPT_USE_INDEX 2   /* classify with the loaded index (1) or the linear lists (0)                  */
 #define RSA_OPT_FILTER_SLICE 5 /* auto filter: first 1/N (>= 1M lines) of a large batch builds the bound (default 256)       */
-#define RSA_OPT_FILTER_STEPS 7 /* auto filter: bound refinements, each after 4x the previous lines (default 1)  */
+#define RSA_OPT_FILTER_STEPS 7 /* auto filter: bound refinements, each after 4x the previous lines (default 3)  */
 #define RSA_OPT_FORCE_DEFER 8  /* TESTING: every index candidate goes to the exact deferred-line path        */
 #define RSA_OPT_PROFILE_SKIP 3 /* PROFILING ONLY, results invalid: bit0 skips counters, bit1 skips the table  */
 
@@ -141,11 +164,12 @@ int rsa_version(void);
 int rsa_load_rules(rsa_ctx *ctx, const rsa_rule_entry *h_entries, uint32_t n_entries,
                    const uint32_t *h_list_offsets, uint32_t n_lists, uint32_t n_rules);
 
-/* Upload a perfect-hash tuple-space index over the lists of rsa_load_rules
- * (h_lists has n_lists entries, same list ids).  Enables RSA_OPT_USE_INDEX.
- * Every offset and slot is validated against the loaded lists. */
-int rsa_load_index(rsa_ctx *ctx, const rsa_pht_list *h_lists, const rsa_pht_group *h_groups, uint32_t n_groups,
-                   const uint32_t *h_image, uint32_t image_words, const rsa_rule_entry *h_resid, uint32_t n_resid);
+/* Upload a pruned perfect-hash tuple-space index image over the lists of
+ * rsa_load_rules (same list ids) and its residual entries.  Enables
+ * RSA_OPT_USE_INDEX.  Every record, offset, table and slot value is validated
+ * against the image and the loaded lists, so no kernel can read out of bounds. */
+int rsa_load_index(rsa_ctx *ctx, const uint32_t *h_image, uint32_t image_words, const rsa_rule_entry *h_resid,
+                   uint32_t n_resid);
 
 /* Bind caller-owned device counters, each n_rules long (n_rules from
  * rsa_load_rules, or rsa_set_rule_count when no rules are loaded):

@@ -165,7 +165,7 @@ class CompiledRules(object):
     def n_lists(self):
         return len(self._lists)
 
-    def index(self, prefix=32):
+    def index(self, prefix=0):
         """Perfect-hash tuple-space index of the current lists (cached until a list is added)."""
         ent, off = self.packed()
         if getattr(self, '_index', None) is None or self._index[0] is not self._packed or self._index[1] != prefix:
@@ -183,31 +183,43 @@ class CompiledRules(object):
                     pass
 
 
-# ---- perfect-hash tuple-space index (LDS-resident on the GPU) ----------------------
+# ---- pruned perfect-hash tuple-space index (LDS-resident on the GPU) -----------------
 #
 # Per candidate list: entries [0, prefix) are scanned linearly (early exit —
-# short first matches never touch the index); entries >= prefix whose address
+# short first matches never touch the index).  Entries >= prefix whose address
 # ranges are prefixes and whose ports are "any" or one value are grouped by
-# shape (src mask, dst mask, port mask).  Each shape owns a CHD perfect-hash
-# table (hash-and-displace): key (src & smask, dst & dmask, ports & pmask) ->
-# one 32-bit slot word (tag16 << 16 | list-local entry index16, tag = low half of
-# the key hash) holding the
-# smallest entry index with that key.  Everything else (odd ranges, keys whose
-# 32-bit hash collides inside a shape, lists of >= 65535 entries) is residual,
-# scanned linearly.  A query takes the minimum candidate index over all shapes;
-# the GPU verifies it against the full entry (a 16-bit tag can collide) and
-# defers the line to an exact scan when it fails.  First match = min gid, so
-# the answer is the linear scan's.
-PHT_GROUP_DTYPE = np.dtype([('src_mask', '<u4'), ('dst_mask', '<u4'), ('min_idx', '<u4'), ('n_real', '<u4')] +
-                           [(f, '<u4') for c in range(4) for f in ('slot_off%d' % c, 'disp_off%d' % c,
-                                                                      'n_slots%d' % c, 'disp_mask%d' % c)])
-PHT_LIST_DTYPE = np.dtype([('group_beg', '<u4'), ('group_end', '<u4'), ('resid_beg', '<u4'), ('resid_end', '<u4'),
-                           ('prefix', '<u4'), ('reserved0', '<u4'), ('reserved1', '<u4'), ('reserved2', '<u4')])
-assert PHT_GROUP_DTYPE.itemsize == 80 and PHT_LIST_DTYPE.itemsize == 32
+# (src mask, dst mask); inside a group, by port class (PORT_CLASSES).  Each
+# (group, class) owns a CHD perfect-hash table (hash-and-displace): key
+# (src & smask, dst & dmask, ports & pmask) -> one 32-bit slot word
+# (tag16 << 16 | list-local entry index16, tag = low half of the key hash)
+# holding the smallest entry index with that key.  Groups are sorted by their
+# smallest entry index and at most PHT_MAX_GROUPS are indexed per list.
+#
+# Pruning: per distinct non-zero src mask m of a list, a CHD table maps the
+# prefix (src & m) to a bitmap of the groups with src mask m that hold a rule
+# on that prefix (groups with src mask 0 are always candidates); likewise for
+# dst masks.  A lane probes only the groups in (src bitmap & dst bitmap), in
+# ascending min-index order, and stops at the first group whose smallest index
+# cannot beat its best candidate.  A 16-bit tag can collide, so the GPU
+# verifies the minimum candidate against the full entry; on a failure it
+# repeats the probes above that candidate (a false bitmap bit only costs a
+# probe).  Everything else (odd ranges, keys whose 32-bit hash collides inside
+# a table, groups past the limit, lists of >= 65535 entries) is residual,
+# scanned linearly.  First match = min gid, so the answer is the linear scan's.
+#
+# Everything lives in ONE uint32 image (include/ruleset_hip.h, rsa_load_index):
+#   [0] 0xFFFFFFFF (the empty slot)  [1] PHT_MAGIC  [2] n_lists  [3] list_off
+#   list records (PHT_LIST_WORDS each), group records, mask records, bitmaps
+#   (uint64, lo word first), CHD displacements (uint16) and slot words.
+PHT_MAGIC = 0x33415352              # 'RSA3'
+PHT_LIST_WORDS, PHT_GROUP_WORDS, PHT_MASK_WORDS = 16, 20, 8
+PHT_MAX_GROUPS = 64
+PHT_ATTEMPTS = 4                    # verification failures before a line is deferred
 # the four port classes of a group, probe order: key ports & mask
 PORT_CLASSES = (0x00000000, 0xFFFF0000, 0x0000FFFF, 0xFFFFFFFF)    # any, dport, sport, both
 M32 = 0xFFFFFFFF
 PHT_EMPTY = 0xFFFFFFFF
+PHT_NONE = 0xFFFF
 PHT_MAX_IDX = 0xFFFE
 SALT_S, SALT_D, SALT_P = 0x9E3779B9, 0x7F4A7C15, 0x2545F491
 
@@ -225,9 +237,14 @@ def fmix32(x):
 
 
 def pht_hash(ks, kd, kp):
-    """H of masked keys (csrc: pht_hash)."""
+    """H of a group key (csrc: index_candidate)."""
     return fmix32(np.asarray(ks, np.uint32) ^ np.uint32(SALT_S)) ^ fmix32(np.asarray(kd, np.uint32) ^ np.uint32(SALT_D)) \
         ^ fmix32(np.asarray(kp, np.uint32) ^ np.uint32(SALT_P))
+
+
+def field_hash(k, side):
+    """H of a pruning key: one address field (side 0 src, 1 dst)."""
+    return fmix32(np.asarray(k, np.uint32) ^ np.uint32(SALT_D if side else SALT_S))
 
 
 def pht_slot(H, d, n_slots):
@@ -303,102 +320,210 @@ def _chd(H, load=0.9, trials=4096):
         m += m // 8 + 1
 
 
-def build_index(ent, off, prefix=64, min_entries=96):
-    """Perfect-hash tuple-space index over packed lists (rsa_load_index arrays).
+class _Image(object):
+    """Append-only uint32 image; chunks stay mutable until build()."""
 
-    Returns (lists PHT_LIST_DTYPE[n_lists], groups PHT_GROUP_DTYPE[], image
-    uint32[], resid RULE_DTYPE[]).  A group = one (src mask, dst mask) pair of a
-    list with a table per port class (PORT_CLASSES; an absent class points at
-    image word 0, an always-empty one-slot table).  A list shorter than
-    ``min_entries`` (or of >= 65535 entries) gets no groups: everything after
-    its prefix is residual."""
+    def __init__(self):
+        self.chunks = [np.array([PHT_EMPTY, PHT_MAGIC, 0, 0], dtype=np.uint32)]
+        self.n = 4
+
+    def alloc(self, arr, align=1):
+        pad = (-self.n) % align
+        if pad:
+            self.chunks.append(np.zeros(pad, dtype=np.uint32))
+            self.n += pad
+        arr = np.ascontiguousarray(arr, dtype=np.uint32)
+        off = self.n
+        self.chunks.append(arr)
+        self.n += len(arr)
+        return off, arr
+
+    def table(self, H, vals):
+        """CHD table of distinct hashes H -> 16-bit values; returns (slot_off, disp_off, n_slots, disp_mask)."""
+        nslots, dmask, disp, slot_of = _chd(H)
+        dwords = np.zeros(((dmask + 2) // 2) * 2, dtype=np.uint16)
+        dwords[:dmask + 1] = disp
+        doff, _ = self.alloc(dwords.view(np.uint32))
+        slots = np.full(nslots, PHT_EMPTY, dtype=np.uint32)
+        slots[slot_of] = ((H.astype(np.uint32) & np.uint32(0xFFFF)) << np.uint32(16)) | np.asarray(vals, np.uint32)
+        soff, _ = self.alloc(slots)
+        return (soff, 2 * doff, nslots, dmask)
+
+    def build(self):
+        return np.concatenate(self.chunks)
+
+
+def _list_shapes(e, pre):
+    """{(sm, dm, pm): {key: min index}}, {(sm, dm, pm): [all indices]}, residual indices."""
+    shapes, members, resid = {}, {}, []
+    for k in range(pre, len(e)):
+        x = e[k]
+        sm = _prefix_mask(x['src_lo'], x['src_span'])
+        dm = _prefix_mask(x['dst_lo'], x['dst_span'])
+        pl, ps = int(x['port_lo']), int(x['port_span'])
+        spm = _port_mask(pl & 0xFFFF, ps & 0xFFFF)
+        dpm = _port_mask(pl >> 16, ps >> 16)
+        if sm is None or dm is None or spm is None or dpm is None:
+            resid.append(k)
+            continue
+        pm = spm | (dpm << 16)
+        key = (int(x['src_lo']), int(x['dst_lo']), pl & pm)
+        g = shapes.setdefault((sm, dm, pm), {})
+        if key not in g:                 # entries are gid-ascending: first = min index
+            g[key] = k
+        members.setdefault((sm, dm, pm), []).append(k)
+    return shapes, members, resid
+
+
+def build_index(ent, off, prefix=0, min_entries=96, max_groups=PHT_MAX_GROUPS):
+    """Pruned perfect-hash tuple-space index over packed lists.
+
+    Returns (image uint32[], resid RULE_DTYPE[]) — the rsa_load_index
+    arguments.  A list shorter than ``min_entries`` (or of >= 65535 entries)
+    gets no groups: everything after its prefix is residual."""
     n_lists = len(off) - 1
-    lists = np.zeros(n_lists, dtype=PHT_LIST_DTYPE)
-    groups_out, image, resid_parts = [], [np.array([PHT_EMPTY], np.uint32)], []
-    n_img = 1
-    n_resid = 0
+    img = _Image()
+    list_off, lrec = img.alloc(np.zeros(PHT_LIST_WORDS * n_lists, dtype=np.uint32), align=4)
+    img.chunks[0][2] = n_lists
+    img.chunks[0][3] = list_off
+    resid_parts, n_resid = [], 0
     for L in range(n_lists):
         e = ent[off[L]:off[L + 1]]
         ne = len(e)
         pre = min(prefix, ne)
-        lists[L]['prefix'] = pre
-        lists[L]['group_beg'] = len(groups_out)
-        shapes = {}
+        rec = lrec[PHT_LIST_WORDS * L: PHT_LIST_WORDS * (L + 1)]
+        rec[6] = pre
+        rec[12] = int(off[L])
+        rec[13] = ne
         resid_idx = []
-        indexable = ne >= min_entries and ne <= PHT_MAX_IDX
-        for k in range(pre, ne):
-            x = e[k]
-            if not indexable:
-                resid_idx.append(k)
-                continue
-            sm = _prefix_mask(x['src_lo'], x['src_span'])
-            dm = _prefix_mask(x['dst_lo'], x['dst_span'])
-            pl, ps = int(x['port_lo']), int(x['port_span'])
-            spm = _port_mask(pl & 0xFFFF, ps & 0xFFFF)
-            dpm = _port_mask(pl >> 16, ps >> 16)
-            if sm is None or dm is None or spm is None or dpm is None:
-                resid_idx.append(k)
-                continue
-            pm = spm | (dpm << 16)
-            key = (int(x['src_lo']), int(x['dst_lo']), pl & pm)
-            g = shapes.setdefault((sm, dm, pm), {})
-            if key not in g:                 # entries are gid-ascending: first = min index
-                g[key] = k
-        by_sd = {}
-        for (sm, dm, pm) in shapes:
-            by_sd.setdefault((sm, dm), {})[pm] = shapes[(sm, dm, pm)]
-        for (sm, dm) in sorted(by_sd):
-            rec = [sm, dm, 0xFFFFFFFF, 0]
-            for pm in PORT_CLASSES:
-                keys = by_sd[(sm, dm)].get(pm)
-                if not keys:
-                    rec += [0, 0, 1, 0]          # dummy: image word 0 is an empty slot
-                    continue
-                ks = np.array(list(keys.keys()), dtype=np.uint64).astype(np.uint32).reshape(-1, 3)
-                idx = np.array(list(keys.values()), dtype=np.int64)
-                H = pht_hash(ks[:, 0], ks[:, 1], ks[:, 2])
-                # a full 32-bit hash collision between two keys of one shape: keep the
-                # smaller index in the table, the other goes residual (still exact)
-                o = np.lexsort((idx, H))
-                H, idx = H[o], idx[o]
-                dup = np.zeros(len(H), dtype=bool)
-                dup[1:] = H[1:] == H[:-1]
-                resid_idx.extend(idx[dup].tolist())
-                H, idx = H[~dup], idx[~dup]
-                nslots, dmask, disp, slot_of = _chd(H)
-                nwords_disp = (dmask + 2) // 2
-                disp_off = 2 * n_img                               # in uint16 units
-                dwords = np.zeros(nwords_disp * 2, dtype=np.uint16)
-                dwords[:dmask + 1] = disp
-                image.append(dwords.view(np.uint32))
-                n_img += nwords_disp
-                slots = np.full(nslots, PHT_EMPTY, dtype=np.uint32)
-                slots[slot_of] = ((H & np.uint32(0xFFFF)).astype(np.uint32) << np.uint32(16)) | idx.astype(np.uint32)
-                rec += [n_img, disp_off, nslots, dmask]
-                rec[2] = min(rec[2], int(idx.min()))
-                rec[3] += 1
-                image.append(slots)
-                n_img += nslots
-            groups_out.append(tuple(rec))
-        lists[L]['group_end'] = len(groups_out)
-        resid_idx = sorted(resid_idx)
-        lists[L]['resid_beg'] = n_resid
+        groups = []
+        if ne >= min_entries and ne <= PHT_MAX_IDX:
+            shapes, members, resid_idx = _list_shapes(e, pre)
+            by_sd = {}
+            for (sm, dm, pm), keys in shapes.items():
+                by_sd.setdefault((sm, dm), {})[pm] = keys
+            ranked = sorted(by_sd.items(), key=lambda kv: (min(min(k.values()) for k in kv[1].values()), kv[0]))
+            for (sm, dm), tabs in ranked[max_groups:]:
+                for pm in tabs:
+                    resid_idx.extend(members[(sm, dm, pm)])
+            groups = ranked[:max_groups]
+        else:
+            resid_idx = list(range(pre, ne))
+        if groups:
+            goff, grec = img.alloc(np.zeros(PHT_GROUP_WORDS * len(groups), dtype=np.uint32), align=4)
+            src_sets, dst_sets = [], []
+            src_any = dst_any = 0
+            for j, ((sm, dm), tabs) in enumerate(groups):
+                g = grec[PHT_GROUP_WORDS * j: PHT_GROUP_WORDS * (j + 1)]
+                g[0], g[1] = sm, dm
+                mins, real = [], 0
+                ss, ds = set(), set()
+                for c, pm in enumerate(PORT_CLASSES):
+                    keys = tabs.get(pm)
+                    if not keys:
+                        g[4 + 4 * c: 8 + 4 * c] = (0, 0, 1, 0)    # image word 0: always empty
+                        continue
+                    ks = np.array(list(keys.keys()), dtype=np.uint64).astype(np.uint32).reshape(-1, 3)
+                    idx = np.array(list(keys.values()), dtype=np.int64)
+                    ss.update(ks[:, 0].tolist())
+                    ds.update(ks[:, 1].tolist())
+                    H = pht_hash(ks[:, 0], ks[:, 1], ks[:, 2])
+                    # a full 32-bit hash collision between two keys of one table: keep the
+                    # smaller index in the table, the other goes residual (still exact)
+                    o = np.lexsort((idx, H))
+                    H, idx = H[o], idx[o]
+                    dup = np.zeros(len(H), dtype=bool)
+                    dup[1:] = H[1:] == H[:-1]
+                    resid_idx.extend(idx[dup].tolist())
+                    H, idx = H[~dup], idx[~dup]
+                    g[4 + 4 * c: 8 + 4 * c] = img.table(H, idx)
+                    mins.append(int(idx.min()))
+                    real += 1
+                g[2] = min(mins)
+                g[3] = real
+                src_sets.append(ss)
+                dst_sets.append(ds)
+                if sm == 0:
+                    src_any |= 1 << j
+                if dm == 0:
+                    dst_any |= 1 << j
+            # pruning tables: per non-zero mask of each side, prefix -> group bitmap
+            tables = []
+            for side, sets in ((0, src_sets), (1, dst_sets)):
+                by_mask = {}
+                for j, ((sm, dm), _tabs) in enumerate(groups):
+                    m = dm if side else sm
+                    if m == 0:
+                        continue
+                    bm = by_mask.setdefault(m, {})
+                    for k in sets[j]:
+                        bm[k] = bm.get(k, 0) | (1 << j)
+                for m in sorted(by_mask):
+                    keys = np.array(sorted(by_mask[m]), dtype=np.uint64).astype(np.uint32)
+                    H = field_hash(keys, side)
+                    merged = {}
+                    for h, k in zip(H.tolist(), keys.tolist()):   # full-hash collision: OR (a superset is safe)
+                        merged[h] = merged.get(h, 0) | by_mask[m][k]
+                    tables.append((m, side, merged))
+            distinct = sorted({b for _m, _s, mg in tables for b in mg.values()})
+            bm_index = {b: i for i, b in enumerate(distinct)}
+            if len(distinct) > PHT_MAX_IDX:
+                raise OverflowError('too many distinct group bitmaps in one list')
+            bm_words = np.zeros(2 * max(len(distinct), 1), dtype=np.uint32)
+            for i, b in enumerate(distinct):
+                bm_words[2 * i] = b & M32
+                bm_words[2 * i + 1] = b >> 32
+            bm_off, _ = img.alloc(bm_words, align=2)
+            moff, mrec = img.alloc(np.zeros(PHT_MASK_WORDS * max(len(tables), 1), dtype=np.uint32), align=4)
+            for q, (m, side, merged) in enumerate(tables):
+                H = np.array(list(merged.keys()), dtype=np.uint32)
+                vals = np.array([bm_index[b] for b in merged.values()], dtype=np.uint32)
+                r = mrec[PHT_MASK_WORDS * q: PHT_MASK_WORDS * (q + 1)]
+                r[0], r[1] = m, side
+                r[4:8] = img.table(H, vals)
+            rec[0:4] = (goff, len(groups), moff, len(tables))
+            rec[7] = bm_off
+            rec[8], rec[9] = src_any & M32, src_any >> 32
+            rec[10], rec[11] = dst_any & M32, dst_any >> 32
+            rec[14] = len(distinct)
+        resid_idx = sorted(set(resid_idx))
+        rec[4] = n_resid
         resid_parts.append(e[resid_idx])
         n_resid += len(resid_idx)
-        lists[L]['resid_end'] = n_resid
-    grp = np.array(groups_out, dtype=PHT_GROUP_DTYPE) if groups_out else np.zeros(0, PHT_GROUP_DTYPE)
-    img = np.concatenate(image)
+        rec[5] = n_resid
+    image = img.build()
     resid = np.concatenate(resid_parts) if resid_parts else np.zeros(0, RULE_DTYPE)
-    return lists, grp, img, resid
+    return image, resid
+
+
+def index_stats(index):
+    """Per list: (prefix, groups, masks, residual entries) — tests and tuning."""
+    image, _resid = index
+    n_lists, lo = int(image[2]), int(image[3])
+    out = []
+    for L in range(n_lists):
+        r = image[lo + PHT_LIST_WORDS * L: lo + PHT_LIST_WORDS * (L + 1)]
+        out.append((int(r[6]), int(r[1]), int(r[3]), int(r[5] - r[4])))
+    return out
+
+
+def _probe(image, H, t):
+    """One CHD probe (csrc: pht_probe): the slot's 16-bit value or PHT_NONE."""
+    slot_off, disp_off, n_slots, disp_mask = (int(v) for v in t)
+    H = int(H)
+    d = int(image.view(np.uint16)[disp_off + ((H >> 16) & disp_mask)])
+    w = int(image[slot_off + int(pht_slot(H, d, n_slots))])
+    return (w & 0xFFFF) if (w >> 16) == (H & 0xFFFF) else PHT_NONE
 
 
 def pht_lookup(index, ent, off, L, src, dst, ports):
     """Host model of the GPU classifier for one tuple (tests): the first-match
     list-local index, -1, or 'defer'.  Follows the device order exactly: prefix
-    scan, min candidate over the groups' port-class probes, verification,
-    residual scan."""
-    lists, grp, img, resid = index
-    h = lists[L]
+    scan, pruning bitmaps, group probes in min-index order with verification
+    and retry above a failed candidate, residual scan."""
+    image, resid = index
+    lo = int(image[3])
+    r = [int(v) for v in image[lo + PHT_LIST_WORDS * L: lo + PHT_LIST_WORDS * (L + 1)]]
     e = ent[off[L]:off[L + 1]]
 
     def match(x):
@@ -407,27 +532,50 @@ def pht_lookup(index, ent, off, L, src, dst, ports):
             ((dst - int(x['dst_lo'])) & M32) <= int(x['dst_span']) and \
             ((ports & 0xFFFF) - (pl & 0xFFFF)) & 0xFFFF <= (ps & 0xFFFF) and \
             ((ports >> 16) - (pl >> 16)) & 0xFFFF <= (ps >> 16)
-    for k in range(int(h['prefix'])):
+    for k in range(r[6]):
         if match(e[k]):
             return k
-    cand = 0xFFFF
-    d16 = img.view(np.uint16)
-    for g in grp[int(h['group_beg']):int(h['group_end'])]:
-        for c, pm in enumerate(PORT_CLASSES):
-            H = int(pht_hash(src & int(g['src_mask']), dst & int(g['dst_mask']), ports & pm))
-            tag = H & 0xFFFF
-            d = int(d16[int(g['disp_off%d' % c]) + ((H >> 16) & int(g['disp_mask%d' % c]))])
-            slot = int(pht_slot(H, d, int(g['n_slots%d' % c])))
-            w = int(img[int(g['slot_off%d' % c]) + slot])
-            if (w >> 16) == tag:
-                cand = min(cand, w & 0xFFFF)
     best = None
-    if cand != 0xFFFF:
-        if not match(e[cand]):
+    goff, ng, moff, nm = r[0:4]
+    if ng:
+        S = r[8] | (r[9] << 32)
+        D = r[10] | (r[11] << 32)
+        for q in range(nm):
+            mr = [int(v) for v in image[moff + PHT_MASK_WORDS * q: moff + PHT_MASK_WORDS * (q + 1)]]
+            side = mr[1]
+            key = (dst if side else src) & mr[0]
+            v = _probe(image, field_hash(key, side), mr[4:8])
+            if v != PHT_NONE:
+                bits = int(image[r[7] + 2 * v]) | (int(image[r[7] + 2 * v + 1]) << 32)
+                if side:
+                    D |= bits
+                else:
+                    S |= bits
+        cand0 = S & D
+        floor = 0
+        for _attempt in range(PHT_ATTEMPTS):
+            bi = PHT_NONE
+            for j in range(ng):
+                if not (cand0 >> j) & 1:
+                    continue
+                g = [int(v) for v in image[goff + PHT_GROUP_WORDS * j: goff + PHT_GROUP_WORDS * (j + 1)]]
+                if g[2] >= bi:
+                    break
+                for c, pm in enumerate(PORT_CLASSES):
+                    H = int(pht_hash(src & g[0], dst & g[1], ports & pm))
+                    v = _probe(image, H, g[4 + 4 * c: 8 + 4 * c])
+                    if v >= floor:
+                        bi = min(bi, v)
+            if bi == PHT_NONE:
+                break
+            if match(e[bi]):
+                best = bi
+                break
+            floor = bi + 1
+        else:
             return 'defer'
-        best = cand
     gid_best = int(e[best]['gid']) if best is not None else None
-    for x in resid[int(h['resid_beg']):int(h['resid_end'])]:
+    for x in resid[r[4]:r[5]]:
         if gid_best is not None and int(x['gid']) >= gid_best:
             break
         if match(x):

@@ -65,7 +65,8 @@ static_assert(sizeof(Slot) == 64, "slot layout");
 static_assert(sizeof(rsa_tuple) == 16, "tuple layout");
 static_assert(sizeof(rsa_rule_entry) == 32, "rule layout");
 static_assert(sizeof(rsa_pht_group) == 80, "group layout");
-static_assert(sizeof(rsa_pht_list) == 32, "list header layout");
+static_assert(sizeof(rsa_pht_mask) == 32, "mask layout");
+static_assert(sizeof(rsa_pht_list) == 64, "list record layout");
 static_assert(sizeof(rsa_conn_record) == 40, "record layout");
 
 // Rule data is read through the constant address space so that wave-uniform
@@ -80,12 +81,13 @@ struct Rules {
   const const_u32* off;         // n_lists + 1
   uint32_t n_lists;
   uint32_t n_rules;
-  // perfect-hash tuple-space index (optional)
-  const const_v4u* hdr;         // per list 2 x v4u: {group_beg, group_end, resid_beg, resid_end}, {prefix, ...}
-  const const_v4u* groups;      // per group 5 x v4u: {smask, dmask, min_idx, n_real}, 4 x {slot_off, disp_off, n_slots, disp_mask}
+  // pruned perfect-hash tuple-space index (optional): one uint32 image
+  // (include/ruleset_hip.h) holding list, group and mask records, bitmaps and
+  // the CHD tables; read per lane (LDS copy or global)
   const const_v4u* resid;       // residual entries (gid-ascending per list)
-  const uint32_t* img;          // slot + displacement image (global copy)
+  const uint32_t* img;          // the image (global copy)
   uint32_t img_words;
+  uint32_t list_off;            // word offset of the list records
   int indexed;
   int force_defer;              // testing: every index candidate takes the exact deferred path
 };
@@ -214,110 +216,156 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t x) {
 }
 constexpr uint32_t kSaltS = 0x9E3779B9u, kSaltD = 0x7F4A7C15u, kSaltP = 0x2545F491u;
 
-// One CHD probe (compile.py pht_slot): H -> candidate list index or kNoCand.
-// img: the slot/displacement image (LDS or global).
+// Index image reads: the LDS copy through address-space-3 pointers (ds_read),
+// the global copy through plain pointers.
+typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+typedef __attribute__((address_space(3))) const uint16_t lds_u16;
+typedef __attribute__((address_space(3))) const v4u lds_v4u;
+__device__ __forceinline__ v4u rd4(const lds_u32* img, uint32_t w) { return *reinterpret_cast<const lds_v4u*>(img + w); }
+__device__ __forceinline__ v4u rd4(const uint32_t* img, uint32_t w) { return *reinterpret_cast<const v4u*>(img + w); }
+__device__ __forceinline__ uint32_t rd16(const lds_u32* img, uint32_t h) { return reinterpret_cast<const lds_u16*>(img)[h]; }
+__device__ __forceinline__ uint32_t rd16(const uint32_t* img, uint32_t h) { return reinterpret_cast<const uint16_t*>(img)[h]; }
+
+// One CHD probe (compile.py pht_slot / _probe): H -> the slot's 16-bit value,
+// or kNoCand.  b = {slot_off, disp_off (uint16 units), n_slots, disp_mask}.
 template <typename P32>
 __device__ __forceinline__ uint32_t pht_probe(P32 img, uint32_t H, v4u b) {
   const uint32_t hi = H >> 16;
-  const uint32_t d = reinterpret_cast<const uint16_t*>(img)[b.y + (hi & b.w)];
+  const uint32_t d = rd16(img, b.y + (hi & b.w));
   const uint32_t x = H + (__umul24(d, hi | 1u) << 16);
   const uint32_t slot = __umulhi(x, b.z);
   const uint32_t w = img[b.x + slot];
   return ((w >> 16) == (H & 0xFFFFu)) ? (w & 0xFFFFu) : kNoCand;
 }
 
-// Port-class hash components of a tuple (PORT_CLASSES order: any, dport, sport, both).
-struct PortHash {
-  uint32_t h0, h1, h2, h3;
-};
-__device__ __forceinline__ PortHash port_hashes(uint32_t ports) {
-  PortHash p;
-  p.h0 = fmix32(0u ^ kSaltP);
-  p.h1 = fmix32((ports & 0xFFFF0000u) ^ kSaltP);
-  p.h2 = fmix32((ports & 0x0000FFFFu) ^ kSaltP);
-  p.h3 = fmix32(ports ^ kSaltP);
-  return p;
-}
+constexpr int kAttempts = 4;   // compile.py PHT_ATTEMPTS
+constexpr uint32_t kListWords = 16, kGroupWords = 20, kMaskWords = 8;
 
-// First match for the `mine` lanes of list L (wave-uniform).  Without the
-// index: a linear scan of the whole list.  With it: prefix scan, then (only if
-// some lane is still open) four independent probes per (src mask, dst mask)
-// group, verification of the minimum candidate and the residual scan.
-// Returns gid, kNoGid or kDefer.
+// Index lookup for ONE lane (divergent code: the lanes of a wave may be on
+// different lists; compile.py pht_lookup is the host model).  h0..h2: the
+// lane's list record {group_off, n_groups, mask_off, n_masks},
+// {resid_beg, resid_end, prefix, bm_off}, {src_any, dst_any}; ebeg: the list's
+// first entry.  (1) pruning: each src/dst mask table maps the masked address to
+// a bitmap of the groups holding a rule on that prefix; (2) the groups in
+// src & dst bitmaps, ascending min index, four port-class probes each, until
+// a group's min index cannot beat the best candidate; (3) verification of the
+// candidate against its entry (16-bit tags collide), retried above a failed
+// candidate.  Returns gid, kNoGid or kDefer.
 template <typename P32>
-__device__ __forceinline__ uint32_t classify_list(const Rules& R, P32 img, uint32_t L, bool mine, uint32_t src,
-                                                  uint32_t dst, uint32_t ports, const PortHash& ph) {
-  const uint32_t beg = R.off[L], end = R.off[L + 1];
-  if (!R.indexed) return scan_list(R.e, beg, end, mine, kNoGid, src, dst, ports);
-  const v4u h0 = R.hdr[2 * L], h1 = R.hdr[2 * L + 1];
-  uint32_t best = scan_list(R.e, beg, beg + h1.x, mine, kNoGid, src, dst, ports);
-  const bool open = mine && best == kNoGid;
-  if (__ballot(open) == 0) return best;
-  uint32_t cand = kNoCand;
-  uint32_t hs = 0, psm = 0;
-  for (uint32_t g = h0.x; g < h0.y; ++g) {
-    const v4u a = R.groups[5 * g];
-    const v4u t0 = R.groups[5 * g + 1], t1 = R.groups[5 * g + 2], t2 = R.groups[5 * g + 3],
-              t3 = R.groups[5 * g + 4];
-    if (g == h0.x || a.x != psm) {   // groups are sorted by src mask: wave-uniform branch
-      hs = fmix32((src & a.x) ^ kSaltS);
-      psm = a.x;
+__device__ __forceinline__ uint32_t index_lookup(const Rules& R, P32 img, v4u h0, v4u h1, v4u h2, uint32_t ebeg,
+                                                 uint32_t src, uint32_t dst, uint32_t ports) {
+  unsigned long long S = ((unsigned long long)h2.y << 32) | h2.x;
+  unsigned long long D = ((unsigned long long)h2.w << 32) | h2.z;
+  for (uint32_t k = 0; k < h0.w; ++k) {
+    const uint32_t mw = h0.z + kMaskWords * k;
+    const v4u m0 = rd4(img, mw), m1 = rd4(img, mw + 4);
+    const bool dside = m0.y != 0;
+    const uint32_t H = fmix32(((dside ? dst : src) & m0.x) ^ (dside ? kSaltD : kSaltS));
+    const uint32_t v = pht_probe(img, H, m1);
+    if (v != kNoCand) {
+      const uint32_t bw = h1.w + 2 * v;
+      const unsigned long long bits = ((unsigned long long)img[bw + 1] << 32) | img[bw];
+      if (dside) {
+        D |= bits;
+      } else {
+        S |= bits;
+      }
     }
-    const uint32_t hsd = hs ^ fmix32((dst & a.y) ^ kSaltD);
-    const uint32_t c0 = pht_probe(img, hsd ^ ph.h0, t0);
-    const uint32_t c1 = pht_probe(img, hsd ^ ph.h1, t1);
-    const uint32_t c2 = pht_probe(img, hsd ^ ph.h2, t2);
-    const uint32_t c3 = pht_probe(img, hsd ^ ph.h3, t3);
-    cand = min(cand, min(min(c0, c1), min(c2, c3)));
   }
-  uint32_t res = kNoGid;
-  if (open && cand != kNoCand) {
-    const v4u ea = R.eg[2 * (size_t)(beg + cand)], eb = R.eg[2 * (size_t)(beg + cand) + 1];
-    res = (entry_match(ea, eb, src, dst, ports) && !R.force_defer) ? eb.z : kDefer;
+  const unsigned long long cand0 = S & D;
+  if (!cand0) return kNoGid;
+  // port-class hash components (compile.py PORT_CLASSES: any, dport, sport, both)
+  const uint32_t hp0 = fmix32(0u ^ kSaltP), hp1 = fmix32((ports & 0xFFFF0000u) ^ kSaltP),
+                 hp2 = fmix32((ports & 0x0000FFFFu) ^ kSaltP), hp3 = fmix32(ports ^ kSaltP);
+  uint32_t floor = 0;
+  for (int attempt = 0; attempt < kAttempts; ++attempt) {
+    uint32_t bi = kNoCand;
+    unsigned long long cand = cand0;
+    while (cand) {
+      const uint32_t g = (uint32_t)__builtin_ctzll(cand);
+      cand &= cand - 1;
+      const uint32_t gw = h0.x + kGroupWords * g;
+      const v4u a = rd4(img, gw);
+      if (a.z >= bi) break;   // groups ascend in min index: no later group can do better
+      const v4u t0 = rd4(img, gw + 4), t1 = rd4(img, gw + 8), t2 = rd4(img, gw + 12), t3 = rd4(img, gw + 16);
+      const uint32_t hsd = fmix32((src & a.x) ^ kSaltS) ^ fmix32((dst & a.y) ^ kSaltD);
+      uint32_t c0 = pht_probe(img, hsd ^ hp0, t0);
+      uint32_t c1 = pht_probe(img, hsd ^ hp1, t1);
+      uint32_t c2 = pht_probe(img, hsd ^ hp2, t2);
+      uint32_t c3 = pht_probe(img, hsd ^ hp3, t3);
+      c0 = c0 >= floor ? c0 : kNoCand;
+      c1 = c1 >= floor ? c1 : kNoCand;
+      c2 = c2 >= floor ? c2 : kNoCand;
+      c3 = c3 >= floor ? c3 : kNoCand;
+      bi = min(bi, min(min(c0, c1), min(c2, c3)));
+    }
+    if (bi == kNoCand) return kNoGid;
+    if (R.force_defer) return kDefer;
+    const v4u ea = R.eg[2 * (size_t)(ebeg + bi)], eb = R.eg[2 * (size_t)(ebeg + bi) + 1];
+    if (entry_match(ea, eb, src, dst, ports)) return eb.z;
+    floor = bi + 1;   // a tag collision: every true candidate lies above bi
   }
-  if (h0.z < h0.w) res = scan_list(R.resid, h0.z, h0.w, open && res != kDefer, res, src, dst, ports);
-  return open ? res : best;
+  return kDefer;
 }
 
-constexpr uint32_t kDeferList = 0xFFFFFFFDu;   // stage 0: not the wave's majority list
-
-// First-match classification of one wave of tuples: waterfall over the distinct
-// candidate lists present in the wave (list id broadcast by readlane).
-// kExact: ignore the index (linear scan of whole lists) — the deferred-line path.
-// kMajority: classify only the wave's (approximate) majority list; lanes of
-// other lists return kDeferList (a later launch over those lanes sees mostly
-// single-list waves, so a wave pays for one list's probes, not two).
-template <bool kExact, bool kMajority, typename P32>
+// First-match classification of one wave of tuples.  Linear scans (the whole
+// list without the index; the prefix and the residual entries with it) run as
+// a waterfall over the distinct lists present in the wave (list id broadcast
+// by readlane, so entries are wave-uniform scalar loads); the index lookup
+// runs per lane.  kExact: ignore the index (the deferred-line path).
+template <bool kExact, typename P32>
 __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Rules& R, P32 img, unsigned int* flags) {
   const uint32_t list = t.w & 0xFFFFu;
   if (active && list >= R.n_lists) {
     atomicOr(&flags[1], 1u);
     active = false;
   }
-  PortHash ph = {0u, 0u, 0u, 0u};
-  if (!kExact && R.indexed) ph = port_hashes(t.z);
   uint32_t best = kNoGid;
-  unsigned long long pending = __ballot(active);
-  if (kMajority && pending) {
-    uint32_t L = __builtin_amdgcn_readlane(list, __builtin_ctzll(pending));
-    const unsigned long long m1 = __ballot(active && list == L);
-    if (2 * __popcll(m1) < __popcll(pending)) L = __builtin_amdgcn_readlane(list, __builtin_ctzll(pending & ~m1));
-    const bool mine = active && list == L;
-    const uint32_t b = classify_list(R, img, L, mine, t.x, t.y, t.z, ph);
-    if (!active) return kNoGid;
-    return mine ? b : kDeferList;
+  if (kExact || !R.indexed) {
+    unsigned long long pending = __ballot(active);
+    while (pending) {
+      const int leader = __builtin_ctzll(pending);
+      const uint32_t L = __builtin_amdgcn_readlane(list, leader);
+      const bool mine = active && list == L;
+      pending &= ~__ballot(mine);
+      const uint32_t b = scan_list(R.e, R.off[L], R.off[L + 1], mine, kNoGid, t.x, t.y, t.z);
+      if (mine) best = b;
+    }
+    return active ? best : kNoGid;
   }
+  v4u h0 = {0u, 0u, 0u, 0u}, h1 = {0u, 0u, 0u, 0u}, h2 = {0u, 0u, 0u, 0u}, h3 = {0u, 0u, 0u, 0u};
+  if (active) {
+    const uint32_t lw = R.list_off + kListWords * list;
+    h0 = rd4(img, lw);
+    h1 = rd4(img, lw + 4);
+    h2 = rd4(img, lw + 8);
+    h3 = rd4(img, lw + 12);
+  }
+  // 1. prefix scans
+  unsigned long long pending = __ballot(active && h1.z != 0);
   while (pending) {
     const int leader = __builtin_ctzll(pending);
     const uint32_t L = __builtin_amdgcn_readlane(list, leader);
     const bool mine = active && list == L;
     pending &= ~__ballot(mine);
-    uint32_t b;
-    if (kExact) {
-      b = scan_list(R.e, R.off[L], R.off[L + 1], mine, kNoGid, t.x, t.y, t.z);
-    } else {
-      b = classify_list(R, img, L, mine, t.x, t.y, t.z, ph);
-    }
+    const uint32_t beg = R.off[L];
+    const uint32_t pre = __builtin_amdgcn_readlane(h1.z, leader);
+    const uint32_t b = scan_list(R.e, beg, beg + pre, mine, kNoGid, t.x, t.y, t.z);
+    if (mine) best = b;
+  }
+  // 2. the index, per lane
+  const bool open = active && best == kNoGid;
+  if (open && h0.y != 0) best = index_lookup(R, img, h0, h1, h2, h3.x, t.x, t.y, t.z);
+  // 3. residual scans for lanes the prefix did not match and that are not deferred
+  const bool want = open && best != kDefer && h1.x < h1.y;
+  pending = __ballot(want);
+  while (pending) {
+    const int leader = __builtin_ctzll(pending);
+    const uint32_t L = __builtin_amdgcn_readlane(list, leader);
+    const bool mine = want && list == L;
+    pending &= ~__ballot(mine);
+    const uint32_t rb = __builtin_amdgcn_readlane(h1.x, leader), re = __builtin_amdgcn_readlane(h1.y, leader);
+    const uint32_t b = scan_list(R.resid, rb, re, mine, best, t.x, t.y, t.z);
     if (mine) best = b;
   }
   return active ? best : kNoGid;
@@ -421,56 +469,47 @@ __device__ __forceinline__ void finish_line(bool in, unsigned long long i, uint4
   if (fresh) A.used[pos] = (uint32_t)slot;
 }
 
-// Workgroup-aggregated append of two streams (a, b) to global cursors: one
-// device atomic per stream per workgroup call.  Every thread of the workgroup
-// must call it (workgroup-uniform control flow).  sh: 4 LDS words.
-__device__ __forceinline__ void block_append2(bool a, bool b, unsigned long long* cur_a, unsigned long long* cur_b,
-                                              unsigned long long* sh, unsigned long long& pos_a,
-                                              unsigned long long& pos_b) {
-  const unsigned long long ma = __ballot(a), mb = __ballot(b);
+// Workgroup-aggregated append to one global cursor: one device atomic per
+// workgroup call.  Every thread of the workgroup must call it
+// (workgroup-uniform control flow).  sh: 2 LDS words, sh[0] zero on entry.
+__device__ __forceinline__ unsigned long long block_append(bool a, unsigned long long* cur, unsigned long long* sh) {
+  const unsigned long long ma = __ballot(a);
   const unsigned lane = __lane_id();
-  const unsigned long long below = (1ull << lane) - 1ull;
-  unsigned long long wa = 0, wb = 0;
-  if (lane == 0) {
-    if (ma) wa = atomicAdd(&sh[0], (unsigned long long)__popcll(ma));
-    if (mb) wb = atomicAdd(&sh[1], (unsigned long long)__popcll(mb));
-  }
+  unsigned long long wa = 0;
+  if (lane == 0 && ma) wa = atomicAdd(&sh[0], (unsigned long long)__popcll(ma));
   wa = __shfl(wa, 0);
-  wb = __shfl(wb, 0);
   __syncthreads();
   if (threadIdx.x == 0) {
-    sh[2] = sh[0] ? atomicAdd(cur_a, sh[0]) : 0ull;
-    sh[3] = sh[1] ? atomicAdd(cur_b, sh[1]) : 0ull;
+    sh[1] = sh[0] ? atomicAdd(cur, sh[0]) : 0ull;
     sh[0] = 0;
-    sh[1] = 0;
   }
   __syncthreads();
-  pos_a = sh[2] + wa + __popcll(ma & below);
-  pos_b = sh[3] + wb + __popcll(mb & below);
+  const unsigned long long pos = sh[1] + wa + __popcll(ma & ((1ull << lane) - 1ull));
+  __syncthreads();   // sh[1] is rewritten by the next call
+  return pos;
 }
 
-// Pass 1 classification with the index (staged in LDS when kImg > 0).
-// kStage 0: every line; a wave classifies its majority list and defers the
-// other lanes to tailA.  kStage 1: the lines of tailA, all lists of a wave.
-// Lines whose index candidate fails verification go to tailB (k_tail).
-template <int kMode, int kImg, int kStage>
+// Pass 1 classification (index image staged in LDS when kImg > 0).  Lines
+// whose index candidate failed verification kAttempts times go to `tail`
+// (k_tail scans them exactly).
+template <int kMode, int kImg>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kImgSmallMax ? 4 : 8, 8))) void k_classify(
     const uint4* __restrict__ T, const uint32_t* __restrict__ TS, const unsigned long long* __restrict__ ORD,
     unsigned long long n, const int32_t* __restrict__ gin, int32_t* __restrict__ gout, uint32_t* __restrict__ gtag,
-    Rules R, Agg A, uint32_t* tailA, unsigned long long* tailA_n, uint32_t* tailB, unsigned long long* tailB_n) {
-  __shared__ uint32_t lds_img[kImg > 0 ? kImg : 1];
-  __shared__ unsigned long long lds_app[4];
-  if (threadIdx.x < 4) lds_app[threadIdx.x] = 0;
+    Rules R, Agg A, uint32_t* tail, unsigned long long* tail_n) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds_img[kImg > 0 ? kImg : 4];
+  __shared__ unsigned long long lds_app[2];
+  if (threadIdx.x < 2) lds_app[threadIdx.x] = 0;
   if (kImg > 0 && kMode != kGivenAgg && R.indexed) {
-    for (uint32_t w = threadIdx.x; w < R.img_words; w += blockDim.x) lds_img[w] = R.img[w];
+    const uint4* src = reinterpret_cast<const uint4*>(R.img);
+    uint4* dst = reinterpret_cast<uint4*>(lds_img);
+    for (uint32_t w = threadIdx.x; w < (R.img_words + 3) / 4; w += blockDim.x) dst[w] = src[w];
   }
   __syncthreads();
-  if (kStage == 1) n = *tailA_n;
   const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
   for (unsigned long long base = (unsigned long long)blockIdx.x * blockDim.x; base < n; base += stride) {
-    const unsigned long long j = base + threadIdx.x;
-    const bool in = j < n;
-    const unsigned long long i = kStage == 1 ? (in ? tailA[j] : 0u) : j;
+    const unsigned long long i = base + threadIdx.x;
+    const bool in = i < n;
     const uint4 t = in ? T[i] : make_uint4(0u, 0u, 0u, 0u);
     const bool valid = in && (((t.w >> 16) & 0xFFu) & RSA_F_VALID);
     uint32_t gid;
@@ -478,17 +517,16 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kIm
       gid = in ? (uint32_t)gin[i] : kNoGid;
     } else {
       if (kImg > 0) {
-        gid = classify_wave<false, kStage == 0>(t, valid, R, (const uint32_t*)lds_img, A.flags);
+        gid = classify_wave<false>(t, valid, R, (const lds_u32*)lds_img, A.flags);
       } else {
-        gid = classify_wave<false, kStage == 0>(t, valid, R, R.img, A.flags);
+        gid = classify_wave<false>(t, valid, R, R.img, A.flags);
       }
-      const bool to_a = gid == kDeferList;
-      const bool to_b = gid == kDefer;
-      unsigned long long pa, pb;
-      block_append2(to_a, to_b, tailA_n, tailB_n, lds_app, pa, pb);
-      if (to_a) tailA[pa] = (uint32_t)i;
-      if (to_b) tailB[pb] = (uint32_t)i;
-      if (to_a || to_b) continue;   // finished by a later launch
+      const bool defer = gid == kDefer;
+      if (__syncthreads_or(defer)) {   // rare: workgroup-aggregated append
+        const unsigned long long pos = block_append(defer, tail_n, lds_app);
+        if (defer) tail[pos] = (uint32_t)i;
+      }
+      if (defer) continue;   // finished by k_tail
     }
     finish_line<kMode>(in, i, t, gid, TS, ORD, gout, gtag, R.n_rules, A);
   }
@@ -508,7 +546,7 @@ __global__ __launch_bounds__(kBlock) void k_tail(const uint4* __restrict__ T, co
     const unsigned long long i = in ? tail[j] : 0u;
     const uint4 t = in ? T[i] : make_uint4(0u, 0u, 0u, 0u);
     const bool valid = in && (((t.w >> 16) & 0xFFu) & RSA_F_VALID);
-    const uint32_t gid = classify_wave<true, false>(t, valid, R, R.img, A.flags);
+    const uint32_t gid = classify_wave<true>(t, valid, R, R.img, A.flags);
     finish_line<kMode>(in, i, t, gid, TS, ORD, gout, gtag, R.n_rules, A);
   }
 }
@@ -884,9 +922,8 @@ struct rsa_ctx {
   uint32_t n_rules = 0;
   bool rules_loaded = false;
   // perfect-hash tuple-space index
-  rsa_pht_list* d_hdr = nullptr;
-  rsa_pht_group* d_groups = nullptr;
   uint32_t* d_img = nullptr;
+  uint32_t list_off = 0;
   uint32_t img_words = 0;
   rsa_rule_entry* d_resid = nullptr;
   bool index_loaded = false;
@@ -913,7 +950,7 @@ struct rsa_ctx {
   bool tightened = false;
   uint32_t profile_skip = 0;
   uint32_t filter_slice = 256;
-  uint32_t filter_steps = 1;          // filter refinements (each after 4x the previous lines)        // auto filter: the first 1/filter_slice of a large batch builds the bound
+  uint32_t filter_steps = 3;          // auto filter: bound refinements (each after 4x the previous lines)
   uint32_t* d_tail = nullptr;         // deferred line indices
   unsigned long long* d_tail_n = nullptr;
   unsigned long long tail_alloc = 0;
@@ -961,8 +998,7 @@ Rules rules_of(const rsa_ctx* c) {
   r.off = (const const_u32*)(c->d_off);
   r.n_lists = c->n_lists;
   r.n_rules = c->n_rules;
-  r.hdr = (const const_v4u*)(c->d_hdr);
-  r.groups = (const const_v4u*)(c->d_groups);
+  r.list_off = c->list_off;
   r.resid = (const const_v4u*)(c->d_resid);
   r.img = c->d_img;
   r.img_words = c->img_words;
@@ -1097,16 +1133,15 @@ int cap_select(rsa_ctx* c, unsigned long long* out, uint32_t* h_n_capped) {
   return RSA_OK;
 }
 
-// Two deferred-line regions of `tail_alloc` entries each (list-deferred and
-// verification-deferred lines) and their counters.
+// Deferred-line region of `tail_alloc` entries and its counter.
 int ensure_tail(rsa_ctx* c, unsigned long long n) {
-  if (!c->d_tail_n) HIPCHK(c, hipMalloc(&c->d_tail_n, 2 * sizeof(unsigned long long)));
+  if (!c->d_tail_n) HIPCHK(c, hipMalloc(&c->d_tail_n, sizeof(unsigned long long)));
   if (n <= c->tail_alloc) return RSA_OK;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   hipFree(c->d_tail);
   c->d_tail = nullptr;
   c->tail_alloc = 0;
-  HIPCHK(c, hipMalloc(&c->d_tail, 2 * n * sizeof(uint32_t)));
+  HIPCHK(c, hipMalloc(&c->d_tail, n * sizeof(uint32_t)));
   c->tail_alloc = n;
   return RSA_OK;
 }
@@ -1135,21 +1170,7 @@ int ensure_events(rsa_ctx* c) {
 constexpr int kImgSmall = kImgSmallMax;   // 62.5 KiB: two 1024-thread workgroups per CU (32 waves)
 constexpr int kImgLarge = 38912;   // 152 KiB: one workgroup per CU
 
-template <int kMode, int kImg>
-void launch_stages(rsa_ctx* c, unsigned per_cu, const uint4* t, const uint32_t* ts, const unsigned long long* o,
-                   uint64_t m, const int32_t* gi, int32_t* go, uint32_t* gt, const Rules& r, const Agg& ag) {
-  uint32_t* ta = c->d_tail;
-  uint32_t* tb = c->d_tail + c->tail_alloc;
-  unsigned long long* na = c->d_tail_n;
-  unsigned long long* nb = c->d_tail_n + 1;
-  k_classify<kMode, kImg, 0><<<grid_for_threads(c, m, 1024, per_cu), 1024, 0, c->stream>>>(t, ts, o, m, gi, go, gt,
-                                                                                          r, ag, ta, na, tb, nb);
-  if (kMode != kGivenAgg)   // list-deferred lines (their number is read on the device: no host sync)
-    k_classify<kMode, kImg, 1><<<c->cu_count * per_cu, 1024, 0, c->stream>>>(t, ts, o, m, gi, go, gt, r, ag, ta, na,
-                                                                             tb, nb);
-}
-
-// Classification launches + exact tail for lines [0, m) of T (already offset).
+// Classification launch + exact tail for lines [0, m) of T (already offset).
 template <int kMode>
 int launch_classify(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsigned long long* o, uint64_t m,
                     const int32_t* gi, int32_t* go, uint32_t* gt) {
@@ -1157,20 +1178,22 @@ int launch_classify(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsign
   const Agg ag = agg_of(c);
   int rc = ensure_tail(c, m);
   if (rc) return rc;
-  HIPCHK(c, hipMemsetAsync(c->d_tail_n, 0, 2 * sizeof(unsigned long long), c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_tail_n, 0, sizeof(unsigned long long), c->stream));
   const bool lds = kMode != kGivenAgg && c->indexed;
   if (lds && c->img_words <= (uint32_t)kImgSmall) {
-    launch_stages<kMode, kImgSmall>(c, 2, t, ts, o, m, gi, go, gt, r, ag);
+    k_classify<kMode, kImgSmall><<<grid_for_threads(c, m, 1024, 2), 1024, 0, c->stream>>>(
+        t, ts, o, m, gi, go, gt, r, ag, c->d_tail, c->d_tail_n);
   } else if (lds && c->img_words <= (uint32_t)kImgLarge) {
-    launch_stages<kMode, kImgLarge>(c, 1, t, ts, o, m, gi, go, gt, r, ag);
+    k_classify<kMode, kImgLarge><<<grid_for_threads(c, m, 1024, 1), 1024, 0, c->stream>>>(
+        t, ts, o, m, gi, go, gt, r, ag, c->d_tail, c->d_tail_n);
   } else {
-    launch_stages<kMode, 0>(c, 2, t, ts, o, m, gi, go, gt, r, ag);
+    k_classify<kMode, 0><<<grid_for_threads(c, m, 1024, 2), 1024, 0, c->stream>>>(t, ts, o, m, gi, go, gt, r, ag,
+                                                                                c->d_tail, c->d_tail_n);
   }
   HIPCHK(c, hipGetLastError());
   if (kMode != kGivenAgg) {
-    // verification-deferred lines
-    k_tail<kMode><<<c->cu_count * 4, kBlock, 0, c->stream>>>(t, ts, o, go, gt, r, ag, c->d_tail + c->tail_alloc,
-                                                             c->d_tail_n + 1);
+    // deferred lines (their number is read on the device: no host sync)
+    k_tail<kMode><<<c->cu_count * 4, kBlock, 0, c->stream>>>(t, ts, o, go, gt, r, ag, c->d_tail, c->d_tail_n);
     HIPCHK(c, hipGetLastError());
   }
   return RSA_OK;
@@ -1301,7 +1324,7 @@ int rsa_ctx_destroy(rsa_ctx* c) {
   if (!c) return RSA_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->d_tail, c->d_tail_n, c->d_gtag, c->d_gscratch, c->d_entries, c->d_off, c->d_hdr, c->d_groups,
+  void* bufs[] = {c->d_tail, c->d_tail_n, c->d_gtag, c->d_gscratch, c->d_entries, c->d_off,
                   c->d_img, c->d_resid,
                   c->d_slots, c->d_used, c->d_used_n, c->d_filter, c->d_flags, c->d_cursor, c->d_cidx,
                   c->d_capped_gid, c->d_capped_cnt, c->d_capped_start, c->d_keys};
@@ -1385,33 +1408,62 @@ int rsa_load_rules(rsa_ctx* c, const rsa_rule_entry* h_entries, uint32_t n_entri
   return RSA_OK;
 }
 
-int rsa_load_index(rsa_ctx* c, const rsa_pht_list* h_lists, const rsa_pht_group* h_groups, uint32_t n_groups,
-                   const uint32_t* h_image, uint32_t image_words, const rsa_rule_entry* h_resid, uint32_t n_resid) {
-  if (!c || !h_lists || (n_groups && !h_groups) || !h_image || (n_resid && !h_resid))
-    return fail(c, RSA_ERR_ARG, "null argument");
+namespace {
+
+// A CHD table inside the image whose slot values are all < `limit`.
+bool table_ok(const uint32_t* img, uint32_t words, const rsa_pht_table& t, uint32_t limit) {
+  if (t.n_slots == 0 || (uint64_t)t.slot_off + t.n_slots > words || (t.disp_mask & (t.disp_mask + 1)) != 0 ||
+      (uint64_t)t.disp_off + t.disp_mask + 1 > 2ull * words)
+    return false;
+  for (uint32_t q = 0; q < t.n_slots; ++q) {
+    const uint32_t w = img[t.slot_off + q];
+    if (w != 0xFFFFFFFFu && (w & 0xFFFFu) >= limit) return false;
+  }
+  return true;
+}
+
+}  // namespace
+
+int rsa_load_index(rsa_ctx* c, const uint32_t* img, uint32_t words, const rsa_rule_entry* h_resid, uint32_t n_resid) {
+  if (!c || !img || (n_resid && !h_resid)) return fail(c, RSA_ERR_ARG, "null argument");
   if (!c->rules_loaded) return fail(c, RSA_ERR_STATE, "load the candidate lists first");
-  if (image_words == 0 || h_image[0] != 0xFFFFFFFFu) return fail(c, RSA_ERR_ARG, "image word 0 must be an empty slot");
+  if (words < 4 || img[0] != 0xFFFFFFFFu || img[1] != RSA_PHT_MAGIC)
+    return fail(c, RSA_ERR_ARG, "not an index image (word 0 must be empty, word 1 RSA_PHT_MAGIC)");
   const uint32_t nl = c->n_lists;
+  if (img[2] != nl) return fail(c, RSA_ERR_ARG, "image has %u lists, %u are loaded", img[2], nl);
+  const uint32_t lo = img[3];
+  const uint32_t lw = sizeof(rsa_pht_list) / 4, gw = sizeof(rsa_pht_group) / 4, mw = sizeof(rsa_pht_mask) / 4;
+  if (lo % 4 || (uint64_t)lo + (uint64_t)lw * nl > words) return fail(c, RSA_ERR_ARG, "list records outside the image");
   // validate everything the kernels index with, so no launch can read out of bounds
   for (uint32_t l = 0; l < nl; ++l) {
-    const rsa_pht_list& h = h_lists[l];
+    rsa_pht_list h;
+    memcpy(&h, img + lo + (size_t)lw * l, sizeof h);
     const uint32_t len = c->h_off[l + 1] - c->h_off[l];
-    if (h.group_beg > h.group_end || h.group_end > n_groups || h.resid_beg > h.resid_end || h.resid_end > n_resid)
-      return fail(c, RSA_ERR_ARG, "list %u: group/residual range out of bounds", l);
+    if (h.entry_beg != c->h_off[l] || h.entry_len != len)
+      return fail(c, RSA_ERR_ARG, "list %u: entry range differs from the loaded lists", l);
+    if (h.resid_beg > h.resid_end || h.resid_end > n_resid)
+      return fail(c, RSA_ERR_ARG, "list %u: residual range out of bounds", l);
     if (h.prefix > len) return fail(c, RSA_ERR_ARG, "list %u: prefix %u > list length %u", l, h.prefix, len);
-    if (h.group_beg < h.group_end && len > 0xFFFEu) return fail(c, RSA_ERR_ARG, "list %u: indexed list too long", l);
-    for (uint32_t g = h.group_beg; g < h.group_end; ++g) {
-      for (int k = 0; k < 4; ++k) {
-        const rsa_pht_table& tb = h_groups[g].table[k];
-        if (tb.n_slots == 0 || (uint64_t)tb.slot_off + tb.n_slots > image_words ||
-            (tb.disp_mask & (tb.disp_mask + 1)) != 0 || ((uint64_t)tb.disp_off + tb.disp_mask + 1) > 2ull * image_words)
-          return fail(c, RSA_ERR_ARG, "group %u class %d: table outside the image", g, k);
-        for (uint32_t q = 0; q < tb.n_slots; ++q) {
-          const uint32_t w = h_image[tb.slot_off + q];
-          if (w != 0xFFFFFFFFu && (w & 0xFFFFu) >= len)
-            return fail(c, RSA_ERR_ARG, "group %u class %d: slot index out of list", g, k);
-        }
-      }
+    if (h.n_groups == 0) continue;
+    if (h.n_groups > 64) return fail(c, RSA_ERR_ARG, "list %u: more than 64 groups", l);
+    if (len > 0xFFFEu) return fail(c, RSA_ERR_ARG, "list %u: indexed list too long", l);
+    if (h.group_off % 4 || (uint64_t)h.group_off + (uint64_t)gw * h.n_groups > words || h.mask_off % 4 ||
+        (uint64_t)h.mask_off + (uint64_t)mw * h.n_masks > words || h.bm_off % 2 ||
+        (uint64_t)h.bm_off + 2ull * h.n_bitmaps > words)
+      return fail(c, RSA_ERR_ARG, "list %u: records outside the image", l);
+    for (uint32_t g = 0; g < h.n_groups; ++g) {
+      rsa_pht_group G;
+      memcpy(&G, img + h.group_off + (size_t)gw * g, sizeof G);
+      for (int k = 0; k < 4; ++k)
+        if (!table_ok(img, words, G.table[k], len))
+          return fail(c, RSA_ERR_ARG, "list %u group %u class %d: table outside the image or index out of list", l, g, k);
+    }
+    for (uint32_t m = 0; m < h.n_masks; ++m) {
+      rsa_pht_mask M;
+      memcpy(&M, img + h.mask_off + (size_t)mw * m, sizeof M);
+      if (M.side > 1) return fail(c, RSA_ERR_ARG, "list %u mask %u: side must be 0 or 1", l, m);
+      if (!table_ok(img, words, M.table, h.n_bitmaps))
+        return fail(c, RSA_ERR_ARG, "list %u mask %u: table outside the image or bitmap out of range", l, m);
     }
     for (uint32_t e = h.resid_beg; e < h.resid_end; ++e) {
       if (h_resid[e].gid >= c->n_rules) return fail(c, RSA_ERR_ARG, "residual entry %u gid out of range", e);
@@ -1421,12 +1473,14 @@ int rsa_load_index(rsa_ctx* c, const rsa_pht_list* h_lists, const rsa_pht_group*
   }
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  int rc = upload(c, &c->d_hdr, h_lists, nl);
-  if (!rc) rc = upload(c, &c->d_groups, h_groups, n_groups);
-  if (!rc) rc = upload(c, &c->d_img, h_image, image_words);
+  // padded to whole 16-B vectors (the LDS staging copies uint4s)
+  std::vector<uint32_t> padded(img, img + words);
+  padded.resize((words + 3) / 4 * 4, 0u);
+  int rc = upload(c, &c->d_img, padded.data(), padded.size());
   if (!rc) rc = upload(c, &c->d_resid, h_resid, n_resid);
   if (rc) return rc;
-  c->img_words = image_words;
+  c->img_words = words;
+  c->list_off = lo;
   c->index_loaded = true;
   c->indexed = true;
   return RSA_OK;

@@ -90,12 +90,11 @@ class Engine(object):
         self._bind(n_rules)
 
     def load_index(self, index):
-        """Upload a compile.build_index() result (lists, shapes, image, residual)."""
-        lists, shapes, image, resid = (np.ascontiguousarray(a) for a in index)
-        self._index_hold = (lists, shapes, image, resid)
+        """Upload a compile.build_index() result (image, residual entries)."""
+        image, resid = (np.ascontiguousarray(a) for a in index)
+        self._index_hold = (image, resid)
         v = lambda a: a.ctypes.data_as(ctypes.c_void_p)
-        self.ctx.call('rsa_load_index', v(lists), v(shapes), ctypes.c_uint32(len(shapes)), v(image),
-                      ctypes.c_uint32(len(image)), v(resid), ctypes.c_uint32(len(resid)))
+        self.ctx.call('rsa_load_index', v(image), ctypes.c_uint32(len(image)), v(resid), ctypes.c_uint32(len(resid)))
 
     def set_option(self, option, value):
         self.ctx.call('rsa_set_option', ctypes.c_int(option), ctypes.c_int64(int(value)))
@@ -111,7 +110,7 @@ class Engine(object):
         self.ctx.call('rsa_last_pass1_ms', ctypes.byref(ms))
         return float(ms.value)
 
-    def load_compiled(self, compiled, index=True, prefix=64):
+    def load_compiled(self, compiled, index=True, prefix=0):
         """Upload a CompiledRules' lists (and its perfect-hash tuple-space index,
         whose first ``prefix`` entries per list are scanned linearly)."""
         ent, off = compiled.packed()

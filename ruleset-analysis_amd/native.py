@@ -48,7 +48,7 @@ SYMBOLS = {
     'rsa_last_error': (ctypes.c_char_p, [P]),
     'rsa_set_stream': (I32, [P, P]),
     'rsa_set_option': (I32, [P, I32, ctypes.c_int64]),
-    'rsa_load_index': (I32, [P, P, P, U32, P, U32, P, U32]),
+    'rsa_load_index': (I32, [P, P, U32, P, U32]),
     'rsa_last_pass1_ms': (I32, [P, ctypes.POINTER(ctypes.c_float)]),
     'rsa_load_rules': (I32, [P, P, U32, P, U32, U32]),
     'rsa_bind_counters': (I32, [P, P, P, P, P]),

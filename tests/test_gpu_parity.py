@@ -47,7 +47,7 @@ def test_golden_mapper_stream(engine, case):
 
 
 def _gpu_vs_oracle(engine, n_rules, n_lines, cap, seed, zipf=None, interfaces=('outside',), batches=1,
-                   shuffle=False, index=True, broad=True, prefix=64):
+                   shuffle=False, index=True, broad=True, prefix=0):
     dbj, info = synth.make_db(seed, n_rules, interfaces=interfaces, broad=broad)
     tr = synth.make_traffic((dbj, info), n_lines, seed=seed + 1, zipf=zipf)
     if shuffle:   # input order no longer follows the sort order

@@ -32,6 +32,7 @@ def timed(fn, reps):
         torch.cuda.synchronize()
         out.append(a.elapsed_time(b))
     out.sort()
+    print('timed: %.3f ms' % out[len(out) // 2], file=sys.stderr, flush=True)
     return out[len(out) // 2]
 
 
@@ -79,10 +80,10 @@ def main():
         eng.set_option(native.RSA_OPT_PROFILE_SKIP, mask)
         res['pass1_%s_ms' % name] = timed(p1, args.reps)
     eng.set_option(native.RSA_OPT_PROFILE_SKIP, 0)
-    for steps in (2, 3, 4):
+    for steps in (1, 2, 4, 5):
         eng.set_option(native.RSA_OPT_FILTER_STEPS, steps)
         res['reset_pass1_steps%d_ms' % steps] = timed(p1, args.reps)
-    eng.set_option(native.RSA_OPT_FILTER_STEPS, 1)
+    eng.set_option(native.RSA_OPT_FILTER_STEPS, 3)   # library default
     eng.reset(int(size * 1.25), cap)
     eng.pass1(batch, g)
     t = time.perf_counter()
