@@ -41,6 +41,7 @@ HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
 # int32 VALU lane-ops/s: 256 CUs x 4 SIMDs x 32 lanes/cycle x 2.4 GHz (MI355X_MICROARCH.md:
 # a wave issues one VALU instruction over 2 cycles, 32 lanes per cycle)
 VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9
+SCATTER_ATOMIC_PEAK = 0.08e12 / 4   # 4-B device atomics/s, 64 lanes in 64 rows (MI355X_MICROARCH.md)
 OPS_PER_EVAL = 8             # 2 per address range test x 2 + 2 per port range test x 2
 CONFIGS = {
     # name: (rules, lines per GPU, cap, seed, zipf, interfaces, broad)
@@ -148,7 +149,7 @@ def main():
     ap.add_argument('--filter-slice', type=int, default=0, help='override RSA_OPT_FILTER_SLICE')
     ap.add_argument('--opt', action='append', default=[], help='NAME=VALUE library option (e.g. FILTER_STEPS=3)')
     ap.add_argument('--no-index', action='store_true', help='classify with the plain linear scan')
-    ap.add_argument('--prefix', type=int, default=64, help='entries per list scanned before the index')
+    ap.add_argument('--prefix', type=int, default=0, help='entries per list scanned before the index')
     args = ap.parse_args()
 
     import torch
@@ -195,7 +196,7 @@ def main():
         eng.reset(capacity, cap)
         eng.pass1(batch, gbuf)
         if timed:
-            pass1_launch_ms.append(eng.last_pass1_ms())
+            pass1_launch_ms.append(eng.last_pass1_times())
         if world == 1:
             if eng.resolve_cap():
                 eng.pass2(batch, gbuf)
@@ -222,7 +223,16 @@ def main():
         tt = torch.tensor([dt], dtype=torch.float64, device=eng.device)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
-    pass1_ms = float(np.mean(pass1_launch_ms))
+    classify_ms = float(np.mean([a for a, _b in pass1_launch_ms]))
+    aggregate_ms = float(np.mean([b for _a, b in pass1_launch_ms]))
+    pass1_ms = classify_ms + aggregate_ms
+    # table-work counters of one more (untimed) step: lines combined, slot atomics
+    eng.set_option(native.RSA_OPT_STATS, 1)
+    eng.stats()
+    step(False)
+    torch.cuda.synchronize()
+    tstats = eng.stats()
+    eng.set_option(native.RSA_OPT_STATS, 0)
     sum_e = scan_work(compiled, batch, gbuf) if rank == 0 else 0
     if rank == 0:
         total_lines = lines * world * args.steps
@@ -243,8 +253,20 @@ def main():
                        'records': n_rec},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
-                         'kernel': 'pass 1 = k_classify<kClassifyAgg> + k_tail + k_count (per step: filter slice(s) + '
-                                   'rest)', 'kernel_ms': pass1_ms, 'bytes_per_line': BYTES_PER_LINE,
+                         'kernel': 'pass 1 = k_classify + k_tail + k_aggregate (per step: filter slices + rest)',
+                         'kernel_ms': pass1_ms, 'bytes_per_line': BYTES_PER_LINE,
+                         'kernels': {
+                             'classify_ms': classify_ms,
+                             'aggregate_ms': aggregate_ms,
+                             'classify_gbs': BYTES_PER_LINE * lines / (classify_ms * 1e-3) / 1e9,
+                             'aggregate_table_lines': tstats[0],
+                             'aggregate_slot_atomics': tstats[3],
+                             'aggregate_atomic_rate_g_s': tstats[3] / (aggregate_ms * 1e-3) / 1e9,
+                             'scattered_atomic_peak_g_s': SCATTER_ATOMIC_PEAK / 1e9,
+                             'note': 'k_aggregate is bound by scattered device atomics (one lane per 64-B row: '
+                                     'MI355X_MICROARCH.md Global atomics, 0.08 TB/s of 4-B adds = 20 G/s); '
+                                     'slot atomics = count/min/max updates of existing entries + claim and publish of new '
+                                     'ones (their fields are written by stores)'},
                          'valu': {'achieved': OPS_PER_EVAL * sum_e / (pass1_ms * 1e-3) / 1e12,
                                   'peak': VALU_PEAK_OPS / 1e12, 'unit': 'Tops/s',
                                   'frac': OPS_PER_EVAL * sum_e / (pass1_ms * 1e-3) / VALU_PEAK_OPS,

@@ -71,7 +71,7 @@ typedef struct rsa_rule_entry {
  * (src & src_mask, dst & dst_mask, ports & port_mask), ports = sport | dport << 16:
  *   H    = fmix32(ks ^ 0x9E3779B9) ^ fmix32(kd ^ 0x7F4A7C15) ^ fmix32(kp ^ 0x2545F491)
  *   d    = disp[disp_off + ((H >> 16) & disp_mask)]            (uint16 units of the image)
- *   slot = hi32((H + ((d * ((H >> 16) | 1)) << 16)) * n_slots)  (32-bit wrap)
+ *   slot = hi32((H + d * ((H * 0x2C1B3C6D) | 1)) * n_slots)    (32-bit wrap)
  *   word = image[slot_off + slot] = (H & 0xFFFF) << 16 | list-local entry index,
  *          0xFFFFFFFF = empty (image word 0 is always empty: absent classes
  *          point there with n_slots = 1)
@@ -129,7 +129,9 @@ typedef struct rsa_pht_list {    /* 64 B */
 #define RSA_OPT_FILTER_SLICE 5 /* auto filter: first 1/N (>= 1M lines) of a large batch builds the bound (default 256)       */
 #define RSA_OPT_FILTER_STEPS 7 /* auto filter: bound refinements, each after 4x the previous lines (default 3)  */
 #define RSA_OPT_FORCE_DEFER 8  /* TESTING: every index candidate goes to the exact deferred-line path        */
-#define RSA_OPT_PROFILE_SKIP 3 /* PROFILING ONLY, results invalid: bit0 skips counters, bit1 skips the table  */
+#define RSA_OPT_PROFILE_SKIP 3 /* PROFILING ONLY, results invalid: bit0 skips counters, bit1 skips the table, bit2 skips table updates */
+#define RSA_OPT_PRECHECK 9     /* pre-check monotone slot fields with a plain load before their atomics (default 1)       */
+#define RSA_OPT_STATS 10       /* PROFILING: count table work into the rsa_stats counters (default 0)                 */
 
 /* One distinct (rule, connection) aggregate, 40 B (connlist-reducer.py:162-176). */
 typedef struct rsa_conn_record {
@@ -206,6 +208,9 @@ int rsa_aggregate_gids(rsa_ctx *ctx, const rsa_tuple *d_tuples, const uint32_t *
 /* Device time (ms, HIP events on the ctx stream) of the pass-1 kernel launches
  * of the last rsa_classify / rsa_aggregate_gids call (waits for them). */
 int rsa_last_pass1_ms(rsa_ctx *ctx, float *h_ms);
+/* The same time split into classification (k_classify + k_tail) and
+ * aggregation (k_aggregate) launches. */
+int rsa_last_pass1_times(rsa_ctx *ctx, float *h_classify_ms, float *h_aggregate_ms);
 
 /* Resolve the cap (connlist-reducer.py:151): for every rule with
  * distinct >= cap, P = the order key of the line that inserted the cap-th
@@ -230,6 +235,12 @@ int rsa_emit(rsa_ctx *ctx, rsa_conn_record *d_out, uint64_t max_records, uint64_
 int rsa_table_size(rsa_ctx *ctx, uint64_t *h_n);
 int rsa_export(rsa_ctx *ctx, int which, rsa_conn_record *d_out, uint64_t max_records, uint64_t *h_n);
 int rsa_import(rsa_ctx *ctx, int which, const rsa_conn_record *d_in, uint64_t n);
+
+/* Profiling counters (collected while RSA_OPT_STATS is on): h_out[0] lines
+ * combined into the table, [1] probes beyond a line's home slot, [2] probes that
+ * took the atomic (claim) path, [3] slot-field atomics issued.  reset != 0
+ * zeroes them after the read. */
+int rsa_stats(rsa_ctx *ctx, uint64_t *h_out4, int reset);
 
 /* Synchronise the ctx stream (tests, host hand-off). */
 int rsa_sync(rsa_ctx *ctx);

@@ -222,6 +222,7 @@ PHT_EMPTY = 0xFFFFFFFF
 PHT_NONE = 0xFFFF
 PHT_MAX_IDX = 0xFFFE
 SALT_S, SALT_D, SALT_P = 0x9E3779B9, 0x7F4A7C15, 0x2545F491
+PHT_MUL = 0x2C1B3C6D                # odd multiplier of the CHD step hash (csrc kPhtMul)
 
 
 def fmix32(x):
@@ -248,12 +249,14 @@ def field_hash(k, side):
 
 
 def pht_slot(H, d, n_slots):
-    """slot = hi32(x * n_slots), x = (H + ((d * ((H >> 16) | 1)) << 16)) mod 2^32.
-    The slot depends on the high half of H, the tag is the low half and the
-    displacement bucket is (H >> 16) & disp_mask (csrc: pht_probe)."""
+    """slot = hi32(x * n_slots), x = (H + d * ((H * PHT_MUL) | 1)) mod 2^32.
+    The displacement bucket is (H >> 16) & disp_mask and the tag the low half of
+    H.  The step (H * PHT_MUL) | 1 is a second hash of the key, so keys of one
+    bucket that share the high half of H (a 16-bit birthday collision) still
+    separate as d grows (csrc: pht_probe)."""
     H = np.asarray(H, np.uint64)
-    hi = H >> np.uint64(16)
-    x = (H + ((np.asarray(d, np.uint64) * (hi | np.uint64(1))) << np.uint64(16))) & np.uint64(M32)
+    step = ((H * np.uint64(PHT_MUL)) & np.uint64(M32)) | np.uint64(1)
+    x = (H + np.asarray(d, np.uint64) * step) & np.uint64(M32)
     return ((x * np.uint64(n_slots)) >> np.uint64(32)).astype(np.int64)
 
 
@@ -280,7 +283,7 @@ def _pow2_at_least(x):
     return p
 
 
-def _chd(H, load=0.9, trials=4096):
+def _chd(H, load=0.98, trials=4096):
     """Hash-and-displace placement of distinct 32-bit hashes H into
     m = ceil(n / load) slots.  Returns (m, disp_mask, disp uint16[r], slot_of_key int64[n])."""
     n = len(H)

@@ -38,6 +38,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
+#include <cstddef>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -53,15 +54,20 @@ constexpr uint32_t kNoGid = 0xFFFFFFFFu;
 constexpr int kBlock = 256;
 
 // One distinct (rule, connection) aggregate in HBM, 64 B.
+// min_order, first and last share one 16-B group so that a single vector load
+// can pre-check all three monotone fields.
 struct alignas(64) Slot {
   unsigned long long kA;         // for_ip << 32 | to_ip
   unsigned long long kB;         // gid << 32 | pspell << 16 | to_port ; kEmpty / kBusy
   unsigned long long min_order;  // first occurrence (reducer input order)
-  unsigned int count, first, last;      // pass-1 aggregates
+  unsigned int first, last;      // pass-1 timestamp range
+  unsigned int count;            // pass-1 occurrences
   unsigned int count2, first2, last2;   // pass-2 aggregates (order <= P only)
   unsigned int pad[4];
 };
 static_assert(sizeof(Slot) == 64, "slot layout");
+static_assert(offsetof(Slot, first) % 8 == 0 && offsetof(Slot, last) == offsetof(Slot, first) + 4,
+              "first/last form one 8-B word");
 static_assert(sizeof(rsa_tuple) == 16, "tuple layout");
 static_assert(sizeof(rsa_rule_entry) == 32, "rule layout");
 static_assert(sizeof(rsa_pht_group) == 80, "group layout");
@@ -104,7 +110,9 @@ struct Agg {
   unsigned long long* used_n;
   unsigned int* flags;               // [0] overflow, [1] bad gid/list/state
   uint32_t cap;
-  uint32_t skip;                     // profiling only (RSA_OPT_PROFILE_SKIP): 1 counters, 2 table
+  uint32_t skip;                     // profiling only (RSA_OPT_PROFILE_SKIP): 1 counters, 2 table, 4 table updates
+  uint32_t precheck;                 // RSA_OPT_PRECHECK: plain-load pre-check of the monotone slot fields
+  unsigned long long* stats;         // RSA_OPT_STATS: [0] table lines, [1] extra probes, [2] atomic-path probes, [3] atomics
 };
 
 __device__ __forceinline__ unsigned long long mix64(unsigned long long x) {
@@ -215,6 +223,7 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t x) {
   return x;
 }
 constexpr uint32_t kSaltS = 0x9E3779B9u, kSaltD = 0x7F4A7C15u, kSaltP = 0x2545F491u;
+constexpr uint32_t kPhtMul = 0x2C1B3C6Du;   // compile.py PHT_MUL
 
 // Index image reads: the LDS copy through address-space-3 pointers (ds_read),
 // the global copy through plain pointers.
@@ -230,9 +239,8 @@ __device__ __forceinline__ uint32_t rd16(const uint32_t* img, uint32_t h) { retu
 // or kNoCand.  b = {slot_off, disp_off (uint16 units), n_slots, disp_mask}.
 template <typename P32>
 __device__ __forceinline__ uint32_t pht_probe(P32 img, uint32_t H, v4u b) {
-  const uint32_t hi = H >> 16;
-  const uint32_t d = rd16(img, b.y + (hi & b.w));
-  const uint32_t x = H + (__umul24(d, hi | 1u) << 16);
+  const uint32_t d = rd16(img, b.y + ((H >> 16) & b.w));
+  const uint32_t x = H + d * ((H * kPhtMul) | 1u);
   const uint32_t slot = __umulhi(x, b.z);
   const uint32_t w = img[b.x + slot];
   return ((w >> 16) == (H & 0xFFFFu)) ? (w & 0xFFFFu) : kNoCand;
@@ -372,48 +380,113 @@ __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Ru
 }
 
 // Insert-or-combine (kA, kB) into the open-addressing table.  A slot is claimed
-// EMPTY->BUSY, its kA published, then kB published; a lane that reads BUSY
-// retries the same slot on its next iteration.  Every key word is only ever
-// accessed by device atomics (executed beyond the per-XCD L2s), so no XCD can
-// observe a stale copy.  Returns the slot index (or ~0 on overflow); *fresh is
-// set when this call created the entry.
-__device__ __forceinline__ unsigned long long table_combine(const Agg& A, unsigned long long kA,
-                                                            unsigned long long kB, unsigned int cnt,
-                                                            unsigned int first, unsigned int last,
-                                                            unsigned long long order, bool* fresh) {
-  unsigned long long h = slot_hash(kA, kB) & A.mask;
-  unsigned long long probes = 0;
+// EMPTY->BUSY by a device atomic (executed at the memory side, beyond the
+// per-XCD L2s), its kA published, then kB published, both by atomics.  A
+// published key never changes during a job, so each probe first reads the
+// slot's head {kA, kB} and {min_order, first, last} with plain 16-B loads: the
+// line they come from (possibly a stale per-XCD copy) is a snapshot of memory,
+// and kA was final in memory before kB was, so a published kB in the snapshot
+// comes with its final kA.  A match or another published key is therefore
+// decided without atomics; only a slot that looks EMPTY or BUSY takes the
+// atomic path (CAS; a lane that sees BUSY re-reads the slot).  The three
+// monotone fields are then updated only where the snapshot does not already
+// rule the update out (min_order/first only decrease, last only increases, so
+// any value the snapshot holds bounds the current one).  Returns the slot index
+// (or kEmpty on overflow); *fresh is set when this call created the entry.
+struct SlotHead {
+  v4u k;   // kA lo, kA hi, kB lo, kB hi
+  v4u m;   // min_order lo, min_order hi, first, last
+};
+
+__device__ __forceinline__ SlotHead load_head(const Slot* c) {
+  SlotHead r;
+  r.k = *reinterpret_cast<const volatile v4u*>(&c->kA);
+  r.m = *reinterpret_cast<const volatile v4u*>(&c->min_order);
+  return r;
+}
+
+__device__ __forceinline__ unsigned long long table_combine_at(const Agg& A, unsigned long long kA,
+                                                               unsigned long long kB, unsigned int cnt,
+                                                               unsigned int first, unsigned int last,
+                                                               unsigned long long order, bool* fresh,
+                                                               unsigned long long h, SlotHead hd,
+                                                               uint32_t* st = nullptr) {
+  unsigned long long probes = 0, atomic_probes = 0;
   unsigned long long found = kEmpty;
   while (true) {
     Slot* c = &A.slots[h];
-    const unsigned long long cur = atomicCAS(&c->kB, kEmpty, kBusy);
-    if (cur == kEmpty) {
-      // publish kA before kB: wait for the kA atomic to complete at the memory side
-      atomicExch(&c->kA, kA);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      atomicExch(&c->kB, kB);
-      *fresh = true;
-      found = h;
-      break;
-    }
-    if (cur == kBusy) continue;
-    if (cur == kB && atomicOr(&c->kA, 0ull) == kA) {
-      found = h;
-      break;
+    const unsigned long long pa = ((unsigned long long)hd.k.y << 32) | hd.k.x;
+    const unsigned long long pb = ((unsigned long long)hd.k.w << 32) | hd.k.z;
+    if (pb != kEmpty && pb != kBusy) {
+      if (pb == kB && pa == kA) {
+        found = h;
+        break;
+      }
+    } else {
+      ++atomic_probes;
+      const unsigned long long cur = atomicCAS(&c->kB, kEmpty, kBusy);
+      if (cur == kEmpty) {
+        // The slot is ours and invisible until kB is published: write kA and the
+        // aggregates with agent-scope (write-through) stores, wait for them to
+        // complete, then publish kB.  Finders only update the fields after they
+        // have seen kB, so their atomics act on these values.
+        __hip_atomic_store(&c->kA, kA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&c->min_order, order, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(&c->first),
+                           ((unsigned long long)last << 32) | first, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&c->count, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        atomicExch(&c->kB, kB);
+        *fresh = true;
+        if (st) {
+          st[0] += 1;
+          st[1] += (uint32_t)probes;
+          st[2] += (uint32_t)atomic_probes;
+          st[3] += 2;
+        }
+        return h;
+      }
+      if (cur == kBusy) {
+        hd = load_head(c);
+        continue;
+      }
+      if (cur == kB && atomicOr(&c->kA, 0ull) == kA) {
+        found = h;
+        break;
+      }
     }
     h = (h + 1) & A.mask;
     if (++probes > A.mask) break;
+    hd = load_head(&A.slots[h]);
   }
   if (found == kEmpty) {
     atomicOr(&A.flags[0], 1u);
     return kEmpty;
   }
   Slot* s = &A.slots[found];
+  if (A.skip & 4u) return found;   // profiling only
   atomicAdd(&s->count, cnt);
-  atomicMin(&s->first, first);
-  atomicMax(&s->last, last);
-  atomicMin(&s->min_order, order);
+  const unsigned long long mo = ((unsigned long long)hd.m.y << 32) | hd.m.x;
+  const bool all = !A.precheck;
+  const bool u0 = all || order < mo, u1 = all || first < hd.m.z, u2 = all || last > hd.m.w;
+  if (u0) atomicMin(&s->min_order, order);
+  if (u1) atomicMin(&s->first, first);
+  if (u2) atomicMax(&s->last, last);
+  if (st) {
+    st[0] += 1;
+    st[1] += (uint32_t)probes;
+    st[2] += (uint32_t)atomic_probes;
+    st[3] += 1u + u0 + u1 + u2 + (atomic_probes ? 1u : 0u);
+  }
   return found;
+}
+
+__device__ __forceinline__ unsigned long long table_combine(const Agg& A, unsigned long long kA,
+                                                            unsigned long long kB, unsigned int cnt,
+                                                            unsigned int first, unsigned int last,
+                                                            unsigned long long order, bool* fresh) {
+  const unsigned long long h = slot_hash(kA, kB) & A.mask;
+  return table_combine_at(A, kA, kB, cnt, first, last, order, fresh, h, load_head(&A.slots[h]));
 }
 
 // Find an existing key (after pass 1 completed: plain loads are coherent across
@@ -428,45 +501,6 @@ __device__ __forceinline__ Slot* table_find(const Agg& A, unsigned long long kA,
     h = (h + 1) & A.mask;
   }
   return nullptr;
-}
-
-// Pass-1 modes: classify + aggregate (mapper fused with reducer), aggregate with
-// the gid given per tuple (reducer drop-in), classify only (mapper drop-in).
-enum { kClassifyAgg = 0, kGivenAgg = 1, kClassifyOnly = 2 };
-
-constexpr uint32_t kTagHit = 0x80000000u;   // gtag word: gid | hit bit; 0xFFFFFFFF = no match
-
-// Everything pass 1 does with a classified line: the mapper output (gout), the
-// gid|hit word the per-rule histogram counts (gtag), and the reducer's
-// distinct-connection table (connlist-reducer.py:146-176) for hit lines the
-// BUILT regex matched.  Wave-uniform control flow.
-template <int kMode>
-__device__ __forceinline__ void finish_line(bool in, unsigned long long i, uint4 t, uint32_t gid,
-                                            const uint32_t* __restrict__ TS, const unsigned long long* __restrict__ ORD,
-                                            int32_t* __restrict__ gout, uint32_t* __restrict__ gtag, uint32_t n_rules,
-                                            const Agg& A) {
-  const uint32_t flags = (t.w >> 16) & 0xFFu;
-  if (kMode != kGivenAgg && gout && in) gout[i] = (int32_t)gid;
-  if (kMode == kClassifyOnly) return;
-  if (in && gid != kNoGid && gid >= n_rules) atomicOr(&A.flags[1], 2u);
-  const bool matched = in && gid < n_rules;
-  const bool hit = matched && (flags & RSA_F_HIT);
-  if (in && !(A.skip & 1u)) gtag[i] = matched ? (gid | (hit ? kTagHit : 0u)) : 0xFFFFFFFFu;
-  bool fresh = false;
-  unsigned long long slot = kEmpty;
-  if (hit && (flags & RSA_F_BUILT) && A.cap > 0 && !(A.skip & 2u)) {
-    const unsigned long long o = ORD[i];
-    // exact skip: the rule is already capped with threshold <= filter < o
-    if (o <= A.filter[gid]) {
-      unsigned long long kA, kB;
-      conn_key(t, gid, kA, kB);
-      const uint32_t ts = TS[i];
-      slot = table_combine(A, kA, kB, 1u, ts, ts, o, &fresh);
-    }
-  }
-  wave_count_by_key(fresh, gid, A.distinct);
-  const unsigned long long pos = wave_append(fresh, A.used_n);
-  if (fresh) A.used[pos] = (uint32_t)slot;
 }
 
 // Workgroup-aggregated append to one global cursor: one device atomic per
@@ -489,18 +523,18 @@ __device__ __forceinline__ unsigned long long block_append(bool a, unsigned long
   return pos;
 }
 
-// Pass 1 classification (index image staged in LDS when kImg > 0).  Lines
-// whose index candidate failed verification kAttempts times go to `tail`
-// (k_tail scans them exactly).
-template <int kMode, int kImg>
+// Pass 1a — first-match classification (mapper.py:159-189): gid or RSA_NO_RULE
+// per tuple into gout (index image staged in LDS when kImg > 0).  Lines whose
+// index candidate failed verification kAttempts times go to `tail` (k_tail
+// scans them exactly).
+template <int kImg>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kImgSmallMax ? 4 : 8, 8))) void k_classify(
-    const uint4* __restrict__ T, const uint32_t* __restrict__ TS, const unsigned long long* __restrict__ ORD,
-    unsigned long long n, const int32_t* __restrict__ gin, int32_t* __restrict__ gout, uint32_t* __restrict__ gtag,
-    Rules R, Agg A, uint32_t* tail, unsigned long long* tail_n) {
+    const uint4* __restrict__ T, unsigned long long n, int32_t* __restrict__ gout, Rules R, unsigned int* flags,
+    uint32_t* tail, unsigned long long* tail_n) {
   __shared__ __attribute__((aligned(16))) uint32_t lds_img[kImg > 0 ? kImg : 4];
   __shared__ unsigned long long lds_app[2];
   if (threadIdx.x < 2) lds_app[threadIdx.x] = 0;
-  if (kImg > 0 && kMode != kGivenAgg && R.indexed) {
+  if (kImg > 0 && R.indexed) {
     const uint4* src = reinterpret_cast<const uint4*>(R.img);
     uint4* dst = reinterpret_cast<uint4*>(lds_img);
     for (uint32_t w = threadIdx.x; w < (R.img_words + 3) / 4; w += blockDim.x) dst[w] = src[w];
@@ -513,31 +547,24 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kIm
     const uint4 t = in ? T[i] : make_uint4(0u, 0u, 0u, 0u);
     const bool valid = in && (((t.w >> 16) & 0xFFu) & RSA_F_VALID);
     uint32_t gid;
-    if (kMode == kGivenAgg) {
-      gid = in ? (uint32_t)gin[i] : kNoGid;
+    if (kImg > 0) {
+      gid = classify_wave<false>(t, valid, R, (const lds_u32*)lds_img, flags);
     } else {
-      if (kImg > 0) {
-        gid = classify_wave<false>(t, valid, R, (const lds_u32*)lds_img, A.flags);
-      } else {
-        gid = classify_wave<false>(t, valid, R, R.img, A.flags);
-      }
-      const bool defer = gid == kDefer;
-      if (__syncthreads_or(defer)) {   // rare: workgroup-aggregated append
-        const unsigned long long pos = block_append(defer, tail_n, lds_app);
-        if (defer) tail[pos] = (uint32_t)i;
-      }
-      if (defer) continue;   // finished by k_tail
+      gid = classify_wave<false>(t, valid, R, R.img, flags);
     }
-    finish_line<kMode>(in, i, t, gid, TS, ORD, gout, gtag, R.n_rules, A);
+    const bool defer = gid == kDefer;
+    if (__syncthreads_or(defer)) {   // rare: workgroup-aggregated append
+      const unsigned long long pos = block_append(defer, tail_n, lds_app);
+      if (defer) tail[pos] = (uint32_t)i;
+    }
+    if (in && !defer) gout[i] = (int32_t)gid;
   }
 }
 
-// Pass 1, deferred lines: exact linear scan of their whole list.
-template <int kMode>
-__global__ __launch_bounds__(kBlock) void k_tail(const uint4* __restrict__ T, const uint32_t* __restrict__ TS,
-                                                 const unsigned long long* __restrict__ ORD, int32_t* __restrict__ gout,
-                                                 uint32_t* __restrict__ gtag, Rules R, Agg A,
-                                                 const uint32_t* __restrict__ tail, const unsigned long long* tail_n) {
+// Pass 1a, deferred lines: exact linear scan of their whole list.
+__global__ __launch_bounds__(kBlock) void k_tail(const uint4* __restrict__ T, int32_t* __restrict__ gout, Rules R,
+                                                 unsigned int* flags, const uint32_t* __restrict__ tail,
+                                                 const unsigned long long* tail_n) {
   const unsigned long long n = *tail_n;
   const unsigned long long stride = (unsigned long long)gridDim.x * kBlock;
   for (unsigned long long base = (unsigned long long)blockIdx.x * kBlock; base < n; base += stride) {
@@ -546,8 +573,8 @@ __global__ __launch_bounds__(kBlock) void k_tail(const uint4* __restrict__ T, co
     const unsigned long long i = in ? tail[j] : 0u;
     const uint4 t = in ? T[i] : make_uint4(0u, 0u, 0u, 0u);
     const bool valid = in && (((t.w >> 16) & 0xFFu) & RSA_F_VALID);
-    const uint32_t gid = classify_wave<true>(t, valid, R, R.img, A.flags);
-    finish_line<kMode>(in, i, t, gid, TS, ORD, gout, gtag, R.n_rules, A);
+    const uint32_t gid = classify_wave<true>(t, valid, R, R.img, flags);
+    if (in) gout[i] = (int32_t)gid;
   }
 }
 
@@ -571,46 +598,107 @@ __device__ __forceinline__ void wave_count2(bool m, bool h, uint32_t key, unsign
   }
 }
 
-// Per-rule line and hit counters from the gid|hit words of one pass-1 call:
-// privatised in LDS for up to kLds rules, flushed once per (persistent)
-// workgroup; wave-aggregated device atomics beyond that.
+// Pass 1b — the reducer's aggregation of classified lines
+// (connlist-reducer.py:62-79,146-176): per-rule line and hit counters
+// (privatised in LDS for up to kLds rules, flushed once per persistent
+// workgroup; wave-aggregated device atomics beyond that) and, for hit lines
+// the BUILT regex matched, the distinct-connection table.  Each lane takes
+// kU lines per iteration and issues their loads (gids and tuples, then order
+// keys and filter bounds, then the first slot probes) before using any of
+// them: the table probes are random HBM accesses, so memory-level parallelism
+// rather than instruction count sets the rate.  Lines whose rule is capped
+// with threshold bound filter[gid] < order cannot change any output and skip
+// the table.
+constexpr int kAggU = 4;
 template <int kLds>
-__global__ __launch_bounds__(1024) void k_count(const uint32_t* __restrict__ gtag, unsigned long long n,
-                                                uint32_t n_rules, unsigned long long* matches,
-                                                unsigned long long* hits) {
-  __shared__ uint32_t cnt[kLds > 0 ? 2 * kLds : 1];
+__global__ __launch_bounds__(1024) void k_aggregate(const uint4* __restrict__ T, const uint32_t* __restrict__ TS,
+                                                    const unsigned long long* __restrict__ ORD,
+                                                    const int32_t* __restrict__ G, unsigned long long n,
+                                                    uint32_t n_rules, Agg A) {
+  __shared__ uint32_t cnt[kLds > 0 ? 3 * kLds : 1];   // matches, hits, distinct
+  const bool counters = !(A.skip & 1u);
   if (kLds > 0) {
-    for (uint32_t r = threadIdx.x; r < 2u * kLds; r += blockDim.x) cnt[r] = 0;
+    for (uint32_t r = threadIdx.x; r < 3u * kLds; r += blockDim.x) cnt[r] = 0;
     __syncthreads();
   }
-  const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x * 4;
-  for (unsigned long long base = ((unsigned long long)blockIdx.x * blockDim.x + threadIdx.x) * 4; base < n;
-       base += stride) {
-    uint32_t w[4];
-    if (base + 4 <= n && (base & 3) == 0) {
-      const uint4 v = *reinterpret_cast<const uint4*>(gtag + base);
-      w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
-    } else {
-      for (int k = 0; k < 4; ++k) w[k] = base + k < n ? gtag[base + k] : 0xFFFFFFFFu;
+  uint32_t st[4] = {0u, 0u, 0u, 0u};
+  uint32_t* stp = A.stats ? st : nullptr;
+  const bool table = A.cap > 0 && !(A.skip & 2u);
+  const unsigned long long span = (unsigned long long)blockDim.x * kAggU;
+  for (unsigned long long base = (unsigned long long)blockIdx.x * span; base < n;
+       base += (unsigned long long)gridDim.x * span) {
+    uint32_t gid[kAggU];
+    uint4 t[kAggU];
+#pragma unroll
+    for (int k = 0; k < kAggU; ++k) {
+      const unsigned long long i = base + (unsigned long long)k * blockDim.x + threadIdx.x;
+      const bool in = i < n;
+      gid[k] = in ? (uint32_t)G[i] : kNoGid;
+      t[k] = in ? T[i] : make_uint4(0u, 0u, 0u, 0u);
     }
-    for (int k = 0; k < 4; ++k) {
-      const bool m = w[k] != 0xFFFFFFFFu;
-      const uint32_t g = w[k] & ~kTagHit;
-      const bool h = m && (w[k] & kTagHit);
-      if (kLds > 0) {
-        if (m) atomicAdd(&cnt[g], 1u);
-        if (h) atomicAdd(&cnt[kLds + g], 1u);
-      } else {
-        wave_count2(m, h, g, matches, hits);
+    bool need[kAggU];
+    unsigned long long o[kAggU], f[kAggU];
+#pragma unroll
+    for (int k = 0; k < kAggU; ++k) {
+      const unsigned long long i = base + (unsigned long long)k * blockDim.x + threadIdx.x;
+      const uint32_t flags = (t[k].w >> 16) & 0xFFu;
+      if (gid[k] != kNoGid && gid[k] >= n_rules) atomicOr(&A.flags[1], 2u);
+      const bool matched = gid[k] < n_rules;
+      const bool hit = matched && (flags & RSA_F_HIT);
+      if (counters) {
+        if (kLds > 0) {
+          if (matched) atomicAdd(&cnt[gid[k]], 1u);
+          if (hit) atomicAdd(&cnt[kLds + gid[k]], 1u);
+        } else {
+          wave_count2(matched, hit, gid[k], A.matches, A.hits);
+        }
       }
+      need[k] = table && hit && (flags & RSA_F_BUILT);
+      o[k] = need[k] ? ORD[i] : 0ull;
+      f[k] = need[k] ? A.filter[gid[k]] : 0ull;
+    }
+    unsigned long long kA[kAggU], kB[kAggU], h[kAggU];
+    uint32_t ts[kAggU];
+    SlotHead hd[kAggU];
+#pragma unroll
+    for (int k = 0; k < kAggU; ++k) {
+      const unsigned long long i = base + (unsigned long long)k * blockDim.x + threadIdx.x;
+      need[k] = need[k] && o[k] <= f[k];   // exact skip: capped with threshold <= filter < order
+      if (need[k]) {
+        conn_key(t[k], gid[k], kA[k], kB[k]);
+        h[k] = slot_hash(kA[k], kB[k]) & A.mask;
+        hd[k] = load_head(&A.slots[h[k]]);
+        ts[k] = TS[i];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kAggU; ++k) {
+      bool fresh = false;
+      unsigned long long slot = kEmpty;
+      if (need[k]) slot = table_combine_at(A, kA[k], kB[k], 1u, ts[k], ts[k], o[k], &fresh, h[k], hd[k], stp);
+      if (kLds > 0) {
+        if (fresh) atomicAdd(&cnt[2 * kLds + gid[k]], 1u);
+      } else {
+        wave_count_by_key(fresh, gid[k], A.distinct);
+      }
+      const unsigned long long pos = wave_append(fresh, A.used_n);
+      if (fresh) A.used[pos] = (uint32_t)slot;
     }
   }
   if (kLds > 0) {
     __syncthreads();
     for (uint32_t r = threadIdx.x; r < n_rules; r += blockDim.x) {
-      const uint32_t m = cnt[r], h = cnt[kLds + r];
-      if (m) atomicAdd(&matches[r], (unsigned long long)m);
-      if (h) atomicAdd(&hits[r], (unsigned long long)h);
+      const uint32_t m = cnt[r], hh = cnt[kLds + r], d = cnt[2 * kLds + r];
+      if (m) atomicAdd(&A.matches[r], (unsigned long long)m);
+      if (hh) atomicAdd(&A.hits[r], (unsigned long long)hh);
+      if (d) atomicAdd(&A.distinct[r], d);
+    }
+  }
+  if (A.stats) {
+    for (int q = 0; q < 4; ++q) {
+      unsigned long long v = st[q];
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+      if (__lane_id() == 0 && v) atomicAdd(&A.stats[q], v);
     }
   }
 }
@@ -652,9 +740,9 @@ __device__ __forceinline__ void slot_clear(Slot* S, unsigned long long i) {
   s.kA = 0;
   s.kB = kEmpty;
   s.min_order = kEmpty;
-  s.count = 0;
   s.first = 0xFFFFFFFFu;
   s.last = 0;
+  s.count = 0;
   s.count2 = 0;
   s.first2 = 0xFFFFFFFFu;
   s.last2 = 0;
@@ -949,14 +1037,15 @@ struct rsa_ctx {
   bool auto_tighten = true;
   bool tightened = false;
   uint32_t profile_skip = 0;
+  bool precheck = true;
+  bool stats_on = false;
+  unsigned long long* d_stats = nullptr;   // 4 counters (RSA_OPT_STATS)
   uint32_t filter_slice = 256;
   uint32_t filter_steps = 3;          // auto filter: bound refinements (each after 4x the previous lines)
   uint32_t* d_tail = nullptr;         // deferred line indices
   unsigned long long* d_tail_n = nullptr;
   unsigned long long tail_alloc = 0;
-  uint32_t* d_gtag = nullptr;         // per-line gid|hit words of the current pass-1 call
-  unsigned long long gtag_alloc = 0;
-  int32_t* d_gscratch = nullptr;      // classify-only gids for a recount without pass-1 gids
+  int32_t* d_gscratch = nullptr;      // gids of a pass 1 / recount whose caller keeps none
   unsigned long long gscratch_alloc = 0;
   unsigned int* d_flags = nullptr;       // 4 words
   unsigned long long* d_cursor = nullptr;
@@ -969,7 +1058,7 @@ struct rsa_ctx {
   unsigned long long* d_keys = nullptr;   // capped rules' min_order keys, one segment per rule
   unsigned long long sort_alloc = 0;
   // pass-1 kernel timing (HIP events on the ctx stream)
-  hipEvent_t ev[32] = {};
+  hipEvent_t ev[48] = {};             // per pass-1 launch: start, classified, aggregated
   int ev_used = 0;
 };
 
@@ -1021,6 +1110,8 @@ Agg agg_of(const rsa_ctx* c) {
   a.flags = c->d_flags;
   a.cap = c->cap;
   a.skip = c->profile_skip;
+  a.precheck = c->precheck ? 1u : 0u;
+  a.stats = c->stats_on ? c->d_stats : nullptr;
   return a;
 }
 
@@ -1158,7 +1249,7 @@ int ensure_buf(rsa_ctx* c, T** p, unsigned long long* have, unsigned long long n
   return RSA_OK;
 }
 
-constexpr int kMaxEvents = 32;
+constexpr int kMaxEvents = 48;
 
 int ensure_events(rsa_ctx* c) {
   for (int k = 0; k < kMaxEvents; ++k)
@@ -1170,84 +1261,80 @@ int ensure_events(rsa_ctx* c) {
 constexpr int kImgSmall = kImgSmallMax;   // 62.5 KiB: two 1024-thread workgroups per CU (32 waves)
 constexpr int kImgLarge = 38912;   // 152 KiB: one workgroup per CU
 
-// Classification launch + exact tail for lines [0, m) of T (already offset).
-template <int kMode>
-int launch_classify(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsigned long long* o, uint64_t m,
-                    const int32_t* gi, int32_t* go, uint32_t* gt) {
+// Classification (+ exact tail) of lines [0, m) of T (already offset) into go.
+int launch_classify(rsa_ctx* c, const uint4* t, uint64_t m, int32_t* go) {
   const Rules r = rules_of(c);
-  const Agg ag = agg_of(c);
   int rc = ensure_tail(c, m);
   if (rc) return rc;
   HIPCHK(c, hipMemsetAsync(c->d_tail_n, 0, sizeof(unsigned long long), c->stream));
-  const bool lds = kMode != kGivenAgg && c->indexed;
-  if (lds && c->img_words <= (uint32_t)kImgSmall) {
-    k_classify<kMode, kImgSmall><<<grid_for_threads(c, m, 1024, 2), 1024, 0, c->stream>>>(
-        t, ts, o, m, gi, go, gt, r, ag, c->d_tail, c->d_tail_n);
-  } else if (lds && c->img_words <= (uint32_t)kImgLarge) {
-    k_classify<kMode, kImgLarge><<<grid_for_threads(c, m, 1024, 1), 1024, 0, c->stream>>>(
-        t, ts, o, m, gi, go, gt, r, ag, c->d_tail, c->d_tail_n);
+  if (c->indexed && c->img_words <= (uint32_t)kImgSmall) {
+    k_classify<kImgSmall><<<grid_for_threads(c, m, 1024, 2), 1024, 0, c->stream>>>(t, m, go, r, c->d_flags, c->d_tail,
+                                                                                 c->d_tail_n);
+  } else if (c->indexed && c->img_words <= (uint32_t)kImgLarge) {
+    k_classify<kImgLarge><<<grid_for_threads(c, m, 1024, 1), 1024, 0, c->stream>>>(t, m, go, r, c->d_flags, c->d_tail,
+                                                                                 c->d_tail_n);
   } else {
-    k_classify<kMode, 0><<<grid_for_threads(c, m, 1024, 2), 1024, 0, c->stream>>>(t, ts, o, m, gi, go, gt, r, ag,
-                                                                                c->d_tail, c->d_tail_n);
+    k_classify<0><<<grid_for_threads(c, m, 1024, 2), 1024, 0, c->stream>>>(t, m, go, r, c->d_flags, c->d_tail,
+                                                                         c->d_tail_n);
   }
   HIPCHK(c, hipGetLastError());
-  if (kMode != kGivenAgg) {
-    // deferred lines (their number is read on the device: no host sync)
-    k_tail<kMode><<<c->cu_count * 4, kBlock, 0, c->stream>>>(t, ts, o, go, gt, r, ag, c->d_tail, c->d_tail_n);
-    HIPCHK(c, hipGetLastError());
-  }
+  // deferred lines (their number is read on the device: no host sync)
+  k_tail<<<c->cu_count * 4, kBlock, 0, c->stream>>>(t, go, r, c->d_flags, c->d_tail, c->d_tail_n);
+  HIPCHK(c, hipGetLastError());
   return RSA_OK;
 }
 
-// LDS-privatised counter capacities (rules): 2 x 4 B per rule.
-constexpr int kCntSmall = 10240;   // 80 KiB: two 1024-thread workgroups per CU
-constexpr int kCntLarge = 20480;   // 160 KiB: one workgroup per CU
+// LDS-privatised counter capacity (rules): 3 x 4 B per rule, 156 KiB.  One
+// 1024-thread workgroup per CU (k_aggregate's registers allow no more).
+constexpr int kCnt = 13312;
 
-int launch_count(rsa_ctx* c, const uint32_t* gt, uint64_t m) {
-  if (c->profile_skip & 1u) return RSA_OK;
-  const uint64_t quads = (m + 3) / 4;
-  if (c->n_rules <= (uint32_t)kCntSmall) {
-    k_count<kCntSmall><<<grid_for_threads(c, quads, 1024, 2), 1024, 0, c->stream>>>(gt, m, c->n_rules, c->d_matches,
-                                                                                    c->d_hits);
-  } else if (c->n_rules <= (uint32_t)kCntLarge) {
-    k_count<kCntLarge><<<grid_for_threads(c, quads, 1024, 1), 1024, 0, c->stream>>>(gt, m, c->n_rules, c->d_matches,
-                                                                                    c->d_hits);
+int launch_aggregate(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsigned long long* o, const int32_t* g,
+                     uint64_t m) {
+  const Agg ag = agg_of(c);
+  const uint64_t units = (m + kAggU - 1) / kAggU;
+  if (c->n_rules <= (uint32_t)kCnt) {
+    k_aggregate<kCnt><<<grid_for_threads(c, units, 1024, 1), 1024, 0, c->stream>>>(t, ts, o, g, m, c->n_rules, ag);
   } else {
-    k_count<0><<<grid_for_threads(c, quads, 1024, 4), 1024, 0, c->stream>>>(gt, m, c->n_rules, c->d_matches,
-                                                                            c->d_hits);
+    k_aggregate<0><<<grid_for_threads(c, units, 1024, 1), 1024, 0, c->stream>>>(t, ts, o, g, m, c->n_rules, ag);
   }
   HIPCHK(c, hipGetLastError());
   return RSA_OK;
 }
 
-// Pass 1 over one batch.  With auto-tightening, a large first batch is split:
-// the first 1/filter_slice builds the table, the filter is computed, and the
-// rest of the batch skips the table for lines that cannot change any output;
-// with filter_steps > 1 the filter is refined again after 4x, 16x, ... that
-// many lines.
-int run_pass1(rsa_ctx* c, int mode, const rsa_tuple* T, const uint32_t* TS, const uint64_t* ORD, const int32_t* G,
+// Pass 1 over one batch: classification into gids (gout, or the ctx scratch),
+// then aggregation of the classified lines; with given gids (reducer drop-in)
+// aggregation only.  With auto-tightening, a large first batch is split: the
+// first 1/filter_slice builds the table, the filter is computed, and the rest
+// of the batch skips the table for lines that cannot change any output; with
+// filter_steps > 1 the filter is refined again after 4x, 16x, ... that many
+// lines.
+int run_pass1(rsa_ctx* c, int classify, const rsa_tuple* T, const uint32_t* TS, const uint64_t* ORD, const int32_t* G,
               int32_t* gout, uint64_t n) {
   int rc = ensure_events(c);
   if (rc) return rc;
   c->ev_used = 0;
   if (n > 0x7FFFFFFFull) return fail(c, RSA_ERR_ARG, "batch larger than 2^31 tuples: split it");
-  rc = ensure_buf(c, &c->d_gtag, &c->gtag_alloc, n);
-  if (rc) return rc;
+  if (classify && !gout) {
+    rc = ensure_buf(c, &c->d_gscratch, &c->gscratch_alloc, n);
+    if (rc) return rc;
+    gout = c->d_gscratch;
+  }
   auto launch = [&](uint64_t a, uint64_t m) -> int {
     if (m == 0) return RSA_OK;
-    if (c->ev_used + 2 > kMaxEvents) return fail(c, RSA_ERR_STATE, "too many pass-1 launches in one call");
+    if (c->ev_used + 3 > kMaxEvents) return fail(c, RSA_ERR_STATE, "too many pass-1 launches in one call");
     const uint4* t = reinterpret_cast<const uint4*>(T) + a;
     const unsigned long long* o = reinterpret_cast<const unsigned long long*>(ORD) + a;
     HIPCHK(c, hipEventRecord(c->ev[c->ev_used], c->stream));
-    int32_t* go = gout ? gout + a : nullptr;
-    const int32_t* gi = G ? G + a : nullptr;
-    int rc2 = mode == kClassifyAgg ? launch_classify<kClassifyAgg>(c, t, TS + a, o, m, nullptr, go, c->d_gtag + a)
-                                   : launch_classify<kGivenAgg>(c, t, TS + a, o, m, gi, nullptr, c->d_gtag + a);
-    if (rc2) return rc2;
-    rc2 = launch_count(c, c->d_gtag + a, m);
-    if (rc2) return rc2;
+    const int32_t* g = G ? G + a : gout + a;
+    if (classify) {
+      const int rc2 = launch_classify(c, t, m, gout + a);
+      if (rc2) return rc2;
+    }
     HIPCHK(c, hipEventRecord(c->ev[c->ev_used + 1], c->stream));
-    c->ev_used += 2;
+    const int rc2 = launch_aggregate(c, t, TS + a, o, g, m);
+    if (rc2) return rc2;
+    HIPCHK(c, hipEventRecord(c->ev[c->ev_used + 2], c->stream));
+    c->ev_used += 3;
     return RSA_OK;
   };
   c->table_dirty = true;
@@ -1324,7 +1411,7 @@ int rsa_ctx_destroy(rsa_ctx* c) {
   if (!c) return RSA_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->d_tail, c->d_tail_n, c->d_gtag, c->d_gscratch, c->d_entries, c->d_off,
+  void* bufs[] = {c->d_tail, c->d_tail_n, c->d_gscratch, c->d_stats, c->d_entries, c->d_off,
                   c->d_img, c->d_resid,
                   c->d_slots, c->d_used, c->d_used_n, c->d_filter, c->d_flags, c->d_cursor, c->d_cidx,
                   c->d_capped_gid, c->d_capped_cnt, c->d_capped_start, c->d_keys};
@@ -1362,6 +1449,16 @@ int rsa_set_option(rsa_ctx* c, int option, int64_t value) {
       return RSA_OK;
     case RSA_OPT_PROFILE_SKIP:
       c->profile_skip = (uint32_t)value;
+      return RSA_OK;
+    case RSA_OPT_PRECHECK:
+      c->precheck = value != 0;
+      return RSA_OK;
+    case RSA_OPT_STATS:
+      if (value && !c->d_stats) {
+        HIPCHK(c, hipMalloc(&c->d_stats, 4 * sizeof(unsigned long long)));
+        HIPCHK(c, hipMemset(c->d_stats, 0, 4 * sizeof(unsigned long long)));
+      }
+      c->stats_on = value != 0;
       return RSA_OK;
     case RSA_OPT_USE_INDEX:
       if (value && !c->index_loaded) return fail(c, RSA_ERR_STATE, "no index loaded");
@@ -1566,7 +1663,7 @@ int rsa_classify(rsa_ctx* c, const rsa_tuple* T, const uint32_t* TS, const uint6
   if (rc) return rc;
   if (n == 0) return RSA_OK;
   if (!T || !TS || !ORD) return fail(c, RSA_ERR_ARG, "null tuple/ts/order pointer");
-  return run_pass1(c, kClassifyAgg, T, TS, ORD, nullptr, gout, n);
+  return run_pass1(c, 1, T, TS, ORD, nullptr, gout, n);
 }
 
 int rsa_classify_only(rsa_ctx* c, const rsa_tuple* T, uint64_t n, int32_t* gout) {
@@ -1576,8 +1673,7 @@ int rsa_classify_only(rsa_ctx* c, const rsa_tuple* T, uint64_t n, int32_t* gout)
   if (!T || !gout) return fail(c, RSA_ERR_ARG, "null tuple/gid pointer");
   if (!c->d_flags) return fail(c, RSA_ERR_STATE, "ctx not initialised");
   if (n > 0x7FFFFFFFull) return fail(c, RSA_ERR_ARG, "batch larger than 2^31 tuples");
-  return launch_classify<kClassifyOnly>(c, reinterpret_cast<const uint4*>(T), nullptr, nullptr, n, nullptr, gout,
-                                        nullptr);
+  return launch_classify(c, reinterpret_cast<const uint4*>(T), n, gout);
 }
 
 int rsa_aggregate_gids(rsa_ctx* c, const rsa_tuple* T, const uint32_t* TS, const uint64_t* ORD, const int32_t* G,
@@ -1587,19 +1683,31 @@ int rsa_aggregate_gids(rsa_ctx* c, const rsa_tuple* T, const uint32_t* TS, const
   if (rc) return rc;
   if (n == 0) return RSA_OK;
   if (!T || !TS || !ORD || !G) return fail(c, RSA_ERR_ARG, "null tuple/ts/order/gid pointer");
-  return run_pass1(c, kGivenAgg, T, TS, ORD, G, nullptr, n);
+  return run_pass1(c, 0, T, TS, ORD, G, nullptr, n);
+}
+
+int rsa_last_pass1_times(rsa_ctx* c, float* h_classify_ms, float* h_aggregate_ms) {
+  if (!c || !h_classify_ms || !h_aggregate_ms) return RSA_ERR_ARG;
+  float tc = 0.f, ta = 0.f;
+  for (int k = 0; k + 3 <= c->ev_used; k += 3) {
+    HIPCHK(c, hipEventSynchronize(c->ev[k + 2]));
+    float a = 0.f, b = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&a, c->ev[k], c->ev[k + 1]));
+    HIPCHK(c, hipEventElapsedTime(&b, c->ev[k + 1], c->ev[k + 2]));
+    tc += a;
+    ta += b;
+  }
+  *h_classify_ms = tc;
+  *h_aggregate_ms = ta;
+  return RSA_OK;
 }
 
 int rsa_last_pass1_ms(rsa_ctx* c, float* h_ms) {
-  if (!c || !h_ms) return RSA_ERR_ARG;
-  float total = 0.f;
-  for (int k = 0; k + 1 < c->ev_used; k += 2) {
-    HIPCHK(c, hipEventSynchronize(c->ev[k + 1]));
-    float ms = 0.f;
-    HIPCHK(c, hipEventElapsedTime(&ms, c->ev[k], c->ev[k + 1]));
-    total += ms;
-  }
-  *h_ms = total;
+  if (!h_ms) return RSA_ERR_ARG;
+  float a = 0.f, b = 0.f;
+  const int rc = rsa_last_pass1_times(c, &a, &b);
+  if (rc) return rc;
+  *h_ms = a + b;
   return RSA_OK;
 }
 
@@ -1651,6 +1759,18 @@ int rsa_import(rsa_ctx* c, int which, const rsa_conn_record* in, uint64_t n) {
   c->table_dirty = true;
   k_import<<<grid_for(c, n, 16), kBlock, 0, c->stream>>>(in, n, which, agg_of(c));
   HIPCHK(c, hipGetLastError());
+  return RSA_OK;
+}
+
+int rsa_stats(rsa_ctx* c, uint64_t* h_out, int reset) {
+  if (!c || !h_out) return RSA_ERR_ARG;
+  if (!c->d_stats) {
+    for (int k = 0; k < 4; ++k) h_out[k] = 0;
+    return RSA_OK;
+  }
+  HIPCHK(c, hipMemcpyAsync(h_out, c->d_stats, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (reset) HIPCHK(c, hipMemsetAsync(c->d_stats, 0, 4 * sizeof(uint64_t), c->stream));
   return RSA_OK;
 }
 

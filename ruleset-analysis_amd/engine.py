@@ -105,6 +105,12 @@ class Engine(object):
     def auto_filter(self, on):
         self.set_option(native.RSA_OPT_AUTO_FILTER, 1 if on else 0)
 
+    def last_pass1_times(self):
+        """(classification ms, aggregation ms) of the last pass-1 call (HIP events on the ctx stream)."""
+        a, b = ctypes.c_float(0), ctypes.c_float(0)
+        self.ctx.call('rsa_last_pass1_times', ctypes.byref(a), ctypes.byref(b))
+        return float(a.value), float(b.value)
+
     def last_pass1_ms(self):
         ms = ctypes.c_float(0)
         self.ctx.call('rsa_last_pass1_ms', ctypes.byref(ms))
@@ -155,6 +161,12 @@ class Engine(object):
     def pass2(self, b, gids=None):
         g = b.gids if b.gids is not None else gids
         self.ctx.call('rsa_recount', _ptr(b.tuples), _ptr(b.ts), _ptr(b.order), _ptr(g), ctypes.c_uint64(b.n))
+
+    def stats(self, reset=True):
+        """Profiling counters (RSA_OPT_STATS): table lines, extra probes, atomic-path probes, slot atomics."""
+        out = (ctypes.c_uint64 * 4)()
+        self.ctx.call('rsa_stats', out, ctypes.c_int(1 if reset else 0))
+        return [int(v) for v in out]
 
     def table_size(self):
         n = ctypes.c_uint64(0)

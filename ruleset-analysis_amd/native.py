@@ -32,6 +32,8 @@ class NativeError(RuntimeError):
 RSA_OK, RSA_ERR_ARG, RSA_ERR_HIP, RSA_ERR_STATE, RSA_ERR_CAPACITY = 0, -1, -2, -3, -4
 RSA_OPT_AUTO_FILTER, RSA_OPT_USE_INDEX, RSA_OPT_PROFILE_SKIP, RSA_OPT_FILTER_SLICE, RSA_OPT_FILTER_STEPS = 1, 2, 3, 5, 7
 RSA_OPT_FORCE_DEFER = 8
+RSA_OPT_PRECHECK = 9
+RSA_OPT_STATS = 10
 
 P = ctypes.c_void_p
 U32 = ctypes.c_uint32
@@ -50,6 +52,7 @@ SYMBOLS = {
     'rsa_set_option': (I32, [P, I32, ctypes.c_int64]),
     'rsa_load_index': (I32, [P, P, U32, P, U32]),
     'rsa_last_pass1_ms': (I32, [P, ctypes.POINTER(ctypes.c_float)]),
+    'rsa_last_pass1_times': (I32, [P, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
     'rsa_load_rules': (I32, [P, P, U32, P, U32, U32]),
     'rsa_bind_counters': (I32, [P, P, P, P, P]),
     'rsa_set_rule_count': (I32, [P, U32]),
@@ -61,6 +64,7 @@ SYMBOLS = {
     'rsa_recount': (I32, [P, P, P, P, P, U64]),
     'rsa_emit': (I32, [P, P, U64, PU64]),
     'rsa_table_size': (I32, [P, PU64]),
+    'rsa_stats': (I32, [P, PU64, I32]),
     'rsa_export': (I32, [P, I32, P, U64, PU64]),
     'rsa_import': (I32, [P, I32, P, U64]),
     'rsa_sync': (I32, [P]),

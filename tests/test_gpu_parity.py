@@ -167,7 +167,17 @@ def test_synth_parity_filter_steps(engine):
         _gpu_vs_oracle(engine, 1500, 5_000_000, 40, seed=24, zipf=1.1, broad=False,
                        interfaces=('outside', 'partner'))
     finally:
-        engine.set_option(native.RSA_OPT_FILTER_STEPS, 1)
+        engine.set_option(native.RSA_OPT_FILTER_STEPS, 3)
+
+
+def test_synth_parity_no_precheck(engine):
+    """Slot updates without the plain-load pre-check (every field by atomics)."""
+    from ruleset_analysis_amd import native
+    engine.set_option(native.RSA_OPT_PRECHECK, 0)
+    try:
+        _gpu_vs_oracle(engine, 1500, 5_000_000, 40, seed=26, zipf=1.1, broad=False, shuffle=True)
+    finally:
+        engine.set_option(native.RSA_OPT_PRECHECK, 1)
 
 
 def test_deterministic(engine):

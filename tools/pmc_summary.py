@@ -32,14 +32,21 @@ def main():
         int(sys.argv[5])
     f, fn = per_dispatch(fetch_csv, 'FETCH_SIZE')
     w, wn = per_dispatch(write_csv, 'WRITE_SIZE')
-    # every classify+aggregate launch of pass 1 (main slices and their deferred tails)
-    fk = [v for d, v in sorted(f.items()) if 'k_pass1<0,' in fn[d]]
-    wk = [v for d, v in sorted(w.items()) if 'k_pass1<0,' in wn[d]]
+    # every pass-1 launch (classification, deferred tails, aggregation) of every slice
+    kinds = ('k_classify', 'k_tail', 'k_aggregate')
+    pick = lambda name: any(k in name for k in kinds)
+    fk = [v for d, v in sorted(f.items()) if pick(fn[d])]
+    wk = [v for d, v in sorted(w.items()) if pick(wn[d])]
     read = 2 * 1024 * sum(fk) / steps
     write = 1024 * sum(wk) / steps
+    split = {}
+    for k in kinds:
+        split[k] = {'read_bytes_per_step': 2 * 1024 * sum(v for d, v in f.items() if k in fn[d]) / steps,
+                    'write_bytes_per_step': 1024 * sum(v for d, v in w.items() if k in wn[d]) / steps}
     res = {'hbm_bytes_per_step': read + write, 'read_bytes_per_step': read, 'write_bytes_per_step': write,
            'lines_per_step': lines, 'steps_seen': steps, 'bytes_per_line': (read + write) / lines,
-           'method': 'rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes), k_pass1 launches, '
+           'kernels': split,
+           'method': 'rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes), pass-1 launches, '
                      'FETCH_SIZE x2 gfx950 correction'}
     json.dump(res, open(out, 'w'), indent=1)
     print(json.dumps(res))
