@@ -106,13 +106,16 @@ struct Agg {
   const unsigned long long* filter;  // per rule: lines with order > filter cannot matter
   Slot* slots;
   unsigned long long mask;           // capacity - 1 (power of two)
-  uint32_t* used;                    // used-slot list
+  unsigned long long* used;          // used-slot list: gid << 32 | slot
   unsigned long long* used_n;
   unsigned int* flags;               // [0] overflow, [1] bad gid/list/state
   uint32_t cap;
   uint32_t skip;                     // profiling only (RSA_OPT_PROFILE_SKIP): 1 counters, 2 table, 4 table updates
   uint32_t precheck;                 // RSA_OPT_PRECHECK: plain-load pre-check of the monotone slot fields
   unsigned long long* stats;         // RSA_OPT_STATS: [0] table lines, [1] extra probes, [2] atomic-path probes, [3] atomics
+  uint32_t* occ;                     // occupancy bitmap of the slots (one bit per slot)
+  uint32_t rs_bits;                  // region = 2^rs_bits slots (linear probing wraps inside a region)
+  uint32_t np_bits;                  // 2^np_bits regions; a key's region = top np_bits of its slot hash
 };
 
 __device__ __forceinline__ unsigned long long mix64(unsigned long long x) {
@@ -154,6 +157,17 @@ __device__ __forceinline__ unsigned long long wave_append(bool ok, unsigned long
   if ((int)lane == leader) base = atomicAdd(cursor, (unsigned long long)__popcll(mask));
   base = __shfl(base, leader);
   return base + __popcll(mask & ((1ull << lane) - 1ull));
+}
+
+// Home slot of a key hash: region = top np_bits, offset = low rs_bits.
+__device__ __forceinline__ unsigned long long slot_home(const Agg& A, unsigned long long hh) {
+  const unsigned long long r = A.np_bits ? (hh >> (64 - A.np_bits)) : 0ull;
+  return (r << A.rs_bits) | (hh & ((1ull << A.rs_bits) - 1ull));
+}
+
+__device__ __forceinline__ unsigned long long slot_next(const Agg& A, unsigned long long s) {
+  const unsigned long long m = (1ull << A.rs_bits) - 1ull;
+  return (s & ~m) | ((s + 1ull) & m);
 }
 
 // Reducer key of a tuple (connlist-reducer.py:162: PROTO;FROMIP;TOIP;TOPORT).
@@ -405,6 +419,32 @@ __device__ __forceinline__ SlotHead load_head(const Slot* c) {
   return r;
 }
 
+// Combine one occurrence into an existing entry s whose head snapshot is hd;
+// returns the number of atomics issued.
+__device__ __forceinline__ uint32_t slot_update(const Agg& A, Slot* s, const SlotHead& hd, unsigned int cnt,
+                                                unsigned int first, unsigned int last, unsigned long long order) {
+  if (A.skip & 4u) return 0;   // profiling only
+  atomicAdd(&s->count, cnt);
+  const unsigned long long mo = ((unsigned long long)hd.m.y << 32) | hd.m.x;
+  const bool all = !A.precheck;
+  const bool u0 = all || order < mo, u1 = all || first < hd.m.z, u2 = all || last > hd.m.w;
+  if (u0) atomicMin(&s->min_order, order);
+  if (u1) atomicMin(&s->first, first);
+  if (u2) atomicMax(&s->last, last);
+  return 1u + u0 + u1 + u2;
+}
+
+// Agent-scope (write-through) stores of a claimed slot's key half kA and its
+// aggregates; the caller waits for them before publishing kB.
+__device__ __forceinline__ void slot_init(Slot* c, unsigned long long kA, unsigned int cnt, unsigned int first,
+                                          unsigned int last, unsigned long long order) {
+  __hip_atomic_store(&c->kA, kA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&c->min_order, order, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(&c->first), ((unsigned long long)last << 32) | first,
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&c->count, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ unsigned long long table_combine_at(const Agg& A, unsigned long long kA,
                                                                unsigned long long kB, unsigned int cnt,
                                                                unsigned int first, unsigned int last,
@@ -430,11 +470,8 @@ __device__ __forceinline__ unsigned long long table_combine_at(const Agg& A, uns
         // aggregates with agent-scope (write-through) stores, wait for them to
         // complete, then publish kB.  Finders only update the fields after they
         // have seen kB, so their atomics act on these values.
-        __hip_atomic_store(&c->kA, kA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&c->min_order, order, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(reinterpret_cast<unsigned long long*>(&c->first),
-                           ((unsigned long long)last << 32) | first, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&c->count, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        slot_init(c, kA, cnt, first, last, order);
+        atomicOr(&A.occ[h >> 5], 1u << (h & 31));
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         atomicExch(&c->kB, kB);
         *fresh = true;
@@ -455,28 +492,20 @@ __device__ __forceinline__ unsigned long long table_combine_at(const Agg& A, uns
         break;
       }
     }
-    h = (h + 1) & A.mask;
-    if (++probes > A.mask) break;
+    h = slot_next(A, h);
+    if (++probes >= (1ull << A.rs_bits)) break;
     hd = load_head(&A.slots[h]);
   }
   if (found == kEmpty) {
     atomicOr(&A.flags[0], 1u);
     return kEmpty;
   }
-  Slot* s = &A.slots[found];
-  if (A.skip & 4u) return found;   // profiling only
-  atomicAdd(&s->count, cnt);
-  const unsigned long long mo = ((unsigned long long)hd.m.y << 32) | hd.m.x;
-  const bool all = !A.precheck;
-  const bool u0 = all || order < mo, u1 = all || first < hd.m.z, u2 = all || last > hd.m.w;
-  if (u0) atomicMin(&s->min_order, order);
-  if (u1) atomicMin(&s->first, first);
-  if (u2) atomicMax(&s->last, last);
+  const uint32_t n_at = slot_update(A, &A.slots[found], hd, cnt, first, last, order);
   if (st) {
     st[0] += 1;
     st[1] += (uint32_t)probes;
     st[2] += (uint32_t)atomic_probes;
-    st[3] += 1u + u0 + u1 + u2 + (atomic_probes ? 1u : 0u);
+    st[3] += n_at + (uint32_t)atomic_probes;
   }
   return found;
 }
@@ -485,20 +514,20 @@ __device__ __forceinline__ unsigned long long table_combine(const Agg& A, unsign
                                                             unsigned long long kB, unsigned int cnt,
                                                             unsigned int first, unsigned int last,
                                                             unsigned long long order, bool* fresh) {
-  const unsigned long long h = slot_hash(kA, kB) & A.mask;
+  const unsigned long long h = slot_home(A, slot_hash(kA, kB));
   return table_combine_at(A, kA, kB, cnt, first, last, order, fresh, h, load_head(&A.slots[h]));
 }
 
 // Find an existing key (after pass 1 completed: plain loads are coherent across
 // the kernel boundary).
 __device__ __forceinline__ Slot* table_find(const Agg& A, unsigned long long kA, unsigned long long kB) {
-  unsigned long long h = slot_hash(kA, kB) & A.mask;
-  for (unsigned long long probes = 0; probes <= A.mask; ++probes) {
+  unsigned long long h = slot_home(A, slot_hash(kA, kB));
+  for (unsigned long long probes = 0; probes < (1ull << A.rs_bits); ++probes) {
     Slot* c = &A.slots[h];
     const unsigned long long cb = c->kB;
     if (cb == kEmpty) return nullptr;
     if (cb == kB && c->kA == kA) return c;
-    h = (h + 1) & A.mask;
+    h = slot_next(A, h);
   }
   return nullptr;
 }
@@ -598,31 +627,73 @@ __device__ __forceinline__ void wave_count2(bool m, bool h, uint32_t key, unsign
   }
 }
 
-// Pass 1b — the reducer's aggregation of classified lines
-// (connlist-reducer.py:62-79,146-176): per-rule line and hit counters
-// (privatised in LDS for up to kLds rules, flushed once per persistent
-// workgroup; wave-aggregated device atomics beyond that) and, for hit lines
-// the BUILT regex matched, the distinct-connection table.  Each lane takes
-// kU lines per iteration and issues their loads (gids and tuples, then order
-// keys and filter bounds, then the first slot probes) before using any of
-// them: the table probes are random HBM accesses, so memory-level parallelism
-// rather than instruction count sets the rate.  Lines whose rule is capped
-// with threshold bound filter[gid] < order cannot change any output and skip
-// the table.
+// ---- Pass 1b — the reducer's aggregation of classified lines
+// (connlist-reducer.py:62-79,146-176), as an on-chip shuffle.
+//
+// The distinct-connection table is split into regions of 2^rs_bits slots; a
+// key's region is the top np_bits of its slot hash and its home slot lies in
+// that region (linear probing wraps inside it).  Table writes are scattered
+// memory transactions (the chip sustains ~20 G/s of them against ~125 G/s of
+// 64-B streaming lines), so instead of one read-modify-write per line:
+//   k_aggregate   per-rule line/hit counters (LDS histogram) and, for each hit
+//                 line the BUILT regex matched that can still change an output
+//                 (order <= filter[gid]), a 32-B record appended in line order;
+//   k_part_hist / exclusive scan / k_part_scatter
+//                 a stable-free counting sort of the records by region;
+//   k_reduce      one workgroup per region: records aggregated in an LDS hash
+//                 table (count, first, last, min_order per key), then merged
+//                 into the region's slots with plain loads and stores — the
+//                 workgroup owns its region for the whole kernel, new slots are
+//                 claimed in an LDS copy of the region's occupancy bitmap.
+// Records per key shrink to one merge per LDS round.
+
+struct alignas(32) Rec {
+  unsigned long long kA, kB, order;
+  uint32_t ts, region;
+};
+static_assert(sizeof(Rec) == 32, "record layout");
+
+__device__ __forceinline__ uint32_t key_region(const Agg& A, unsigned long long hh) {
+  return A.np_bits ? (uint32_t)(hh >> (64 - A.np_bits)) : 0u;
+}
+
+// Workgroup exclusive scan of one uint32 per thread (blockDim.x <= 1024);
+// returns the thread's offset and writes the total to *total.  sh: >= 16 words.
+__device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t* sh, uint32_t* total) {
+  const unsigned lane = __lane_id(), w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  uint32_t x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if ((int)lane >= o) x += y;
+  }
+  if (lane == 63) sh[w] = x;
+  __syncthreads();
+  uint32_t before = 0, all = 0;
+  for (unsigned q = 0; q < nw; ++q) {
+    const uint32_t t = sh[q];
+    if (q < w) before += t;
+    all += t;
+  }
+  __syncthreads();
+  *total = all;
+  return before + x - v;
+}
+
 constexpr int kAggU = 4;
 template <int kLds>
 __global__ __launch_bounds__(1024) void k_aggregate(const uint4* __restrict__ T, const uint32_t* __restrict__ TS,
                                                     const unsigned long long* __restrict__ ORD,
                                                     const int32_t* __restrict__ G, unsigned long long n,
-                                                    uint32_t n_rules, Agg A) {
-  __shared__ uint32_t cnt[kLds > 0 ? 3 * kLds : 1];   // matches, hits, distinct
+                                                    uint32_t n_rules, Agg A, Rec* __restrict__ recs,
+                                                    uint16_t* __restrict__ regs, unsigned long long* __restrict__ n_recs) {
+  __shared__ uint32_t cnt[kLds > 0 ? 2 * kLds : 1];   // matches, hits
+  __shared__ uint32_t sh[18];
+  __shared__ unsigned long long sh_base;
   const bool counters = !(A.skip & 1u);
   if (kLds > 0) {
-    for (uint32_t r = threadIdx.x; r < 3u * kLds; r += blockDim.x) cnt[r] = 0;
+    for (uint32_t r = threadIdx.x; r < 2u * kLds; r += blockDim.x) cnt[r] = 0;
     __syncthreads();
   }
-  uint32_t st[4] = {0u, 0u, 0u, 0u};
-  uint32_t* stp = A.stats ? st : nullptr;
   const bool table = A.cap > 0 && !(A.skip & 2u);
   const unsigned long long span = (unsigned long long)blockDim.x * kAggU;
   for (unsigned long long base = (unsigned long long)blockIdx.x * span; base < n;
@@ -657,50 +728,269 @@ __global__ __launch_bounds__(1024) void k_aggregate(const uint4* __restrict__ T,
       o[k] = need[k] ? ORD[i] : 0ull;
       f[k] = need[k] ? A.filter[gid[k]] : 0ull;
     }
-    unsigned long long kA[kAggU], kB[kAggU], h[kAggU];
-    uint32_t ts[kAggU];
-    SlotHead hd[kAggU];
+    uint32_t c = 0;
 #pragma unroll
     for (int k = 0; k < kAggU; ++k) {
-      const unsigned long long i = base + (unsigned long long)k * blockDim.x + threadIdx.x;
       need[k] = need[k] && o[k] <= f[k];   // exact skip: capped with threshold <= filter < order
-      if (need[k]) {
-        conn_key(t[k], gid[k], kA[k], kB[k]);
-        h[k] = slot_hash(kA[k], kB[k]) & A.mask;
-        hd[k] = load_head(&A.slots[h[k]]);
-        ts[k] = TS[i];
-      }
+      c += need[k] ? 1u : 0u;
     }
+    uint32_t total;
+    const uint32_t off = block_exscan(c, sh, &total);
+    if (total == 0) continue;   // workgroup-uniform
+    if (threadIdx.x == 0) sh_base = atomicAdd(n_recs, (unsigned long long)total);
+    __syncthreads();
+    unsigned long long pos = sh_base + off;
+    __syncthreads();   // sh_base is rewritten by the next iteration
 #pragma unroll
     for (int k = 0; k < kAggU; ++k) {
-      bool fresh = false;
-      unsigned long long slot = kEmpty;
-      if (need[k]) slot = table_combine_at(A, kA[k], kB[k], 1u, ts[k], ts[k], o[k], &fresh, h[k], hd[k], stp);
-      if (kLds > 0) {
-        if (fresh) atomicAdd(&cnt[2 * kLds + gid[k]], 1u);
-      } else {
-        wave_count_by_key(fresh, gid[k], A.distinct);
-      }
-      const unsigned long long pos = wave_append(fresh, A.used_n);
-      if (fresh) A.used[pos] = (uint32_t)slot;
+      if (!need[k]) continue;
+      const unsigned long long i = base + (unsigned long long)k * blockDim.x + threadIdx.x;
+      Rec r;
+      conn_key(t[k], gid[k], r.kA, r.kB);
+      r.order = o[k];
+      r.ts = TS[i];
+      r.region = key_region(A, slot_hash(r.kA, r.kB));
+      regs[pos] = (uint16_t)r.region;
+      recs[pos++] = r;
     }
   }
   if (kLds > 0) {
     __syncthreads();
     for (uint32_t r = threadIdx.x; r < n_rules; r += blockDim.x) {
-      const uint32_t m = cnt[r], hh = cnt[kLds + r], d = cnt[2 * kLds + r];
+      const uint32_t m = cnt[r], hh = cnt[kLds + r];
       if (m) atomicAdd(&A.matches[r], (unsigned long long)m);
       if (hh) atomicAdd(&A.hits[r], (unsigned long long)hh);
-      if (d) atomicAdd(&A.distinct[r], d);
     }
   }
-  if (A.stats) {
-    for (int q = 0; q < 4; ++q) {
-      unsigned long long v = st[q];
-      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-      if (__lane_id() == 0 && v) atomicAdd(&A.stats[q], v);
-    }
+}
+
+// Counting sort of the records by region.  Tiles of kPartTile records; the
+// histogram matrix is region-major (hist[region * n_tiles + tile]) so that its
+// exclusive scan gives every (region, tile) run its output offset.
+constexpr int kPartTile = 32768;
+constexpr int kMaxRegions = 4096;
+
+__global__ __launch_bounds__(1024) void k_part_hist(const uint16_t* __restrict__ regs, unsigned long long n,
+                                                    uint32_t n_regions, uint32_t n_tiles, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t hcount[kMaxRegions];
+  const uint32_t tile = blockIdx.x;
+  for (uint32_t r = threadIdx.x; r < n_regions; r += blockDim.x) hcount[r] = 0;
+  __syncthreads();
+  const unsigned long long beg = (unsigned long long)tile * kPartTile;
+  const unsigned long long end = beg + kPartTile < n ? beg + kPartTile : n;
+  for (unsigned long long j = beg + threadIdx.x; j < end; j += blockDim.x) atomicAdd(&hcount[regs[j]], 1u);
+  __syncthreads();
+  for (uint32_t r = threadIdx.x; r < n_regions; r += blockDim.x) hist[(size_t)r * n_tiles + tile] = hcount[r];
+}
+
+__global__ __launch_bounds__(1024) void k_part_scatter(const Rec* __restrict__ recs, unsigned long long n,
+                                                       uint32_t n_regions, uint32_t n_tiles,
+                                                       const uint32_t* __restrict__ offs, Rec* __restrict__ out) {
+  __shared__ uint32_t cur[kMaxRegions];
+  const uint32_t tile = blockIdx.x;
+  for (uint32_t r = threadIdx.x; r < n_regions; r += blockDim.x) cur[r] = offs[(size_t)r * n_tiles + tile];
+  __syncthreads();
+  const unsigned long long beg = (unsigned long long)tile * kPartTile;
+  const unsigned long long end = beg + kPartTile < n ? beg + kPartTile : n;
+  for (unsigned long long j = beg + threadIdx.x; j < end; j += blockDim.x) {
+    const Rec r = recs[j];
+    out[atomicAdd(&cur[r.region], 1u)] = r;
   }
+}
+
+// Exclusive scan of n uint32 (three launches: per-block scan + block sums,
+// scan of the block sums in one workgroup, add).  kScanBlock elements per block.
+constexpr int kScanBlock = 4096;
+
+__global__ __launch_bounds__(1024) void k_scan_blocks(uint32_t* __restrict__ a, unsigned long long n,
+                                                      uint32_t* __restrict__ sums) {
+  __shared__ uint32_t sh[18];
+  const unsigned long long beg = (unsigned long long)blockIdx.x * kScanBlock + threadIdx.x * 4;
+  uint32_t v[4], c = 0;
+  for (int k = 0; k < 4; ++k) {
+    v[k] = beg + k < n ? a[beg + k] : 0u;
+    c += v[k];
+  }
+  uint32_t total;
+  uint32_t run = block_exscan(c, sh, &total);
+  for (int k = 0; k < 4; ++k) {
+    if (beg + k < n) a[beg + k] = run;
+    run += v[k];
+  }
+  if (threadIdx.x == 0) sums[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(1024) void k_scan_sums(uint32_t* __restrict__ sums, uint32_t nb) {
+  __shared__ uint32_t sh[18];
+  uint32_t carry = 0;
+  for (uint32_t b0 = 0; b0 < nb; b0 += blockDim.x) {
+    const uint32_t j = b0 + threadIdx.x;
+    const uint32_t v = j < nb ? sums[j] : 0u;
+    uint32_t total;
+    const uint32_t ex = block_exscan(v, sh, &total);
+    if (j < nb) sums[j] = carry + ex;
+    carry += total;
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_scan_add(uint32_t* __restrict__ a, unsigned long long n,
+                                                   const uint32_t* __restrict__ sums) {
+  const unsigned long long beg = (unsigned long long)blockIdx.x * kScanBlock + threadIdx.x * 4;
+  const uint32_t add = sums[blockIdx.x];
+  for (int k = 0; k < 4; ++k)
+    if (beg + k < n) a[beg + k] += add;
+}
+
+// One workgroup per region: LDS aggregation of the region's records in rounds
+// (a round takes at most as many records as the LDS table has free entries
+// below 3/4 load, so it can never overflow; the table is flushed once it is
+// half full and at the end), each flush merging every LDS entry into the
+// region's slots.  Only this workgroup touches the region during the kernel:
+// existing keys are found through the region's occupancy bitmap (slots
+// occupied before this flush hold published keys; a slot claimed during this
+// flush belongs to a DIFFERENT key, since the keys of one flush are distinct)
+// and updated with plain loads and stores; a new key claims a free slot with
+// an LDS atomic on the bitmap copy and writes the whole slot.
+constexpr int kRedE = 2048;                 // LDS hash entries (a multiple of the 1024-thread block)
+constexpr int kRegionMaxBits = 16;          // region <= 65536 slots (bitmap copy 8 KiB)
+
+__global__ __launch_bounds__(1024) void k_reduce(const Rec* __restrict__ recs, const uint32_t* __restrict__ offs,
+                                                 uint32_t n_tiles, unsigned long long n_recs, Agg A) {
+  __shared__ unsigned long long e_kA[kRedE], e_kB[kRedE], e_mo[kRedE];
+  __shared__ uint32_t e_first[kRedE], e_last[kRedE], e_cnt[kRedE];
+  __shared__ uint32_t occ[1u << (kRegionMaxBits - 5)];     // occupied before this flush
+  __shared__ uint32_t claim[1u << (kRegionMaxBits - 5)];   // claimed during this flush
+  __shared__ uint32_t used;
+  __shared__ uint32_t sh[18];
+  __shared__ unsigned long long sh_base;
+  const uint32_t region = blockIdx.x;
+  const uint32_t n_regions = 1u << A.np_bits;
+  const unsigned long long beg = offs[(size_t)region * n_tiles];
+  const unsigned long long end = region + 1 < n_regions ? offs[(size_t)(region + 1) * n_tiles] : n_recs;
+  if (beg >= end) return;   // workgroup-uniform
+  const uint32_t rs = 1u << A.rs_bits, words = (rs + 31) / 32;
+  const unsigned long long rbase = (unsigned long long)region << A.rs_bits;
+  uint32_t* gocc = A.occ + (rbase >> 5);
+  for (uint32_t w = threadIdx.x; w < words; w += blockDim.x) {
+    occ[w] = gocc[w];
+    claim[w] = 0;
+  }
+  for (uint32_t e = threadIdx.x; e < kRedE; e += blockDim.x) e_kB[e] = kEmpty;
+  if (threadIdx.x == 0) used = 0;
+  __syncthreads();
+  unsigned long long pos = beg;
+  while (pos < end) {
+    const uint32_t room = (3u * kRedE) / 4 - used;
+    const unsigned long long take = end - pos < room ? end - pos : room;
+    __syncthreads();   // every thread has read `used` before any insert changes it
+    for (unsigned long long j = threadIdx.x; j < take; j += blockDim.x) {
+      const Rec r = recs[pos + j];
+      uint32_t e = (uint32_t)mix64(r.kA ^ (r.kB * 0x9e3779b97f4a7c15ull)) & (kRedE - 1);
+      while (true) {
+        const unsigned long long cur = __hip_atomic_load(&e_kB[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (cur == kEmpty) {
+          if (atomicCAS(&e_kB[e], kEmpty, kBusy) == kEmpty) {
+            e_kA[e] = r.kA;
+            e_mo[e] = r.order;
+            e_first[e] = r.ts;
+            e_last[e] = r.ts;
+            e_cnt[e] = 1u;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            atomicExch(&e_kB[e], r.kB);
+            atomicAdd(&used, 1u);
+            break;
+          }
+          continue;
+        }
+        if (cur == kBusy) continue;
+        if (cur == r.kB && __hip_atomic_load(&e_kA[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == r.kA) {
+          atomicAdd(&e_cnt[e], 1u);
+          atomicMin(&e_first[e], r.ts);
+          atomicMax(&e_last[e], r.ts);
+          atomicMin(&e_mo[e], r.order);
+          break;
+        }
+        e = (e + 1) & (kRedE - 1);
+      }
+    }
+    pos += take;
+    __syncthreads();
+    if (used <= kRedE / 2 && pos < end) continue;   // workgroup-uniform
+    // flush: merge every LDS entry into the region; new slots are appended to
+    // the used list with ONE device atomic per flush (a per-wave append on the
+    // single cursor word would serialise ~30 atomics per workgroup on it)
+    constexpr int kPer = kRedE / 1024;
+    unsigned long long new_slot[kPer];
+    uint32_t n_new = 0;
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      const uint32_t e = threadIdx.x + q * blockDim.x;
+      const unsigned long long kB = e_kB[e];
+      bool fresh = false;
+      unsigned long long slot = kEmpty;
+      const uint32_t gid = (uint32_t)(kB >> 32);
+      if (kB != kEmpty) {
+        const unsigned long long kA = e_kA[e];
+        uint32_t loc = (uint32_t)slot_hash(kA, kB) & (rs - 1);
+        for (uint32_t probes = 0; probes < rs; ++probes, loc = (loc + 1) & (rs - 1)) {
+          const uint32_t bit = 1u << (loc & 31);
+          if (occ[loc >> 5] & bit) {
+            Slot* sl = &A.slots[rbase + loc];
+            const v4u k = *reinterpret_cast<const v4u*>(&sl->kA);
+            if ((((unsigned long long)k.w << 32) | k.z) != kB || (((unsigned long long)k.y << 32) | k.x) != kA)
+              continue;
+            const v4u m = *reinterpret_cast<const v4u*>(&sl->min_order);
+            const unsigned long long mo = ((unsigned long long)m.y << 32) | m.x;
+            const unsigned long long nmo = e_mo[e] < mo ? e_mo[e] : mo;
+            v4u nm;
+            nm.x = (uint32_t)nmo;
+            nm.y = (uint32_t)(nmo >> 32);
+            nm.z = min(m.z, e_first[e]);
+            nm.w = max(m.w, e_last[e]);
+            *reinterpret_cast<v4u*>(&sl->min_order) = nm;
+            sl->count += e_cnt[e];
+            slot = rbase + loc;
+            break;
+          }
+          if (atomicOr(&claim[loc >> 5], bit) & bit) continue;   // claimed in this flush by another key
+          Slot ns;
+          ns.kA = kA;
+          ns.kB = kB;
+          ns.min_order = e_mo[e];
+          ns.first = e_first[e];
+          ns.last = e_last[e];
+          ns.count = e_cnt[e];
+          ns.count2 = 0;
+          ns.first2 = 0xFFFFFFFFu;
+          ns.last2 = 0;
+          ns.pad[0] = ns.pad[1] = ns.pad[2] = ns.pad[3] = 0;
+          A.slots[rbase + loc] = ns;
+          slot = rbase + loc;
+          fresh = true;
+          break;
+        }
+        if (slot == kEmpty) atomicOr(&A.flags[0], 1u);   // region full
+        e_kB[e] = kEmpty;
+      }
+      wave_count_by_key(fresh, gid, A.distinct);
+      if (fresh) new_slot[n_new++] = ((unsigned long long)gid << 32) | (uint32_t)slot;
+    }
+    {
+      uint32_t total;
+      const uint32_t off = block_exscan(n_new, sh, &total);
+      if (threadIdx.x == 0 && total) sh_base = atomicAdd(A.used_n, (unsigned long long)total);
+      __syncthreads();
+      for (uint32_t q = 0; q < n_new; ++q) A.used[sh_base + off + q] = new_slot[q];
+    }
+    __syncthreads();
+    for (uint32_t w = threadIdx.x; w < words; w += blockDim.x) {
+      occ[w] |= claim[w];
+      claim[w] = 0;
+    }
+    if (threadIdx.x == 0) used = 0;
+    __syncthreads();
+  }
+  for (uint32_t w = threadIdx.x; w < words; w += blockDim.x) gocc[w] = occ[w];
 }
 
 // Pass 2: lines with order <= P of capped rules recount count/first/last into
@@ -757,10 +1047,10 @@ __global__ void k_table_init(Slot* S, unsigned long long cap) {
 }
 
 // Reset only the slots the last job used.
-__global__ void k_table_clear(Slot* S, const uint32_t* used, unsigned long long n) {
+__global__ void k_table_clear(Slot* S, const unsigned long long* used, unsigned long long n) {
   const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
   for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-    slot_clear(S, used[i]);
+    slot_clear(S, (uint32_t)used[i]);
 }
 
 // ---- cap resolution (exact): P = cap-th smallest min_order among a rule's entries.
@@ -788,7 +1078,8 @@ __global__ void k_cap_mark(const unsigned int* distinct, uint32_t n_rules, uint3
 // Scatter the capped rules' min_order keys into their segments.  Lanes of one
 // wave that share a rule take their positions from one atomic (hot rules would
 // otherwise serialise thousands of atomics on one counter).
-__global__ __launch_bounds__(kBlock) void k_cap_scatter(const Slot* S, const uint32_t* used, unsigned long long n_used,
+__global__ __launch_bounds__(kBlock) void k_cap_scatter(const Slot* S, const unsigned long long* used,
+                                                        unsigned long long n_used,
                                                         const uint32_t* cidx, const uint32_t* capped_start,
                                                         uint32_t* capped_fill, unsigned long long* keys,
                                                         unsigned long long max_keys, unsigned int* flags) {
@@ -798,24 +1089,15 @@ __global__ __launch_bounds__(kBlock) void k_cap_scatter(const Slot* S, const uin
     uint32_t c = 0xFFFFFFFFu;
     unsigned long long key = 0;
     if (i < n_used) {
-      const Slot* s = &S[used[i]];
-      c = cidx[s->kB >> 32];
-      key = s->min_order;
+      const unsigned long long u = used[i];
+      c = cidx[u >> 32];   // only the capped rules' entries are read
+      if (c != 0xFFFFFFFFu) key = S[(uint32_t)u].min_order;
     }
     const bool ok = c != 0xFFFFFFFFu;
-    unsigned long long pending = __ballot(ok);
-    const unsigned lane = __lane_id();
+    // one returning atomic per lane, all in flight together (a per-wave loop
+    // over the distinct rules would wait for each in turn)
     unsigned long long pos = 0;
-    while (pending) {
-      const int leader = __builtin_ctzll(pending);
-      const uint32_t k = __builtin_amdgcn_readlane(c, leader);
-      const unsigned long long peers = __ballot(ok && c == k);
-      pending &= ~peers;
-      uint32_t b = 0;
-      if ((int)lane == leader) b = atomicAdd(&capped_fill[k], (uint32_t)__popcll(peers));
-      b = __shfl(b, leader);
-      if (ok && c == k) pos = (unsigned long long)capped_start[k] + b + __popcll(peers & ((1ull << lane) - 1ull));
-    }
+    if (ok) pos = (unsigned long long)capped_start[c] + atomicAdd(&capped_fill[c], 1u);
     if (ok) {
       if (pos < max_keys) keys[pos] = key;
       else atomicOr(&flags[1], 16u);
@@ -937,28 +1219,51 @@ __device__ __forceinline__ rsa_conn_record make_record(const Slot& s, int which)
 }
 
 // mode 0: final report rows; mode 1: export pass-1 aggregates; mode 2: export pass-2.
-__global__ __launch_bounds__(kBlock) void k_emit(const Slot* S, const uint32_t* used, unsigned long long n_used,
-                                                 const unsigned long long* thresh, int mode, rsa_conn_record* out,
-                                                 unsigned long long max_out, unsigned long long* cursor) {
-  const unsigned long long stride = (unsigned long long)gridDim.x * kBlock;
-  for (unsigned long long base = (unsigned long long)blockIdx.x * kBlock; base < n_used; base += stride) {
-    const unsigned long long i = base + threadIdx.x;
-    int which = -1;
-    Slot s;
-    if (i < n_used) {
-      s = S[used[i]];
-      if (mode == 0) {
-        const unsigned long long P = thresh[s.kB >> 32];
-        if (P == RSA_NO_THRESHOLD) which = 0;
-        else if (s.min_order <= P) which = 1;
-      } else if (mode == 1) {
-        which = 0;
-      } else if (s.count2 != 0) {
-        which = 1;
+// Each thread takes kEmitU entries per iteration; one device atomic per
+// workgroup iteration reserves the output rows (a per-wave append on the one
+// cursor word serialises there).
+constexpr int kEmitU = 4;
+__global__ __launch_bounds__(1024) void k_emit(const Slot* S, const unsigned long long* used, unsigned long long n_used,
+                                               const unsigned long long* thresh, int mode, rsa_conn_record* out,
+                                               unsigned long long max_out, unsigned long long* cursor) {
+  __shared__ uint32_t sh[18];
+  __shared__ unsigned long long sh_base;
+  const unsigned long long span = (unsigned long long)blockDim.x * kEmitU;
+  for (unsigned long long base = (unsigned long long)blockIdx.x * span; base < n_used;
+       base += (unsigned long long)gridDim.x * span) {
+    int which[kEmitU];
+    Slot sl[kEmitU];
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < kEmitU; ++k) {
+      const unsigned long long i = base + (unsigned long long)k * blockDim.x + threadIdx.x;
+      which[k] = -1;
+      if (i < n_used) {
+        sl[k] = S[(uint32_t)used[i]];
+        if (mode == 0) {
+          const unsigned long long P = thresh[sl[k].kB >> 32];
+          if (P == RSA_NO_THRESHOLD) which[k] = 0;
+          else if (sl[k].min_order <= P) which[k] = 1;
+        } else if (mode == 1) {
+          which[k] = 0;
+        } else if (sl[k].count2 != 0) {
+          which[k] = 1;
+        }
       }
+      c += which[k] >= 0 ? 1u : 0u;
     }
-    const unsigned long long k = wave_append(which >= 0, cursor);
-    if (which >= 0 && k < max_out) out[k] = make_record(s, which);
+    uint32_t total;
+    const uint32_t off = block_exscan(c, sh, &total);
+    if (threadIdx.x == 0) sh_base = total ? atomicAdd(cursor, (unsigned long long)total) : 0ull;
+    __syncthreads();
+    unsigned long long pos = sh_base + off;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kEmitU; ++k) {
+      if (which[k] < 0) continue;
+      if (pos < max_out) out[pos] = make_record(sl[k], which[k]);
+      ++pos;
+    }
   }
 }
 
@@ -990,7 +1295,7 @@ __global__ __launch_bounds__(kBlock) void k_import(const rsa_conn_record* __rest
     }
     wave_count_by_key(fresh, gid, A.distinct);
     const unsigned long long pos = wave_append(fresh, A.used_n);
-    if (fresh) A.used[pos] = (uint32_t)slot;
+    if (fresh) A.used[pos] = ((unsigned long long)gid << 32) | (uint32_t)slot;
   }
 }
 
@@ -1026,7 +1331,7 @@ struct rsa_ctx {
   Slot* d_slots = nullptr;
   unsigned long long slot_cap = 0;    // power of two in use
   unsigned long long slot_alloc = 0;  // allocated (and initialised) slots
-  uint32_t* d_used = nullptr;
+  unsigned long long* d_used = nullptr;
   unsigned long long* d_used_n = nullptr;
   unsigned long long used_last = 0;   // used slots at the last host read (upper bound for clearing)
   bool table_dirty = false;           // used list may be non-empty
@@ -1046,6 +1351,21 @@ struct rsa_ctx {
   unsigned long long* d_tail_n = nullptr;
   unsigned long long tail_alloc = 0;
   int32_t* d_gscratch = nullptr;      // gids of a pass 1 / recount whose caller keeps none
+  // on-chip shuffle of pass 1b: records, their region-sorted copy, histograms
+  void* d_recs = nullptr;
+  void* d_recs2 = nullptr;
+  unsigned long long recs_alloc = 0;
+  unsigned long long recs2_alloc = 0;
+  uint16_t* d_regs = nullptr;          // region of each record (the histogram pass reads only these)
+  unsigned long long regs_alloc = 0;
+  unsigned long long* d_nrecs = nullptr;
+  uint32_t* d_hist = nullptr;
+  unsigned long long hist_alloc = 0;
+  uint32_t* d_scan_sums = nullptr;
+  unsigned long long scan_sums_alloc = 0;
+  uint32_t* d_occ = nullptr;          // slot occupancy bitmap
+  unsigned long long occ_alloc = 0;   // words
+  uint32_t rs_bits = 10, np_bits = 0;
   unsigned long long gscratch_alloc = 0;
   unsigned int* d_flags = nullptr;       // 4 words
   unsigned long long* d_cursor = nullptr;
@@ -1112,6 +1432,9 @@ Agg agg_of(const rsa_ctx* c) {
   a.skip = c->profile_skip;
   a.precheck = c->precheck ? 1u : 0u;
   a.stats = c->stats_on ? c->d_stats : nullptr;
+  a.occ = c->d_occ;
+  a.rs_bits = c->rs_bits;
+  a.np_bits = c->np_bits;
   return a;
 }
 
@@ -1288,15 +1611,59 @@ int launch_classify(rsa_ctx* c, const uint4* t, uint64_t m, int32_t* go) {
 // 1024-thread workgroup per CU (k_aggregate's registers allow no more).
 constexpr int kCnt = 13312;
 
+// Exclusive scan of n uint32 in place (device).
+int exclusive_scan(rsa_ctx* c, uint32_t* d, unsigned long long n) {
+  if (n == 0) return RSA_OK;
+  const unsigned long long nb = (n + kScanBlock - 1) / kScanBlock;
+  int rc = ensure_buf(c, &c->d_scan_sums, &c->scan_sums_alloc, nb);
+  if (rc) return rc;
+  k_scan_blocks<<<(unsigned)nb, 1024, 0, c->stream>>>(d, n, c->d_scan_sums);
+  k_scan_sums<<<1, 1024, 0, c->stream>>>(c->d_scan_sums, (uint32_t)nb);
+  k_scan_add<<<(unsigned)nb, 1024, 0, c->stream>>>(d, n, c->d_scan_sums);
+  HIPCHK(c, hipGetLastError());
+  return RSA_OK;
+}
+
+// Pass 1b over lines [0, m): counters + records (k_aggregate), counting sort of
+// the records by region, per-region LDS reduction and merge (k_reduce).
 int launch_aggregate(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsigned long long* o, const int32_t* g,
                      uint64_t m) {
   const Agg ag = agg_of(c);
+  int rc = ensure_buf(c, reinterpret_cast<Rec**>(&c->d_recs), &c->recs_alloc, m);
+  if (!rc) rc = ensure_buf(c, &c->d_regs, &c->regs_alloc, m);
+  if (rc) return rc;
+  if (!c->d_nrecs) HIPCHK(c, hipMalloc(&c->d_nrecs, sizeof(unsigned long long)));
+  HIPCHK(c, hipMemsetAsync(c->d_nrecs, 0, sizeof(unsigned long long), c->stream));
+  Rec* recs = reinterpret_cast<Rec*>(c->d_recs);
   const uint64_t units = (m + kAggU - 1) / kAggU;
   if (c->n_rules <= (uint32_t)kCnt) {
-    k_aggregate<kCnt><<<grid_for_threads(c, units, 1024, 1), 1024, 0, c->stream>>>(t, ts, o, g, m, c->n_rules, ag);
+    k_aggregate<kCnt><<<grid_for_threads(c, units, 1024, 2), 1024, 0, c->stream>>>(t, ts, o, g, m, c->n_rules, ag,
+                                                                                   recs, c->d_regs, c->d_nrecs);
   } else {
-    k_aggregate<0><<<grid_for_threads(c, units, 1024, 1), 1024, 0, c->stream>>>(t, ts, o, g, m, c->n_rules, ag);
+    k_aggregate<0><<<grid_for_threads(c, units, 1024, 2), 1024, 0, c->stream>>>(t, ts, o, g, m, c->n_rules, ag, recs,
+                                                                                c->d_regs, c->d_nrecs);
   }
+  HIPCHK(c, hipGetLastError());
+  unsigned long long nr = 0;
+  HIPCHK(c, hipMemcpyAsync(&nr, c->d_nrecs, sizeof nr, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (nr == 0) return RSA_OK;
+  if (nr > m) return fail(c, RSA_ERR_STATE, "record count %llu exceeds the batch", nr);
+  rc = ensure_buf(c, reinterpret_cast<Rec**>(&c->d_recs2), &c->recs2_alloc, nr);
+  if (rc) return rc;
+  Rec* sorted = reinterpret_cast<Rec*>(c->d_recs2);
+  const uint32_t n_regions = 1u << c->np_bits;
+  const uint32_t n_tiles = (uint32_t)((nr + kPartTile - 1) / kPartTile);
+  const unsigned long long hl = (unsigned long long)n_regions * n_tiles;
+  rc = ensure_buf(c, &c->d_hist, &c->hist_alloc, hl);
+  if (rc) return rc;
+  k_part_hist<<<n_tiles, 1024, 0, c->stream>>>(c->d_regs, nr, n_regions, n_tiles, c->d_hist);
+  HIPCHK(c, hipGetLastError());
+  rc = exclusive_scan(c, c->d_hist, hl);
+  if (rc) return rc;
+  k_part_scatter<<<n_tiles, 1024, 0, c->stream>>>(recs, nr, n_regions, n_tiles, c->d_hist, sorted);
+  HIPCHK(c, hipGetLastError());
+  k_reduce<<<n_regions, 1024, 0, c->stream>>>(sorted, c->d_hist, n_tiles, nr, ag);
   HIPCHK(c, hipGetLastError());
   return RSA_OK;
 }
@@ -1368,8 +1735,8 @@ int emit_mode(rsa_ctx* c, int mode, rsa_conn_record* out, uint64_t max_out, uint
   if (rc) return rc;
   HIPCHK(c, hipMemsetAsync(c->d_cursor, 0, sizeof(unsigned long long), c->stream));
   if (n_used)
-    k_emit<<<grid_for(c, n_used, 8), kBlock, 0, c->stream>>>(c->d_slots, c->d_used, n_used, c->d_thresh, mode, out,
-                                                             max_out, c->d_cursor);
+    k_emit<<<grid_for_threads(c, (n_used + kEmitU - 1) / kEmitU, 1024, 2), 1024, 0, c->stream>>>(
+        c->d_slots, c->d_used, n_used, c->d_thresh, mode, out, max_out, c->d_cursor);
   HIPCHK(c, hipGetLastError());
   unsigned long long n = 0;
   HIPCHK(c, hipMemcpyAsync(&n, c->d_cursor, sizeof n, hipMemcpyDeviceToHost, c->stream));
@@ -1411,7 +1778,8 @@ int rsa_ctx_destroy(rsa_ctx* c) {
   if (!c) return RSA_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->d_tail, c->d_tail_n, c->d_gscratch, c->d_stats, c->d_entries, c->d_off,
+  void* bufs[] = {c->d_tail, c->d_tail_n, c->d_gscratch, c->d_stats, c->d_recs, c->d_recs2, c->d_regs, c->d_nrecs, c->d_hist,
+                  c->d_scan_sums, c->d_occ, c->d_entries, c->d_off,
                   c->d_img, c->d_resid,
                   c->d_slots, c->d_used, c->d_used_n, c->d_filter, c->d_flags, c->d_cursor, c->d_cidx,
                   c->d_capped_gid, c->d_capped_cnt, c->d_capped_start, c->d_keys};
@@ -1602,12 +1970,30 @@ int rsa_bind_counters(rsa_ctx* c, uint64_t* m, uint64_t* h, uint32_t* d, uint64_
 int rsa_reset(rsa_ctx* c, uint64_t capacity, uint32_t cap) {
   if (!c) return RSA_ERR_ARG;
   if (!c->d_matches) return fail(c, RSA_ERR_STATE, "counters not bound (rsa_bind_counters)");
-  if (capacity > (1ull << 31)) return fail(c, RSA_ERR_ARG, "capacity %llu > 2^31 entries",
-                                           (unsigned long long)capacity);
+  // the table is at most kMaxRegions regions of 2^kRegionMaxBits slots
+  const unsigned long long max_slots = (unsigned long long)kMaxRegions << kRegionMaxBits;
+  const unsigned long long max_cap = (max_slots - 64) / 3 * 2;
+  if (capacity > max_cap)
+    return fail(c, RSA_ERR_ARG, "capacity %llu > %llu distinct entries per ctx", (unsigned long long)capacity, max_cap);
   HIPCHK(c, hipSetDevice(c->device));
   unsigned long long want = 1024;
   const unsigned long long need = capacity + capacity / 2 + 64;
   while (want < need) want <<= 1;
+  if (c->occ_alloc < want / 32) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    hipFree(c->d_occ);
+    c->d_occ = nullptr;
+    c->occ_alloc = 0;
+    HIPCHK(c, hipMalloc(&c->d_occ, want / 32 * sizeof(uint32_t)));
+    c->occ_alloc = want / 32;
+  }
+  HIPCHK(c, hipMemsetAsync(c->d_occ, 0, want / 32 * sizeof(uint32_t), c->stream));
+  {
+    uint32_t bits = 0;
+    while ((1ull << bits) < want) ++bits;
+    c->rs_bits = bits < (uint32_t)kRegionMaxBits ? bits : (uint32_t)kRegionMaxBits;
+    c->np_bits = bits - c->rs_bits;
+  }
   if (want > c->slot_alloc) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     hipFree(c->d_slots);
@@ -1616,7 +2002,7 @@ int rsa_reset(rsa_ctx* c, uint64_t capacity, uint32_t cap) {
     c->d_used = nullptr;
     c->slot_alloc = 0;
     HIPCHK(c, hipMalloc(&c->d_slots, want * sizeof(Slot)));
-    HIPCHK(c, hipMalloc(&c->d_used, want * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(&c->d_used, want * sizeof(unsigned long long)));
     k_table_init<<<grid_for(c, want, 8), kBlock, 0, c->stream>>>(c->d_slots, want);
     HIPCHK(c, hipGetLastError());
     c->slot_alloc = want;

@@ -83,8 +83,13 @@ def main():
             timed(st, lambda: eng.classify_only(batch, g), args.reps)
         elif st == 'pass1':
             timed(st, p1, args.reps)
-            say('  pass1 library events: %.3f ms; table entries %d (capacity %d)' % (
-                eng.last_pass1_ms(), eng.table_size(), capacity))
+            say('  pass1 library events: classify %.3f ms, aggregate %.3f ms; table entries %d (capacity %d)' % (
+                eng.last_pass1_times() + (eng.table_size(), capacity)))
+        elif st.startswith('rskip'):
+            eng.set_option(native.RSA_OPT_PROFILE_SKIP, int(st[5:]))
+            timed(st, p1, args.reps)
+            say('  pass1 library events: classify %.3f ms, aggregate %.3f ms' % eng.last_pass1_times())
+            eng.set_option(native.RSA_OPT_PROFILE_SKIP, 0)
         elif st.startswith('skip'):
             eng.set_option(native.RSA_OPT_PROFILE_SKIP, int(st[4:]))
             timed(st, p1, args.reps)
