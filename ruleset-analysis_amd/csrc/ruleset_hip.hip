@@ -854,8 +854,17 @@ __global__ __launch_bounds__(1024) void k_scan_add(uint32_t* __restrict__ a, uns
 constexpr int kRedE = 2048;                 // LDS hash entries (a multiple of the 1024-thread block)
 constexpr int kRegionMaxBits = 16;          // region <= 65536 slots (bitmap copy 8 KiB)
 
-__global__ __launch_bounds__(1024) void k_reduce(const Rec* __restrict__ recs, const uint32_t* __restrict__ offs,
-                                                 uint32_t n_tiles, unsigned long long n_recs, Agg A) {
+// kPass 1: the pass-1 reduction above.  kPass 2: the cap recount
+// (connlist-reducer.py:151-176 after the dict froze) from the records pass 1
+// kept: records of capped rules with order <= P are aggregated the same way
+// into the pass-2 fields of their (existing) slots; nothing is inserted.  A
+// region's records may lie in several segments (one per pass-1 launch):
+// starts[s * (n_regions + 1) + r] .. starts[s * (n_regions + 1) + r + 1].
+constexpr int kMaxSegs = 16;
+template <int kPass>
+__global__ __launch_bounds__(1024) void k_reduce(const Rec* __restrict__ recs,
+                                                 const unsigned long long* __restrict__ starts, uint32_t n_segs,
+                                                 Agg A) {
   __shared__ unsigned long long e_kA[kRedE], e_kB[kRedE], e_mo[kRedE];
   __shared__ uint32_t e_first[kRedE], e_last[kRedE], e_cnt[kRedE];
   __shared__ uint32_t occ[1u << (kRegionMaxBits - 5)];     // occupied before this flush
@@ -865,9 +874,10 @@ __global__ __launch_bounds__(1024) void k_reduce(const Rec* __restrict__ recs, c
   __shared__ unsigned long long sh_base;
   const uint32_t region = blockIdx.x;
   const uint32_t n_regions = 1u << A.np_bits;
-  const unsigned long long beg = offs[(size_t)region * n_tiles];
-  const unsigned long long end = region + 1 < n_regions ? offs[(size_t)(region + 1) * n_tiles] : n_recs;
-  if (beg >= end) return;   // workgroup-uniform
+  unsigned long long total_recs = 0;
+  for (uint32_t sg = 0; sg < n_segs; ++sg)
+    total_recs += starts[(size_t)sg * (n_regions + 1) + region + 1] - starts[(size_t)sg * (n_regions + 1) + region];
+  if (total_recs == 0) return;   // workgroup-uniform
   const uint32_t rs = 1u << A.rs_bits, words = (rs + 31) / 32;
   const unsigned long long rbase = (unsigned long long)region << A.rs_bits;
   uint32_t* gocc = A.occ + (rbase >> 5);
@@ -878,119 +888,156 @@ __global__ __launch_bounds__(1024) void k_reduce(const Rec* __restrict__ recs, c
   for (uint32_t e = threadIdx.x; e < kRedE; e += blockDim.x) e_kB[e] = kEmpty;
   if (threadIdx.x == 0) used = 0;
   __syncthreads();
-  unsigned long long pos = beg;
-  while (pos < end) {
-    const uint32_t room = (3u * kRedE) / 4 - used;
-    const unsigned long long take = end - pos < room ? end - pos : room;
-    __syncthreads();   // every thread has read `used` before any insert changes it
-    for (unsigned long long j = threadIdx.x; j < take; j += blockDim.x) {
-      const Rec r = recs[pos + j];
-      uint32_t e = (uint32_t)mix64(r.kA ^ (r.kB * 0x9e3779b97f4a7c15ull)) & (kRedE - 1);
-      while (true) {
-        const unsigned long long cur = __hip_atomic_load(&e_kB[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (cur == kEmpty) {
-          if (atomicCAS(&e_kB[e], kEmpty, kBusy) == kEmpty) {
-            e_kA[e] = r.kA;
-            e_mo[e] = r.order;
-            e_first[e] = r.ts;
-            e_last[e] = r.ts;
-            e_cnt[e] = 1u;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            atomicExch(&e_kB[e], r.kB);
-            atomicAdd(&used, 1u);
+  uint32_t sg = 0;
+  unsigned long long pos = starts[region], end = starts[region + 1];
+  while (true) {
+    while (pos >= end && sg + 1 < n_segs) {   // workgroup-uniform: next segment
+      ++sg;
+      pos = starts[(size_t)sg * (n_regions + 1) + region];
+      end = starts[(size_t)sg * (n_regions + 1) + region + 1];
+    }
+    const bool last_round = pos >= end;
+    if (!last_round) {
+      const uint32_t room = (3u * kRedE) / 4 - used;
+      const unsigned long long take = end - pos < room ? end - pos : room;
+      __syncthreads();   // every thread has read `used` before any insert changes it
+      for (unsigned long long j = threadIdx.x; j < take; j += blockDim.x) {
+        const Rec r = recs[pos + j];
+        if (kPass == 2) {
+          const unsigned long long P = A.thresh[r.kB >> 32];
+          if (P == RSA_NO_THRESHOLD || r.order > P) continue;
+        }
+        uint32_t e = (uint32_t)mix64(r.kA ^ (r.kB * 0x9e3779b97f4a7c15ull)) & (kRedE - 1);
+        while (true) {
+          const unsigned long long cur = __hip_atomic_load(&e_kB[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (cur == kEmpty) {
+            if (atomicCAS(&e_kB[e], kEmpty, kBusy) == kEmpty) {
+              e_kA[e] = r.kA;
+              e_mo[e] = r.order;
+              e_first[e] = r.ts;
+              e_last[e] = r.ts;
+              e_cnt[e] = 1u;
+              __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+              atomicExch(&e_kB[e], r.kB);
+              atomicAdd(&used, 1u);
+              break;
+            }
+            continue;
+          }
+          if (cur == kBusy) continue;
+          if (cur == r.kB && __hip_atomic_load(&e_kA[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == r.kA) {
+            atomicAdd(&e_cnt[e], 1u);
+            atomicMin(&e_first[e], r.ts);
+            atomicMax(&e_last[e], r.ts);
+            if (kPass == 1) atomicMin(&e_mo[e], r.order);
             break;
           }
-          continue;
+          e = (e + 1) & (kRedE - 1);
         }
-        if (cur == kBusy) continue;
-        if (cur == r.kB && __hip_atomic_load(&e_kA[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == r.kA) {
-          atomicAdd(&e_cnt[e], 1u);
-          atomicMin(&e_first[e], r.ts);
-          atomicMax(&e_last[e], r.ts);
-          atomicMin(&e_mo[e], r.order);
-          break;
-        }
-        e = (e + 1) & (kRedE - 1);
       }
-    }
-    pos += take;
-    __syncthreads();
-    if (used <= kRedE / 2 && pos < end) continue;   // workgroup-uniform
-    // flush: merge every LDS entry into the region; new slots are appended to
-    // the used list with ONE device atomic per flush (a per-wave append on the
-    // single cursor word would serialise ~30 atomics per workgroup on it)
-    constexpr int kPer = kRedE / 1024;
-    unsigned long long new_slot[kPer];
-    uint32_t n_new = 0;
-#pragma unroll
-    for (int q = 0; q < kPer; ++q) {
-      const uint32_t e = threadIdx.x + q * blockDim.x;
-      const unsigned long long kB = e_kB[e];
-      bool fresh = false;
-      unsigned long long slot = kEmpty;
-      const uint32_t gid = (uint32_t)(kB >> 32);
-      if (kB != kEmpty) {
-        const unsigned long long kA = e_kA[e];
-        uint32_t loc = (uint32_t)slot_hash(kA, kB) & (rs - 1);
-        for (uint32_t probes = 0; probes < rs; ++probes, loc = (loc + 1) & (rs - 1)) {
-          const uint32_t bit = 1u << (loc & 31);
-          if (occ[loc >> 5] & bit) {
-            Slot* sl = &A.slots[rbase + loc];
-            const v4u k = *reinterpret_cast<const v4u*>(&sl->kA);
-            if ((((unsigned long long)k.w << 32) | k.z) != kB || (((unsigned long long)k.y << 32) | k.x) != kA)
-              continue;
-            const v4u m = *reinterpret_cast<const v4u*>(&sl->min_order);
-            const unsigned long long mo = ((unsigned long long)m.y << 32) | m.x;
-            const unsigned long long nmo = e_mo[e] < mo ? e_mo[e] : mo;
-            v4u nm;
-            nm.x = (uint32_t)nmo;
-            nm.y = (uint32_t)(nmo >> 32);
-            nm.z = min(m.z, e_first[e]);
-            nm.w = max(m.w, e_last[e]);
-            *reinterpret_cast<v4u*>(&sl->min_order) = nm;
-            sl->count += e_cnt[e];
-            slot = rbase + loc;
-            break;
-          }
-          if (atomicOr(&claim[loc >> 5], bit) & bit) continue;   // claimed in this flush by another key
-          Slot ns;
-          ns.kA = kA;
-          ns.kB = kB;
-          ns.min_order = e_mo[e];
-          ns.first = e_first[e];
-          ns.last = e_last[e];
-          ns.count = e_cnt[e];
-          ns.count2 = 0;
-          ns.first2 = 0xFFFFFFFFu;
-          ns.last2 = 0;
-          ns.pad[0] = ns.pad[1] = ns.pad[2] = ns.pad[3] = 0;
-          A.slots[rbase + loc] = ns;
-          slot = rbase + loc;
-          fresh = true;
-          break;
-        }
-        if (slot == kEmpty) atomicOr(&A.flags[0], 1u);   // region full
-        e_kB[e] = kEmpty;
-      }
-      wave_count_by_key(fresh, gid, A.distinct);
-      if (fresh) new_slot[n_new++] = ((unsigned long long)gid << 32) | (uint32_t)slot;
-    }
-    {
-      uint32_t total;
-      const uint32_t off = block_exscan(n_new, sh, &total);
-      if (threadIdx.x == 0 && total) sh_base = atomicAdd(A.used_n, (unsigned long long)total);
+      pos += take;
       __syncthreads();
-      for (uint32_t q = 0; q < n_new; ++q) A.used[sh_base + off + q] = new_slot[q];
+      bool more = pos < end;
+      for (uint32_t q = sg + 1; q < n_segs && !more; ++q)
+        more = starts[(size_t)q * (n_regions + 1) + region + 1] > starts[(size_t)q * (n_regions + 1) + region];
+      if (used <= kRedE / 2 && more) continue;   // workgroup-uniform
     }
-    __syncthreads();
-    for (uint32_t w = threadIdx.x; w < words; w += blockDim.x) {
-      occ[w] |= claim[w];
-      claim[w] = 0;
+    if (used > 0) {   // workgroup-uniform (read after a barrier)
+      // flush: merge every LDS entry into the region; new slots are appended to
+      // the used list with ONE device atomic per flush (a per-wave append on
+      // the single cursor word would serialise ~30 atomics per workgroup on it)
+      constexpr int kPer = kRedE / 1024;
+      unsigned long long new_slot[kPer];
+      uint32_t n_new = 0;
+#pragma unroll
+      for (int q = 0; q < kPer; ++q) {
+        const uint32_t e = threadIdx.x + q * blockDim.x;
+        const unsigned long long kB = e_kB[e];
+        bool fresh = false;
+        unsigned long long slot = kEmpty;
+        const uint32_t gid = (uint32_t)(kB >> 32);
+        if (kB != kEmpty) {
+          const unsigned long long kA = e_kA[e];
+          uint32_t loc = (uint32_t)slot_hash(kA, kB) & (rs - 1);
+          for (uint32_t probes = 0; probes < rs; ++probes, loc = (loc + 1) & (rs - 1)) {
+            const uint32_t bit = 1u << (loc & 31);
+            if (occ[loc >> 5] & bit) {
+              Slot* sl = &A.slots[rbase + loc];
+              const v4u k = *reinterpret_cast<const v4u*>(&sl->kA);
+              if ((((unsigned long long)k.w << 32) | k.z) != kB || (((unsigned long long)k.y << 32) | k.x) != kA)
+                continue;
+              if (kPass == 1) {
+                const v4u m = *reinterpret_cast<const v4u*>(&sl->min_order);
+                const unsigned long long mo = ((unsigned long long)m.y << 32) | m.x;
+                const unsigned long long nmo = e_mo[e] < mo ? e_mo[e] : mo;
+                v4u nm;
+                nm.x = (uint32_t)nmo;
+                nm.y = (uint32_t)(nmo >> 32);
+                nm.z = min(m.z, e_first[e]);
+                nm.w = max(m.w, e_last[e]);
+                *reinterpret_cast<v4u*>(&sl->min_order) = nm;
+                sl->count += e_cnt[e];
+              } else {
+                sl->count2 += e_cnt[e];
+                sl->first2 = min(sl->first2, e_first[e]);
+                sl->last2 = max(sl->last2, e_last[e]);
+              }
+              slot = rbase + loc;
+              break;
+            }
+            if (kPass == 2) break;   // every pass-2 key was inserted in pass 1
+            if (atomicOr(&claim[loc >> 5], bit) & bit) continue;   // claimed in this flush by another key
+            Slot ns;
+            ns.kA = kA;
+            ns.kB = kB;
+            ns.min_order = e_mo[e];
+            ns.first = e_first[e];
+            ns.last = e_last[e];
+            ns.count = e_cnt[e];
+            ns.count2 = 0;
+            ns.first2 = 0xFFFFFFFFu;
+            ns.last2 = 0;
+            ns.pad[0] = ns.pad[1] = ns.pad[2] = ns.pad[3] = 0;
+            A.slots[rbase + loc] = ns;
+            slot = rbase + loc;
+            fresh = true;
+            break;
+          }
+          if (slot == kEmpty) atomicOr(&A.flags[kPass == 1 ? 0 : 1], kPass == 1 ? 1u : 4u);
+          e_kB[e] = kEmpty;
+        }
+        if (kPass == 1) {
+          wave_count_by_key(fresh, gid, A.distinct);
+          if (fresh) new_slot[n_new++] = ((unsigned long long)gid << 32) | (uint32_t)slot;
+        }
+      }
+      if (kPass == 1) {
+        uint32_t total;
+        const uint32_t off = block_exscan(n_new, sh, &total);
+        if (threadIdx.x == 0 && total) sh_base = atomicAdd(A.used_n, (unsigned long long)total);
+        __syncthreads();
+        for (uint32_t q = 0; q < n_new; ++q) A.used[sh_base + off + q] = new_slot[q];
+      }
+      __syncthreads();
+      for (uint32_t w = threadIdx.x; w < words; w += blockDim.x) {
+        occ[w] |= claim[w];
+        claim[w] = 0;
+      }
+      if (threadIdx.x == 0) used = 0;
+      __syncthreads();
     }
-    if (threadIdx.x == 0) used = 0;
-    __syncthreads();
+    if (last_round) break;
   }
-  for (uint32_t w = threadIdx.x; w < words; w += blockDim.x) gocc[w] = occ[w];
+  if (kPass == 1)
+    for (uint32_t w = threadIdx.x; w < words; w += blockDim.x) gocc[w] = occ[w];
+}
+
+// Segment starts of one pass-1 launch: starts[r] = base + offs[r * n_tiles].
+__global__ void k_seg_starts(const uint32_t* __restrict__ offs, uint32_t n_tiles, uint32_t n_regions,
+                             unsigned long long base, unsigned long long n_recs, unsigned long long* starts) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < n_regions) starts[r] = base + offs[(size_t)r * n_tiles];
+  if (r == n_regions) starts[r] = base + n_recs;
 }
 
 // Pass 2: lines with order <= P of capped rules recount count/first/last into
@@ -1094,10 +1141,27 @@ __global__ __launch_bounds__(kBlock) void k_cap_scatter(const Slot* S, const uns
       if (c != 0xFFFFFFFFu) key = S[(uint32_t)u].min_order;
     }
     const bool ok = c != 0xFFFFFFFFu;
-    // one returning atomic per lane, all in flight together (a per-wave loop
-    // over the distinct rules would wait for each in turn)
-    unsigned long long pos = 0;
-    if (ok) pos = (unsigned long long)capped_start[c] + atomicAdd(&capped_fill[c], 1u);
+    // lanes that share a rule are grouped first (ballots only, no memory
+    // waits), then every group leader reserves its group's positions with ONE
+    // returning atomic, all leaders' atomics in flight together
+    const unsigned lane = __lane_id();
+    unsigned long long pending = __ballot(ok);
+    uint32_t my_leader = lane, my_rank = 0, my_cnt = 0;
+    while (pending) {
+      const int leader = __builtin_ctzll(pending);
+      const uint32_t k = __builtin_amdgcn_readlane(c, leader);
+      const unsigned long long peers = __ballot(ok && c == k);
+      pending &= ~peers;
+      if (ok && c == k) {
+        my_leader = (uint32_t)leader;
+        my_rank = __popcll(peers & ((1ull << lane) - 1ull));
+        my_cnt = __popcll(peers);
+      }
+    }
+    uint32_t b = 0;
+    if (ok && lane == my_leader) b = atomicAdd(&capped_fill[c], my_cnt);
+    b = __shfl(b, (int)my_leader);
+    const unsigned long long pos = ok ? (unsigned long long)capped_start[c] + b + my_rank : 0ull;
     if (ok) {
       if (pos < max_keys) keys[pos] = key;
       else atomicOr(&flags[1], 16u);
@@ -1366,6 +1430,14 @@ struct rsa_ctx {
   uint32_t* d_occ = nullptr;          // slot occupancy bitmap
   unsigned long long occ_alloc = 0;   // words
   uint32_t rs_bits = 10, np_bits = 0;
+  // pass-1 records kept for the recount: one batch per job, one segment per launch
+  unsigned long long* d_starts = nullptr;   // kMaxSegs x (regions + 1)
+  unsigned long long seg_base = 0;
+  uint32_t n_segs = 0;
+  bool rec_cache = false;
+  const void* cache_T = nullptr;
+  unsigned long long cache_n = 0;
+  uint32_t pass1_calls = 0;
   unsigned long long gscratch_alloc = 0;
   unsigned int* d_flags = nullptr;       // 4 words
   unsigned long long* d_cursor = nullptr;
@@ -1649,9 +1721,16 @@ int launch_aggregate(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsig
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (nr == 0) return RSA_OK;
   if (nr > m) return fail(c, RSA_ERR_STATE, "record count %llu exceeds the batch", nr);
-  rc = ensure_buf(c, reinterpret_cast<Rec**>(&c->d_recs2), &c->recs2_alloc, nr);
-  if (rc) return rc;
-  Rec* sorted = reinterpret_cast<Rec*>(c->d_recs2);
+  // region-sorted records: appended after the previous launches' while this
+  // job's records are kept for the recount (rsa_recount), else from 0
+  if (c->rec_cache && (c->n_segs >= (uint32_t)kMaxSegs || c->seg_base + nr > c->recs2_alloc)) c->rec_cache = false;
+  if (!c->rec_cache) {
+    c->seg_base = 0;
+    c->n_segs = 0;
+    rc = ensure_buf(c, reinterpret_cast<Rec**>(&c->d_recs2), &c->recs2_alloc, nr);
+    if (rc) return rc;
+  }
+  Rec* sorted = reinterpret_cast<Rec*>(c->d_recs2) + c->seg_base;
   const uint32_t n_regions = 1u << c->np_bits;
   const uint32_t n_tiles = (uint32_t)((nr + kPartTile - 1) / kPartTile);
   const unsigned long long hl = (unsigned long long)n_regions * n_tiles;
@@ -1663,8 +1742,14 @@ int launch_aggregate(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsig
   if (rc) return rc;
   k_part_scatter<<<n_tiles, 1024, 0, c->stream>>>(recs, nr, n_regions, n_tiles, c->d_hist, sorted);
   HIPCHK(c, hipGetLastError());
-  k_reduce<<<n_regions, 1024, 0, c->stream>>>(sorted, c->d_hist, n_tiles, nr, ag);
+  unsigned long long* st = c->d_starts + (size_t)c->n_segs * (n_regions + 1);
+  k_seg_starts<<<(n_regions + 1 + 255) / 256, 256, 0, c->stream>>>(c->d_hist, n_tiles, n_regions, c->seg_base, nr, st);
+  k_reduce<1><<<n_regions, 1024, 0, c->stream>>>(reinterpret_cast<const Rec*>(c->d_recs2), st, 1, ag);
   HIPCHK(c, hipGetLastError());
+  if (c->rec_cache) {
+    c->seg_base += nr;
+    ++c->n_segs;
+  }
   return RSA_OK;
 }
 
@@ -1685,6 +1770,18 @@ int run_pass1(rsa_ctx* c, int classify, const rsa_tuple* T, const uint32_t* TS, 
     rc = ensure_buf(c, &c->d_gscratch, &c->gscratch_alloc, n);
     if (rc) return rc;
     gout = c->d_gscratch;
+  }
+  // the records of a job's only batch are kept for its recount
+  if (c->pass1_calls++ == 0) {
+    rc = ensure_buf(c, reinterpret_cast<Rec**>(&c->d_recs2), &c->recs2_alloc, n);
+    if (rc) return rc;
+    c->rec_cache = true;
+    c->cache_T = T;
+    c->cache_n = n;
+    c->seg_base = 0;
+    c->n_segs = 0;
+  } else {
+    c->rec_cache = false;
   }
   auto launch = [&](uint64_t a, uint64_t m) -> int {
     if (m == 0) return RSA_OK;
@@ -1778,7 +1875,7 @@ int rsa_ctx_destroy(rsa_ctx* c) {
   if (!c) return RSA_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->d_tail, c->d_tail_n, c->d_gscratch, c->d_stats, c->d_recs, c->d_recs2, c->d_regs, c->d_nrecs, c->d_hist,
+  void* bufs[] = {c->d_tail, c->d_tail_n, c->d_gscratch, c->d_stats, c->d_recs, c->d_recs2, c->d_regs, c->d_nrecs, c->d_starts, c->d_hist,
                   c->d_scan_sums, c->d_occ, c->d_entries, c->d_off,
                   c->d_img, c->d_resid,
                   c->d_slots, c->d_used, c->d_used_n, c->d_filter, c->d_flags, c->d_cursor, c->d_cidx,
@@ -1988,6 +2085,12 @@ int rsa_reset(rsa_ctx* c, uint64_t capacity, uint32_t cap) {
     c->occ_alloc = want / 32;
   }
   HIPCHK(c, hipMemsetAsync(c->d_occ, 0, want / 32 * sizeof(uint32_t), c->stream));
+  if (!c->d_starts)
+    HIPCHK(c, hipMalloc(&c->d_starts, (size_t)kMaxSegs * (kMaxRegions + 1) * sizeof(unsigned long long)));
+  c->pass1_calls = 0;
+  c->rec_cache = false;
+  c->n_segs = 0;
+  c->seg_base = 0;
   {
     uint32_t bits = 0;
     while ((1ull << bits) < want) ++bits;
@@ -2111,6 +2214,14 @@ int rsa_recount(rsa_ctx* c, const rsa_tuple* T, const uint32_t* TS, const uint64
   if (rc) return rc;
   if (n == 0) return RSA_OK;
   if (!T || !TS || !ORD) return fail(c, RSA_ERR_ARG, "null tuple/ts/order pointer");
+  if (c->rec_cache && c->cache_T == (const void*)T && c->cache_n == n && c->n_segs > 0) {
+    // every occurrence with order <= P of a capped rule produced a pass-1
+    // record (P <= the filter bound in force when its line was aggregated)
+    k_reduce<2><<<1u << c->np_bits, 1024, 0, c->stream>>>(reinterpret_cast<const Rec*>(c->d_recs2), c->d_starts,
+                                                         c->n_segs, agg_of(c));
+    HIPCHK(c, hipGetLastError());
+    return RSA_OK;
+  }
   if (!G) {
     // re-classify into scratch gids
     if (!c->rules_loaded) return fail(c, RSA_ERR_STATE, "no rules loaded (recount without gids re-classifies)");
