@@ -8,7 +8,8 @@ Correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE is in KiB and on gfx950 reads
 also issues scattered atomics whose accounting is uncalibrated, so the figure
 is a best estimate (it is reported beside, not instead of, the algorithmic
 bytes).  Usage: pmc_summary.py FETCH_CSV WRITE_CSV OUT_JSON LINES STEPS_TOTAL
-(STEPS_TOTAL = warmup + timed steps of the profiled bench run)."""
+(STEPS_TOTAL = warmup + timed steps + 1 untimed stats step of the profiled
+bench run)."""
 import csv
 import json
 import sys
@@ -32,8 +33,10 @@ def main():
         int(sys.argv[5])
     f, fn = per_dispatch(fetch_csv, 'FETCH_SIZE')
     w, wn = per_dispatch(write_csv, 'WRITE_SIZE')
-    # every pass-1 launch (classification, deferred tails, aggregation) of every slice
-    kinds = ('k_classify', 'k_tail', 'k_aggregate')
+    # every pass-1 launch of every slice: classification, deferred tails,
+    # aggregation (record append, region histogram, region scatter, per-region
+    # reduction) -- the kernels bracketed by the pass-1 HIP events
+    kinds = ('k_classify', 'k_tail', 'k_aggregate', 'k_part_hist', 'k_part_scatter', 'k_seg_starts', 'k_reduce<1>')
     pick = lambda name: any(k in name for k in kinds)
     fk = [v for d, v in sorted(f.items()) if pick(fn[d])]
     wk = [v for d, v in sorted(w.items()) if pick(wn[d])]
