@@ -253,7 +253,8 @@ def main():
                        'records': n_rec},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
-                         'kernel': 'pass 1 = k_classify + k_tail + k_aggregate (per step: filter slices + rest)',
+                         'kernel': 'pass 1 = k_classify + k_tail + aggregation (k_aggregate, k_part_hist/scan/k_part_scatter, '
+                                   'k_reduce<1>) over the filter slices + rest of one step',
                          'kernel_ms': pass1_ms, 'bytes_per_line': BYTES_PER_LINE,
                          'kernels': {
                              'classify_ms': classify_ms,
@@ -261,12 +262,9 @@ def main():
                              'classify_gbs': BYTES_PER_LINE * lines / (classify_ms * 1e-3) / 1e9,
                              'aggregate_table_lines': tstats[0],
                              'aggregate_slot_atomics': tstats[3],
-                             'aggregate_atomic_rate_g_s': tstats[3] / (aggregate_ms * 1e-3) / 1e9,
-                             'scattered_atomic_peak_g_s': SCATTER_ATOMIC_PEAK / 1e9,
-                             'note': 'k_aggregate is bound by scattered device atomics (one lane per 64-B row: '
-                                     'MI355X_MICROARCH.md Global atomics, 0.08 TB/s of 4-B adds = 20 G/s); '
-                                     'slot atomics = count/min/max updates of existing entries + claim and publish of new '
-                                     'ones (their fields are written by stores)'},
+                             'note': 'aggregation = record append in line order, counting sort by table region, '
+                                     'per-region LDS reduction merged into region-owned slots with plain stores; '
+                                     'table counters are collected only in the untimed stats step'},
                          'valu': {'achieved': OPS_PER_EVAL * sum_e / (pass1_ms * 1e-3) / 1e12,
                                   'peak': VALU_PEAK_OPS / 1e12, 'unit': 'Tops/s',
                                   'frac': OPS_PER_EVAL * sum_e / (pass1_ms * 1e-3) / VALU_PEAK_OPS,
