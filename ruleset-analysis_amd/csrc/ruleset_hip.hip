@@ -764,34 +764,37 @@ __global__ __launch_bounds__(1024) void k_aggregate(const uint4* __restrict__ T,
   }
 }
 
-// Counting sort of the records by region.  Tiles of kPartTile records; the
-// histogram matrix is region-major (hist[region * n_tiles + tile]) so that its
-// exclusive scan gives every (region, tile) run its output offset.
-constexpr int kPartTile = 32768;
+// Counting sort of the records by region.  Tiles of `tile` records (a power of
+// two between kPartTileMin and kPartTileMax, chosen per launch so that a small
+// batch still spreads over ~kPartTilesWant workgroups instead of a few dozen);
+// the histogram matrix is region-major (hist[region * n_tiles + tile]) so that
+// its exclusive scan gives every (region, tile) run its output offset.
+constexpr uint32_t kPartTileMin = 4096, kPartTileMax = 32768, kPartTilesWant = 1024;
 constexpr int kMaxRegions = 4096;
 
 __global__ __launch_bounds__(1024) void k_part_hist(const uint16_t* __restrict__ regs, unsigned long long n,
-                                                    uint32_t n_regions, uint32_t n_tiles, uint32_t* __restrict__ hist) {
+                                                    uint32_t n_regions, uint32_t n_tiles, uint32_t tile_len,
+                                                    uint32_t* __restrict__ hist) {
   __shared__ uint32_t hcount[kMaxRegions];
   const uint32_t tile = blockIdx.x;
   for (uint32_t r = threadIdx.x; r < n_regions; r += blockDim.x) hcount[r] = 0;
   __syncthreads();
-  const unsigned long long beg = (unsigned long long)tile * kPartTile;
-  const unsigned long long end = beg + kPartTile < n ? beg + kPartTile : n;
+  const unsigned long long beg = (unsigned long long)tile * tile_len;
+  const unsigned long long end = beg + tile_len < n ? beg + tile_len : n;
   for (unsigned long long j = beg + threadIdx.x; j < end; j += blockDim.x) atomicAdd(&hcount[regs[j]], 1u);
   __syncthreads();
   for (uint32_t r = threadIdx.x; r < n_regions; r += blockDim.x) hist[(size_t)r * n_tiles + tile] = hcount[r];
 }
 
 __global__ __launch_bounds__(1024) void k_part_scatter(const Rec* __restrict__ recs, unsigned long long n,
-                                                       uint32_t n_regions, uint32_t n_tiles,
+                                                       uint32_t n_regions, uint32_t n_tiles, uint32_t tile_len,
                                                        const uint32_t* __restrict__ offs, Rec* __restrict__ out) {
   __shared__ uint32_t cur[kMaxRegions];
   const uint32_t tile = blockIdx.x;
   for (uint32_t r = threadIdx.x; r < n_regions; r += blockDim.x) cur[r] = offs[(size_t)r * n_tiles + tile];
   __syncthreads();
-  const unsigned long long beg = (unsigned long long)tile * kPartTile;
-  const unsigned long long end = beg + kPartTile < n ? beg + kPartTile : n;
+  const unsigned long long beg = (unsigned long long)tile * tile_len;
+  const unsigned long long end = beg + tile_len < n ? beg + tile_len : n;
   for (unsigned long long j = beg + threadIdx.x; j < end; j += blockDim.x) {
     const Rec r = recs[j];
     out[atomicAdd(&cur[r.region], 1u)] = r;
@@ -1732,15 +1735,17 @@ int launch_aggregate(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsig
   }
   Rec* sorted = reinterpret_cast<Rec*>(c->d_recs2) + c->seg_base;
   const uint32_t n_regions = 1u << c->np_bits;
-  const uint32_t n_tiles = (uint32_t)((nr + kPartTile - 1) / kPartTile);
+  uint32_t tile_len = kPartTileMin;
+  while (tile_len < kPartTileMax && (unsigned long long)tile_len * kPartTilesWant < nr) tile_len <<= 1;
+  const uint32_t n_tiles = (uint32_t)((nr + tile_len - 1) / tile_len);
   const unsigned long long hl = (unsigned long long)n_regions * n_tiles;
   rc = ensure_buf(c, &c->d_hist, &c->hist_alloc, hl);
   if (rc) return rc;
-  k_part_hist<<<n_tiles, 1024, 0, c->stream>>>(c->d_regs, nr, n_regions, n_tiles, c->d_hist);
+  k_part_hist<<<n_tiles, 1024, 0, c->stream>>>(c->d_regs, nr, n_regions, n_tiles, tile_len, c->d_hist);
   HIPCHK(c, hipGetLastError());
   rc = exclusive_scan(c, c->d_hist, hl);
   if (rc) return rc;
-  k_part_scatter<<<n_tiles, 1024, 0, c->stream>>>(recs, nr, n_regions, n_tiles, c->d_hist, sorted);
+  k_part_scatter<<<n_tiles, 1024, 0, c->stream>>>(recs, nr, n_regions, n_tiles, tile_len, c->d_hist, sorted);
   HIPCHK(c, hipGetLastError());
   unsigned long long* st = c->d_starts + (size_t)c->n_segs * (n_regions + 1);
   k_seg_starts<<<(n_regions + 1 + 255) / 256, 256, 0, c->stream>>>(c->d_hist, n_tiles, n_regions, c->seg_base, nr, st);
