@@ -1172,6 +1172,52 @@ __global__ __launch_bounds__(kBlock) void k_cap_scatter(const Slot* S, const uns
   }
 }
 
+// The same scatter when the capped rules fit an LDS counter array (n_capped <=
+// kCapLds): each workgroup takes a contiguous chunk of the used list, ranks its
+// entries per rule with LDS atomics, reserves every rule's run with one global
+// atomic per (workgroup, rule), then writes the keys.  Constant work per entry,
+// where the wave grouping above loops once per distinct rule in the wave.
+constexpr int kCapLds = 16384;
+constexpr int kCapPer = 16;                 // entries per thread (1024 threads: a chunk of 16384)
+__global__ __launch_bounds__(1024) void k_cap_scatter_lds(const Slot* S, const unsigned long long* used,
+                                                          unsigned long long n_used, uint32_t n_capped,
+                                                          const uint32_t* cidx, const uint32_t* capped_start,
+                                                          uint32_t* capped_fill, unsigned long long* keys,
+                                                          unsigned long long max_keys, unsigned int* flags) {
+  __shared__ uint32_t cnt[kCapLds];
+  for (uint32_t r = threadIdx.x; r < n_capped; r += blockDim.x) cnt[r] = 0;
+  __syncthreads();
+  const unsigned long long base = (unsigned long long)blockIdx.x * (1024ull * kCapPer);
+  uint32_t cc[kCapPer], rank[kCapPer];
+  unsigned long long key[kCapPer];
+#pragma unroll
+  for (int k = 0; k < kCapPer; ++k) {
+    const unsigned long long i = base + (unsigned long long)k * blockDim.x + threadIdx.x;
+    cc[k] = 0xFFFFFFFFu;
+    key[k] = 0;
+    if (i < n_used) {
+      const unsigned long long u = used[i];
+      cc[k] = cidx[u >> 32];
+      if (cc[k] != 0xFFFFFFFFu) key[k] = S[(uint32_t)u].min_order;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kCapPer; ++k) rank[k] = cc[k] != 0xFFFFFFFFu ? atomicAdd(&cnt[cc[k]], 1u) : 0u;
+  __syncthreads();
+  for (uint32_t r = threadIdx.x; r < n_capped; r += blockDim.x) {
+    const uint32_t m = cnt[r];
+    if (m) cnt[r] = atomicAdd(&capped_fill[r], m);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kCapPer; ++k) {
+    if (cc[k] == 0xFFFFFFFFu) continue;
+    const unsigned long long pos = (unsigned long long)capped_start[cc[k]] + cnt[cc[k]] + rank[k];
+    if (pos < max_keys) keys[pos] = key[k];
+    else atomicOr(&flags[1], 16u);
+  }
+}
+
 // One workgroup per capped rule: the cap-th smallest key of its segment.  A
 // min/max pass bounds the keys; radix select then runs on (key - min) in 8-bit
 // digits from the highest set bit of (max - min) down, so the digits of keys
@@ -1612,9 +1658,17 @@ int cap_select(rsa_ctx* c, unsigned long long* out, uint32_t* h_n_capped) {
     HIPCHK(c, hipMalloc(&c->d_keys, want * sizeof(unsigned long long)));
     c->sort_alloc = want;
   }
-  k_cap_scatter<<<grid_for(c, n_used, 8), kBlock, 0, c->stream>>>(c->d_slots, c->d_used, n_used, c->d_cidx,
-                                                                  c->d_capped_start, c->d_capped_cnt, c->d_keys,
-                                                                  c->sort_alloc, c->d_flags);
+  if (n_used == 0) {
+  } else if (ncap <= (unsigned)kCapLds) {
+    const unsigned long long chunk = 1024ull * kCapPer;
+    k_cap_scatter_lds<<<(unsigned)((n_used + chunk - 1) / chunk), 1024, 0, c->stream>>>(
+        c->d_slots, c->d_used, n_used, ncap, c->d_cidx, c->d_capped_start, c->d_capped_cnt, c->d_keys, c->sort_alloc,
+        c->d_flags);
+  } else {
+    k_cap_scatter<<<grid_for(c, n_used, 8), kBlock, 0, c->stream>>>(c->d_slots, c->d_used, n_used, c->d_cidx,
+                                                                    c->d_capped_start, c->d_capped_cnt, c->d_keys,
+                                                                    c->sort_alloc, c->d_flags);
+  }
   HIPCHK(c, hipGetLastError());
   k_cap_select<<<ncap, kSelThreads, 0, c->stream>>>(c->d_keys, c->d_capped_start, c->d_capped_cnt, c->d_capped_gid,
                                                     c->cap, out);
