@@ -131,6 +131,7 @@ typedef struct rsa_pht_list {    /* 64 B */
 #define RSA_OPT_FORCE_DEFER 8  /* TESTING: every index candidate goes to the exact deferred-line path        */
 #define RSA_OPT_PROFILE_SKIP 3 /* PROFILING ONLY, results invalid: bit0 skips counters, bit1 skips the table, bit2 skips table updates */
 #define RSA_OPT_PRECHECK 9     /* pre-check monotone slot fields with a plain load before their atomics (default 1)       */
+#define RSA_OPT_WAVE_CAP_SCATTER 11 /* TESTING: cap scatter by wave grouping (the path for > 16384 capped rules) */
 #define RSA_OPT_STATS 10       /* PROFILING: count table work into the rsa_stats counters (default 0)                 */
 
 /* One distinct (rule, connection) aggregate, 40 B (connlist-reducer.py:162-176). */

@@ -1435,6 +1435,7 @@ struct rsa_ctx {
   bool index_loaded = false;
   bool indexed = false;
   bool force_defer = false;
+  bool wave_cap_scatter = false;       // testing: cap scatter by wave grouping (the > kCapLds path)
   // caller-owned counters
   unsigned long long* d_matches = nullptr;
   unsigned long long* d_hits = nullptr;
@@ -1659,7 +1660,7 @@ int cap_select(rsa_ctx* c, unsigned long long* out, uint32_t* h_n_capped) {
     c->sort_alloc = want;
   }
   if (n_used == 0) {
-  } else if (ncap <= (unsigned)kCapLds) {
+  } else if (ncap <= (unsigned)kCapLds && !c->wave_cap_scatter) {
     const unsigned long long chunk = 1024ull * kCapPer;
     k_cap_scatter_lds<<<(unsigned)((n_used + chunk - 1) / chunk), 1024, 0, c->stream>>>(
         c->d_slots, c->d_used, n_used, ncap, c->d_cidx, c->d_capped_start, c->d_capped_cnt, c->d_keys, c->sort_alloc,
@@ -1966,6 +1967,9 @@ int rsa_set_option(rsa_ctx* c, int option, int64_t value) {
       return RSA_OK;
     case RSA_OPT_FORCE_DEFER:
       c->force_defer = value != 0;
+      return RSA_OK;
+    case RSA_OPT_WAVE_CAP_SCATTER:
+      c->wave_cap_scatter = value != 0;
       return RSA_OK;
     case RSA_OPT_FILTER_STEPS:
       if (value < 1 || value > 8) return fail(c, RSA_ERR_ARG, "filter steps must be in [1, 8]");

@@ -34,6 +34,7 @@ RSA_OPT_AUTO_FILTER, RSA_OPT_USE_INDEX, RSA_OPT_PROFILE_SKIP, RSA_OPT_FILTER_SLI
 RSA_OPT_FORCE_DEFER = 8
 RSA_OPT_PRECHECK = 9
 RSA_OPT_STATS = 10
+RSA_OPT_WAVE_CAP_SCATTER = 11
 
 P = ctypes.c_void_p
 U32 = ctypes.c_uint32

@@ -109,6 +109,17 @@ def test_synth_parity_deferred_tail(engine):
         engine.set_option(native.RSA_OPT_FORCE_DEFER, 0)
 
 
+def test_synth_parity_wave_cap_scatter(engine):
+    """Cap resolution through the wave-grouped scatter (taken above 16384
+    capped rules; forced here) agrees with the oracle like the LDS-ranked one."""
+    from ruleset_analysis_amd import native
+    engine.set_option(native.RSA_OPT_WAVE_CAP_SCATTER, 1)
+    try:
+        _gpu_vs_oracle(engine, 2000, 300000, 5, seed=29, zipf=1.1)
+    finally:
+        engine.set_option(native.RSA_OPT_WAVE_CAP_SCATTER, 0)
+
+
 @pytest.mark.parametrize('broad,prefix', [(True, 64), (False, 64), (False, 0), (False, 4096)])
 def test_index_and_scan_agree_10k(engine, broad, prefix):
     """The perfect-hash index (after a linear prefix) and the plain linear scan
