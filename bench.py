@@ -12,13 +12,24 @@ classification fused with per-rule counters and the distinct-connection
 table), cap resolution, pass 2 when any rule is capped, and emission of the
 final connection records into HBM; for N > 1 also the merge (all_reduce of
 counters, all_to_all of records to owner ranks, threshold all_reduce, pass-2
-exchange, gather of the owners' records to rank 0).
+exchange, gather of the owners' records to rank 0) -- the MI355X replacement of
+the Hadoop shuffle (runAnalysis.sh:12,42-56).
 
-Prints ONE JSON line on rank 0.
+Ranks: ``--gpus N`` spawns N rank processes (one per GPU, torch
+multiprocessing, spawn context, before any GPU call in the parent); under
+``torch.distributed.run`` the ranks come from RANK/WORLD_SIZE/LOCAL_RANK and
+must agree with ``--gpus``.  Backend nccl (= RCCL over xGMI); ``--force-dist``
+runs the distributed merge even at N = 1.  ``--cpu-model`` (TESTING, no GPU)
+replaces the HIP library by tests/cpu_model.py so the spawn + merge path runs
+on CPU with gloo.
+
+Prints ONE JSON line on rank 0; after the timed
+steps, untimed full-size checks (``checks``) unless ``--no-check``.
 """
 import argparse
 import json
 import os
+import socket
 import sys
 import time
 
@@ -32,16 +43,15 @@ import rsa_pkg  # noqa: E402
 rsa_pkg.load()
 
 from ruleset_analysis_amd import acldb, synth  # noqa: E402
-from ruleset_analysis_amd.compile import CompiledRules  # noqa: E402
-from ruleset_analysis_amd.engine import DeviceBatch, Engine  # noqa: E402
+from ruleset_analysis_amd.compile import CompiledRules, RECORD_DTYPE, TUPLE_DTYPE  # noqa: E402
 from ruleset_analysis_amd.pipeline import built_hit_count  # noqa: E402
 
 BYTES_PER_LINE = 28          # 16 B tuple + 4 B timestamp code + 8 B order key
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
+N_SIMD = 256 * 4             # 256 CUs x 4 SIMDs
 # int32 VALU lane-ops/s: 256 CUs x 4 SIMDs x 32 lanes/cycle x 2.4 GHz (MI355X_MICROARCH.md:
-# a wave issues one VALU instruction over 2 cycles, 32 lanes per cycle)
-VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9
-SCATTER_ATOMIC_PEAK = 0.08e12 / 4   # 4-B device atomics/s, 64 lanes in 64 rows (MI355X_MICROARCH.md)
+# a wave64 VALU instruction occupies its SIMD for 2 cycles)
+VALU_PEAK_OPS = N_SIMD * 32 * 2.4e9
 OPS_PER_EVAL = 8             # 2 per address range test x 2 + 2 per port range test x 2
 CONFIGS = {
     # name: (rules, lines per GPU, cap, seed, zipf, interfaces, broad)
@@ -56,14 +66,14 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def build_shard(dbj, info, compiled, n, rank, seed, zipf, device, chunk=8_000_000, world=1):
-    """Generate this rank's contiguous slice of the global synthetic log straight
-    into HBM, in chunks (host memory stays bounded)."""
-    import torch
-    tuples = torch.empty((n, 4), dtype=torch.int32, device=device)
-    ts = torch.empty(n, dtype=torch.int32, device=device)
-    order = torch.empty(n, dtype=torch.int64, device=device)
-    n_hb = 0
+def die(msg, code=2):
+    log('bench.py: ' + msg)
+    sys.exit(code)
+
+
+def shard_chunks(dbj, info, compiled, n, rank, seed, zipf, world=1, chunk=8_000_000):
+    """This rank's contiguous slice of the global synthetic log, in chunks:
+    yields (offset, traffic dict, packed tuples, ts codes, order keys)."""
     span_total = 3 * 3600 * world
     for k, a in enumerate(range(0, n, chunk)):
         m = min(chunk, n - a)
@@ -73,11 +83,24 @@ def build_shard(dbj, info, compiled, n, rank, seed, zipf, device, chunk=8_000_00
         tr = synth.make_traffic((dbj, info), m, seed=seed * 1_000_003 + rank * 1009 + k, zipf=zipf, t0=t0,
                                 span=max(t1 - t0, 1), cid0=1_000_000 + g0)
         tup, t, o = synth.pack(tr, compiled)
+        yield a, tr, tup, t, o
+
+
+def build_shard(dbj, info, compiled, n, rank, seed, zipf, device, world=1):
+    """Generate this rank's shard straight into device memory (host memory stays bounded)."""
+    import torch
+    from ruleset_analysis_amd.engine import DeviceBatch
+    tuples = torch.empty((n, 4), dtype=torch.int32, device=device)
+    ts = torch.empty(n, dtype=torch.int32, device=device)
+    order = torch.empty(n, dtype=torch.int64, device=device)
+    n_hb = 0
+    for a, _tr, tup, t, o in shard_chunks(dbj, info, compiled, n, rank, seed, zipf, world):
+        m = len(tup)
         n_hb += built_hit_count(tup)
         tuples[a:a + m].copy_(torch.from_numpy(tup.view(np.int32).reshape(-1, 4)))
         ts[a:a + m].copy_(torch.from_numpy(t.view(np.int32)))
         order[a:a + m].copy_(torch.from_numpy(o.view(np.int64)))
-        log('shard: %d / %d lines generated' % (a + m, n))
+        log('rank %d shard: %d / %d lines generated' % (rank, a + m, n))
     return DeviceBatch(tuples, ts, order), n_hb
 
 
@@ -100,7 +123,7 @@ def cpu_baseline(dbj, info, seconds=15.0):
     t = time.perf_counter()
     op.run_pipeline(text, 'fw1', acls, fws, cap=1000)
     dt = time.perf_counter() - t
-    return {'value': n / dt, 'unit': 'lines/s', 'cores': 1, 'kind': 'port',
+    return {'value': n / dt, 'unit': 'lines/s', 'cores': 1, 'kind': 'port', 'host_cpus': os.cpu_count(),
             'sample': '%d lines of the same 10k-rule workload through oracle/pipeline.py '
                       '(mapper | LC_ALL=C sort | reducer restated in Python, 1 process), %.1f s' % (n, dt)}
 
@@ -126,51 +149,113 @@ def scan_work(compiled, batch, gids):
     return int(e.sum().item())
 
 
-def read_traffic(name):
-    """HBM bytes of the pass-1 kernel launches of one step (the 1/16 slice and the
-    rest, summed like `achieved`) from a committed rocprofv3 PMC summary
-    (profiles/<name>, written by tools/pmc_summary.py with the gfx950 FETCH_SIZE
-    correction of MI355X_MICROARCH.md §HBM), if present for this workload."""
+def read_profile(name):
     path = os.path.join(ROOT, 'profiles', name)
     if not os.path.exists(path):
         return None
     with open(path) as f:
-        return json.load(f).get('hbm_bytes_per_step')
+        return json.load(f)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=5)
-    ap.add_argument('--warmup', type=int, default=2)
-    ap.add_argument('--config', default='cfg3', choices=sorted(CONFIGS))
-    ap.add_argument('--lines', type=int, default=0, help='override lines per GPU')
-    ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--filter-slice', type=int, default=0, help='override RSA_OPT_FILTER_SLICE')
-    ap.add_argument('--opt', action='append', default=[], help='NAME=VALUE library option (e.g. FILTER_STEPS=3)')
-    ap.add_argument('--no-index', action='store_true', help='classify with the plain linear scan')
-    ap.add_argument('--prefix', type=int, default=0, help='entries per list scanned before the index')
-    args = ap.parse_args()
+def valu_busy(sq, kernel_prefix):
+    """VALU busy of one kernel from a committed rocprofv3 SQ-counter summary:
+    2 cycles per wave64 VALU instruction (MI355X_MICROARCH.md cycle table) x
+    SQ_INSTS_VALU / (SIMDs x per-XCD active cycles, GRBM_GUI_ACTIVE / 8)."""
+    if not sq:
+        return None
+    for name, c in sq.items():
+        if name.startswith(kernel_prefix) and c.get('GRBM_GUI_ACTIVE'):
+            return 2.0 * c['SQ_INSTS_VALU'] / (N_SIMD * c['GRBM_GUI_ACTIVE'] / 8.0)
+    return None
 
+
+def record_checksum(recs_u8):
+    """Order-independent checksum of a record set (sum of a 64-bit mix of each
+    40-B row, mod 2^64) on the device."""
     import torch
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if recs_u8.numel() == 0:
+        return 0
+    w = recs_u8.view(-1, 40)[:, :40].contiguous().view(torch.int64).view(-1, 5)
+    x = w[:, 0] * 0x100000001B3 + w[:, 1] * 0x9E3779B1 + w[:, 2] * 0x7F4A7C15 + w[:, 3] * 0x2545F491 + w[:, 4]
+    x = x ^ (x >> 29)
+    x = x * 0x5DEECE66D
+    x = x ^ (x >> 31)
+    return int(x.sum().item()) & 0xFFFFFFFFFFFFFFFF
+
+
+def full_size_checks(eng, batch, gbuf, n_rules, cap, recs_final, owner_rows=None):
+    """Untimed properties of the benched job at full size (no oracle: too large):
+    matches == per-rule line counts of the gids, hits likewise over hit lines,
+    every uncapped rule's connection counts sum to its hit+BUILT lines, and the
+    index-classified gids equal a linear scan of the whole lists."""
+    import torch
+    out = {}
+    flags = (batch.tuples[:, 3] >> 16) & 0xFF
+    g = gbuf.long()
+    ok = g >= 0
+    m = torch.bincount(g[ok], minlength=n_rules)[:n_rules]
+    hitm = ok & ((flags & 2) != 0)
+    h = torch.bincount(g[hitm], minlength=n_rules)[:n_rules]
+    out['matches_eq_gid_histogram'] = bool(torch.equal(m, eng.counters['matches'][:n_rules]))
+    out['hits_eq_gid_histogram'] = bool(torch.equal(h, eng.counters['hits'][:n_rules]))
+    out['sum_matches_eq_classified_lines'] = int(eng.counters['matches'][:n_rules].sum().item()) == int(ok.sum().item())
+    hb = hitm & ((flags & 4) != 0)
+    need = torch.bincount(g[hb], minlength=n_rules)[:n_rules]
+    rows = recs_final.view(-1, 40)
+    rg = rows[:, 8:12].contiguous().view(torch.int32).view(-1).long()
+    rc = rows[:, 24:28].contiguous().view(torch.int32).view(-1).long()
+    got = torch.zeros(n_rules, dtype=torch.int64, device=g.device).index_add_(0, rg, rc)
+    unc = eng.counters['thresh'][:n_rules] == -1
+    if cap == 0:
+        unc = torch.zeros_like(unc)
+    out['uncapped_rules_checked'] = int(unc.sum().item())
+    out['uncapped_count_sum_eq_hit_built_lines'] = bool(torch.equal(got[unc], need[unc]))
+    # the index vs the plain linear scan of the compiled lists, every line
+    eng.use_index(False)
+    g2 = eng.classify_only(batch)
+    eng.use_index(True)
+    out['index_gids_eq_linear_scan'] = bool(torch.equal(g2, gbuf))
+    out['ok'] = all(v for k, v in out.items() if isinstance(v, bool))
+    return out
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def rank_main(args, rank, world, local):
+    import torch
     dist = None
-    if world > 1:
+    if world > 1 or args.force_dist:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if args.backend == 'nccl':
+            torch.cuda.set_device(local)
+            dist.init_process_group('nccl', rank=rank, world_size=world, device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group('gloo', rank=rank, world_size=world)
     rules, lines, cap, seed, zipf, ifcs, broad = CONFIGS[args.config]
     if args.lines:
         lines = args.lines
+    if args.rules:
+        rules = args.rules
+    if args.cap is not None:
+        cap = args.cap
     t_setup = time.perf_counter()
     dbj, info = synth.make_db(seed, rules, interfaces=ifcs, broad=broad)
     compiled = CompiledRules(acldb.load_json(dbj))
     compiled.ensure_lists()
+    if args.cpu_model:
+        return _cpu_model_rank(args, dbj, info, compiled, lines, cap, seed, zipf, rank, world, dist)
+
+    from ruleset_analysis_amd import native
+    from ruleset_analysis_amd.dist import EngineBackend, merge
+    from ruleset_analysis_amd.engine import Engine
     eng = Engine(local)
     eng.load_compiled(compiled, index=not args.no_index, prefix=args.prefix)
-    from ruleset_analysis_amd import native
     if args.filter_slice:
         eng.set_option(native.RSA_OPT_FILTER_SLICE, args.filter_slice)
     for kv in args.opt:
@@ -179,7 +264,7 @@ def main():
     ent, _off = compiled.packed()
     batch, n_hb = build_shard(dbj, info, compiled, lines, rank, seed, zipf, eng.device, world=world)
     owner = None
-    if world > 1:
+    if dist is not None:
         owner = Engine(local)
         owner.set_rule_count(compiled.n_rules)
     gbuf = torch.empty(lines, dtype=torch.int32, device=eng.device)
@@ -187,23 +272,26 @@ def main():
     log('rank %d setup %.1fs: %d rules, %d lists, %d entries, %d lines, %d hit+built' % (
         rank, time.perf_counter() - t_setup, compiled.n_rules, compiled.n_lists(), len(ent), lines, n_hb))
 
-    # table capacity: the exact upper bound (every hit line a new connection);
-    # only the slots a job uses are cleared between jobs
+    # table capacity: the exact upper bound (every hit line a new connection),
+    # clamped by the library to its largest table; only the slots a job uses
+    # are cleared between jobs
     capacity = max(n_hb, 1)
     pass1_launch_ms = []
+    last = {}
 
     def step(timed):
         eng.reset(capacity, cap)
         eng.pass1(batch, gbuf)
         if timed:
             pass1_launch_ms.append(eng.last_pass1_times())
-        if world == 1:
+        if dist is None:
             if eng.resolve_cap():
                 eng.pass2(batch, gbuf)
             recs = eng.emit_device('final')
-            return recs.numel()
-        from ruleset_analysis_amd.dist import EngineBackend, merge
+            last['recs'] = recs
+            return recs.numel() // RECORD_DTYPE.itemsize
         out = merge(EngineBackend(eng, owner, [batch], [gbuf], cap), dist, world, rank)
+        last['merged'] = out
         return 0 if out is None else len(out[0])
 
     for _ in range(args.warmup):
@@ -226,19 +314,26 @@ def main():
     classify_ms = float(np.mean([a for a, _b in pass1_launch_ms]))
     aggregate_ms = float(np.mean([b for _a, b in pass1_launch_ms]))
     pass1_ms = classify_ms + aggregate_ms
-    # table-work counters of one more (untimed) step: lines combined, slot atomics
-    eng.set_option(native.RSA_OPT_STATS, 1)
-    eng.stats()
-    step(False)
-    torch.cuda.synchronize()
-    tstats = eng.stats()
-    eng.set_option(native.RSA_OPT_STATS, 0)
+    if args.dump and rank == 0:
+        _dump(args.dump, last, eng, cap)
+    checks = None
+    if not args.no_check and dist is None:
+        # untimed: a second job must give the bit-identical record set, then the
+        # full-size properties of its result
+        c1 = record_checksum(last['recs'])
+        step(False)
+        c2 = record_checksum(last['recs'])
+        checks = {'rerun_identical_records': c1 == c2, 'record_checksum': '%016x' % c1}
+        checks.update(full_size_checks(eng, batch, gbuf, compiled.n_rules, cap, last['recs']))
+        checks['ok'] = checks['ok'] and checks['rerun_identical_records']
+        log('checks: %s' % json.dumps(checks))
     sum_e = scan_work(compiled, batch, gbuf) if rank == 0 else 0
     if rank == 0:
         total_lines = lines * world * args.steps
         value = total_lines / dt
         achieved = BYTES_PER_LINE * lines / (pass1_ms * 1e-3) / 1e9
-        traffic = read_traffic('%s_pass1_pmc.json' % args.config)
+        pmc = read_profile('%s_pass1_pmc.json' % args.config)
+        sq = read_profile('%s_sq.json' % args.config)
         res = {
             'metric': 'log lines/sec classified (node) at %d rules; %% of HBM roofline' % rules,
             'value': value, 'unit': 'lines/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
@@ -250,35 +345,152 @@ def main():
             'config': {'workload': '%s: %d-rule ACL, %d lines per GPU, cap %d' % (args.config, compiled.n_rules,
                                                                                   lines, cap),
                        'rules': compiled.n_rules, 'lines_per_gpu': lines, 'cap': cap, 'parallelism': 'dp%d' % world,
-                       'records': n_rec},
+                       'backend': args.backend if dist is not None else 'none', 'records': n_rec},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                         'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
+                         'frac': achieved / HBM_PEAK_GBS,
+                         'traffic': pmc.get('hbm_bytes_per_step') if pmc else None,
+                         'traffic_source': 'profiles/%s_pass1_pmc.json' % args.config if pmc else None,
                          'kernel': 'pass 1 = k_classify + k_tail + aggregation (k_aggregate, k_part_hist/scan/k_part_scatter, '
                                    'k_reduce<1>) over the filter slices + rest of one step',
                          'kernel_ms': pass1_ms, 'bytes_per_line': BYTES_PER_LINE,
                          'kernels': {
                              'classify_ms': classify_ms,
                              'aggregate_ms': aggregate_ms,
-                             'classify_gbs': BYTES_PER_LINE * lines / (classify_ms * 1e-3) / 1e9,
-                             'aggregate_table_lines': tstats[0],
-                             'aggregate_slot_atomics': tstats[3],
-                             'note': 'aggregation = record append in line order, counting sort by table region, '
-                                     'per-region LDS reduction merged into region-owned slots with plain stores; '
-                                     'table counters are collected only in the untimed stats step'},
-                         'valu': {'achieved': OPS_PER_EVAL * sum_e / (pass1_ms * 1e-3) / 1e12,
-                                  'peak': VALU_PEAK_OPS / 1e12, 'unit': 'Tops/s',
-                                  'frac': OPS_PER_EVAL * sum_e / (pass1_ms * 1e-3) / VALU_PEAK_OPS,
-                                  'mean_scan_position': sum_e / lines,
-                                  'definition': 'SURVEY.md 8d linear-scan work: 8 int ops x E(t) per line, E = '
-                                                '1-based first-match position in the permit-only candidate list '
-                                                '(list length if unmatched); the index does less work than this, '
-                                                'so frac > 1 is possible'}},
+                             'classify_gbs': BYTES_PER_LINE * lines / (classify_ms * 1e-3) / 1e9},
+                         'valu': {'busy_classify': valu_busy(sq, 'k_classify'),
+                                  'busy_aggregate': valu_busy(sq, 'k_aggregate'),
+                                  'source': 'profiles/%s_sq.json' % args.config if sq else None,
+                                  'definition': '2 cycles x SQ_INSTS_VALU / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)'}},
+            'scan_work': {'mean_scan_position': sum_e / lines,
+                          'linear_scan_equivalent_tops': OPS_PER_EVAL * sum_e / (pass1_ms * 1e-3) / 1e12,
+                          'valu_peak_tops': VALU_PEAK_OPS / 1e12,
+                          'definition': 'SURVEY.md 8d linear-scan work: 8 int ops x E(t) per line, E = 1-based '
+                                        'first-match position in the permit-only candidate list (list length if '
+                                        'unmatched); the index does far less work than this, so this is a '
+                                        'scan-equivalent rate, not a utilisation'},
+            'checks': checks,
         }
         if world == 1 and not args.no_cpu_baseline:
             res['cpu_baseline'] = cpu_baseline(dbj, info)
         print(json.dumps(res), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+    return 0
+
+
+def _dump(path, last, eng, cap):
+    """TESTING: rank 0 writes the merged (or single-GPU) result as npz."""
+    if 'merged' in last:
+        recs, matches, hits, distinct, thresh = last['merged']
+    else:
+        res = eng.results(cap)
+        recs, matches, hits, distinct, thresh = res.records, res.matches, res.hits, res.distinct, res.thresh
+    np.savez(path, records=recs.view(np.uint8), matches=matches, hits=hits, distinct=distinct, thresh=thresh)
+
+
+def _cpu_model_rank(args, dbj, info, compiled, lines, cap, seed, zipf, rank, world, dist):
+    """TESTING: one rank of the spawn + merge path with the CPU model of
+    tests/cpu_model.py in place of the HIP library (no GPU)."""
+    sys.path.insert(0, os.path.join(ROOT, 'tests'))
+    import cpu_model
+    from ruleset_analysis_amd.dist import merge
+    ent, off = compiled.packed()
+    parts = list(shard_chunks(dbj, info, compiled, lines, rank, seed, zipf, world))
+    tup = np.concatenate([p[2] for p in parts])
+    ts = np.concatenate([p[3] for p in parts])
+    order = np.concatenate([p[4] for p in parts])
+    gids = cpu_model.classify_entries(ent, off, tup)
+    t0 = time.perf_counter()
+    out = None
+    for _ in range(max(args.steps, 1)):
+        out = merge(cpu_model.NumpyBackend.from_packed(compiled.n_rules, cap, gids, tup, ts, order), dist, world, rank)
+    dist.barrier()
+    dt = time.perf_counter() - t0
+    if rank == 0:
+        if args.dump:
+            recs, matches, hits, distinct, thresh = out
+            np.savez(args.dump, records=recs.view(np.uint8), matches=matches, hits=hits, distinct=distinct,
+                     thresh=thresh)
+        print(json.dumps({'metric': 'TESTING cpu-model merge (not a measurement)', 'value': lines * world / dt,
+                          'unit': 'lines/s', 'n_gpus': world, 'steps': args.steps, 'cpu_model': True,
+                          'records': len(out[0])}), flush=True)
+    dist.destroy_process_group()
+    return 0
+
+
+def _spawned(args, rank, world, port):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.exit(rank_main(args, rank, world, rank))
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=5)
+    ap.add_argument('--warmup', type=int, default=2)
+    ap.add_argument('--config', default='cfg3', choices=sorted(CONFIGS))
+    ap.add_argument('--lines', type=int, default=0, help='override lines per GPU')
+    ap.add_argument('--rules', type=int, default=0, help='override the expanded rule count')
+    ap.add_argument('--cap', type=int, default=None, help='override the per-rule connection cap')
+    ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'])
+    ap.add_argument('--force-dist', action='store_true', help='run the distributed merge even with one rank')
+    ap.add_argument('--cpu-model', action='store_true', help='TESTING: CPU model instead of the HIP library')
+    ap.add_argument('--dump', default='', help='TESTING: rank 0 writes the final result (npz) here')
+    ap.add_argument('--no-check', action='store_true', help='skip the untimed full-size checks')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--filter-slice', type=int, default=0, help='override RSA_OPT_FILTER_SLICE')
+    ap.add_argument('--opt', action='append', default=[], help='NAME=VALUE library option (e.g. FILTER_STEPS=3)')
+    ap.add_argument('--no-index', action='store_true', help='classify with the plain linear scan')
+    ap.add_argument('--prefix', type=int, default=0, help='entries per list scanned before the index')
+    return ap.parse_args(argv)
+
+
+def main():
+    args = parse_args()
+    if args.cpu_model and args.backend != 'gloo':
+        die('--cpu-model runs without a GPU: use --backend gloo')
+    if 'WORLD_SIZE' in os.environ and 'RANK' in os.environ:
+        # launched by torch.distributed.run: one process per rank already
+        world = int(os.environ['WORLD_SIZE'])
+        if world != args.gpus:
+            die('WORLD_SIZE=%d but --gpus %d: launch with --nproc-per-node equal to --gpus' % (world, args.gpus))
+        sys.exit(rank_main(args, int(os.environ['RANK']), world, int(os.environ.get('LOCAL_RANK', '0'))))
+    world = args.gpus
+    if world < 1:
+        die('--gpus must be >= 1')
+    if not args.cpu_model:
+        import torch
+        n_dev = torch.cuda.device_count()   # counts devices without initialising the GPU
+        if world > n_dev:
+            die('--gpus %d but %d GPU(s) visible' % (world, n_dev))
+    if world == 1:
+        if args.force_dist:
+            os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(_free_port()), RANK='0', WORLD_SIZE='1',
+                              LOCAL_RANK='0')
+        sys.exit(rank_main(args, 0, 1, 0))
+    # one process per rank; this parent never touches the GPU
+    import torch.multiprocessing as mp
+    ctx = mp.get_context('spawn')
+    port = _free_port()
+    procs = [ctx.Process(target=_spawned, args=(args, r, world, port)) for r in range(world)]
+    for p in procs:
+        p.start()
+    rc = 0
+    while procs:
+        for p in list(procs):
+            p.join(timeout=1.0)
+            if p.exitcode is None:
+                continue
+            procs.remove(p)
+            if p.exitcode != 0:
+                rc = rc or (p.exitcode if p.exitcode > 0 else 1)
+                log('bench.py: a rank exited with %d; stopping the others' % p.exitcode)
+                for q in procs:
+                    q.join(timeout=30)
+                    if q.exitcode is None:
+                        q.terminate()
+    sys.exit(rc)
 
 
 if __name__ == '__main__':

@@ -186,7 +186,10 @@ int rsa_set_rule_count(rsa_ctx *ctx, uint32_t n_rules);
 
 /* (Re)initialise the distinct-connection table with room for `capacity`
  * distinct (rule, connection) pairs, zero the bound counters and set the
- * per-rule cap (config.py:15 MAX_NUMBER_OF_CONNECTIONS_PER_RULE). */
+ * per-rule cap (config.py:15 MAX_NUMBER_OF_CONNECTIONS_PER_RULE).  `capacity`
+ * is an upper bound: it is clamped to the largest table (4096 regions of 65536
+ * slots at 2/3 load, ~179M entries); more distinct entries than the table holds
+ * fail the job with RSA_ERR_CAPACITY. */
 int rsa_reset(rsa_ctx *ctx, uint64_t capacity, uint32_t cap);
 
 /* Pass 1 — classify + aggregate a batch resident in HBM (mapper.py:123-189 fused

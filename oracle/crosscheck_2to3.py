@@ -8,7 +8,12 @@ box).  For each fixture case it:
    directory under /tmp (the converted code is never written into the repo);
 2. adds two shims next to them: ``IPy.py`` (this oracle's ``ipy`` restatement —
    IPy itself is not installed) and ``libfwregex.py`` (this oracle's
-   ``get_builtconn`` — the ``lib/fw-regex`` submodule is absent);
+   ``get_builtconn`` — the ``lib/fw-regex`` submodule is absent); Python 3
+   dicts iterate in insertion order where the reference's Python 2 dicts
+   iterate in hash-slot order, so the converted reducer's ``conns.keys()``
+   (``connlist-reducer.py:109,190``, the only dict whose order reaches the
+   output) is wrapped in ``oracle.py2dict``'s replay of CPython 2.7's slot order
+   (``py2order.py``), fed by the Python 3 dict's insertion order;
 3. builds ``accesslists.db`` with Python 3 ``shelve`` from the converted
    ``FirewallRule`` class, sets the cap in ``config.py``;
 4. runs ``mapred_input_dir=/x/<host>/y python3 mapper.py < log | LC_ALL=C sort |
@@ -71,6 +76,17 @@ def run_reference(work, db_json, log_text, host, cap):
     os.makedirs(work, exist_ok=True)
     for name in ('mapper.py', 'connlist-reducer.py', 'firewallrule.py', 'config.py'):
         _convert(os.path.join(REF, name), os.path.join(work, name))
+    red = os.path.join(work, 'connlist-reducer.py')
+    with open(red) as f:
+        code = f.read()
+    n_sites = code.count('entries = list(conns.keys())')
+    if n_sites != 2:
+        raise RuntimeError('expected 2 conns.keys() sites in the converted reducer, found %d' % n_sites)
+    code = code.replace('entries = list(conns.keys())', 'entries = _py2_keys(list(conns.keys()))')
+    code = 'from py2order import py2_keys as _py2_keys\n' + code
+    with open(red, 'w') as f:
+        f.write(code)
+    shutil.copy(os.path.join(HERE, 'py2dict.py'), os.path.join(work, 'py2order.py'))
     with open(os.path.join(work, 'config.py')) as f:
         cfg = f.read()
     cfg = cfg.replace('MAX_NUMBER_OF_CONNECTIONS_PER_RULE = 1000', 'MAX_NUMBER_OF_CONNECTIONS_PER_RULE = %d' % cap)

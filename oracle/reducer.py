@@ -6,9 +6,9 @@ Python-2 semantics that matter and how they are kept:
 * input lines are ``str`` decoded as latin-1 (byte-transparent); ``strip()`` is
   restricted to the ASCII whitespace Python 2's byte ``str.strip()`` removes;
 * connection-table rows are ordered by the ``"TOIP TOPORT"`` string
-  (``connlist-reducer.py:109-110``) with ties in dict order — Python 2's hash
-  order is unreproducible, so ties fall back to insertion (first-seen) order, the
-  order a Python 3 dict gives (SURVEY.md trap 8);
+  (``connlist-reducer.py:109-110``), a stable sort of ``conns.keys()``, so ties
+  keep CPython 2.7 dict order, replayed by ``oracle.py2dict`` from the
+  insertion order (SURVEY.md trap 8);
 * the distinct-connection cap ``len(conns) < MAX`` guards every update
   (``:151``), so once the cap-th connection is inserted the table freezes.
 
@@ -17,6 +17,8 @@ per-block result list used by the parity tests.
 """
 
 import re
+
+from .py2dict import py2_keys
 
 # connlist-reducer.py:25
 BUILT = re.compile(r'[a-zA-Z]+ [0-9 ]?[0-9] ([0-9:]+) ([a-zA-Z]+) ([0-9]+) ([0-9]+) .* Built (out|in)bound '
@@ -29,7 +31,7 @@ HEADER = '%6s %4s  %-15s %-14s %-5s %-19s  %-19s' % ('COUNT', 'PROTO', 'FROM IP'
 
 def _block(out, rule, hits, conns, first, last, cap):
     # connlist-reducer.py:108-126 / 185-206
-    order = sorted(conns, key=lambda c: ' '.join(c.split(';')[2:4]))
+    order = sorted(py2_keys(list(conns)), key=lambda c: ' '.join(c.split(';')[2:4]))
     out.append('{0}: access-list {1}, rule {2}: {3}'.format(rule.hostname, rule.accesslist, rule.ruleindex, str(rule)))
     out.append('{0}'.format(rule.original))
     out.append('Total number of hits: {0}'.format(hits))

@@ -192,7 +192,7 @@ def reducer_main(argv=None):
 
 
 def _reduce_text(events, runs, res, cap, ts_table, spells, ips, ports, finished=True):
-    from .report import NOISE1, HEADER
+    from .report import NOISE1, HEADER, table_order
     by_run = {}
     rec = res.records
     for k in np.argsort(rec['gid'], kind='stable'):
@@ -202,7 +202,12 @@ def _reduce_text(events, runs, res, cap, ts_table, spells, ips, ports, finished=
     def block(r):
         key, host, acl, rule = runs[r]
         rws = by_run.get(r, [])
-        rws = sorted(rws, key=lambda x: (ips[int(x['to_ip'])] + ' ' + ports[int(x['to_port'])], int(x['min_order'])))
+        if rws:
+            rws = [rws[k] for k in table_order([spells[int(x['pspell'])] for x in rws],
+                                               [ips[int(x['for_ip'])] for x in rws],
+                                               [ips[int(x['to_ip'])] for x in rws],
+                                               [ports[int(x['to_port'])] for x in rws],
+                                               [int(x['min_order']) for x in rws])]
         lines = ['{0}: access-list {1}, rule {2}: {3}'.format(host, acl, rule.ruleindex, str(rule)),
                  '{0}'.format(rule.original), 'Total number of hits: {0}'.format(int(res.hits[r]))]
         if cap == 0 or int(res.thresh[r]) != 0xFFFFFFFFFFFFFFFF:

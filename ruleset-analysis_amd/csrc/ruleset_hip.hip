@@ -1737,8 +1737,9 @@ int launch_classify(rsa_ctx* c, const uint4* t, uint64_t m, int32_t* go) {
   return RSA_OK;
 }
 
-// LDS-privatised counter capacity (rules): 3 x 4 B per rule, 156 KiB.  One
-// 1024-thread workgroup per CU (k_aggregate's registers allow no more).
+// LDS-privatised counter capacity (rules): 2 x 4 B per rule (lines, hits),
+// 104 KiB, so one 1024-thread workgroup is resident per CU; the grid is sized
+// for two per CU (launch_aggregate), i.e. two rounds of workgroups.
 constexpr int kCnt = 13312;
 
 // Exclusive scan of n uint32 in place (device).
@@ -2132,9 +2133,11 @@ int rsa_reset(rsa_ctx* c, uint64_t capacity, uint32_t cap) {
   if (!c->d_matches) return fail(c, RSA_ERR_STATE, "counters not bound (rsa_bind_counters)");
   // the table is at most kMaxRegions regions of 2^kRegionMaxBits slots
   const unsigned long long max_slots = (unsigned long long)kMaxRegions << kRegionMaxBits;
+  // A caller's capacity is an upper bound (callers pass the number of hit
+  // lines, the case where every line is a new connection): clamp it to the
+  // largest table; a real overflow still fails the job (RSA_ERR_CAPACITY).
   const unsigned long long max_cap = (max_slots - 64) / 3 * 2;
-  if (capacity > max_cap)
-    return fail(c, RSA_ERR_ARG, "capacity %llu > %llu distinct entries per ctx", (unsigned long long)capacity, max_cap);
+  if (capacity > max_cap) capacity = max_cap;
   HIPCHK(c, hipSetDevice(c->device));
   unsigned long long want = 1024;
   const unsigned long long need = capacity + capacity / 2 + 64;

@@ -9,13 +9,15 @@
   before a key group becomes the "Unable to unpack" noise pair
   (``:66-79``); every rule block is a blank line, the header, the original ACL
   line, the hit count, the cap NOTE (``:113-116``), the column header and the
-  connection rows (``:119-126``) ordered by the ``"TOIP TOPORT"`` string, ties by
-  first-seen order (trap 8).
+  connection rows (``:119-126``) ordered by the ``"TOIP TOPORT"`` string, a
+  stable sort of ``conns.keys()``: ties keep CPython 2.7 dict order, replayed
+  from the first-seen order by ``py2dict`` (trap 8).
 """
 
 import numpy as np
 
 from .logparse import PY2_WS, D_CLASSIFY, D_MISSING
+from .py2dict import iteration_order
 
 __all__ = ['mapper_output', 'reducer_report', 'block_lines', 'HEADER', 'dotted']
 
@@ -59,6 +61,20 @@ def _rows_by_gid(records):
     return {int(g): recs[s:e] for g, s, e in zip(gids, starts, ends)}
 
 
+def table_order(spell, from_ip, to_ip, to_port, first_seen):
+    """Row order of one rule's connection table (connlist-reducer.py:109-110):
+    ``conns.keys()`` of the Python 2 dict the rows were inserted into in
+    first-seen order, stable-sorted by ``"TOIP TOPORT"``."""
+    n = len(to_ip)
+    sort_key = [to_ip[k] + ' ' + to_port[k] for k in range(n)]
+    ins = sorted(range(n), key=lambda k: int(first_seen[k]))
+    if len(set(sort_key)) == n:            # no ties: dict order cannot show
+        return sorted(range(n), key=sort_key.__getitem__)
+    keys = [';'.join((spell[k], from_ip[k], to_ip[k], to_port[k])) for k in ins]
+    py2 = [ins[j] for j in iteration_order(keys)]
+    return sorted(py2, key=sort_key.__getitem__)
+
+
 def block_lines(host, acl, rule, hits, rows, capped, cap, ts_decode, pspell_table):
     """One rule block without the leading blank line (connlist-reducer.py:113-126)."""
     out = ['{0}: access-list {1}, rule {2}: {3}'.format(host, acl, rule.ruleindex, str(rule)),
@@ -68,14 +84,15 @@ def block_lines(host, acl, rule, hits, rows, capped, cap, ts_decode, pspell_tabl
                    'displayed.'.format(cap))
     out.append(HEADER)
     if rows is not None and len(rows):
+        spell = [pspell_table[int(p)] for p in rows['pspell']]
+        from_ip = [dotted(v) for v in rows['for_ip']]
         to_ip = [dotted(v) for v in rows['to_ip']]
         to_port = [str(int(p)) for p in rows['to_port']]
-        keyed = sorted(range(len(rows)), key=lambda k: (to_ip[k] + ' ' + to_port[k], int(rows['min_order'][k])))
-        for k in keyed:
+        for k in table_order(spell, from_ip, to_ip, to_port, rows['min_order']):
             r = rows[k]
-            out.append('%6d %4s %15s  %15s %-5s %19s  %19s' % (int(r['count']), pspell_table[int(r['pspell'])],
-                                                                 dotted(r['for_ip']), to_ip[k], to_port[k],
-                                                                 ts_decode(int(r['first'])), ts_decode(int(r['last']))))
+            out.append('%6d %4s %15s  %15s %-5s %19s  %19s' % (int(r['count']), spell[k], from_ip[k], to_ip[k],
+                                                                 to_port[k], ts_decode(int(r['first'])),
+                                                                 ts_decode(int(r['last']))))
     return out
 
 

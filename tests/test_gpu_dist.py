@@ -90,3 +90,17 @@ def test_two_ranks_one_gpu(cap):
     want = sorted(zip(*(rows[k].astype(int).tolist() for k in ('gid', 'pspell', 'for_ip', 'to_ip', 'to_port',
                                                                   'count', 'first', 'last'))))
     assert got == want
+
+
+@pytest.mark.parametrize('backend', ['nccl', 'gloo'])
+def test_bench_force_dist_one_gpu(tmp_path, backend):
+    """bench.py's distributed step at world 1 on the box's GPU: RCCL (nccl) moves
+    the device tensors itself (all_reduce, all_to_all_single with split sizes,
+    all_gather), gloo stages them through host memory; the merged result must
+    equal the C oracle."""
+    from test_bench_spawn import check_dump_against_oracle, run_bench
+    rules, lines, cap = 800, 400000, 40
+    line, got = run_bench(tmp_path, ['--gpus', '1', '--force-dist', '--backend', backend, '--rules', str(rules),
+                                     '--lines', str(lines), '--cap', str(cap), '--no-check'], timeout=400)
+    assert line['n_gpus'] == 1 and line['config']['backend'] == backend
+    check_dump_against_oracle(got, 1, rules, lines, cap)

@@ -160,8 +160,10 @@ def test_synth_parity_10k_rules(engine):
 
 
 def test_synth_parity_tightened_filter(engine):
-    # > 4M lines in one batch: the library aggregates 1/16, derives the per-rule
-    # filter, and skips the table for lines beyond it
+    # > 4M lines in one batch: the library aggregates the first 1M lines (the
+    # default slice is 1/256 of the batch, at least 1M), derives the per-rule
+    # filter, refines it after 4M and 16M lines, and skips the table for lines
+    # beyond it
     res, ref = _gpu_vs_oracle(engine, 800, 5_000_000, 40, seed=16, zipf=1.2)
     assert (ref['n_conns'] >= 40).sum() > 0           # the cap is engaged
 
@@ -170,15 +172,35 @@ def test_synth_parity_tightened_filter_shuffled(engine):
     _gpu_vs_oracle(engine, 800, 5_000_000, 40, seed=17, zipf=1.2, shuffle=True)
 
 
-def test_synth_parity_filter_steps(engine):
-    """Filter refined three times (after 1/256, 1/64, 1/16 of the batch)."""
+@pytest.mark.parametrize('steps,slice_', [(1, 256), (2, 256), (4, 256), (3, 16)])
+def test_synth_parity_filter_schedule(engine, steps, slice_):
+    """Other filter schedules: 1, 2 or 4 refinements, and a 1/16 first slice."""
     from ruleset_analysis_amd import native
-    engine.set_option(native.RSA_OPT_FILTER_STEPS, 3)
+    engine.set_option(native.RSA_OPT_FILTER_STEPS, steps)
+    engine.set_option(native.RSA_OPT_FILTER_SLICE, slice_)
     try:
         _gpu_vs_oracle(engine, 1500, 5_000_000, 40, seed=24, zipf=1.1, broad=False,
                        interfaces=('outside', 'partner'))
     finally:
         engine.set_option(native.RSA_OPT_FILTER_STEPS, 3)
+        engine.set_option(native.RSA_OPT_FILTER_SLICE, 256)
+
+
+def test_capacity_above_table_limit_is_clamped(engine):
+    """rsa_reset clamps a capacity above the largest table (callers pass the
+    hit-line count, an upper bound) instead of refusing the job."""
+    dbj, info = synth.make_db(33, 200)
+    tr = synth.make_traffic((dbj, info), 20000, seed=34)
+    compiled = CompiledRules(acldb.load_json(dbj))
+    tup, ts, order = synth.pack(tr, compiled)
+    engine.load_compiled(compiled)
+    b = DeviceBatch.from_numpy(tup, ts, order, engine.device)
+    res = engine.run([b], 1000, capacity=10 ** 12)
+    R = coracle.OracleRules(dbj)
+    cols, ots, oorder = coracle.inputs_from_traffic(R, tr)
+    ref = coracle.run(R, cols, ots, oorder, 1000)
+    assert np.array_equal(res.matches, ref['matches']) and len(res.records) == len(ref['rows']['gid'])
+    engine.reset(1024, 1000)   # back to a small table for the other tests
 
 
 def test_synth_parity_no_precheck(engine):
