@@ -54,12 +54,53 @@ N_SIMD = 256 * 4             # 256 CUs x 4 SIMDs
 VALU_PEAK_OPS = N_SIMD * 32 * 2.4e9
 OPS_PER_EVAL = 8             # 2 per address range test x 2 + 2 per port range test x 2
 CONFIGS = {
-    # name: (rules, lines per GPU, cap, seed, zipf, interfaces, broad)
-    'cfg3': (10000, 125_000_000, 1000, 3, None, ('outside',), False),
-    'cfg3_broad': (10000, 125_000_000, 1000, 3, None, ('outside',), True),
-    'cfg2': (1000, 100_000_000, 1000, 2, None, ('outside',), False),
-    'cfg5': (2500, 100_000_000, 1000, 5, 1.1, ('outside', 'partner', 'vpn', 'extranet'), False),
+    # ASA-shaped expanded ACLs (synth.make_db): rules, lines per GPU, cap, seed, zipf, interfaces, broad
+    'cfg3': dict(kind='asa', rules=10000, lines=125_000_000, cap=1000, seed=3, zipf=None, ifcs=('outside',),
+                 broad=False),
+    'cfg3_broad': dict(kind='asa', rules=10000, lines=125_000_000, cap=1000, seed=3, zipf=None, ifcs=('outside',),
+                       broad=True),
+    'cfg2': dict(kind='asa', rules=1000, lines=100_000_000, cap=1000, seed=2, zipf=None, ifcs=('outside',),
+                 broad=False),
+    'cfg5': dict(kind='asa', rules=2500, lines=100_000_000, cap=1000, seed=5, zipf=1.1,
+                 ifcs=('outside', 'partner', 'vpn', 'extranet'), broad=False),
+    # FortiGate policy set (synth_fg.make_config): 160 policies, 3 with 1024-65535 ranges, >= 3M expanded rules,
+    # traffic biased to late or no match (BASELINE config 4, the long-scan worst case)
+    'cfg4': dict(kind='fortigate', policies=160, wide=3, lines=100_000_000, cap=1000, seed=4, zipf=None),
 }
+
+
+class Workload(object):
+    """A benchmark configuration: the rule DB, its compiled lists, and a
+    generator of the global synthetic log."""
+
+    def __init__(self, name, rules=0, cap=None):
+        spec = dict(CONFIGS[name])
+        self.name, self.kind = name, spec['kind']
+        self.lines, self.seed, self.zipf = spec['lines'], spec['seed'], spec.get('zipf')
+        self.cap = spec['cap'] if cap is None else cap
+        if self.kind == 'asa':
+            self.rules = rules or spec['rules']
+            self.dbj, self.info = synth.make_db(self.seed, self.rules, interfaces=spec['ifcs'], broad=spec['broad'])
+            self.db = acldb.load_json(self.dbj)
+            self.describe = '%d-rule ACL' % self.rules
+            self.data = 'seeded ASA-shaped ACL, %s' % ('catch-all permits allowed' if spec['broad']
+                                                        else 'no catch-all permit')
+        else:
+            from ruleset_analysis_amd import fortigate, synth_fg
+            self.text, self.info = synth_fg.make_config(self.seed, n_policies=rules or spec['policies'],
+                                                        n_wide=spec['wide'])
+            self.db = fortigate.build_db(self.text)
+            self.describe = 'FortiGate %d-policy set' % (rules or spec['policies'])
+            self.data = 'seeded FortiGate config through the restated preprocessor; late/no-match traffic'
+        self.compiled = CompiledRules(self.db)
+        self.compiled.ensure_lists()
+
+    def traffic(self, m, seed, t0, span, cid0):
+        if self.kind == 'asa':
+            return synth.make_traffic((self.dbj, self.info), m, seed=seed, zipf=self.zipf, t0=t0, span=span,
+                                      cid0=cid0)
+        from ruleset_analysis_amd import synth_fg
+        return synth_fg.make_traffic(self.info, m, seed=seed, t0=t0, span=span, cid0=cid0)
 
 
 def log(*a):
@@ -71,7 +112,7 @@ def die(msg, code=2):
     sys.exit(code)
 
 
-def shard_chunks(dbj, info, compiled, n, rank, seed, zipf, world=1, chunk=8_000_000):
+def shard_chunks(wl, n, rank, world=1, chunk=8_000_000):
     """This rank's contiguous slice of the global synthetic log, in chunks:
     yields (offset, traffic dict, packed tuples, ts codes, order keys)."""
     span_total = 3 * 3600 * world
@@ -80,13 +121,12 @@ def shard_chunks(dbj, info, compiled, n, rank, seed, zipf, world=1, chunk=8_000_
         g0 = rank * n + a                                # global line index of the chunk
         t0 = 15 * 86400 + (g0 * span_total) // (n * world)
         t1 = 15 * 86400 + ((g0 + m) * span_total) // (n * world)
-        tr = synth.make_traffic((dbj, info), m, seed=seed * 1_000_003 + rank * 1009 + k, zipf=zipf, t0=t0,
-                                span=max(t1 - t0, 1), cid0=1_000_000 + g0)
-        tup, t, o = synth.pack(tr, compiled)
+        tr = wl.traffic(m, wl.seed * 1_000_003 + rank * 1009 + k, t0, max(t1 - t0, 1), 1_000_000 + g0)
+        tup, t, o = synth.pack(tr, wl.compiled)
         yield a, tr, tup, t, o
 
 
-def build_shard(dbj, info, compiled, n, rank, seed, zipf, device, world=1):
+def build_shard(wl, n, rank, device, world=1):
     """Generate this rank's shard straight into device memory (host memory stays bounded)."""
     import torch
     from ruleset_analysis_amd.engine import DeviceBatch
@@ -94,7 +134,7 @@ def build_shard(dbj, info, compiled, n, rank, seed, zipf, device, world=1):
     ts = torch.empty(n, dtype=torch.int32, device=device)
     order = torch.empty(n, dtype=torch.int64, device=device)
     n_hb = 0
-    for a, _tr, tup, t, o in shard_chunks(dbj, info, compiled, n, rank, seed, zipf, world):
+    for a, _tr, tup, t, o in shard_chunks(wl, n, rank, world):
         m = len(tup)
         n_hb += built_hit_count(tup)
         tuples[a:a + m].copy_(torch.from_numpy(tup.view(np.int32).reshape(-1, 4)))
@@ -104,14 +144,30 @@ def build_shard(dbj, info, compiled, n, rank, seed, zipf, device, world=1):
     return DeviceBatch(tuples, ts, order), n_hb
 
 
-def cpu_baseline(dbj, info, seconds=15.0):
-    """The oracle's restatement of the reference pipeline (mapper | sort | reducer,
-    pure Python like the reference) on a bounded sample of the same workload,
-    one core."""
+def cpu_baseline(wl, seconds=15.0):
+    """The reference pipeline restated on the CPU, timed on a bounded sample of
+    the same workload.  ASA configs: the oracle's pure-Python mapper | sort |
+    reducer (like the reference, one process).  FortiGate config: the expanded
+    DB has millions of rules (no Python objects for them), so the C oracle
+    (classify = the mapper's first-match scan, OpenMP over lines; reduce = the
+    reducer loop) is timed instead."""
+    if wl.kind != 'asa':
+        from oracle import coracle
+        R = coracle.OracleRules.from_fortigate(wl.text)
+        n = 20000
+        tr = wl.traffic(n, 99, 15 * 86400, 3 * 3600, 1_000_000)
+        cols, ts, order = coracle.inputs_from_traffic(R, tr)
+        t = time.perf_counter()
+        coracle.run(R, cols, ts, order, wl.cap)
+        dt = time.perf_counter() - t
+        threads = int(os.environ.get('OMP_NUM_THREADS', os.cpu_count() or 1))
+        return {'value': n / dt, 'unit': 'lines/s', 'cores': threads, 'kind': 'port', 'host_cpus': os.cpu_count(),
+                'sample': '%d lines of the same workload through oracle/rsa_oracle.c (linear first-match scan of the '
+                          'expanded rules, OpenMP over lines, + reducer loop), %.1f s' % (n, dt)}
     from oracle import pipeline as op
     from oracle.crosscheck_2to3 import oracle_db
-    acls, fws = oracle_db(dbj)
-    tr = synth.make_traffic((dbj, info), 200_000, seed=99)
+    acls, fws = oracle_db(wl.dbj)
+    tr = synth.make_traffic((wl.dbj, wl.info), 200_000, seed=99)
     lines = synth.render_lines(tr)
     # calibrate on a small prefix, then size the timed sample to ~`seconds`
     probe = 200
@@ -128,23 +184,127 @@ def cpu_baseline(dbj, info, seconds=15.0):
                       '(mapper | LC_ALL=C sort | reducer restated in Python, 1 process), %.1f s' % (n, dt)}
 
 
+def _hadoop_partition(key, n):
+    """org.apache.hadoop.mapred.lib.HashPartitioner over a streaming Text key:
+    (WritableComparator.hashBytes(key) & Integer.MAX_VALUE) % n, hashBytes =
+    31 * h + (signed) byte from h = 1, 32-bit wrap (runAnalysis.sh:44 uses 4
+    reducers)."""
+    h = 1
+    for b in key:
+        h = (31 * h + (b - 256 if b > 127 else b)) & 0xFFFFFFFF
+    return (h & 0x7FFFFFFF) % n
+
+
+def reference_pipeline_baseline(n_lines=1_000_000, rules=200, seed=1, procs=None, reducers=4):
+    """SURVEY.md §8d CPU baseline, BASELINE config 1: a 200-rule ACL and 1M
+    synthetic ASA log lines through the reference's job restated in Python
+    (oracle.cli: mapper.py / connlist-reducer.py as Unix filters), run as real
+    processes on this host:
+
+    (1) ``mapper | LC_ALL=C sort | reducer`` (SURVEY.md §3.1, one process each);
+    (2) Hadoop-like: ``procs`` mappers over contiguous splits, map output
+        partitioned by Hadoop's key hash into ``reducers`` parts
+        (runAnalysis.sh:12,44), ``LC_ALL=C sort --parallel``, one reducer per part.
+    """
+    import shutil
+    import subprocess
+    import tempfile
+    procs = procs or min(os.cpu_count() or 1, 16)
+    dbj, info = synth.make_db(seed, rules)
+    tr = synth.make_traffic((dbj, info), n_lines, seed=seed + 100)
+    text = ''.join(l + '\n' for l in synth.render_lines(tr))
+    work = tempfile.mkdtemp(prefix='rsa_cpu_baseline_')
+    try:
+        with open(os.path.join(work, 'db.json'), 'w') as f:
+            json.dump(dbj, f)
+        with open(os.path.join(work, 'log.txt'), 'w', encoding='latin-1', newline='') as f:
+            f.write(text)
+        env = dict(os.environ, LC_ALL='C', mapred_input_dir='/logs/fw1/part-00000', PYTHONPATH=ROOT,
+                   OMP_NUM_THREADS='1')
+        py = sys.executable
+        t = time.perf_counter()
+        subprocess.run('%s -m oracle.cli map db.json < log.txt | LC_ALL=C sort | %s -m oracle.cli reduce db.json 1000 '
+                       '> report.txt' % (py, py), shell=True, cwd=work, env=env, check=True)
+        t_single = time.perf_counter() - t
+        # Hadoop-like job
+        lines = text.splitlines(True)
+        cuts = np.linspace(0, len(lines), procs + 1).astype(int)
+        for k in range(procs):
+            with open(os.path.join(work, 'split%d.txt' % k), 'w', encoding='latin-1', newline='') as f:
+                f.write(''.join(lines[cuts[k]:cuts[k + 1]]))
+        t = time.perf_counter()
+        mappers = [subprocess.Popen('%s -m oracle.cli map db.json < split%d.txt > map%d.txt' % (py, k, k), shell=True,
+                                    cwd=work, env=env) for k in range(procs)]
+        for m in mappers:
+            if m.wait() != 0:
+                raise RuntimeError('mapper failed')
+        parts = [[] for _ in range(reducers)]
+        for k in range(procs):
+            with open(os.path.join(work, 'map%d.txt' % k), 'rb') as f:
+                for rec in f:
+                    body = rec[:-1] if rec.endswith(b'\n') else rec
+                    tab = body.find(b'\t')
+                    parts[_hadoop_partition(body if tab < 0 else body[:tab], reducers)].append(rec)
+        for r in range(reducers):
+            with open(os.path.join(work, 'part%d.txt' % r), 'wb') as f:
+                f.write(b''.join(parts[r]))
+        red = [subprocess.Popen('LC_ALL=C sort --parallel=%d part%d.txt | %s -m oracle.cli reduce db.json 1000 > '
+                                'red%d.txt' % (max(procs // reducers, 1), r, py, r), shell=True, cwd=work, env=env)
+               for r in range(reducers)]
+        for m in red:
+            if m.wait() != 0:
+                raise RuntimeError('reducer failed')
+        t_hadoop = time.perf_counter() - t
+        hits = lambda txt: sum(int(l.split(': ')[1]) for l in txt.splitlines() if l.startswith('Total number of hits'))
+        with open(os.path.join(work, 'report.txt'), encoding='latin-1') as f:
+            h1 = hits(f.read())
+        h2 = 0
+        for r in range(reducers):
+            with open(os.path.join(work, 'red%d.txt' % r), encoding='latin-1') as f:
+                h2 += hits(f.read())
+        if h1 != h2:
+            raise RuntimeError('the partitioned job disagrees with the single pipeline (%d vs %d hits)' % (h1, h2))
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
+    return {'config': 'BASELINE config 1: %d-rule ACL, %d synthetic ASA lines, seed %d' % (rules, n_lines, seed),
+            'single': {'value': n_lines / t_single, 'unit': 'lines/s', 'wall_s': t_single, 'cores': 1,
+                       'kind': 'port', 'pipeline': 'oracle.cli map | LC_ALL=C sort | oracle.cli reduce'},
+            'hadoop_like': {'value': n_lines / t_hadoop, 'unit': 'lines/s', 'wall_s': t_hadoop, 'cores': procs,
+                            'kind': 'port', 'pipeline': '%d mappers, Hadoop HashPartitioner to %d parts, '
+                                                        'sort --parallel, %d reducers' % (procs, reducers, reducers)},
+            'host_cpus': os.cpu_count(), 'total_hits': h1}
+
+
 def scan_work(compiled, batch, gids):
     """Sum over lines of E(t): the 1-based position of the
-    first match in the line's compiled permit-only candidate list, or the list
-    length when nothing matches; 0 for lines that are not classified.  Computed
-    on the GPU from the pass-1 gids (a searchsorted per line)."""
+    first match in the line's permit-only candidate list of EXPANDED rules, or
+    the list length when nothing matches; 0 for lines that are not classified.
+    Computed on the GPU from the pass-1 gids: the expanded rules of a list at or
+    before gid g are, per entry, the rules of its run with gid <= g."""
     import torch
     ent, off = compiled.packed()
     dev = gids.device
     lists = (batch.tuples[:, 3] & 0xFFFF).long()
     valid = ((batch.tuples[:, 3] >> 16) & 1) == 1
-    off_t = torch.from_numpy(off.astype(np.int64)).to(dev)
-    length = (off_t[1:] - off_t[:-1])[lists]
-    key = torch.from_numpy((np.repeat(np.arange(len(off) - 1, dtype=np.int64), np.diff(off).astype(np.int64)) << 32)
-                           | ent['gid'].astype(np.int64)).to(dev)
+    step = ent['step'].astype(np.int64)
+    stride = step & 0x7FFFFFFF
+    span = np.where(step >> 31, ent['port_span'].astype(np.int64) & 0xFFFF, ent['port_span'].astype(np.int64) >> 16)
+    count = np.where(stride > 0, span + 1, 1)
+    # expanded gids of every list, ascending (runs unrolled)
+    L = np.repeat(np.arange(len(off) - 1, dtype=np.int64), np.diff(off).astype(np.int64))
+    Lx = np.repeat(L, count)
+    base = np.repeat(ent['gid'].astype(np.int64), count)
+    k = np.arange(len(base)) - np.repeat(np.cumsum(count) - count, count)
+    g = base + k * np.repeat(stride, count)
+    key_np = np.unique((Lx << 32) | g)
+    lens = np.bincount(key_np >> 32, minlength=len(off) - 1)
+    starts = np.concatenate([[0], np.cumsum(lens)])
+    key = torch.from_numpy(key_np).to(dev)
+    st = torch.from_numpy(starts.astype(np.int64)).to(dev)
+    ln = torch.from_numpy(lens.astype(np.int64)).to(dev)
     q = (lists << 32) | gids.long().clamp(min=0)
-    pos = torch.searchsorted(key, q) - off_t[lists] + 1
-    e = torch.where(gids >= 0, pos, length)
+    pos = torch.searchsorted(key, q) - st[lists] + 1
+    e = torch.where(gids >= 0, pos, ln[lists])
     e = torch.where(valid, e, torch.zeros_like(e))
     return int(e.sum().item())
 
@@ -237,19 +397,13 @@ def rank_main(args, rank, world, local):
             dist.init_process_group('nccl', rank=rank, world_size=world, device_id=torch.device('cuda', local))
         else:
             dist.init_process_group('gloo', rank=rank, world_size=world)
-    rules, lines, cap, seed, zipf, ifcs, broad = CONFIGS[args.config]
-    if args.lines:
-        lines = args.lines
-    if args.rules:
-        rules = args.rules
-    if args.cap is not None:
-        cap = args.cap
     t_setup = time.perf_counter()
-    dbj, info = synth.make_db(seed, rules, interfaces=ifcs, broad=broad)
-    compiled = CompiledRules(acldb.load_json(dbj))
-    compiled.ensure_lists()
+    wl = Workload(args.config, rules=args.rules, cap=args.cap)
+    lines = args.lines or wl.lines
+    cap = wl.cap
+    compiled = wl.compiled
     if args.cpu_model:
-        return _cpu_model_rank(args, dbj, info, compiled, lines, cap, seed, zipf, rank, world, dist)
+        return _cpu_model_rank(args, wl, lines, cap, rank, world, dist)
 
     from ruleset_analysis_amd import native
     from ruleset_analysis_amd.dist import EngineBackend, merge
@@ -262,7 +416,7 @@ def rank_main(args, rank, world, local):
         k, v = kv.split('=')
         eng.set_option(getattr(native, 'RSA_OPT_' + k), int(v))
     ent, _off = compiled.packed()
-    batch, n_hb = build_shard(dbj, info, compiled, lines, rank, seed, zipf, eng.device, world=world)
+    batch, n_hb = build_shard(wl, lines, rank, eng.device, world=world)
     owner = None
     if dist is not None:
         owner = Engine(local)
@@ -335,16 +489,16 @@ def rank_main(args, rank, world, local):
         pmc = read_profile('%s_pass1_pmc.json' % args.config)
         sq = read_profile('%s_sq.json' % args.config)
         res = {
-            'metric': 'log lines/sec classified (node) at %d rules; %% of HBM roofline' % rules,
+            'metric': 'log lines/sec classified (node) at %d rules; %% of HBM roofline' % (
+                wl.rules if wl.kind == 'asa' else compiled.n_rules),
             'value': value, 'unit': 'lines/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
             'ms_per_step': dt / args.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
-            'vs_baseline': None, 'dtype': 'u32', 'data': 'synthetic (seeded ASA connection tuples, pre-parsed, '
-                                                          'resident in HBM; seeded ACL, %s)' % (
-                                                              'catch-all permits allowed' if broad else
-                                                              'no catch-all permit'),
-            'config': {'workload': '%s: %d-rule ACL, %d lines per GPU, cap %d' % (args.config, compiled.n_rules,
-                                                                                  lines, cap),
-                       'rules': compiled.n_rules, 'lines_per_gpu': lines, 'cap': cap, 'parallelism': 'dp%d' % world,
+            'vs_baseline': None, 'dtype': 'u32',
+            'data': 'synthetic (seeded ASA connection tuples, pre-parsed, resident in HBM; %s)' % wl.data,
+            'config': {'workload': '%s: %s (%d expanded rules, %d candidate-list entries), %d lines per GPU, cap %d'
+                                   % (args.config, wl.describe, compiled.n_rules, len(ent), lines, cap),
+                       'rules': compiled.n_rules, 'entries': len(ent), 'lines_per_gpu': lines, 'cap': cap,
+                       'parallelism': 'dp%d' % world,
                        'backend': args.backend if dist is not None else 'none', 'records': n_rec},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': achieved / HBM_PEAK_GBS,
@@ -371,7 +525,7 @@ def rank_main(args, rank, world, local):
             'checks': checks,
         }
         if world == 1 and not args.no_cpu_baseline:
-            res['cpu_baseline'] = cpu_baseline(dbj, info)
+            res['cpu_baseline'] = cpu_baseline(wl)
         print(json.dumps(res), flush=True)
     if dist is not None:
         dist.destroy_process_group()
@@ -388,14 +542,15 @@ def _dump(path, last, eng, cap):
     np.savez(path, records=recs.view(np.uint8), matches=matches, hits=hits, distinct=distinct, thresh=thresh)
 
 
-def _cpu_model_rank(args, dbj, info, compiled, lines, cap, seed, zipf, rank, world, dist):
+def _cpu_model_rank(args, wl, lines, cap, rank, world, dist):
     """TESTING: one rank of the spawn + merge path with the CPU model of
     tests/cpu_model.py in place of the HIP library (no GPU)."""
     sys.path.insert(0, os.path.join(ROOT, 'tests'))
     import cpu_model
     from ruleset_analysis_amd.dist import merge
+    compiled = wl.compiled
     ent, off = compiled.packed()
-    parts = list(shard_chunks(dbj, info, compiled, lines, rank, seed, zipf, world))
+    parts = list(shard_chunks(wl, lines, rank, world))
     tup = np.concatenate([p[2] for p in parts])
     ts = np.concatenate([p[3] for p in parts])
     order = np.concatenate([p[4] for p in parts])
@@ -439,6 +594,10 @@ def parse_args(argv=None):
     ap.add_argument('--dump', default='', help='TESTING: rank 0 writes the final result (npz) here')
     ap.add_argument('--no-check', action='store_true', help='skip the untimed full-size checks')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-baseline-only', action='store_true',
+                    help='run only the SURVEY.md 8d CPU baseline (config 1 through the restated reference job)')
+    ap.add_argument('--baseline-lines', type=int, default=1_000_000)
+    ap.add_argument('--baseline-procs', type=int, default=0)
     ap.add_argument('--filter-slice', type=int, default=0, help='override RSA_OPT_FILTER_SLICE')
     ap.add_argument('--opt', action='append', default=[], help='NAME=VALUE library option (e.g. FILTER_STEPS=3)')
     ap.add_argument('--no-index', action='store_true', help='classify with the plain linear scan')
@@ -448,6 +607,10 @@ def parse_args(argv=None):
 
 def main():
     args = parse_args()
+    if args.cpu_baseline_only:
+        print(json.dumps(reference_pipeline_baseline(n_lines=args.baseline_lines, procs=args.baseline_procs or None)),
+              flush=True)
+        return
     if args.cpu_model and args.backend != 'gloo':
         die('--cpu-model runs without a GPU: use --backend gloo')
     if 'WORLD_SIZE' in os.environ and 'RANK' in os.environ:

@@ -51,44 +51,58 @@ typedef struct rsa_tuple {
 /* One compiled candidate-list entry, 32 B: an expanded permit rule reduced to
  * the integer predicate of FirewallRule.__contains__ (firewallrule.py:128-174).
  * Deny rules and rules whose protocol cannot match the list's protocol are
- * dropped at compile time (they can never be a connection's first match). */
+ * dropped at compile time (they can never be a connection's first match).
+ *
+ * A run entry (step != 0) stands for the rules gid, gid + stride, ...,
+ * gid + span * stride that the preprocessors expanded from one port range
+ * (preprosess_access_lists.py:58-89,256-276; preprosess_fortigate_acl.py:90-100,
+ * 184-186), each holding ONE port of the range: a connection with port p in
+ * [lo, lo + span] matches the rule gid + (p - lo) * stride of the run.  Lists
+ * are in ascending first-gid order (the gid field). */
+#define RSA_STEP_SPORT 0x80000000u /* run over the source port (else the destination port) */
 typedef struct rsa_rule_entry {
   uint32_t src_lo, src_span;  /* (src - src_lo) <= src_span: IPy containment, */
   uint32_t dst_lo, dst_span;  /* net.ip <= x < net.ip + net.len()            */
   uint32_t port_lo;           /* sport_lo | dport_lo << 16                 */
   uint32_t port_span;         /* (sport_hi-sport_lo) | (dport_hi-dport_lo) << 16 */
-  uint32_t gid;               /* global rule id = acl base + expanded ruleindex */
-  uint32_t reserved;
+  uint32_t gid;               /* global rule id = acl base + expanded ruleindex (first rule of a run) */
+  uint32_t step;              /* 0, or run stride | RSA_STEP_SPORT if the run varies the source port */
 } rsa_rule_entry;
 
 /* Pruned perfect-hash tuple-space index (optional; compile.py build_index).
  * Per candidate list: entries [0, prefix) are scanned linearly; entries >= prefix
- * whose addresses are prefixes and whose ports are "any" or one value are
- * grouped by (src mask, dst mask) (<= 64 groups per list, ascending smallest
- * entry index) and, inside a group, by port class c = 0..3 with port mask
- * {0, 0xFFFF0000 (dport), 0x0000FFFF (sport), 0xFFFFFFFF}.  Each (group, class)
- * owns a CHD (hash-and-displace) perfect-hash table over the masked key
- * (src & src_mask, dst & dst_mask, ports & port_mask), ports = sport | dport << 16:
+ * whose addresses are prefixes and whose ports are "any" or one value (and that
+ * are not run entries) are grouped by (src mask, dst mask) (<= 64 groups per
+ * record, ascending smallest entry index) and, inside a group, by port class
+ * c = 0..3 with port mask {0, 0xFFFF0000 (dport), 0x0000FFFF (sport),
+ * 0xFFFFFFFF}.  Each (group, class) owns a CHD (hash-and-displace) perfect-hash
+ * table over the masked key (src & src_mask, dst & dst_mask, ports & port_mask),
+ * ports = sport | dport << 16:
  *   H    = fmix32(ks ^ 0x9E3779B9) ^ fmix32(kd ^ 0x7F4A7C15) ^ fmix32(kp ^ 0x2545F491)
  *   d    = disp[disp_off + ((H >> 16) & disp_mask)]            (uint16 units of the image)
  *   slot = hi32((H + d * ((H * 0x2C1B3C6D) | 1)) * n_slots)    (32-bit wrap)
- *   word = image[slot_off + slot] = (H & 0xFFFF) << 16 | list-local entry index,
+ *   word = image[slot_off + slot] = (H & 0xFFFF) << 16 | record-local entry index,
  *          0xFFFFFFFF = empty (image word 0 is always empty: absent classes
  *          point there with n_slots = 1)
  * holding the smallest entry index with that key.  Pruning: per non-zero src
- * (dst) mask of a list, a CHD table over H = fmix32((src & mask) ^ 0x9E3779B9)
+ * (dst) mask of a record, a CHD table over H = fmix32((src & mask) ^ 0x9E3779B9)
  * (dst: ^ 0x7F4A7C15) whose word value indexes a uint64 bitmap of the groups
  * holding a rule on that prefix; groups with mask 0 are in src_any (dst_any).
  * A tuple probes only the groups in (src bitmap & dst bitmap).  All other
- * entries are residual (a gid-ascending list scanned linearly).  The answer is
- * identical to the linear scan: the minimum matching gid (the device verifies
- * the hashed candidate against the full entry).
+ * entries are residual (a first-gid-ascending list scanned linearly).
+ *
+ * Lists longer than 0xFFFE entries are chains of records, one per chunk of
+ * 0xFFFE entries (records n_lists .. n_records-1 are the continuation chunks):
+ * a lane moves to record `next` only while its best gid exceeds `next_min`.
+ * The answer is identical to the linear scan: the minimum matching gid (the
+ * device verifies the hashed candidate against the full entry).
  *
  * Everything lives in ONE uint32 image: word 0 = 0xFFFFFFFF, word 1 =
- * RSA_PHT_MAGIC, word 2 = n_lists, word 3 = list_off (word offset of n_lists
- * rsa_pht_list records); records sit at 4-word aligned offsets, bitmaps at
- * even offsets (low word first). */
-#define RSA_PHT_MAGIC 0x33415352u
+ * RSA_PHT_MAGIC, word 2 = n_lists, word 3 = list_off (word offset of n_records
+ * rsa_pht_list records), word 4 = n_records, words 5..7 = 0; records sit at
+ * 4-word aligned offsets, bitmaps at even offsets (low word first). */
+#define RSA_PHT_MAGIC 0x34415352u
+#define RSA_PHT_NONE 0xFFFFFFFFu
 
 typedef struct rsa_pht_table {
   uint32_t slot_off;   /* first slot word in the image                           */
@@ -99,7 +113,7 @@ typedef struct rsa_pht_table {
 
 typedef struct rsa_pht_group {   /* 80 B */
   uint32_t src_mask, dst_mask;
-  uint32_t min_idx;          /* smallest list-local entry index in the group      */
+  uint32_t min_idx;          /* smallest record-local entry index in the group    */
   uint32_t n_real;           /* classes with a real table                         */
   rsa_pht_table table[4];    /* port classes any, dport, sport, sport+dport       */
 } rsa_pht_group;
@@ -111,16 +125,19 @@ typedef struct rsa_pht_mask {    /* 32 B: one pruning table */
   rsa_pht_table table;       /* word value = bitmap index                         */
 } rsa_pht_mask;
 
-typedef struct rsa_pht_list {    /* 64 B */
+typedef struct rsa_pht_list {    /* 80 B: one list (or one chained chunk of a list) */
   uint32_t group_off, n_groups;  /* rsa_pht_group records (image word offset)     */
   uint32_t mask_off, n_masks;    /* rsa_pht_mask records                          */
-  uint32_t resid_beg, resid_end; /* this list's residual entries                 */
-  uint32_t prefix;               /* entries scanned linearly before the index    */
+  uint32_t resid_beg, resid_end; /* this record's residual entries               */
+  uint32_t prefix;               /* entries scanned linearly before the index (first record only) */
   uint32_t bm_off;               /* uint64 bitmaps (image word offset, even)     */
   uint32_t src_any_lo, src_any_hi, dst_any_lo, dst_any_hi;
-  uint32_t entry_beg, entry_len; /* the list in rsa_load_rules' entries          */
+  uint32_t entry_beg, entry_len; /* this record's entries in rsa_load_rules' entries */
   uint32_t n_bitmaps;
-  uint32_t reserved;
+  uint32_t after_min;            /* smallest gid of the list's entries >= prefix (RSA_PHT_NONE: none) */
+  uint32_t next;                 /* continuation record, or RSA_PHT_NONE           */
+  uint32_t next_min;             /* smallest gid of the continuation chunk          */
+  uint32_t reserved[2];
 } rsa_pht_list;
 
 /* Options (rsa_set_option). */

@@ -30,7 +30,7 @@ _lib = None
 def build():
     os.makedirs(BUILD, exist_ok=True)
     if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(SRC):
-        subprocess.run(['gcc', '-O2', '-shared', '-fPIC', '-o', LIB, SRC], check=True)
+        subprocess.run(['gcc', '-O2', '-fopenmp', '-shared', '-fPIC', '-o', LIB, SRC], check=True)
     return LIB
 
 
@@ -84,6 +84,47 @@ class OracleRules(object):
         self.dp_off = np.array(dp_off, np.uint32); self.dp_len = np.array(dp_len, np.uint32)
         self.lists = {}
         self.cand = []
+
+    @classmethod
+    def from_fortigate(cls, text):
+        """Rules of a FortiGate config expanded by oracle.fortigate (the
+        restated preprocessor), as the arrays the C oracle scans."""
+        from . import fortigate
+        host, firewalls, acls = fortigate.expand(text)
+        self = cls.__new__(cls)
+        self.groups, self.base = [], {}
+        self.proto_names = dict(PROTO_ID)
+        parts = []
+        n = 0
+        for acl in sorted(acls):
+            self.base[(host, acl)] = n
+            self.groups.append((host, acl))
+            c = fortigate.as_columns(acls[acl])
+            parts.append(c)
+            n += len(c['action'])
+        self.n_rules = n
+        self.dbj = {'firewalls': firewalls,
+                    'accesslists': {host: {acl: {'protocols': acls[acl].protocols} for acl in acls}}}
+        cat = lambda k, dt: np.concatenate([p[k] for p in parts]).astype(dt) if parts else np.zeros(0, dt)
+        self.action = cat('action', np.uint8)
+        self.proto = np.array([self._pid(x) for p in parts for x in p['proto']], np.uint8)
+        self.v4src = np.ones(n, np.uint8)
+        self.v4dst = np.ones(n, np.uint8)
+        self.src, self.dst = cat('src', np.uint32), cat('dst', np.uint32)
+        self.src_len, self.dst_len = cat('src_len', np.uint64), cat('dst_len', np.uint64)
+        ports = np.empty(2 * n, np.int32)
+        ports[0::2] = cat('sport', np.int32)
+        ports[1::2] = cat('dport', np.int32)
+        self.ports = ports if n else np.zeros(1, np.int32)
+        self.sp_off = (2 * np.arange(n)).astype(np.uint32)
+        self.dp_off = self.sp_off + 1
+        self.sp_len = np.ones(n, np.uint32)
+        self.dp_len = np.ones(n, np.uint32)
+        self.rules = None
+        self.lists = {}
+        self.cand = []
+        self.host = host
+        return self
 
     def _pid(self, name):
         if name not in self.proto_names:
@@ -215,13 +256,15 @@ def inputs_from_traffic(R, tr):
     host = tr['host']
     names = ('tcp', 'udp')
     lst = np.full(n, -1, np.int64)
+    acl_of = tr.get('acl_of') or ['%s_access_in' % ifc for ifc in tr['interfaces']]
     for p in (0, 1):
         for k, ifc in enumerate(tr['interfaces']):
             w = np.isin(form, [F_BUILT_FORM, F_NONHIT, F_NOYEAR]) & (tr['ifc'] == k) & (tr['proto'] == p)
-            lst[w] = R.list_id(host, '%s_access_in' % ifc, names[p])
+            if w.any():
+                lst[w] = R.list_id(host, acl_of[k], names[p])
         w = (form == F_OUTBOUND) & (tr['proto'] == p)
         if w.any():
-            lst[w] = R.list_id(host, 'inside_access_in', names[p])
+            lst[w] = R.list_id(host, tr.get('inside_acl', 'inside_access_in'), names[p])
     proto = np.where(tr['proto'] == 0, PROTO_ID['tcp'], PROTO_ID['udp'])
     flags = (np.where(np.isin(form, [F_BUILT_FORM, F_NOYEAR, F_OUTBOUND]), F_HIT, 0)
              | np.where(np.isin(form, [F_BUILT_FORM, F_NONHIT, F_OUTBOUND]), F_BUILT, 0)

@@ -69,7 +69,11 @@ void rsa_oracle_classify(uint64_t n, const int32_t *list_of, const uint32_t *pro
                          uint64_t *evals_out) {
   rules_t R = {action, proto, v4src, v4dst, rsrc, rdst, src_len, dst_len, sp_off, sp_len, dp_off, dp_len, ports};
   uint64_t evals = 0;
-  for (uint64_t i = 0; i < n; ++i) {
+  /* lines are independent (one mapper call each): spread them over the host's
+   * cores; each line is still the reference's sequential first-match scan */
+#pragma omp parallel for schedule(dynamic, 16) reduction(+ : evals)
+  for (int64_t ii = 0; ii < (int64_t)n; ++ii) {
+    const uint64_t i = (uint64_t)ii;
     gid_out[i] = -1;
     const int32_t l = list_of[i];
     if (l < 0) continue;

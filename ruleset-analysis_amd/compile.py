@@ -25,7 +25,9 @@ from .firewallrule import FirewallRule
 __all__ = ['RULE_DTYPE', 'TUPLE_DTYPE', 'RECORD_DTYPE', 'CompiledRules']
 
 RULE_DTYPE = np.dtype([('src_lo', '<u4'), ('src_span', '<u4'), ('dst_lo', '<u4'), ('dst_span', '<u4'),
-                       ('port_lo', '<u4'), ('port_span', '<u4'), ('gid', '<u4'), ('reserved', '<u4')])
+                       ('port_lo', '<u4'), ('port_span', '<u4'), ('gid', '<u4'), ('step', '<u4')])
+STEP_SPORT = 0x80000000     # rsa_rule_entry.step: the run varies the source port (else the destination port)
+RUN_MIN = 16                # shorter runs stay single-port entries (the hashed index takes those)
 TUPLE_DTYPE = np.dtype([('src', '<u4'), ('dst', '<u4'), ('sport', '<u2'), ('dport', '<u2'), ('list', '<u2'),
                         ('flags', 'u1'), ('pspell', 'u1')])
 RECORD_DTYPE = np.dtype([('min_order', '<u8'), ('gid', '<u4'), ('for_ip', '<u4'), ('to_ip', '<u4'),
@@ -60,17 +62,100 @@ def _addr_range(ip):
 
 
 def candidate_indices(protocols, proto):
-    """mapper.py:159-166, including its KeyError behaviour."""
+    """mapper.py:159-166, including its KeyError behaviour (index lists may be
+    Python lists or, for columnar rule stores, integer arrays)."""
     if proto in ('tcp', 'udp'):
         if proto in protocols:
-            return sorted(protocols[proto] + protocols['ip'])
+            a, b = protocols[proto], protocols['ip']
+            if isinstance(a, np.ndarray) or isinstance(b, np.ndarray):
+                return np.sort(np.concatenate([np.asarray(a, np.int64), np.asarray(b, np.int64)]), kind='stable')
+            return sorted(a + b)
         return protocols['ip']
     return protocols[proto]
 
 
+def compress_runs(rows, min_run=RUN_MIN):
+    """Collapse runs of single-port entries into stepped range entries (module
+    docstring).  ``rows``: RULE_DTYPE entries of one candidate list in
+    ascending gid order; returns the compressed list, ascending first gid."""
+    if len(rows) < min_run:
+        return rows
+    out = rows
+    for dim in (1, 0):                     # destination-port runs first, then source-port runs
+        out = _compress_dim(out, dim, min_run)
+    return out
+
+
+def _compress_dim(rows, dim, min_run):
+    n = len(rows)
+    pl = rows['port_lo'].astype(np.int64)
+    ps = rows['port_span'].astype(np.int64)
+    shift = 16 if dim else 0
+    port = (pl >> shift) & 0xFFFF
+    single = ((ps >> shift) & 0xFFFF) == 0
+    other_lo = (pl >> (16 - shift)) & 0xFFFF
+    other_span = (ps >> (16 - shift)) & 0xFFFF
+    cand = single & (rows['step'] == 0)
+    if cand.sum() < min_run:
+        return rows
+    gid = rows['gid'].astype(np.int64)
+    # class = everything but the varying port; within a class, gid order
+    o = np.lexsort((gid, other_span, other_lo, rows['dst_span'], rows['dst_lo'], rows['src_span'], rows['src_lo'],
+                    ~cand))
+    o = o[cand[o]]
+    k = len(o)
+    same = np.zeros(k, bool)
+    if k > 1:
+        a, b = o[:-1], o[1:]
+        same[1:] = ((rows['src_lo'][a] == rows['src_lo'][b]) & (rows['src_span'][a] == rows['src_span'][b])
+                    & (rows['dst_lo'][a] == rows['dst_lo'][b]) & (rows['dst_span'][a] == rows['dst_span'][b])
+                    & (other_lo[a] == other_lo[b]) & (other_span[a] == other_span[b]))
+    d = np.zeros(k, np.int64)
+    d[1:] = gid[o[1:]] - gid[o[:-1]]
+    link = np.zeros(k, bool)
+    link[1:] = same[1:] & (port[o[1:]] == port[o[:-1]] + 1) & (d[1:] > 0)
+    prev = np.zeros(k, bool)
+    prev[1:] = link[:-1]
+    brk = ~link | (prev & (d != np.roll(d, 1)))
+    run = np.cumsum(brk) - 1
+    n_runs = int(run[-1]) + 1 if k else 0
+    length = np.bincount(run, minlength=n_runs)
+    start = np.flatnonzero(brk)
+    long_run = length >= min_run
+    if not long_run.any():
+        return rows
+    keep = np.ones(n, bool)
+    members = o[long_run[run]]
+    keep[members] = False
+    heads = o[start[long_run]]
+    new = rows[heads].copy()
+    span = (length[long_run] - 1).astype(np.int64)
+    stride = d[start[long_run] + 1]
+    if dim:
+        new['port_span'] = (rows['port_span'][heads].astype(np.int64) & 0xFFFF) | (span << 16)
+        new['step'] = stride.astype(np.uint32)
+    else:
+        new['port_span'] = (rows['port_span'][heads].astype(np.int64) & 0xFFFF0000) | span
+        new['step'] = (stride | STEP_SPORT).astype(np.uint32)
+    assert (stride > 0).all() and (stride < STEP_SPORT).all()
+    out = np.concatenate([rows[keep], new])
+    return out[np.argsort(out['gid'], kind='stable')]
+
+
+def entry_gid(e, sport, dport):
+    """gid an entry assigns to a connection it matches (host model of the device)."""
+    st = int(e['step'])
+    if st == 0:
+        return int(e['gid'])
+    if st & STEP_SPORT:
+        return int(e['gid']) + (sport - (int(e['port_lo']) & 0xFFFF)) * (st & ~STEP_SPORT)
+    return int(e['gid']) + (dport - (int(e['port_lo']) >> 16)) * st
+
+
 class CompiledRules(object):
-    def __init__(self, db):
+    def __init__(self, db, run_min=RUN_MIN):
         self.db = db
+        self.run_min = run_min           # 0: no run compression (every expanded rule its own entry)
         self.groups = []       # [(host, acl)] in gid order
         self.base = {}
         gid = 0
@@ -109,6 +194,8 @@ class CompiledRules(object):
         entry = self.db.accesslists[host][acl]
         idxs = candidate_indices(entry['protocols'], proto)
         rows = self._lower(entry['rules'], idxs, proto, self.base[(host, acl)])
+        if self.run_min:
+            rows = compress_runs(rows, self.run_min)
         if len(self._lists) >= MAX_LISTS:
             raise OverflowError('more than %d (host, acl, protocol) candidate lists' % MAX_LISTS)
         lid = len(self._lists)
@@ -120,9 +207,13 @@ class CompiledRules(object):
 
     @staticmethod
     def _lower(rules, idxs, proto, base):
+        lower_cols = getattr(rules, 'lower', None)
+        if lower_cols is not None:          # columnar rule store (rulecols.RuleColumns)
+            return lower_cols(idxs, proto, base)
         rows = []
         seen = set()
         for i in idxs:
+            i = int(i)
             rule = rules[i]
             if i in seen:          # duplicate index in the list: same rule, same answer
                 continue
@@ -143,33 +234,33 @@ class CompiledRules(object):
                 for dlo, dhi in (dps or [(0, 65535)]):
                     rows.append((s[0], s[1], d[0], d[1], slo | (dlo << 16), (shi - slo) | ((dhi - dlo) << 16),
                                  base + i, 0))
-        return rows
+        out = np.zeros(len(rows), dtype=RULE_DTYPE)
+        if rows:
+            arr = np.array(rows, dtype=np.uint64)
+            for j, name in enumerate(RULE_DTYPE.names):
+                out[name] = arr[:, j]
+        return out
 
     def packed(self):
         """(entries RULE_DTYPE array, offsets uint32 array of n_lists+1)."""
         if self._packed is None:
-            total = sum(len(r) for r in self._lists)
-            ent = np.zeros(total, dtype=RULE_DTYPE)
+            ent = np.concatenate(self._lists) if self._lists else np.zeros(0, RULE_DTYPE)
             off = np.zeros(len(self._lists) + 1, dtype=np.uint32)
-            k = 0
-            for li, rows in enumerate(self._lists):
-                if rows:
-                    arr = np.array(rows, dtype=np.uint64)
-                    for j, name in enumerate(RULE_DTYPE.names):
-                        ent[name][k:k + len(rows)] = arr[:, j]
-                k += len(rows)
-                off[li + 1] = k
+            off[1:] = np.cumsum([len(r) for r in self._lists])
             self._packed = (ent, off)
         return self._packed
 
     def n_lists(self):
         return len(self._lists)
 
-    def index(self, prefix=0):
-        """Perfect-hash tuple-space index of the current lists (cached until a list is added)."""
+    def index(self, prefix=0, chunk=None):
+        """Perfect-hash tuple-space index of the current lists (cached until a list
+        is added); ``chunk``: entries per chained record (default PHT_CHUNK)."""
         ent, off = self.packed()
-        if getattr(self, '_index', None) is None or self._index[0] is not self._packed or self._index[1] != prefix:
-            self._index = (self._packed, prefix, build_index(ent, off, prefix=prefix))
+        chunk = chunk or PHT_CHUNK
+        if getattr(self, '_index', None) is None or self._index[0] is not self._packed or \
+                self._index[1] != (prefix, chunk):
+            self._index = (self._packed, (prefix, chunk), build_index(ent, off, prefix=prefix, chunk=chunk))
         return self._index[2]
 
     def ensure_lists(self, protos=('tcp', 'udp')):
@@ -207,12 +298,20 @@ class CompiledRules(object):
 # a table, groups past the limit, lists of >= 65535 entries) is residual,
 # scanned linearly.  First match = min gid, so the answer is the linear scan's.
 #
+# A list longer than PHT_CHUNK entries (slot values are 16-bit list-local
+# indices) is indexed as a chain of records, one per chunk of PHT_CHUNK
+# entries: a lane probes chunk k+1 only while its best candidate exceeds the
+# smallest gid of chunk k+1 (entries are in ascending first-gid order).
+#
 # Everything lives in ONE uint32 image (include/ruleset_hip.h, rsa_load_index):
 #   [0] 0xFFFFFFFF (the empty slot)  [1] PHT_MAGIC  [2] n_lists  [3] list_off
+#   [4] n_records (>= n_lists: records n_lists.. are chained chunks)  [5..7] 0
 #   list records (PHT_LIST_WORDS each), group records, mask records, bitmaps
 #   (uint64, lo word first), CHD displacements (uint16) and slot words.
-PHT_MAGIC = 0x33415352              # 'RSA3'
-PHT_LIST_WORDS, PHT_GROUP_WORDS, PHT_MASK_WORDS = 16, 20, 8
+PHT_MAGIC = 0x34415352              # 'RSA4'
+PHT_LIST_WORDS, PHT_GROUP_WORDS, PHT_MASK_WORDS = 20, 20, 8
+PHT_HEADER_WORDS = 8
+PHT_CHUNK = 0xFFFE                  # entries per chained record (local indices 0..0xFFFD)
 PHT_MAX_GROUPS = 64
 PHT_ATTEMPTS = 4                    # verification failures before a line is deferred
 # the four port classes of a group, probe order: key ports & mask
@@ -327,8 +426,8 @@ class _Image(object):
     """Append-only uint32 image; chunks stay mutable until build()."""
 
     def __init__(self):
-        self.chunks = [np.array([PHT_EMPTY, PHT_MAGIC, 0, 0], dtype=np.uint32)]
-        self.n = 4
+        self.chunks = [np.array([PHT_EMPTY, PHT_MAGIC, 0, 0, 0, 0, 0, 0], dtype=np.uint32)]
+        self.n = PHT_HEADER_WORDS
 
     def alloc(self, arr, align=1):
         pad = (-self.n) % align
@@ -366,7 +465,9 @@ def _list_shapes(e, pre):
         pl, ps = int(x['port_lo']), int(x['port_span'])
         spm = _port_mask(pl & 0xFFFF, ps & 0xFFFF)
         dpm = _port_mask(pl >> 16, ps >> 16)
-        if sm is None or dm is None or spm is None or dpm is None:
+        if sm is None or dm is None or spm is None or dpm is None or x['step'] != 0:
+            # stepped run entries stay residual: their gid depends on the port, so
+            # the smallest entry index of a key need not be the smallest gid
             resid.append(k)
             continue
         pm = spm | (dpm << 16)
@@ -378,136 +479,166 @@ def _list_shapes(e, pre):
     return shapes, members, resid
 
 
-def build_index(ent, off, prefix=0, min_entries=96, max_groups=PHT_MAX_GROUPS):
+def _index_record(img, rec, e, pre, min_entries, max_groups):
+    """Fill one list record over entries e (list-local indices; [0, pre) are the
+    linear prefix).  Returns the local indices left to the residual scan."""
+    ne = len(e)
+    resid_idx = []
+    groups = []
+    if ne >= min_entries and ne <= PHT_CHUNK:
+        shapes, members, resid_idx = _list_shapes(e, pre)
+        by_sd = {}
+        for (sm, dm, pm), keys in shapes.items():
+            by_sd.setdefault((sm, dm), {})[pm] = keys
+        ranked = sorted(by_sd.items(), key=lambda kv: (min(min(k.values()) for k in kv[1].values()), kv[0]))
+        for (sm, dm), tabs in ranked[max_groups:]:
+            for pm in tabs:
+                resid_idx.extend(members[(sm, dm, pm)])
+        groups = ranked[:max_groups]
+    else:
+        resid_idx = list(range(pre, ne))
+    if groups:
+        goff, grec = img.alloc(np.zeros(PHT_GROUP_WORDS * len(groups), dtype=np.uint32), align=4)
+        src_sets, dst_sets = [], []
+        src_any = dst_any = 0
+        for j, ((sm, dm), tabs) in enumerate(groups):
+            g = grec[PHT_GROUP_WORDS * j: PHT_GROUP_WORDS * (j + 1)]
+            g[0], g[1] = sm, dm
+            mins, real = [], 0
+            ss, ds = set(), set()
+            for c, pm in enumerate(PORT_CLASSES):
+                keys = tabs.get(pm)
+                if not keys:
+                    g[4 + 4 * c: 8 + 4 * c] = (0, 0, 1, 0)    # image word 0: always empty
+                    continue
+                ks = np.array(list(keys.keys()), dtype=np.uint64).astype(np.uint32).reshape(-1, 3)
+                idx = np.array(list(keys.values()), dtype=np.int64)
+                ss.update(ks[:, 0].tolist())
+                ds.update(ks[:, 1].tolist())
+                H = pht_hash(ks[:, 0], ks[:, 1], ks[:, 2])
+                # a full 32-bit hash collision between two keys of one table: keep the
+                # smaller index in the table, the other goes residual (still exact)
+                o = np.lexsort((idx, H))
+                H, idx = H[o], idx[o]
+                dup = np.zeros(len(H), dtype=bool)
+                dup[1:] = H[1:] == H[:-1]
+                resid_idx.extend(idx[dup].tolist())
+                H, idx = H[~dup], idx[~dup]
+                g[4 + 4 * c: 8 + 4 * c] = img.table(H, idx)
+                mins.append(int(idx.min()))
+                real += 1
+            g[2] = min(mins)
+            g[3] = real
+            src_sets.append(ss)
+            dst_sets.append(ds)
+            if sm == 0:
+                src_any |= 1 << j
+            if dm == 0:
+                dst_any |= 1 << j
+        # pruning tables: per non-zero mask of each side, prefix -> group bitmap
+        tables = []
+        for side, sets in ((0, src_sets), (1, dst_sets)):
+            by_mask = {}
+            for j, ((sm, dm), _tabs) in enumerate(groups):
+                m = dm if side else sm
+                if m == 0:
+                    continue
+                bm = by_mask.setdefault(m, {})
+                for k in sets[j]:
+                    bm[k] = bm.get(k, 0) | (1 << j)
+            for m in sorted(by_mask):
+                keys = np.array(sorted(by_mask[m]), dtype=np.uint64).astype(np.uint32)
+                H = field_hash(keys, side)
+                merged = {}
+                for h, k in zip(H.tolist(), keys.tolist()):   # full-hash collision: OR (a superset is safe)
+                    merged[h] = merged.get(h, 0) | by_mask[m][k]
+                tables.append((m, side, merged))
+        distinct = sorted({b for _m, _s, mg in tables for b in mg.values()})
+        bm_index = {b: i for i, b in enumerate(distinct)}
+        if len(distinct) > PHT_MAX_IDX:
+            raise OverflowError('too many distinct group bitmaps in one list')
+        bm_words = np.zeros(2 * max(len(distinct), 1), dtype=np.uint32)
+        for i, b in enumerate(distinct):
+            bm_words[2 * i] = b & M32
+            bm_words[2 * i + 1] = b >> 32
+        bm_off, _ = img.alloc(bm_words, align=2)
+        moff, mrec = img.alloc(np.zeros(PHT_MASK_WORDS * max(len(tables), 1), dtype=np.uint32), align=4)
+        for q, (m, side, merged) in enumerate(tables):
+            H = np.array(list(merged.keys()), dtype=np.uint32)
+            vals = np.array([bm_index[b] for b in merged.values()], dtype=np.uint32)
+            r = mrec[PHT_MASK_WORDS * q: PHT_MASK_WORDS * (q + 1)]
+            r[0], r[1] = m, side
+            r[4:8] = img.table(H, vals)
+        rec[0:4] = (goff, len(groups), moff, len(tables))
+        rec[7] = bm_off
+        rec[8], rec[9] = src_any & M32, src_any >> 32
+        rec[10], rec[11] = dst_any & M32, dst_any >> 32
+        rec[14] = len(distinct)
+    return sorted(set(resid_idx))
+
+
+def build_index(ent, off, prefix=0, min_entries=96, max_groups=PHT_MAX_GROUPS, chunk=PHT_CHUNK):
     """Pruned perfect-hash tuple-space index over packed lists.
 
     Returns (image uint32[], resid RULE_DTYPE[]) — the rsa_load_index
-    arguments.  A list shorter than ``min_entries`` (or of >= 65535 entries)
-    gets no groups: everything after its prefix is residual."""
+    arguments.  A list shorter than ``min_entries`` gets no groups: everything
+    after its prefix is residual.  A list longer than ``chunk`` entries becomes
+    a chain of records (records n_lists.. of the image)."""
     n_lists = len(off) - 1
+    spans = []                                     # per list: [(beg, end) local chunk ranges]
+    for L in range(n_lists):
+        ne = int(off[L + 1] - off[L])
+        spans.append([(a, min(a + chunk, ne)) for a in range(0, max(ne, 1), chunk)] if ne > chunk else [(0, ne)])
+    n_records = n_lists + sum(len(sp) - 1 for sp in spans)
     img = _Image()
-    list_off, lrec = img.alloc(np.zeros(PHT_LIST_WORDS * n_lists, dtype=np.uint32), align=4)
+    list_off, lrec = img.alloc(np.zeros(PHT_LIST_WORDS * n_records, dtype=np.uint32), align=4)
     img.chunks[0][2] = n_lists
     img.chunks[0][3] = list_off
+    img.chunks[0][4] = n_records
     resid_parts, n_resid = [], 0
+    next_virtual = n_lists
     for L in range(n_lists):
-        e = ent[off[L]:off[L + 1]]
-        ne = len(e)
+        e_all = ent[off[L]:off[L + 1]]
+        ne = len(e_all)
         pre = min(prefix, ne)
-        rec = lrec[PHT_LIST_WORDS * L: PHT_LIST_WORDS * (L + 1)]
-        rec[6] = pre
-        rec[12] = int(off[L])
-        rec[13] = ne
-        resid_idx = []
-        groups = []
-        if ne >= min_entries and ne <= PHT_MAX_IDX:
-            shapes, members, resid_idx = _list_shapes(e, pre)
-            by_sd = {}
-            for (sm, dm, pm), keys in shapes.items():
-                by_sd.setdefault((sm, dm), {})[pm] = keys
-            ranked = sorted(by_sd.items(), key=lambda kv: (min(min(k.values()) for k in kv[1].values()), kv[0]))
-            for (sm, dm), tabs in ranked[max_groups:]:
-                for pm in tabs:
-                    resid_idx.extend(members[(sm, dm, pm)])
-            groups = ranked[:max_groups]
-        else:
-            resid_idx = list(range(pre, ne))
-        if groups:
-            goff, grec = img.alloc(np.zeros(PHT_GROUP_WORDS * len(groups), dtype=np.uint32), align=4)
-            src_sets, dst_sets = [], []
-            src_any = dst_any = 0
-            for j, ((sm, dm), tabs) in enumerate(groups):
-                g = grec[PHT_GROUP_WORDS * j: PHT_GROUP_WORDS * (j + 1)]
-                g[0], g[1] = sm, dm
-                mins, real = [], 0
-                ss, ds = set(), set()
-                for c, pm in enumerate(PORT_CLASSES):
-                    keys = tabs.get(pm)
-                    if not keys:
-                        g[4 + 4 * c: 8 + 4 * c] = (0, 0, 1, 0)    # image word 0: always empty
-                        continue
-                    ks = np.array(list(keys.keys()), dtype=np.uint64).astype(np.uint32).reshape(-1, 3)
-                    idx = np.array(list(keys.values()), dtype=np.int64)
-                    ss.update(ks[:, 0].tolist())
-                    ds.update(ks[:, 1].tolist())
-                    H = pht_hash(ks[:, 0], ks[:, 1], ks[:, 2])
-                    # a full 32-bit hash collision between two keys of one table: keep the
-                    # smaller index in the table, the other goes residual (still exact)
-                    o = np.lexsort((idx, H))
-                    H, idx = H[o], idx[o]
-                    dup = np.zeros(len(H), dtype=bool)
-                    dup[1:] = H[1:] == H[:-1]
-                    resid_idx.extend(idx[dup].tolist())
-                    H, idx = H[~dup], idx[~dup]
-                    g[4 + 4 * c: 8 + 4 * c] = img.table(H, idx)
-                    mins.append(int(idx.min()))
-                    real += 1
-                g[2] = min(mins)
-                g[3] = real
-                src_sets.append(ss)
-                dst_sets.append(ds)
-                if sm == 0:
-                    src_any |= 1 << j
-                if dm == 0:
-                    dst_any |= 1 << j
-            # pruning tables: per non-zero mask of each side, prefix -> group bitmap
-            tables = []
-            for side, sets in ((0, src_sets), (1, dst_sets)):
-                by_mask = {}
-                for j, ((sm, dm), _tabs) in enumerate(groups):
-                    m = dm if side else sm
-                    if m == 0:
-                        continue
-                    bm = by_mask.setdefault(m, {})
-                    for k in sets[j]:
-                        bm[k] = bm.get(k, 0) | (1 << j)
-                for m in sorted(by_mask):
-                    keys = np.array(sorted(by_mask[m]), dtype=np.uint64).astype(np.uint32)
-                    H = field_hash(keys, side)
-                    merged = {}
-                    for h, k in zip(H.tolist(), keys.tolist()):   # full-hash collision: OR (a superset is safe)
-                        merged[h] = merged.get(h, 0) | by_mask[m][k]
-                    tables.append((m, side, merged))
-            distinct = sorted({b for _m, _s, mg in tables for b in mg.values()})
-            bm_index = {b: i for i, b in enumerate(distinct)}
-            if len(distinct) > PHT_MAX_IDX:
-                raise OverflowError('too many distinct group bitmaps in one list')
-            bm_words = np.zeros(2 * max(len(distinct), 1), dtype=np.uint32)
-            for i, b in enumerate(distinct):
-                bm_words[2 * i] = b & M32
-                bm_words[2 * i + 1] = b >> 32
-            bm_off, _ = img.alloc(bm_words, align=2)
-            moff, mrec = img.alloc(np.zeros(PHT_MASK_WORDS * max(len(tables), 1), dtype=np.uint32), align=4)
-            for q, (m, side, merged) in enumerate(tables):
-                H = np.array(list(merged.keys()), dtype=np.uint32)
-                vals = np.array([bm_index[b] for b in merged.values()], dtype=np.uint32)
-                r = mrec[PHT_MASK_WORDS * q: PHT_MASK_WORDS * (q + 1)]
-                r[0], r[1] = m, side
-                r[4:8] = img.table(H, vals)
-            rec[0:4] = (goff, len(groups), moff, len(tables))
-            rec[7] = bm_off
-            rec[8], rec[9] = src_any & M32, src_any >> 32
-            rec[10], rec[11] = dst_any & M32, dst_any >> 32
-            rec[14] = len(distinct)
-        resid_idx = sorted(set(resid_idx))
-        rec[4] = n_resid
-        resid_parts.append(e[resid_idx])
-        n_resid += len(resid_idx)
-        rec[5] = n_resid
+        rec_ids = [L] + list(range(next_virtual, next_virtual + len(spans[L]) - 1))
+        next_virtual += len(spans[L]) - 1
+        after = int(e_all['gid'][pre:].min()) if pre < ne else PHT_EMPTY
+        for q, (a, b) in enumerate(spans[L]):
+            r = rec_ids[q]
+            rec = lrec[PHT_LIST_WORDS * r: PHT_LIST_WORDS * (r + 1)]
+            e = e_all[a:b]
+            p = max(0, min(pre - a, b - a))
+            rec[6] = p if q == 0 else 0
+            rec[12] = int(off[L]) + a
+            rec[13] = b - a
+            rec[15] = after if q == 0 else (int(e['gid'].min()) if len(e) else PHT_EMPTY)
+            if q + 1 < len(spans[L]):
+                rec[16] = rec_ids[q + 1]
+                rec[17] = int(e_all['gid'][spans[L][q + 1][0]:].min())
+            else:
+                rec[16] = PHT_EMPTY
+                rec[17] = PHT_EMPTY
+            # linear prefix entries of later chunks do not exist: the prefix lies in chunk 0
+            resid_idx = _index_record(img, rec, e, p if q == 0 else 0, min_entries, max_groups)
+            rec[4] = n_resid
+            resid_parts.append(e[resid_idx])
+            n_resid += len(resid_idx)
+            rec[5] = n_resid
     image = img.build()
     resid = np.concatenate(resid_parts) if resid_parts else np.zeros(0, RULE_DTYPE)
     return image, resid
 
 
+def _records(image):
+    lo, nrec = int(image[3]), int(image[4])
+    return [[int(v) for v in image[lo + PHT_LIST_WORDS * r: lo + PHT_LIST_WORDS * (r + 1)]] for r in range(nrec)]
+
+
 def index_stats(index):
-    """Per list: (prefix, groups, masks, residual entries) — tests and tuning."""
+    """Per list record: (prefix, groups, masks, residual entries) — tests and tuning."""
     image, _resid = index
-    n_lists, lo = int(image[2]), int(image[3])
-    out = []
-    for L in range(n_lists):
-        r = image[lo + PHT_LIST_WORDS * L: lo + PHT_LIST_WORDS * (L + 1)]
-        out.append((int(r[6]), int(r[1]), int(r[3]), int(r[5] - r[4])))
-    return out
+    return [(r[6], r[1], r[3], r[5] - r[4]) for r in _records(image)]
 
 
 def _probe(image, H, t):
@@ -519,68 +650,83 @@ def _probe(image, H, t):
     return (w & 0xFFFF) if (w >> 16) == (H & 0xFFFF) else PHT_NONE
 
 
+def _match(x, src, dst, ports):
+    pl, ps = int(x['port_lo']), int(x['port_span'])
+    return ((src - int(x['src_lo'])) & M32) <= int(x['src_span']) and \
+        ((dst - int(x['dst_lo'])) & M32) <= int(x['dst_span']) and \
+        ((ports & 0xFFFF) - (pl & 0xFFFF)) & 0xFFFF <= (ps & 0xFFFF) and \
+        ((ports >> 16) - (pl >> 16)) & 0xFFFF <= (ps >> 16)
+
+
+def _scan(entries, src, dst, ports, best):
+    """Linear scan with the device's early exit: stop once best <= an entry's first gid."""
+    for x in entries:
+        if best is not None and int(x['gid']) >= best:
+            break
+        if _match(x, src, dst, ports):
+            g = entry_gid(x, ports & 0xFFFF, ports >> 16)
+            best = g if best is None else min(best, g)
+    return best
+
+
 def pht_lookup(index, ent, off, L, src, dst, ports):
     """Host model of the GPU classifier for one tuple (tests): the first-match
-    list-local index, -1, or 'defer'.  Follows the device order exactly: prefix
-    scan, pruning bitmaps, group probes in min-index order with verification
-    and retry above a failed candidate, residual scan."""
+    gid, -1, or 'defer'.  Follows the device order exactly: prefix scan, then
+    per chained record the pruning bitmaps, group probes in min-index order with
+    verification and retry above a failed candidate, and the residual scan."""
     image, resid = index
-    lo = int(image[3])
-    r = [int(v) for v in image[lo + PHT_LIST_WORDS * L: lo + PHT_LIST_WORDS * (L + 1)]]
-    e = ent[off[L]:off[L + 1]]
-
-    def match(x):
-        pl, ps = int(x['port_lo']), int(x['port_span'])
-        return ((src - int(x['src_lo'])) & M32) <= int(x['src_span']) and \
-            ((dst - int(x['dst_lo'])) & M32) <= int(x['dst_span']) and \
-            ((ports & 0xFFFF) - (pl & 0xFFFF)) & 0xFFFF <= (ps & 0xFFFF) and \
-            ((ports >> 16) - (pl >> 16)) & 0xFFFF <= (ps >> 16)
-    for k in range(r[6]):
-        if match(e[k]):
-            return k
-    best = None
-    goff, ng, moff, nm = r[0:4]
-    if ng:
-        S = r[8] | (r[9] << 32)
-        D = r[10] | (r[11] << 32)
-        for q in range(nm):
-            mr = [int(v) for v in image[moff + PHT_MASK_WORDS * q: moff + PHT_MASK_WORDS * (q + 1)]]
-            side = mr[1]
-            key = (dst if side else src) & mr[0]
-            v = _probe(image, field_hash(key, side), mr[4:8])
-            if v != PHT_NONE:
-                bits = int(image[r[7] + 2 * v]) | (int(image[r[7] + 2 * v + 1]) << 32)
-                if side:
-                    D |= bits
-                else:
-                    S |= bits
-        cand0 = S & D
-        floor = 0
-        for _attempt in range(PHT_ATTEMPTS):
-            bi = PHT_NONE
-            for j in range(ng):
-                if not (cand0 >> j) & 1:
-                    continue
-                g = [int(v) for v in image[goff + PHT_GROUP_WORDS * j: goff + PHT_GROUP_WORDS * (j + 1)]]
-                if g[2] >= bi:
+    recs = _records(image)
+    r = recs[L]
+    best = _scan(ent[off[L]:off[L] + r[6]], src, dst, ports, None)
+    if best is not None and r[15] != PHT_EMPTY and best <= r[15]:
+        return best
+    if r[15] == PHT_EMPTY:
+        return -1 if best is None else best
+    while True:
+        e = ent[r[12]:r[12] + r[13]]
+        goff, ng, moff, nm = r[0:4]
+        if ng:
+            S = r[8] | (r[9] << 32)
+            D = r[10] | (r[11] << 32)
+            for q in range(nm):
+                mr = [int(v) for v in image[moff + PHT_MASK_WORDS * q: moff + PHT_MASK_WORDS * (q + 1)]]
+                side = mr[1]
+                key = (dst if side else src) & mr[0]
+                v = _probe(image, field_hash(key, side), mr[4:8])
+                if v != PHT_NONE:
+                    bits = int(image[r[7] + 2 * v]) | (int(image[r[7] + 2 * v + 1]) << 32)
+                    if side:
+                        D |= bits
+                    else:
+                        S |= bits
+            cand0 = S & D
+            floor = 0
+            found = None
+            for _attempt in range(PHT_ATTEMPTS):
+                bi = PHT_NONE
+                for j in range(ng):
+                    if not (cand0 >> j) & 1:
+                        continue
+                    g = [int(v) for v in image[goff + PHT_GROUP_WORDS * j: goff + PHT_GROUP_WORDS * (j + 1)]]
+                    if g[2] >= bi:
+                        break
+                    for c, pm in enumerate(PORT_CLASSES):
+                        H = int(pht_hash(src & g[0], dst & g[1], ports & pm))
+                        v = _probe(image, H, g[4 + 4 * c: 8 + 4 * c])
+                        if v >= floor:
+                            bi = min(bi, v)
+                if bi == PHT_NONE:
                     break
-                for c, pm in enumerate(PORT_CLASSES):
-                    H = int(pht_hash(src & g[0], dst & g[1], ports & pm))
-                    v = _probe(image, H, g[4 + 4 * c: 8 + 4 * c])
-                    if v >= floor:
-                        bi = min(bi, v)
-            if bi == PHT_NONE:
-                break
-            if match(e[bi]):
-                best = bi
-                break
-            floor = bi + 1
-        else:
-            return 'defer'
-    gid_best = int(e[best]['gid']) if best is not None else None
-    for x in resid[r[4]:r[5]]:
-        if gid_best is not None and int(x['gid']) >= gid_best:
+                if _match(e[bi], src, dst, ports):
+                    found = entry_gid(e[bi], ports & 0xFFFF, ports >> 16)
+                    break
+                floor = bi + 1
+            else:
+                return 'defer'
+            if found is not None:
+                best = found if best is None else min(best, found)
+        best = _scan(resid[r[4]:r[5]], src, dst, ports, best)
+        if r[16] == PHT_EMPTY or (best is not None and best <= r[17]):
             break
-        if match(x):
-            return int(np.searchsorted(e['gid'], x['gid']))
+        r = recs[r[16]]
     return -1 if best is None else best

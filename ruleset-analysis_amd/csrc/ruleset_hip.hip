@@ -40,6 +40,7 @@
 #include <cstdarg>
 #include <cstddef>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -72,7 +73,7 @@ static_assert(sizeof(rsa_tuple) == 16, "tuple layout");
 static_assert(sizeof(rsa_rule_entry) == 32, "rule layout");
 static_assert(sizeof(rsa_pht_group) == 80, "group layout");
 static_assert(sizeof(rsa_pht_mask) == 32, "mask layout");
-static_assert(sizeof(rsa_pht_list) == 64, "list record layout");
+static_assert(sizeof(rsa_pht_list) == 80, "list record layout");
 static_assert(sizeof(rsa_conn_record) == 40, "record layout");
 
 // Rule data is read through the constant address space so that wave-uniform
@@ -200,25 +201,37 @@ __device__ __forceinline__ bool entry_match(v4u a, v4u b, uint32_t src, uint32_t
   return ((src - a.x) <= a.y) & ((dst - a.z) <= a.w) & (as_u32(m) == as_u32(d));
 }
 
+// gid a matching entry assigns to the connection: the entry's gid, or for a
+// run entry (step != 0) the rule of the run holding the connection's port,
+// gid + (p - lo) * stride (include/ruleset_hip.h rsa_rule_entry).
+__device__ __forceinline__ uint32_t entry_gid(v4u b, uint32_t ports) {
+  const uint32_t st = b.w;
+  const bool on_sport = st & RSA_STEP_SPORT;
+  const uint32_t p = on_sport ? (ports & 0xFFFFu) : (ports >> 16);
+  const uint32_t lo = on_sport ? (b.x & 0xFFFFu) : (b.x >> 16);
+  return b.z + (p - lo) * (st & ~RSA_STEP_SPORT);
+}
+
 // Linear first-match scan of entries [beg, end) for the `mine` lanes.  Entries
-// are gid-ascending, so within a block of four the first match is selected in
-// reverse order, and the wave stops once no searching lane can improve.
+// are in ascending first-gid order and an entry never yields a gid below its
+// own, so the wave stops once no searching lane's best exceeds the first gid
+// of the entries still ahead.
 __device__ __forceinline__ uint32_t scan_list(const const_v4u* E, uint32_t beg, uint32_t end, bool mine, uint32_t best,
                                               uint32_t src, uint32_t dst, uint32_t ports) {
   uint32_t e = beg;
   const const_v4u* p = E + 2 * (size_t)beg;
   for (; e + 4 <= end; e += 4, p += 8) {
     const v4u a0 = p[0], b0 = p[1], a1 = p[2], b1 = p[3], a2 = p[4], b2 = p[5], a3 = p[6], b3 = p[7];
-    uint32_t c = entry_match(a3, b3, src, dst, ports) ? b3.z : kNoGid;
-    c = entry_match(a2, b2, src, dst, ports) ? b2.z : c;
-    c = entry_match(a1, b1, src, dst, ports) ? b1.z : c;
-    c = entry_match(a0, b0, src, dst, ports) ? b0.z : c;
-    if (mine) best = min(best, c);
+    const uint32_t c0 = entry_match(a0, b0, src, dst, ports) ? entry_gid(b0, ports) : kNoGid;
+    const uint32_t c1 = entry_match(a1, b1, src, dst, ports) ? entry_gid(b1, ports) : kNoGid;
+    const uint32_t c2 = entry_match(a2, b2, src, dst, ports) ? entry_gid(b2, ports) : kNoGid;
+    const uint32_t c3 = entry_match(a3, b3, src, dst, ports) ? entry_gid(b3, ports) : kNoGid;
+    if (mine) best = min(best, min(min(c0, c1), min(c2, c3)));
     if (__ballot(mine && best > b3.z) == 0) return best;
   }
   for (; e < end; ++e, p += 2) {
     const v4u a = p[0], b = p[1];
-    if (mine && entry_match(a, b, src, dst, ports)) best = min(best, b.z);
+    if (mine && entry_match(a, b, src, dst, ports)) best = min(best, entry_gid(b, ports));
   }
   return best;
 }
@@ -261,7 +274,7 @@ __device__ __forceinline__ uint32_t pht_probe(P32 img, uint32_t H, v4u b) {
 }
 
 constexpr int kAttempts = 4;   // compile.py PHT_ATTEMPTS
-constexpr uint32_t kListWords = 16, kGroupWords = 20, kMaskWords = 8;
+constexpr uint32_t kListWords = 20, kGroupWords = 20, kMaskWords = 8;
 
 // Index lookup for ONE lane (divergent code: the lanes of a wave may be on
 // different lists; compile.py pht_lookup is the host model).  h0..h2: the
@@ -324,7 +337,7 @@ __device__ __forceinline__ uint32_t index_lookup(const Rules& R, P32 img, v4u h0
     if (bi == kNoCand) return kNoGid;
     if (R.force_defer) return kDefer;
     const v4u ea = R.eg[2 * (size_t)(ebeg + bi)], eb = R.eg[2 * (size_t)(ebeg + bi) + 1];
-    if (entry_match(ea, eb, src, dst, ports)) return eb.z;
+    if (entry_match(ea, eb, src, dst, ports)) return entry_gid(eb, ports);
     floor = bi + 1;   // a tag collision: every true candidate lies above bi
   }
   return kDefer;
@@ -355,13 +368,18 @@ __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Ru
     }
     return active ? best : kNoGid;
   }
+  // record words: h0 {group_off, n_groups, mask_off, n_masks}, h1 {resid_beg,
+  // resid_end, prefix, bm_off}, h2 {src_any, dst_any}, h3 {entry_beg,
+  // entry_len, n_bitmaps, after_min}, h4 {next, next_min, -, -}
   v4u h0 = {0u, 0u, 0u, 0u}, h1 = {0u, 0u, 0u, 0u}, h2 = {0u, 0u, 0u, 0u}, h3 = {0u, 0u, 0u, 0u};
+  v4u h4 = {0u, 0u, 0u, 0u};
   if (active) {
     const uint32_t lw = R.list_off + kListWords * list;
     h0 = rd4(img, lw);
     h1 = rd4(img, lw + 4);
     h2 = rd4(img, lw + 8);
     h3 = rd4(img, lw + 12);
+    h4 = rd4(img, lw + 16);
   }
   // 1. prefix scans
   unsigned long long pending = __ballot(active && h1.z != 0);
@@ -375,21 +393,45 @@ __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Ru
     const uint32_t b = scan_list(R.e, beg, beg + pre, mine, kNoGid, t.x, t.y, t.z);
     if (mine) best = b;
   }
-  // 2. the index, per lane
-  const bool open = active && best == kNoGid;
-  if (open && h0.y != 0) best = index_lookup(R, img, h0, h1, h2, h3.x, t.x, t.y, t.z);
-  // 3. residual scans for lanes the prefix did not match and that are not deferred
-  const bool want = open && best != kDefer && h1.x < h1.y;
-  pending = __ballot(want);
-  while (pending) {
-    const int leader = __builtin_ctzll(pending);
-    const uint32_t L = __builtin_amdgcn_readlane(list, leader);
-    const bool mine = want && list == L;
-    pending &= ~__ballot(mine);
-    const uint32_t rb = __builtin_amdgcn_readlane(h1.x, leader), re = __builtin_amdgcn_readlane(h1.y, leader);
-    const uint32_t b = scan_list(R.resid, rb, re, mine, best, t.x, t.y, t.z);
-    if (mine) best = b;
+  // 2. per record of the lane's chain: the index (per lane), then the residual
+  // scan (waterfall over the records present); the next chunk only while the
+  // lane's best exceeds its smallest gid
+  bool go = active && best > h3.w;
+  bool deferred = false;
+  uint32_t rec = list;
+  while (__ballot(go)) {
+    if (go && h0.y != 0) {
+      const uint32_t c = index_lookup(R, img, h0, h1, h2, h3.x, t.x, t.y, t.z);
+      if (c == kDefer) {
+        deferred = true;
+        go = false;
+      } else {
+        best = min(best, c);
+      }
+    }
+    const bool want = go && h1.x < h1.y;
+    pending = __ballot(want);
+    while (pending) {
+      const int leader = __builtin_ctzll(pending);
+      const uint32_t Q = __builtin_amdgcn_readlane(rec, leader);
+      const bool mine = want && rec == Q;
+      pending &= ~__ballot(mine);
+      const uint32_t rb = __builtin_amdgcn_readlane(h1.x, leader), re = __builtin_amdgcn_readlane(h1.y, leader);
+      const uint32_t b = scan_list(R.resid, rb, re, mine, best, t.x, t.y, t.z);
+      if (mine) best = b;
+    }
+    go = go && h4.x != RSA_PHT_NONE && best > h4.y;
+    if (go) {
+      rec = h4.x;
+      const uint32_t lw = R.list_off + kListWords * rec;
+      h0 = rd4(img, lw);
+      h1 = rd4(img, lw + 4);
+      h2 = rd4(img, lw + 8);
+      h3 = rd4(img, lw + 12);
+      h4 = rd4(img, lw + 16);
+    }
   }
+  if (deferred) return kDefer;
   return active ? best : kNoGid;
 }
 
@@ -1502,6 +1544,7 @@ struct rsa_ctx {
   // pass-1 kernel timing (HIP events on the ctx stream)
   hipEvent_t ev[48] = {};             // per pass-1 launch: start, classified, aggregated
   int ev_used = 0;
+  bool debug = false;                 // RSA_DEBUG=1 in the environment: per-launch counts on stderr
 };
 
 namespace {
@@ -1650,6 +1693,7 @@ int cap_select(rsa_ctx* c, unsigned long long* out, uint32_t* h_n_capped) {
   rc = used_count(c, &n_used);  // synchronises
   if (rc) return rc;
   *h_n_capped = ncap;
+  if (c->debug) fprintf(stderr, "[rsa] cap select: %u capped rules, %llu table entries\n", ncap, n_used);
   if (ncap == 0) return RSA_OK;
   if (c->sort_alloc < n_used) {
     hipFree(c->d_keys);
@@ -1778,6 +1822,7 @@ int launch_aggregate(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsig
   unsigned long long nr = 0;
   HIPCHK(c, hipMemcpyAsync(&nr, c->d_nrecs, sizeof nr, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (c->debug) fprintf(stderr, "[rsa] pass-1 launch: %llu lines -> %llu records\n", (unsigned long long)m, nr);
   if (nr == 0) return RSA_OK;
   if (nr > m) return fail(c, RSA_ERR_STATE, "record count %llu exceeds the batch", nr);
   // region-sorted records: appended after the previous launches' while this
@@ -1917,6 +1962,8 @@ int rsa_ctx_create(int device, rsa_ctx** out) {
   if (hipSetDevice(device) != hipSuccess) return RSA_ERR_HIP;
   rsa_ctx* c = new rsa_ctx();
   c->device = device;
+  const char* dbg = getenv("RSA_DEBUG");
+  c->debug = dbg && dbg[0] == '1';
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     c->cu_count = prop.multiProcessorCount;
@@ -2014,6 +2061,12 @@ int rsa_load_rules(rsa_ctx* c, const rsa_rule_entry* h_entries, uint32_t n_entri
     if (h_off[l + 1] < h_off[l]) return fail(c, RSA_ERR_ARG, "list offsets not monotone at %u", l);
     for (uint32_t e = h_off[l]; e < h_off[l + 1]; ++e) {
       if (h_entries[e].gid >= n_rules) return fail(c, RSA_ERR_ARG, "entry %u gid %u >= n_rules", e, h_entries[e].gid);
+      const uint32_t st = h_entries[e].step;
+      if (st) {   // a run: its last rule must exist too
+        const uint32_t span = (st & RSA_STEP_SPORT) ? (h_entries[e].port_span & 0xFFFFu) : (h_entries[e].port_span >> 16);
+        if ((uint64_t)h_entries[e].gid + (uint64_t)span * (st & ~RSA_STEP_SPORT) >= n_rules)
+          return fail(c, RSA_ERR_ARG, "entry %u: run reaches past n_rules", e);
+      }
       if (e > h_off[l] && h_entries[e].gid < h_entries[e - 1].gid)
         return fail(c, RSA_ERR_ARG, "list %u not in ascending gid order at entry %u", l, e);
     }
@@ -2053,49 +2106,67 @@ bool table_ok(const uint32_t* img, uint32_t words, const rsa_pht_table& t, uint3
 int rsa_load_index(rsa_ctx* c, const uint32_t* img, uint32_t words, const rsa_rule_entry* h_resid, uint32_t n_resid) {
   if (!c || !img || (n_resid && !h_resid)) return fail(c, RSA_ERR_ARG, "null argument");
   if (!c->rules_loaded) return fail(c, RSA_ERR_STATE, "load the candidate lists first");
-  if (words < 4 || img[0] != 0xFFFFFFFFu || img[1] != RSA_PHT_MAGIC)
+  if (words < 8 || img[0] != 0xFFFFFFFFu || img[1] != RSA_PHT_MAGIC)
     return fail(c, RSA_ERR_ARG, "not an index image (word 0 must be empty, word 1 RSA_PHT_MAGIC)");
   const uint32_t nl = c->n_lists;
   if (img[2] != nl) return fail(c, RSA_ERR_ARG, "image has %u lists, %u are loaded", img[2], nl);
-  const uint32_t lo = img[3];
+  const uint32_t lo = img[3], nrec = img[4];
   const uint32_t lw = sizeof(rsa_pht_list) / 4, gw = sizeof(rsa_pht_group) / 4, mw = sizeof(rsa_pht_mask) / 4;
-  if (lo % 4 || (uint64_t)lo + (uint64_t)lw * nl > words) return fail(c, RSA_ERR_ARG, "list records outside the image");
-  // validate everything the kernels index with, so no launch can read out of bounds
+  if (nrec < nl || lo % 4 || (uint64_t)lo + (uint64_t)lw * nrec > words)
+    return fail(c, RSA_ERR_ARG, "list records outside the image");
+  // validate everything the kernels index with, so no launch can read out of
+  // bounds and every chain terminates: a list's records cover its entries in
+  // order, continuation records have larger ids than their predecessor
+  std::vector<uint8_t> claimed(nrec, 0);
   for (uint32_t l = 0; l < nl; ++l) {
-    rsa_pht_list h;
-    memcpy(&h, img + lo + (size_t)lw * l, sizeof h);
-    const uint32_t len = c->h_off[l + 1] - c->h_off[l];
-    if (h.entry_beg != c->h_off[l] || h.entry_len != len)
-      return fail(c, RSA_ERR_ARG, "list %u: entry range differs from the loaded lists", l);
-    if (h.resid_beg > h.resid_end || h.resid_end > n_resid)
-      return fail(c, RSA_ERR_ARG, "list %u: residual range out of bounds", l);
-    if (h.prefix > len) return fail(c, RSA_ERR_ARG, "list %u: prefix %u > list length %u", l, h.prefix, len);
-    if (h.n_groups == 0) continue;
-    if (h.n_groups > 64) return fail(c, RSA_ERR_ARG, "list %u: more than 64 groups", l);
-    if (len > 0xFFFEu) return fail(c, RSA_ERR_ARG, "list %u: indexed list too long", l);
-    if (h.group_off % 4 || (uint64_t)h.group_off + (uint64_t)gw * h.n_groups > words || h.mask_off % 4 ||
-        (uint64_t)h.mask_off + (uint64_t)mw * h.n_masks > words || h.bm_off % 2 ||
-        (uint64_t)h.bm_off + 2ull * h.n_bitmaps > words)
-      return fail(c, RSA_ERR_ARG, "list %u: records outside the image", l);
-    for (uint32_t g = 0; g < h.n_groups; ++g) {
-      rsa_pht_group G;
-      memcpy(&G, img + h.group_off + (size_t)gw * g, sizeof G);
-      for (int k = 0; k < 4; ++k)
-        if (!table_ok(img, words, G.table[k], len))
-          return fail(c, RSA_ERR_ARG, "list %u group %u class %d: table outside the image or index out of list", l, g, k);
+    uint32_t r = l, at = c->h_off[l];
+    while (true) {
+      if (claimed[r]) return fail(c, RSA_ERR_ARG, "record %u claimed twice", r);
+      claimed[r] = 1;
+      rsa_pht_list h;
+      memcpy(&h, img + lo + (size_t)lw * r, sizeof h);
+      if (h.entry_beg != at || (uint64_t)h.entry_beg + h.entry_len > c->h_off[l + 1])
+        return fail(c, RSA_ERR_ARG, "list %u record %u: entry range differs from the loaded list", l, r);
+      const uint32_t len = h.entry_len;
+      if (h.resid_beg > h.resid_end || h.resid_end > n_resid)
+        return fail(c, RSA_ERR_ARG, "list %u record %u: residual range out of bounds", l, r);
+      if (h.prefix > len || (r != l && h.prefix != 0))
+        return fail(c, RSA_ERR_ARG, "list %u record %u: bad prefix %u", l, r, h.prefix);
+      for (uint32_t e = h.resid_beg; e < h.resid_end; ++e) {
+        if (h_resid[e].gid >= c->n_rules) return fail(c, RSA_ERR_ARG, "residual entry %u gid out of range", e);
+        if (e > h.resid_beg && h_resid[e].gid < h_resid[e - 1].gid)
+          return fail(c, RSA_ERR_ARG, "list %u: residual not gid-ascending", l);
+      }
+      if (h.n_groups != 0) {
+        if (h.n_groups > 64) return fail(c, RSA_ERR_ARG, "list %u: more than 64 groups", l);
+        if (len > 0xFFFEu) return fail(c, RSA_ERR_ARG, "list %u record %u: indexed chunk too long", l, r);
+        if (h.group_off % 4 || (uint64_t)h.group_off + (uint64_t)gw * h.n_groups > words || h.mask_off % 4 ||
+            (uint64_t)h.mask_off + (uint64_t)mw * h.n_masks > words || h.bm_off % 2 ||
+            (uint64_t)h.bm_off + 2ull * h.n_bitmaps > words)
+          return fail(c, RSA_ERR_ARG, "list %u: records outside the image", l);
+        for (uint32_t g = 0; g < h.n_groups; ++g) {
+          rsa_pht_group G;
+          memcpy(&G, img + h.group_off + (size_t)gw * g, sizeof G);
+          for (int k = 0; k < 4; ++k)
+            if (!table_ok(img, words, G.table[k], len))
+              return fail(c, RSA_ERR_ARG, "list %u group %u class %d: table outside the image or index out of list", l,
+                          g, k);
+        }
+        for (uint32_t m = 0; m < h.n_masks; ++m) {
+          rsa_pht_mask M;
+          memcpy(&M, img + h.mask_off + (size_t)mw * m, sizeof M);
+          if (M.side > 1) return fail(c, RSA_ERR_ARG, "list %u mask %u: side must be 0 or 1", l, m);
+          if (!table_ok(img, words, M.table, h.n_bitmaps))
+            return fail(c, RSA_ERR_ARG, "list %u mask %u: table outside the image or bitmap out of range", l, m);
+        }
+      }
+      at = h.entry_beg + h.entry_len;
+      if (h.next == RSA_PHT_NONE) break;
+      if (h.next <= r || h.next < nl || h.next >= nrec)
+        return fail(c, RSA_ERR_ARG, "list %u record %u: bad continuation record %u", l, r, h.next);
+      r = h.next;
     }
-    for (uint32_t m = 0; m < h.n_masks; ++m) {
-      rsa_pht_mask M;
-      memcpy(&M, img + h.mask_off + (size_t)mw * m, sizeof M);
-      if (M.side > 1) return fail(c, RSA_ERR_ARG, "list %u mask %u: side must be 0 or 1", l, m);
-      if (!table_ok(img, words, M.table, h.n_bitmaps))
-        return fail(c, RSA_ERR_ARG, "list %u mask %u: table outside the image or bitmap out of range", l, m);
-    }
-    for (uint32_t e = h.resid_beg; e < h.resid_end; ++e) {
-      if (h_resid[e].gid >= c->n_rules) return fail(c, RSA_ERR_ARG, "residual entry %u gid out of range", e);
-      if (e > h.resid_beg && h_resid[e].gid < h_resid[e - 1].gid)
-        return fail(c, RSA_ERR_ARG, "list %u: residual not gid-ascending", l);
-    }
+    if (at != c->h_off[l + 1]) return fail(c, RSA_ERR_ARG, "list %u: records do not cover its entries", l);
   }
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));

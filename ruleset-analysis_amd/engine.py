@@ -116,13 +116,14 @@ class Engine(object):
         self.ctx.call('rsa_last_pass1_ms', ctypes.byref(ms))
         return float(ms.value)
 
-    def load_compiled(self, compiled, index=True, prefix=0):
+    def load_compiled(self, compiled, index=True, prefix=0, chunk=None):
         """Upload a CompiledRules' lists (and its perfect-hash tuple-space index,
-        whose first ``prefix`` entries per list are scanned linearly)."""
+        whose first ``prefix`` entries per list are scanned linearly and whose
+        records hold at most ``chunk`` entries each, chained)."""
         ent, off = compiled.packed()
         self.load_rules(ent, off, compiled.n_rules)
         if index:
-            self.load_index(compiled.index(prefix=prefix))
+            self.load_index(compiled.index(prefix=prefix, chunk=chunk))
 
     def set_rule_count(self, n_rules):
         self.ctx.call('rsa_set_rule_count', ctypes.c_uint32(n_rules))

@@ -270,6 +270,7 @@ def render_lines(tr):
     out = []
     P = ('TCP', 'UDP')
     MID = ('302013', '302015')
+    inside = tr.get('inside_ifc', 'inside')
     for i in range(len(tr['form'])):
         f = int(tr['form'][i])
         day, hms = _clock(int(tr['t'][i]))
@@ -294,8 +295,8 @@ def render_lines(tr):
             out.append('%s%%ASA-6-302014: Teardown %s connection %s for %s:%s/%d to inside:%s/%d duration 0:00:01 '
                        'bytes 1024 TCP FINs' % (head, P[pr], cid, ifc, s, sp, d, dp))
         else:  # outbound: initiator (src) is inside, 'for' side is the outside peer
-            out.append('%s%%ASA-6-%s: Built outbound %s connection %s for outside:%s/%d (%s/%d) to inside:%s/%d '
-                       '(%s/%d)' % (head, MID[pr], P[pr], cid, d, dp, d, dp, s, sp, s, sp))
+            out.append('%s%%ASA-6-%s: Built outbound %s connection %s for outside:%s/%d (%s/%d) to %s:%s/%d '
+                       '(%s/%d)' % (head, MID[pr], P[pr], cid, d, dp, d, dp, inside, s, sp, s, sp))
     return out
 
 
@@ -336,14 +337,15 @@ def pack(tr, compiled):
     valid = np.isin(form, [F_BUILT, F_NONHIT, F_NOYEAR, F_OUTBOUND])
     lists = np.zeros(n, dtype=np.int64)
     names = ('tcp', 'udp')
+    acl_of = tr.get('acl_of') or ['%s_access_in' % ifc for ifc in ifcs]
     for p in (0, 1):
         for k, ifc in enumerate(ifcs):
             w = valid & (form != F_OUTBOUND) & (tr['ifc'] == k) & (tr['proto'] == p)
             if w.any():
-                lists[w] = compiled.list_id(host, '%s_access_in' % ifc, names[p])
+                lists[w] = compiled.list_id(host, acl_of[k], names[p])
         w = (form == F_OUTBOUND) & (tr['proto'] == p)
         if w.any():
-            lists[w] = compiled.list_id(host, 'inside_access_in', names[p])
+            lists[w] = compiled.list_id(host, tr.get('inside_acl', 'inside_access_in'), names[p])
     out['list'] = lists.astype(np.uint16)
     flags = np.where(valid, FL_VALID, 0)
     flags = flags | np.where(np.isin(form, [F_BUILT, F_NOYEAR, F_OUTBOUND]), FL_HIT, 0)

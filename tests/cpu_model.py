@@ -36,8 +36,8 @@ def classify_entries(ent, off, tup, chunk=2048):
         dlo, dsp = e['dst_lo'].astype(np.int64), e['dst_span'].astype(np.int64)
         pl, ps = e['port_lo'].astype(np.int64), e['port_span'].astype(np.int64)
         gid = e['gid'].astype(np.int64)
-        stride = (e['reserved'].astype(np.int64) & 0x7FFFFFFF)
-        on_sport = (e['reserved'].astype(np.int64) >> 31) & 1
+        stride = (e['step'].astype(np.int64) & 0x7FFFFFFF)
+        on_sport = (e['step'].astype(np.int64) >> 31) & 1
         for a in range(0, len(sel), chunk):
             idx = sel[a:a + chunk]
             s = tup['src'][idx].astype(np.int64)[:, None]

@@ -14,8 +14,7 @@ import numpy as np
 import pytest
 
 from oracle import coracle
-from ruleset_analysis_amd import acldb, synth
-from ruleset_analysis_amd.compile import CompiledRules, RECORD_DTYPE
+from ruleset_analysis_amd.compile import RECORD_DTYPE
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NO = 0xFFFFFFFFFFFFFFFF
@@ -35,11 +34,10 @@ def run_bench(tmp_path, extra, timeout=600):
 def check_dump_against_oracle(got, world, rules, lines, cap, seed=3):
     """rank 0's dumped result vs the C oracle over the ranks' shards in rank order."""
     import bench
-    _r, _l, _c, _s, zipf, ifcs, broad = bench.CONFIGS['cfg3']
-    dbj, info = synth.make_db(seed, rules, interfaces=ifcs, broad=broad)
-    compiled = CompiledRules(acldb.load_json(dbj))
-    compiled.ensure_lists()
-    trs = [c[1] for r in range(world) for c in bench.shard_chunks(dbj, info, compiled, lines, r, seed, zipf, world)]
+    wl = bench.Workload('cfg3', rules=rules, cap=cap)
+    assert wl.seed == seed
+    dbj = wl.dbj
+    trs = [c[1] for r in range(world) for c in bench.shard_chunks(wl, lines, r, world)]
     tr = {k: np.concatenate([t[k] for t in trs]) for k in ('src', 'dst', 'sport', 'dport', 'proto', 'ifc', 'form',
                                                           't', 'cid')}
     tr.update(interfaces=trs[0]['interfaces'], host=trs[0]['host'])

@@ -109,8 +109,8 @@ def _emulate_index(tuples, index, ent, off):
         if k == 'defer':
             n_defer += 1
             out[i] = exact[i]
-        elif k >= 0:
-            out[i] = int(ent[int(off[L]) + k]['gid'])
+        else:
+            out[i] = k
     return out
 
 
