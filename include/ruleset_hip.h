@@ -121,8 +121,10 @@ typedef struct rsa_pht_group {   /* 80 B */
 typedef struct rsa_pht_mask {    /* 32 B: one pruning table */
   uint32_t mask;             /* address mask (non-zero)                           */
   uint32_t side;             /* 0: src, 1: dst                                    */
-  uint32_t reserved[2];
-  rsa_pht_table table;       /* word value = bitmap index                         */
+  uint32_t slot_bits;        /* 32: slots as above; 16: uint16 slots (H & 0xFF) << 8 | value,
+                                0xFFFF empty, slot_off in uint16 units, values < 255 */
+  uint32_t reserved;
+  rsa_pht_table table;       /* slot value = bitmap index                         */
 } rsa_pht_mask;
 
 typedef struct rsa_pht_list {    /* 80 B: one list (or one chained chunk of a list) */

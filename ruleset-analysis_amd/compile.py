@@ -451,6 +451,19 @@ class _Image(object):
         soff, _ = self.alloc(slots)
         return (soff, 2 * doff, nslots, dmask)
 
+    def table16(self, H, vals):
+        """CHD table with 16-bit slots (8-bit tag << 8 | 8-bit value, 0xFFFF
+        empty) for values < 255; offsets in uint16 units of the image."""
+        nslots, dmask, disp, slot_of = _chd(H)
+        dwords = np.zeros(((dmask + 2) // 2) * 2, dtype=np.uint16)
+        dwords[:dmask + 1] = disp
+        doff, _ = self.alloc(dwords.view(np.uint32))
+        slots = np.full(nslots + (nslots & 1), 0xFFFF, dtype=np.uint16)
+        slots[slot_of] = ((H.astype(np.uint32) & np.uint32(0xFF)) << np.uint32(8)).astype(np.uint16) | \
+            np.asarray(vals, np.uint16)
+        soff, _ = self.alloc(slots.view(np.uint32))
+        return (2 * soff, 2 * doff, nslots, dmask)
+
     def build(self):
         return np.concatenate(self.chunks)
 
@@ -568,7 +581,12 @@ def _index_record(img, rec, e, pre, min_entries, max_groups):
             vals = np.array([bm_index[b] for b in merged.values()], dtype=np.uint32)
             r = mrec[PHT_MASK_WORDS * q: PHT_MASK_WORDS * (q + 1)]
             r[0], r[1] = m, side
-            r[4:8] = img.table(H, vals)
+            if len(distinct) < 0xFF:        # 16-bit slots: half the LDS of the pruning tables
+                r[2] = 16
+                r[4:8] = img.table16(H, vals)
+            else:
+                r[2] = 32
+                r[4:8] = img.table(H, vals)
         rec[0:4] = (goff, len(groups), moff, len(tables))
         rec[7] = bm_off
         rec[8], rec[9] = src_any & M32, src_any >> 32
@@ -650,6 +668,16 @@ def _probe(image, H, t):
     return (w & 0xFFFF) if (w >> 16) == (H & 0xFFFF) else PHT_NONE
 
 
+def _probe16(image, H, t):
+    """One probe of a 16-bit-slot CHD table (csrc: pht_probe16): value or PHT_NONE."""
+    slot_off, disp_off, n_slots, disp_mask = (int(v) for v in t)
+    H = int(H)
+    h16 = image.view(np.uint16)
+    d = int(h16[disp_off + ((H >> 16) & disp_mask)])
+    w = int(h16[slot_off + int(pht_slot(H, d, n_slots))])
+    return (w & 0xFF) if w != 0xFFFF and (w >> 8) == (H & 0xFF) else PHT_NONE
+
+
 def _match(x, src, dst, ports):
     pl, ps = int(x['port_lo']), int(x['port_span'])
     return ((src - int(x['src_lo'])) & M32) <= int(x['src_span']) and \
@@ -692,7 +720,7 @@ def pht_lookup(index, ent, off, L, src, dst, ports):
                 mr = [int(v) for v in image[moff + PHT_MASK_WORDS * q: moff + PHT_MASK_WORDS * (q + 1)]]
                 side = mr[1]
                 key = (dst if side else src) & mr[0]
-                v = _probe(image, field_hash(key, side), mr[4:8])
+                v = (_probe16 if mr[2] == 16 else _probe)(image, field_hash(key, side), mr[4:8])
                 if v != PHT_NONE:
                     bits = int(image[r[7] + 2 * v]) | (int(image[r[7] + 2 * v + 1]) << 32)
                     if side:

@@ -238,7 +238,7 @@ __device__ __forceinline__ uint32_t scan_list(const const_v4u* E, uint32_t beg, 
 
 constexpr uint32_t kDefer = 0xFFFFFFFEu;   // the index candidate failed verification: exact scan later
 constexpr uint32_t kNoCand = 0xFFFFu;
-constexpr int kImgSmallMax = 16000;   // LDS image words that still allow two 1024-thread workgroups per CU
+constexpr int kImgSmallMax = 19456;   // LDS image words that still allow two 1024-thread workgroups per CU (2 x 76 KiB)
 
 // murmur3 finaliser; must equal compile.py fmix32.
 __device__ __forceinline__ uint32_t fmix32(uint32_t x) {
@@ -273,6 +273,18 @@ __device__ __forceinline__ uint32_t pht_probe(P32 img, uint32_t H, v4u b) {
   return ((w >> 16) == (H & 0xFFFFu)) ? (w & 0xFFFFu) : kNoCand;
 }
 
+// The same probe of a table with 16-bit slots (8-bit tag, 8-bit value; the
+// pruning tables): b.x, b.y in uint16 units.  A tag false positive only adds
+// candidate groups (bitmaps are ORed; a superset is safe).
+template <typename P32>
+__device__ __forceinline__ uint32_t pht_probe16(P32 img, uint32_t H, v4u b) {
+  const uint32_t d = rd16(img, b.y + ((H >> 16) & b.w));
+  const uint32_t x = H + d * ((H * kPhtMul) | 1u);
+  const uint32_t slot = __umulhi(x, b.z);
+  const uint32_t w = rd16(img, b.x + slot);
+  return (w != 0xFFFFu && (w >> 8) == (H & 0xFFu)) ? (w & 0xFFu) : kNoCand;
+}
+
 constexpr int kAttempts = 4;   // compile.py PHT_ATTEMPTS
 constexpr uint32_t kListWords = 20, kGroupWords = 20, kMaskWords = 8;
 
@@ -287,18 +299,23 @@ constexpr uint32_t kListWords = 20, kGroupWords = 20, kMaskWords = 8;
 // candidate against its entry (16-bit tags collide), retried above a failed
 // candidate.  Returns gid, kNoGid or kDefer.
 template <typename P32>
-__device__ __forceinline__ uint32_t index_lookup(const Rules& R, P32 img, v4u h0, v4u h1, v4u h2, uint32_t ebeg,
-                                                 uint32_t src, uint32_t dst, uint32_t ports) {
+__device__ __forceinline__ uint32_t index_lookup(const Rules& R, P32 img, uint32_t lw, uint32_t src, uint32_t dst,
+                                                 uint32_t ports) {
+  // record fields are read where they are used (LDS reads are cheap; registers
+  // bound the occupancy): h0 {group_off, n_groups, mask_off, n_masks}
+  const v4u h0 = rd4(img, lw);
+  const v4u h2 = rd4(img, lw + 8);
   unsigned long long S = ((unsigned long long)h2.y << 32) | h2.x;
   unsigned long long D = ((unsigned long long)h2.w << 32) | h2.z;
+  const uint32_t bm_off = img[lw + 7];
   for (uint32_t k = 0; k < h0.w; ++k) {
     const uint32_t mw = h0.z + kMaskWords * k;
     const v4u m0 = rd4(img, mw), m1 = rd4(img, mw + 4);
     const bool dside = m0.y != 0;
     const uint32_t H = fmix32(((dside ? dst : src) & m0.x) ^ (dside ? kSaltD : kSaltS));
-    const uint32_t v = pht_probe(img, H, m1);
+    const uint32_t v = m0.z == 16u ? pht_probe16(img, H, m1) : pht_probe(img, H, m1);
     if (v != kNoCand) {
-      const uint32_t bw = h1.w + 2 * v;
+      const uint32_t bw = bm_off + 2 * v;
       const unsigned long long bits = ((unsigned long long)img[bw + 1] << 32) | img[bw];
       if (dside) {
         D |= bits;
@@ -309,9 +326,10 @@ __device__ __forceinline__ uint32_t index_lookup(const Rules& R, P32 img, v4u h0
   }
   const unsigned long long cand0 = S & D;
   if (!cand0) return kNoGid;
+  const uint32_t group_off = h0.x;
   // port-class hash components (compile.py PORT_CLASSES: any, dport, sport, both)
-  const uint32_t hp0 = fmix32(0u ^ kSaltP), hp1 = fmix32((ports & 0xFFFF0000u) ^ kSaltP),
-                 hp2 = fmix32((ports & 0x0000FFFFu) ^ kSaltP), hp3 = fmix32(ports ^ kSaltP);
+  const uint32_t hp1 = fmix32((ports & 0xFFFF0000u) ^ kSaltP), hp2 = fmix32((ports & 0x0000FFFFu) ^ kSaltP),
+                 hp3 = fmix32(ports ^ kSaltP);
   uint32_t floor = 0;
   for (int attempt = 0; attempt < kAttempts; ++attempt) {
     uint32_t bi = kNoCand;
@@ -319,15 +337,14 @@ __device__ __forceinline__ uint32_t index_lookup(const Rules& R, P32 img, v4u h0
     while (cand) {
       const uint32_t g = (uint32_t)__builtin_ctzll(cand);
       cand &= cand - 1;
-      const uint32_t gw = h0.x + kGroupWords * g;
+      const uint32_t gw = group_off + kGroupWords * g;
       const v4u a = rd4(img, gw);
       if (a.z >= bi) break;   // groups ascend in min index: no later group can do better
-      const v4u t0 = rd4(img, gw + 4), t1 = rd4(img, gw + 8), t2 = rd4(img, gw + 12), t3 = rd4(img, gw + 16);
       const uint32_t hsd = fmix32((src & a.x) ^ kSaltS) ^ fmix32((dst & a.y) ^ kSaltD);
-      uint32_t c0 = pht_probe(img, hsd ^ hp0, t0);
-      uint32_t c1 = pht_probe(img, hsd ^ hp1, t1);
-      uint32_t c2 = pht_probe(img, hsd ^ hp2, t2);
-      uint32_t c3 = pht_probe(img, hsd ^ hp3, t3);
+      uint32_t c0 = pht_probe(img, hsd ^ fmix32(0u ^ kSaltP), rd4(img, gw + 4));
+      uint32_t c1 = pht_probe(img, hsd ^ hp1, rd4(img, gw + 8));
+      uint32_t c2 = pht_probe(img, hsd ^ hp2, rd4(img, gw + 12));
+      uint32_t c3 = pht_probe(img, hsd ^ hp3, rd4(img, gw + 16));
       c0 = c0 >= floor ? c0 : kNoCand;
       c1 = c1 >= floor ? c1 : kNoCand;
       c2 = c2 >= floor ? c2 : kNoCand;
@@ -336,6 +353,7 @@ __device__ __forceinline__ uint32_t index_lookup(const Rules& R, P32 img, v4u h0
     }
     if (bi == kNoCand) return kNoGid;
     if (R.force_defer) return kDefer;
+    const uint32_t ebeg = img[lw + 12];
     const v4u ea = R.eg[2 * (size_t)(ebeg + bi)], eb = R.eg[2 * (size_t)(ebeg + bi) + 1];
     if (entry_match(ea, eb, src, dst, ports)) return entry_gid(eb, ports);
     floor = bi + 1;   // a tag collision: every true candidate lies above bi
@@ -368,40 +386,30 @@ __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Ru
     }
     return active ? best : kNoGid;
   }
-  // record words: h0 {group_off, n_groups, mask_off, n_masks}, h1 {resid_beg,
-  // resid_end, prefix, bm_off}, h2 {src_any, dst_any}, h3 {entry_beg,
-  // entry_len, n_bitmaps, after_min}, h4 {next, next_min, -, -}
-  v4u h0 = {0u, 0u, 0u, 0u}, h1 = {0u, 0u, 0u, 0u}, h2 = {0u, 0u, 0u, 0u}, h3 = {0u, 0u, 0u, 0u};
-  v4u h4 = {0u, 0u, 0u, 0u};
-  if (active) {
-    const uint32_t lw = R.list_off + kListWords * list;
-    h0 = rd4(img, lw);
-    h1 = rd4(img, lw + 4);
-    h2 = rd4(img, lw + 8);
-    h3 = rd4(img, lw + 12);
-    h4 = rd4(img, lw + 16);
-  }
+  // list record fields (include/ruleset_hip.h rsa_pht_list) are read from the
+  // image where they are used: lw = the lane's current record
+  uint32_t lw = R.list_off + kListWords * (active ? list : 0u);
   // 1. prefix scans
-  unsigned long long pending = __ballot(active && h1.z != 0);
+  const uint32_t pre_n = active ? img[lw + 6] : 0u;
+  unsigned long long pending = __ballot(active && pre_n != 0);
   while (pending) {
     const int leader = __builtin_ctzll(pending);
     const uint32_t L = __builtin_amdgcn_readlane(list, leader);
     const bool mine = active && list == L;
     pending &= ~__ballot(mine);
     const uint32_t beg = R.off[L];
-    const uint32_t pre = __builtin_amdgcn_readlane(h1.z, leader);
+    const uint32_t pre = __builtin_amdgcn_readlane(pre_n, leader);
     const uint32_t b = scan_list(R.e, beg, beg + pre, mine, kNoGid, t.x, t.y, t.z);
     if (mine) best = b;
   }
   // 2. per record of the lane's chain: the index (per lane), then the residual
   // scan (waterfall over the records present); the next chunk only while the
   // lane's best exceeds its smallest gid
-  bool go = active && best > h3.w;
+  bool go = active && best > img[lw + 15];
   bool deferred = false;
-  uint32_t rec = list;
   while (__ballot(go)) {
-    if (go && h0.y != 0) {
-      const uint32_t c = index_lookup(R, img, h0, h1, h2, h3.x, t.x, t.y, t.z);
+    if (go && img[lw + 1] != 0) {
+      const uint32_t c = index_lookup(R, img, lw, t.x, t.y, t.z);
       if (c == kDefer) {
         deferred = true;
         go = false;
@@ -409,26 +417,22 @@ __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Ru
         best = min(best, c);
       }
     }
-    const bool want = go && h1.x < h1.y;
+    const uint32_t rb = go ? img[lw + 4] : 0u, re = go ? img[lw + 5] : 0u;
+    const bool want = go && rb < re;
     pending = __ballot(want);
     while (pending) {
       const int leader = __builtin_ctzll(pending);
-      const uint32_t Q = __builtin_amdgcn_readlane(rec, leader);
-      const bool mine = want && rec == Q;
+      const uint32_t Q = __builtin_amdgcn_readlane(lw, leader);
+      const bool mine = want && lw == Q;
       pending &= ~__ballot(mine);
-      const uint32_t rb = __builtin_amdgcn_readlane(h1.x, leader), re = __builtin_amdgcn_readlane(h1.y, leader);
-      const uint32_t b = scan_list(R.resid, rb, re, mine, best, t.x, t.y, t.z);
+      const uint32_t b = scan_list(R.resid, __builtin_amdgcn_readlane(rb, leader), __builtin_amdgcn_readlane(re, leader),
+                                   mine, best, t.x, t.y, t.z);
       if (mine) best = b;
     }
-    go = go && h4.x != RSA_PHT_NONE && best > h4.y;
     if (go) {
-      rec = h4.x;
-      const uint32_t lw = R.list_off + kListWords * rec;
-      h0 = rd4(img, lw);
-      h1 = rd4(img, lw + 4);
-      h2 = rd4(img, lw + 8);
-      h3 = rd4(img, lw + 12);
-      h4 = rd4(img, lw + 16);
+      const uint32_t next = img[lw + 16];
+      go = next != RSA_PHT_NONE && best > img[lw + 17];
+      if (go) lw = R.list_off + kListWords * next;
     }
   }
   if (deferred) return kDefer;
@@ -594,101 +598,6 @@ __device__ __forceinline__ unsigned long long block_append(bool a, unsigned long
   return pos;
 }
 
-// Pass 1a — first-match classification (mapper.py:159-189): gid or RSA_NO_RULE
-// per tuple into gout (index image staged in LDS when kImg > 0).  Lines whose
-// index candidate failed verification kAttempts times go to `tail` (k_tail
-// scans them exactly).
-template <int kImg>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kImgSmallMax ? 4 : 8, 8))) void k_classify(
-    const uint4* __restrict__ T, unsigned long long n, int32_t* __restrict__ gout, Rules R, unsigned int* flags,
-    uint32_t* tail, unsigned long long* tail_n) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds_img[kImg > 0 ? kImg : 4];
-  __shared__ unsigned long long lds_app[2];
-  if (threadIdx.x < 2) lds_app[threadIdx.x] = 0;
-  if (kImg > 0 && R.indexed) {
-    const uint4* src = reinterpret_cast<const uint4*>(R.img);
-    uint4* dst = reinterpret_cast<uint4*>(lds_img);
-    for (uint32_t w = threadIdx.x; w < (R.img_words + 3) / 4; w += blockDim.x) dst[w] = src[w];
-  }
-  __syncthreads();
-  const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
-  for (unsigned long long base = (unsigned long long)blockIdx.x * blockDim.x; base < n; base += stride) {
-    const unsigned long long i = base + threadIdx.x;
-    const bool in = i < n;
-    const uint4 t = in ? T[i] : make_uint4(0u, 0u, 0u, 0u);
-    const bool valid = in && (((t.w >> 16) & 0xFFu) & RSA_F_VALID);
-    uint32_t gid;
-    if (kImg > 0) {
-      gid = classify_wave<false>(t, valid, R, (const lds_u32*)lds_img, flags);
-    } else {
-      gid = classify_wave<false>(t, valid, R, R.img, flags);
-    }
-    const bool defer = gid == kDefer;
-    if (__syncthreads_or(defer)) {   // rare: workgroup-aggregated append
-      const unsigned long long pos = block_append(defer, tail_n, lds_app);
-      if (defer) tail[pos] = (uint32_t)i;
-    }
-    if (in && !defer) gout[i] = (int32_t)gid;
-  }
-}
-
-// Pass 1a, deferred lines: exact linear scan of their whole list.
-__global__ __launch_bounds__(kBlock) void k_tail(const uint4* __restrict__ T, int32_t* __restrict__ gout, Rules R,
-                                                 unsigned int* flags, const uint32_t* __restrict__ tail,
-                                                 const unsigned long long* tail_n) {
-  const unsigned long long n = *tail_n;
-  const unsigned long long stride = (unsigned long long)gridDim.x * kBlock;
-  for (unsigned long long base = (unsigned long long)blockIdx.x * kBlock; base < n; base += stride) {
-    const unsigned long long j = base + threadIdx.x;
-    const bool in = j < n;
-    const unsigned long long i = in ? tail[j] : 0u;
-    const uint4 t = in ? T[i] : make_uint4(0u, 0u, 0u, 0u);
-    const bool valid = in && (((t.w >> 16) & 0xFFu) & RSA_F_VALID);
-    const uint32_t gid = classify_wave<true>(t, valid, R, R.img, flags);
-    if (in) gout[i] = (int32_t)gid;
-  }
-}
-
-// matches[key] += 1 for lanes with `m`, hits[key] += 1 for lanes with `h` (h
-// implies m): one loop over the wave's distinct keys, one device atomic per
-// key and counter.  Wave-uniform control flow.
-__device__ __forceinline__ void wave_count2(bool m, bool h, uint32_t key, unsigned long long* matches,
-                                            unsigned long long* hits) {
-  unsigned long long pending = __ballot(m);
-  const unsigned long long hm = __ballot(h);
-  while (pending) {
-    const int leader = __builtin_ctzll(pending);
-    const uint32_t k = __builtin_amdgcn_readlane(key, leader);
-    const unsigned long long peers = __ballot(m && key == k);
-    pending &= ~peers;
-    if ((int)__lane_id() == leader) {
-      atomicAdd(&matches[k], (unsigned long long)__popcll(peers));
-      const unsigned long long hp = peers & hm;
-      if (hp) atomicAdd(&hits[k], (unsigned long long)__popcll(hp));
-    }
-  }
-}
-
-// ---- Pass 1b — the reducer's aggregation of classified lines
-// (connlist-reducer.py:62-79,146-176), as an on-chip shuffle.
-//
-// The distinct-connection table is split into regions of 2^rs_bits slots; a
-// key's region is the top np_bits of its slot hash and its home slot lies in
-// that region (linear probing wraps inside it).  Table writes are scattered
-// memory transactions (the chip sustains ~20 G/s of them against ~125 G/s of
-// 64-B streaming lines), so instead of one read-modify-write per line:
-//   k_aggregate   per-rule line/hit counters (LDS histogram) and, for each hit
-//                 line the BUILT regex matched that can still change an output
-//                 (order <= filter[gid]), a 32-B record appended in line order;
-//   k_part_hist / exclusive scan / k_part_scatter
-//                 a stable-free counting sort of the records by region;
-//   k_reduce      one workgroup per region: records aggregated in an LDS hash
-//                 table (count, first, last, min_order per key), then merged
-//                 into the region's slots with plain loads and stores — the
-//                 workgroup owns its region for the whole kernel, new slots are
-//                 claimed in an LDS copy of the region's occupancy bitmap.
-// Records per key shrink to one merge per LDS round.
-
 struct alignas(32) Rec {
   unsigned long long kA, kB, order;
   uint32_t ts, region;
@@ -721,16 +630,199 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t* sh, uint3
   return before + x - v;
 }
 
+// Where pass 1 puts its per-line results (k_classify / k_tail with kEmit), all
+// indexed by the line (no appends, so no atomics or workgroup barriers in the
+// classifier): the gid|hit word for the per-rule counters (k_count), and for
+// every hit + BUILT line below its rule's filter bound a 32-B record plus its
+// table region (0xFFFF: no record) for the region sort of the table reduction
+// (connlist-reducer.py:146-176).
+struct Emit {
+  uint32_t* gh;                         // gid | hit << 31, 0xFFFFFFFF: no rule
+  const uint32_t* ts;
+  const unsigned long long* ord;
+  Rec* recs;                            // line-indexed, written only where regs != 0xFFFF
+  uint16_t* regs;                       // line-indexed region or kNoRegion
+};
+constexpr uint32_t kNoRegion = 0xFFFFu;
+
+__device__ __forceinline__ void emit_line(uint32_t i, uint4 t, uint32_t gid, const Agg& A, const Emit& E) {
+  const uint32_t flags = (t.w >> 16) & 0xFFu;
+  const bool matched = gid != kNoGid;
+  const bool hit = matched && (flags & RSA_F_HIT);
+  E.gh[i] = matched ? (gid | (hit ? 0x80000000u : 0u)) : 0xFFFFFFFFu;
+  bool need = hit && (flags & RSA_F_BUILT) && A.cap > 0 && !(A.skip & 2u);
+  unsigned long long o = 0;
+  if (need) {
+    o = E.ord[i];
+    need = o <= A.filter[gid];   // exact skip: capped with threshold <= filter < order
+  }
+  uint32_t region = kNoRegion;
+  if (need) {
+    Rec r;
+    conn_key(t, gid, r.kA, r.kB);
+    r.order = o;
+    r.ts = E.ts[i];
+    r.region = key_region(A, slot_hash(r.kA, r.kB));
+    region = r.region;
+    E.recs[i] = r;
+  }
+  E.regs[i] = (uint16_t)region;
+}
+
+// Pass 1a — first-match classification (mapper.py:159-189): gid or RSA_NO_RULE
+// per tuple into gout (nullable), index image staged in LDS when kImg > 0;
+// with kEmit the line's counter word and table record (emit_line).  Lines
+// whose index candidate failed verification kAttempts times go to `tail`
+// (k_tail scans and emits them exactly).
+template <int kImg, bool kEmit>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kImgSmallMax ? 4 : 8, 8))) void k_classify(
+    const uint4* __restrict__ T, unsigned long long n, int32_t* __restrict__ gout, Rules R, unsigned int* flags,
+    uint32_t* tail, unsigned long long* tail_n, Agg A, Emit E) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds_img[kImg > 0 ? kImg : 4];
+  __shared__ unsigned long long lds_app[2];
+  if (threadIdx.x < 2) lds_app[threadIdx.x] = 0;
+  if (kImg > 0 && R.indexed) {
+    const uint4* src = reinterpret_cast<const uint4*>(R.img);
+    uint4* dst = reinterpret_cast<uint4*>(lds_img);
+    for (uint32_t w = threadIdx.x; w < (R.img_words + 3) / 4; w += blockDim.x) dst[w] = src[w];
+  }
+  __syncthreads();
+  // 32-bit line indices: batches are < 2^31 lines (run_pass1, rsa_classify_only)
+  const uint32_t n32 = (uint32_t)n;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t base = blockIdx.x * blockDim.x; base < n32; base += stride) {
+    const uint32_t i = base + threadIdx.x;
+    const bool in = i < n32;
+    const uint4 t = in ? T[i] : make_uint4(0u, 0u, 0u, 0u);
+    const bool valid = in && (((t.w >> 16) & 0xFFu) & RSA_F_VALID);
+    uint32_t gid;
+    if (kImg > 0) {
+      gid = classify_wave<false>(t, valid, R, (const lds_u32*)lds_img, flags);
+    } else {
+      gid = classify_wave<false>(t, valid, R, R.img, flags);
+    }
+    const bool defer = gid == kDefer;
+    if (__syncthreads_or(defer)) {   // rare: workgroup-aggregated append
+      const unsigned long long pos = block_append(defer, tail_n, lds_app);
+      if (defer) tail[pos] = (uint32_t)i;
+    }
+    if (gout && in && !defer) gout[i] = (int32_t)gid;
+    if (kEmit && in && !defer) emit_line(i, t, gid, A, E);
+  }
+}
+
+// Pass 1a, deferred lines: exact linear scan of their whole list (+ emission).
+template <bool kEmit>
+__global__ __launch_bounds__(kBlock) void k_tail(const uint4* __restrict__ T, int32_t* __restrict__ gout, Rules R,
+                                                 unsigned int* flags, const uint32_t* __restrict__ tail,
+                                                 const unsigned long long* tail_n, Agg A, Emit E) {
+  const unsigned long long n = *tail_n;
+  const unsigned long long stride = (unsigned long long)gridDim.x * kBlock;
+  for (unsigned long long base = (unsigned long long)blockIdx.x * kBlock; base < n; base += stride) {
+    const unsigned long long j = base + threadIdx.x;
+    const bool in = j < n;
+    const unsigned long long i = in ? tail[j] : 0u;
+    const uint4 t = in ? T[i] : make_uint4(0u, 0u, 0u, 0u);
+    const bool valid = in && (((t.w >> 16) & 0xFFu) & RSA_F_VALID);
+    const uint32_t gid = classify_wave<true>(t, valid, R, R.img, flags);
+    if (gout && in) gout[i] = (int32_t)gid;
+    if (kEmit && in) emit_line((uint32_t)i, t, gid, A, E);
+  }
+}
+
+// matches[key] += 1 for lanes with `m`, hits[key] += 1 for lanes with `h` (h
+// implies m): one loop over the wave's distinct keys, one device atomic per
+// key and counter.  Wave-uniform control flow.
+__device__ __forceinline__ void wave_count2(bool m, bool h, uint32_t key, unsigned long long* matches,
+                                            unsigned long long* hits) {
+  unsigned long long pending = __ballot(m);
+  const unsigned long long hm = __ballot(h);
+  while (pending) {
+    const int leader = __builtin_ctzll(pending);
+    const uint32_t k = __builtin_amdgcn_readlane(key, leader);
+    const unsigned long long peers = __ballot(m && key == k);
+    pending &= ~peers;
+    if ((int)__lane_id() == leader) {
+      atomicAdd(&matches[k], (unsigned long long)__popcll(peers));
+      const unsigned long long hp = peers & hm;
+      if (hp) atomicAdd(&hits[k], (unsigned long long)__popcll(hp));
+    }
+  }
+}
+
+// Per-rule line / hit counters from the gid|hit words of pass 1a
+// (connlist-reducer.py:146-148 and the mapper's per-rule output lines):
+// LDS-privatised when the rules fit (kLds), else wave-aggregated atomics.
+template <int kLds>
+__global__ __launch_bounds__(1024) void k_count(const uint32_t* __restrict__ gh, unsigned long long n, uint32_t n_rules,
+                                                Agg A) {
+  __shared__ uint32_t cnt[kLds > 0 ? 2 * kLds : 1];
+  if (kLds > 0) {
+    for (uint32_t r = threadIdx.x; r < 2u * kLds; r += blockDim.x) cnt[r] = 0;
+    __syncthreads();
+  }
+  const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x * 4;
+  for (unsigned long long base = (unsigned long long)blockIdx.x * blockDim.x * 4; base < n; base += stride) {
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const unsigned long long i = base + (unsigned long long)k * blockDim.x + threadIdx.x;
+      w[k] = i < n ? gh[i] : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool m = w[k] != 0xFFFFFFFFu;
+      const uint32_t g = w[k] & 0x7FFFFFFFu;
+      const bool h = m && (w[k] >> 31);
+      if (kLds > 0) {
+        if (m) atomicAdd(&cnt[g], 1u);
+        if (h) atomicAdd(&cnt[kLds + g], 1u);
+      } else {
+        wave_count2(m, h, g, A.matches, A.hits);
+      }
+    }
+  }
+  if (kLds > 0) {
+    __syncthreads();
+    for (uint32_t r = threadIdx.x; r < n_rules; r += blockDim.x) {
+      const uint32_t m = cnt[r], hh = cnt[kLds + r];
+      if (m) atomicAdd(&A.matches[r], (unsigned long long)m);
+      if (hh) atomicAdd(&A.hits[r], (unsigned long long)hh);
+    }
+  }
+}
+
+// ---- Pass 1b — the reducer's aggregation of classified lines
+// (connlist-reducer.py:62-79,146-176), as an on-chip shuffle.
+//
+// The distinct-connection table is split into regions of 2^rs_bits slots; a
+// key's region is the top np_bits of its slot hash and its home slot lies in
+// that region (linear probing wraps inside it).  Table writes are scattered
+// memory transactions (the chip sustains ~20 G/s of them against ~125 G/s of
+// 64-B streaming lines), so instead of one read-modify-write per line:
+//   k_aggregate   per-rule line/hit counters (LDS histogram) and, for each hit
+//                 line the BUILT regex matched that can still change an output
+//                 (order <= filter[gid]), a 32-B record appended in line order;
+//   k_part_hist / exclusive scan / k_part_scatter
+//                 a stable-free counting sort of the records by region;
+//   k_reduce      one workgroup per region: records aggregated in an LDS hash
+//                 table (count, first, last, min_order per key), then merged
+//                 into the region's slots with plain loads and stores — the
+//                 workgroup owns its region for the whole kernel, new slots are
+//                 claimed in an LDS copy of the region's occupancy bitmap.
+// Records per key shrink to one merge per LDS round.
+
 constexpr int kAggU = 4;
+// Pass 1b with the rule already known per line (rsa_aggregate_gids, the
+// reducer drop-in): per-rule counters (LDS histogram when the rules fit) and
+// the line-indexed records of emit_line.
 template <int kLds>
 __global__ __launch_bounds__(1024) void k_aggregate(const uint4* __restrict__ T, const uint32_t* __restrict__ TS,
                                                     const unsigned long long* __restrict__ ORD,
                                                     const int32_t* __restrict__ G, unsigned long long n,
                                                     uint32_t n_rules, Agg A, Rec* __restrict__ recs,
-                                                    uint16_t* __restrict__ regs, unsigned long long* __restrict__ n_recs) {
+                                                    uint16_t* __restrict__ regs) {
   __shared__ uint32_t cnt[kLds > 0 ? 2 * kLds : 1];   // matches, hits
-  __shared__ uint32_t sh[18];
-  __shared__ unsigned long long sh_base;
   const bool counters = !(A.skip & 1u);
   if (kLds > 0) {
     for (uint32_t r = threadIdx.x; r < 2u * kLds; r += blockDim.x) cnt[r] = 0;
@@ -740,60 +832,45 @@ __global__ __launch_bounds__(1024) void k_aggregate(const uint4* __restrict__ T,
   const unsigned long long span = (unsigned long long)blockDim.x * kAggU;
   for (unsigned long long base = (unsigned long long)blockIdx.x * span; base < n;
        base += (unsigned long long)gridDim.x * span) {
-    uint32_t gid[kAggU];
-    uint4 t[kAggU];
 #pragma unroll
     for (int k = 0; k < kAggU; ++k) {
       const unsigned long long i = base + (unsigned long long)k * blockDim.x + threadIdx.x;
       const bool in = i < n;
-      gid[k] = in ? (uint32_t)G[i] : kNoGid;
-      t[k] = in ? T[i] : make_uint4(0u, 0u, 0u, 0u);
-    }
-    bool need[kAggU];
-    unsigned long long o[kAggU], f[kAggU];
-#pragma unroll
-    for (int k = 0; k < kAggU; ++k) {
-      const unsigned long long i = base + (unsigned long long)k * blockDim.x + threadIdx.x;
-      const uint32_t flags = (t[k].w >> 16) & 0xFFu;
-      if (gid[k] != kNoGid && gid[k] >= n_rules) atomicOr(&A.flags[1], 2u);
-      const bool matched = gid[k] < n_rules;
+      uint32_t gid = in ? (uint32_t)G[i] : kNoGid;
+      const uint4 t = in ? T[i] : make_uint4(0u, 0u, 0u, 0u);
+      const uint32_t flags = (t.w >> 16) & 0xFFu;
+      if (gid != kNoGid && gid >= n_rules) {
+        atomicOr(&A.flags[1], 2u);
+        gid = kNoGid;
+      }
+      const bool matched = gid != kNoGid;
       const bool hit = matched && (flags & RSA_F_HIT);
       if (counters) {
         if (kLds > 0) {
-          if (matched) atomicAdd(&cnt[gid[k]], 1u);
-          if (hit) atomicAdd(&cnt[kLds + gid[k]], 1u);
+          if (matched) atomicAdd(&cnt[gid], 1u);
+          if (hit) atomicAdd(&cnt[kLds + gid], 1u);
         } else {
-          wave_count2(matched, hit, gid[k], A.matches, A.hits);
+          wave_count2(matched, hit, gid, A.matches, A.hits);
         }
       }
-      need[k] = table && hit && (flags & RSA_F_BUILT);
-      o[k] = need[k] ? ORD[i] : 0ull;
-      f[k] = need[k] ? A.filter[gid[k]] : 0ull;
-    }
-    uint32_t c = 0;
-#pragma unroll
-    for (int k = 0; k < kAggU; ++k) {
-      need[k] = need[k] && o[k] <= f[k];   // exact skip: capped with threshold <= filter < order
-      c += need[k] ? 1u : 0u;
-    }
-    uint32_t total;
-    const uint32_t off = block_exscan(c, sh, &total);
-    if (total == 0) continue;   // workgroup-uniform
-    if (threadIdx.x == 0) sh_base = atomicAdd(n_recs, (unsigned long long)total);
-    __syncthreads();
-    unsigned long long pos = sh_base + off;
-    __syncthreads();   // sh_base is rewritten by the next iteration
-#pragma unroll
-    for (int k = 0; k < kAggU; ++k) {
-      if (!need[k]) continue;
-      const unsigned long long i = base + (unsigned long long)k * blockDim.x + threadIdx.x;
-      Rec r;
-      conn_key(t[k], gid[k], r.kA, r.kB);
-      r.order = o[k];
-      r.ts = TS[i];
-      r.region = key_region(A, slot_hash(r.kA, r.kB));
-      regs[pos] = (uint16_t)r.region;
-      recs[pos++] = r;
+      bool need = table && hit && (flags & RSA_F_BUILT);
+      unsigned long long o = 0;
+      if (need) {
+        o = ORD[i];
+        need = o <= A.filter[gid];
+      }
+      if (!in) continue;
+      uint32_t region = kNoRegion;
+      if (need) {
+        Rec r;
+        conn_key(t, gid, r.kA, r.kB);
+        r.order = o;
+        r.ts = TS[i];
+        r.region = key_region(A, slot_hash(r.kA, r.kB));
+        region = r.region;
+        recs[i] = r;
+      }
+      regs[i] = (uint16_t)region;
     }
   }
   if (kLds > 0) {
@@ -823,14 +900,18 @@ __global__ __launch_bounds__(1024) void k_part_hist(const uint16_t* __restrict__
   __syncthreads();
   const unsigned long long beg = (unsigned long long)tile * tile_len;
   const unsigned long long end = beg + tile_len < n ? beg + tile_len : n;
-  for (unsigned long long j = beg + threadIdx.x; j < end; j += blockDim.x) atomicAdd(&hcount[regs[j]], 1u);
+  for (unsigned long long j = beg + threadIdx.x; j < end; j += blockDim.x) {
+    const uint32_t r = regs[j];
+    if (r != kNoRegion) atomicAdd(&hcount[r], 1u);
+  }
   __syncthreads();
   for (uint32_t r = threadIdx.x; r < n_regions; r += blockDim.x) hist[(size_t)r * n_tiles + tile] = hcount[r];
 }
 
-__global__ __launch_bounds__(1024) void k_part_scatter(const Rec* __restrict__ recs, unsigned long long n,
-                                                       uint32_t n_regions, uint32_t n_tiles, uint32_t tile_len,
-                                                       const uint32_t* __restrict__ offs, Rec* __restrict__ out) {
+__global__ __launch_bounds__(1024) void k_part_scatter(const Rec* __restrict__ recs, const uint16_t* __restrict__ regs,
+                                                       unsigned long long n, uint32_t n_regions, uint32_t n_tiles,
+                                                       uint32_t tile_len, const uint32_t* __restrict__ offs,
+                                                       Rec* __restrict__ out) {
   __shared__ uint32_t cur[kMaxRegions];
   const uint32_t tile = blockIdx.x;
   for (uint32_t r = threadIdx.x; r < n_regions; r += blockDim.x) cur[r] = offs[(size_t)r * n_tiles + tile];
@@ -838,8 +919,9 @@ __global__ __launch_bounds__(1024) void k_part_scatter(const Rec* __restrict__ r
   const unsigned long long beg = (unsigned long long)tile * tile_len;
   const unsigned long long end = beg + tile_len < n ? beg + tile_len : n;
   for (unsigned long long j = beg + threadIdx.x; j < end; j += blockDim.x) {
-    const Rec r = recs[j];
-    out[atomicAdd(&cur[r.region], 1u)] = r;
+    const uint32_t g = regs[j];
+    if (g == kNoRegion) continue;
+    out[atomicAdd(&cur[g], 1u)] = recs[j];
   }
 }
 
@@ -865,6 +947,7 @@ __global__ __launch_bounds__(1024) void k_scan_blocks(uint32_t* __restrict__ a, 
   if (threadIdx.x == 0) sums[blockIdx.x] = total;
 }
 
+// (sums[nb] receives the grand total)
 __global__ __launch_bounds__(1024) void k_scan_sums(uint32_t* __restrict__ sums, uint32_t nb) {
   __shared__ uint32_t sh[18];
   uint32_t carry = 0;
@@ -876,6 +959,7 @@ __global__ __launch_bounds__(1024) void k_scan_sums(uint32_t* __restrict__ sums,
     if (j < nb) sums[j] = carry + ex;
     carry += total;
   }
+  if (threadIdx.x == 0) sums[nb] = carry;
 }
 
 __global__ __launch_bounds__(1024) void k_scan_add(uint32_t* __restrict__ a, unsigned long long n,
@@ -1077,12 +1161,13 @@ __global__ __launch_bounds__(1024) void k_reduce(const Rec* __restrict__ recs,
     for (uint32_t w = threadIdx.x; w < words; w += blockDim.x) gocc[w] = occ[w];
 }
 
-// Segment starts of one pass-1 launch: starts[r] = base + offs[r * n_tiles].
+// Segment starts of one pass-1 launch: starts[r] = base + offs[r * n_tiles],
+// starts[n_regions] = base + the record total (written by k_scan_sums).
 __global__ void k_seg_starts(const uint32_t* __restrict__ offs, uint32_t n_tiles, uint32_t n_regions,
-                             unsigned long long base, unsigned long long n_recs, unsigned long long* starts) {
+                             unsigned long long base, const uint32_t* __restrict__ total, unsigned long long* starts) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r < n_regions) starts[r] = base + offs[(size_t)r * n_tiles];
-  if (r == n_regions) starts[r] = base + n_recs;
+  if (r == n_regions) starts[r] = base + *total;
 }
 
 // Pass 2: lines with order <= P of capped rules recount count/first/last into
@@ -1506,7 +1591,9 @@ struct rsa_ctx {
   uint32_t* d_tail = nullptr;         // deferred line indices
   unsigned long long* d_tail_n = nullptr;
   unsigned long long tail_alloc = 0;
-  int32_t* d_gscratch = nullptr;      // gids of a pass 1 / recount whose caller keeps none
+  int32_t* d_gscratch = nullptr;      // gids of a recount whose caller keeps none
+  uint32_t* d_gh = nullptr;           // pass-1 gid | hit << 31 per line (k_count input)
+  unsigned long long gh_alloc = 0;
   // on-chip shuffle of pass 1b: records, their region-sorted copy, histograms
   void* d_recs = nullptr;
   void* d_recs2 = nullptr;
@@ -1755,30 +1842,39 @@ int ensure_events(rsa_ctx* c) {
 }
 
 // LDS image capacities (32-bit words) of k_classify.
-constexpr int kImgSmall = kImgSmallMax;   // 62.5 KiB: two 1024-thread workgroups per CU (32 waves)
+constexpr int kImgSmall = kImgSmallMax;   // 76 KiB: two 1024-thread workgroups per CU (32 waves)
 constexpr int kImgLarge = 38912;   // 152 KiB: one workgroup per CU
 
-// Classification (+ exact tail) of lines [0, m) of T (already offset) into go.
-int launch_classify(rsa_ctx* c, const uint4* t, uint64_t m, int32_t* go) {
+// Classification (+ exact tail) of lines [0, m) of T (already offset) into go
+// (nullable); with `e` also the pass-1 emission (counter words, records).
+template <bool kEmit>
+int launch_classify_t(rsa_ctx* c, const uint4* t, uint64_t m, int32_t* go, const Emit& e) {
   const Rules r = rules_of(c);
-  int rc = ensure_tail(c, m);
-  if (rc) return rc;
-  HIPCHK(c, hipMemsetAsync(c->d_tail_n, 0, sizeof(unsigned long long), c->stream));
+  const Agg ag = agg_of(c);
   if (c->indexed && c->img_words <= (uint32_t)kImgSmall) {
-    k_classify<kImgSmall><<<grid_for_threads(c, m, 1024, 2), 1024, 0, c->stream>>>(t, m, go, r, c->d_flags, c->d_tail,
-                                                                                 c->d_tail_n);
+    k_classify<kImgSmall, kEmit><<<grid_for_threads(c, m, 1024, 2), 1024, 0, c->stream>>>(
+        t, m, go, r, c->d_flags, c->d_tail, c->d_tail_n, ag, e);
   } else if (c->indexed && c->img_words <= (uint32_t)kImgLarge) {
-    k_classify<kImgLarge><<<grid_for_threads(c, m, 1024, 1), 1024, 0, c->stream>>>(t, m, go, r, c->d_flags, c->d_tail,
-                                                                                 c->d_tail_n);
+    k_classify<kImgLarge, kEmit><<<grid_for_threads(c, m, 1024, 1), 1024, 0, c->stream>>>(
+        t, m, go, r, c->d_flags, c->d_tail, c->d_tail_n, ag, e);
   } else {
-    k_classify<0><<<grid_for_threads(c, m, 1024, 2), 1024, 0, c->stream>>>(t, m, go, r, c->d_flags, c->d_tail,
-                                                                         c->d_tail_n);
+    k_classify<0, kEmit><<<grid_for_threads(c, m, 1024, 2), 1024, 0, c->stream>>>(t, m, go, r, c->d_flags, c->d_tail,
+                                                                                   c->d_tail_n, ag, e);
   }
   HIPCHK(c, hipGetLastError());
   // deferred lines (their number is read on the device: no host sync)
-  k_tail<<<c->cu_count * 4, kBlock, 0, c->stream>>>(t, go, r, c->d_flags, c->d_tail, c->d_tail_n);
+  k_tail<kEmit><<<c->cu_count * 4, kBlock, 0, c->stream>>>(t, go, r, c->d_flags, c->d_tail, c->d_tail_n, ag, e);
   HIPCHK(c, hipGetLastError());
   return RSA_OK;
+}
+
+int launch_classify(rsa_ctx* c, const uint4* t, uint64_t m, int32_t* go, const Emit* e) {
+  int rc = ensure_tail(c, m);
+  if (rc) return rc;
+  HIPCHK(c, hipMemsetAsync(c->d_tail_n, 0, sizeof(unsigned long long), c->stream));
+  if (e) return launch_classify_t<true>(c, t, m, go, *e);
+  Emit none = {};
+  return launch_classify_t<false>(c, t, m, go, none);
 }
 
 // LDS-privatised counter capacity (rules): 2 x 4 B per rule (lines, hits),
@@ -1786,12 +1882,17 @@ int launch_classify(rsa_ctx* c, const uint4* t, uint64_t m, int32_t* go) {
 // for two per CU (launch_aggregate), i.e. two rounds of workgroups.
 constexpr int kCnt = 13312;
 
-// Exclusive scan of n uint32 in place (device).
-int exclusive_scan(rsa_ctx* c, uint32_t* d, unsigned long long n) {
-  if (n == 0) return RSA_OK;
-  const unsigned long long nb = (n + kScanBlock - 1) / kScanBlock;
-  int rc = ensure_buf(c, &c->d_scan_sums, &c->scan_sums_alloc, nb);
+// Exclusive scan of n uint32 in place (device); returns the device address of
+// the grand total.
+int exclusive_scan(rsa_ctx* c, uint32_t* d, unsigned long long n, uint32_t** total) {
+  const unsigned long long nb = n ? (n + kScanBlock - 1) / kScanBlock : 1;
+  int rc = ensure_buf(c, &c->d_scan_sums, &c->scan_sums_alloc, nb + 1);
   if (rc) return rc;
+  *total = c->d_scan_sums + nb;
+  if (n == 0) {
+    HIPCHK(c, hipMemsetAsync(*total, 0, sizeof(uint32_t), c->stream));
+    return RSA_OK;
+  }
   k_scan_blocks<<<(unsigned)nb, 1024, 0, c->stream>>>(d, n, c->d_scan_sums);
   k_scan_sums<<<1, 1024, 0, c->stream>>>(c->d_scan_sums, (uint32_t)nb);
   k_scan_add<<<(unsigned)nb, 1024, 0, c->stream>>>(d, n, c->d_scan_sums);
@@ -1799,62 +1900,82 @@ int exclusive_scan(rsa_ctx* c, uint32_t* d, unsigned long long n) {
   return RSA_OK;
 }
 
-// Pass 1b over lines [0, m): counters + records (k_aggregate), counting sort of
-// the records by region, per-region LDS reduction and merge (k_reduce).
-int launch_aggregate(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsigned long long* o, const int32_t* g,
-                     uint64_t m) {
-  const Agg ag = agg_of(c);
+// Line-indexed record buffers of a pass-1 launch over m lines.
+int prepare_records(rsa_ctx* c, uint64_t m) {
   int rc = ensure_buf(c, reinterpret_cast<Rec**>(&c->d_recs), &c->recs_alloc, m);
   if (!rc) rc = ensure_buf(c, &c->d_regs, &c->regs_alloc, m);
-  if (rc) return rc;
-  if (!c->d_nrecs) HIPCHK(c, hipMalloc(&c->d_nrecs, sizeof(unsigned long long)));
-  HIPCHK(c, hipMemsetAsync(c->d_nrecs, 0, sizeof(unsigned long long), c->stream));
-  Rec* recs = reinterpret_cast<Rec*>(c->d_recs);
-  const uint64_t units = (m + kAggU - 1) / kAggU;
-  if (c->n_rules <= (uint32_t)kCnt) {
-    k_aggregate<kCnt><<<grid_for_threads(c, units, 1024, 2), 1024, 0, c->stream>>>(t, ts, o, g, m, c->n_rules, ag,
-                                                                                   recs, c->d_regs, c->d_nrecs);
+  return rc;
+}
+
+// Pass 1b over lines [a, a + m) of the batch: the per-rule counters (k_count
+// over the gid|hit words `gh` of a classifying pass 1a, or k_aggregate over
+// given gids, which also writes the line-indexed records), then the counting
+// sort of the records by table region into d_recs2[a ..] (records <= lines,
+// so no record count is needed on the host) and the per-region LDS reduction
+// and merge (k_reduce).
+int launch_aggregate(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsigned long long* o, const int32_t* g,
+                     const uint32_t* gh, uint64_t a, uint64_t m) {
+  const Agg ag = agg_of(c);
+  int rc = RSA_OK;
+  if (gh) {
+    if (!(ag.skip & 1u)) {
+      const uint64_t units = (m + 3) / 4;
+      if (c->n_rules <= (uint32_t)kCnt) {
+        k_count<kCnt><<<grid_for_threads(c, units, 1024, 2), 1024, 0, c->stream>>>(gh, m, c->n_rules, ag);
+      } else {
+        k_count<0><<<grid_for_threads(c, units, 1024, 8), 1024, 0, c->stream>>>(gh, m, c->n_rules, ag);
+      }
+    }
   } else {
-    k_aggregate<0><<<grid_for_threads(c, units, 1024, 2), 1024, 0, c->stream>>>(t, ts, o, g, m, c->n_rules, ag, recs,
-                                                                                c->d_regs, c->d_nrecs);
+    rc = prepare_records(c, m);
+    if (rc) return rc;
+    const uint64_t units = (m + kAggU - 1) / kAggU;
+    Rec* recs = reinterpret_cast<Rec*>(c->d_recs);
+    if (c->n_rules <= (uint32_t)kCnt) {
+      k_aggregate<kCnt><<<grid_for_threads(c, units, 1024, 2), 1024, 0, c->stream>>>(t, ts, o, g, m, c->n_rules, ag,
+                                                                                     recs, c->d_regs);
+    } else {
+      k_aggregate<0><<<grid_for_threads(c, units, 1024, 2), 1024, 0, c->stream>>>(t, ts, o, g, m, c->n_rules, ag,
+                                                                                  recs, c->d_regs);
+    }
   }
   HIPCHK(c, hipGetLastError());
-  unsigned long long nr = 0;
-  HIPCHK(c, hipMemcpyAsync(&nr, c->d_nrecs, sizeof nr, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  if (c->debug) fprintf(stderr, "[rsa] pass-1 launch: %llu lines -> %llu records\n", (unsigned long long)m, nr);
-  if (nr == 0) return RSA_OK;
-  if (nr > m) return fail(c, RSA_ERR_STATE, "record count %llu exceeds the batch", nr);
-  // region-sorted records: appended after the previous launches' while this
-  // job's records are kept for the recount (rsa_recount), else from 0
-  if (c->rec_cache && (c->n_segs >= (uint32_t)kMaxSegs || c->seg_base + nr > c->recs2_alloc)) c->rec_cache = false;
+  if (ag.cap == 0 || (ag.skip & 2u)) return RSA_OK;   // no table this job
+  const Rec* recs = reinterpret_cast<const Rec*>(c->d_recs);
+  // region-sorted records: at the launch's line offset while this job's
+  // records are kept for the recount (rsa_recount), else from 0
+  if (c->rec_cache && (c->n_segs >= (uint32_t)kMaxSegs || a + m > c->recs2_alloc)) c->rec_cache = false;
+  const unsigned long long seg_base = c->rec_cache ? a : 0;
   if (!c->rec_cache) {
-    c->seg_base = 0;
     c->n_segs = 0;
-    rc = ensure_buf(c, reinterpret_cast<Rec**>(&c->d_recs2), &c->recs2_alloc, nr);
+    rc = ensure_buf(c, reinterpret_cast<Rec**>(&c->d_recs2), &c->recs2_alloc, m);
     if (rc) return rc;
   }
-  Rec* sorted = reinterpret_cast<Rec*>(c->d_recs2) + c->seg_base;
+  Rec* sorted = reinterpret_cast<Rec*>(c->d_recs2) + seg_base;
   const uint32_t n_regions = 1u << c->np_bits;
   uint32_t tile_len = kPartTileMin;
-  while (tile_len < kPartTileMax && (unsigned long long)tile_len * kPartTilesWant < nr) tile_len <<= 1;
-  const uint32_t n_tiles = (uint32_t)((nr + tile_len - 1) / tile_len);
+  while (tile_len < kPartTileMax && (unsigned long long)tile_len * kPartTilesWant < m) tile_len <<= 1;
+  const uint32_t n_tiles = (uint32_t)((m + tile_len - 1) / tile_len);
   const unsigned long long hl = (unsigned long long)n_regions * n_tiles;
   rc = ensure_buf(c, &c->d_hist, &c->hist_alloc, hl);
   if (rc) return rc;
-  k_part_hist<<<n_tiles, 1024, 0, c->stream>>>(c->d_regs, nr, n_regions, n_tiles, tile_len, c->d_hist);
+  k_part_hist<<<n_tiles, 1024, 0, c->stream>>>(c->d_regs, m, n_regions, n_tiles, tile_len, c->d_hist);
   HIPCHK(c, hipGetLastError());
-  rc = exclusive_scan(c, c->d_hist, hl);
+  uint32_t* total = nullptr;
+  rc = exclusive_scan(c, c->d_hist, hl, &total);
   if (rc) return rc;
-  k_part_scatter<<<n_tiles, 1024, 0, c->stream>>>(recs, nr, n_regions, n_tiles, tile_len, c->d_hist, sorted);
+  k_part_scatter<<<n_tiles, 1024, 0, c->stream>>>(recs, c->d_regs, m, n_regions, n_tiles, tile_len, c->d_hist, sorted);
   HIPCHK(c, hipGetLastError());
   unsigned long long* st = c->d_starts + (size_t)c->n_segs * (n_regions + 1);
-  k_seg_starts<<<(n_regions + 1 + 255) / 256, 256, 0, c->stream>>>(c->d_hist, n_tiles, n_regions, c->seg_base, nr, st);
+  k_seg_starts<<<(n_regions + 1 + 255) / 256, 256, 0, c->stream>>>(c->d_hist, n_tiles, n_regions, seg_base, total, st);
   k_reduce<1><<<n_regions, 1024, 0, c->stream>>>(reinterpret_cast<const Rec*>(c->d_recs2), st, 1, ag);
   HIPCHK(c, hipGetLastError());
-  if (c->rec_cache) {
-    c->seg_base += nr;
-    ++c->n_segs;
+  if (c->rec_cache) ++c->n_segs;
+  if (c->debug) {
+    uint32_t nr = 0;
+    HIPCHK(c, hipMemcpyAsync(&nr, total, sizeof nr, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    fprintf(stderr, "[rsa] pass-1 launch: %llu lines -> %u records\n", (unsigned long long)m, nr);
   }
   return RSA_OK;
 }
@@ -1872,11 +1993,6 @@ int run_pass1(rsa_ctx* c, int classify, const rsa_tuple* T, const uint32_t* TS, 
   if (rc) return rc;
   c->ev_used = 0;
   if (n > 0x7FFFFFFFull) return fail(c, RSA_ERR_ARG, "batch larger than 2^31 tuples: split it");
-  if (classify && !gout) {
-    rc = ensure_buf(c, &c->d_gscratch, &c->gscratch_alloc, n);
-    if (rc) return rc;
-    gout = c->d_gscratch;
-  }
   // the records of a job's only batch are kept for its recount
   if (c->pass1_calls++ == 0) {
     rc = ensure_buf(c, reinterpret_cast<Rec**>(&c->d_recs2), &c->recs2_alloc, n);
@@ -1884,10 +2000,15 @@ int run_pass1(rsa_ctx* c, int classify, const rsa_tuple* T, const uint32_t* TS, 
     c->rec_cache = true;
     c->cache_T = T;
     c->cache_n = n;
-    c->seg_base = 0;
     c->n_segs = 0;
   } else {
     c->rec_cache = false;
+  }
+  uint32_t* gh = nullptr;
+  if (classify) {
+    rc = ensure_buf(c, &c->d_gh, &c->gh_alloc, n);
+    if (rc) return rc;
+    gh = c->d_gh;
   }
   auto launch = [&](uint64_t a, uint64_t m) -> int {
     if (m == 0) return RSA_OK;
@@ -1895,13 +2016,20 @@ int run_pass1(rsa_ctx* c, int classify, const rsa_tuple* T, const uint32_t* TS, 
     const uint4* t = reinterpret_cast<const uint4*>(T) + a;
     const unsigned long long* o = reinterpret_cast<const unsigned long long*>(ORD) + a;
     HIPCHK(c, hipEventRecord(c->ev[c->ev_used], c->stream));
-    const int32_t* g = G ? G + a : gout + a;
     if (classify) {
-      const int rc2 = launch_classify(c, t, m, gout + a);
+      int rc2 = prepare_records(c, m);
+      if (rc2) return rc2;
+      Emit e;
+      e.gh = gh + a;
+      e.ts = TS + a;
+      e.ord = o;
+      e.recs = reinterpret_cast<Rec*>(c->d_recs);
+      e.regs = c->d_regs;
+      rc2 = launch_classify(c, t, m, gout ? gout + a : nullptr, &e);
       if (rc2) return rc2;
     }
     HIPCHK(c, hipEventRecord(c->ev[c->ev_used + 1], c->stream));
-    const int rc2 = launch_aggregate(c, t, TS + a, o, g, m);
+    const int rc2 = launch_aggregate(c, t, TS + a, o, G ? G + a : nullptr, classify ? gh + a : nullptr, a, m);
     if (rc2) return rc2;
     HIPCHK(c, hipEventRecord(c->ev[c->ev_used + 2], c->stream));
     c->ev_used += 3;
@@ -1983,7 +2111,7 @@ int rsa_ctx_destroy(rsa_ctx* c) {
   if (!c) return RSA_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->d_tail, c->d_tail_n, c->d_gscratch, c->d_stats, c->d_recs, c->d_recs2, c->d_regs, c->d_nrecs, c->d_starts, c->d_hist,
+  void* bufs[] = {c->d_tail, c->d_tail_n, c->d_gscratch, c->d_gh, c->d_stats, c->d_recs, c->d_recs2, c->d_regs, c->d_nrecs, c->d_starts, c->d_hist,
                   c->d_scan_sums, c->d_occ, c->d_entries, c->d_off,
                   c->d_img, c->d_resid,
                   c->d_slots, c->d_used, c->d_used_n, c->d_filter, c->d_flags, c->d_cursor, c->d_cidx,
@@ -2089,6 +2217,19 @@ int rsa_load_rules(rsa_ctx* c, const rsa_rule_entry* h_entries, uint32_t n_entri
 
 namespace {
 
+// A 16-bit-slot CHD table inside the image whose slot values are all < `limit`.
+bool table16_ok(const uint32_t* img, uint32_t words, const rsa_pht_table& t, uint32_t limit) {
+  if (t.n_slots == 0 || (uint64_t)t.slot_off + t.n_slots > 2ull * words || (t.disp_mask & (t.disp_mask + 1)) != 0 ||
+      (uint64_t)t.disp_off + t.disp_mask + 1 > 2ull * words || limit > 0xFFu)
+    return false;
+  const uint16_t* h = reinterpret_cast<const uint16_t*>(img);
+  for (uint32_t q = 0; q < t.n_slots; ++q) {
+    const uint32_t w = h[t.slot_off + q];
+    if (w != 0xFFFFu && (w & 0xFFu) >= limit) return false;
+  }
+  return true;
+}
+
 // A CHD table inside the image whose slot values are all < `limit`.
 bool table_ok(const uint32_t* img, uint32_t words, const rsa_pht_table& t, uint32_t limit) {
   if (t.n_slots == 0 || (uint64_t)t.slot_off + t.n_slots > words || (t.disp_mask & (t.disp_mask + 1)) != 0 ||
@@ -2156,7 +2297,9 @@ int rsa_load_index(rsa_ctx* c, const uint32_t* img, uint32_t words, const rsa_ru
           rsa_pht_mask M;
           memcpy(&M, img + h.mask_off + (size_t)mw * m, sizeof M);
           if (M.side > 1) return fail(c, RSA_ERR_ARG, "list %u mask %u: side must be 0 or 1", l, m);
-          if (!table_ok(img, words, M.table, h.n_bitmaps))
+          if (M.slot_bits != 16 && M.slot_bits != 32)
+            return fail(c, RSA_ERR_ARG, "list %u mask %u: slot_bits must be 16 or 32", l, m);
+          if (M.slot_bits == 16 ? !table16_ok(img, words, M.table, h.n_bitmaps) : !table_ok(img, words, M.table, h.n_bitmaps))
             return fail(c, RSA_ERR_ARG, "list %u mask %u: table outside the image or bitmap out of range", l, m);
         }
       }
@@ -2299,7 +2442,7 @@ int rsa_classify_only(rsa_ctx* c, const rsa_tuple* T, uint64_t n, int32_t* gout)
   if (!T || !gout) return fail(c, RSA_ERR_ARG, "null tuple/gid pointer");
   if (!c->d_flags) return fail(c, RSA_ERR_STATE, "ctx not initialised");
   if (n > 0x7FFFFFFFull) return fail(c, RSA_ERR_ARG, "batch larger than 2^31 tuples");
-  return launch_classify(c, reinterpret_cast<const uint4*>(T), n, gout);
+  return launch_classify(c, reinterpret_cast<const uint4*>(T), n, gout, nullptr);
 }
 
 int rsa_aggregate_gids(rsa_ctx* c, const rsa_tuple* T, const uint32_t* TS, const uint64_t* ORD, const int32_t* G,
