@@ -265,6 +265,23 @@ int rsa_import(rsa_ctx *ctx, int which, const rsa_conn_record *d_in, uint64_t n)
  * zeroes them after the read. */
 int rsa_stats(rsa_ctx *ctx, uint64_t *h_out4, int reset);
 
+/* Shadowed-rule analysis (preprosess_access_lists.py:508-521): for every rule i
+ * of one access list, the smallest j < i whose rule CONTAINS rule i
+ * (FirewallRule.__contains__, firewallrule.py:128-174: equal action, protocol
+ * 'ip' or equal, src and dst networks contained, ports "no port" or equal), or
+ * -1.  Rules are given in list order; one port per side (the preprocessors'
+ * expansion, SURVEY.md trap 3).  Host buffers in and out. */
+typedef struct rsa_shadow_rule {
+  uint32_t src_lo, src_span;  /* IPv4 network [lo, lo + span]                      */
+  uint32_t dst_lo, dst_span;
+  int32_t sport, dport;       /* one port, or -1 = NO_PORT                         */
+  uint16_t proto;             /* protocol id, 0 = 'ip'                              */
+  uint8_t action;             /* 1 permit, 0 deny                                   */
+  uint8_t v4;                 /* 1: both addresses IPv4 (else never contains/contained) */
+  uint32_t reserved;
+} rsa_shadow_rule;
+int rsa_shadowed(rsa_ctx *ctx, const rsa_shadow_rule *h_rules, uint32_t n, int32_t *h_cover);
+
 /* Synchronise the ctx stream (tests, host hand-off). */
 int rsa_sync(rsa_ctx *ctx);
 

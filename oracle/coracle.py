@@ -169,6 +169,19 @@ def classify(R, list_of, proto_of, src, dst, sport, dport):
     return gid, int(evals.value)
 
 
+def shadow(R, host, acl):
+    """preprosess_access_lists.py:508-521 for one ACL: per rule the first rule
+    above it that contains it (list-local index) or -1."""
+    beg = R.base[(host, acl)]
+    ends = sorted(b for b in R.base.values() if b > beg)
+    end = ends[0] if ends else R.n_rules
+    cover = np.empty(end - beg, np.int32)
+    lib().rsa_oracle_shadow(ctypes.c_uint32(beg), ctypes.c_uint32(end), _p(R.action), _p(R.proto), _p(R.v4src),
+                            _p(R.v4dst), _p(R.src), _p(R.dst), _p(R.src_len), _p(R.dst_len), _p(R.sp_off),
+                            _p(R.sp_len), _p(R.dp_off), _p(R.dp_len), _p(R.ports), _p(cover))
+    return cover
+
+
 def reduce(R, gid, flags, pspell, src, dst, sport, dport, ts, order, cap):
     n = len(gid)
     nr = R.n_rules

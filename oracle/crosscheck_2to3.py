@@ -21,7 +21,10 @@ box).  For each fixture case it:
 5. checks the oracle (``oracle.pipeline``) gives the same mapper text and the
    same reducer text, and writes the case under ``tests/golden/<case>/``:
    ``db.json`` (input), ``log.txt`` (input), ``params.json``,
-   ``mapper.sha256`` and ``report.txt`` (outputs of the converted reference).
+   ``mapper.sha256`` and ``report.txt`` (outputs of the converted reference);
+6. runs the converted ``postprocess_ruleset_analysis.py`` on the report in
+   Hadoop's output form (``hadoop.txt``, input) and keeps its stdout
+   (``postprocess.txt``).
 
 Usage: ``python3 oracle/crosscheck_2to3.py [--cases NAME ...]``.
 """
@@ -115,6 +118,40 @@ def run_reference(work, db_json, log_text, host, cap):
     return m.stdout.decode('latin-1'), r.stdout.decode('latin-1')
 
 
+def run_postprocess(work, hadoop_text):
+    """The converted postprocess_ruleset_analysis.py (``-f`` the Hadoop-form
+    reducer output) in a work dir prepared by run_reference (same DB)."""
+    _convert(os.path.join(REF, 'postprocess_ruleset_analysis.py'), os.path.join(work, 'postprocess.py'))
+    with open(os.path.join(work, 'config.py')) as f:
+        cfg = f.read()
+    cfg = cfg.replace("ACCESSLIST_DATABASE = './input/{0}'.format(ACCESSLIST_DATABASE_FILENAME)",
+                      "ACCESSLIST_DATABASE = ACCESSLIST_DATABASE_FILENAME")
+    with open(os.path.join(work, 'config.py'), 'w') as f:
+        f.write(cfg)
+    with open(os.path.join(work, 'hadoop.txt'), 'w', encoding='latin-1', newline='') as f:
+        f.write(hadoop_text)
+    env = dict(os.environ, PYTHONIOENCODING='latin-1', LC_ALL='C', PYTHONHASHSEED='0')
+    r = subprocess.run([sys.executable, 'postprocess.py', '-f', 'hadoop.txt'], cwd=work, env=env,
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+    if r.returncode != 0:
+        raise RuntimeError('reference postprocessor failed: %s' % r.stderr.decode('latin-1')[-2000:])
+    return r.stdout.decode('latin-1')
+
+
+def hadoop_part(report_text):
+    """The Hadoop TextOutputFormat form (line + '\t\n') of a reducer report
+    without its leading noise records (what a reduce partition that received
+    no empty mapper records writes; the noise entry would stop the
+    postprocessor at postprocess_ruleset_analysis.py:96)."""
+    lines = report_text.split('\n')[:-1]
+    if not any(': access-list ' in l for l in lines):
+        return ''                  # no rule block: the postprocessor has nothing to attach (IndexError at :96)
+    k = 0
+    while k < len(lines) and lines[k] != '':
+        k += 1
+    return ''.join(l + '\t\n' for l in lines[k:])
+
+
 def oracle_db(dbj):
     from oracle.firewallrule import FirewallRule
     acls = {}
@@ -171,6 +208,8 @@ def main():
         db, text, cap = make()
         with tempfile.TemporaryDirectory(prefix='rsa_xref_') as work:
             ref_map, ref_red = run_reference(work, db, text, 'fw1', cap)
+            hadoop = hadoop_part(ref_red)
+            ref_post = run_postprocess(work, hadoop) if hadoop else None
         acls, fws = oracle_db(db)
         o_map, _srt, o_red, _blocks = op.run_pipeline(text, 'fw1', acls, fws, cap=cap)
         o_red_text = ''.join(l + '\n' for l in o_red)
@@ -190,6 +229,11 @@ def main():
             f.write(ref_red)
         with open(os.path.join(out, 'mapper.sha256'), 'w') as f:
             f.write(hashlib.sha256(ref_map.encode('latin-1')).hexdigest() + '\n')
+        if ref_post is not None:
+            with open(os.path.join(out, 'hadoop.txt'), 'w', encoding='latin-1', newline='') as f:
+                f.write(hadoop)
+            with open(os.path.join(out, 'postprocess.txt'), 'w', encoding='latin-1', newline='') as f:
+                f.write(ref_post)
         with open(os.path.join(out, 'params.json'), 'w') as f:
             json.dump({'host': 'fw1', 'cap': cap, 'source': 'lib2to3-converted reference, oracle/crosscheck_2to3.py'},
                       f, sort_keys=True)

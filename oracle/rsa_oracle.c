@@ -202,3 +202,42 @@ done:
   free(ins);
   return rc;
 }
+
+/* preprosess_access_lists.py:508-521 over rules [beg, end): cover[k] = the first
+ * j in [beg, beg + k) with rule (beg + k) in rule j (FirewallRule.__contains__,
+ * firewallrule.py:128-174, rule vs rule), or -1.  A plain double loop. */
+static int rule_in_rule(const rules_t *R, uint32_t j, uint32_t i) {
+  if (R->action[j] != R->action[i]) return 0;                   /* :146 */
+  if (R->proto[j] != 0 && R->proto[j] != R->proto[i]) return 0; /* :150 */
+  if (!R->v4src[j] || !R->v4src[i] || !R->v4dst[j] || !R->v4dst[i]) return 0;
+  if (!((uint64_t)R->src[i] >= R->src[j] && (uint64_t)R->src[i] + R->src_len[i] <= (uint64_t)R->src[j] + R->src_len[j]))
+    return 0;                                                    /* :154 */
+  if (!((uint64_t)R->dst[i] >= R->dst[j] && (uint64_t)R->dst[i] + R->dst_len[i] <= (uint64_t)R->dst[j] + R->dst_len[j]))
+    return 0;                                                    /* :158 */
+  const int32_t *sj = R->ports + R->sp_off[j], *si = R->ports + R->sp_off[i];
+  if (!(R->sp_len[j] == 1 && sj[0] == -1))                      /* :162-165 */
+    for (uint32_t q = 0; q < R->sp_len[i]; ++q)
+      if (!port_in(sj, R->sp_len[j], (uint32_t)si[q])) return 0;
+  const int32_t *dj = R->ports + R->dp_off[j], *di = R->ports + R->dp_off[i];
+  if (!(R->dp_len[j] == 1 && dj[0] == -1))                      /* :168-171 */
+    for (uint32_t q = 0; q < R->dp_len[i]; ++q)
+      if (!port_in(dj, R->dp_len[j], (uint32_t)di[q])) return 0;
+  return 1;
+}
+
+void rsa_oracle_shadow(uint32_t beg, uint32_t end, const uint8_t *action, const uint8_t *proto, const uint8_t *v4src,
+                       const uint8_t *v4dst, const uint32_t *rsrc, const uint32_t *rdst, const uint64_t *src_len,
+                       const uint64_t *dst_len, const uint32_t *sp_off, const uint32_t *sp_len, const uint32_t *dp_off,
+                       const uint32_t *dp_len, const int32_t *ports, int32_t *cover) {
+  rules_t R = {action, proto, v4src, v4dst, rsrc, rdst, src_len, dst_len, sp_off, sp_len, dp_off, dp_len, ports};
+#pragma omp parallel for schedule(dynamic, 16)
+  for (int64_t k = 0; k < (int64_t)(end - beg); ++k) {
+    const uint32_t i = beg + (uint32_t)k;
+    cover[k] = -1;
+    for (uint32_t j = beg; j < i; ++j)
+      if (rule_in_rule(&R, j, i)) {
+        cover[k] = (int32_t)(j - beg);
+        break;
+      }
+  }
+}

@@ -246,12 +246,31 @@ def _host_of(path):
 def run_main(argv=None):
     import argparse
     ap = argparse.ArgumentParser(description='Fused GPU ruleset analysis: logs -> reducer report')
-    ap.add_argument('--db', required=True, help='accesslists.db (shelve) or .json')
+    src = ap.add_mutually_exclusive_group(required=True)
+    src.add_argument('--db', help='accesslists.db (shelve) or .json')
+    src.add_argument('--fortigate', help='a FortiGate config: the rule DB preprosess_fortigate_acl.py would store '
+                                         '(restated, ruleset-analysis_amd/fortigate.py)')
     ap.add_argument('--cap', type=int, default=1000, help='MAX_NUMBER_OF_CONNECTIONS_PER_RULE')
     ap.add_argument('--host', help='firewall host for every input (default: parent directory name)')
-    ap.add_argument('logs', nargs='+')
+    ap.add_argument('--hadoop-output', action='store_true',
+                    help="print the report as Hadoop streaming stores it (every line + '\\t\\n', the form "
+                         'postprocess_ruleset_analysis.py reads)')
+    ap.add_argument('--postprocess', action='store_true',
+                    help='print the postprocess_ruleset_analysis.py report (hit counts, zero-hit ACL lines, '
+                         'connection lists) instead of the reducer report')
+    ap.add_argument('--shadowed', action='store_true',
+                    help='also log the rules shadowed by a more generic rule above them '
+                         '(preprosess_access_lists.py:508-521) to stderr, computed on the GPU')
+    ap.add_argument('logs', nargs='*')
     args = ap.parse_args(argv)
-    db = acldb.load(args.db)
+    if args.db:
+        db = acldb.load(args.db)
+    else:
+        from . import fortigate
+        with open(args.fortigate, encoding='latin-1') as f:
+            text = f.read()
+        db = fortigate.build_db(text, timestamp=os.stat(args.fortigate).st_mtime,
+                                log=lambda m: sys.stderr.write(m))
     inputs = []
     for path in args.logs:
         with open(path, 'rb') as f:
@@ -266,6 +285,25 @@ def run_main(argv=None):
             lines.append(text[start:i + 1])
             start = i + 1
         inputs.append((args.host or _host_of(path), lines))
-    out, _res = analyze(inputs, db, cap=args.cap)
+    engine = None
+    if args.shadowed:
+        from .engine import Engine
+        from .shadow import shadow_messages
+        engine = Engine(0)
+        for host in db.accesslists:
+            for m in shadow_messages(engine, {a: e['rules'] for a, e in db.accesslists[host].items()}):
+                sys.stderr.write('INFO - ' + m + '\n')
+    if not inputs:
+        return 0
+    out, _res = analyze(inputs, db, cap=args.cap, engine=engine)
+    if args.postprocess or args.hadoop_output:
+        from .postprocess import hadoop_output, postprocess
+        k = out.index('') if '' in out else len(out)   # the noise records of the empty mapper records
+        hadoop = hadoop_output(out[k:]) if args.postprocess else hadoop_output(out)
+        if args.postprocess:
+            _write(''.join(l + '\n' for l in postprocess(db.accesslists, hadoop)))
+        else:
+            _write(hadoop)
+        return 0
     _write(''.join(l + '\n' for l in out))
     return 0

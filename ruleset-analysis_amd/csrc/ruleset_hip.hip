@@ -630,48 +630,75 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t* sh, uint3
   return before + x - v;
 }
 
-// Where pass 1 puts its per-line results (k_classify / k_tail with kEmit), all
-// indexed by the line (no appends, so no atomics or workgroup barriers in the
-// classifier): the gid|hit word for the per-rule counters (k_count), and for
-// every hit + BUILT line below its rule's filter bound a 32-B record plus its
-// table region (0xFFFF: no record) for the region sort of the table reduction
-// (connlist-reducer.py:146-176).
+// Where pass 1 puts its per-line results (k_classify / k_tail with kEmit),
+// without appends to shared cursors (no atomics or workgroup barriers in the
+// classifier): the line's gid|hit word for the per-rule counters (k_count);
+// for every hit + BUILT line below its rule's filter bound a 32-B record and
+// its table region (connlist-reducer.py:146-176), compacted per 64-line
+// window (a wave's lines): window w holds its wcnt[w] records in slots
+// [64 w, 64 w + wcnt[w]) of the line-indexed record arrays.
+constexpr uint32_t kWin = 64;
 struct Emit {
   uint32_t* gh;                         // gid | hit << 31, 0xFFFFFFFF: no rule
   const uint32_t* ts;
   const unsigned long long* ord;
-  Rec* recs;                            // line-indexed, written only where regs != 0xFFFF
-  uint16_t* regs;                       // line-indexed region or kNoRegion
+  Rec* recs;                            // window-compacted records
+  uint16_t* regs;                       // their regions
+  uint32_t* wcnt;                       // records per 64-line window
 };
-constexpr uint32_t kNoRegion = 0xFFFFu;
 
-__device__ __forceinline__ void emit_line(uint32_t i, uint4 t, uint32_t gid, const Agg& A, const Emit& E) {
+// The record of one line, or false (need).
+__device__ __forceinline__ bool make_rec(uint32_t i, uint4 t, uint32_t gid, const Agg& A, const Emit& E, Rec& r) {
+  const uint32_t flags = (t.w >> 16) & 0xFFu;
+  bool need = gid != kNoGid && (flags & RSA_F_HIT) && (flags & RSA_F_BUILT) && A.cap > 0 && !(A.skip & 2u);
+  if (!need) return false;
+  const unsigned long long o = E.ord[i];
+  if (o > A.filter[gid]) return false;   // exact skip: capped with threshold <= filter < order
+  conn_key(t, gid, r.kA, r.kB);
+  r.order = o;
+  r.ts = E.ts[i];
+  r.region = key_region(A, slot_hash(r.kA, r.kB));
+  return true;
+}
+
+// Emission for one wave of classified lines (wave-uniform call; lanes with
+// !in do nothing).  i = the lane's line, lines of a wave are i - lane .. + 63.
+__device__ __forceinline__ void emit_wave(uint32_t i, uint32_t n, bool in, uint4 t, uint32_t gid, const Agg& A,
+                                          const Emit& E) {
+  const uint32_t flags = (t.w >> 16) & 0xFFu;
+  const bool matched = in && gid != kNoGid;
+  const bool hit = matched && (flags & RSA_F_HIT);
+  if (in) E.gh[i] = matched ? (gid | (hit ? 0x80000000u : 0u)) : 0xFFFFFFFFu;
+  Rec r;
+  const bool need = in && make_rec(i, t, gid, A, E, r);
+  const unsigned long long mask = __ballot(need);
+  const uint32_t lane = __lane_id();
+  const uint32_t w0 = i - lane;   // the window's first line (waves cover aligned 64-line windows)
+  if (need) {
+    const uint32_t slot = w0 + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+    E.recs[slot] = r;
+    E.regs[slot] = (uint16_t)r.region;
+  }
+  if (lane == 0 && w0 < n) E.wcnt[w0 / kWin] = (uint32_t)__popcll(mask);
+}
+
+// Emission of one deferred line (k_tail): appended to its window's records.
+__device__ __forceinline__ void emit_one(uint32_t i, uint4 t, uint32_t gid, const Agg& A, const Emit& E) {
   const uint32_t flags = (t.w >> 16) & 0xFFu;
   const bool matched = gid != kNoGid;
   const bool hit = matched && (flags & RSA_F_HIT);
   E.gh[i] = matched ? (gid | (hit ? 0x80000000u : 0u)) : 0xFFFFFFFFu;
-  bool need = hit && (flags & RSA_F_BUILT) && A.cap > 0 && !(A.skip & 2u);
-  unsigned long long o = 0;
-  if (need) {
-    o = E.ord[i];
-    need = o <= A.filter[gid];   // exact skip: capped with threshold <= filter < order
-  }
-  uint32_t region = kNoRegion;
-  if (need) {
-    Rec r;
-    conn_key(t, gid, r.kA, r.kB);
-    r.order = o;
-    r.ts = E.ts[i];
-    r.region = key_region(A, slot_hash(r.kA, r.kB));
-    region = r.region;
-    E.recs[i] = r;
-  }
-  E.regs[i] = (uint16_t)region;
+  Rec r;
+  if (!make_rec(i, t, gid, A, E, r)) return;
+  const uint32_t w = i / kWin;
+  const uint32_t slot = w * kWin + atomicAdd(&E.wcnt[w], 1u);   // < 64: a window has 64 lines
+  E.recs[slot] = r;
+  E.regs[slot] = (uint16_t)r.region;
 }
 
 // Pass 1a — first-match classification (mapper.py:159-189): gid or RSA_NO_RULE
 // per tuple into gout (nullable), index image staged in LDS when kImg > 0;
-// with kEmit the line's counter word and table record (emit_line).  Lines
+// with kEmit the line's counter word and table record (emit_wave).  Lines
 // whose index candidate failed verification kAttempts times go to `tail`
 // (k_tail scans and emits them exactly).
 template <int kImg, bool kEmit>
@@ -707,7 +734,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kIm
       if (defer) tail[pos] = (uint32_t)i;
     }
     if (gout && in && !defer) gout[i] = (int32_t)gid;
-    if (kEmit && in && !defer) emit_line(i, t, gid, A, E);
+    if (kEmit) emit_wave(i, n32, in && !defer, t, gid, A, E);
   }
 }
 
@@ -726,7 +753,7 @@ __global__ __launch_bounds__(kBlock) void k_tail(const uint4* __restrict__ T, in
     const bool valid = in && (((t.w >> 16) & 0xFFu) & RSA_F_VALID);
     const uint32_t gid = classify_wave<true>(t, valid, R, R.img, flags);
     if (gout && in) gout[i] = (int32_t)gid;
-    if (kEmit && in) emit_line((uint32_t)i, t, gid, A, E);
+    if (kEmit && in) emit_one((uint32_t)i, t, gid, A, E);
   }
 }
 
@@ -815,13 +842,13 @@ __global__ __launch_bounds__(1024) void k_count(const uint32_t* __restrict__ gh,
 constexpr int kAggU = 4;
 // Pass 1b with the rule already known per line (rsa_aggregate_gids, the
 // reducer drop-in): per-rule counters (LDS histogram when the rules fit) and
-// the line-indexed records of emit_line.
+// the window-compacted records of emit_wave.
 template <int kLds>
 __global__ __launch_bounds__(1024) void k_aggregate(const uint4* __restrict__ T, const uint32_t* __restrict__ TS,
                                                     const unsigned long long* __restrict__ ORD,
                                                     const int32_t* __restrict__ G, unsigned long long n,
                                                     uint32_t n_rules, Agg A, Rec* __restrict__ recs,
-                                                    uint16_t* __restrict__ regs) {
+                                                    uint16_t* __restrict__ regs, uint32_t* __restrict__ wcnt) {
   __shared__ uint32_t cnt[kLds > 0 ? 2 * kLds : 1];   // matches, hits
   const bool counters = !(A.skip & 1u);
   if (kLds > 0) {
@@ -859,18 +886,21 @@ __global__ __launch_bounds__(1024) void k_aggregate(const uint4* __restrict__ T,
         o = ORD[i];
         need = o <= A.filter[gid];
       }
-      if (!in) continue;
-      uint32_t region = kNoRegion;
+      need = need && in;
+      const unsigned long long mask = __ballot(need);
+      const uint32_t lane = __lane_id();
+      const unsigned long long w0 = i - lane;   // the wave's 64-line window
       if (need) {
         Rec r;
         conn_key(t, gid, r.kA, r.kB);
         r.order = o;
         r.ts = TS[i];
         r.region = key_region(A, slot_hash(r.kA, r.kB));
-        region = r.region;
-        recs[i] = r;
+        const unsigned long long slot = w0 + __popcll(mask & ((1ull << lane) - 1ull));
+        recs[slot] = r;
+        regs[slot] = (uint16_t)r.region;
       }
-      regs[i] = (uint16_t)region;
+      if (lane == 0 && w0 < n) wcnt[w0 / kWin] = (uint32_t)__popcll(mask);
     }
   }
   if (kLds > 0) {
@@ -883,17 +913,19 @@ __global__ __launch_bounds__(1024) void k_aggregate(const uint4* __restrict__ T,
   }
 }
 
-// Counting sort of the records by region.  Tiles of `tile` records (a power of
-// two between kPartTileMin and kPartTileMax, chosen per launch so that a small
-// batch still spreads over ~kPartTilesWant workgroups instead of a few dozen);
-// the histogram matrix is region-major (hist[region * n_tiles + tile]) so that
-// its exclusive scan gives every (region, tile) run its output offset.
-constexpr uint32_t kPartTileMin = 4096, kPartTileMax = 32768, kPartTilesWant = 1024;
+// Counting sort of the records by region.  The records are window-compacted
+// (window w's wcnt[w] records in slots 64 w ..), tiles are `tile` lines (a
+// power of two multiple of 64, chosen per launch so that a launch spreads
+// over ~kPartTilesWant workgroups, as few as keep the scatter's runs per
+// region long); the histogram matrix is region-major (hist[region * n_tiles +
+// tile]) so that its exclusive scan gives every (region, tile) run its output
+// offset.
+constexpr uint32_t kPartTileMin = 8192, kPartTileMax = 262144, kPartTilesWant = 512;
 constexpr int kMaxRegions = 4096;
 
-__global__ __launch_bounds__(1024) void k_part_hist(const uint16_t* __restrict__ regs, unsigned long long n,
-                                                    uint32_t n_regions, uint32_t n_tiles, uint32_t tile_len,
-                                                    uint32_t* __restrict__ hist) {
+__global__ __launch_bounds__(1024) void k_part_hist(const uint16_t* __restrict__ regs, const uint32_t* __restrict__ wcnt,
+                                                    unsigned long long n, uint32_t n_regions, uint32_t n_tiles,
+                                                    uint32_t tile_len, uint32_t* __restrict__ hist) {
   __shared__ uint32_t hcount[kMaxRegions];
   const uint32_t tile = blockIdx.x;
   for (uint32_t r = threadIdx.x; r < n_regions; r += blockDim.x) hcount[r] = 0;
@@ -901,17 +933,17 @@ __global__ __launch_bounds__(1024) void k_part_hist(const uint16_t* __restrict__
   const unsigned long long beg = (unsigned long long)tile * tile_len;
   const unsigned long long end = beg + tile_len < n ? beg + tile_len : n;
   for (unsigned long long j = beg + threadIdx.x; j < end; j += blockDim.x) {
-    const uint32_t r = regs[j];
-    if (r != kNoRegion) atomicAdd(&hcount[r], 1u);
+    if ((uint32_t)(j % kWin) >= wcnt[j / kWin]) continue;
+    atomicAdd(&hcount[regs[j]], 1u);
   }
   __syncthreads();
   for (uint32_t r = threadIdx.x; r < n_regions; r += blockDim.x) hist[(size_t)r * n_tiles + tile] = hcount[r];
 }
 
 __global__ __launch_bounds__(1024) void k_part_scatter(const Rec* __restrict__ recs, const uint16_t* __restrict__ regs,
-                                                       unsigned long long n, uint32_t n_regions, uint32_t n_tiles,
-                                                       uint32_t tile_len, const uint32_t* __restrict__ offs,
-                                                       Rec* __restrict__ out) {
+                                                       const uint32_t* __restrict__ wcnt, unsigned long long n,
+                                                       uint32_t n_regions, uint32_t n_tiles, uint32_t tile_len,
+                                                       const uint32_t* __restrict__ offs, Rec* __restrict__ out) {
   __shared__ uint32_t cur[kMaxRegions];
   const uint32_t tile = blockIdx.x;
   for (uint32_t r = threadIdx.x; r < n_regions; r += blockDim.x) cur[r] = offs[(size_t)r * n_tiles + tile];
@@ -919,9 +951,8 @@ __global__ __launch_bounds__(1024) void k_part_scatter(const Rec* __restrict__ r
   const unsigned long long beg = (unsigned long long)tile * tile_len;
   const unsigned long long end = beg + tile_len < n ? beg + tile_len : n;
   for (unsigned long long j = beg + threadIdx.x; j < end; j += blockDim.x) {
-    const uint32_t g = regs[j];
-    if (g == kNoRegion) continue;
-    out[atomicAdd(&cur[g], 1u)] = recs[j];
+    if ((uint32_t)(j % kWin) >= wcnt[j / kWin]) continue;
+    out[atomicAdd(&cur[regs[j]], 1u)] = recs[j];
   }
 }
 
@@ -1539,6 +1570,54 @@ __global__ __launch_bounds__(kBlock) void k_import(const rsa_conn_record* __rest
   }
 }
 
+// ---- Shadowed-rule analysis (preprosess_access_lists.py:508-521): cover[i] =
+// the smallest j < i with rule j containing rule i (firewallrule.py:128-174),
+// or -1.  One thread per rule i; candidate rules j are staged in LDS tiles of
+// kShadowTile, ascending; a workgroup stops once every thread has its cover
+// or the tiles pass its largest i.
+constexpr int kShadowTile = 1024;
+static_assert(sizeof(rsa_shadow_rule) == 32, "shadow rule layout");
+
+__device__ __forceinline__ bool rule_contains(const rsa_shadow_rule& a, const rsa_shadow_rule& b) {
+  if (a.action != b.action) return false;                         // :146
+  if (a.proto != 0 && a.proto != b.proto) return false;           // :150
+  if (!a.v4 || !b.v4) return false;                               // IPy: another version is never contained
+  const unsigned long long as = a.src_lo, bs = b.src_lo, ad = a.dst_lo, bd = b.dst_lo;
+  if (bs < as || bs + b.src_span > as + a.src_span) return false;   // :154 other.src in self.src
+  if (bd < ad || bd + b.dst_span > ad + a.dst_span) return false;   // :158
+  if (a.sport != -1 && b.sport != a.sport) return false;          // :162-165
+  if (a.dport != -1 && b.dport != a.dport) return false;          // :168-171
+  return true;
+}
+
+__global__ __launch_bounds__(1024) void k_shadow(const rsa_shadow_rule* __restrict__ rules, uint32_t n,
+                                                 int32_t* __restrict__ cover) {
+  __shared__ rsa_shadow_rule tile[kShadowTile];
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool in = i < n;
+  rsa_shadow_rule me = {};
+  if (in) me = rules[i];
+  int32_t found = -1;
+  const uint32_t last = min(n, (blockIdx.x + 1) * blockDim.x) - 1;   // largest i of the workgroup
+  for (uint32_t t0 = 0; t0 < last; t0 += kShadowTile) {
+    if (__syncthreads_and(!in || found >= 0)) break;   // workgroup-uniform
+    for (uint32_t q = threadIdx.x; q < kShadowTile; q += blockDim.x)
+      if (t0 + q < n) tile[q] = rules[t0 + q];
+    __syncthreads();
+    if (in && found < 0) {
+      const uint32_t lim = min((uint32_t)kShadowTile, i > t0 ? i - t0 : 0u);
+      for (uint32_t q = 0; q < lim; ++q) {
+        if (rule_contains(tile[q], me)) {
+          found = (int32_t)(t0 + q);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (in) cover[i] = found;
+}
+
 }  // namespace
 
 struct rsa_ctx {
@@ -1601,6 +1680,8 @@ struct rsa_ctx {
   unsigned long long recs2_alloc = 0;
   uint16_t* d_regs = nullptr;          // region of each record (the histogram pass reads only these)
   unsigned long long regs_alloc = 0;
+  uint32_t* d_wcnt = nullptr;          // records per 64-line window
+  unsigned long long wcnt_alloc = 0;
   unsigned long long* d_nrecs = nullptr;
   uint32_t* d_hist = nullptr;
   unsigned long long hist_alloc = 0;
@@ -1900,10 +1981,12 @@ int exclusive_scan(rsa_ctx* c, uint32_t* d, unsigned long long n, uint32_t** tot
   return RSA_OK;
 }
 
-// Line-indexed record buffers of a pass-1 launch over m lines.
+// Window-compacted record buffers of a pass-1 launch over m lines.
 int prepare_records(rsa_ctx* c, uint64_t m) {
-  int rc = ensure_buf(c, reinterpret_cast<Rec**>(&c->d_recs), &c->recs_alloc, m);
-  if (!rc) rc = ensure_buf(c, &c->d_regs, &c->regs_alloc, m);
+  const uint64_t mw = (m + kWin - 1) / kWin * kWin;
+  int rc = ensure_buf(c, reinterpret_cast<Rec**>(&c->d_recs), &c->recs_alloc, mw);
+  if (!rc) rc = ensure_buf(c, &c->d_regs, &c->regs_alloc, mw);
+  if (!rc) rc = ensure_buf(c, &c->d_wcnt, &c->wcnt_alloc, mw / kWin);
   return rc;
 }
 
@@ -1933,10 +2016,10 @@ int launch_aggregate(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsig
     Rec* recs = reinterpret_cast<Rec*>(c->d_recs);
     if (c->n_rules <= (uint32_t)kCnt) {
       k_aggregate<kCnt><<<grid_for_threads(c, units, 1024, 2), 1024, 0, c->stream>>>(t, ts, o, g, m, c->n_rules, ag,
-                                                                                     recs, c->d_regs);
+                                                                                     recs, c->d_regs, c->d_wcnt);
     } else {
       k_aggregate<0><<<grid_for_threads(c, units, 1024, 2), 1024, 0, c->stream>>>(t, ts, o, g, m, c->n_rules, ag,
-                                                                                  recs, c->d_regs);
+                                                                                  recs, c->d_regs, c->d_wcnt);
     }
   }
   HIPCHK(c, hipGetLastError());
@@ -1959,12 +2042,13 @@ int launch_aggregate(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsig
   const unsigned long long hl = (unsigned long long)n_regions * n_tiles;
   rc = ensure_buf(c, &c->d_hist, &c->hist_alloc, hl);
   if (rc) return rc;
-  k_part_hist<<<n_tiles, 1024, 0, c->stream>>>(c->d_regs, m, n_regions, n_tiles, tile_len, c->d_hist);
+  k_part_hist<<<n_tiles, 1024, 0, c->stream>>>(c->d_regs, c->d_wcnt, m, n_regions, n_tiles, tile_len, c->d_hist);
   HIPCHK(c, hipGetLastError());
   uint32_t* total = nullptr;
   rc = exclusive_scan(c, c->d_hist, hl, &total);
   if (rc) return rc;
-  k_part_scatter<<<n_tiles, 1024, 0, c->stream>>>(recs, c->d_regs, m, n_regions, n_tiles, tile_len, c->d_hist, sorted);
+  k_part_scatter<<<n_tiles, 1024, 0, c->stream>>>(recs, c->d_regs, c->d_wcnt, m, n_regions, n_tiles, tile_len, c->d_hist,
+                                                  sorted);
   HIPCHK(c, hipGetLastError());
   unsigned long long* st = c->d_starts + (size_t)c->n_segs * (n_regions + 1);
   k_seg_starts<<<(n_regions + 1 + 255) / 256, 256, 0, c->stream>>>(c->d_hist, n_tiles, n_regions, seg_base, total, st);
@@ -2025,6 +2109,7 @@ int run_pass1(rsa_ctx* c, int classify, const rsa_tuple* T, const uint32_t* TS, 
       e.ord = o;
       e.recs = reinterpret_cast<Rec*>(c->d_recs);
       e.regs = c->d_regs;
+      e.wcnt = c->d_wcnt;
       rc2 = launch_classify(c, t, m, gout ? gout + a : nullptr, &e);
       if (rc2) return rc2;
     }
@@ -2111,7 +2196,7 @@ int rsa_ctx_destroy(rsa_ctx* c) {
   if (!c) return RSA_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->d_tail, c->d_tail_n, c->d_gscratch, c->d_gh, c->d_stats, c->d_recs, c->d_recs2, c->d_regs, c->d_nrecs, c->d_starts, c->d_hist,
+  void* bufs[] = {c->d_tail, c->d_tail_n, c->d_gscratch, c->d_gh, c->d_stats, c->d_recs, c->d_recs2, c->d_regs, c->d_wcnt, c->d_nrecs, c->d_starts, c->d_hist,
                   c->d_scan_sums, c->d_occ, c->d_entries, c->d_off,
                   c->d_img, c->d_resid,
                   c->d_slots, c->d_used, c->d_used_n, c->d_filter, c->d_flags, c->d_cursor, c->d_cidx,
@@ -2537,6 +2622,31 @@ int rsa_import(rsa_ctx* c, int which, const rsa_conn_record* in, uint64_t n) {
   k_import<<<grid_for(c, n, 16), kBlock, 0, c->stream>>>(in, n, which, agg_of(c));
   HIPCHK(c, hipGetLastError());
   return RSA_OK;
+}
+
+int rsa_shadowed(rsa_ctx* c, const rsa_shadow_rule* h_rules, uint32_t n, int32_t* h_cover) {
+  if (!c || (n && (!h_rules || !h_cover))) return fail(c, RSA_ERR_ARG, "null argument");
+  if (n == 0) return RSA_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  rsa_shadow_rule* d_rules = nullptr;
+  int32_t* d_cover = nullptr;
+  HIPCHK(c, hipMalloc(&d_rules, (size_t)n * sizeof(rsa_shadow_rule)));
+  if (hipMalloc(&d_cover, (size_t)n * sizeof(int32_t)) != hipSuccess) {
+    hipFree(d_rules);
+    return fail(c, RSA_ERR_HIP, "hipMalloc of the cover array failed");
+  }
+  int rc = RSA_OK;
+  hipError_t e = hipMemcpyAsync(d_rules, h_rules, (size_t)n * sizeof(rsa_shadow_rule), hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) {
+    k_shadow<<<(n + 1023) / 1024, 1024, 0, c->stream>>>(d_rules, n, d_cover);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(h_cover, d_cover, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess) rc = fail(c, RSA_ERR_HIP, "rsa_shadowed: %s", hipGetErrorString(e));
+  hipFree(d_rules);
+  hipFree(d_cover);
+  return rc;
 }
 
 int rsa_stats(rsa_ctx* c, uint64_t* h_out, int reset) {

@@ -68,6 +68,7 @@ SYMBOLS = {
     'rsa_stats': (I32, [P, PU64, I32]),
     'rsa_export': (I32, [P, I32, P, U64, PU64]),
     'rsa_import': (I32, [P, I32, P, U64]),
+    'rsa_shadowed': (I32, [P, P, U32, P]),
     'rsa_sync': (I32, [P]),
 }
 

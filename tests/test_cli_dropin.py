@@ -59,3 +59,17 @@ def test_mapper_unknown_host(tmp_path):
                        input=b'', stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=600)
     assert m.returncode == 1
     assert m.stdout == b'Firewall nosuchfw not present in data structure. Aborting.\n'
+
+
+@pytest.mark.parametrize('case', ['small_200r', 'multi_acl'])
+def test_fused_run_postprocess_cli(tmp_path, case):
+    """rsa_run.py --postprocess prints what postprocess_ruleset_analysis.py
+    prints for the job's Hadoop output (golden: the converted reference)."""
+    text, report, sha, params, logfile = _setup(tmp_path, case)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, 'rsa_run.py'), '--db', 'accesslists.json', '--cap',
+                        str(params['cap']), '--postprocess', '--shadowed', str(logfile)], cwd=tmp_path,
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=600)
+    assert r.returncode == 0, r.stderr.decode()[-2000:]
+    with open(os.path.join(ROOT, 'tests', 'golden', case, 'postprocess.txt'), encoding='latin-1', newline='') as f:
+        assert r.stdout.decode('latin-1') == f.read()
+    assert b'INFO - Found rule which never gets hits' in r.stderr

@@ -247,3 +247,18 @@ def test_export_import_roundtrip(engine):
     got = engine.results(cap)
     f = ['gid', 'for_ip', 'to_ip', 'to_port', 'pspell', 'count', 'first', 'last', 'min_order']
     assert np.array_equal(np.sort(got.records[f], order=f), np.sort(ref.records[f], order=f))
+
+
+def test_cfg2_shape_20m_lines(engine):
+    """BASELINE config 2's shape (one ACL of 1k expanded rules, no catch-all
+    permit) at 20M lines, cap 1000, against the C oracle."""
+    res, ref = _gpu_vs_oracle(engine, 1000, 20_000_000, 1000, seed=2, broad=False)
+    assert int(res.matches.sum()) > 10_000_000
+
+
+def test_cfg5_shape_zipf_multi_acl_10m_lines(engine):
+    """BASELINE config 5's shape: 4 interface ACLs x 2.5k rules, Zipf 1.1
+    traffic, cap 1000 engaged, 10M lines, shuffled input order."""
+    res, ref = _gpu_vs_oracle(engine, 2500, 10_000_000, 1000, seed=5, zipf=1.1,
+                              interfaces=('outside', 'partner', 'vpn', 'extranet'), broad=False, shuffle=True)
+    assert (ref['n_conns'] >= 1000).sum() > 20          # the cap is engaged on many rules

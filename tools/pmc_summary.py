@@ -36,16 +36,20 @@ def main():
     # every pass-1 launch of every slice: classification, deferred tails,
     # aggregation (record append, region histogram, region scatter, per-region
     # reduction) -- the kernels bracketed by the pass-1 HIP events
-    kinds = ('k_classify', 'k_tail', 'k_aggregate', 'k_part_hist', 'k_part_scatter', 'k_seg_starts', 'k_reduce<1>')
-    pick = lambda name: any(k in name for k in kinds)
+    kinds = ('k_classify', 'k_tail', 'k_count', 'k_aggregate', 'k_part_hist', 'k_scan_blocks', 'k_scan_sums',
+             'k_scan_add', 'k_part_scatter', 'k_seg_starts', 'k_reduce<1>')
+    # pass-1 launches only: the classifier instantiated with emission (the
+    # classify-only launches of bench's untimed checks are excluded)
+    pick = lambda name: any(k in name for k in kinds) and not ('k_classify' in name and 'false>' in name) and \
+        not ('k_tail' in name and 'false>' in name)
     fk = [v for d, v in sorted(f.items()) if pick(fn[d])]
     wk = [v for d, v in sorted(w.items()) if pick(wn[d])]
     read = 2 * 1024 * sum(fk) / steps
     write = 1024 * sum(wk) / steps
     split = {}
     for k in kinds:
-        split[k] = {'read_bytes_per_step': 2 * 1024 * sum(v for d, v in f.items() if k in fn[d]) / steps,
-                    'write_bytes_per_step': 1024 * sum(v for d, v in w.items() if k in wn[d]) / steps}
+        split[k] = {'read_bytes_per_step': 2 * 1024 * sum(v for d, v in f.items() if k in fn[d] and pick(fn[d])) / steps,
+                    'write_bytes_per_step': 1024 * sum(v for d, v in w.items() if k in wn[d] and pick(wn[d])) / steps}
     res = {'hbm_bytes_per_step': read + write, 'read_bytes_per_step': read, 'write_bytes_per_step': write,
            'lines_per_step': lines, 'steps_seen': steps, 'bytes_per_line': (read + write) / lines,
            'kernels': split,
