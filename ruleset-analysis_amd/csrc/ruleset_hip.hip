@@ -915,13 +915,19 @@ __global__ __launch_bounds__(1024) void k_aggregate(const uint4* __restrict__ T,
 
 // Counting sort of the records by region.  The records are window-compacted
 // (window w's wcnt[w] records in slots 64 w ..), tiles are `tile` lines (a
-// power of two multiple of 64, chosen per launch so that a launch spreads
-// over ~kPartTilesWant workgroups, as few as keep the scatter's runs per
-// region long); the histogram matrix is region-major (hist[region * n_tiles +
+// power of two multiple of 64, chosen per launch as the largest that still
+// gives >= kPartTilesWant workgroups, capped at kPartTileMax so the scatter's
+// runs per region stay ~10 records); the histogram matrix is region-major (hist[region * n_tiles +
 // tile]) so that its exclusive scan gives every (region, tile) run its output
 // offset.
-constexpr uint32_t kPartTileMin = 8192, kPartTileMax = 262144, kPartTilesWant = 512;
+constexpr uint32_t kPartTileMin = 8192, kPartTileMax = 262144, kPartTilesWant = 384;
 constexpr int kMaxRegions = 4096;
+
+// k_part_hist walks its tile kPartU windows per thread per iteration with
+// every load issued before the LDS atomics (one outstanding load per wave
+// left it latency-bound).  A wave's lanes cover one 64-slot window, so the
+// window's record count is a wave-uniform load.
+constexpr int kPartU = 4;
 
 __global__ __launch_bounds__(1024) void k_part_hist(const uint16_t* __restrict__ regs, const uint32_t* __restrict__ wcnt,
                                                     unsigned long long n, uint32_t n_regions, uint32_t n_tiles,
@@ -932,9 +938,18 @@ __global__ __launch_bounds__(1024) void k_part_hist(const uint16_t* __restrict__
   __syncthreads();
   const unsigned long long beg = (unsigned long long)tile * tile_len;
   const unsigned long long end = beg + tile_len < n ? beg + tile_len : n;
-  for (unsigned long long j = beg + threadIdx.x; j < end; j += blockDim.x) {
-    if ((uint32_t)(j % kWin) >= wcnt[j / kWin]) continue;
-    atomicAdd(&hcount[regs[j]], 1u);
+  for (unsigned long long base = beg + threadIdx.x; base < end; base += (unsigned long long)blockDim.x * kPartU) {
+    uint32_t rg[kPartU];
+    bool live[kPartU];
+#pragma unroll
+    for (int k = 0; k < kPartU; ++k) {
+      const unsigned long long j = base + (unsigned long long)k * blockDim.x;
+      live[k] = j < end && (uint32_t)(j % kWin) < wcnt[j / kWin];
+      rg[k] = live[k] ? regs[j] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kPartU; ++k)
+      if (live[k]) atomicAdd(&hcount[rg[k]], 1u);
   }
   __syncthreads();
   for (uint32_t r = threadIdx.x; r < n_regions; r += blockDim.x) hist[(size_t)r * n_tiles + tile] = hcount[r];
@@ -1003,15 +1018,21 @@ __global__ __launch_bounds__(1024) void k_scan_add(uint32_t* __restrict__ a, uns
 
 // One workgroup per region: LDS aggregation of the region's records in rounds
 // (a round takes at most as many records as the LDS table has free entries
-// below 3/4 load, so it can never overflow; the table is flushed once it is
-// half full and at the end), each flush merging every LDS entry into the
+// below 3/4 load, so it can never overflow; the table is flushed once fewer than
+// 512 free entries remain below that load, and at the end), each flush merging every LDS entry into the
 // region's slots.  Only this workgroup touches the region during the kernel:
 // existing keys are found through the region's occupancy bitmap (slots
 // occupied before this flush hold published keys; a slot claimed during this
 // flush belongs to a DIFFERENT key, since the keys of one flush are distinct)
 // and updated with plain loads and stores; a new key claims a free slot with
 // an LDS atomic on the bitmap copy and writes the whole slot.
-constexpr int kRedE = 2048;                 // LDS hash entries (a multiple of the 1024-thread block)
+// LDS hash entries (a multiple of the 1024-thread block): 3072 (108 KiB) for
+// pass 1, 2048 for the sparser pass-2 recount — one workgroup per CU either way.
+#ifndef RSA_RED1
+#define RSA_RED1 3072
+#endif
+template <int kPass>
+constexpr int kRedE = kPass == 1 ? RSA_RED1 : 2048;
 constexpr int kRegionMaxBits = 16;          // region <= 65536 slots (bitmap copy 8 KiB)
 
 // kPass 1: the pass-1 reduction above.  kPass 2: the cap recount
@@ -1021,12 +1042,17 @@ constexpr int kRegionMaxBits = 16;          // region <= 65536 slots (bitmap cop
 // region's records may lie in several segments (one per pass-1 launch):
 // starts[s * (n_regions + 1) + r] .. starts[s * (n_regions + 1) + r + 1].
 constexpr int kMaxSegs = 16;
+constexpr int kHotTries = 2, kHotMin = 8;
+__device__ __forceinline__ unsigned long long readlane64(unsigned long long v, int l) {
+  return ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) |
+         __builtin_amdgcn_readlane((uint32_t)v, l);
+}
 template <int kPass>
 __global__ __launch_bounds__(1024) void k_reduce(const Rec* __restrict__ recs,
                                                  const unsigned long long* __restrict__ starts, uint32_t n_segs,
                                                  Agg A) {
-  __shared__ unsigned long long e_kA[kRedE], e_kB[kRedE], e_mo[kRedE];
-  __shared__ uint32_t e_first[kRedE], e_last[kRedE], e_cnt[kRedE];
+  __shared__ unsigned long long e_kA[kRedE<kPass>], e_kB[kRedE<kPass>], e_mo[kRedE<kPass>];
+  __shared__ uint32_t e_first[kRedE<kPass>], e_last[kRedE<kPass>], e_cnt[kRedE<kPass>];
   __shared__ uint32_t occ[1u << (kRegionMaxBits - 5)];     // occupied before this flush
   __shared__ uint32_t claim[1u << (kRegionMaxBits - 5)];   // claimed during this flush
   __shared__ uint32_t used;
@@ -1045,7 +1071,7 @@ __global__ __launch_bounds__(1024) void k_reduce(const Rec* __restrict__ recs,
     occ[w] = gocc[w];
     claim[w] = 0;
   }
-  for (uint32_t e = threadIdx.x; e < kRedE; e += blockDim.x) e_kB[e] = kEmpty;
+  for (uint32_t e = threadIdx.x; e < kRedE<kPass>; e += blockDim.x) e_kB[e] = kEmpty;
   if (threadIdx.x == 0) used = 0;
   __syncthreads();
   uint32_t sg = 0;
@@ -1058,25 +1084,65 @@ __global__ __launch_bounds__(1024) void k_reduce(const Rec* __restrict__ recs,
     }
     const bool last_round = pos >= end;
     if (!last_round) {
-      const uint32_t room = (3u * kRedE) / 4 - used;
+      const uint32_t room = (3u * kRedE<kPass>) / 4 - used;
       const unsigned long long take = end - pos < room ? end - pos : room;
       __syncthreads();   // every thread has read `used` before any insert changes it
-      for (unsigned long long j = threadIdx.x; j < take; j += blockDim.x) {
-        const Rec r = recs[pos + j];
-        if (kPass == 2) {
+      for (unsigned long long jb = 0; jb < take; jb += blockDim.x) {   // workgroup-uniform trip count
+        const unsigned long long j = jb + threadIdx.x;
+        bool have = j < take;
+        Rec r;
+        if (have) r = recs[pos + j];
+        if (kPass == 2 && have) {
           const unsigned long long P = A.thresh[r.kB >> 32];
-          if (P == RSA_NO_THRESHOLD || r.order > P) continue;
+          if (P == RSA_NO_THRESHOLD || r.order > P) have = false;
         }
-        uint32_t e = (uint32_t)mix64(r.kA ^ (r.kB * 0x9e3779b97f4a7c15ull)) & (kRedE - 1);
+        uint32_t cnt = 1u, first = r.ts, last = r.ts;
+        unsigned long long mo = r.order;
+        // hot keys: a rule with one distinct connection puts all its records
+        // into one region; lanes sharing the key of one of the wave's first
+        // live lanes are combined with wave reductions and enter the LDS table
+        // as ONE insert (LDS atomics on one address serialise over the lanes)
+        unsigned long long pending = __ballot(have);
+        for (int att = 0; att < kHotTries && pending; ++att) {
+          const int l0 = __builtin_ctzll(pending);
+          const unsigned long long kA0 = readlane64(r.kA, l0), kB0 = readlane64(r.kB, l0);
+          const bool dom = have && r.kA == kA0 && r.kB == kB0;
+          const unsigned long long dm = __ballot(dom);
+          pending &= ~dm;
+          if (__popcll(dm) >= kHotMin) {
+            uint32_t f = dom ? r.ts : 0xFFFFFFFFu, l = dom ? r.ts : 0u;
+            unsigned long long o = dom ? r.order : ~0ull;
+#pragma unroll
+            for (int sh = 32; sh; sh >>= 1) {
+              f = min(f, (uint32_t)__shfl_xor((int)f, sh));
+              l = max(l, (uint32_t)__shfl_xor((int)l, sh));
+              const unsigned long long oo = __shfl_xor(o, sh);
+              o = oo < o ? oo : o;
+            }
+            if (dom) {
+              if ((int)__lane_id() == l0) {
+                cnt = (uint32_t)__popcll(dm);
+                first = f;
+                last = l;
+                mo = o;
+              } else {
+                have = false;
+              }
+            }
+          }
+        }
+        if (!have) continue;
+        const uint32_t h = (uint32_t)mix64(r.kA ^ (r.kB * 0x9e3779b97f4a7c15ull));
+        uint32_t e = (kRedE<kPass> & (kRedE<kPass> - 1)) == 0 ? (h & (kRedE<kPass> - 1)) : __umulhi(h, (uint32_t)kRedE<kPass>);
         while (true) {
           const unsigned long long cur = __hip_atomic_load(&e_kB[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           if (cur == kEmpty) {
             if (atomicCAS(&e_kB[e], kEmpty, kBusy) == kEmpty) {
               e_kA[e] = r.kA;
-              e_mo[e] = r.order;
-              e_first[e] = r.ts;
-              e_last[e] = r.ts;
-              e_cnt[e] = 1u;
+              e_mo[e] = mo;
+              e_first[e] = first;
+              e_last[e] = last;
+              e_cnt[e] = cnt;
               __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
               atomicExch(&e_kB[e], r.kB);
               atomicAdd(&used, 1u);
@@ -1086,13 +1152,13 @@ __global__ __launch_bounds__(1024) void k_reduce(const Rec* __restrict__ recs,
           }
           if (cur == kBusy) continue;
           if (cur == r.kB && __hip_atomic_load(&e_kA[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == r.kA) {
-            atomicAdd(&e_cnt[e], 1u);
-            atomicMin(&e_first[e], r.ts);
-            atomicMax(&e_last[e], r.ts);
-            if (kPass == 1) atomicMin(&e_mo[e], r.order);
+            atomicAdd(&e_cnt[e], cnt);
+            atomicMin(&e_first[e], first);
+            atomicMax(&e_last[e], last);
+            if (kPass == 1) atomicMin(&e_mo[e], mo);
             break;
           }
-          e = (e + 1) & (kRedE - 1);
+          e = e + 1 == (uint32_t)kRedE<kPass> ? 0u : e + 1;
         }
       }
       pos += take;
@@ -1100,15 +1166,36 @@ __global__ __launch_bounds__(1024) void k_reduce(const Rec* __restrict__ recs,
       bool more = pos < end;
       for (uint32_t q = sg + 1; q < n_segs && !more; ++q)
         more = starts[(size_t)q * (n_regions + 1) + region + 1] > starts[(size_t)q * (n_regions + 1) + region];
-      if (used <= kRedE / 2 && more) continue;   // workgroup-uniform
+      if (used + 512u <= (3u * kRedE<kPass>) / 4 && more) continue;   // workgroup-uniform: room for 512 more
     }
     if (used > 0) {   // workgroup-uniform (read after a barrier)
       // flush: merge every LDS entry into the region; new slots are appended to
       // the used list with ONE device atomic per flush (a per-wave append on
       // the single cursor word would serialise ~30 atomics per workgroup on it)
-      constexpr int kPer = kRedE / 1024;
-      unsigned long long new_slot[kPer];
-      uint32_t n_new = 0;
+      constexpr int kPer = kRedE<kPass> / 1024;
+      unsigned long long new_slot[kPer];   // statically indexed (a counter index would spill it)
+      bool is_new[kPer];
+      // the home slots of this thread's entries first, every load in flight
+      // at once (the table is ~3% full, so nearly every key is settled at its
+      // home slot: an update there needs no further round trip).  Slots
+      // occupied before this flush are written only by the workgroup's one
+      // entry of their key, so the prefetched words stay current.
+      uint32_t home[kPer];
+      bool at_home[kPer];
+      v4u pk[kPer], pm[kPer], pc[kPer];
+#pragma unroll
+      for (int q = 0; q < kPer; ++q) {
+        const uint32_t e = threadIdx.x + q * blockDim.x;
+        const unsigned long long kB = e_kB[e];
+        home[q] = kB != kEmpty ? (uint32_t)slot_hash(e_kA[e], kB) & (rs - 1) : 0u;
+        at_home[q] = kB != kEmpty && ((occ[home[q] >> 5] >> (home[q] & 31)) & 1u);
+        if (at_home[q]) {
+          const Slot* sl = &A.slots[rbase + home[q]];
+          pk[q] = *reinterpret_cast<const v4u*>(&sl->kA);
+          if (kPass == 1) pm[q] = *reinterpret_cast<const v4u*>(&sl->min_order);
+          pc[q] = *reinterpret_cast<const v4u*>(&sl->count);
+        }
+      }
 #pragma unroll
       for (int q = 0; q < kPer; ++q) {
         const uint32_t e = threadIdx.x + q * blockDim.x;
@@ -1116,9 +1203,31 @@ __global__ __launch_bounds__(1024) void k_reduce(const Rec* __restrict__ recs,
         bool fresh = false;
         unsigned long long slot = kEmpty;
         const uint32_t gid = (uint32_t)(kB >> 32);
-        if (kB != kEmpty) {
-          const unsigned long long kA = e_kA[e];
-          uint32_t loc = (uint32_t)slot_hash(kA, kB) & (rs - 1);
+        const unsigned long long kA = e_kA[e];
+        if (at_home[q] && (((unsigned long long)pk[q].w << 32) | pk[q].z) == kB &&
+            (((unsigned long long)pk[q].y << 32) | pk[q].x) == kA) {
+          Slot* sl = &A.slots[rbase + home[q]];
+          v4u c = pc[q];
+          if (kPass == 1) {
+            const v4u m = pm[q];
+            const unsigned long long mo = ((unsigned long long)m.y << 32) | m.x;
+            const unsigned long long nmo = e_mo[e] < mo ? e_mo[e] : mo;
+            v4u nm;
+            nm.x = (uint32_t)nmo;
+            nm.y = (uint32_t)(nmo >> 32);
+            nm.z = min(m.z, e_first[e]);
+            nm.w = max(m.w, e_last[e]);
+            *reinterpret_cast<v4u*>(&sl->min_order) = nm;
+            c.x += e_cnt[e];
+          } else {
+            c.y += e_cnt[e];
+            c.z = min(c.z, e_first[e]);
+            c.w = max(c.w, e_last[e]);
+          }
+          *reinterpret_cast<v4u*>(&sl->count) = c;
+          e_kB[e] = kEmpty;
+        } else if (kB != kEmpty) {
+          uint32_t loc = home[q];
           for (uint32_t probes = 0; probes < rs; ++probes, loc = (loc + 1) & (rs - 1)) {
             const uint32_t bit = 1u << (loc & 31);
             if (occ[loc >> 5] & bit) {
@@ -1168,15 +1277,21 @@ __global__ __launch_bounds__(1024) void k_reduce(const Rec* __restrict__ recs,
         }
         if (kPass == 1) {
           wave_count_by_key(fresh, gid, A.distinct);
-          if (fresh) new_slot[n_new++] = ((unsigned long long)gid << 32) | (uint32_t)slot;
+          is_new[q] = fresh;
+          new_slot[q] = ((unsigned long long)gid << 32) | (uint32_t)slot;
         }
       }
       if (kPass == 1) {
-        uint32_t total;
+        uint32_t total, n_new = 0;
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) n_new += is_new[q] ? 1u : 0u;
         const uint32_t off = block_exscan(n_new, sh, &total);
         if (threadIdx.x == 0 && total) sh_base = atomicAdd(A.used_n, (unsigned long long)total);
         __syncthreads();
-        for (uint32_t q = 0; q < n_new; ++q) A.used[sh_base + off + q] = new_slot[q];
+        uint32_t k = 0;
+#pragma unroll
+        for (int q = 0; q < kPer; ++q)
+          if (is_new[q]) A.used[sh_base + off + k++] = new_slot[q];
       }
       __syncthreads();
       for (uint32_t w = threadIdx.x; w < words; w += blockDim.x) {
@@ -2037,7 +2152,7 @@ int launch_aggregate(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsig
   Rec* sorted = reinterpret_cast<Rec*>(c->d_recs2) + seg_base;
   const uint32_t n_regions = 1u << c->np_bits;
   uint32_t tile_len = kPartTileMin;
-  while (tile_len < kPartTileMax && (unsigned long long)tile_len * kPartTilesWant < m) tile_len <<= 1;
+  while (tile_len < kPartTileMax && (unsigned long long)tile_len * 2 * kPartTilesWant <= m) tile_len <<= 1;
   const uint32_t n_tiles = (uint32_t)((m + tile_len - 1) / tile_len);
   const unsigned long long hl = (unsigned long long)n_regions * n_tiles;
   rc = ensure_buf(c, &c->d_hist, &c->hist_alloc, hl);
