@@ -282,6 +282,63 @@ typedef struct rsa_shadow_rule {
 } rsa_shadow_rule;
 int rsa_shadowed(rsa_ctx *ctx, const rsa_shadow_rule *h_rules, uint32_t n, int32_t *h_cover);
 
+/* ---- Text parse: one firewall's log text resident in
+ * HBM -> the packed inputs of rsa_classify.  Replaces the per-line Python of
+ * mapper.py:123-166 (get_builtconn, Connection, ACL of the ingress interface,
+ * candidate list) and connlist-reducer.py:146-165 (hit test, BUILT regex, key,
+ * timestamp).  Lines end at '\n' (the terminator belongs to its line; a final
+ * line may lack it).  The device parses the canonical grammar of the ASA
+ * "Built {inbound,outbound} {TCP,UDP}" message and of the reducer's BUILT
+ * regex (Python `re` backtracking order restated: lazy `.*?`, greedy `.*`,
+ * leftmost search); a line outside it (non-canonical address/port text, an
+ * unknown protocol spelling, a timestamp outside the code range, an interface
+ * whose lookup raises) is marked RSA_LINE_HOST and the host parser decides it. */
+#define RSA_LINE_IGNORE 0   /* no Built message: the mapper skips the line (mapper.py:124-126)   */
+#define RSA_LINE_NOACL 1    /* ingress interface without ACL (mapper.py:145-150)                 */
+#define RSA_LINE_MISSING 2  /* ACL missing from the DB (mapper.py:151-156); disp >> 8 = interface */
+#define RSA_LINE_CLASSIFY 3 /* tuple valid: classify it                                         */
+#define RSA_LINE_HOST 4     /* outside the device grammar: the host parser decides              */
+#define RSA_LIST_HOST 0xFFFFu /* rsa_parse_ifc list id: the host decides (list lookup raises)    */
+#define RSA_IFC_NAME_MAX 47
+
+/* One interface of the firewall (db.firewalls[host]), 64 B. */
+typedef struct rsa_parse_ifc {
+  char name[48];               /* name bytes (len <= RSA_IFC_NAME_MAX)                        */
+  uint32_t len;
+  uint32_t kind;               /* RSA_LINE_CLASSIFY, RSA_LINE_MISSING or RSA_LINE_HOST       */
+  uint16_t list_tcp, list_udp; /* candidate list ids (kind CLASSIFY), or RSA_LIST_HOST         */
+  uint32_t reserved;
+} rsa_parse_ifc;
+
+/* One protocol spelling of the reducer key (connlist-reducer.py:155), 16 B;
+ * its index in the table is the rsa_tuple.pspell id. */
+typedef struct rsa_parse_spell {
+  char word[15];
+  uint8_t len;
+} rsa_parse_spell;
+
+/* Timestamp codes written by rsa_parse_text, order-isomorphic to the reducer's
+ * 'YYYY-MM-DD HH:MM:SS' strings (connlist-reducer.py:163-165) for years
+ * 2000..2127: ((((Y - 2000) * 12 + M - 1) * 32 + D) * 86400 + h * 3600 + m * 60 + s. */
+#define RSA_TS_YEAR0 2000
+
+/* Number of lines of text[0, n_bytes). */
+int rsa_text_count_lines(rsa_ctx *ctx, const uint8_t *d_text, uint64_t n_bytes, uint64_t *h_n_lines);
+/* Line start offsets: d_off[0 .. n_lines] (d_off[n_lines] = n_bytes). */
+int rsa_text_line_offsets(rsa_ctx *ctx, const uint8_t *d_text, uint64_t n_bytes, uint64_t *d_off, uint64_t n_lines);
+/* Parse every line: d_tuples (zero unless CLASSIFY), d_ts (codes, 0 unless
+ * hit+BUILT), d_disp (RSA_LINE_* | interface index << 8).  h_ifcs / h_spells are
+ * host tables (n_ifcs <= 4096, n_spells <= 64). */
+int rsa_parse_text(rsa_ctx *ctx, const uint8_t *d_text, const uint64_t *d_off, uint64_t n_lines,
+                   const rsa_parse_ifc *h_ifcs, uint32_t n_ifcs, const rsa_parse_spell *h_spells, uint32_t n_spells,
+                   rsa_tuple *d_tuples, uint32_t *d_ts, uint32_t *d_disp);
+/* Order keys: d_order[i] = base + rank of line i (without its '\n') in unsigned
+ * byte order, ties by line index — the order LC_ALL=C sort gives the reducer
+ * within one key (runAnalysis.sh:42-56).  Device string sort: 7-byte chunks,
+ * groups refined by radix sorts until every line is settled. */
+int rsa_order_keys(rsa_ctx *ctx, const uint8_t *d_text, const uint64_t *d_off, uint64_t n_lines, uint64_t base,
+                   uint64_t *d_order);
+
 /* Synchronise the ctx stream (tests, host hand-off). */
 int rsa_sync(rsa_ctx *ctx);
 

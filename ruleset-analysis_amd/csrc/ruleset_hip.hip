@@ -46,6 +46,7 @@
 #include <vector>
 
 #include "../../include/ruleset_hip.h"
+#include "rsa_internal.h"
 
 namespace {
 
@@ -2372,6 +2373,9 @@ int rsa_set_option(rsa_ctx* c, int option, int64_t value) {
       return fail(c, RSA_ERR_ARG, "unknown option %d", option);
   }
 }
+
+hipStream_t rsa_internal_stream(rsa_ctx* c) { return c->stream; }
+int rsa_internal_fail(rsa_ctx* c, int code, const char* msg) { return fail(c, code, "%s", msg); }
 
 int rsa_sync(rsa_ctx* c) {
   if (!c) return RSA_ERR_ARG;

@@ -1,0 +1,445 @@
+// textparse.hip — device parse of firewall log text for MI355X (gfx950):
+// SURVEY.md §8f row 1, the step before the hot path.  Text of one firewall
+// sits in HBM; the kernels here produce what rsa_classify consumes.
+//
+//   k_nl_count / k_nl_write   line split: '\n' bytes counted per 64-KiB block
+//                             (16-B loads, exact zero-byte test), block offsets
+//                             by a device scan, line starts written in order;
+//   k_parse                   one lane per line: the mapper's message parse
+//                             (get_builtconn, mapper.py:124-142 — restated by
+//                             logparse._GB), the ACL of the
+//                             ingress interface and its candidate list
+//                             (mapper.py:145-166), and the reducer's facts for
+//                             the same line (connlist-reducer.py:146-165): hit
+//                             test, BUILT regex with Python `re`'s backtracking
+//                             order, key (SWAP or not), timestamp code;
+//   order keys                the rank of each line's bytes (LC_ALL=C sort of
+//                             the mapper stream, runAnalysis.sh:42-56): 7-byte
+//                             big-endian chunks + a length field, groups of
+//                             equal prefixes refined by stable radix sorts
+//                             (rocPRIM) until every line is settled.
+//
+// Anything outside the canonical grammar is marked RSA_LINE_HOST: the host
+// parser (logparse._parse_one) decides those lines, so every error the
+// reference raises is raised by the same code and message.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <string>
+
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_reduce.hpp>
+#include <rocprim/device/device_scan.hpp>
+
+#include "../../include/ruleset_hip.h"
+#include "rsa_internal.h"
+#include "textparse_line.h"
+
+namespace {
+
+#define TPCHK(c, expr)                                                            \
+  do {                                                                            \
+    hipError_t e_ = (expr);                                                       \
+    if (e_ != hipSuccess) {                                                       \
+      const std::string m_ = std::string(#expr ": ") + hipGetErrorString(e_);     \
+      return rsa_internal_fail((c), RSA_ERR_HIP, m_.c_str());                     \
+    }                                                                             \
+  } while (0)
+
+// ---------------------------------------------------------------------------
+// Line split
+constexpr uint32_t kSplitThreads = 1024, kSplitPer = 64;
+constexpr uint64_t kSplitBlock = (uint64_t)kSplitThreads * kSplitPer;   // 64 KiB per workgroup
+
+// high bit of every byte of w that equals '\n' (exact: no borrow between bytes)
+__device__ __forceinline__ uint32_t nl_bits(uint32_t w) {
+  const uint32_t x = w ^ 0x0A0A0A0Au;
+  const uint32_t t = (x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+  return ~(t | x | 0x7F7F7F7Fu);
+}
+
+// '\n' count of this thread's 64 bytes [a, a + 64) clipped to n
+__device__ __forceinline__ uint32_t seg_count(const uint8_t* __restrict__ text, uint64_t a, uint64_t n, bool aligned) {
+  uint32_t cnt = 0;
+  if (aligned && a + kSplitPer <= n) {
+    const uint4* q = reinterpret_cast<const uint4*>(text + a);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint4 v = q[k];
+      cnt += __popc(nl_bits(v.x)) + __popc(nl_bits(v.y)) + __popc(nl_bits(v.z)) + __popc(nl_bits(v.w));
+    }
+  } else {
+    for (uint64_t i = a; i < a + kSplitPer && i < n; ++i) cnt += text[i] == '\n';
+  }
+  return cnt;
+}
+
+// exclusive scan over the 1024 threads of a block; *total = block sum
+__device__ uint32_t block_exscan(uint32_t v, uint32_t* sh, uint32_t* total) {
+  const uint32_t lane = __lane_id(), wave = threadIdx.x / 64;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) sh[wave] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (uint32_t w = 0; w < blockDim.x / 64; ++w) {
+      const uint32_t t = sh[w];
+      sh[w] = acc;
+      acc += t;
+    }
+    sh[16] = acc;
+  }
+  __syncthreads();
+  *total = sh[16];
+  return sh[wave] + x - v;
+}
+
+__global__ __launch_bounds__(kSplitThreads) void k_nl_count(const uint8_t* __restrict__ text, uint64_t n, int aligned,
+                                                             uint32_t* __restrict__ counts) {
+  __shared__ uint32_t sh[17];
+  const uint64_t a = (uint64_t)blockIdx.x * kSplitBlock + (uint64_t)threadIdx.x * kSplitPer;
+  uint32_t total;
+  block_exscan(seg_count(text, a, n, aligned != 0), sh, &total);
+  if (threadIdx.x == 0) counts[blockIdx.x] = total;
+}
+
+// incl = inclusive scan of the block counts; line k + 1 starts after the k-th '\n'
+__global__ __launch_bounds__(kSplitThreads) void k_nl_write(const uint8_t* __restrict__ text, uint64_t n, int aligned,
+                                                             const uint32_t* __restrict__ counts,
+                                                             const uint64_t* __restrict__ incl, uint64_t* __restrict__ off,
+                                                             uint64_t n_lines) {
+  __shared__ uint32_t sh[17];
+  const uint64_t a = (uint64_t)blockIdx.x * kSplitBlock + (uint64_t)threadIdx.x * kSplitPer;
+  uint32_t total;
+  const uint32_t mine = seg_count(text, a, n, aligned != 0);
+  uint64_t k = incl[blockIdx.x] - counts[blockIdx.x] + block_exscan(mine, sh, &total);
+  if (!mine) return;
+  for (uint64_t i = a; i < a + kSplitPer && i < n; ++i)
+    if (text[i] == '\n') {
+      if (k + 1 <= n_lines) off[k + 1] = i + 1;
+      ++k;
+    }
+}
+
+__global__ void k_set_u64(uint64_t* p, uint64_t v) { *p = v; }
+
+__global__ __launch_bounds__(256) void k_parse(const uint8_t* __restrict__ text, const uint64_t* __restrict__ off,
+                                               uint64_t n_lines, const rsa_parse_ifc* __restrict__ ifcs,
+                                               uint32_t n_ifcs, const rsa_parse_spell* __restrict__ spells,
+                                               uint32_t n_spells, rsa_tuple* __restrict__ tuples,
+                                               uint32_t* __restrict__ ts_out, uint32_t* __restrict__ disp) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_lines) return;
+  const uint64_t a = off[i], b = off[i + 1];
+  uint64_t len = b - a;
+  if (len && text[b - 1] == '\n') --len;
+  rsa_tuple tup;
+  uint32_t ts, d;
+  rsa_text::parse_line(text, a, len, ifcs, n_ifcs, spells, n_spells, tup, ts, d);
+  tuples[i] = tup;
+  ts_out[i] = ts;
+  disp[i] = d;
+}
+
+// ---------------------------------------------------------------------------
+// Order keys.  Round r key of a line: bytes [7r, 7r + 7) big-endian (0 past the
+// end) << 8 | min(bytes left, 8): equal keys <=> equal 7-byte windows with the
+// same "ended here" status, and key order is byte order (a prefix sorts
+// first).  A line is settled once its group (equal keys so far) is a singleton
+// or its bytes ended in this window (then the whole group is equal strings,
+// already in line-index order: the sorts are stable).
+__device__ __forceinline__ uint64_t chunk_key(const uint8_t* __restrict__ text, const uint64_t* __restrict__ off,
+                                              uint32_t line, uint32_t round) {
+  const uint64_t a = off[line], b = off[line + 1];
+  uint64_t len = b - a;
+  if (len && text[b - 1] == '\n') --len;
+  const uint64_t pos = (uint64_t)round * 7;
+  const uint64_t rem = len > pos ? len - pos : 0;
+  uint64_t k = 0;
+  for (int j = 0; j < 7; ++j) k = k << 8 | ((uint64_t)j < rem ? text[a + pos + j] : 0u);
+  return k << 8 | (rem < 8 ? rem : 8);
+}
+
+__global__ void k_keys0(const uint8_t* __restrict__ text, const uint64_t* __restrict__ off, uint32_t n,
+                        uint64_t* __restrict__ keys, uint32_t* __restrict__ ids) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  keys[j] = chunk_key(text, off, j, 0);
+  ids[j] = j;
+}
+
+struct Act {               // an unsettled line: its id and the position its group starts at
+  uint32_t id, gs;
+};
+
+__global__ void k_keys(const uint8_t* __restrict__ text, const uint64_t* __restrict__ off, const Act* __restrict__ act,
+                       uint32_t m, uint32_t round, uint64_t* __restrict__ keys, uint64_t* __restrict__ vals) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const Act x = act[j];
+  keys[j] = chunk_key(text, off, x.id, round);
+  vals[j] = (uint64_t)x.gs << 32 | x.id;
+}
+
+__global__ void k_split_gs(const uint64_t* __restrict__ vals, uint32_t m, uint32_t* __restrict__ gs,
+                           uint32_t* __restrict__ ids) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  gs[j] = (uint32_t)(vals[j] >> 32);
+  ids[j] = (uint32_t)vals[j];
+}
+
+// first index of each gs run (max-scan input): j at a run start, else 0
+__global__ void k_run_first(const uint32_t* __restrict__ gs, uint32_t m, uint32_t* __restrict__ out) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  out[j] = (j == 0 || gs[j] != gs[j - 1]) ? j : 0u;
+}
+
+// After the sort of round r: element j sits at position pos = gs + (j - first);
+// pos_start = pos at a new-group boundary, else 0 (max-scanned by the caller).
+__global__ void k_bounds(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ gs,
+                         const uint32_t* __restrict__ first, uint32_t m, uint32_t* __restrict__ pos,
+                         uint32_t* __restrict__ bstart) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const uint32_t g = gs ? gs[j] : 0u;
+  const uint32_t p = gs ? g + (j - first[j]) : j;
+  pos[j] = p;
+  const bool b = j == 0 || keys[j] != keys[j - 1] || (gs && gs[j] != gs[j - 1]);
+  bstart[j] = b ? p + 1 : 0u;   // +1: position 0 is a valid group start
+}
+
+// settle or keep each element; kept ones get a flag for the compaction scan
+__global__ void k_settle(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ gs,
+                         const uint32_t* __restrict__ ids, const uint32_t* __restrict__ pos,
+                         const uint32_t* __restrict__ ngs1, uint32_t m, uint64_t base, uint64_t* __restrict__ order,
+                         uint32_t* __restrict__ keep) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const bool last_in_group =
+      j + 1 == m || keys[j + 1] != keys[j] || (gs && gs[j + 1] != gs[j]);
+  const bool first_in_group = ngs1[j] == pos[j] + 1;
+  const bool ended = (keys[j] & 0xFFu) < 8u;
+  const bool settled = ended || (first_in_group && last_in_group);
+  if (settled) order[ids[j]] = base + pos[j];
+  keep[j] = settled ? 0u : 1u;
+}
+
+__global__ void k_compact(const uint32_t* __restrict__ ids, const uint32_t* __restrict__ ngs1,
+                          const uint32_t* __restrict__ keep, const uint32_t* __restrict__ slot, uint32_t m,
+                          Act* __restrict__ out) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m || !keep[j]) return;
+  out[slot[j]] = Act{ids[j], ngs1[j] - 1};
+}
+
+inline uint32_t blocks(uint64_t n, uint32_t t) { return (uint32_t)((n + t - 1) / t); }
+
+struct Scratch {           // one hipMallocAsync'd arena, freed on the stream at the end
+  rsa_ctx* c;
+  hipStream_t st;
+  void* base = nullptr;
+  ~Scratch() {
+    if (base) (void)hipFreeAsync(base, st);
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+int rsa_text_count_lines(rsa_ctx* c, const uint8_t* d_text, uint64_t n, uint64_t* h_n_lines) {
+  if (!c || !h_n_lines || (n && !d_text)) return RSA_ERR_ARG;
+  *h_n_lines = 0;
+  if (!n) return RSA_OK;
+  hipStream_t st = rsa_internal_stream(c);
+  const uint64_t nb = (n + kSplitBlock - 1) / kSplitBlock;
+  if (nb > 0xFFFFFFFFull) return rsa_internal_fail(c, RSA_ERR_ARG, "text too large");
+  const int aligned = (reinterpret_cast<uintptr_t>(d_text) & 15u) == 0;
+  Scratch S{c, st};
+  size_t tmp = 0;
+  TPCHK(c, rocprim::reduce(nullptr, tmp, (uint32_t*)nullptr, (uint64_t*)nullptr, (uint64_t)0, (size_t)nb,
+                           rocprim::plus<uint64_t>(), st));
+  const size_t need = nb * 4 + 16 + tmp + 256;
+  TPCHK(c, hipMallocAsync(&S.base, need, st));
+  uint32_t* counts = static_cast<uint32_t*>(S.base);
+  uint64_t* total = reinterpret_cast<uint64_t*>(static_cast<char*>(S.base) + ((nb * 4 + 15) / 16) * 16);
+  void* t = reinterpret_cast<char*>(total) + 16;
+  hipLaunchKernelGGL(k_nl_count, dim3((uint32_t)nb), dim3(kSplitThreads), 0, st, d_text, n, aligned, counts);
+  TPCHK(c, hipGetLastError());
+  TPCHK(c, rocprim::reduce(t, tmp, counts, total, (uint64_t)0, (size_t)nb, rocprim::plus<uint64_t>(), st));
+  uint64_t h_total = 0;
+  uint8_t last = 0;
+  TPCHK(c, hipMemcpyAsync(&h_total, total, 8, hipMemcpyDeviceToHost, st));
+  TPCHK(c, hipMemcpyAsync(&last, d_text + n - 1, 1, hipMemcpyDeviceToHost, st));
+  TPCHK(c, hipStreamSynchronize(st));
+  *h_n_lines = h_total + (last != '\n' ? 1 : 0);
+  return RSA_OK;
+}
+
+int rsa_text_line_offsets(rsa_ctx* c, const uint8_t* d_text, uint64_t n, uint64_t* d_off, uint64_t n_lines) {
+  if (!c || !d_off || (n && !d_text)) return RSA_ERR_ARG;
+  hipStream_t st = rsa_internal_stream(c);
+  hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(1), 0, st, d_off, (uint64_t)0);
+  if (n) {
+    const uint64_t nb = (n + kSplitBlock - 1) / kSplitBlock;
+    if (nb > 0xFFFFFFFFull) return rsa_internal_fail(c, RSA_ERR_ARG, "text too large");
+    const int aligned = (reinterpret_cast<uintptr_t>(d_text) & 15u) == 0;
+    Scratch S{c, st};
+    size_t tmp = 0;
+    TPCHK(c, rocprim::inclusive_scan(nullptr, tmp, (uint32_t*)nullptr, (uint64_t*)nullptr, (size_t)nb,
+                                     rocprim::plus<uint64_t>(), st));
+    const size_t cnt_bytes = ((nb * 4 + 15) / 16) * 16;
+    TPCHK(c, hipMallocAsync(&S.base, cnt_bytes + nb * 8 + tmp + 256, st));
+    uint32_t* counts = static_cast<uint32_t*>(S.base);
+    uint64_t* incl = reinterpret_cast<uint64_t*>(static_cast<char*>(S.base) + cnt_bytes);
+    void* t = incl + nb;
+    hipLaunchKernelGGL(k_nl_count, dim3((uint32_t)nb), dim3(kSplitThreads), 0, st, d_text, n, aligned, counts);
+    TPCHK(c, rocprim::inclusive_scan(t, tmp, counts, incl, (size_t)nb, rocprim::plus<uint64_t>(), st));
+    hipLaunchKernelGGL(k_nl_write, dim3((uint32_t)nb), dim3(kSplitThreads), 0, st, d_text, n, aligned, counts, incl,
+                       d_off, n_lines);
+    TPCHK(c, hipGetLastError());
+  }
+  hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(1), 0, st, d_off + n_lines, n);
+  TPCHK(c, hipGetLastError());
+  return RSA_OK;
+}
+
+int rsa_parse_text(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_off, uint64_t n_lines,
+                   const rsa_parse_ifc* h_ifcs, uint32_t n_ifcs, const rsa_parse_spell* h_spells, uint32_t n_spells,
+                   rsa_tuple* d_tuples, uint32_t* d_ts, uint32_t* d_disp) {
+  if (!c || (n_lines && (!d_text || !d_off || !d_tuples || !d_ts || !d_disp))) return RSA_ERR_ARG;
+  if (n_ifcs > 4096 || n_spells > 64 || (n_ifcs && !h_ifcs) || (n_spells && !h_spells))
+    return rsa_internal_fail(c, RSA_ERR_ARG, "rsa_parse_text: bad interface/spelling table");
+  for (uint32_t k = 0; k < n_ifcs; ++k)
+    if (h_ifcs[k].len > RSA_IFC_NAME_MAX || h_ifcs[k].len == 0)
+      return rsa_internal_fail(c, RSA_ERR_ARG, "rsa_parse_text: interface name length out of range");
+  for (uint32_t k = 0; k < n_spells; ++k)
+    if (h_spells[k].len > 15) return rsa_internal_fail(c, RSA_ERR_ARG, "rsa_parse_text: spelling too long");
+  if (!n_lines) return RSA_OK;
+  hipStream_t st = rsa_internal_stream(c);
+  Scratch S{c, st};
+  const size_t ib = (size_t)n_ifcs * sizeof(rsa_parse_ifc), sb = (size_t)n_spells * sizeof(rsa_parse_spell);
+  TPCHK(c, hipMallocAsync(&S.base, ib + sb + 64, st));
+  rsa_parse_ifc* d_ifcs = static_cast<rsa_parse_ifc*>(S.base);
+  rsa_parse_spell* d_spells = reinterpret_cast<rsa_parse_spell*>(static_cast<char*>(S.base) + ib);
+  if (ib) TPCHK(c, hipMemcpyAsync(d_ifcs, h_ifcs, ib, hipMemcpyHostToDevice, st));
+  if (sb) TPCHK(c, hipMemcpyAsync(d_spells, h_spells, sb, hipMemcpyHostToDevice, st));
+  TPCHK(c, hipStreamSynchronize(st));   // the host tables may go away after return
+  const uint64_t nb = (n_lines + 255) / 256;
+  if (nb > 0x7FFFFFFFull) return rsa_internal_fail(c, RSA_ERR_ARG, "too many lines");
+  hipLaunchKernelGGL(k_parse, dim3((uint32_t)nb), dim3(256), 0, st, d_text, d_off, n_lines, d_ifcs, n_ifcs, d_spells,
+                     n_spells, d_tuples, d_ts, d_disp);
+  TPCHK(c, hipGetLastError());
+  return RSA_OK;
+}
+
+int rsa_order_keys(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_off, uint64_t n_lines, uint64_t base,
+                   uint64_t* d_order) {
+  if (!c || (n_lines && (!d_text || !d_off || !d_order))) return RSA_ERR_ARG;
+  if (n_lines >= 0x7FFFFFFFull) return rsa_internal_fail(c, RSA_ERR_ARG, "rsa_order_keys: too many lines");
+  if (!n_lines) return RSA_OK;
+  hipStream_t st = rsa_internal_stream(c);
+  const uint32_t n = (uint32_t)n_lines;
+  // temp sizes of every primitive at the largest size
+  size_t t_sort64 = 0, t_sort0 = 0, t_sort32 = 0, t_scan = 0, t_exscan = 0;
+  TPCHK(c, rocprim::radix_sort_pairs(nullptr, t_sort0, (uint64_t*)nullptr, (uint64_t*)nullptr, (uint32_t*)nullptr,
+                                     (uint32_t*)nullptr, (size_t)n, 0, 64, st));
+  TPCHK(c, rocprim::radix_sort_pairs(nullptr, t_sort64, (uint64_t*)nullptr, (uint64_t*)nullptr, (uint64_t*)nullptr,
+                                     (uint64_t*)nullptr, (size_t)n, 0, 64, st));
+  TPCHK(c, rocprim::radix_sort_pairs(nullptr, t_sort32, (uint32_t*)nullptr, (uint32_t*)nullptr, (uint64_t*)nullptr,
+                                     (uint64_t*)nullptr, (size_t)n, 0, 32, st));
+  TPCHK(c, rocprim::inclusive_scan(nullptr, t_scan, (uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)n,
+                                   rocprim::maximum<uint32_t>(), st));
+  TPCHK(c, rocprim::exclusive_scan(nullptr, t_exscan, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u, (size_t)n,
+                                   rocprim::plus<uint32_t>(), st));
+  size_t tmp = t_sort64;
+  if (t_sort0 > tmp) tmp = t_sort0;
+  if (t_sort32 > tmp) tmp = t_sort32;
+  if (t_scan > tmp) tmp = t_scan;
+  if (t_exscan > tmp) tmp = t_exscan;
+  tmp = (tmp + 255) / 256 * 256;
+  const size_t N = ((size_t)n + 63) / 64 * 64;
+  // keysA/keysB u64, valsA/valsB u64, gs/ids/first/pos/bstart/keep/slot u32, act/act2 Act, count
+  const size_t bytes = tmp + N * (8 * 4 + 4 * 7 + 8 * 2) + 256;
+  Scratch S{c, st};
+  TPCHK(c, hipMallocAsync(&S.base, bytes, st));
+  char* p = static_cast<char*>(S.base);
+  void* t = p;
+  p += tmp;
+  uint64_t* keysA = reinterpret_cast<uint64_t*>(p); p += N * 8;
+  uint64_t* keysB = reinterpret_cast<uint64_t*>(p); p += N * 8;
+  uint64_t* valsA = reinterpret_cast<uint64_t*>(p); p += N * 8;
+  uint64_t* valsB = reinterpret_cast<uint64_t*>(p); p += N * 8;
+  uint32_t* gs = reinterpret_cast<uint32_t*>(p); p += N * 4;
+  uint32_t* ids = reinterpret_cast<uint32_t*>(p); p += N * 4;
+  uint32_t* first = reinterpret_cast<uint32_t*>(p); p += N * 4;
+  uint32_t* pos = reinterpret_cast<uint32_t*>(p); p += N * 4;
+  uint32_t* bstart = reinterpret_cast<uint32_t*>(p); p += N * 4;
+  uint32_t* keep = reinterpret_cast<uint32_t*>(p); p += N * 4;
+  uint32_t* slot = reinterpret_cast<uint32_t*>(p); p += N * 4;
+  Act* act = reinterpret_cast<Act*>(p); p += N * 8;
+  Act* act2 = reinterpret_cast<Act*>(p); p += N * 8;
+  uint32_t* idsA = reinterpret_cast<uint32_t*>(valsA);   // round 0 reuses the value arrays as u32 ids
+  uint32_t* idsB = reinterpret_cast<uint32_t*>(valsB);
+  (void)act2;
+
+  // round 0: all lines
+  hipLaunchKernelGGL(k_keys0, dim3(blocks(n, 256)), dim3(256), 0, st, d_text, d_off, n, keysA, idsA);
+  size_t tt = tmp;
+  TPCHK(c, rocprim::radix_sort_pairs(t, tt, keysA, keysB, idsA, idsB, (size_t)n, 0, 64, st));
+  hipLaunchKernelGGL(k_bounds, dim3(blocks(n, 256)), dim3(256), 0, st, keysB, (const uint32_t*)nullptr,
+                     (const uint32_t*)nullptr, n, pos, bstart);
+  tt = tmp;
+  TPCHK(c, rocprim::inclusive_scan(t, tt, bstart, first, (size_t)n, rocprim::maximum<uint32_t>(), st));
+  hipLaunchKernelGGL(k_settle, dim3(blocks(n, 256)), dim3(256), 0, st, keysB, (const uint32_t*)nullptr, idsB, pos,
+                     first, n, base, d_order, keep);
+  tt = tmp;
+  TPCHK(c, rocprim::exclusive_scan(t, tt, keep, slot, 0u, (size_t)n, rocprim::plus<uint32_t>(), st));
+  hipLaunchKernelGGL(k_compact, dim3(blocks(n, 256)), dim3(256), 0, st, idsB, first, keep, slot, n, act);
+  uint32_t m = 0, lastk = 0;
+  TPCHK(c, hipMemcpyAsync(&m, slot + n - 1, 4, hipMemcpyDeviceToHost, st));
+  TPCHK(c, hipMemcpyAsync(&lastk, keep + n - 1, 4, hipMemcpyDeviceToHost, st));
+  TPCHK(c, hipStreamSynchronize(st));
+  m += lastk;
+  for (uint32_t round = 1; m > 0; ++round) {
+    hipLaunchKernelGGL(k_keys, dim3(blocks(m, 256)), dim3(256), 0, st, d_text, d_off, act, m, round, keysA, valsA);
+    tt = tmp;   // stable LSD: by the chunk key, then by the group start
+    TPCHK(c, rocprim::radix_sort_pairs(t, tt, keysA, keysB, valsA, valsB, (size_t)m, 0, 64, st));
+    hipLaunchKernelGGL(k_split_gs, dim3(blocks(m, 256)), dim3(256), 0, st, valsB, m, gs, ids);
+    tt = tmp;
+    TPCHK(c, rocprim::radix_sort_pairs(t, tt, gs, first, keysB, keysA, (size_t)m, 0, 32, st));
+    tt = tmp;
+    TPCHK(c, rocprim::radix_sort_pairs(t, tt, gs, pos, valsB, valsA, (size_t)m, 0, 32, st));
+    // now: first = gs sorted, keysA = chunk keys, valsA = gs<<32|id in (gs, key) order
+    hipLaunchKernelGGL(k_split_gs, dim3(blocks(m, 256)), dim3(256), 0, st, valsA, m, gs, ids);
+    hipLaunchKernelGGL(k_run_first, dim3(blocks(m, 256)), dim3(256), 0, st, gs, m, bstart);
+    tt = tmp;
+    TPCHK(c, rocprim::inclusive_scan(t, tt, bstart, first, (size_t)m, rocprim::maximum<uint32_t>(), st));
+    hipLaunchKernelGGL(k_bounds, dim3(blocks(m, 256)), dim3(256), 0, st, keysA, gs, first, m, pos, bstart);
+    tt = tmp;
+    TPCHK(c, rocprim::inclusive_scan(t, tt, bstart, slot, (size_t)m, rocprim::maximum<uint32_t>(), st));
+    hipLaunchKernelGGL(k_settle, dim3(blocks(m, 256)), dim3(256), 0, st, keysA, gs, ids, pos, slot, m, base, d_order,
+                       keep);
+    // slot (new group start + 1) is still needed by k_compact: scan the keep flags into `first`
+    tt = tmp;
+    TPCHK(c, rocprim::exclusive_scan(t, tt, keep, first, 0u, (size_t)m, rocprim::plus<uint32_t>(), st));
+    hipLaunchKernelGGL(k_compact, dim3(blocks(m, 256)), dim3(256), 0, st, ids, slot, keep, first, m, act);
+    uint32_t nm = 0;
+    TPCHK(c, hipMemcpyAsync(&nm, first + m - 1, 4, hipMemcpyDeviceToHost, st));
+    TPCHK(c, hipMemcpyAsync(&lastk, keep + m - 1, 4, hipMemcpyDeviceToHost, st));
+    TPCHK(c, hipStreamSynchronize(st));
+    m = nm + lastk;
+  }
+  TPCHK(c, hipGetLastError());
+  return RSA_OK;
+}
+
+}  // extern "C"

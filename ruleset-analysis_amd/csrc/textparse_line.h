@@ -1,0 +1,439 @@
+// textparse_line.h — the per-line parse of textparse.hip (k_parse), as
+// __host__ __device__ code so that tests can also run it on the CPU
+// (tests/native/textparse_host.cpp) against the Python host parser.
+#ifndef RSA_TEXTPARSE_LINE_H
+#define RSA_TEXTPARSE_LINE_H
+
+#include <stdint.h>
+
+#include "../../include/ruleset_hip.h"
+
+#ifndef __HIPCC__
+#define __host__
+#define __device__
+#define __forceinline__ inline
+#endif
+
+namespace rsa_text {
+
+#define RSA_HD __host__ __device__ __forceinline__
+
+// One lane per line, bytes read through the line accessor.
+struct Ln {
+  const uint8_t* p;
+  uint32_t n;   // length without the '\n' terminator
+  RSA_HD uint32_t operator[](uint32_t i) const { return p[i]; }
+};
+
+RSA_HD bool is_dig(uint32_t c) { return c - '0' < 10u; }
+RSA_HD bool is_upper(uint32_t c) { return c - 'A' < 26u; }
+RSA_HD bool is_lower(uint32_t c) { return c - 'a' < 26u; }
+RSA_HD bool is_alpha(uint32_t c) { return (c | 32u) - 'a' < 26u; }
+RSA_HD bool is_ifc(uint32_t c) { return is_alpha(c) || is_dig(c) || c == '_' || c == '-'; }
+RSA_HD bool is_ipch(uint32_t c) { return is_dig(c) || c == '.'; }
+RSA_HD bool is_tsch(uint32_t c) { return is_dig(c) || c == ':'; }
+
+enum Cls { kDig, kAlpha, kIfc, kIp, kTs };
+template <int C>
+RSA_HD bool in_cls(uint32_t c) {
+  return C == kDig ? is_dig(c) : C == kAlpha ? is_alpha(c) : C == kIfc ? is_ifc(c) : C == kIp ? is_ipch(c) : is_tsch(c);
+}
+// end of the run of class C starting at p
+template <int C>
+RSA_HD uint32_t run(const Ln& s, uint32_t p) {
+  while (p < s.n && in_cls<C>(s[p])) ++p;
+  return p;
+}
+// s[p ..] starts with the literal
+template <int N>
+RSA_HD bool lit(const Ln& s, uint32_t p, const char (&w)[N]) {
+  if (p + (N - 1) > s.n) return false;
+#pragma unroll
+  for (int i = 0; i < N - 1; ++i)
+    if (s[p + i] != (uint8_t)w[i]) return false;
+  return true;
+}
+// largest k in [lo, hi] where the literal starts, or -1
+template <int N>
+RSA_HD int64_t last_lit(const Ln& s, int64_t lo, int64_t hi, const char (&w)[N]) {
+  if (hi > (int64_t)s.n - (N - 1)) hi = (int64_t)s.n - (N - 1);
+  for (int64_t k = hi; k >= lo; --k)
+    if (lit(s, (uint32_t)k, w)) return k;
+  return -1;
+}
+// \d\d:\d\d:\d\d
+RSA_HD bool hms(const Ln& s, uint32_t p) {
+  return p + 8 <= s.n && is_dig(s[p]) && is_dig(s[p + 1]) && s[p + 2] == ':' && is_dig(s[p + 3]) &&
+         is_dig(s[p + 4]) && s[p + 5] == ':' && is_dig(s[p + 6]) && is_dig(s[p + 7]);
+}
+
+struct Span {
+  uint32_t a, b;
+};
+
+struct Mapped {             // get_builtconn's fields
+  bool inbound, udp;
+  Span if1, ip1, p1, if2, ip2, p2;
+};
+
+// The rest of logparse._GB after `.*?`, at the '%' + 1 position p.
+RSA_HD bool gb_rest(const Ln& s, uint32_t p, Mapped& m) {
+  if (lit(s, p, "ASA")) p += 3;
+  else if (lit(s, p, "FWSM")) p += 4;
+  else if (lit(s, p, "PIX")) p += 3;
+  else return false;
+  if (p + 3 > s.n || s[p] != '-' || !is_dig(s[p + 1]) || s[p + 2] != '-') return false;
+  p += 3;
+  if (p + 6 > s.n) return false;
+  for (int i = 0; i < 6; ++i)
+    if (!is_dig(s[p + i])) return false;
+  p += 6;
+  if (!lit(s, p, ": Built ")) return false;
+  p += 8;
+  if (lit(s, p, "inbound ")) {
+    m.inbound = true;
+    p += 8;
+  } else if (lit(s, p, "outbound ")) {
+    m.inbound = false;
+    p += 9;
+  } else {
+    return false;
+  }
+  if (lit(s, p, "TCP")) m.udp = false;
+  else if (lit(s, p, "UDP")) m.udp = true;
+  else return false;
+  p += 3;
+  if (!lit(s, p, " connection ")) return false;
+  p += 12;
+  uint32_t e = run<kDig>(s, p);
+  if (e == p || e >= s.n || s[e] != ' ') return false;
+  p = e + 1;
+  if (!lit(s, p, "for ")) return false;
+  p += 4;
+  e = run<kIfc>(s, p);
+  if (e == p || e >= s.n || s[e] != ':') return false;
+  m.if1 = {p, e};
+  p = e + 1;
+  e = run<kIp>(s, p);
+  if (e == p || e >= s.n || s[e] != '/') return false;
+  m.ip1 = {p, e};
+  p = e + 1;
+  e = run<kDig>(s, p);
+  if (e == p || !lit(s, e, " (")) return false;
+  m.p1 = {p, e};
+  p = e + 2;
+  while (p < s.n && s[p] != ')') ++p;   // [^)]*
+  if (p >= s.n) return false;
+  ++p;
+  if (!lit(s, p, " to ")) return false;
+  p += 4;
+  e = run<kIfc>(s, p);
+  if (e == p || e >= s.n || s[e] != ':') return false;
+  m.if2 = {p, e};
+  p = e + 1;
+  e = run<kIp>(s, p);
+  if (e == p || e >= s.n || s[e] != '/') return false;
+  m.ip2 = {p, e};
+  p = e + 1;
+  e = run<kDig>(s, p);
+  if (e == p) return false;
+  m.p2 = {p, e};
+  return true;
+}
+
+// logparse._GB.match(line): header, optional device date, lazy .*? over the
+// '%' positions (the first one whose rest matches wins).  The optional group
+// is taken when it matches: skipping it cannot change the outcome, since its
+// text holds no '%'.
+RSA_HD bool gb_match(const Ln& s, Mapped& m) {
+  if (s.n < 3 || !is_upper(s[0]) || !is_lower(s[1]) || !is_lower(s[2])) return false;
+  uint32_t p = 3;
+  if (p >= s.n || s[p] != ' ') return false;
+  while (p < s.n && s[p] == ' ') ++p;
+  uint32_t e = run<kDig>(s, p);
+  if (e - p < 1 || e - p > 2 || e >= s.n || s[e] != ' ') return false;
+  p = e + 1;
+  if (!hms(s, p) || p + 8 >= s.n || s[p + 8] != ' ') return false;
+  p += 9;
+  uint32_t q = p;
+  {
+    uint32_t t = p;
+    if (t + 3 <= s.n && is_upper(s[t]) && is_lower(s[t + 1]) && is_lower(s[t + 2]) && t + 3 < s.n && s[t + 3] == ' ') {
+      t += 3;
+      while (t < s.n && s[t] == ' ') ++t;
+      e = run<kDig>(s, t);
+      if (e - t >= 1 && e - t <= 2 && e < s.n && s[e] == ' ') {
+        t = e + 1;
+        e = run<kDig>(s, t);
+        if (e - t == 4 && e < s.n && s[e] == ' ') {
+          t = e + 1;
+          if (hms(s, t) && t + 10 <= s.n && s[t + 8] == ':' && s[t + 9] == ' ') q = t + 10;
+        }
+      }
+    }
+  }
+  for (uint32_t k = q; k < s.n; ++k)
+    if (s[k] == '%' && gb_rest(s, k + 1, m)) return true;
+  return false;
+}
+
+struct Reduced {            // connlist-reducer.py:25 BUILT captures used downstream
+  Span time, mon, day, year, word, for_ip, to_ip, to_port;
+};
+
+// After `[a-zA-Z]+ [0-9 ]?[0-9] `: groups 1-4, then the three greedy `.*`
+// (candidates tried from the last occurrence down, nested as the engine does).
+RSA_HD bool built_tail(const Ln& s, uint32_t p, Reduced& r) {
+  uint32_t e = run<kTs>(s, p);
+  if (e == p || e >= s.n || s[e] != ' ') return false;
+  r.time = {p, e};
+  p = e + 1;
+  e = run<kAlpha>(s, p);
+  if (e == p || e >= s.n || s[e] != ' ') return false;
+  r.mon = {p, e};
+  p = e + 1;
+  e = run<kDig>(s, p);
+  if (e == p || e >= s.n || s[e] != ' ') return false;
+  r.day = {p, e};
+  p = e + 1;
+  e = run<kDig>(s, p);
+  if (e == p || e >= s.n || s[e] != ' ') return false;
+  r.year = {p, e};
+  p = e + 1;
+  for (int64_t k1 = last_lit(s, p, (int64_t)s.n, " Built "); k1 >= (int64_t)p;
+       k1 = last_lit(s, p, k1 - 1, " Built ")) {
+    uint32_t t = (uint32_t)k1 + 7;
+    if (lit(s, t, "out")) t += 3;
+    else if (lit(s, t, "in")) t += 2;
+    else continue;
+    if (!lit(s, t, "bound ")) continue;
+    t += 6;
+    e = run<kAlpha>(s, t);
+    if (e == t || e >= s.n || s[e] != ' ') continue;
+    r.word = {t, e};
+    const uint32_t q2 = e + 1;
+    for (int64_t k2 = last_lit(s, q2, (int64_t)s.n, " for "); k2 >= (int64_t)q2;
+         k2 = last_lit(s, q2, k2 - 1, " for ")) {
+      uint32_t u = (uint32_t)k2 + 5;
+      e = run<kIfc>(s, u);
+      if (e == u || e >= s.n || s[e] != ':') continue;
+      u = e + 1;
+      e = run<kIp>(s, u);
+      if (e == u || e >= s.n || s[e] != '/') continue;
+      r.for_ip = {u, e};
+      u = e + 1;
+      e = run<kDig>(s, u);
+      if (e == u || e >= s.n || s[e] != ' ') continue;
+      const uint32_t q3 = e + 1;
+      for (int64_t k3 = last_lit(s, q3, (int64_t)s.n, " to "); k3 >= (int64_t)q3;
+           k3 = last_lit(s, q3, k3 - 1, " to ")) {
+        uint32_t v = (uint32_t)k3 + 4;
+        e = run<kIfc>(s, v);
+        if (e == v || e >= s.n || s[e] != ':') continue;
+        v = e + 1;
+        e = run<kIp>(s, v);
+        if (e == v || e >= s.n || s[e] != '/') continue;
+        r.to_ip = {v, e};
+        v = e + 1;
+        e = run<kDig>(s, v);
+        if (e == v) continue;
+        r.to_port = {v, e};
+        return true;
+      }
+    }
+  }
+  return false;
+}
+
+// BUILT.search(line): leftmost start.  A start inside a letter run has the
+// same continuation as the run's first letter, so only run starts are tried;
+// `[0-9 ]?` is tried taken, then skipped.
+RSA_HD bool built_search(const Ln& s, Reduced& r) {
+  for (uint32_t s0 = 0; s0 < s.n; ++s0) {
+    if (!is_alpha(s[s0])) continue;
+    const uint32_t e = run<kAlpha>(s, s0);
+    const uint32_t p = e + 1;
+    if (e < s.n && s[e] == ' ') {
+      if (p + 2 < s.n && (is_dig(s[p]) || s[p] == ' ') && is_dig(s[p + 1]) && s[p + 2] == ' ' &&
+          built_tail(s, p + 3, r))
+        return true;
+      if (p + 1 < s.n && is_dig(s[p]) && s[p + 1] == ' ' && built_tail(s, p + 2, r)) return true;
+    }
+    s0 = e;   // the next start is past this run (the loop's ++ skips the non-letter at e)
+  }
+  return false;
+}
+
+RSA_HD bool hit_test(const Ln& s) {   // '-6-302013' / '-6-302015' anywhere (connlist-reducer.py:146)
+  if (s.n < 9) return false;
+  for (uint32_t k = 0; k + 9 <= s.n; ++k)
+    if (s[k] == '-' && s[k + 1] == '6' && lit(s, k + 2, "-30201") && (s[k + 8] == '3' || s[k + 8] == '5')) return true;
+  return false;
+}
+
+RSA_HD bool span_eq(const Ln& s, Span x, Span y) {
+  if (x.b - x.a != y.b - y.a) return false;
+  for (uint32_t i = 0; i < x.b - x.a; ++i)
+    if (s[x.a + i] != s[y.a + i]) return false;
+  return true;
+}
+
+// canonical dotted quad (what str(IP) prints back) -> value
+RSA_HD bool ipv4_canon(const Ln& s, Span x, uint32_t& v) {
+  uint32_t p = x.a, val = 0;
+  for (int o = 0; o < 4; ++o) {
+    const uint32_t e = run<kDig>(s, p);
+    if (e > x.b || e == p || e - p > 3 || (e - p > 1 && s[p] == '0')) return false;
+    uint32_t octet = 0;
+    for (uint32_t i = p; i < e; ++i) octet = octet * 10 + (s[i] - '0');
+    if (octet > 255) return false;
+    val = val << 8 | octet;
+    if (o < 3) {
+      if (e >= x.b || s[e] != '.') return false;
+      p = e + 1;
+    } else if (e != x.b) {
+      return false;
+    }
+  }
+  v = val;
+  return true;
+}
+
+// int(text) of a digit run, saturating above 65535 (the caller defers those)
+RSA_HD uint32_t port_val(const Ln& s, Span x) {
+  uint32_t v = 0;
+  for (uint32_t i = x.a; i < x.b; ++i) {
+    v = v * 10 + (s[i] - '0');
+    if (v > 65535u) return 65536u;
+  }
+  return v;
+}
+
+RSA_HD bool port_canon(const Ln& s, Span x) { return x.b - x.a == 1 || s[x.a] != '0'; }
+
+RSA_HD uint32_t small_num(const Ln& s, Span x) {   // <= 4 digits
+  uint32_t v = 0;
+  for (uint32_t i = x.a; i < x.b; ++i) v = v * 10 + (s[i] - '0');
+  return v;
+}
+
+// connlist-reducer.py:163-165 as a code: year(4 digits, 2000..2127)-MM-DD
+// (day zfill(2) <= 31) HH:MM:SS (h < 24, m, s < 60); false = not codable
+RSA_HD bool ts_code(const Ln& s, const Reduced& r, uint32_t& code) {
+  const char* const months = "JanFebMarAprMayJunJulAugSepOctNovDec";
+  if (r.mon.b - r.mon.a != 3) return false;
+  int mo = -1;
+  for (int k = 0; k < 12; ++k)
+    if (s[r.mon.a] == (uint8_t)months[3 * k] && s[r.mon.a + 1] == (uint8_t)months[3 * k + 1] &&
+        s[r.mon.a + 2] == (uint8_t)months[3 * k + 2]) {
+      mo = k;
+      break;
+    }
+  if (mo < 0) return false;
+  if (r.year.b - r.year.a != 4 || r.day.b - r.day.a > 2 || r.time.b - r.time.a != 8) return false;
+  const uint32_t y = small_num(s, r.year), d = small_num(s, r.day);
+  if (y < RSA_TS_YEAR0 || y >= RSA_TS_YEAR0 + 128 || d > 31) return false;
+  const uint32_t t = r.time.a;
+  if (!hms(s, t)) return false;
+  const uint32_t hh = (s[t] - '0') * 10 + (s[t + 1] - '0'), mm = (s[t + 3] - '0') * 10 + (s[t + 4] - '0'),
+                 ss = (s[t + 6] - '0') * 10 + (s[t + 7] - '0');
+  if (hh > 23 || mm > 59 || ss > 59) return false;
+  code = ((((y - RSA_TS_YEAR0) * 12u + (uint32_t)mo) * 32u + d) * 86400u) + hh * 3600u + mm * 60u + ss;
+  return true;
+}
+
+// The whole line: disposition (RSA_LINE_* | interface << 8), tuple, timestamp code.
+RSA_HD void parse_line(const uint8_t* text, uint64_t a, uint64_t len, const rsa_parse_ifc* ifcs, uint32_t n_ifcs,
+                       const rsa_parse_spell* spells, uint32_t n_spells, rsa_tuple& tup_out, uint32_t& ts_out,
+                       uint32_t& d_out) {
+  rsa_tuple tup = {0u, 0u, 0, 0, 0, 0, 0};
+  uint32_t ts = 0, d = RSA_LINE_IGNORE;
+  if (len >= 0xFFFFFFFFull) {
+    d = RSA_LINE_HOST;
+  } else {
+    const Ln s{text + a, (uint32_t)len};
+    Mapped m;
+    if (gb_match(s, m)) {
+      d = RSA_LINE_CLASSIFY;
+      const Span src = m.inbound ? m.ip1 : m.ip2, dst = m.inbound ? m.ip2 : m.ip1;
+      const Span sp = m.inbound ? m.p1 : m.p2, dp = m.inbound ? m.p2 : m.p1;
+      const Span ifc = m.inbound ? m.if1 : m.if2;
+      uint32_t vs = 0, vd = 0;
+      const uint32_t ps = port_val(s, sp), pd = port_val(s, dp);
+      // FirewallRule._address validation of the text (mapper.py:138-142): the
+      // device takes canonical dotted quads only
+      if (!ipv4_canon(s, src, vs) || !ipv4_canon(s, dst, vd)) d = RSA_LINE_HOST;
+      int32_t found = -1;
+      const uint32_t il = ifc.b - ifc.a;
+      if (d == RSA_LINE_CLASSIFY) {
+        if (il > RSA_IFC_NAME_MAX) {
+          d = RSA_LINE_HOST;
+        } else {
+          for (uint32_t k = 0; k < n_ifcs && found < 0; ++k) {
+            if (ifcs[k].len != il) continue;
+            bool eq = true;
+            for (uint32_t c = 0; c < il && eq; ++c) eq = s[ifc.a + c] == (uint8_t)ifcs[k].name[c];
+            if (eq) found = (int32_t)k;
+          }
+          if (found < 0) {
+            d = RSA_LINE_NOACL;
+          } else if (ifcs[found].kind == RSA_LINE_MISSING) {
+            d = RSA_LINE_MISSING | ((uint32_t)found << 8);
+          } else if (ifcs[found].kind != RSA_LINE_CLASSIFY) {
+            d = RSA_LINE_HOST;
+          }
+        }
+      }
+      if (d == RSA_LINE_CLASSIFY) {
+        const uint32_t lid = m.udp ? ifcs[found].list_udp : ifcs[found].list_tcp;
+        if (lid == RSA_LIST_HOST || ps > 65535u || pd > 65535u) d = RSA_LINE_HOST;
+        tup.src = vs;
+        tup.dst = vd;
+        tup.sport = (uint16_t)ps;
+        tup.dport = (uint16_t)pd;
+        tup.list = (uint16_t)lid;
+        uint32_t flags = RSA_F_VALID;
+        const bool hit = hit_test(s);
+        if (hit) flags |= RSA_F_HIT;
+        Reduced r;
+        if (d == RSA_LINE_CLASSIFY && built_search(s, r)) {
+          flags |= RSA_F_BUILT;
+          uint32_t vf = 0, vt = 0;
+          if (span_eq(s, r.for_ip, src) && span_eq(s, r.to_ip, dst) && span_eq(s, r.to_port, dp)) {
+          } else if (span_eq(s, r.for_ip, dst) && span_eq(s, r.to_ip, src) && span_eq(s, r.to_port, sp)) {
+            flags |= RSA_F_SWAP;
+          } else {
+            d = RSA_LINE_HOST;
+          }
+          if (!ipv4_canon(s, r.for_ip, vf) || !ipv4_canon(s, r.to_ip, vt) || !port_canon(s, r.to_port))
+            d = RSA_LINE_HOST;
+          if (hit && !ts_code(s, r, ts)) d = RSA_LINE_HOST;
+          int32_t sid = -1;
+          const uint32_t wl = r.word.b - r.word.a;
+          for (uint32_t k = 0; k < n_spells && sid < 0; ++k) {
+            if (spells[k].len != wl) continue;
+            bool eq = true;
+            for (uint32_t c = 0; c < wl && eq; ++c) eq = s[r.word.a + c] == (uint8_t)spells[k].word[c];
+            if (eq) sid = (int32_t)k;
+          }
+          if (sid < 0) d = RSA_LINE_HOST;
+          else tup.pspell = (uint8_t)sid;
+        }
+        tup.flags = (uint8_t)flags;
+      }
+      if (d != RSA_LINE_CLASSIFY) {
+        tup = rsa_tuple{0u, 0u, 0, 0, 0, 0, 0};
+        ts = 0;
+      }
+    }
+  }
+  tup_out = tup;
+  ts_out = ts;
+  d_out = d;
+}
+
+#undef RSA_HD
+
+}  // namespace rsa_text
+
+#endif

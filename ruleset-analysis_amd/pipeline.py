@@ -15,7 +15,7 @@ from .engine import Engine, DeviceBatch
 from .logparse import parse_logs, D_CLASSIFY, D_MISSING
 from .report import reducer_report
 
-__all__ = ['analyze', 'assemble_report', 'built_hit_count']
+__all__ = ['analyze', 'analyze_text', 'assemble_report', 'built_hit_count']
 
 
 def built_hit_count(tuples):
@@ -34,7 +34,9 @@ def assemble_report(parsed, gids, results, compiled, cap, ts_decode=None, pspell
         groups.append((key + '\t', gid, host, acl, db.accesslists[host][acl]['rules'][i]))
     groups.sort(key=lambda g: g[0])
     disp = parsed.disposition
-    nl = np.array([l.endswith('\n') for l in parsed.lines], dtype=bool) if parsed.n else np.zeros(0, bool)
+    nl = getattr(parsed, 'nl', None)
+    if nl is None:
+        nl = np.array([l.endswith('\n') for l in parsed.lines], dtype=bool) if parsed.n else np.zeros(0, bool)
     matched = (disp == D_CLASSIFY) & (gids >= 0)
     n_blank = int(np.count_nonzero(matched & nl))
     noise = []
@@ -49,7 +51,7 @@ def assemble_report(parsed, gids, results, compiled, cap, ts_decode=None, pspell
         if nl[i]:
             n_blank += 1
     if ts_decode is None:
-        ts_decode = parsed.ts_table.__getitem__
+        ts_decode = getattr(parsed, 'ts_decode', None) or parsed.ts_table.__getitem__
     if pspell_table is None:
         pspell_table = parsed.pspell_table
     return reducer_report(results, groups, noise, cap, ts_decode, pspell_table, n_blank=n_blank)
@@ -66,4 +68,34 @@ def analyze(inputs, db, cap=1000, device=0, engine=None):
     batch = DeviceBatch.from_numpy(parsed.tuples, parsed.ts, parsed.order, eng.device)
     results = eng.run([batch], cap, capacity=max(built_hit_count(parsed.tuples), 1))
     gids = eng.last_gids[0].cpu().numpy() if parsed.n else np.zeros(0, np.int32)
+    return assemble_report(parsed, gids, results, compiled, cap), results
+
+
+def analyze_text(inputs, db, cap=1000, device=0, engine=None):
+    """The fused job from raw log bytes: inputs = iterable of (host, bytes).
+    The text is parsed on the GPU (textparse); returns (report lines, results)."""
+    from . import textparse
+    compiled = CompiledRules(db)
+    compiled.ensure_lists()
+    eng = engine if engine is not None else Engine(device)
+    parts, pspell, base = [], {}, 0
+    for host, data in inputs:
+        p = textparse.parse_text(eng, host, data, db, compiled, pspell=pspell, order_base=base)
+        parts.append(p)
+        base += p.n
+        if p.error is not None:
+            break
+    parsed = textparse.concat(parts, eng.torch)
+    if parsed.error is not None:
+        raise parsed.error[1]
+    eng.load_compiled(compiled)
+    if parsed.n == 0:
+        results = eng.run([], cap, capacity=1)
+        return assemble_report(parsed, np.zeros(0, np.int32), results, compiled, cap), results
+    batch = parsed.batch()
+    flags = (batch.tuples[:, 3] >> 16) & 0xFF
+    both = F_HIT | F_BUILT
+    n_hb = int(((flags & both) == both).sum().item())
+    results = eng.run([batch], cap, capacity=max(n_hb, 1))
+    gids = eng.last_gids[0].cpu().numpy()
     return assemble_report(parsed, gids, results, compiled, cap), results

@@ -1,0 +1,16 @@
+// Test harness: the device line parser (csrc/textparse_line.h, the body of
+// k_parse) compiled for the CPU, so tests/test_textparse.py can check its
+// decisions against the Python host parser without a GPU.  Test
+// infrastructure only: nothing in the product loads this library.
+#include "../../ruleset-analysis_amd/csrc/textparse_line.h"
+
+extern "C" void parse_lines_host(const uint8_t* text, const uint64_t* off, uint64_t n, const rsa_parse_ifc* ifcs,
+                                 uint32_t n_ifcs, const rsa_parse_spell* spells, uint32_t n_spells,
+                                 rsa_tuple* tuples, uint32_t* ts, uint32_t* disp) {
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t a = off[i], b = off[i + 1];
+    uint64_t len = b - a;
+    if (len && text[b - 1] == '\n') --len;
+    rsa_text::parse_line(text, a, len, ifcs, n_ifcs, spells, n_spells, tuples[i], ts[i], disp[i]);
+  }
+}
