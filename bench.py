@@ -532,6 +532,157 @@ def rank_main(args, rank, world, local):
     return 0
 
 
+_TEXT_WL = None
+
+
+def _render_chunk(job):
+    """(offset, m, rank) -> the rendered log bytes of that chunk (fork worker)."""
+    a, m, k = job
+    wl = _TEXT_WL
+    t0 = 15 * 86400 + a // 2000
+    tr = wl.traffic(m, wl.seed * 1_000_003 + 7919 + k, t0, max(m // 2000, 1), 1_000_000 + a)
+    return ('\n'.join(synth.render_lines(tr)) + '\n').encode('latin-1'), a
+
+
+def text_main(args):
+    """--text: the fused job from log TEXT resident in HBM:
+    line split + parse + order keys (textparse.hip) + classify + aggregate.
+    The text is rendered on the host by forked workers before the GPU is
+    touched (not timed)."""
+    global _TEXT_WL
+    import multiprocessing
+    wl = Workload(args.config, rules=args.rules, cap=args.cap)
+    if wl.kind != 'asa':
+        die('--text renders ASA log lines: use an ASA config')
+    lines = args.lines or 16_000_000
+    chunk = 500_000
+    _TEXT_WL = wl
+    t_r = time.perf_counter()
+    jobs = [(a, min(chunk, lines - a), k) for k, a in enumerate(range(0, lines, chunk))]
+    with multiprocessing.get_context('fork').Pool(min(16, len(jobs))) as pool:
+        parts = sorted(pool.map(_render_chunk, jobs), key=lambda x: x[1])
+    data = b''.join(p for p, _a in parts)
+    del parts
+    log('rendered %d lines, %.2f GB of text in %.1fs' % (lines, len(data) / 1e9, time.perf_counter() - t_r))
+    import ctypes
+    import torch
+    from ruleset_analysis_amd import textparse
+    from ruleset_analysis_amd.engine import DeviceBatch, Engine
+    compiled = wl.compiled
+    eng = Engine(0)
+    ifcs, _names = textparse.interface_table(wl.db, compiled, wl.info['host'])
+    spells = textparse.spell_table(list(textparse.DEFAULT_SPELLS))
+    eng.load_compiled(compiled, index=not args.no_index, prefix=args.prefix)
+    dev = eng.device
+    text = textparse._device_bytes(torch, data, dev)
+    n = lines
+    off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    tup = torch.empty((n, 4), dtype=torch.int32, device=dev)
+    ts = torch.empty(n, dtype=torch.int32, device=dev)
+    disp = torch.empty(n, dtype=torch.int32, device=dev)
+    order = torch.empty(n, dtype=torch.int64, device=dev)
+    gbuf = torch.empty(n, dtype=torch.int32, device=dev)
+    v = lambda t: ctypes.c_void_p(t.data_ptr())
+    hp = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    ctx = eng.ctx
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+    phases = []
+    last = {}
+
+    def step(timed):
+        ev[0].record()
+        nl = ctypes.c_uint64(0)
+        ctx.call('rsa_text_count_lines', v(text), ctypes.c_uint64(len(data)), ctypes.byref(nl))
+        if nl.value != n:
+            die('line count %d != %d' % (nl.value, n))
+        ctx.call('rsa_text_line_offsets', v(text), ctypes.c_uint64(len(data)), v(off), ctypes.c_uint64(n))
+        ev[1].record()
+        ctx.call('rsa_parse_text', v(text), v(off), ctypes.c_uint64(n), hp(ifcs), ctypes.c_uint32(len(ifcs)),
+                 hp(spells), ctypes.c_uint32(len(spells)), v(tup), v(ts), v(disp))
+        ev[2].record()
+        ctx.call('rsa_order_keys', v(text), v(off), ctypes.c_uint64(n), ctypes.c_uint64(0), v(order))
+        ev[3].record()
+        n_host = int(((disp & 0xFF) == textparse.LINE_HOST).sum().item())
+        if n_host:
+            die('%d synthetic lines outside the device grammar' % n_host)
+        flags = (tup[:, 3] >> 16) & 0xFF
+        both = 0x06
+        n_hb = int(((flags & both) == both).sum().item())
+        b = DeviceBatch(tup, ts, order)
+        eng.reset(max(n_hb, 1), wl.cap)
+        eng.pass1(b, gbuf)
+        if eng.resolve_cap():
+            eng.pass2(b, gbuf)
+        last['recs'] = eng.emit_device('final')
+        ev[4].record()
+        if timed:
+            torch.cuda.synchronize()
+            phases.append([ev[k].elapsed_time(ev[k + 1]) for k in range(4)])
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ph = np.mean(np.array(phases), axis=0)
+    checks = None
+    if not args.no_check:
+        # untimed: the device parse equals the generator's packed form, order
+        # keys rank the line bytes (sampled adjacent pairs), and the job's
+        # records equal those of the same job from the packed tuples
+        ok = True
+        h_off = off.cpu().numpy()
+        gt = tup.cpu().numpy().reshape(-1).view(np.uint8).view(TUPLE_DTYPE)
+        pk = []
+        for (a, m, k) in jobs:
+            tr = wl.traffic(m, wl.seed * 1_000_003 + 7919 + k, 15 * 86400 + a // 2000, max(m // 2000, 1),
+                            1_000_000 + a)
+            pk.append(synth.pack(tr, compiled)[0])
+        pk = np.concatenate(pk)
+        cls = (disp & 0xFF).cpu().numpy() == textparse.LINE_CLASSIFY
+        same_tuples = bool(np.array_equal(gt[cls].view(np.uint8), pk[cls].view(np.uint8))) and \
+            not pk['flags'][~cls].any()
+        perm = torch.argsort(order).cpu().numpy()
+        rng = np.random.default_rng(0)
+        sample = rng.integers(0, n - 1, 100_000)
+        line = lambda i: data[h_off[i]:h_off[i + 1] - 1]
+        sorted_pairs = all(line(perm[j]) <= line(perm[j + 1]) for j in sample)
+        distinct = bool(torch.unique(order).numel() == n)
+        c_text = record_checksum(last['recs'])
+        b2 = DeviceBatch.from_numpy(pk, ts.cpu().numpy().view(np.uint32), order.cpu().numpy().view(np.uint64), dev)
+        eng.reset(max(built_hit_count(pk), 1), wl.cap)
+        eng.pass1(b2, gbuf)
+        if eng.resolve_cap():
+            eng.pass2(b2, gbuf)
+        c_packed = record_checksum(eng.emit_device('final'))
+        ok = same_tuples and sorted_pairs and distinct and c_text == c_packed
+        checks = {'tuples_eq_generator': same_tuples, 'order_sorted_sampled_pairs': bool(sorted_pairs),
+                  'order_keys_distinct': distinct, 'records_eq_packed_job': c_text == c_packed, 'ok': bool(ok)}
+        log('checks: %s' % json.dumps(checks))
+    text_bytes = len(data)
+    parse_gbs = (text_bytes + 32 * n) / (ph[1] * 1e-3) / 1e9
+    res = {
+        'metric': 'log lines/sec from TEXT in HBM: line split + parse + order keys + classify + aggregate (1 GPU)',
+        'value': n * args.steps / dt, 'unit': 'lines/s', 'n_gpus': 1, 'steps': args.steps, 'warmup': args.warmup,
+        'ms_per_step': dt / args.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+        'dtype': 'u8',
+        'data': 'synthetic ASA log text rendered on the host (%s), resident in HBM' % wl.data,
+        'config': {'workload': '%s text: %d lines, %.2f GB, %d expanded rules, cap %d'
+                               % (args.config, n, text_bytes / 1e9, compiled.n_rules, wl.cap),
+                   'lines': n, 'text_bytes': text_bytes, 'parallelism': 'dp1'},
+        'phases_ms': {'split': ph[0], 'parse': ph[1], 'order_keys': ph[2], 'classify_aggregate_job': ph[3]},
+        'roofline': {'bound': 'hbm', 'kernel': 'k_parse', 'achieved': parse_gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                     'frac': parse_gbs / HBM_PEAK_GBS, 'traffic': None,
+                     'bytes': 'text bytes read + 32 B/line (off 8, tuple 16, ts 4, disp 4)'},
+        'checks': checks,
+    }
+    print(json.dumps(res), flush=True)
+    return 0
+
+
 def _dump(path, last, eng, cap):
     """TESTING: rank 0 writes the merged (or single-GPU) result as npz."""
     if 'merged' in last:
@@ -602,6 +753,8 @@ def parse_args(argv=None):
     ap.add_argument('--opt', action='append', default=[], help='NAME=VALUE library option (e.g. FILTER_STEPS=3)')
     ap.add_argument('--no-index', action='store_true', help='classify with the plain linear scan')
     ap.add_argument('--prefix', type=int, default=0, help='entries per list scanned before the index')
+    ap.add_argument('--text', action='store_true',
+                    help='the fused job from log text in HBM (GPU parse + order keys + classify + aggregate)')
     return ap.parse_args(argv)
 
 
@@ -611,6 +764,10 @@ def main():
         print(json.dumps(reference_pipeline_baseline(n_lines=args.baseline_lines, procs=args.baseline_procs or None)),
               flush=True)
         return
+    if args.text:
+        if args.gpus != 1 or 'WORLD_SIZE' in os.environ:
+            die('--text runs on one GPU')
+        sys.exit(text_main(args))
     if args.cpu_model and args.backend != 'gloo':
         die('--cpu-model runs without a GPU: use --backend gloo')
     if 'WORLD_SIZE' in os.environ and 'RANK' in os.environ:

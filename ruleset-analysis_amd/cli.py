@@ -4,14 +4,15 @@
   streaming: same CWD files (``config.py``, the DB named by
   ``ACCESSLIST_DATABASE_FILENAME``), same ``mapred_input_dir`` host rule
   (``mapper.py:107-117``), same stdout bytes (``mapper.py:154-155,184-186``);
-  classification runs on the GPU.
+  the log text is parsed (``textparse``) and classified on the GPU.
 * ``reducer_main`` — replaces ``connlist-reducer.py`` (and ``reducer.py``):
   sorted mapper stream on stdin, the reference report on stdout
   (``connlist-reducer.py:62-211``); aggregation runs on the GPU, one group per
   run of equal keys, so even unsorted input prints what the reference prints.
 * ``run_main`` — the fused job (``mapper | sort | reducer`` in one GPU pass):
   ``rsa_run.py --db accesslists.db [--cap N] LOGFILE...``; the host of each
-  file is its parent directory name, as Hadoop's ``mapred_input_dir`` gives it.
+  file is its parent directory name, as Hadoop's ``mapred_input_dir`` gives it;
+  the text is parsed on the GPU, order keys included (``textparse``).
 
 Error behaviour follows the reference: the same exception classes at the same
 validation points (``KeyError`` for a missing ``'in'`` binding or protocol
@@ -27,11 +28,10 @@ import numpy as np
 from . import acldb
 from .compile import CompiledRules, TUPLE_DTYPE, F_HIT, F_BUILT
 from .engine import DeviceBatch, Engine
-from .logparse import parse_logs, reducer_fields, reducer_timestamp, PY2_WS
-from .pipeline import analyze
+from .logparse import reducer_fields, reducer_timestamp, PY2_WS
+from .pipeline import analyze_text
+from .textparse import parse_text
 from .report import mapper_output, reducer_report
-
-CHUNK_LINES = 1 << 22
 
 
 def _stdin_lines():
@@ -86,23 +86,19 @@ def mapper_main(argv=None):
     compiled = CompiledRules(db)
     compiled.ensure_lists()
     eng = Engine(0)
-    loaded = None
-    lines = _stdin_lines()
-    for a in range(0, max(len(lines), 1), CHUNK_LINES):
-        chunk = lines[a:a + CHUNK_LINES]
-        parsed = parse_logs([(hostname, chunk)], db, compiled, need_order=False)
-        if parsed.n:
-            if loaded != compiled.n_lists():
-                eng.load_compiled(compiled)
-                loaded = compiled.n_lists()
-            b = DeviceBatch.from_numpy(parsed.tuples, parsed.ts, parsed.order, eng.device)
-            gids = eng.classify_only(b).cpu().numpy()
-        else:
-            gids = np.zeros(0, np.int32)
-        _write(mapper_output(parsed, gids, compiled))
-        sys.stdout.flush()
-        if parsed.error is not None:
-            raise parsed.error[1]
+    data = sys.stdin.buffer.read()
+    # the log text is parsed on the GPU (textparse); lines outside the device
+    # grammar are decided by the host parser, in line order
+    parsed = parse_text(eng, hostname, data, db, compiled, need_order=False)
+    if parsed.n:
+        eng.load_compiled(compiled)
+        gids = eng.classify_only(parsed.batch()).cpu().numpy()
+    else:
+        gids = np.zeros(0, np.int32)
+    _write(mapper_output(parsed, gids, compiled))
+    sys.stdout.flush()
+    if parsed.error is not None:
+        raise parsed.error[1]
     return 0
 
 
@@ -274,17 +270,7 @@ def run_main(argv=None):
     inputs = []
     for path in args.logs:
         with open(path, 'rb') as f:
-            text = f.read().decode('latin-1')
-        lines, start = [], 0
-        while True:
-            i = text.find('\n', start)
-            if i < 0:
-                if start < len(text):
-                    lines.append(text[start:])
-                break
-            lines.append(text[start:i + 1])
-            start = i + 1
-        inputs.append((args.host or _host_of(path), lines))
+            inputs.append((args.host or _host_of(path), f.read()))
     engine = None
     if args.shadowed:
         from .engine import Engine
@@ -295,7 +281,7 @@ def run_main(argv=None):
                 sys.stderr.write('INFO - ' + m + '\n')
     if not inputs:
         return 0
-    out, _res = analyze(inputs, db, cap=args.cap, engine=engine)
+    out, _res = analyze_text(inputs, db, cap=args.cap, engine=engine)
     if args.postprocess or args.hadoop_output:
         from .postprocess import hadoop_output, postprocess
         k = out.index('') if '' in out else len(out)   # the noise records of the empty mapper records

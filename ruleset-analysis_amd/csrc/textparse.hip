@@ -120,6 +120,23 @@ __global__ __launch_bounds__(kSplitThreads) void k_nl_write(const uint8_t* __res
   const uint32_t mine = seg_count(text, a, n, aligned != 0);
   uint64_t k = incl[blockIdx.x] - counts[blockIdx.x] + block_exscan(mine, sh, &total);
   if (!mine) return;
+  if (aligned && a + kSplitPer <= n) {
+    const uint4* q = reinterpret_cast<const uint4*>(text + a);
+    for (int c = 0; c < 4; ++c) {
+      const uint4 v = q[c];
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+      for (int e = 0; e < 4; ++e) {
+        uint32_t bits = nl_bits(w[e]);
+        while (bits) {
+          const uint32_t byte = (uint32_t)__builtin_ctz(bits) >> 3;
+          bits &= bits - 1;
+          if (k + 1 <= n_lines) off[k + 1] = a + 16 * c + 4 * e + byte + 1;
+          ++k;
+        }
+      }
+    }
+    return;
+  }
   for (uint64_t i = a; i < a + kSplitPer && i < n; ++i)
     if (text[i] == '\n') {
       if (k + 1 <= n_lines) off[k + 1] = i + 1;
@@ -129,19 +146,56 @@ __global__ __launch_bounds__(kSplitThreads) void k_nl_write(const uint8_t* __res
 
 __global__ void k_set_u64(uint64_t* p, uint64_t v) { *p = v; }
 
-__global__ __launch_bounds__(256) void k_parse(const uint8_t* __restrict__ text, const uint64_t* __restrict__ off,
-                                               uint64_t n_lines, const rsa_parse_ifc* __restrict__ ifcs,
-                                               uint32_t n_ifcs, const rsa_parse_spell* __restrict__ spells,
-                                               uint32_t n_spells, rsa_tuple* __restrict__ tuples,
-                                               uint32_t* __restrict__ ts_out, uint32_t* __restrict__ disp) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_lines) return;
+// k_parse: a workgroup stages the text of its kParseWG lines in LDS with
+// coalesced 4-byte loads, then every lane parses its line from LDS through
+// the word-cached accessor (one LDS read per 4 bytes scanned).  A workgroup
+// whose lines do not fit parses straight from HBM with byte loads.
+constexpr uint32_t kParseWG = 128, kStageBytes = 32768;
+
+__global__ __launch_bounds__(kParseWG) void k_parse(const uint8_t* __restrict__ text, const uint64_t* __restrict__ off,
+                                                    uint64_t n_lines, const rsa_parse_ifc* __restrict__ ifcs,
+                                                    uint32_t n_ifcs, const rsa_parse_spell* __restrict__ spells,
+                                                    uint32_t n_spells, rsa_tuple* __restrict__ tuples,
+                                                    uint32_t* __restrict__ ts_out, uint32_t* __restrict__ disp) {
+  __shared__ uint32_t sm[kStageBytes / 4];
+  const uint64_t l0 = (uint64_t)blockIdx.x * kParseWG;
+  const uint64_t l1 = l0 + kParseWG < n_lines ? l0 + kParseWG : n_lines;
+  const uint64_t n_bytes = off[n_lines];
+  const uint64_t base = off[l0] & ~3ull, span = off[l1] - base;
+  const bool staged = span <= kStageBytes;   // workgroup-uniform
+  if (staged) {
+    const uint32_t nw = (uint32_t)((span + 3) / 4);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(text + base);
+    for (uint32_t w = threadIdx.x; w < nw; w += blockDim.x) {
+      const uint64_t at = base + 4ull * w;
+      uint32_t x;
+      if (at + 4 <= n_bytes) {
+        x = src[w];
+      } else {
+        x = 0;
+        for (uint32_t k = 0; k < 4; ++k)
+          if (at + k < n_bytes) x |= (uint32_t)text[at + k] << (8 * k);
+      }
+      sm[w] = x;
+    }
+  }
+  __syncthreads();
+  const uint64_t i = l0 + threadIdx.x;
+  if (i >= l1) return;
   const uint64_t a = off[i], b = off[i + 1];
   uint64_t len = b - a;
   if (len && text[b - 1] == '\n') --len;
-  rsa_tuple tup;
-  uint32_t ts, d;
-  rsa_text::parse_line(text, a, len, ifcs, n_ifcs, spells, n_spells, tup, ts, d);
+  rsa_tuple tup = {0u, 0u, 0, 0, 0, 0, 0};
+  uint32_t ts = 0, d = RSA_LINE_HOST;
+  if (len < 0xFFFFFFFFull) {
+    if (staged) {
+      const rsa_text::WordLn s{sm, (uint32_t)(a - base), (uint32_t)len, 0xFFFFFFFFu, 0u};
+      rsa_text::parse_line(s, ifcs, n_ifcs, spells, n_spells, tup, ts, d);
+    } else {
+      const rsa_text::ByteLn s{text + a, (uint32_t)len};
+      rsa_text::parse_line(s, ifcs, n_ifcs, spells, n_spells, tup, ts, d);
+    }
+  }
   tuples[i] = tup;
   ts_out[i] = ts;
   disp[i] = d;
@@ -154,23 +208,41 @@ __global__ __launch_bounds__(256) void k_parse(const uint8_t* __restrict__ text,
 // first).  A line is settled once its group (equal keys so far) is a singleton
 // or its bytes ended in this window (then the whole group is equal strings,
 // already in line-index order: the sorts are stable).
-__device__ __forceinline__ uint64_t chunk_key(const uint8_t* __restrict__ text, const uint64_t* __restrict__ off,
-                                              uint32_t line, uint32_t round) {
-  const uint64_t a = off[line], b = off[line + 1];
-  uint64_t len = b - a;
-  if (len && text[b - 1] == '\n') --len;
+__device__ __forceinline__ uint64_t chunk_key(const uint8_t* __restrict__ text, uint64_t n_bytes, uint64_t a,
+                                              uint32_t len, uint32_t round) {
   const uint64_t pos = (uint64_t)round * 7;
-  const uint64_t rem = len > pos ? len - pos : 0;
-  uint64_t k = 0;
-  for (int j = 0; j < 7; ++j) k = k << 8 | ((uint64_t)j < rem ? text[a + pos + j] : 0u);
-  return k << 8 | (rem < 8 ? rem : 8);
+  const uint32_t rem = len > pos ? (uint32_t)(len - pos) : 0u;
+  if (!rem) return 0;
+  const uint64_t p = a + pos;
+  uint64_t k;
+  if (p + 12 <= n_bytes) {   // three aligned words hold bytes p .. p + 6 (text is 4-byte aligned)
+    const uint32_t* t32 = reinterpret_cast<const uint32_t*>(text);
+    const uint64_t q = p >> 2;
+    const uint32_t sh = (uint32_t)(p & 3) * 8;
+    const uint64_t lo = (uint64_t)t32[q] | ((uint64_t)t32[q + 1] << 32);
+    const uint64_t x = sh ? (lo >> sh) | ((uint64_t)t32[q + 2] << (64 - sh)) : lo;   // bytes p .. p + 7, little endian
+    k = __builtin_bswap64(x) & ~0xFFull;                                               // b0 .. b6 big endian, << 8
+    if (rem < 7) k &= ~0ull << (64 - 8 * rem);
+  } else {
+    k = 0;
+    for (uint32_t j = 0; j < 7; ++j) k = k << 8 | (j < rem ? text[p + j] : 0u);
+    k <<= 8;
+  }
+  return k | (rem < 8 ? rem : 8u);
 }
 
+// round 0: every line's length without '\n' (kept for the later rounds) and its first key
 __global__ void k_keys0(const uint8_t* __restrict__ text, const uint64_t* __restrict__ off, uint32_t n,
-                        uint64_t* __restrict__ keys, uint32_t* __restrict__ ids) {
+                        uint64_t n_bytes, uint32_t* __restrict__ lens, uint64_t* __restrict__ keys,
+                        uint32_t* __restrict__ ids) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
-  keys[j] = chunk_key(text, off, j, 0);
+  const uint64_t a = off[j], b = off[j + 1];
+  uint64_t len = b - a;
+  if (len && text[b - 1] == '\n') --len;
+  const uint32_t l32 = len < 0xFFFFFFFFull ? (uint32_t)len : 0xFFFFFFFFu;
+  lens[j] = l32;
+  keys[j] = chunk_key(text, n_bytes, a, l32, 0);
   ids[j] = j;
 }
 
@@ -178,21 +250,45 @@ struct Act {               // an unsettled line: its id and the position its gro
   uint32_t id, gs;
 };
 
-__global__ void k_keys(const uint8_t* __restrict__ text, const uint64_t* __restrict__ off, const Act* __restrict__ act,
-                       uint32_t m, uint32_t round, uint64_t* __restrict__ keys, uint64_t* __restrict__ vals) {
+__global__ void k_keys(const uint8_t* __restrict__ text, const uint64_t* __restrict__ off,
+                       const uint32_t* __restrict__ lens, uint64_t n_bytes, const Act* __restrict__ act, uint32_t m,
+                       uint32_t round, uint64_t* __restrict__ keys, uint64_t* __restrict__ vals) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= m) return;
   const Act x = act[j];
-  keys[j] = chunk_key(text, off, x.id, round);
+  keys[j] = chunk_key(text, n_bytes, off[x.id], lens[x.id], round);
   vals[j] = (uint64_t)x.gs << 32 | x.id;
 }
 
-__global__ void k_split_gs(const uint64_t* __restrict__ vals, uint32_t m, uint32_t* __restrict__ gs,
-                           uint32_t* __restrict__ ids) {
+// 1 if this round can change anything: a group whose keys differ, or a line
+// that ends in this window (else the round is skipped: no sort, no settle)
+__global__ void k_round_live(const uint64_t* __restrict__ keys, const Act* __restrict__ act, uint32_t m,
+                             uint32_t* __restrict__ live) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const bool ended = (keys[j] & 0xFFu) < 8u;
+  const bool split = j > 0 && act[j].gs == act[j - 1].gs && keys[j] != keys[j - 1];
+  if (ended || split) *live = 1u;
+}
+
+__global__ void k_gs_iota(const uint64_t* __restrict__ vals, uint32_t m, uint32_t* __restrict__ gs,
+                          uint32_t* __restrict__ idx) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= m) return;
   gs[j] = (uint32_t)(vals[j] >> 32);
-  ids[j] = (uint32_t)vals[j];
+  idx[j] = j;
+}
+
+__global__ void k_gather(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ vals,
+                         const uint32_t* __restrict__ perm, uint32_t m, uint64_t* __restrict__ keys_out,
+                         uint32_t* __restrict__ gs, uint32_t* __restrict__ ids) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const uint32_t q = perm[j];
+  keys_out[j] = keys[q];
+  const uint64_t v = vals[q];
+  gs[j] = (uint32_t)(v >> 32);
+  ids[j] = (uint32_t)v;
 }
 
 // first index of each gs run (max-scan input): j at a run start, else 0
@@ -333,9 +429,11 @@ int rsa_parse_text(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_off, uin
   if (ib) TPCHK(c, hipMemcpyAsync(d_ifcs, h_ifcs, ib, hipMemcpyHostToDevice, st));
   if (sb) TPCHK(c, hipMemcpyAsync(d_spells, h_spells, sb, hipMemcpyHostToDevice, st));
   TPCHK(c, hipStreamSynchronize(st));   // the host tables may go away after return
-  const uint64_t nb = (n_lines + 255) / 256;
+  if (reinterpret_cast<uintptr_t>(d_text) & 3u)
+    return rsa_internal_fail(c, RSA_ERR_ARG, "rsa_parse_text: d_text must be 4-byte aligned");
+  const uint64_t nb = (n_lines + kParseWG - 1) / kParseWG;
   if (nb > 0x7FFFFFFFull) return rsa_internal_fail(c, RSA_ERR_ARG, "too many lines");
-  hipLaunchKernelGGL(k_parse, dim3((uint32_t)nb), dim3(256), 0, st, d_text, d_off, n_lines, d_ifcs, n_ifcs, d_spells,
+  hipLaunchKernelGGL(k_parse, dim3((uint32_t)nb), dim3(kParseWG), 0, st, d_text, d_off, n_lines, d_ifcs, n_ifcs, d_spells,
                      n_spells, d_tuples, d_ts, d_disp);
   TPCHK(c, hipGetLastError());
   return RSA_OK;
@@ -345,17 +443,21 @@ int rsa_order_keys(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_off, uin
                    uint64_t* d_order) {
   if (!c || (n_lines && (!d_text || !d_off || !d_order))) return RSA_ERR_ARG;
   if (n_lines >= 0x7FFFFFFFull) return rsa_internal_fail(c, RSA_ERR_ARG, "rsa_order_keys: too many lines");
+  if (reinterpret_cast<uintptr_t>(d_text) & 3u)
+    return rsa_internal_fail(c, RSA_ERR_ARG, "rsa_order_keys: d_text must be 4-byte aligned");
   if (!n_lines) return RSA_OK;
   hipStream_t st = rsa_internal_stream(c);
   const uint32_t n = (uint32_t)n_lines;
   // temp sizes of every primitive at the largest size
   size_t t_sort64 = 0, t_sort0 = 0, t_sort32 = 0, t_scan = 0, t_exscan = 0;
+  unsigned gbits = 1;
+  while (gbits < 32 && (1ull << gbits) < (uint64_t)n) ++gbits;
   TPCHK(c, rocprim::radix_sort_pairs(nullptr, t_sort0, (uint64_t*)nullptr, (uint64_t*)nullptr, (uint32_t*)nullptr,
                                      (uint32_t*)nullptr, (size_t)n, 0, 64, st));
   TPCHK(c, rocprim::radix_sort_pairs(nullptr, t_sort64, (uint64_t*)nullptr, (uint64_t*)nullptr, (uint64_t*)nullptr,
                                      (uint64_t*)nullptr, (size_t)n, 0, 64, st));
-  TPCHK(c, rocprim::radix_sort_pairs(nullptr, t_sort32, (uint32_t*)nullptr, (uint32_t*)nullptr, (uint64_t*)nullptr,
-                                     (uint64_t*)nullptr, (size_t)n, 0, 32, st));
+  TPCHK(c, rocprim::radix_sort_pairs(nullptr, t_sort32, (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                     (uint32_t*)nullptr, (size_t)n, 0, 32, st));
   TPCHK(c, rocprim::inclusive_scan(nullptr, t_scan, (uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)n,
                                    rocprim::maximum<uint32_t>(), st));
   TPCHK(c, rocprim::exclusive_scan(nullptr, t_exscan, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u, (size_t)n,
@@ -368,7 +470,7 @@ int rsa_order_keys(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_off, uin
   tmp = (tmp + 255) / 256 * 256;
   const size_t N = ((size_t)n + 63) / 64 * 64;
   // keysA/keysB u64, valsA/valsB u64, gs/ids/first/pos/bstart/keep/slot u32, act/act2 Act, count
-  const size_t bytes = tmp + N * (8 * 4 + 4 * 7 + 8 * 2) + 256;
+  const size_t bytes = tmp + N * (8 * 4 + 4 * 8 + 8 * 2) + 256;
   Scratch S{c, st};
   TPCHK(c, hipMallocAsync(&S.base, bytes, st));
   char* p = static_cast<char*>(S.base);
@@ -387,12 +489,15 @@ int rsa_order_keys(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_off, uin
   uint32_t* slot = reinterpret_cast<uint32_t*>(p); p += N * 4;
   Act* act = reinterpret_cast<Act*>(p); p += N * 8;
   Act* act2 = reinterpret_cast<Act*>(p); p += N * 8;
+  uint32_t* lens = reinterpret_cast<uint32_t*>(p); p += N * 4;
   uint32_t* idsA = reinterpret_cast<uint32_t*>(valsA);   // round 0 reuses the value arrays as u32 ids
   uint32_t* idsB = reinterpret_cast<uint32_t*>(valsB);
-  (void)act2;
 
   // round 0: all lines
-  hipLaunchKernelGGL(k_keys0, dim3(blocks(n, 256)), dim3(256), 0, st, d_text, d_off, n, keysA, idsA);
+  uint64_t n_bytes = 0;
+  TPCHK(c, hipMemcpyAsync(&n_bytes, d_off + n, 8, hipMemcpyDeviceToHost, st));
+  TPCHK(c, hipStreamSynchronize(st));
+  hipLaunchKernelGGL(k_keys0, dim3(blocks(n, 256)), dim3(256), 0, st, d_text, d_off, n, n_bytes, lens, keysA, idsA);
   size_t tt = tmp;
   TPCHK(c, rocprim::radix_sort_pairs(t, tt, keysA, keysB, idsA, idsB, (size_t)n, 0, 64, st));
   hipLaunchKernelGGL(k_bounds, dim3(blocks(n, 256)), dim3(256), 0, st, keysB, (const uint32_t*)nullptr,
@@ -409,17 +514,25 @@ int rsa_order_keys(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_off, uin
   TPCHK(c, hipMemcpyAsync(&lastk, keep + n - 1, 4, hipMemcpyDeviceToHost, st));
   TPCHK(c, hipStreamSynchronize(st));
   m += lastk;
+  uint32_t* live = reinterpret_cast<uint32_t*>(act2);   // act2 is spare: one flag word
   for (uint32_t round = 1; m > 0; ++round) {
-    hipLaunchKernelGGL(k_keys, dim3(blocks(m, 256)), dim3(256), 0, st, d_text, d_off, act, m, round, keysA, valsA);
+    hipLaunchKernelGGL(k_keys, dim3(blocks(m, 256)), dim3(256), 0, st, d_text, d_off, lens, n_bytes, act, m, round,
+                       keysA, valsA);
+    // rounds inside a shared prefix (e.g. lines of one second share ~90 bytes)
+    // change nothing: detect them with one pass and skip the sorts
+    TPCHK(c, hipMemsetAsync(live, 0, 4, st));
+    hipLaunchKernelGGL(k_round_live, dim3(blocks(m, 256)), dim3(256), 0, st, keysA, act, m, live);
+    uint32_t h_live = 0;
+    TPCHK(c, hipMemcpyAsync(&h_live, live, 4, hipMemcpyDeviceToHost, st));
+    TPCHK(c, hipStreamSynchronize(st));
+    if (!h_live) continue;
     tt = tmp;   // stable LSD: by the chunk key, then by the group start
     TPCHK(c, rocprim::radix_sort_pairs(t, tt, keysA, keysB, valsA, valsB, (size_t)m, 0, 64, st));
-    hipLaunchKernelGGL(k_split_gs, dim3(blocks(m, 256)), dim3(256), 0, st, valsB, m, gs, ids);
-    tt = tmp;
-    TPCHK(c, rocprim::radix_sort_pairs(t, tt, gs, first, keysB, keysA, (size_t)m, 0, 32, st));
-    tt = tmp;
-    TPCHK(c, rocprim::radix_sort_pairs(t, tt, gs, pos, valsB, valsA, (size_t)m, 0, 32, st));
-    // now: first = gs sorted, keysA = chunk keys, valsA = gs<<32|id in (gs, key) order
-    hipLaunchKernelGGL(k_split_gs, dim3(blocks(m, 256)), dim3(256), 0, st, valsA, m, gs, ids);
+    hipLaunchKernelGGL(k_gs_iota, dim3(blocks(m, 256)), dim3(256), 0, st, valsB, m, gs, ids);
+    tt = tmp;   // by group start (only the bits a position can have), carrying the index
+    TPCHK(c, rocprim::radix_sort_pairs(t, tt, gs, first, ids, pos, (size_t)m, 0, gbits, st));
+    hipLaunchKernelGGL(k_gather, dim3(blocks(m, 256)), dim3(256), 0, st, keysB, valsB, pos, m, keysA, gs, ids);
+    // now keysA / gs / ids are in (group start, chunk key) order
     hipLaunchKernelGGL(k_run_first, dim3(blocks(m, 256)), dim3(256), 0, st, gs, m, bstart);
     tt = tmp;
     TPCHK(c, rocprim::inclusive_scan(t, tt, bstart, first, (size_t)m, rocprim::maximum<uint32_t>(), st));

@@ -19,10 +19,25 @@ namespace rsa_text {
 #define RSA_HD __host__ __device__ __forceinline__
 
 // One lane per line, bytes read through the line accessor.
-struct Ln {
+// Line accessors: s[i] = byte i of the line, s.n = its length without '\n'.
+struct ByteLn {              // plain byte loads (any buffer)
   const uint8_t* p;
-  uint32_t n;   // length without the '\n' terminator
+  uint32_t n;
   RSA_HD uint32_t operator[](uint32_t i) const { return p[i]; }
+};
+struct WordLn {              // 4-byte loads with a one-word cache: a scan reads each word once
+  const uint32_t* w32;       // 4-byte aligned buffer, readable up to the word holding the line's last byte
+  uint32_t o;                // byte offset of the line in it
+  uint32_t n;
+  mutable uint32_t ci, cw;
+  RSA_HD uint32_t operator[](uint32_t i) const {
+    const uint32_t pos = o + i, wi = pos >> 2;
+    if (wi != ci) {
+      ci = wi;
+      cw = w32[wi];
+    }
+    return (cw >> ((pos & 3u) * 8u)) & 0xFFu;
+  }
 };
 
 RSA_HD bool is_dig(uint32_t c) { return c - '0' < 10u; }
@@ -39,14 +54,14 @@ RSA_HD bool in_cls(uint32_t c) {
   return C == kDig ? is_dig(c) : C == kAlpha ? is_alpha(c) : C == kIfc ? is_ifc(c) : C == kIp ? is_ipch(c) : is_tsch(c);
 }
 // end of the run of class C starting at p
-template <int C>
-RSA_HD uint32_t run(const Ln& s, uint32_t p) {
+template <int C, class S>
+RSA_HD uint32_t run(const S& s, uint32_t p) {
   while (p < s.n && in_cls<C>(s[p])) ++p;
   return p;
 }
 // s[p ..] starts with the literal
-template <int N>
-RSA_HD bool lit(const Ln& s, uint32_t p, const char (&w)[N]) {
+template <class S, int N>
+RSA_HD bool lit(const S& s, uint32_t p, const char (&w)[N]) {
   if (p + (N - 1) > s.n) return false;
 #pragma unroll
   for (int i = 0; i < N - 1; ++i)
@@ -54,15 +69,16 @@ RSA_HD bool lit(const Ln& s, uint32_t p, const char (&w)[N]) {
   return true;
 }
 // largest k in [lo, hi] where the literal starts, or -1
-template <int N>
-RSA_HD int64_t last_lit(const Ln& s, int64_t lo, int64_t hi, const char (&w)[N]) {
+template <class S, int N>
+RSA_HD int64_t last_lit(const S& s, int64_t lo, int64_t hi, const char (&w)[N]) {
   if (hi > (int64_t)s.n - (N - 1)) hi = (int64_t)s.n - (N - 1);
   for (int64_t k = hi; k >= lo; --k)
     if (lit(s, (uint32_t)k, w)) return k;
   return -1;
 }
 // \d\d:\d\d:\d\d
-RSA_HD bool hms(const Ln& s, uint32_t p) {
+template <class S>
+RSA_HD bool hms(const S& s, uint32_t p) {
   return p + 8 <= s.n && is_dig(s[p]) && is_dig(s[p + 1]) && s[p + 2] == ':' && is_dig(s[p + 3]) &&
          is_dig(s[p + 4]) && s[p + 5] == ':' && is_dig(s[p + 6]) && is_dig(s[p + 7]);
 }
@@ -77,7 +93,8 @@ struct Mapped {             // get_builtconn's fields
 };
 
 // The rest of logparse._GB after `.*?`, at the '%' + 1 position p.
-RSA_HD bool gb_rest(const Ln& s, uint32_t p, Mapped& m) {
+template <class S>
+RSA_HD bool gb_rest(const S& s, uint32_t p, Mapped& m) {
   if (lit(s, p, "ASA")) p += 3;
   else if (lit(s, p, "FWSM")) p += 4;
   else if (lit(s, p, "PIX")) p += 3;
@@ -145,7 +162,8 @@ RSA_HD bool gb_rest(const Ln& s, uint32_t p, Mapped& m) {
 // '%' positions (the first one whose rest matches wins).  The optional group
 // is taken when it matches: skipping it cannot change the outcome, since its
 // text holds no '%'.
-RSA_HD bool gb_match(const Ln& s, Mapped& m) {
+template <class S>
+RSA_HD bool gb_match(const S& s, Mapped& m) {
   if (s.n < 3 || !is_upper(s[0]) || !is_lower(s[1]) || !is_lower(s[2])) return false;
   uint32_t p = 3;
   if (p >= s.n || s[p] != ' ') return false;
@@ -183,7 +201,8 @@ struct Reduced {            // connlist-reducer.py:25 BUILT captures used downst
 
 // After `[a-zA-Z]+ [0-9 ]?[0-9] `: groups 1-4, then the three greedy `.*`
 // (candidates tried from the last occurrence down, nested as the engine does).
-RSA_HD bool built_tail(const Ln& s, uint32_t p, Reduced& r) {
+template <class S>
+RSA_HD bool built_tail(const S& s, uint32_t p, Reduced& r) {
   uint32_t e = run<kTs>(s, p);
   if (e == p || e >= s.n || s[e] != ' ') return false;
   r.time = {p, e};
@@ -248,7 +267,8 @@ RSA_HD bool built_tail(const Ln& s, uint32_t p, Reduced& r) {
 // BUILT.search(line): leftmost start.  A start inside a letter run has the
 // same continuation as the run's first letter, so only run starts are tried;
 // `[0-9 ]?` is tried taken, then skipped.
-RSA_HD bool built_search(const Ln& s, Reduced& r) {
+template <class S>
+RSA_HD bool built_search(const S& s, Reduced& r) {
   for (uint32_t s0 = 0; s0 < s.n; ++s0) {
     if (!is_alpha(s[s0])) continue;
     const uint32_t e = run<kAlpha>(s, s0);
@@ -264,14 +284,16 @@ RSA_HD bool built_search(const Ln& s, Reduced& r) {
   return false;
 }
 
-RSA_HD bool hit_test(const Ln& s) {   // '-6-302013' / '-6-302015' anywhere (connlist-reducer.py:146)
+template <class S>
+RSA_HD bool hit_test(const S& s) {   // '-6-302013' / '-6-302015' anywhere (connlist-reducer.py:146)
   if (s.n < 9) return false;
   for (uint32_t k = 0; k + 9 <= s.n; ++k)
     if (s[k] == '-' && s[k + 1] == '6' && lit(s, k + 2, "-30201") && (s[k + 8] == '3' || s[k + 8] == '5')) return true;
   return false;
 }
 
-RSA_HD bool span_eq(const Ln& s, Span x, Span y) {
+template <class S>
+RSA_HD bool span_eq(const S& s, Span x, Span y) {
   if (x.b - x.a != y.b - y.a) return false;
   for (uint32_t i = 0; i < x.b - x.a; ++i)
     if (s[x.a + i] != s[y.a + i]) return false;
@@ -279,7 +301,8 @@ RSA_HD bool span_eq(const Ln& s, Span x, Span y) {
 }
 
 // canonical dotted quad (what str(IP) prints back) -> value
-RSA_HD bool ipv4_canon(const Ln& s, Span x, uint32_t& v) {
+template <class S>
+RSA_HD bool ipv4_canon(const S& s, Span x, uint32_t& v) {
   uint32_t p = x.a, val = 0;
   for (int o = 0; o < 4; ++o) {
     const uint32_t e = run<kDig>(s, p);
@@ -300,7 +323,8 @@ RSA_HD bool ipv4_canon(const Ln& s, Span x, uint32_t& v) {
 }
 
 // int(text) of a digit run, saturating above 65535 (the caller defers those)
-RSA_HD uint32_t port_val(const Ln& s, Span x) {
+template <class S>
+RSA_HD uint32_t port_val(const S& s, Span x) {
   uint32_t v = 0;
   for (uint32_t i = x.a; i < x.b; ++i) {
     v = v * 10 + (s[i] - '0');
@@ -309,9 +333,11 @@ RSA_HD uint32_t port_val(const Ln& s, Span x) {
   return v;
 }
 
-RSA_HD bool port_canon(const Ln& s, Span x) { return x.b - x.a == 1 || s[x.a] != '0'; }
+template <class S>
+RSA_HD bool port_canon(const S& s, Span x) { return x.b - x.a == 1 || s[x.a] != '0'; }
 
-RSA_HD uint32_t small_num(const Ln& s, Span x) {   // <= 4 digits
+template <class S>
+RSA_HD uint32_t small_num(const S& s, Span x) {   // <= 4 digits
   uint32_t v = 0;
   for (uint32_t i = x.a; i < x.b; ++i) v = v * 10 + (s[i] - '0');
   return v;
@@ -319,7 +345,8 @@ RSA_HD uint32_t small_num(const Ln& s, Span x) {   // <= 4 digits
 
 // connlist-reducer.py:163-165 as a code: year(4 digits, 2000..2127)-MM-DD
 // (day zfill(2) <= 31) HH:MM:SS (h < 24, m, s < 60); false = not codable
-RSA_HD bool ts_code(const Ln& s, const Reduced& r, uint32_t& code) {
+template <class S>
+RSA_HD bool ts_code(const S& s, const Reduced& r, uint32_t& code) {
   const char* const months = "JanFebMarAprMayJunJulAugSepOctNovDec";
   if (r.mon.b - r.mon.a != 3) return false;
   int mo = -1;
@@ -343,15 +370,12 @@ RSA_HD bool ts_code(const Ln& s, const Reduced& r, uint32_t& code) {
 }
 
 // The whole line: disposition (RSA_LINE_* | interface << 8), tuple, timestamp code.
-RSA_HD void parse_line(const uint8_t* text, uint64_t a, uint64_t len, const rsa_parse_ifc* ifcs, uint32_t n_ifcs,
-                       const rsa_parse_spell* spells, uint32_t n_spells, rsa_tuple& tup_out, uint32_t& ts_out,
-                       uint32_t& d_out) {
+template <class S>
+RSA_HD void parse_line(const S& s, const rsa_parse_ifc* ifcs, uint32_t n_ifcs, const rsa_parse_spell* spells,
+                       uint32_t n_spells, rsa_tuple& tup_out, uint32_t& ts_out, uint32_t& d_out) {
   rsa_tuple tup = {0u, 0u, 0, 0, 0, 0, 0};
   uint32_t ts = 0, d = RSA_LINE_IGNORE;
-  if (len >= 0xFFFFFFFFull) {
-    d = RSA_LINE_HOST;
-  } else {
-    const Ln s{text + a, (uint32_t)len};
+  {
     Mapped m;
     if (gb_match(s, m)) {
       d = RSA_LINE_CLASSIFY;

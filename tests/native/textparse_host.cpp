@@ -4,13 +4,22 @@
 // infrastructure only: nothing in the product loads this library.
 #include "../../ruleset-analysis_amd/csrc/textparse_line.h"
 
+// text: 4-byte aligned, readable up to a multiple of 4 bytes past off[n];
+// word = 1 parses through the word-cached accessor (the device's LDS path),
+// 0 through byte loads (its fallback path).
 extern "C" void parse_lines_host(const uint8_t* text, const uint64_t* off, uint64_t n, const rsa_parse_ifc* ifcs,
                                  uint32_t n_ifcs, const rsa_parse_spell* spells, uint32_t n_spells,
-                                 rsa_tuple* tuples, uint32_t* ts, uint32_t* disp) {
+                                 rsa_tuple* tuples, uint32_t* ts, uint32_t* disp, int word) {
   for (uint64_t i = 0; i < n; ++i) {
     const uint64_t a = off[i], b = off[i + 1];
     uint64_t len = b - a;
     if (len && text[b - 1] == '\n') --len;
-    rsa_text::parse_line(text, a, len, ifcs, n_ifcs, spells, n_spells, tuples[i], ts[i], disp[i]);
+    if (word) {
+      const rsa_text::WordLn s{reinterpret_cast<const uint32_t*>(text), (uint32_t)a, (uint32_t)len, 0xFFFFFFFFu, 0u};
+      rsa_text::parse_line(s, ifcs, n_ifcs, spells, n_spells, tuples[i], ts[i], disp[i]);
+    } else {
+      const rsa_text::ByteLn s{text + a, (uint32_t)len};
+      rsa_text::parse_line(s, ifcs, n_ifcs, spells, n_spells, tuples[i], ts[i], disp[i]);
+    }
   }
 }

@@ -182,7 +182,7 @@ def _harness():
     return ctypes.CDLL(out)
 
 
-def _device_stage_on_cpu(lib, host, lines, db, compiled, spells):
+def _device_stage_on_cpu(lib, host, lines, db, compiled, spells, word=1):
     data = ''.join(lines).encode('latin-1')
     off = np.cumsum([0] + [len(l) for l in lines]).astype(np.uint64)
     ifcs, names = textparse.interface_table(db, compiled, host)
@@ -191,15 +191,16 @@ def _device_stage_on_cpu(lib, host, lines, db, compiled, spells):
     tup = np.zeros(n, TUPLE_DTYPE)
     ts = np.zeros(n, np.uint32)
     disp = np.zeros(n, np.uint32)
-    buf = np.frombuffer(data, np.uint8) if data else np.zeros(1, np.uint8)
+    buf = np.zeros((len(data) + 8) // 4 * 4, np.uint8)      # 4-byte aligned, padded
+    buf[:len(data)] = np.frombuffer(data, np.uint8)
     p = lambda a: a.ctypes.data_as(ctypes.c_void_p)
     lib.parse_lines_host(p(buf), p(off), ctypes.c_uint64(n), p(ifcs), ctypes.c_uint32(len(ifcs)), p(sp),
-                         ctypes.c_uint32(len(sp)), p(tup), p(ts), p(disp))
+                         ctypes.c_uint32(len(sp)), p(tup), p(ts), p(disp), ctypes.c_int(word))
     return tup, ts, disp, names
 
 
-@pytest.mark.parametrize('seed', [1, 2, 3])
-def test_device_line_parser_on_cpu_equals_host_parser(seed):
+@pytest.mark.parametrize('seed,word', [(1, 1), (2, 1), (3, 0)])
+def test_device_line_parser_on_cpu_equals_host_parser(seed, word):
     """Every line the device parser decides itself (not RSA_LINE_HOST) gets
     exactly the host parser's disposition, tuple, list, spelling and
     timestamp string; a line the host parser fails on is never decided."""
@@ -207,7 +208,7 @@ def test_device_line_parser_on_cpu_equals_host_parser(seed):
     db, lines = _fuzz_lines(seed, 8000)
     spells = list(textparse.DEFAULT_SPELLS)
     cg = CompiledRules(db)
-    tup, ts, disp, names = _device_stage_on_cpu(lib, 'fw1', lines, db, cg, spells)
+    tup, ts, disp, names = _device_stage_on_cpu(lib, 'fw1', lines, db, cg, spells, word)
     kind = disp & 0xFF
     n_host = 0
     seen = set()
