@@ -114,7 +114,7 @@ typedef struct rsa_pht_table {
 typedef struct rsa_pht_group {   /* 80 B */
   uint32_t src_mask, dst_mask;
   uint32_t min_idx;          /* smallest record-local entry index in the group    */
-  uint32_t n_real;           /* classes with a real table                         */
+  uint32_t class_mask;       /* bit c: port class c has a real table (else it points at word 0) */
   rsa_pht_table table[4];    /* port classes any, dport, sport, sport+dport       */
 } rsa_pht_group;
 

@@ -246,6 +246,8 @@ def run_main(argv=None):
     src.add_argument('--db', help='accesslists.db (shelve) or .json')
     src.add_argument('--fortigate', help='a FortiGate config: the rule DB preprosess_fortigate_acl.py would store '
                                          '(restated, ruleset-analysis_amd/fortigate.py)')
+    src.add_argument('--asa', help='a Cisco ASA/FWSM config: the rule DB preprosess_access_lists.py would store '
+                                   '(restated, ruleset-analysis_amd/asa.py)')
     ap.add_argument('--cap', type=int, default=1000, help='MAX_NUMBER_OF_CONNECTIONS_PER_RULE')
     ap.add_argument('--host', help='firewall host for every input (default: parent directory name)')
     ap.add_argument('--hadoop-output', action='store_true',
@@ -261,6 +263,11 @@ def run_main(argv=None):
     args = ap.parse_args(argv)
     if args.db:
         db = acldb.load(args.db)
+    elif args.asa:
+        from . import asa
+        with open(args.asa, encoding='latin-1') as f:
+            text = f.read()
+        db = asa.build_db(text, timestamp=os.stat(args.asa).st_mtime, log=lambda m: sys.stderr.write(m))
     else:
         from . import fortigate
         with open(args.fortigate, encoding='latin-1') as f:

@@ -517,7 +517,7 @@ def _index_record(img, rec, e, pre, min_entries, max_groups):
         for j, ((sm, dm), tabs) in enumerate(groups):
             g = grec[PHT_GROUP_WORDS * j: PHT_GROUP_WORDS * (j + 1)]
             g[0], g[1] = sm, dm
-            mins, real = [], 0
+            mins, real = [], 0          # real: bit c = port class c has a table
             ss, ds = set(), set()
             for c, pm in enumerate(PORT_CLASSES):
                 keys = tabs.get(pm)
@@ -539,7 +539,7 @@ def _index_record(img, rec, e, pre, min_entries, max_groups):
                 H, idx = H[~dup], idx[~dup]
                 g[4 + 4 * c: 8 + 4 * c] = img.table(H, idx)
                 mins.append(int(idx.min()))
-                real += 1
+                real |= 1 << c
             g[2] = min(mins)
             g[3] = real
             src_sets.append(ss)

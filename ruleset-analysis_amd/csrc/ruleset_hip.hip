@@ -579,26 +579,6 @@ __device__ __forceinline__ Slot* table_find(const Agg& A, unsigned long long kA,
   return nullptr;
 }
 
-// Workgroup-aggregated append to one global cursor: one device atomic per
-// workgroup call.  Every thread of the workgroup must call it
-// (workgroup-uniform control flow).  sh: 2 LDS words, sh[0] zero on entry.
-__device__ __forceinline__ unsigned long long block_append(bool a, unsigned long long* cur, unsigned long long* sh) {
-  const unsigned long long ma = __ballot(a);
-  const unsigned lane = __lane_id();
-  unsigned long long wa = 0;
-  if (lane == 0 && ma) wa = atomicAdd(&sh[0], (unsigned long long)__popcll(ma));
-  wa = __shfl(wa, 0);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    sh[1] = sh[0] ? atomicAdd(cur, sh[0]) : 0ull;
-    sh[0] = 0;
-  }
-  __syncthreads();
-  const unsigned long long pos = sh[1] + wa + __popcll(ma & ((1ull << lane) - 1ull));
-  __syncthreads();   // sh[1] is rewritten by the next call
-  return pos;
-}
-
 struct alignas(32) Rec {
   unsigned long long kA, kB, order;
   uint32_t ts, region;
@@ -707,8 +687,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kIm
     const uint4* __restrict__ T, unsigned long long n, int32_t* __restrict__ gout, Rules R, unsigned int* flags,
     uint32_t* tail, unsigned long long* tail_n, Agg A, Emit E) {
   __shared__ __attribute__((aligned(16))) uint32_t lds_img[kImg > 0 ? kImg : 4];
-  __shared__ unsigned long long lds_app[2];
-  if (threadIdx.x < 2) lds_app[threadIdx.x] = 0;
   if (kImg > 0 && R.indexed) {
     const uint4* src = reinterpret_cast<const uint4*>(R.img);
     uint4* dst = reinterpret_cast<uint4*>(lds_img);
@@ -730,9 +708,14 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kIm
       gid = classify_wave<false>(t, valid, R, R.img, flags);
     }
     const bool defer = gid == kDefer;
-    if (__syncthreads_or(defer)) {   // rare: workgroup-aggregated append
-      const unsigned long long pos = block_append(defer, tail_n, lds_app);
-      if (defer) tail[pos] = (uint32_t)i;
+    const unsigned long long dm = __ballot(defer);
+    if (dm) {   // rare: one device atomic per wave (no workgroup barrier in the loop)
+      const int leader = __builtin_ctzll(dm);
+      unsigned long long pos = 0;
+      if ((int)__lane_id() == leader) pos = atomicAdd(tail_n, (unsigned long long)__popcll(dm));
+      pos = ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(pos >> 32), leader) << 32) |
+            __builtin_amdgcn_readlane((uint32_t)pos, leader);
+      if (defer) tail[pos + __popcll(dm & ((1ull << __lane_id()) - 1ull))] = (uint32_t)i;
     }
     if (gout && in && !defer) gout[i] = (int32_t)gid;
     if (kEmit) emit_wave(i, n32, in && !defer, t, gid, A, E);
@@ -2492,10 +2475,16 @@ int rsa_load_index(rsa_ctx* c, const uint32_t* img, uint32_t words, const rsa_ru
         for (uint32_t g = 0; g < h.n_groups; ++g) {
           rsa_pht_group G;
           memcpy(&G, img + h.group_off + (size_t)gw * g, sizeof G);
-          for (int k = 0; k < 4; ++k)
+          if (G.class_mask > 0xFu) return fail(c, RSA_ERR_ARG, "list %u group %u: class_mask beyond 4 classes", l, g);
+          for (int k = 0; k < 4; ++k) {
             if (!table_ok(img, words, G.table[k], len))
               return fail(c, RSA_ERR_ARG, "list %u group %u class %d: table outside the image or index out of list", l,
                           g, k);
+            // a class outside the mask is skipped by whole waves: it must be the empty table
+            if (!(G.class_mask >> k & 1u) && (G.table[k].slot_off != 0 || G.table[k].n_slots != 1))
+              return fail(c, RSA_ERR_ARG, "list %u group %u class %d: not in class_mask but not the empty table", l,
+                          g, k);
+          }
         }
         for (uint32_t m = 0; m < h.n_masks; ++m) {
           rsa_pht_mask M;
