@@ -100,10 +100,17 @@ def run_reference(work, text):
 
 
 def shadow_by_acl(stderr_text):
-    """'INFO - ...' triples of the -v run, grouped per ACL (the reference logs
-    ACLs in its dict order; the converted run iterates in insertion order)."""
+    """INFO triples of the -v run, grouped per ACL (the reference logs ACLs in
+    its dict order; the converted run iterates in insertion order).  Python 2
+    formats them 'INFO - msg' (the reference sets logging.BASIC_FORMAT before
+    basicConfig); Python 3's basicConfig ignores that global and prints
+    'INFO:root:msg' — both prefixes are accepted."""
     out = {}
-    lines = [l[len('INFO - '):] for l in stderr_text.split('\n') if l.startswith('INFO - ')]
+    lines = []
+    for l in stderr_text.split('\n'):
+        for pre in ('INFO - ', 'INFO:root:'):
+            if l.startswith(pre):
+                lines.append(l[len(pre):])
     k = 0
     while k < len(lines):
         head = lines[k]

@@ -100,6 +100,39 @@ def test_synth_asa_configs_parse():
             assert len(rules) > 0 and rules[len(rules) - 1].original.endswith('deny ip any any')
 
 
+def _shadow_lines(acl, rules, cover):
+    out = []
+    for index in np.nonzero(cover >= 0)[0]:
+        index, i = int(index), int(cover[index])
+        out.append('Found rule which never gets hits since it is covered by a more generic rule above it in '
+                   'access-list {0}.'.format(acl))
+        out.append('Specific rule ' + str(index) + ': ' + str(rules[index]))
+        out.append('Generic rule ' + str(i) + ': ' + str(rules[i]))
+    return out
+
+
+@pytest.mark.parametrize('case', CASES)
+def test_c_oracle_shadow_equals_reference_messages(case):
+    """The C oracle's double loop (the checker of the GPU scan) on the DB asa.py
+    builds reproduces the converted reference's -v messages."""
+    from oracle import coracle
+    from ruleset_analysis_amd import acldb
+    text, _sha, _summary, shadow = _case(case)
+    db = asa.build_db(text)
+    dbj = acldb.to_json_obj(db)
+    for hs in dbj['accesslists'].values():
+        for e in hs.values():
+            e['protocols'] = {p: [int(x) for x in v] for p, v in e['protocols'].items()}
+    R = coracle.OracleRules(json.loads(json.dumps(dbj)))
+    n = 0
+    for host, acls in db.accesslists.items():
+        for acl, e in acls.items():
+            got = _shadow_lines(acl, e['rules'], coracle.shadow(R, host, acl))
+            assert got == shadow.get(acl, []), acl
+            n += len(got)
+    assert n == sum(len(v) for v in shadow.values())
+
+
 # ---- GPU ----------------------------------------------------------------------------------------------
 
 def _traffic_lines(db, host, n, seed):
