@@ -343,6 +343,41 @@ def record_checksum(recs_u8):
     return int(x.sum().item()) & 0xFFFFFFFFFFFFFFFF
 
 
+def roofline_block(lines, classify_ms, aggregate_ms, launches, step_ms, pmc, sq, config):
+    """Roofline of the dominant kernel, k_classify (+ its k_tail): algorithmic
+    bytes per launch (28 B per line of the launch's filter slice, SURVEY.md
+    8d) / its average launch time, both from the HIP events the library
+    records on its own stream; traffic = the committed rocprofv3 FETCH_SIZE +
+    WRITE_SIZE bytes of k_classify per launch.  Pass 1 as a whole and the
+    whole step are reported beside it at the same 28 B per line."""
+    launches = max(launches, 1.0)
+    per_launch_bytes = BYTES_PER_LINE * lines / launches
+    ms_launch = classify_ms / launches
+    achieved = per_launch_bytes / (ms_launch * 1e-3) / 1e9
+    traffic = None
+    if pmc and 'k_classify' in pmc.get('kernels', {}):
+        k = pmc['kernels']['k_classify']
+        traffic = (k['read_bytes_per_step'] + k['write_bytes_per_step']) / launches
+    pass1_ms = classify_ms + aggregate_ms
+    return {
+        'bound': 'hbm', 'kernel': 'k_classify', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+        'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
+        'traffic_unit': 'HBM bytes per k_classify launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)',
+        'traffic_source': 'profiles/%s_pass1_pmc.json' % config if traffic is not None else None,
+        'launches_per_step': launches, 'ms_per_launch': ms_launch, 'algorithmic_bytes_per_launch': per_launch_bytes,
+        'bytes_per_line': BYTES_PER_LINE,
+        'valu_busy': valu_busy(sq, 'k_classify'),
+        'valu_source': 'profiles/%s_sq.json' % config if sq else None,
+        'valu_definition': '2 cycles x SQ_INSTS_VALU / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)',
+        'pass1': {'ms': pass1_ms, 'classify_ms': classify_ms, 'aggregate_ms': aggregate_ms,
+                  'achieved': BYTES_PER_LINE * lines / (pass1_ms * 1e-3) / 1e9,
+                  'frac': BYTES_PER_LINE * lines / (pass1_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                  'traffic_per_step': pmc.get('hbm_bytes_per_step') if pmc else None},
+        'step': {'ms': step_ms, 'achieved': BYTES_PER_LINE * lines / (step_ms * 1e-3) / 1e9,
+                 'frac': BYTES_PER_LINE * lines / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
+    }
+
+
 def full_size_checks(eng, batch, gbuf, n_rules, cap, recs_final, owner_rows=None):
     """Untimed properties of the benched job at full size (no oracle: too large):
     matches == per-rule line counts of the gids, hits likewise over hit lines,
@@ -431,6 +466,7 @@ def rank_main(args, rank, world, local):
     # are cleared between jobs
     capacity = max(n_hb, 1)
     pass1_launch_ms = []
+    pass1_launches = []
     last = {}
 
     def step(timed):
@@ -438,6 +474,7 @@ def rank_main(args, rank, world, local):
         eng.pass1(batch, gbuf)
         if timed:
             pass1_launch_ms.append(eng.last_pass1_times())
+            pass1_launches.append(eng.last_pass1_launches())
         if dist is None:
             if eng.resolve_cap():
                 eng.pass2(batch, gbuf)
@@ -485,7 +522,6 @@ def rank_main(args, rank, world, local):
     if rank == 0:
         total_lines = lines * world * args.steps
         value = total_lines / dt
-        achieved = BYTES_PER_LINE * lines / (pass1_ms * 1e-3) / 1e9
         pmc = read_profile('%s_pass1_pmc.json' % args.config)
         sq = read_profile('%s_sq.json' % args.config)
         res = {
@@ -500,21 +536,8 @@ def rank_main(args, rank, world, local):
                        'rules': compiled.n_rules, 'entries': len(ent), 'lines_per_gpu': lines, 'cap': cap,
                        'parallelism': 'dp%d' % world,
                        'backend': args.backend if dist is not None else 'none', 'records': n_rec},
-            'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                         'frac': achieved / HBM_PEAK_GBS,
-                         'traffic': pmc.get('hbm_bytes_per_step') if pmc else None,
-                         'traffic_source': 'profiles/%s_pass1_pmc.json' % args.config if pmc else None,
-                         'kernel': 'pass 1 = k_classify + k_tail + aggregation (k_aggregate, k_part_hist/scan/k_part_scatter, '
-                                   'k_reduce<1>) over the filter slices + rest of one step',
-                         'kernel_ms': pass1_ms, 'bytes_per_line': BYTES_PER_LINE,
-                         'kernels': {
-                             'classify_ms': classify_ms,
-                             'aggregate_ms': aggregate_ms,
-                             'classify_gbs': BYTES_PER_LINE * lines / (classify_ms * 1e-3) / 1e9},
-                         'valu': {'busy_classify': valu_busy(sq, 'k_classify'),
-                                  'busy_aggregate': valu_busy(sq, 'k_aggregate'),
-                                  'source': 'profiles/%s_sq.json' % args.config if sq else None,
-                                  'definition': '2 cycles x SQ_INSTS_VALU / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)'}},
+            'roofline': roofline_block(lines, classify_ms, aggregate_ms, float(np.mean(pass1_launches)),
+                                       dt / args.steps * 1e3, pmc, sq, args.config),
             'scan_work': {'mean_scan_position': sum_e / lines,
                           'linear_scan_equivalent_tops': OPS_PER_EVAL * sum_e / (pass1_ms * 1e-3) / 1e12,
                           'valu_peak_tops': VALU_PEAK_OPS / 1e12,

@@ -80,7 +80,8 @@ typedef struct rsa_rule_entry {
  * ports = sport | dport << 16:
  *   H    = fmix32(ks ^ 0x9E3779B9) ^ fmix32(kd ^ 0x7F4A7C15) ^ fmix32(kp ^ 0x2545F491)
  *   d    = disp[disp_off + ((H >> 16) & disp_mask)]            (uint16 units of the image)
- *   slot = hi32((H + d * ((H * 0x2C1B3C6D) | 1)) * n_slots)    (32-bit wrap)
+ *   x    = (H + d * ((H >> 16) | 1)) & 0xFFFF,  slot = (x * n_slots) >> 16,
+ *          n_slots <= 65536 (24-bit multiplier operands)
  *   word = image[slot_off + slot] = (H & 0xFFFF) << 16 | record-local entry index,
  *          0xFFFFFFFF = empty (image word 0 is always empty: absent classes
  *          point there with n_slots = 1)
@@ -91,8 +92,8 @@ typedef struct rsa_rule_entry {
  * A tuple probes only the groups in (src bitmap & dst bitmap).  All other
  * entries are residual (a first-gid-ascending list scanned linearly).
  *
- * Lists longer than 0xFFFE entries are chains of records, one per chunk of
- * 0xFFFE entries (records n_lists .. n_records-1 are the continuation chunks):
+ * Lists longer than 0xF000 entries are chains of records, one per chunk of
+ * 0xF000 entries (records n_lists .. n_records-1 are the continuation chunks):
  * a lane moves to record `next` only while its best gid exceeds `next_min`.
  * The answer is identical to the linear scan: the minimum matching gid (the
  * device verifies the hashed candidate against the full entry).
@@ -118,13 +119,14 @@ typedef struct rsa_pht_group {   /* 80 B */
   rsa_pht_table table[4];    /* port classes any, dport, sport, sport+dport       */
 } rsa_pht_group;
 
-typedef struct rsa_pht_mask {    /* 32 B: one pruning table */
+#define RSA_PHT_NARROW 0x80000000u   /* rsa_pht_mask.slot: 16-bit slots */
+typedef struct rsa_pht_mask {    /* 16 B: one pruning table (src tables first: rsa_pht_list.n_src_masks) */
   uint32_t mask;             /* address mask (non-zero)                           */
-  uint32_t side;             /* 0: src, 1: dst                                    */
-  uint32_t slot_bits;        /* 32: slots as above; 16: uint16 slots (H & 0xFF) << 8 | value,
-                                0xFFFF empty, slot_off in uint16 units, values < 255 */
-  uint32_t reserved;
-  rsa_pht_table table;       /* slot value = bitmap index                         */
+  uint32_t slot;             /* slot_off | RSA_PHT_NARROW: uint16 slots (H & 0xFF) << 8 | value,
+                                0xFFFF empty, slot_off in uint16 units, values < 255;
+                                else 32-bit slots as above                        */
+  uint32_t disp_off;         /* first displacement, uint16 units                  */
+  uint32_t size;             /* n_slots | disp_mask << 17; slot value = bitmap index */
 } rsa_pht_mask;
 
 typedef struct rsa_pht_list {    /* 80 B: one list (or one chained chunk of a list) */
@@ -139,7 +141,8 @@ typedef struct rsa_pht_list {    /* 80 B: one list (or one chained chunk of a li
   uint32_t after_min;            /* smallest gid of the list's entries >= prefix (RSA_PHT_NONE: none) */
   uint32_t next;                 /* continuation record, or RSA_PHT_NONE           */
   uint32_t next_min;             /* smallest gid of the continuation chunk          */
-  uint32_t reserved[2];
+  uint32_t n_src_masks;          /* mask records [0, n_src_masks) are src tables, the rest dst */
+  uint32_t reserved;
 } rsa_pht_list;
 
 /* Options (rsa_set_option). */
@@ -151,6 +154,8 @@ typedef struct rsa_pht_list {    /* 80 B: one list (or one chained chunk of a li
 #define RSA_OPT_PROFILE_SKIP 3 /* PROFILING ONLY, results invalid: bit0 skips counters, bit1 skips the table, bit2 skips table updates */
 #define RSA_OPT_PRECHECK 9     /* pre-check monotone slot fields with a plain load before their atomics (default 1)       */
 #define RSA_OPT_WAVE_CAP_SCATTER 11 /* TESTING: cap scatter by wave grouping (the path for > 16384 capped rules) */
+#define RSA_OPT_GROUP_TASKS 12 /* index lookup: candidate groups dealt out over the wave (1, default) or per-lane loops (0) */
+#define RSA_OPT_PROFILE_CLASSIFY 13 /* PROFILING ONLY, results invalid: bit0 no index lookup, bit1 pruning only, bit2 no verification */
 #define RSA_OPT_STATS 10       /* PROFILING: count table work into the rsa_stats counters (default 0)                 */
 
 /* One distinct (rule, connection) aggregate, 40 B (connlist-reducer.py:162-176). */
@@ -234,6 +239,8 @@ int rsa_last_pass1_ms(rsa_ctx *ctx, float *h_ms);
 /* The same time split into classification (k_classify + k_tail) and
  * aggregation (k_aggregate) launches. */
 int rsa_last_pass1_times(rsa_ctx *ctx, float *h_classify_ms, float *h_aggregate_ms);
+/* Number of classification launches (filter slices) of the last pass-1 call. */
+int rsa_last_pass1_launches(rsa_ctx *ctx, uint32_t *h_n);
 
 /* Resolve the cap (connlist-reducer.py:151): for every rule with
  * distinct >= cap, P = the order key of the line that inserted the cap-th

@@ -309,9 +309,9 @@ class CompiledRules(object):
 #   list records (PHT_LIST_WORDS each), group records, mask records, bitmaps
 #   (uint64, lo word first), CHD displacements (uint16) and slot words.
 PHT_MAGIC = 0x34415352              # 'RSA4'
-PHT_LIST_WORDS, PHT_GROUP_WORDS, PHT_MASK_WORDS = 20, 20, 8
+PHT_LIST_WORDS, PHT_GROUP_WORDS, PHT_MASK_WORDS = 20, 20, 4
 PHT_HEADER_WORDS = 8
-PHT_CHUNK = 0xFFFE                  # entries per chained record (local indices 0..0xFFFD)
+PHT_CHUNK = 0xF000                  # entries per chained record: a table never needs > 2^16 slots
 PHT_MAX_GROUPS = 64
 PHT_ATTEMPTS = 4                    # verification failures before a line is deferred
 # the four port classes of a group, probe order: key ports & mask
@@ -320,8 +320,9 @@ M32 = 0xFFFFFFFF
 PHT_EMPTY = 0xFFFFFFFF
 PHT_NONE = 0xFFFF
 PHT_MAX_IDX = 0xFFFE
+PHT_MAX_SLOTS = 0x10000              # slot index * n_slots must fit the 24-bit multiplier
+MASK_NARROW = 0x80000000            # pruning record word 1: 16-bit slots (offset in uint16 units)
 SALT_S, SALT_D, SALT_P = 0x9E3779B9, 0x7F4A7C15, 0x2545F491
-PHT_MUL = 0x2C1B3C6D                # odd multiplier of the CHD step hash (csrc kPhtMul)
 
 
 def fmix32(x):
@@ -348,15 +349,17 @@ def field_hash(k, side):
 
 
 def pht_slot(H, d, n_slots):
-    """slot = hi32(x * n_slots), x = (H + d * ((H * PHT_MUL) | 1)) mod 2^32.
-    The displacement bucket is (H >> 16) & disp_mask and the tag the low half of
-    H.  The step (H * PHT_MUL) | 1 is a second hash of the key, so keys of one
-    bucket that share the high half of H (a 16-bit birthday collision) still
-    separate as d grows (csrc: pht_probe)."""
+    """slot = (x * n_slots) >> 16, x = (H + d * step) mod 2^16, step = (H >> 16) | 1
+    (16 bits).  The displacement bucket is (H >> 16) & disp_mask and the tag
+    the low half of H.  Every product fits 24-bit multiplier operands (d and
+    step < 2^16, x < 2^16, n_slots <= 2^16), so the device uses full-rate
+    v_mad_u32_u24 / v_mul_u32_u24 (csrc: pht_slot); keys of one bucket differ
+    in their step's bits above the bucket bits or in their low half, so they
+    separate as d grows."""
     H = np.asarray(H, np.uint64)
-    step = ((H * np.uint64(PHT_MUL)) & np.uint64(M32)) | np.uint64(1)
-    x = (H + np.asarray(d, np.uint64) * step) & np.uint64(M32)
-    return ((x * np.uint64(n_slots)) >> np.uint64(32)).astype(np.int64)
+    step = ((H >> np.uint64(16)) | np.uint64(1)) & np.uint64(0xFFFF)
+    x = (H + np.asarray(d, np.uint64) * step) & np.uint64(0xFFFF)
+    return ((x * np.uint64(n_slots)) >> np.uint64(16)).astype(np.int64)
 
 
 def _prefix_mask(lo, span):
@@ -419,7 +422,12 @@ def _chd(H, load=0.98, trials=4096):
             used[sl[d]] = True
         if ok_all:
             return m, r - 1, disp, slot_of
-        m += m // 8 + 1
+        if m < PHT_MAX_SLOTS:
+            m = min(PHT_MAX_SLOTS, m + m // 8 + 1)
+        elif trials < 0x10000:
+            trials *= 4
+        else:
+            raise OverflowError('CHD placement failed for %d keys' % n)
 
 
 class _Image(object):
@@ -580,14 +588,14 @@ def _index_record(img, rec, e, pre, min_entries, max_groups):
             H = np.array(list(merged.keys()), dtype=np.uint32)
             vals = np.array([bm_index[b] for b in merged.values()], dtype=np.uint32)
             r = mrec[PHT_MASK_WORDS * q: PHT_MASK_WORDS * (q + 1)]
-            r[0], r[1] = m, side
-            if len(distinct) < 0xFF:        # 16-bit slots: half the LDS of the pruning tables
-                r[2] = 16
-                r[4:8] = img.table16(H, vals)
-            else:
-                r[2] = 32
-                r[4:8] = img.table(H, vals)
+            narrow = len(distinct) < 0xFF     # 16-bit slots: half the LDS of the pruning tables
+            soff, doff, nslots, dmask = img.table16(H, vals) if narrow else img.table(H, vals)
+            r[0] = m
+            r[1] = soff | (MASK_NARROW if narrow else 0)
+            r[2] = doff
+            r[3] = nslots | (dmask << 17)
         rec[0:4] = (goff, len(groups), moff, len(tables))
+        rec[18] = sum(1 for _m, side, _mg in tables if side == 0)   # src tables come first
         rec[7] = bm_off
         rec[8], rec[9] = src_any & M32, src_any >> 32
         rec[10], rec[11] = dst_any & M32, dst_any >> 32
@@ -716,11 +724,13 @@ def pht_lookup(index, ent, off, L, src, dst, ports):
         if ng:
             S = r[8] | (r[9] << 32)
             D = r[10] | (r[11] << 32)
+            n_src = r[18]
             for q in range(nm):
                 mr = [int(v) for v in image[moff + PHT_MASK_WORDS * q: moff + PHT_MASK_WORDS * (q + 1)]]
-                side = mr[1]
+                side = 0 if q < n_src else 1
                 key = (dst if side else src) & mr[0]
-                v = (_probe16 if mr[2] == 16 else _probe)(image, field_hash(key, side), mr[4:8])
+                t = (mr[1] & ~MASK_NARROW, mr[2], mr[3] & 0x1FFFF, mr[3] >> 17)
+                v = (_probe16 if mr[1] & MASK_NARROW else _probe)(image, field_hash(key, side), t)
                 if v != PHT_NONE:
                     bits = int(image[r[7] + 2 * v]) | (int(image[r[7] + 2 * v + 1]) << 32)
                     if side:

@@ -73,7 +73,7 @@ static_assert(offsetof(Slot, first) % 8 == 0 && offsetof(Slot, last) == offsetof
 static_assert(sizeof(rsa_tuple) == 16, "tuple layout");
 static_assert(sizeof(rsa_rule_entry) == 32, "rule layout");
 static_assert(sizeof(rsa_pht_group) == 80, "group layout");
-static_assert(sizeof(rsa_pht_mask) == 32, "mask layout");
+static_assert(sizeof(rsa_pht_mask) == 16, "mask layout");
 static_assert(sizeof(rsa_pht_list) == 80, "list record layout");
 static_assert(sizeof(rsa_conn_record) == 40, "record layout");
 
@@ -98,6 +98,8 @@ struct Rules {
   uint32_t list_off;            // word offset of the list records
   int indexed;
   int force_defer;              // testing: every index candidate takes the exact deferred path
+  int group_tasks;              // RSA_OPT_GROUP_TASKS: candidate groups dealt out over the wave (index_lookup_wave)
+  int prof;                     // RSA_OPT_PROFILE_CLASSIFY (results invalid): 1 no lookup, 2 pruning only, 4 no verification
 };
 
 struct Agg {
@@ -251,7 +253,6 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t x) {
   return x;
 }
 constexpr uint32_t kSaltS = 0x9E3779B9u, kSaltD = 0x7F4A7C15u, kSaltP = 0x2545F491u;
-constexpr uint32_t kPhtMul = 0x2C1B3C6Du;   // compile.py PHT_MUL
 
 // Index image reads: the LDS copy through address-space-3 pointers (ds_read),
 // the global copy through plain pointers.
@@ -263,103 +264,277 @@ __device__ __forceinline__ v4u rd4(const uint32_t* img, uint32_t w) { return *re
 __device__ __forceinline__ uint32_t rd16(const lds_u32* img, uint32_t h) { return reinterpret_cast<const lds_u16*>(img)[h]; }
 __device__ __forceinline__ uint32_t rd16(const uint32_t* img, uint32_t h) { return reinterpret_cast<const uint16_t*>(img)[h]; }
 
-// One CHD probe (compile.py pht_slot / _probe): H -> the slot's 16-bit value,
-// or kNoCand.  b = {slot_off, disp_off (uint16 units), n_slots, disp_mask}.
+// CHD slot (compile.py pht_slot): x = (H + d * ((H >> 16) | 1)) mod 2^16,
+// slot = (x * n_slots) >> 16.  All operands fit the 24-bit multiplier
+// (n_slots <= 2^16), so both products are full-rate v_mad/v_mul_u32_u24
+// (the 32-bit v_mul_lo/hi and v_mad_u64 they replace issue at quarter rate).
+__device__ __forceinline__ uint32_t pht_slot(uint32_t H, uint32_t d, uint32_t n_slots) {
+  const uint32_t x = (__umul24(d, (H >> 16) | 1u) + H) & 0xFFFFu;
+  return __umul24(x, n_slots) >> 16;
+}
+
+// One CHD probe (compile.py _probe): H -> the slot's 16-bit value, or kNoCand.
+// b = {slot_off, disp_off (uint16 units), n_slots, disp_mask}.
 template <typename P32>
 __device__ __forceinline__ uint32_t pht_probe(P32 img, uint32_t H, v4u b) {
   const uint32_t d = rd16(img, b.y + ((H >> 16) & b.w));
-  const uint32_t x = H + d * ((H * kPhtMul) | 1u);
-  const uint32_t slot = __umulhi(x, b.z);
-  const uint32_t w = img[b.x + slot];
+  const uint32_t w = img[b.x + pht_slot(H, d, b.z)];
   return ((w >> 16) == (H & 0xFFFFu)) ? (w & 0xFFFFu) : kNoCand;
 }
 
-// The same probe of a table with 16-bit slots (8-bit tag, 8-bit value; the
-// pruning tables): b.x, b.y in uint16 units.  A tag false positive only adds
-// candidate groups (bitmaps are ORed; a superset is safe).
+// A pruning-table probe (compile.py _probe/_probe16 by the record's
+// MASK_NARROW bit), branch-free: the slot is read through the dword that holds
+// it.  m = the packed record {mask, slot_off | narrow << 31, disp_off,
+// n_slots | disp_mask << 17}; 16-bit slots hold tag << 8 | value (0xFFFF
+// empty, values < 255), 32-bit slots tag << 16 | value.
 template <typename P32>
-__device__ __forceinline__ uint32_t pht_probe16(P32 img, uint32_t H, v4u b) {
-  const uint32_t d = rd16(img, b.y + ((H >> 16) & b.w));
-  const uint32_t x = H + d * ((H * kPhtMul) | 1u);
-  const uint32_t slot = __umulhi(x, b.z);
-  const uint32_t w = rd16(img, b.x + slot);
-  return (w != 0xFFFFu && (w >> 8) == (H & 0xFFu)) ? (w & 0xFFu) : kNoCand;
+__device__ __forceinline__ uint32_t mask_probe(P32 img, uint32_t H, v4u m) {
+  const uint32_t d = rd16(img, m.z + ((H >> 16) & (m.w >> 17)));
+  const uint32_t narrow = m.y >> 31;
+  const uint32_t hidx = (m.y & 0x7FFFFFFFu) + pht_slot(H, d, m.w & 0x1FFFFu);   // in units of the slot width
+  const uint32_t w32 = img[hidx >> narrow];
+  const uint32_t sh = 16u >> narrow;                                  // tag shift: 16 (wide) or 8 (narrow)
+  const uint32_t u = narrow ? (w32 >> ((hidx & 1u) << 4)) & 0xFFFFu : w32;
+  const uint32_t fm = (1u << sh) - 1u;
+  const uint32_t val = u & fm;
+  return ((u >> sh) == (H & fm) && val != fm) ? val : kNoCand;
 }
 
 constexpr int kAttempts = 4;   // compile.py PHT_ATTEMPTS
-constexpr uint32_t kListWords = 20, kGroupWords = 20, kMaskWords = 8;
+constexpr uint32_t kListWords = 20, kGroupWords = 20, kMaskWords = 4;
 
-// Index lookup for ONE lane (divergent code: the lanes of a wave may be on
-// different lists; compile.py pht_lookup is the host model).  h0..h2: the
-// lane's list record {group_off, n_groups, mask_off, n_masks},
-// {resid_beg, resid_end, prefix, bm_off}, {src_any, dst_any}; ebeg: the list's
-// first entry.  (1) pruning: each src/dst mask table maps the masked address to
-// a bitmap of the groups holding a rule on that prefix; (2) the groups in
-// src & dst bitmaps, ascending min index, four port-class probes each, until
-// a group's min index cannot beat the best candidate; (3) verification of the
-// candidate against its entry (16-bit tags collide), retried above a failed
-// candidate.  Returns gid, kNoGid or kDefer.
+// Pruning stage of the index lookup for ONE lane (compile.py pht_lookup): each
+// src/dst mask table maps the masked address to a bitmap of the groups holding
+// a rule on that prefix; the candidate groups are those in both the src and
+// the dst bitmap.  Masks are probed two at a time, branch-free (an odd count
+// probes its last mask twice: OR is idempotent).  lw: the lane's list record
+// {group_off, n_groups, mask_off, n_masks}, {…, bm_off}, {src_any, dst_any}.
 template <typename P32>
-__device__ __forceinline__ uint32_t index_lookup(const Rules& R, P32 img, uint32_t lw, uint32_t src, uint32_t dst,
-                                                 uint32_t ports) {
-  // record fields are read where they are used (LDS reads are cheap; registers
-  // bound the occupancy): h0 {group_off, n_groups, mask_off, n_masks}
+__device__ __forceinline__ unsigned long long index_candidates(P32 img, uint32_t lw, uint32_t src, uint32_t dst) {
   const v4u h0 = rd4(img, lw);
   const v4u h2 = rd4(img, lw + 8);
   unsigned long long S = ((unsigned long long)h2.y << 32) | h2.x;
   unsigned long long D = ((unsigned long long)h2.w << 32) | h2.z;
   const uint32_t bm_off = img[lw + 7];
-  for (uint32_t k = 0; k < h0.w; ++k) {
-    const uint32_t mw = h0.z + kMaskWords * k;
-    const v4u m0 = rd4(img, mw), m1 = rd4(img, mw + 4);
-    const bool dside = m0.y != 0;
-    const uint32_t H = fmix32(((dside ? dst : src) & m0.x) ^ (dside ? kSaltD : kSaltS));
-    const uint32_t v = m0.z == 16u ? pht_probe16(img, H, m1) : pht_probe(img, H, m1);
-    if (v != kNoCand) {
-      const uint32_t bw = bm_off + 2 * v;
-      const unsigned long long bits = ((unsigned long long)img[bw + 1] << 32) | img[bw];
-      if (dside) {
-        D |= bits;
-      } else {
-        S |= bits;
-      }
+  const uint32_t nm = h0.w, ns = img[lw + 18];   // the first ns records are the src tables
+  constexpr int kU = 4;   // masks in flight per iteration (each a chain of dependent LDS reads)
+  for (uint32_t k = 0; k < nm; k += kU) {
+    // phase by phase over the kU masks, so that the reads of one phase are all
+    // in flight before the first is waited for (a short last batch repeats
+    // its last mask: OR is idempotent)
+    v4u m[kU];
+    uint32_t H[kU], w[kU];
+    bool side[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const uint32_t kk = min(k + u, nm - 1);
+      m[u] = rd4(img, h0.z + kMaskWords * kk);
+      side[u] = kk >= ns;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      H[u] = fmix32(((side[u] ? dst : src) & m[u].x) ^ (side[u] ? kSaltD : kSaltS));
+      w[u] = rd16(img, m[u].z + ((H[u] >> 16) & (m[u].w >> 17)));   // displacement
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const uint32_t narrow = m[u].y >> 31;
+      const uint32_t hidx = (m[u].y & 0x7FFFFFFFu) + pht_slot(H[u], w[u], m[u].w & 0x1FFFFu);
+      m[u].z = hidx;                                   // (reused: slot index in units of the slot width)
+      w[u] = img[hidx >> narrow];
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const uint32_t narrow = m[u].y >> 31, hidx = m[u].z;
+      const uint32_t sh = 16u >> narrow, fm = (1u << sh) - 1u;
+      const uint32_t uu = narrow ? (w[u] >> ((hidx & 1u) << 4)) & 0xFFFFu : w[u];
+      const uint32_t val = uu & fm;
+      w[u] = ((uu >> sh) == (H[u] & fm) && val != fm) ? val : kNoCand;   // (mask_probe)
+      const uint32_t bw = bm_off + 2 * (w[u] == kNoCand ? 0u : w[u]);
+      m[u].x = img[bw];
+      m[u].y = img[bw + 1];
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const unsigned long long b = w[u] == kNoCand ? 0ull : (((unsigned long long)m[u].y << 32) | m[u].x);
+      D |= side[u] ? b : 0ull;
+      S |= side[u] ? 0ull : b;
     }
   }
-  const unsigned long long cand0 = S & D;
-  if (!cand0) return kNoGid;
-  const uint32_t group_off = h0.x;
-  // port-class hash components (compile.py PORT_CLASSES: any, dport, sport, both)
-  const uint32_t hp1 = fmix32((ports & 0xFFFF0000u) ^ kSaltP), hp2 = fmix32((ports & 0x0000FFFFu) ^ kSaltP),
-                 hp3 = fmix32(ports ^ kSaltP);
-  uint32_t floor = 0;
-  for (int attempt = 0; attempt < kAttempts; ++attempt) {
-    uint32_t bi = kNoCand;
-    unsigned long long cand = cand0;
-    while (cand) {
-      const uint32_t g = (uint32_t)__builtin_ctzll(cand);
-      cand &= cand - 1;
-      const uint32_t gw = group_off + kGroupWords * g;
-      const v4u a = rd4(img, gw);
-      if (a.z >= bi) break;   // groups ascend in min index: no later group can do better
-      const uint32_t hsd = fmix32((src & a.x) ^ kSaltS) ^ fmix32((dst & a.y) ^ kSaltD);
-      uint32_t c0 = pht_probe(img, hsd ^ fmix32(0u ^ kSaltP), rd4(img, gw + 4));
-      uint32_t c1 = pht_probe(img, hsd ^ hp1, rd4(img, gw + 8));
-      uint32_t c2 = pht_probe(img, hsd ^ hp2, rd4(img, gw + 12));
-      uint32_t c3 = pht_probe(img, hsd ^ hp3, rd4(img, gw + 16));
-      c0 = c0 >= floor ? c0 : kNoCand;
-      c1 = c1 >= floor ? c1 : kNoCand;
-      c2 = c2 >= floor ? c2 : kNoCand;
-      c3 = c3 >= floor ? c3 : kNoCand;
-      bi = min(bi, min(min(c0, c1), min(c2, c3)));
-    }
+  return S & D;
+}
+
+// A candidate group's record: header and the four port-class tables.
+struct GroupRec {
+  v4u a;        // {src_mask, dst_mask, min_idx, class_mask}
+  v4u t[4];     // the port-class tables
+};
+
+template <typename P32>
+__device__ __forceinline__ GroupRec group_rec(P32 img, uint32_t gw) {
+  GroupRec r;
+  r.a = rd4(img, gw);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) r.t[c] = rd4(img, gw + 4 + 4 * c);
+  return r;
+}
+
+// Port-class hash components of a tuple (compile.py PORT_CLASSES: any, dport,
+// sport, both).
+struct PortHash {
+  uint32_t p1, p2, p3;
+};
+__device__ __forceinline__ PortHash port_hash(uint32_t ports) {
+  return {fmix32((ports & 0xFFFF0000u) ^ kSaltP), fmix32((ports & 0x0000FFFFu) ^ kSaltP), fmix32(ports ^ kSaltP)};
+}
+
+// The four port-class probes of a candidate group for one tuple: the smallest
+// list index >= floor among the group's tables, or kNoCand.
+template <typename P32>
+__device__ __forceinline__ uint32_t group_probe(P32 img, const GroupRec& g, uint32_t src, uint32_t dst,
+                                                const PortHash& hp, uint32_t floor) {
+  const uint32_t hsd = fmix32((src & g.a.x) ^ kSaltS) ^ fmix32((dst & g.a.y) ^ kSaltD);
+  uint32_t c0 = pht_probe(img, hsd ^ fmix32(0u ^ kSaltP), g.t[0]);
+  uint32_t c1 = pht_probe(img, hsd ^ hp.p1, g.t[1]);
+  uint32_t c2 = pht_probe(img, hsd ^ hp.p2, g.t[2]);
+  uint32_t c3 = pht_probe(img, hsd ^ hp.p3, g.t[3]);
+  c0 = c0 >= floor ? c0 : kNoCand;
+  c1 = c1 >= floor ? c1 : kNoCand;
+  c2 = c2 >= floor ? c2 : kNoCand;
+  c3 = c3 >= floor ? c3 : kNoCand;
+  return min(min(c0, c1), min(c2, c3));
+}
+
+// Verification of candidate bi against its entry (16-bit tags collide) and,
+// for ONE lane, the retries above a failed candidate: the candidate groups in
+// ascending min index, until a group's min index cannot beat the best
+// candidate.  Returns gid, kNoGid or kDefer.
+template <typename P32>
+__device__ __forceinline__ uint32_t index_verify(const Rules& R, P32 img, uint32_t lw, unsigned long long cand0,
+                                                 uint32_t bi, uint32_t src, uint32_t dst, uint32_t ports) {
+  const uint32_t group_off = img[lw];
+  for (int attempt = 0;; ++attempt) {
     if (bi == kNoCand) return kNoGid;
     if (R.force_defer) return kDefer;
     const uint32_t ebeg = img[lw + 12];
     const v4u ea = R.eg[2 * (size_t)(ebeg + bi)], eb = R.eg[2 * (size_t)(ebeg + bi) + 1];
     if (entry_match(ea, eb, src, dst, ports)) return entry_gid(eb, ports);
-    floor = bi + 1;   // a tag collision: every true candidate lies above bi
+    if (attempt + 1 >= kAttempts) return kDefer;
+    const uint32_t floor = bi + 1;   // a tag collision: every true candidate lies above bi
+    bi = kNoCand;
+    const PortHash hp = port_hash(ports);
+    unsigned long long cand = cand0;
+    while (cand) {
+      const uint32_t g = (uint32_t)__builtin_ctzll(cand);
+      cand &= cand - 1;
+      const GroupRec G = group_rec(img, group_off + kGroupWords * g);
+      if (G.a.z >= bi) break;   // groups ascend in min index: no later group can do better
+      bi = min(bi, group_probe(img, G, src, dst, hp, floor));
+    }
   }
-  return kDefer;
+}
+
+// Index lookup for ONE lane, all in the lane's own control flow (the
+// RSA_OPT_GROUP_TASKS=0 form): pruning, the candidate groups in ascending
+// min index with early exit, verification.
+template <typename P32>
+__device__ __forceinline__ uint32_t index_lookup(const Rules& R, P32 img, uint32_t lw, uint32_t src, uint32_t dst,
+                                                 uint32_t ports) {
+  if (R.prof & 1) return kNoGid;
+  const unsigned long long cand0 = index_candidates(img, lw, src, dst);
+  if (!cand0 || (R.prof & 2)) return kNoGid;
+  const uint32_t group_off = img[lw];
+  const PortHash hp = port_hash(ports);
+  uint32_t bi = kNoCand;
+  unsigned long long cand = cand0;
+  while (cand) {
+    const uint32_t g = (uint32_t)__builtin_ctzll(cand);
+    cand &= cand - 1;
+    const GroupRec G = group_rec(img, group_off + kGroupWords * g);   // all five reads before the test
+    if (G.a.z >= bi) break;
+    bi = min(bi, group_probe(img, G, src, dst, hp, 0u));
+  }
+  if (R.prof & 4) return bi == kNoCand ? kNoGid : bi;
+  return index_verify(R, img, lw, cand0, bi, src, dst, ports);
+}
+
+typedef __attribute__((address_space(3))) uint32_t lds_w32;
+
+// Order LDS traffic of one wave between lanes: the compiler may not move LDS
+// accesses across this point (the LDS executes one wave's instructions in
+// order).
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Index lookup for the lanes with `ix` (WAVE-UNIFORM call, all lanes).  The
+// pruning stage runs per lane; every lane then probes its own first candidate
+// group (the one of smallest min index), and the remaining candidate (lane,
+// group) pairs of the whole wave are dealt out as tasks, 64 per round, so a
+// lane with many candidate groups no longer holds the wave for the others
+// (per-lane loops ran max-over-lanes iterations: ~4.3 at 10k rules against a
+// mean of 1.6; the remainder is ~0.7 tasks per lane, one round).  All
+// candidate groups are probed (no early exit), so the per-lane minimum equals
+// the serial loop's first attempt.  scr: this wave's 64 LDS words (the task
+// list {group word << 6 | owner lane}, then per-owner minima via ds_min).
+// Returns gid, kNoGid or kDefer for the ix lanes.
+template <typename P32>
+__device__ __forceinline__ uint32_t index_lookup_wave(const Rules& R, P32 img, uint32_t lw, bool ix, uint32_t src,
+                                                      uint32_t dst, uint32_t ports, lds_w32* scr) {
+  if (R.prof & 1) return kNoGid;
+  const unsigned long long cand0 = ix ? index_candidates(img, lw, src, dst) : 0ull;
+  if (__ballot(cand0 != 0ull) == 0ull || (R.prof & 2)) return kNoGid;
+  const uint32_t lane = __lane_id();
+  const uint32_t group_off = ix ? img[lw] : 0u;
+  const PortHash hp = port_hash(ports);
+  // round 0: the lane's own first group
+  uint32_t bi = kNoCand;
+  if (cand0) {
+    const uint32_t g = (uint32_t)__builtin_ctzll(cand0);
+    bi = group_probe(img, group_rec(img, group_off + kGroupWords * g), src, dst, hp, 0u);
+  }
+  unsigned long long rem = cand0 & (cand0 - 1ull);   // this lane's groups not yet probed
+  if (__ballot(rem != 0ull) != 0ull) {
+    // exclusive prefix of the remaining counts over the wave, by bit planes
+    const uint32_t cnt = (uint32_t)__popcll(rem);
+    uint32_t excl = 0;
+    for (uint32_t b = 0; b < 6; ++b) {
+      const unsigned long long plane = __ballot((cnt >> b) & 1u);
+      if (__ballot(cnt >> b) == 0ull) break;
+      excl += (uint32_t)__popcll(plane & ((1ull << lane) - 1ull)) << b;
+    }
+    const uint32_t total = __builtin_amdgcn_readlane(excl + cnt, 63);
+    uint32_t pos = excl;   // wave task index of the lane's next group
+    for (uint32_t base = 0; base < total; base += 64) {
+      while (rem && pos < base + 64) {   // deal this round's tasks
+        const uint32_t g = (uint32_t)__builtin_ctzll(rem);
+        rem &= rem - 1ull;
+        scr[pos - base] = ((group_off + kGroupWords * g) << 6) | lane;
+        ++pos;
+      }
+      wave_lds_fence();
+      const bool has = base + lane < total;
+      const uint32_t task = has ? scr[lane] : lane;
+      wave_lds_fence();
+      scr[lane] = kNoCand;
+      const uint32_t j = task & 63u;
+      const uint32_t s_o = __shfl(src, j), d_o = __shfl(dst, j);
+      const PortHash hp_o = {(uint32_t)__shfl(hp.p1, j), (uint32_t)__shfl(hp.p2, j), (uint32_t)__shfl(hp.p3, j)};
+      wave_lds_fence();
+      if (has) {
+        const uint32_t c = group_probe(img, group_rec(img, task >> 6), s_o, d_o, hp_o, 0u);
+        if (c != kNoCand) __atomic_fetch_min(&scr[j], c, __ATOMIC_RELAXED);
+      }
+      wave_lds_fence();
+      bi = min(bi, scr[lane]);
+      wave_lds_fence();
+    }
+  }
+  if (!ix || cand0 == 0ull) return kNoGid;
+  if (R.prof & 4) return bi == kNoCand ? kNoGid : bi;
+  return index_verify(R, img, lw, cand0, bi, src, dst, ports);
 }
 
 // First-match classification of one wave of tuples.  Linear scans (the whole
@@ -367,8 +542,9 @@ __device__ __forceinline__ uint32_t index_lookup(const Rules& R, P32 img, uint32
 // a waterfall over the distinct lists present in the wave (list id broadcast
 // by readlane, so entries are wave-uniform scalar loads); the index lookup
 // runs per lane.  kExact: ignore the index (the deferred-line path).
-template <bool kExact, typename P32>
-__device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Rules& R, P32 img, unsigned int* flags) {
+template <bool kExact, bool kTasks, typename P32>
+__device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Rules& R, P32 img, unsigned int* flags,
+                                                  lds_w32* scr) {
   const uint32_t list = t.w & 0xFFFFu;
   if (active && list >= R.n_lists) {
     atomicOr(&flags[1], 1u);
@@ -409,8 +585,14 @@ __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Ru
   bool go = active && best > img[lw + 15];
   bool deferred = false;
   while (__ballot(go)) {
-    if (go && img[lw + 1] != 0) {
-      const uint32_t c = index_lookup(R, img, lw, t.x, t.y, t.z);
+    const bool ix = go && img[lw + 1] != 0;
+    uint32_t c = kNoGid;
+    if (kTasks) {
+      c = index_lookup_wave(R, img, lw, ix, t.x, t.y, t.z, scr);
+    } else if (ix) {
+      c = index_lookup(R, img, lw, t.x, t.y, t.z);
+    }
+    if (ix) {
       if (c == kDefer) {
         deferred = true;
         go = false;
@@ -682,11 +864,13 @@ __device__ __forceinline__ void emit_one(uint32_t i, uint4 t, uint32_t gid, cons
 // with kEmit the line's counter word and table record (emit_wave).  Lines
 // whose index candidate failed verification kAttempts times go to `tail`
 // (k_tail scans and emits them exactly).
-template <int kImg, bool kEmit>
+template <int kImg, bool kEmit, bool kTasks>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kImgSmallMax ? 4 : 8, 8))) void k_classify(
     const uint4* __restrict__ T, unsigned long long n, int32_t* __restrict__ gout, Rules R, unsigned int* flags,
     uint32_t* tail, unsigned long long* tail_n, Agg A, Emit E) {
   __shared__ __attribute__((aligned(16))) uint32_t lds_img[kImg > 0 ? kImg : 4];
+  __shared__ uint32_t lds_task[kTasks ? 1024 : 64];   // 64 words per wave (index_lookup_wave)
+  lds_w32* scr = (lds_w32*)lds_task + (kTasks ? (threadIdx.x & ~63u) : 0u);
   if (kImg > 0 && R.indexed) {
     const uint4* src = reinterpret_cast<const uint4*>(R.img);
     uint4* dst = reinterpret_cast<uint4*>(lds_img);
@@ -703,9 +887,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kIm
     const bool valid = in && (((t.w >> 16) & 0xFFu) & RSA_F_VALID);
     uint32_t gid;
     if (kImg > 0) {
-      gid = classify_wave<false>(t, valid, R, (const lds_u32*)lds_img, flags);
+      gid = classify_wave<false, kTasks>(t, valid, R, (const lds_u32*)lds_img, flags, scr);
     } else {
-      gid = classify_wave<false>(t, valid, R, R.img, flags);
+      gid = classify_wave<false, kTasks>(t, valid, R, R.img, flags, scr);
     }
     const bool defer = gid == kDefer;
     const unsigned long long dm = __ballot(defer);
@@ -735,7 +919,7 @@ __global__ __launch_bounds__(kBlock) void k_tail(const uint4* __restrict__ T, in
     const unsigned long long i = in ? tail[j] : 0u;
     const uint4 t = in ? T[i] : make_uint4(0u, 0u, 0u, 0u);
     const bool valid = in && (((t.w >> 16) & 0xFFu) & RSA_F_VALID);
-    const uint32_t gid = classify_wave<true>(t, valid, R, R.img, flags);
+    const uint32_t gid = classify_wave<true, false>(t, valid, R, R.img, flags, nullptr);
     if (gout && in) gout[i] = (int32_t)gid;
     if (kEmit && in) emit_one((uint32_t)i, t, gid, A, E);
   }
@@ -1740,6 +1924,8 @@ struct rsa_ctx {
   bool index_loaded = false;
   bool indexed = false;
   bool force_defer = false;
+  bool group_tasks = true;     // RSA_OPT_GROUP_TASKS
+  uint32_t prof_classify = 0;  // RSA_OPT_PROFILE_CLASSIFY
   bool wave_cap_scatter = false;       // testing: cap scatter by wave grouping (the > kCapLds path)
   // caller-owned counters
   unsigned long long* d_matches = nullptr;
@@ -1845,6 +2031,8 @@ Rules rules_of(const rsa_ctx* c) {
   r.img_words = c->img_words;
   r.indexed = c->indexed ? 1 : 0;
   r.force_defer = c->force_defer ? 1 : 0;
+  r.group_tasks = c->group_tasks ? 1 : 0;
+  r.prof = (int)c->prof_classify;
   return r;
 }
 
@@ -2025,21 +2213,31 @@ int ensure_events(rsa_ctx* c) {
 constexpr int kImgSmall = kImgSmallMax;   // 76 KiB: two 1024-thread workgroups per CU (32 waves)
 constexpr int kImgLarge = 38912;   // 152 KiB: one workgroup per CU
 
+template <bool kEmit, bool kTasks>
+void launch_classify_img(rsa_ctx* c, const uint4* t, uint64_t m, int32_t* go, const Rules& r, const Agg& ag,
+                         const Emit& e) {
+  if (c->indexed && c->img_words <= (uint32_t)kImgSmall) {
+    k_classify<kImgSmall, kEmit, kTasks><<<grid_for_threads(c, m, 1024, 2), 1024, 0, c->stream>>>(
+        t, m, go, r, c->d_flags, c->d_tail, c->d_tail_n, ag, e);
+  } else if (c->indexed && c->img_words <= (uint32_t)kImgLarge) {
+    k_classify<kImgLarge, kEmit, kTasks><<<grid_for_threads(c, m, 1024, 1), 1024, 0, c->stream>>>(
+        t, m, go, r, c->d_flags, c->d_tail, c->d_tail_n, ag, e);
+  } else {
+    k_classify<0, kEmit, kTasks><<<grid_for_threads(c, m, 1024, 2), 1024, 0, c->stream>>>(t, m, go, r, c->d_flags, c->d_tail,
+                                                                                   c->d_tail_n, ag, e);
+  }
+}
+
 // Classification (+ exact tail) of lines [0, m) of T (already offset) into go
 // (nullable); with `e` also the pass-1 emission (counter words, records).
 template <bool kEmit>
 int launch_classify_t(rsa_ctx* c, const uint4* t, uint64_t m, int32_t* go, const Emit& e) {
   const Rules r = rules_of(c);
   const Agg ag = agg_of(c);
-  if (c->indexed && c->img_words <= (uint32_t)kImgSmall) {
-    k_classify<kImgSmall, kEmit><<<grid_for_threads(c, m, 1024, 2), 1024, 0, c->stream>>>(
-        t, m, go, r, c->d_flags, c->d_tail, c->d_tail_n, ag, e);
-  } else if (c->indexed && c->img_words <= (uint32_t)kImgLarge) {
-    k_classify<kImgLarge, kEmit><<<grid_for_threads(c, m, 1024, 1), 1024, 0, c->stream>>>(
-        t, m, go, r, c->d_flags, c->d_tail, c->d_tail_n, ag, e);
+  if (c->group_tasks) {
+    launch_classify_img<kEmit, true>(c, t, m, go, r, ag, e);
   } else {
-    k_classify<0, kEmit><<<grid_for_threads(c, m, 1024, 2), 1024, 0, c->stream>>>(t, m, go, r, c->d_flags, c->d_tail,
-                                                                                   c->d_tail_n, ag, e);
+    launch_classify_img<kEmit, false>(c, t, m, go, r, ag, e);
   }
   HIPCHK(c, hipGetLastError());
   // deferred lines (their number is read on the device: no host sync)
@@ -2328,6 +2526,12 @@ int rsa_set_option(rsa_ctx* c, int option, int64_t value) {
     case RSA_OPT_FORCE_DEFER:
       c->force_defer = value != 0;
       return RSA_OK;
+    case RSA_OPT_PROFILE_CLASSIFY:
+      c->prof_classify = (uint32_t)value;
+      return RSA_OK;
+    case RSA_OPT_GROUP_TASKS:
+      c->group_tasks = value != 0;
+      return RSA_OK;
     case RSA_OPT_WAVE_CAP_SCATTER:
       c->wave_cap_scatter = value != 0;
       return RSA_OK;
@@ -2406,7 +2610,7 @@ namespace {
 
 // A 16-bit-slot CHD table inside the image whose slot values are all < `limit`.
 bool table16_ok(const uint32_t* img, uint32_t words, const rsa_pht_table& t, uint32_t limit) {
-  if (t.n_slots == 0 || (uint64_t)t.slot_off + t.n_slots > 2ull * words || (t.disp_mask & (t.disp_mask + 1)) != 0 ||
+  if (t.n_slots == 0 || t.n_slots > 0x10000u || (uint64_t)t.slot_off + t.n_slots > 2ull * words || (t.disp_mask & (t.disp_mask + 1)) != 0 ||
       (uint64_t)t.disp_off + t.disp_mask + 1 > 2ull * words || limit > 0xFFu)
     return false;
   const uint16_t* h = reinterpret_cast<const uint16_t*>(img);
@@ -2419,7 +2623,7 @@ bool table16_ok(const uint32_t* img, uint32_t words, const rsa_pht_table& t, uin
 
 // A CHD table inside the image whose slot values are all < `limit`.
 bool table_ok(const uint32_t* img, uint32_t words, const rsa_pht_table& t, uint32_t limit) {
-  if (t.n_slots == 0 || (uint64_t)t.slot_off + t.n_slots > words || (t.disp_mask & (t.disp_mask + 1)) != 0 ||
+  if (t.n_slots == 0 || t.n_slots > 0x10000u || (uint64_t)t.slot_off + t.n_slots > words || (t.disp_mask & (t.disp_mask + 1)) != 0 ||
       (uint64_t)t.disp_off + t.disp_mask + 1 > 2ull * words)
     return false;
   for (uint32_t q = 0; q < t.n_slots; ++q) {
@@ -2436,6 +2640,7 @@ int rsa_load_index(rsa_ctx* c, const uint32_t* img, uint32_t words, const rsa_ru
   if (!c->rules_loaded) return fail(c, RSA_ERR_STATE, "load the candidate lists first");
   if (words < 8 || img[0] != 0xFFFFFFFFu || img[1] != RSA_PHT_MAGIC)
     return fail(c, RSA_ERR_ARG, "not an index image (word 0 must be empty, word 1 RSA_PHT_MAGIC)");
+  if (words > (1u << 26)) return fail(c, RSA_ERR_ARG, "index image larger than 2^26 words");   // task words: gw << 6
   const uint32_t nl = c->n_lists;
   if (img[2] != nl) return fail(c, RSA_ERR_ARG, "image has %u lists, %u are loaded", img[2], nl);
   const uint32_t lo = img[3], nrec = img[4];
@@ -2486,13 +2691,12 @@ int rsa_load_index(rsa_ctx* c, const uint32_t* img, uint32_t words, const rsa_ru
                           g, k);
           }
         }
+        if (h.n_src_masks > h.n_masks) return fail(c, RSA_ERR_ARG, "list %u: more src tables than tables", l);
         for (uint32_t m = 0; m < h.n_masks; ++m) {
           rsa_pht_mask M;
           memcpy(&M, img + h.mask_off + (size_t)mw * m, sizeof M);
-          if (M.side > 1) return fail(c, RSA_ERR_ARG, "list %u mask %u: side must be 0 or 1", l, m);
-          if (M.slot_bits != 16 && M.slot_bits != 32)
-            return fail(c, RSA_ERR_ARG, "list %u mask %u: slot_bits must be 16 or 32", l, m);
-          if (M.slot_bits == 16 ? !table16_ok(img, words, M.table, h.n_bitmaps) : !table_ok(img, words, M.table, h.n_bitmaps))
+          const rsa_pht_table T = {M.slot & ~RSA_PHT_NARROW, M.disp_off, M.size & 0x1FFFFu, M.size >> 17};
+          if ((M.slot & RSA_PHT_NARROW) ? !table16_ok(img, words, T, h.n_bitmaps) : !table_ok(img, words, T, h.n_bitmaps))
             return fail(c, RSA_ERR_ARG, "list %u mask %u: table outside the image or bitmap out of range", l, m);
         }
       }
@@ -2661,6 +2865,12 @@ int rsa_last_pass1_times(rsa_ctx* c, float* h_classify_ms, float* h_aggregate_ms
   }
   *h_classify_ms = tc;
   *h_aggregate_ms = ta;
+  return RSA_OK;
+}
+
+int rsa_last_pass1_launches(rsa_ctx* c, uint32_t* h_n) {
+  if (!c || !h_n) return RSA_ERR_ARG;
+  *h_n = (uint32_t)(c->ev_used / 3);
   return RSA_OK;
 }
 

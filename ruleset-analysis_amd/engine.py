@@ -111,6 +111,12 @@ class Engine(object):
         self.ctx.call('rsa_last_pass1_times', ctypes.byref(a), ctypes.byref(b))
         return float(a.value), float(b.value)
 
+    def last_pass1_launches(self):
+        """Classification launches (filter slices) of the last pass-1 call."""
+        n = ctypes.c_uint32(0)
+        self.ctx.call('rsa_last_pass1_launches', ctypes.byref(n))
+        return int(n.value)
+
     def last_pass1_ms(self):
         ms = ctypes.c_float(0)
         self.ctx.call('rsa_last_pass1_ms', ctypes.byref(ms))

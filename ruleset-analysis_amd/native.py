@@ -35,6 +35,8 @@ RSA_OPT_FORCE_DEFER = 8
 RSA_OPT_PRECHECK = 9
 RSA_OPT_STATS = 10
 RSA_OPT_WAVE_CAP_SCATTER = 11
+RSA_OPT_GROUP_TASKS = 12
+RSA_OPT_PROFILE_CLASSIFY = 13
 
 P = ctypes.c_void_p
 U32 = ctypes.c_uint32
@@ -54,6 +56,7 @@ SYMBOLS = {
     'rsa_load_index': (I32, [P, P, U32, P, U32]),
     'rsa_last_pass1_ms': (I32, [P, ctypes.POINTER(ctypes.c_float)]),
     'rsa_last_pass1_times': (I32, [P, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
+    'rsa_last_pass1_launches': (I32, [P, ctypes.POINTER(ctypes.c_uint32)]),
     'rsa_load_rules': (I32, [P, P, U32, P, U32, U32]),
     'rsa_bind_counters': (I32, [P, P, P, P, P]),
     'rsa_set_rule_count': (I32, [P, U32]),
