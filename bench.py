@@ -464,7 +464,7 @@ def rank_main(args, rank, world, local):
     # table capacity: the exact upper bound (every hit line a new connection),
     # clamped by the library to its largest table; only the slots a job uses
     # are cleared between jobs
-    capacity = max(n_hb, 1)
+    capacity = args.capacity or max(n_hb, 1)
     pass1_launch_ms = []
     pass1_launches = []
     last = {}
@@ -775,6 +775,7 @@ def parse_args(argv=None):
     ap.add_argument('--filter-slice', type=int, default=0, help='override RSA_OPT_FILTER_SLICE')
     ap.add_argument('--opt', action='append', default=[], help='NAME=VALUE library option (e.g. FILTER_STEPS=3)')
     ap.add_argument('--no-index', action='store_true', help='classify with the plain linear scan')
+    ap.add_argument('--capacity', type=int, default=0, help='EXPERIMENT: table capacity (default: hit+built lines)')
     ap.add_argument('--prefix', type=int, default=0, help='entries per list scanned before the index')
     ap.add_argument('--text', action='store_true',
                     help='the fused job from log text in HBM (GPU parse + order keys + classify + aggregate)')

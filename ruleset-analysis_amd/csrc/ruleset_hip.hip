@@ -1538,7 +1538,10 @@ __global__ void k_table_init(Slot* S, unsigned long long cap) {
 }
 
 // Reset only the slots the last job used.
-__global__ void k_table_clear(Slot* S, const unsigned long long* used, unsigned long long n) {
+__global__ void k_table_clear(Slot* S, const unsigned long long* used, const unsigned long long* n_p,
+                              unsigned long long cap) {
+  unsigned long long n = *n_p;
+  if (n > cap) n = cap;
   const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
   for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
     slot_clear(S, (uint32_t)used[i]);
@@ -1570,10 +1573,14 @@ __global__ void k_cap_mark(const unsigned int* distinct, uint32_t n_rules, uint3
 // wave that share a rule take their positions from one atomic (hot rules would
 // otherwise serialise thousands of atomics on one counter).
 __global__ __launch_bounds__(kBlock) void k_cap_scatter(const Slot* S, const unsigned long long* used,
-                                                        unsigned long long n_used,
+                                                        const unsigned long long* n_used_p, const unsigned int* n_capped_p,
+                                                        uint32_t lds_max,
                                                         const uint32_t* cidx, const uint32_t* capped_start,
                                                         uint32_t* capped_fill, unsigned long long* keys,
                                                         unsigned long long max_keys, unsigned int* flags) {
+  const unsigned int n_capped = *n_capped_p;
+  if (n_capped == 0 || n_capped <= lds_max) return;   // the LDS variant's case (workgroup-uniform)
+  const unsigned long long n_used = *n_used_p < max_keys ? *n_used_p : max_keys;   // (overflow: flagged elsewhere)
   const unsigned long long stride = (unsigned long long)gridDim.x * kBlock;
   for (unsigned long long base = (unsigned long long)blockIdx.x * kBlock; base < n_used; base += stride) {
     const unsigned long long i = base + threadIdx.x;
@@ -1621,14 +1628,21 @@ __global__ __launch_bounds__(kBlock) void k_cap_scatter(const Slot* S, const uns
 constexpr int kCapLds = 16384;
 constexpr int kCapPer = 16;                 // entries per thread (1024 threads: a chunk of 16384)
 __global__ __launch_bounds__(1024) void k_cap_scatter_lds(const Slot* S, const unsigned long long* used,
-                                                          unsigned long long n_used, uint32_t n_capped,
+                                                          const unsigned long long* n_used_p,
+                                                          const unsigned int* n_capped_p, uint32_t lds_max,
                                                           const uint32_t* cidx, const uint32_t* capped_start,
                                                           uint32_t* capped_fill, unsigned long long* keys,
                                                           unsigned long long max_keys, unsigned int* flags) {
   __shared__ uint32_t cnt[kCapLds];
+  // counts are read on the device (no host round trip): a persistent grid
+  // walks the chunks of the used list
+  const uint32_t n_capped = *n_capped_p;
+  if (n_capped == 0 || n_capped > lds_max) return;   // workgroup-uniform
+  const unsigned long long n_used = *n_used_p < max_keys ? *n_used_p : max_keys;   // (overflow: flagged elsewhere)
+  const unsigned long long chunk = 1024ull * kCapPer;
+  for (unsigned long long base = (unsigned long long)blockIdx.x * chunk; base < n_used; base += gridDim.x * chunk) {
   for (uint32_t r = threadIdx.x; r < n_capped; r += blockDim.x) cnt[r] = 0;
   __syncthreads();
-  const unsigned long long base = (unsigned long long)blockIdx.x * (1024ull * kCapPer);
   uint32_t cc[kCapPer], rank[kCapPer];
   unsigned long long key[kCapPer];
 #pragma unroll
@@ -1657,6 +1671,8 @@ __global__ __launch_bounds__(1024) void k_cap_scatter_lds(const Slot* S, const u
     if (pos < max_keys) keys[pos] = key[k];
     else atomicOr(&flags[1], 16u);
   }
+  __syncthreads();   // cnt is reset for the next chunk
+  }
 }
 
 // One workgroup per capped rule: the cap-th smallest key of its segment.  A
@@ -1668,13 +1684,15 @@ constexpr int kSelThreads = 1024;
 __global__ __launch_bounds__(kSelThreads) void k_cap_select(const unsigned long long* keys,
                                                             const uint32_t* capped_start, const uint32_t* capped_fill,
                                                             const uint32_t* capped_gid, uint32_t cap,
-                                                            unsigned long long* out) {
+                                                            const unsigned int* n_capped_p, unsigned long long* out) {
   constexpr int kWaves = kSelThreads / 64;
   __shared__ uint32_t hist[kWaves][256];
   __shared__ unsigned long long red_min[kWaves], red_max[kWaves];
   __shared__ unsigned long long sh_prefix;
   __shared__ uint32_t sh_k;
-  const uint32_t c = blockIdx.x;
+  // a persistent grid over the capped rules (their number is read on the device)
+  const uint32_t n_capped = *n_capped_p;
+  for (uint32_t c = blockIdx.x; c < n_capped; c += gridDim.x) {
   const unsigned long long* seg = keys + capped_start[c];
   const uint32_t n = capped_fill[c];
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1754,6 +1772,8 @@ __global__ __launch_bounds__(kSelThreads) void k_cap_select(const unsigned long 
     shift = shift >= 8 ? shift - 8 : 0;
   }
   if (threadIdx.x == 0) out[capped_gid[c]] = sh_prefix + mn;
+  __syncthreads();   // the shared state is rewritten for the next rule
+  }
 }
 
 __device__ __forceinline__ rsa_conn_record make_record(const Slot& s, int which) {
@@ -2117,12 +2137,19 @@ int upload(rsa_ctx* c, T** dst, const T* src, size_t n) {
 // upper bound of it (the filter): first-seen orders only decrease and the set
 // of connections only grows as more lines are aggregated.
 int cap_select(rsa_ctx* c, unsigned long long* out, uint32_t* h_n_capped) {
-  int rc = check_flags(c);
-  if (rc) return rc;
+  // h_n_capped == nullptr: no host round trip (the filter steps of pass 1);
+  // the counts the kernels need (capped rules, used slots) are read on the
+  // device, the key buffer holds every slot, and the sticky error flags are
+  // checked by the final selection and the emission
+  if (h_n_capped) {
+    int rc = check_flags(c);
+    if (rc) return rc;
+    *h_n_capped = 0;
+  }
   const uint32_t nr = c->n_rules;
-  *h_n_capped = 0;
   if (nr == 0) return RSA_OK;
   if (c->cidx_len < nr) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     hipFree(c->d_cidx);
     hipFree(c->d_capped_gid);
     hipFree(c->d_capped_cnt);
@@ -2135,6 +2162,14 @@ int cap_select(rsa_ctx* c, unsigned long long* out, uint32_t* h_n_capped) {
     HIPCHK(c, hipMalloc(&c->d_capped_start, (size_t)nr * sizeof(uint32_t)));
     c->cidx_len = nr;
   }
+  if (c->sort_alloc < c->slot_cap) {   // a key per slot at most: sized once per table size
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    hipFree(c->d_keys);
+    c->d_keys = nullptr;
+    c->sort_alloc = 0;
+    HIPCHK(c, hipMalloc(&c->d_keys, c->slot_cap * sizeof(unsigned long long)));
+    c->sort_alloc = c->slot_cap;
+  }
   unsigned int* d_ncap = c->d_flags + 2;
   HIPCHK(c, hipMemsetAsync(d_ncap, 0, sizeof(unsigned int), c->stream));
   HIPCHK(c, hipMemsetAsync(c->d_cursor, 0, sizeof(unsigned long long), c->stream));
@@ -2142,37 +2177,28 @@ int cap_select(rsa_ctx* c, unsigned long long* out, uint32_t* h_n_capped) {
                                                                    c->d_capped_gid, c->d_capped_start,
                                                                    c->d_capped_cnt, d_ncap, c->d_cursor, out);
   HIPCHK(c, hipGetLastError());
-  unsigned int ncap = 0;
-  HIPCHK(c, hipMemcpyAsync(&ncap, d_ncap, sizeof ncap, hipMemcpyDeviceToHost, c->stream));
-  unsigned long long n_used = 0;
-  rc = used_count(c, &n_used);  // synchronises
-  if (rc) return rc;
-  *h_n_capped = ncap;
-  if (c->debug) fprintf(stderr, "[rsa] cap select: %u capped rules, %llu table entries\n", ncap, n_used);
-  if (ncap == 0) return RSA_OK;
-  if (c->sort_alloc < n_used) {
-    hipFree(c->d_keys);
-    c->d_keys = nullptr;
-    c->sort_alloc = 0;
-    const unsigned long long want = n_used + n_used / 4 + 1024;
-    HIPCHK(c, hipMalloc(&c->d_keys, want * sizeof(unsigned long long)));
-    c->sort_alloc = want;
-  }
-  if (n_used == 0) {
-  } else if (ncap <= (unsigned)kCapLds && !c->wave_cap_scatter) {
-    const unsigned long long chunk = 1024ull * kCapPer;
-    k_cap_scatter_lds<<<(unsigned)((n_used + chunk - 1) / chunk), 1024, 0, c->stream>>>(
-        c->d_slots, c->d_used, n_used, ncap, c->d_cidx, c->d_capped_start, c->d_capped_cnt, c->d_keys, c->sort_alloc,
-        c->d_flags);
-  } else {
-    k_cap_scatter<<<grid_for(c, n_used, 8), kBlock, 0, c->stream>>>(c->d_slots, c->d_used, n_used, c->d_cidx,
-                                                                    c->d_capped_start, c->d_capped_cnt, c->d_keys,
-                                                                    c->sort_alloc, c->d_flags);
-  }
+  // both scatter variants are launched; each exits unless the device-side
+  // count of capped rules is its case (LDS counters for <= kCapLds rules)
+  const uint32_t lds_max = c->wave_cap_scatter ? 0u : (uint32_t)kCapLds;
+  k_cap_scatter_lds<<<c->cu_count * 2, 1024, 0, c->stream>>>(c->d_slots, c->d_used, c->d_used_n, d_ncap, lds_max,
+                                                             c->d_cidx, c->d_capped_start, c->d_capped_cnt, c->d_keys,
+                                                             c->sort_alloc, c->d_flags);
+  k_cap_scatter<<<c->cu_count * 8, kBlock, 0, c->stream>>>(c->d_slots, c->d_used, c->d_used_n, d_ncap, lds_max,
+                                                          c->d_cidx, c->d_capped_start, c->d_capped_cnt, c->d_keys,
+                                                          c->sort_alloc, c->d_flags);
   HIPCHK(c, hipGetLastError());
-  k_cap_select<<<ncap, kSelThreads, 0, c->stream>>>(c->d_keys, c->d_capped_start, c->d_capped_cnt, c->d_capped_gid,
-                                                    c->cap, out);
+  const unsigned sel_grid = nr < (uint32_t)c->cu_count * 2 ? nr : (unsigned)c->cu_count * 2;
+  k_cap_select<<<sel_grid, kSelThreads, 0, c->stream>>>(c->d_keys, c->d_capped_start, c->d_capped_cnt, c->d_capped_gid,
+                                                        c->cap, d_ncap, out);
   HIPCHK(c, hipGetLastError());
+  if (h_n_capped) {
+    unsigned int ncap = 0;
+    HIPCHK(c, hipMemcpyAsync(&ncap, d_ncap, sizeof ncap, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    *h_n_capped = ncap;
+    if (c->debug) fprintf(stderr, "[rsa] cap select: %u capped rules\n", ncap);
+    return check_flags(c);
+  }
   return RSA_OK;
 }
 
@@ -2426,8 +2452,7 @@ int run_pass1(rsa_ctx* c, int classify, const rsa_tuple* T, const uint32_t* TS, 
     for (uint32_t step = 0; step < c->filter_steps && next < n; ++step) {
       rc = launch(done, next - done);
       if (rc) return rc;
-      uint32_t ncap = 0;
-      rc = cap_select(c, c->d_filter, &ncap);
+      rc = cap_select(c, c->d_filter, nullptr);   // on the device: no host round trip
       if (rc) return rc;
       done = next;
       next = next * 4;
@@ -2788,12 +2813,9 @@ int rsa_reset(rsa_ctx* c, uint64_t capacity, uint32_t cap) {
     c->slot_alloc = want;
     c->table_dirty = false;
   } else if (c->table_dirty) {
-    // clear exactly the slots the previous job used (they may lie anywhere in the allocation)
-    unsigned long long n_used = 0;
-    int rc = used_count(c, &n_used);
-    if (rc) return rc;
-    if (n_used)
-      k_table_clear<<<grid_for(c, n_used, 8), kBlock, 0, c->stream>>>(c->d_slots, c->d_used, n_used);
+    // clear exactly the slots the previous job used (they may lie anywhere in
+    // the allocation; their number is read on the device)
+    k_table_clear<<<c->cu_count * 8, kBlock, 0, c->stream>>>(c->d_slots, c->d_used, c->d_used_n, c->slot_alloc);
     HIPCHK(c, hipGetLastError());
     c->table_dirty = false;
   }
