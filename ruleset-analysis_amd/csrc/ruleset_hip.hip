@@ -262,6 +262,12 @@ typedef __attribute__((address_space(3))) const v4u lds_v4u;
 __device__ __forceinline__ v4u rd4(const lds_u32* img, uint32_t w) { return *reinterpret_cast<const lds_v4u*>(img + w); }
 __device__ __forceinline__ v4u rd4(const uint32_t* img, uint32_t w) { return *reinterpret_cast<const v4u*>(img + w); }
 __device__ __forceinline__ uint32_t rd16(const lds_u32* img, uint32_t h) { return reinterpret_cast<const lds_u16*>(img)[h]; }
+typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) const v2u lds_v2u;
+// two consecutive words at an even word offset: one ds_read_b64 (64 banks,
+// half the LDS cycles of the ds_read2_b32 pair)
+__device__ __forceinline__ v2u rd2(const lds_u32* img, uint32_t w) { return *reinterpret_cast<const lds_v2u*>(img + w); }
+__device__ __forceinline__ v2u rd2(const uint32_t* img, uint32_t w) { return *reinterpret_cast<const v2u*>(img + w); }
 __device__ __forceinline__ uint32_t rd16(const uint32_t* img, uint32_t h) { return reinterpret_cast<const uint16_t*>(img)[h]; }
 
 // CHD slot (compile.py pht_slot): x = (H + d * ((H >> 16) | 1)) mod 2^16,
@@ -351,8 +357,9 @@ __device__ __forceinline__ unsigned long long index_candidates(P32 img, uint32_t
       const uint32_t val = uu & fm;
       w[u] = ((uu >> sh) == (H[u] & fm) && val != fm) ? val : kNoCand;   // (mask_probe)
       const uint32_t bw = bm_off + 2 * (w[u] == kNoCand ? 0u : w[u]);
-      m[u].x = img[bw];
-      m[u].y = img[bw + 1];
+      const v2u bb = rd2(img, bw);   // bm_off is even (compile.py: alloc align=2)
+      m[u].x = bb.x;
+      m[u].y = bb.y;
     }
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
@@ -1091,11 +1098,38 @@ __global__ __launch_bounds__(1024) void k_aggregate(const uint4* __restrict__ T,
 constexpr uint32_t kPartTileMin = 8192, kPartTileMax = 262144, kPartTilesWant = 384;
 constexpr int kMaxRegions = 4096;
 
-// k_part_hist walks its tile kPartU windows per thread per iteration with
-// every load issued before the LDS atomics (one outstanding load per wave
-// left it latency-bound).  A wave's lanes cover one 64-slot window, so the
-// window's record count is a wave-uniform load.
-constexpr int kPartU = 4;
+// Both partition kernels walk their tile as groups of kPartW windows per wave:
+// the group's window counts are wave-uniform (scalar) loads, and the live
+// records of the group are dealt to the lanes densely (record q of the group ->
+// window k = #{prefix <= q}, slot q - prefix[k]), so a wave does ~one pass per
+// 64 records instead of one per 64 window slots (windows are ~1/3 full).
+// Tiles are multiples of 8192 lines, so a tile's first window is a multiple of
+// kPartW.
+constexpr int kPartW = 4;
+
+struct WinGroup {
+  uint32_t p1, p2, p3, tot;
+};
+
+__device__ __forceinline__ WinGroup win_group(const uint32_t* __restrict__ wcnt, unsigned long long w0,
+                                              unsigned long long wend) {
+  uint32_t c[kPartW];
+#pragma unroll
+  for (int k = 0; k < kPartW; ++k) c[k] = w0 + k < wend ? wcnt[w0 + k] : 0u;
+  WinGroup g;
+  g.p1 = c[0];
+  g.p2 = g.p1 + c[1];
+  g.p3 = g.p2 + c[2];
+  g.tot = g.p3 + c[3];
+  return g;
+}
+
+// line-slot index of record q (< g.tot) of the window group starting at w0
+__device__ __forceinline__ unsigned long long win_slot(const WinGroup& g, unsigned long long w0, uint32_t q) {
+  const uint32_t k = (uint32_t)(q >= g.p1) + (uint32_t)(q >= g.p2) + (uint32_t)(q >= g.p3);
+  const uint32_t pre = k == 0 ? 0u : k == 1 ? g.p1 : k == 2 ? g.p2 : g.p3;
+  return (w0 + k) * kWin + (q - pre);
+}
 
 __global__ __launch_bounds__(1024) void k_part_hist(const uint16_t* __restrict__ regs, const uint32_t* __restrict__ wcnt,
                                                     unsigned long long n, uint32_t n_regions, uint32_t n_tiles,
@@ -1106,18 +1140,17 @@ __global__ __launch_bounds__(1024) void k_part_hist(const uint16_t* __restrict__
   __syncthreads();
   const unsigned long long beg = (unsigned long long)tile * tile_len;
   const unsigned long long end = beg + tile_len < n ? beg + tile_len : n;
-  for (unsigned long long base = beg + threadIdx.x; base < end; base += (unsigned long long)blockDim.x * kPartU) {
-    uint32_t rg[kPartU];
-    bool live[kPartU];
-#pragma unroll
-    for (int k = 0; k < kPartU; ++k) {
-      const unsigned long long j = base + (unsigned long long)k * blockDim.x;
-      live[k] = j < end && (uint32_t)(j % kWin) < wcnt[j / kWin];
-      rg[k] = live[k] ? regs[j] : 0u;
+  const unsigned long long wend = (end + kWin - 1) / kWin;
+  const uint32_t lane = __lane_id(), nwv = blockDim.x >> 6;
+  for (unsigned long long w0 = beg / kWin + (threadIdx.x >> 6) * kPartW; w0 < wend; w0 += (unsigned long long)nwv * kPartW) {
+    const WinGroup g = win_group(wcnt, w0, wend);
+    for (uint32_t q = lane; q < g.tot; q += 2 * kWin) {   // two records per lane in flight
+      const bool two = q + kWin < g.tot;
+      const uint32_t r0 = regs[win_slot(g, w0, q)];
+      const uint32_t r1 = two ? regs[win_slot(g, w0, q + kWin)] : 0u;
+      atomicAdd(&hcount[r0], 1u);
+      if (two) atomicAdd(&hcount[r1], 1u);
     }
-#pragma unroll
-    for (int k = 0; k < kPartU; ++k)
-      if (live[k]) atomicAdd(&hcount[rg[k]], 1u);
   }
   __syncthreads();
   for (uint32_t r = threadIdx.x; r < n_regions; r += blockDim.x) hist[(size_t)r * n_tiles + tile] = hcount[r];
@@ -1133,9 +1166,16 @@ __global__ __launch_bounds__(1024) void k_part_scatter(const Rec* __restrict__ r
   __syncthreads();
   const unsigned long long beg = (unsigned long long)tile * tile_len;
   const unsigned long long end = beg + tile_len < n ? beg + tile_len : n;
-  for (unsigned long long j = beg + threadIdx.x; j < end; j += blockDim.x) {
-    if ((uint32_t)(j % kWin) >= wcnt[j / kWin]) continue;
-    out[atomicAdd(&cur[regs[j]], 1u)] = recs[j];
+  const unsigned long long wend = (end + kWin - 1) / kWin;
+  const uint32_t lane = __lane_id(), nwv = blockDim.x >> 6;
+  for (unsigned long long w0 = beg / kWin + (threadIdx.x >> 6) * kPartW; w0 < wend; w0 += (unsigned long long)nwv * kPartW) {
+    const WinGroup g = win_group(wcnt, w0, wend);
+    for (uint32_t q = lane; q < g.tot; q += kWin) {
+      const unsigned long long j = win_slot(g, w0, q);
+      const uint32_t rg = regs[j];
+      const Rec r = recs[j];
+      out[atomicAdd(&cur[rg], 1u)] = r;
+    }
   }
 }
 
