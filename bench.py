@@ -549,6 +549,13 @@ def rank_main(args, rank, world, local):
         }
         if world == 1 and not args.no_cpu_baseline:
             res['cpu_baseline'] = cpu_baseline(wl)
+            # SURVEY.md 8d's config-1 job (single pipeline and the Hadoop-like
+            # variant), measured by --cpu-baseline-only on the GPU box's host and
+            # committed (it takes minutes, too long for every bench run)
+            c1 = read_profile('config1_cpu_baseline.json')
+            if c1 is not None:
+                c1['source'] = 'profiles/config1_cpu_baseline.json (bench.py --cpu-baseline-only)'
+                res['cpu_baseline']['config1'] = c1
         print(json.dumps(res), flush=True)
     if dist is not None:
         dist.destroy_process_group()
