@@ -481,9 +481,10 @@ def rank_main(args, rank, world, local):
             recs = eng.emit_device('final')
             last['recs'] = recs
             return recs.numel() // RECORD_DTYPE.itemsize
-        out = merge(EngineBackend(eng, owner, [batch], [gbuf], cap), dist, world, rank)
+        # the merged records stay in rank 0's HBM, like the single-GPU result
+        out = merge(EngineBackend(eng, owner, [batch], [gbuf], cap), dist, world, rank, to_host=False)
         last['merged'] = out
-        return 0 if out is None else len(out[0])
+        return 0 if out is None else out[0].numel() // RECORD_DTYPE.itemsize
 
     for _ in range(args.warmup):
         step(False)
@@ -518,6 +519,26 @@ def rank_main(args, rank, world, local):
         checks.update(full_size_checks(eng, batch, gbuf, compiled.n_rules, cap, last['recs']))
         checks['ok'] = checks['ok'] and checks['rerun_identical_records']
         log('checks: %s' % json.dumps(checks))
+    elif not args.no_check:
+        # untimed checks of the distributed merge: the merged line counters
+        # cover every classified line of every shard; at world 1 the merged
+        # record set equals the single-GPU job's
+        n_cls = torch.tensor([int((gbuf >= 0).sum().item())], dtype=torch.int64, device=eng.device)
+        dist.all_reduce(n_cls)
+        if rank == 0:
+            mrecs, mmatches = last['merged'][0], last['merged'][1]
+            checks = {'merged_sum_matches_eq_classified_lines':
+                      int(mmatches[:compiled.n_rules].sum().item()) == int(n_cls.item()),
+                      'merged_record_checksum': '%016x' % record_checksum(mrecs)}
+            if world == 1:
+                eng.reset(capacity, cap)
+                eng.pass1(batch, gbuf)
+                if eng.resolve_cap():
+                    eng.pass2(batch, gbuf)
+                checks['merged_eq_single_gpu_records'] = record_checksum(eng.emit_device('final')) == \
+                    record_checksum(mrecs)
+            checks['ok'] = all(v for k, v in checks.items() if k != 'merged_record_checksum')
+            log('checks: %s' % json.dumps(checks))
     sum_e = scan_work(compiled, batch, gbuf) if rank == 0 else 0
     if rank == 0:
         total_lines = lines * world * args.steps
@@ -716,7 +737,8 @@ def text_main(args):
 def _dump(path, last, eng, cap):
     """TESTING: rank 0 writes the merged (or single-GPU) result as npz."""
     if 'merged' in last:
-        recs, matches, hits, distinct, thresh = last['merged']
+        from ruleset_analysis_amd.dist import merged_to_host
+        recs, matches, hits, distinct, thresh = merged_to_host(last['merged'])
     else:
         res = eng.results(cap)
         recs, matches, hits, distinct, thresh = res.records, res.matches, res.hits, res.distinct, res.thresh

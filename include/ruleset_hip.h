@@ -260,8 +260,12 @@ int rsa_emit(rsa_ctx *ctx, rsa_conn_record *d_out, uint64_t max_records, uint64_
 
 /* Multi-GPU merge (replaces the Hadoop shuffle, runAnalysis.sh:42-56).
  * rsa_export: every table entry with its pass-1 (which=0) or pass-2 (which=1)
- * aggregates; rsa_import: merge such records into this ctx's table (which=0:
- * insert-or-combine; which=1: combine into the pass-2 fields of existing keys). */
+ * aggregates, or (which=2) the pass-1 aggregates of only the entries that can
+ * still reach the report after rsa_resolve_cap on this shard's table: rules
+ * without a threshold, and entries with min_order <= the shard's P (which is
+ * >= the global P, so nothing that can matter is dropped); rsa_import: merge
+ * such records into this ctx's table (which=0: insert-or-combine; which=1:
+ * combine into the pass-2 fields of existing keys). */
 int rsa_table_size(rsa_ctx *ctx, uint64_t *h_n);
 int rsa_export(rsa_ctx *ctx, int which, rsa_conn_record *d_out, uint64_t max_records, uint64_t *h_n);
 int rsa_import(rsa_ctx *ctx, int which, const rsa_conn_record *d_in, uint64_t n);

@@ -1832,16 +1832,23 @@ __device__ __forceinline__ rsa_conn_record make_record(const Slot& s, int which)
   return r;
 }
 
-// mode 0: final report rows; mode 1: export pass-1 aggregates; mode 2: export pass-2.
+// mode 0: final report rows; mode 1: export pass-1 aggregates; mode 2: export pass-2;
+// mode 3: export the pass-1 aggregates of the entries that can still matter
+// under this table's own thresholds (rsa_resolve_cap): no threshold, or
+// min_order <= P (a shard's P bounds the global one from above).
 // Each thread takes kEmitU entries per iteration; one device atomic per
 // workgroup iteration reserves the output rows (a per-wave append on the one
 // cursor word serialises there).
 constexpr int kEmitU = 4;
-__global__ __launch_bounds__(1024) void k_emit(const Slot* S, const unsigned long long* used, unsigned long long n_used,
+__global__ __launch_bounds__(1024) void k_emit(const Slot* S, const unsigned long long* used,
+                                               const unsigned long long* n_used_p, unsigned long long slot_cap,
                                                const unsigned long long* thresh, int mode, rsa_conn_record* out,
                                                unsigned long long max_out, unsigned long long* cursor) {
   __shared__ uint32_t sh[18];
   __shared__ unsigned long long sh_base;
+  // the used-slot count is read on the device (persistent grid): no host
+  // round trip before the launch
+  const unsigned long long n_used = *n_used_p < slot_cap ? *n_used_p : slot_cap;
   const unsigned long long span = (unsigned long long)blockDim.x * kEmitU;
   for (unsigned long long base = (unsigned long long)blockIdx.x * span; base < n_used;
        base += (unsigned long long)gridDim.x * span) {
@@ -1860,6 +1867,9 @@ __global__ __launch_bounds__(1024) void k_emit(const Slot* S, const unsigned lon
           else if (sl[k].min_order <= P) which[k] = 1;
         } else if (mode == 1) {
           which[k] = 0;
+        } else if (mode == 3) {
+          const unsigned long long P = thresh[sl[k].kB >> 32];
+          if (P == RSA_NO_THRESHOLD || sl[k].min_order <= P) which[k] = 0;
         } else if (sl[k].count2 != 0) {
           which[k] = 1;
         }
@@ -2134,10 +2144,8 @@ unsigned grid_for(const rsa_ctx* c, unsigned long long n, unsigned per_cu) {
   return (unsigned)g;
 }
 
-int check_flags(rsa_ctx* c) {
-  unsigned int f[4];
-  HIPCHK(c, hipMemcpyAsync(f, c->d_flags, sizeof f, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+// The sticky error flags (d_flags[0..1]) of a host copy f of d_flags[0..3].
+int flags_status(rsa_ctx* c, const unsigned int* f) {
   if (f[0]) return fail(c, RSA_ERR_CAPACITY, "distinct-connection table overflow (capacity %llu)", c->slot_cap);
   if (f[1] & 1u) return fail(c, RSA_ERR_ARG, "tuple references a candidate list id >= n_lists (%u)", c->n_lists);
   if (f[1] & 2u) return fail(c, RSA_ERR_ARG, "rule id >= n_rules (%u)", c->n_rules);
@@ -2145,6 +2153,13 @@ int check_flags(rsa_ctx* c) {
   if (f[1] & 8u) return fail(c, RSA_ERR_STATE, "pass-2 import of a key absent from the table");
   if (f[1] & 16u) return fail(c, RSA_ERR_STATE, "cap selection: more entries than the table reported");
   return RSA_OK;
+}
+
+int check_flags(rsa_ctx* c) {
+  unsigned int f[4];
+  HIPCHK(c, hipMemcpyAsync(f, c->d_flags, sizeof f, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return flags_status(c, f);
 }
 
 int need_agg(rsa_ctx* c) {
@@ -2181,11 +2196,7 @@ int cap_select(rsa_ctx* c, unsigned long long* out, uint32_t* h_n_capped) {
   // the counts the kernels need (capped rules, used slots) are read on the
   // device, the key buffer holds every slot, and the sticky error flags are
   // checked by the final selection and the emission
-  if (h_n_capped) {
-    int rc = check_flags(c);
-    if (rc) return rc;
-    *h_n_capped = 0;
-  }
+  if (h_n_capped) *h_n_capped = 0;
   const uint32_t nr = c->n_rules;
   if (nr == 0) return RSA_OK;
   if (c->cidx_len < nr) {
@@ -2232,12 +2243,14 @@ int cap_select(rsa_ctx* c, unsigned long long* out, uint32_t* h_n_capped) {
                                                         c->cap, d_ncap, out);
   HIPCHK(c, hipGetLastError());
   if (h_n_capped) {
-    unsigned int ncap = 0;
-    HIPCHK(c, hipMemcpyAsync(&ncap, d_ncap, sizeof ncap, hipMemcpyDeviceToHost, c->stream));
+    // one round trip: the capped-rule count (d_flags[2]) with the sticky
+    // error flags, which also cover every launch before this selection
+    unsigned int f[4];
+    HIPCHK(c, hipMemcpyAsync(f, c->d_flags, sizeof f, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    *h_n_capped = ncap;
-    if (c->debug) fprintf(stderr, "[rsa] cap select: %u capped rules\n", ncap);
-    return check_flags(c);
+    *h_n_capped = f[2];
+    if (c->debug) fprintf(stderr, "[rsa] cap select: %u capped rules\n", f[2]);
+    return flags_status(c, f);
   }
   return RSA_OK;
 }
@@ -2508,17 +2521,18 @@ int emit_mode(rsa_ctx* c, int mode, rsa_conn_record* out, uint64_t max_out, uint
   int rc = need_agg(c);
   if (rc) return rc;
   if (max_out && !out) return fail(c, RSA_ERR_ARG, "null output buffer");
-  unsigned long long n_used = 0;
-  rc = used_count(c, &n_used);
-  if (rc) return rc;
   HIPCHK(c, hipMemsetAsync(c->d_cursor, 0, sizeof(unsigned long long), c->stream));
-  if (n_used)
-    k_emit<<<grid_for_threads(c, (n_used + kEmitU - 1) / kEmitU, 1024, 2), 1024, 0, c->stream>>>(
-        c->d_slots, c->d_used, n_used, c->d_thresh, mode, out, max_out, c->d_cursor);
+  // persistent grid (two 1024-thread workgroups per CU) over the device-side
+  // used count; one round trip for the emitted count and the error flags
+  k_emit<<<c->cu_count * 2, 1024, 0, c->stream>>>(c->d_slots, c->d_used, c->d_used_n, c->slot_cap, c->d_thresh, mode,
+                                                  out, max_out, c->d_cursor);
   HIPCHK(c, hipGetLastError());
   unsigned long long n = 0;
+  unsigned int f[4];
   HIPCHK(c, hipMemcpyAsync(&n, c->d_cursor, sizeof n, hipMemcpyDeviceToHost, c->stream));
-  rc = check_flags(c);  // synchronises
+  HIPCHK(c, hipMemcpyAsync(f, c->d_flags, sizeof f, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  rc = flags_status(c, f);
   if (rc) return rc;
   *h_n = n;
   if (n > max_out) return fail(c, RSA_ERR_CAPACITY, "%llu records do not fit in %llu", n, (unsigned long long)max_out);
@@ -2987,8 +3001,8 @@ int rsa_emit(rsa_ctx* c, rsa_conn_record* out, uint64_t max_out, uint64_t* h_n) 
 }
 
 int rsa_export(rsa_ctx* c, int which, rsa_conn_record* out, uint64_t max_out, uint64_t* h_n) {
-  if (which != 0 && which != 1) return fail(c, RSA_ERR_ARG, "which must be 0 or 1");
-  return emit_mode(c, which ? 2 : 1, out, max_out, h_n);
+  if (which < 0 || which > 2) return fail(c, RSA_ERR_ARG, "which must be 0, 1 or 2");
+  return emit_mode(c, which == 2 ? 3 : which ? 2 : 1, out, max_out, h_n);
 }
 
 int rsa_import(rsa_ctx* c, int which, const rsa_conn_record* in, uint64_t n) {

@@ -26,7 +26,7 @@ import numpy as np
 
 from .compile import RECORD_DTYPE
 
-__all__ = ['merge', 'EngineBackend', 'route_records']
+__all__ = ['merge', 'merged_to_host', 'EngineBackend', 'route_records']
 
 REC = RECORD_DTYPE.itemsize
 NO_THRESHOLD = -1   # 0xFFFF_FFFF_FFFF_FFFF viewed as int64
@@ -70,6 +70,50 @@ def _all_gather(parts, t, dist, group):
         dist.all_gather(parts, t, group=group)
 
 
+def _gather0(t, sizes, rank, world, dist, group):
+    """Rows of every rank to rank 0 only (the emission rank): dist.gather of
+    equal-size padded buffers (RCCL point-to-point sends over xGMI; the other
+    ranks receive nothing).  Returns the list of parts on rank 0, else None."""
+    import torch
+    pad = max(max(sizes), 1)
+    padded = torch.zeros(pad, dtype=torch.uint8, device=t.device)
+    padded[:t.numel()] = t
+    staged = t.is_cuda and _host_staged(dist, group)
+    src = padded.cpu() if staged else padded
+    parts = None
+    if rank == 0:
+        parts = [torch.empty(pad, dtype=torch.uint8, device=src.device) for _ in range(world)]
+    dist.gather(src, gather_list=parts, dst=0, group=group)
+    if rank != 0:
+        return None
+    return [(p.to(t.device) if staged else p)[:s] for p, s in zip(parts, sizes)]
+
+
+class _Trace(object):
+    """RSA_MERGE_TRACE=1: per-phase wall time of the merge on stderr (with a
+    device synchronise per phase, so only for diagnosis)."""
+
+    def __init__(self, rank):
+        import os
+        import time
+        self.on = os.environ.get('RSA_MERGE_TRACE') == '1'
+        self.rank, self.time, self.t, self.parts = rank, time, None, []
+
+    def __call__(self, what, dev=None):
+        if not self.on:
+            return
+        import sys
+        import torch
+        if dev is not None and dev.type == 'cuda':
+            torch.cuda.synchronize(dev)
+        now = self.time.perf_counter()
+        if self.t is not None:
+            self.parts.append('%s %.2f' % (what, (now - self.t) * 1e3))
+        self.t = now
+        if what == 'end':
+            sys.stderr.write('[merge rank %d] ms: %s\n' % (self.rank, ', '.join(self.parts)))
+
+
 def torch_empty_like_cpu(t):
     import torch
     return torch.empty(t.shape, dtype=t.dtype)
@@ -95,45 +139,69 @@ def route_records(buf, world, dist, group=None):
     return out
 
 
-def merge(backend, dist, world, rank, group=None):
-    """Run the protocol; returns (records ndarray, matches, hits, distinct, thresh) on
-    rank 0 and None elsewhere."""
+def merge(backend, dist, world, rank, group=None, to_host=True):
+    """Run the protocol; returns (records, matches, hits, distinct, thresh) on
+    rank 0 and None elsewhere: numpy arrays (records as RECORD_DTYPE rows), or
+    with to_host=False the device tensors as they stand in rank 0's HBM
+    (records as uint8 rows; see merged_to_host), which is where the
+    single-GPU job leaves its result too."""
     import torch
+    tr = _Trace(rank)
     c = backend.local_counters()
+    dev = c['matches'].device
+    tr('start', dev)
     _all_reduce(c['matches'], dist, group)
     _all_reduce(c['hits'], dist, group)
-    recv = route_records(backend.export(0), world, dist, group)
+    tr('counters', dev)
+    exported = backend.export(0)
+    tr('export1', dev)
+    recv = route_records(exported, world, dist, group)
+    tr('route1', dev)
     backend.owner_reset(max(recv.numel() // REC, 1))
     backend.owner_import(recv, 0)
+    tr('import1', dev)
     backend.owner_resolve_cap()
     oc = backend.owner_counters()
     thresh = oc['thresh'].clone()
     _all_reduce(thresh, dist, group, op=dist.ReduceOp.MAX)
     capped_any = bool((thresh != NO_THRESHOLD).any().item())
+    tr('cap', dev)
     if capped_any:
         backend.set_local_thresh(thresh)
         backend.local_recount()
         recv2 = route_records(backend.export(1), world, dist, group)
         backend.owner_import(recv2, 1)
         backend.set_owner_thresh(thresh)
+        tr('pass2', dev)
     final = backend.owner_emit()
     distinct = oc['distinct'].clone()
     _all_reduce(distinct, dist, group)
-    # gather the owners' rows to rank 0 (padded all_gather: sizes first)
+    tr('emit', dev)
+    # the owners' rows to rank 0 (sizes first: one int per rank)
     size = torch.tensor([final.numel()], dtype=torch.int64, device=final.device)
     sizes = [torch.zeros_like(size) for _ in range(world)]
     _all_gather(sizes, size, dist, group)
     sizes = [int(s.item()) for s in sizes]
-    pad = max(max(sizes), 1)
-    padded = torch.zeros(pad, dtype=torch.uint8, device=final.device)
-    padded[:final.numel()] = final
-    parts = [torch.empty(pad, dtype=torch.uint8, device=final.device) for _ in range(world)]
-    _all_gather(parts, padded, dist, group)
+    parts = _gather0(final, sizes, rank, world, dist, group)
+    tr('gather', dev)
     if rank != 0:
+        tr('end')
         return None
-    recs = np.concatenate([p[:s].cpu().numpy() for p, s in zip(parts, sizes)]).view(RECORD_DTYPE)
-    return (recs.copy(), c['matches'].cpu().numpy().view(np.uint64).copy(),
-            c['hits'].cpu().numpy().view(np.uint64).copy(), distinct.cpu().numpy().view(np.uint32).copy(),
+    recs = parts[0] if world == 1 else torch.cat(parts)
+    out = (recs, c['matches'], c['hits'], distinct, thresh)
+    if to_host:
+        out = merged_to_host(out)
+    tr('end', dev)
+    return out
+
+
+def merged_to_host(out):
+    """merge(..., to_host=False)'s device tensors as merge()'s numpy result."""
+    if out is None or isinstance(out[0], np.ndarray):
+        return out
+    recs, matches, hits, distinct, thresh = out
+    return (recs.cpu().numpy().view(RECORD_DTYPE).copy(), matches.cpu().numpy().view(np.uint64).copy(),
+            hits.cpu().numpy().view(np.uint64).copy(), distinct.cpu().numpy().view(np.uint32).copy(),
             thresh.cpu().numpy().view(np.uint64).copy())
 
 
@@ -153,7 +221,14 @@ class EngineBackend(object):
         return self.local.counters
 
     def export(self, which):
-        return self.local.emit_device('pass1' if which == 0 else 'pass2')
+        if which == 0:
+            # the shard's own cap resolution first: its P bounds the global P
+            # from above, so only entries with min_order <= P (or of rules
+            # without a threshold) can reach the report; the rest stay home
+            # (exact; fewer records over xGMI and into the owners' tables)
+            self.local.resolve_cap()
+            return self.local.emit_device('pass1_kept')
+        return self.local.emit_device('pass2')
 
     def owner_reset(self, capacity):
         self.owner.reset(capacity, self.cap)

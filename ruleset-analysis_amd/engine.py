@@ -15,6 +15,7 @@ import ctypes
 import numpy as np
 
 from . import native
+from .native import RSA_ERR_CAPACITY, NativeError
 from .compile import RECORD_DTYPE, TUPLE_DTYPE
 
 __all__ = ['Engine', 'Results', 'DeviceBatch']
@@ -74,6 +75,7 @@ class Engine(object):
         self.device = torch.device('cuda', device)
         torch.cuda.set_device(self.device)
         self.ctx = native.Ctx(device)
+        self._emit_buf, self._emit_cap = None, 0   # emission buffer kept between calls (emit_device)
         self.stream = torch.cuda.current_stream(self.device)
         self.ctx.call('rsa_set_stream', ctypes.c_void_p(self.stream.cuda_stream))
         self.n_rules = 0
@@ -181,17 +183,40 @@ class Engine(object):
         return int(n.value)
 
     def emit_device(self, mode='final'):
-        """Records as a torch uint8 tensor [M*40] on device."""
-        torch = self.torch
-        size = self.table_size()
-        buf = torch.empty(max(size, 1) * RECORD_DTYPE.itemsize, dtype=torch.uint8, device=self.device)
+        """Records as a torch uint8 tensor [M*40] on device (a view of a buffer
+        the engine keeps between calls).  The buffer is sized from the last
+        table size seen; only when the records do not fit (the library reports
+        the count it needed) is the table size read and the emission repeated,
+        so a steady job pays one host round trip here, not two."""
         n = ctypes.c_uint64(0)
-        if mode == 'final':
-            self.ctx.call('rsa_emit', _ptr(buf), ctypes.c_uint64(size), ctypes.byref(n))
-        else:
-            which = 0 if mode == 'pass1' else 1
-            self.ctx.call('rsa_export', ctypes.c_int(which), _ptr(buf), ctypes.c_uint64(size), ctypes.byref(n))
+        size = self._emit_cap
+        if size == 0:
+            size = self.table_size()
+        for _ in range(2):
+            buf = self._emit_buffer(size)
+            try:
+                if mode == 'final':
+                    self.ctx.call('rsa_emit', _ptr(buf), ctypes.c_uint64(size), ctypes.byref(n))
+                else:
+                    which = {'pass1': 0, 'pass2': 1, 'pass1_kept': 2}[mode]
+                    self.ctx.call('rsa_export', ctypes.c_int(which), _ptr(buf), ctypes.c_uint64(size),
+                                  ctypes.byref(n))
+                break
+            except NativeError as e:
+                if e.code != RSA_ERR_CAPACITY or int(n.value) <= size:
+                    raise
+                size = self.table_size()
+        # the buffer is reused by the next emission: callers that keep records
+        # across calls clone them
         return buf[: int(n.value) * RECORD_DTYPE.itemsize]
+
+    def _emit_buffer(self, size):
+        size = max(int(size), 1)
+        if self._emit_buf is None or self._emit_cap < size:
+            self._emit_buf = self.torch.empty(size * RECORD_DTYPE.itemsize, dtype=self.torch.uint8,
+                                              device=self.device)
+            self._emit_cap = size
+        return self._emit_buf
 
     def import_records(self, buf, which):
         n = buf.numel() // RECORD_DTYPE.itemsize

@@ -95,6 +95,16 @@ def test_synth_parity_uncapped(engine):
     _gpu_vs_oracle(engine, 600, 200000, 1000, seed=11)
 
 
+def test_emit_buffer_regrows(engine):
+    """The engine's kept emission buffer starts too small: the library reports
+    the count it needed, the engine grows the buffer and emits again; the
+    records still match the oracle exactly."""
+    engine._emit_buf, engine._emit_cap = None, 0
+    engine._emit_buffer(1)
+    _gpu_vs_oracle(engine, 400, 60000, 30, seed=41)
+    assert engine._emit_cap > 1
+
+
 def test_synth_parity_linear_scan(engine):
     _gpu_vs_oracle(engine, 3000, 200000, 100, seed=18, index=False)
 
