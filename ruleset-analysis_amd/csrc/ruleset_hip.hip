@@ -135,19 +135,21 @@ __device__ __forceinline__ unsigned long long slot_hash(unsigned long long kA, u
   return mix64(kA ^ (kB * 0x9e3779b97f4a7c15ull));
 }
 
-// counter[key] += 1 for every lane with `ok`, one device atomic per distinct key
-// in the wave (lanes sharing a rule are counted first: hot rules would otherwise
-// serialise thousands of atomics on one address).  Wave-uniform control flow.
+// counter[key] += 1 for every lane with `ok`: the lanes sharing the key of the
+// first such lane are counted with one atomic (a rule that dominates the wave),
+// every other lane adds its own (device atomics on distinct addresses proceed
+// in parallel; a full waterfall would serialise up to 64 rounds on waves whose
+// keys are all different, the common case for fresh table entries).
+// Wave-uniform control flow.
 template <typename T>
-__device__ __forceinline__ void wave_count_by_key(bool ok, uint32_t key, T* counter) {
-  unsigned long long pending = __ballot(ok);
-  while (pending) {
-    const int leader = __builtin_ctzll(pending);
-    const uint32_t k = __builtin_amdgcn_readlane(key, leader);
-    const unsigned long long peers = __ballot(ok && key == k);
-    pending &= ~peers;
-    if ((int)__lane_id() == leader) atomicAdd(&counter[k], (T)__popcll(peers));
-  }
+__device__ __forceinline__ void wave_count_hot(bool ok, uint32_t key, T* counter) {
+  const unsigned long long pending = __ballot(ok);
+  if (!pending) return;
+  const int leader = __builtin_ctzll(pending);
+  const uint32_t k = __builtin_amdgcn_readlane(key, leader);
+  const unsigned long long peers = __ballot(ok && key == k);
+  if ((int)__lane_id() == leader) atomicAdd(&counter[k], (T)__popcll(peers));
+  if (ok && key != k) atomicAdd(&counter[key], (T)1);
 }
 
 // Wave-aggregated append to a global cursor: one atomic per wave.  Wave-uniform
@@ -1484,7 +1486,7 @@ __global__ __launch_bounds__(1024) void k_reduce(const Rec* __restrict__ recs,
           e_kB[e] = kEmpty;
         }
         if (kPass == 1) {
-          wave_count_by_key(fresh, gid, A.distinct);
+          wave_count_hot(fresh, gid, A.distinct);
           is_new[q] = fresh;
           new_slot[q] = ((unsigned long long)gid << 32) | (uint32_t)slot;
         }
@@ -1917,7 +1919,7 @@ __global__ __launch_bounds__(kBlock) void k_import(const rsa_conn_record* __rest
         }
       }
     }
-    wave_count_by_key(fresh, gid, A.distinct);
+    wave_count_hot(fresh, gid, A.distinct);
     const unsigned long long pos = wave_append(fresh, A.used_n);
     if (fresh) A.used[pos] = ((unsigned long long)gid << 32) | (uint32_t)slot;
   }
@@ -2153,13 +2155,6 @@ int flags_status(rsa_ctx* c, const unsigned int* f) {
   if (f[1] & 8u) return fail(c, RSA_ERR_STATE, "pass-2 import of a key absent from the table");
   if (f[1] & 16u) return fail(c, RSA_ERR_STATE, "cap selection: more entries than the table reported");
   return RSA_OK;
-}
-
-int check_flags(rsa_ctx* c) {
-  unsigned int f[4];
-  HIPCHK(c, hipMemcpyAsync(f, c->d_flags, sizeof f, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  return flags_status(c, f);
 }
 
 int need_agg(rsa_ctx* c) {

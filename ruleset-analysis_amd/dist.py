@@ -127,7 +127,10 @@ def route_records(buf, world, dist, group=None):
     gid = rows[:, 8:12].contiguous().view(torch.int32).view(-1).to(torch.int64) if n else \
         torch.zeros(0, dtype=torch.int64, device=buf.device)
     owner = gid % world
-    perm = torch.argsort(owner, stable=True)
+    # owner ids as the narrowest key type: the stable device sort is then one
+    # radix pass over 8-bit keys instead of eight over int64
+    okey = owner.to(torch.uint8 if world <= 256 else torch.int32)
+    perm = torch.argsort(okey, stable=True)
     send = rows[perm].contiguous().view(-1)
     counts = torch.bincount(owner, minlength=world).to(torch.int64)
     recv_counts = torch.empty_like(counts)
