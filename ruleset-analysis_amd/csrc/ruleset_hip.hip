@@ -152,19 +152,6 @@ __device__ __forceinline__ void wave_count_hot(bool ok, uint32_t key, T* counter
   if (ok && key != k) atomicAdd(&counter[key], (T)1);
 }
 
-// Wave-aggregated append to a global cursor: one atomic per wave.  Wave-uniform
-// control flow.
-__device__ __forceinline__ unsigned long long wave_append(bool ok, unsigned long long* cursor) {
-  const unsigned long long mask = __ballot(ok);
-  if (mask == 0) return 0;
-  const unsigned lane = __lane_id();
-  const int leader = __builtin_ctzll(mask);
-  unsigned long long base = 0;
-  if ((int)lane == leader) base = atomicAdd(cursor, (unsigned long long)__popcll(mask));
-  base = __shfl(base, leader);
-  return base + __popcll(mask & ((1ull << lane) - 1ull));
-}
-
 // Home slot of a key hash: region = top np_bits, offset = low rs_bits.
 __device__ __forceinline__ unsigned long long slot_home(const Agg& A, unsigned long long hh) {
   const unsigned long long r = A.np_bits ? (hh >> (64 - A.np_bits)) : 0ull;
@@ -1893,10 +1880,15 @@ __global__ __launch_bounds__(1024) void k_emit(const Slot* S, const unsigned lon
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_import(const rsa_conn_record* __restrict__ in, unsigned long long n,
-                                                   int which, Agg A) {
-  const unsigned long long stride = (unsigned long long)gridDim.x * kBlock;
-  for (unsigned long long base = (unsigned long long)blockIdx.x * kBlock; base < n; base += stride) {
+// New slots are appended to the used list with one device atomic per 1024
+// records (workgroup scan), not one per wave: every import record of a fresh
+// owner table is new, and per-wave appends serialise on the one cursor word.
+__global__ __launch_bounds__(1024) void k_import(const rsa_conn_record* __restrict__ in, unsigned long long n,
+                                                 int which, Agg A) {
+  __shared__ uint32_t sh[18];
+  __shared__ unsigned long long sh_base;
+  const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+  for (unsigned long long base = (unsigned long long)blockIdx.x * blockDim.x; base < n; base += stride) {
     const unsigned long long i = base + threadIdx.x;
     bool fresh = false;
     unsigned long long slot = kEmpty;
@@ -1920,8 +1912,12 @@ __global__ __launch_bounds__(kBlock) void k_import(const rsa_conn_record* __rest
       }
     }
     wave_count_hot(fresh, gid, A.distinct);
-    const unsigned long long pos = wave_append(fresh, A.used_n);
-    if (fresh) A.used[pos] = ((unsigned long long)gid << 32) | (uint32_t)slot;
+    uint32_t total;
+    const uint32_t off = block_exscan(fresh ? 1u : 0u, sh, &total);   // workgroup-uniform trip count
+    if (threadIdx.x == 0) sh_base = total ? atomicAdd(A.used_n, (unsigned long long)total) : 0ull;
+    __syncthreads();
+    if (fresh) A.used[sh_base + off] = ((unsigned long long)gid << 32) | (uint32_t)slot;
+    __syncthreads();
   }
 }
 
@@ -3008,7 +3004,7 @@ int rsa_import(rsa_ctx* c, int which, const rsa_conn_record* in, uint64_t n) {
   if (n == 0) return RSA_OK;
   if (!in) return fail(c, RSA_ERR_ARG, "null input records");
   c->table_dirty = true;
-  k_import<<<grid_for(c, n, 16), kBlock, 0, c->stream>>>(in, n, which, agg_of(c));
+  k_import<<<grid_for_threads(c, n, 1024, 4), 1024, 0, c->stream>>>(in, n, which, agg_of(c));
   HIPCHK(c, hipGetLastError());
   return RSA_OK;
 }
