@@ -461,16 +461,45 @@ def rank_main(args, rank, world, local):
     log('rank %d setup %.1fs: %d rules, %d lists, %d entries, %d lines, %d hit+built' % (
         rank, time.perf_counter() - t_setup, compiled.n_rules, compiled.n_lists(), len(ent), lines, n_hb))
 
-    # table capacity: the exact upper bound (every hit line a new connection),
-    # clamped by the library to its largest table; only the slots a job uses
-    # are cleared between jobs
-    capacity = args.capacity or max(n_hb, 1)
+    # table capacity.  The exact upper bound is every hit+BUILT line a new
+    # connection (clamped by the library to its largest table); the first
+    # warmup job runs with it, and later jobs over the same log are sized to 4x
+    # the distinct entries that job actually used (max over ranks), the way a
+    # stream of similar batches is sized from the last one: a 4x smaller table
+    # has 4x fewer regions and spans far fewer pages, so the slot traffic of
+    # the region sort and reduction is cheaper.  A job whose
+    # table overflows anyway fails with RSA_ERR_CAPACITY and is rerun at the
+    # bound (single GPU; the re-run is inside the timed step when it happens).
+    bound = max(n_hb, 1)
+    sizing = {'capacity': args.capacity or bound, 'learn': not args.capacity, 'reruns': 0}
     pass1_launch_ms = []
     pass1_launches = []
     last = {}
 
     def step(timed):
-        eng.reset(capacity, cap)
+        if dist is not None:
+            return job(timed)
+        n_t, n_l = len(pass1_launch_ms), len(pass1_launches)
+        try:
+            r = job(timed)
+        except native.NativeError as e:
+            if e.code != native.RSA_ERR_CAPACITY or sizing['capacity'] >= bound:
+                raise
+            del pass1_launch_ms[n_t:], pass1_launches[n_l:]
+            sizing['capacity'] = bound
+            sizing['reruns'] += 1
+            r = job(timed)
+        return r
+
+    def learn_capacity():
+        used = torch.tensor([eng.table_size()], dtype=torch.int64, device=eng.device)
+        if dist is not None:
+            dist.all_reduce(used, op=dist.ReduceOp.MAX)
+        sizing['capacity'] = min(bound, max(4 * int(used.item()), 1 << 20))
+        sizing['learn'] = False
+
+    def job(timed):
+        eng.reset(sizing['capacity'], cap)
         eng.pass1(batch, gbuf)
         if timed:
             pass1_launch_ms.append(eng.last_pass1_times())
@@ -486,8 +515,10 @@ def rank_main(args, rank, world, local):
         last['merged'] = out
         return 0 if out is None else out[0].numel() // RECORD_DTYPE.itemsize
 
-    for _ in range(args.warmup):
+    for w in range(max(args.warmup, 1 if sizing['learn'] else 0)):
         step(False)
+        if sizing['learn']:
+            learn_capacity()
 
     if dist is not None:
         dist.barrier()
@@ -531,7 +562,7 @@ def rank_main(args, rank, world, local):
                       int(mmatches[:compiled.n_rules].sum().item()) == int(n_cls.item()),
                       'merged_record_checksum': '%016x' % record_checksum(mrecs)}
             if world == 1:
-                eng.reset(capacity, cap)
+                eng.reset(sizing['capacity'], cap)
                 eng.pass1(batch, gbuf)
                 if eng.resolve_cap():
                     eng.pass2(batch, gbuf)
@@ -556,7 +587,11 @@ def rank_main(args, rank, world, local):
                                    % (args.config, wl.describe, compiled.n_rules, len(ent), lines, cap),
                        'rules': compiled.n_rules, 'entries': len(ent), 'lines_per_gpu': lines, 'cap': cap,
                        'parallelism': 'dp%d' % world,
-                       'backend': args.backend if dist is not None else 'none', 'records': n_rec},
+                       'backend': args.backend if dist is not None else 'none', 'records': n_rec,
+                       'table_capacity': sizing['capacity'], 'capacity_bound': bound,
+                       'capacity_reruns': sizing['reruns'],
+                       'capacity_policy': 'first warmup job at the bound (hit+BUILT lines), then 4x the distinct '
+                                          'entries it used; rerun at the bound on overflow'},
             'roofline': roofline_block(lines, classify_ms, aggregate_ms, float(np.mean(pass1_launches)),
                                        dt / args.steps * 1e3, pmc, sq, args.config),
             'scan_work': {'mean_scan_position': sum_e / lines,

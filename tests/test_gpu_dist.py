@@ -104,3 +104,29 @@ def test_bench_force_dist_one_gpu(tmp_path, backend):
                                      '--lines', str(lines), '--cap', str(cap), '--no-check'], timeout=400)
     assert line['n_gpus'] == 1 and line['config']['backend'] == backend
     check_dump_against_oracle(got, 1, rules, lines, cap)
+
+
+def test_bench_capacity_rerun(tmp_path):
+    """bench.py's table sizing: a job whose table is too small overflows
+    (RSA_ERR_CAPACITY), is rerun at the exact bound, and the result still equals
+    the C oracle."""
+    from test_bench_spawn import check_dump_against_oracle, run_bench
+    rules, lines, cap = 800, 400000, 40
+    line, got = run_bench(tmp_path, ['--rules', str(rules), '--lines', str(lines), '--cap', str(cap),
+                                     '--capacity', '2000', '--no-check'], timeout=400)
+    assert line['config']['capacity_reruns'] == 1
+    assert line['config']['table_capacity'] == line['config']['capacity_bound']
+    check_dump_against_oracle(got, 1, rules, lines, cap)
+
+
+def test_bench_learned_capacity(tmp_path):
+    """The default sizing (4x the warmup job's distinct entries, at least 2^20,
+    at most the bound) gives the same result as the oracle, with the full-size
+    checks of the bench green."""
+    from test_bench_spawn import check_dump_against_oracle, run_bench
+    rules, lines, cap = 800, 400000, 40
+    line, got = run_bench(tmp_path, ['--rules', str(rules), '--lines', str(lines), '--cap', str(cap)], timeout=400)
+    assert line['config']['table_capacity'] <= line['config']['capacity_bound']
+    assert line['config']['capacity_reruns'] == 0
+    assert line['checks']['ok']
+    check_dump_against_oracle(got, 1, rules, lines, cap)
