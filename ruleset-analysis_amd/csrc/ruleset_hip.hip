@@ -1244,8 +1244,11 @@ __device__ __forceinline__ unsigned long long readlane64(unsigned long long v, i
   return ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) |
          __builtin_amdgcn_readlane((uint32_t)v, l);
 }
+#ifndef RSA_RED2_WPE
+#define RSA_RED2_WPE 8   // pass 2: 64 VGPRs, two 1024-thread workgroups per CU (73 KiB LDS each)
+#endif
 template <int kPass>
-__global__ __launch_bounds__(1024) void k_reduce(const Rec* __restrict__ recs,
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2 ? RSA_RED2_WPE : 4, 8))) void k_reduce(const Rec* __restrict__ recs,
                                                  const unsigned long long* __restrict__ starts, uint32_t n_segs,
                                                  Agg A) {
   __shared__ unsigned long long e_kA[kRedE<kPass>], e_kB[kRedE<kPass>], e_mo[kRedE<kPass>];
