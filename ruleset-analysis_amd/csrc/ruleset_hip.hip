@@ -1244,6 +1244,9 @@ __device__ __forceinline__ unsigned long long readlane64(unsigned long long v, i
   return ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) |
          __builtin_amdgcn_readlane((uint32_t)v, l);
 }
+#ifndef RSA_COUNT_PER_CU
+#define RSA_COUNT_PER_CU 1   // k_count workgroups per CU (one is resident: 104 KiB LDS); fewer workgroups, fewer histogram-flush atomics
+#endif
 #ifndef RSA_RED2_WPE
 #define RSA_RED2_WPE 8   // pass 2: 64 VGPRs, two 1024-thread workgroups per CU (73 KiB LDS each)
 #endif
@@ -2374,7 +2377,7 @@ int launch_aggregate(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsig
     if (!(ag.skip & 1u)) {
       const uint64_t units = (m + 3) / 4;
       if (c->n_rules <= (uint32_t)kCnt) {
-        k_count<kCnt><<<grid_for_threads(c, units, 1024, 2), 1024, 0, c->stream>>>(gh, m, c->n_rules, ag);
+        k_count<kCnt><<<grid_for_threads(c, units, 1024, RSA_COUNT_PER_CU), 1024, 0, c->stream>>>(gh, m, c->n_rules, ag);
       } else {
         k_count<0><<<grid_for_threads(c, units, 1024, 8), 1024, 0, c->stream>>>(gh, m, c->n_rules, ag);
       }
