@@ -86,19 +86,38 @@ def mapper_main(argv=None):
     compiled = CompiledRules(db)
     compiled.ensure_lists()
     eng = Engine(0)
-    data = sys.stdin.buffer.read()
-    # the log text is parsed on the GPU (textparse); lines outside the device
-    # grammar are decided by the host parser, in line order
-    parsed = parse_text(eng, hostname, data, db, compiled, need_order=False)
-    if parsed.n:
-        eng.load_compiled(compiled)
-        gids = eng.classify_only(parsed.batch()).cpu().numpy()
-    else:
-        gids = np.zeros(0, np.int32)
-    _write(mapper_output(parsed, gids, compiled))
-    sys.stdout.flush()
-    if parsed.error is not None:
-        raise parsed.error[1]
+    eng.load_compiled(compiled)
+    # stdin is streamed in chunks of whole lines (RSA_MAPPER_CHUNK bytes, cut
+    # after the chunk's last '\n'; the final chunk keeps a last line without
+    # one), so output starts before the input ends and memory stays bounded:
+    # the mapper's lines are independent (mapper.py:119-189).  Each chunk's
+    # text is parsed on the GPU (textparse); lines outside the device grammar
+    # are decided by the host parser, in line order; an error line stops the
+    # stream after the lines before it, as the reference dies there.
+    chunk = max(int(os.environ.get('RSA_MAPPER_CHUNK', 256 << 20)), 1)
+    src = sys.stdin.buffer
+    carry = b''
+    while True:
+        block = src.read(chunk)
+        data = carry + block
+        if not data:
+            break
+        if block:
+            cut = data.rfind(b'\n') + 1
+            if cut == 0:          # no complete line yet: read on
+                carry = data
+                continue
+            data, carry = data[:cut], data[cut:]
+        else:
+            carry = b''
+        parsed = parse_text(eng, hostname, data, db, compiled, need_order=False)
+        gids = eng.classify_only(parsed.batch()).cpu().numpy() if parsed.n else np.zeros(0, np.int32)
+        _write(mapper_output(parsed, gids, compiled))
+        sys.stdout.flush()
+        if parsed.error is not None:
+            raise parsed.error[1]
+        if not block:
+            break
     return 0
 
 

@@ -52,6 +52,19 @@ def test_fused_run_cli(tmp_path, case):
     assert r.stdout.decode('latin-1') == report
 
 
+@pytest.mark.parametrize('case', ['small_200r', 'multi_acl'])
+def test_mapper_streamed_chunks(tmp_path, case):
+    """The mapper drop-in streams stdin in chunks of whole lines: with 4 KiB
+    chunks (hundreds of them, lines cut at every boundary, the multi_acl log
+    ending without a newline) its output is still the reference's byte for byte."""
+    text, report, sha, params, logfile = _setup(tmp_path, case)
+    env = dict(os.environ, mapred_input_dir=str(logfile.parent) + '/part-0000', LC_ALL='C', RSA_MAPPER_CHUNK='4096')
+    m = subprocess.run([sys.executable, os.path.join(ROOT, 'rsa_mapper.py')], cwd=tmp_path, env=env,
+                       input=text.encode('latin-1'), stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=600)
+    assert m.returncode == 0, m.stderr.decode()[-2000:]
+    assert hashlib.sha256(m.stdout).hexdigest() == sha
+
+
 def test_mapper_unknown_host(tmp_path):
     text, report, sha, params, logfile = _setup(tmp_path, 'small_200r')
     env = dict(os.environ, mapred_input_dir='/logs/nosuchfw/part-0000')
