@@ -5,7 +5,7 @@ intermediate mapper text or the sort (the reference's
 The output is byte-identical to what the reference pipeline prints for the
 same input (blocks in key byte order, the mapper's blank records turned into
 the reducer's "Unable to unpack" noise pairs first), with connection-table
-ties ordered by first-seen line (SURVEY.md trap 8).
+ties in CPython 2.7 dict order (SURVEY.md trap 8, ``py2dict.py``).
 """
 
 import numpy as np
@@ -78,13 +78,19 @@ def analyze_text(inputs, db, cap=1000, device=0, engine=None):
     compiled = CompiledRules(db)
     compiled.ensure_lists()
     eng = engine if engine is not None else Engine(device)
-    parts, pspell, base = [], {}, 0
+    inputs = list(inputs)
+    single = len(inputs) == 1
+    parts, pspell = [], {}
     for host, data in inputs:
-        p = textparse.parse_text(eng, host, data, db, compiled, pspell=pspell, order_base=base)
+        # one input: its order keys come with the parse; several: ranked together
+        # below, as ``cat f1 f2 | mapper | sort`` orders a key's lines across files
+        p = textparse.parse_text(eng, host, data, db, compiled, pspell=pspell, need_order=single,
+                                 keep_text=not single)
         parts.append(p)
-        base += p.n
         if p.error is not None:
             break
+    if not single:
+        textparse.order_keys_global(eng, parts)
     parsed = textparse.concat(parts, eng.torch)
     if parsed.error is not None:
         raise parsed.error[1]

@@ -190,6 +190,7 @@ class ParsedText(object):
         self.ts_table = None
         self.error = None
         self.n_host = 0               # lines the host parser decided
+        self._d_text = self._d_off = None   # device text / line offsets (parse_text keep_text=True)
 
     def batch(self):
         from .engine import DeviceBatch
@@ -205,9 +206,11 @@ def _device_bytes(torch, data, device):
     return t
 
 
-def parse_text(engine, host, data, db, compiled, pspell=None, order_base=0, need_order=True):
+def parse_text(engine, host, data, db, compiled, pspell=None, order_base=0, need_order=True, keep_text=False):
     """Parse one firewall's log bytes on the GPU.  ``pspell``: the spelling ->
-    id dict shared across calls (ids of new spellings are appended)."""
+    id dict shared across calls (ids of new spellings are appended).
+    ``keep_text``: keep the device text and line offsets on the result
+    (``_d_text``/``_d_off``) for ``order_keys_global`` over several inputs."""
     torch = engine.torch
     ctx = engine.ctx
     P = ParsedText()
@@ -293,10 +296,45 @@ def parse_text(engine, host, data, db, compiled, pspell=None, order_base=0, need
         if not data.endswith(b'\n') and n == int(nl.value):
             P.nl[-1] = False
     P.tuples, P.ts, P.order = tuples[:n], ts[:n], order[:n]
+    if keep_text:
+        P._d_text, P._d_off = text, off
     P.pspell_table = [w for w, _ in sorted(pspell.items(), key=lambda kv: kv[1])]
     if len(P.pspell_table) > 256:
         raise NotImplementedError('more than 256 protocol spellings')
     return P
+
+
+def order_keys_global(engine, parts):
+    """Order keys of all lines of several inputs ranked together: the
+    reference's ``cat f1 f2 ... | mapper | LC_ALL=C sort`` (or Hadoop's shuffle
+    sort over every split, ``runAnalysis.sh:42-56``) orders a key group's lines
+    by their bytes across all inputs, and the cap freeze follows that order
+    (``connlist-reducer.py:151``).  ``parts``: ParsedText from ``parse_text(...,
+    keep_text=True)``; each part's ``order`` is replaced by its lines' global
+    ranks (lines past a part's error are left out), the device text released."""
+    torch = engine.torch
+    live = [p for p in parts if p.n and p._d_text is not None]
+    if live:
+        dev = engine.device
+        texts, offs, shift = [], [], 0
+        for p in live:
+            texts.append(p._d_text)
+            offs.append(p._d_off[:p.n] + shift)
+            shift += p._d_text.numel()
+        offs.append(torch.tensor([shift], dtype=torch.int64, device=dev))
+        text = torch.cat(texts) if len(texts) > 1 else texts[0]
+        off = torch.cat(offs)
+        total = int(off.numel()) - 1
+        order = torch.empty(total, dtype=torch.int64, device=dev)
+        v = lambda t: ctypes.c_void_p(t.data_ptr())
+        engine.ctx.call('rsa_order_keys', v(text), v(off), ctypes.c_uint64(total), ctypes.c_uint64(0), v(order))
+        a = 0
+        for p in live:
+            p.order = order[a:a + p.n]
+            a += p.n
+        del text, off
+    for p in parts:
+        p._d_text = p._d_off = None
 
 
 def concat(parts, torch):
