@@ -5,8 +5,9 @@ row; these are that object's fields).  Written close to the reference's loops:
 
 * config parser ``:296-358`` (sections, ``edit``/``set``/``next``, subnet
   ``' '`` -> ``'/'``);
-* ``expand_addr`` ``:30-57`` (fqdn needs DNS, which fails offline: skipped as the
-  reference skips a failed lookup);
+* ``expand_addr`` ``:30-57`` (an fqdn goes to ``resolve``, the contract of
+  ``socket.gethostbyname_ex``; a failed lookup is skipped as the reference
+  skips it);
 * ``expand_service`` ``:60-140`` (``tcp-portrange`` then ``udp-portrange``;
   ``a-b`` one rule per port, ``1-65535`` NO_PORT; ``a b c``; ``dst:src`` product
   src-major; ICMP/IP port-less);
@@ -20,6 +21,7 @@ vectorised); this one appends rule by rule.
 """
 
 import re
+import socket
 from array import array
 
 import numpy as np
@@ -87,16 +89,21 @@ def parse(text):
     return obj
 
 
-def expand_addr(entry, obj):
+def expand_addr(entry, obj, resolve):
     res = []
     for match in re.finditer(r'(\".*?\")', entry):
         name = match.groups()[0]
         if name in obj['addr']:
             if 'subnet' in obj['addr'][name]:
                 res.append(obj['addr'][name]['subnet'])
+            elif 'fqdn' in obj['addr'][name]:
+                try:
+                    res = res + list(resolve(obj['addr'][name]['fqdn'].replace('"', ''))[2])
+                except Exception:  # noqa: BLE001 - a failed lookup is skipped
+                    pass
         else:
             for member in re.finditer(r'(\".*?\")', obj['addrgrp'][name]['member']):
-                res = res + expand_addr(member.groups()[0], obj)
+                res = res + expand_addr(member.groups()[0], obj, resolve)
     return res
 
 
@@ -160,7 +167,7 @@ class Acl(object):
         return len(self.action)
 
 
-def expand(text):
+def expand(text, resolve=socket.gethostbyname_ex):
     """-> (hostname, firewalls, {acl: Acl})."""
     obj = parse(text)
     acls = {}
@@ -187,9 +194,9 @@ def expand(text):
         A = acls[acl]
         srcs, dsts = [], []
         for m in re.finditer(r'(\".*?\")', p.get('srcaddr', '')):
-            srcs = srcs + expand_addr(m.groups()[0], obj)
+            srcs = srcs + expand_addr(m.groups()[0], obj, resolve)
         for m in re.finditer(r'(\".*?\")', p.get('dstaddr', '')):
-            dsts = dsts + expand_addr(m.groups()[0], obj)
+            dsts = dsts + expand_addr(m.groups()[0], obj, resolve)
         svcs = []
         for part in p['service'].split(' '):
             svcs = svcs + expand_service(part, obj)

@@ -8,8 +8,9 @@ What the reference does (and this module reproduces, rule for rule):
   stores ``' '.join(words[2:])`` for the section's known titles, ``next`` closes
   it; an address ``subnet`` has its space turned into ``/``;
 * ``expand_addr`` (``:30-57``): every quoted name is an address (its subnet;
-  an fqdn needs DNS — unavailable offline, so it is skipped exactly as the
-  reference skips a failed lookup) or an address group (members, recursively);
+  an fqdn is resolved with ``socket.gethostbyname_ex`` as the reference does —
+  a failed lookup is skipped with the reference's message) or an address group
+  (members, recursively);
 * ``expand_service`` (``:60-140``): ``TCP/UDP/SCTP`` services expand
   ``tcp-portrange`` then ``udp-portrange``; ``a-b`` expands to every port
   (``1-65535`` to NO_PORT), ``a b c`` to each port, ``dst:src`` gives the src x
@@ -28,6 +29,7 @@ handful of stepped run entries after ``compile.compress_runs``.
 """
 
 import re
+import socket
 
 import numpy as np
 
@@ -90,8 +92,10 @@ def parse_config(text):
     return obj
 
 
-def expand_addr(entry, obj, log=None):
-    """Subnet strings of every quoted address / address group name in ``entry``."""
+def expand_addr(entry, obj, log=None, resolve=socket.gethostbyname_ex):
+    """Subnet strings of every quoted address / address group name in ``entry``
+    (``resolve``: the DNS lookup of fqdn objects, ``socket.gethostbyname_ex``'s
+    contract; any exception is a failed lookup, :43-46)."""
     res = []
     for m in _QUOTED.finditer(entry):
         name = m.groups()[0]
@@ -100,13 +104,20 @@ def expand_addr(entry, obj, log=None):
             if 'subnet' in a:
                 res.append(a['subnet'])
             elif 'fqdn' in a:
-                if log is not None:   # no DNS here: the reference's failed-lookup path
-                    log('Unable to lookup {0}. Skipping it. \n'.format(a['fqdn'].replace('"', '')))
+                fqdn = a['fqdn'].replace('"', '')
+                found = None
+                try:
+                    found = resolve(fqdn)
+                except Exception:  # noqa: BLE001 - the reference's bare except (:45)
+                    if log is not None:
+                        log('Unable to lookup {0}. Skipping it. \n'.format(fqdn))
+                if found:
+                    res.extend(found[2])
             elif log is not None:
                 log('Unable to expand address "{}" to a subnet. Skipping it.\n'.format(name))
         else:
             for member in _QUOTED.finditer(obj['addrgrp'][name]['member']):
-                res.extend(expand_addr(member.groups()[0], obj, log))
+                res.extend(expand_addr(member.groups()[0], obj, log, resolve))
     return res
 
 
@@ -169,7 +180,11 @@ class _AclBuilder(object):
         return self.proto_names.index(name)
 
     def add_policy(self, p, srcs, dsts, svcs):
-        """Rules of one policy, nested src -> dst -> svc (preprosess_fortigate_acl.py:184-215)."""
+        """Rules of one policy, nested src -> dst -> svc (preprosess_fortigate_acl.py:184-215).
+        The original line and comment are built inside the innermost loop
+        there, so a policy without rules never reads its fields."""
+        if not srcs or not dsts or not svcs:
+            return
         original = 'access-list {}-in {} {} to {} service {}'.format(p['srcintf'].lower(), p['action'], p['srcaddr'],
                                                                     p['dstaddr'], p['service'])
         original = original.replace('"', '').replace('accept', 'permit')
@@ -179,8 +194,6 @@ class _AclBuilder(object):
             comment = 'access-list {}-in remark {}'.format(p['srcintf'].lower(), p['global-label'])
         comment = comment.replace('"', '')
         permit = p['action'] == 'accept'
-        if not srcs or not dsts or not svcs:
-            return
         # per service segment: protocol id and ports; a segment of k rules
         sv_proto = np.concatenate([np.full(len(sp), self.proto_id(pr), np.int64) for pr, sp, _dp in svcs])
         sv_sport = np.concatenate([sp for _pr, sp, _dp in svcs])
@@ -224,10 +237,11 @@ class _AclBuilder(object):
                            cols['comment'], self.comments or [[]], cols['rulenum'], self.rulenums or [-1])
 
 
-def build_db(text, timestamp=0.0, firewalls=None, accesslists=None, log=None):
+def build_db(text, timestamp=0.0, firewalls=None, accesslists=None, log=None, resolve=socket.gethostbyname_ex):
     """The reference's ``main`` (preprosess_fortigate_acl.py:220-434) on config
     text: returns the ``AclDB`` it would store (merged into ``firewalls`` /
-    ``accesslists`` of an existing DB when given)."""
+    ``accesslists`` of an existing DB when given).  ``log`` receives the
+    reference's stderr messages; ``resolve`` does the fqdn lookups."""
     obj = parse_config(text)
     firewalls = {} if firewalls is None else firewalls
     acldb = {} if accesslists is None else accesslists
@@ -249,13 +263,13 @@ def build_db(text, timestamp=0.0, firewalls=None, accesslists=None, log=None):
         for key in p:
             if key.find('addr') != -1:
                 for m in _QUOTED.finditer(p[key]):
-                    data[key] = data[key] + expand_addr(m.groups()[0], obj, log)
+                    data[key] = data[key] + expand_addr(m.groups()[0], obj, log, resolve)
         svcs = []
         if 'service' in p:
             for part in p['service'].split(' '):
                 svcs.extend(expand_service(part, obj, log))
-        else:
-            raise KeyError('service')    # the reference reads data['service'] unconditionally (:186)
+        elif data['srcaddr'] and data['dstaddr']:
+            raise KeyError('service')    # data['service'] is read inside the src/dst loops (:184-186)
         b.add_policy(p, data['srcaddr'], data['dstaddr'], svcs)
     hostname = obj['router']['hostname']
     firewalls.setdefault(hostname, {})
