@@ -53,6 +53,7 @@ import numpy as np
 from .acldb import AclDB
 from .ipaddr import IP
 from .py2dict import iteration_order
+from .py2text import py2_int, py2_split, py2_strip
 from .rulecols import RuleColumns
 
 __all__ = ['PORT_NAMES', 'ICMP_TYPES', 'parse_port_spec', 'parse_acl_entry', 'find_all_children', 'build_db']
@@ -83,7 +84,7 @@ NO_PORT = -1
 
 
 def _num(word, names):
-    return names[word] if word in names else int(word)
+    return names[word] if word in names else py2_int(word)
 
 
 def parse_port_spec(parts, protocol, name2num):
@@ -115,7 +116,7 @@ def parse_acl_entry(line, name2num, icmptype2num, networkgroups, servicegroups):
     """parse_cisco_fw_access_list_entry (:94-291) up to the FirewallRule
     construction: (allow, protocol, original, src list, dst list, sport list,
     dport list), False for a remark, ValueError for anything else."""
-    line = line.strip()
+    line = py2_strip(line)
     m = _RE_ACL.search(line)
     if not m:
         if line.find('remark') != -1:
@@ -123,7 +124,7 @@ def parse_acl_entry(line, name2num, icmptype2num, networkgroups, servicegroups):
         raise ValueError('Unable to parse access-list entry: ' + line)
     _name, action, protocol, rest = m.groups()
     allow = action == 'permit'
-    parts = rest.split()
+    parts = py2_split(rest)
     sourceports, destinationports = [], []
     if parts[0] == 'any':
         src, parts = [parts[0]], parts[1:]
@@ -138,7 +139,7 @@ def parse_acl_entry(line, name2num, icmptype2num, networkgroups, servicegroups):
     if parts[0] == 'object-group':
         if protocol in servicegroups and parts[1] in servicegroups[protocol]:
             for item in servicegroups[protocol][parts[1]]:
-                sourceports.append(item.split())
+                sourceports.append(py2_split(item))
     elif parts[0] in ('eq', 'neq', 'gt', 'lt'):
         sourceports.append(parts[0:2])
         parts = parts[2:]
@@ -161,7 +162,7 @@ def parse_acl_entry(line, name2num, icmptype2num, networkgroups, servicegroups):
         if parts[0] == 'object-group':
             if protocol in servicegroups and parts[1] in servicegroups[protocol]:
                 for item in servicegroups[protocol][parts[1]]:
-                    destinationports.append(item.split())
+                    destinationports.append(py2_split(item))
             parts = parts[2:]
         elif parts[0] in ('eq', 'neq', 'gt', 'lt'):
             destinationports.append(parts[0:2])
@@ -202,7 +203,7 @@ def _descendants(lines, i, ind):
     j = i + 1
     while j < len(lines):
         l = lines[j]
-        if l.strip() == '' or len(l) - len(l.lstrip(' ')) <= ind:
+        if py2_strip(l) == '' or len(l) - len(l.lstrip(' ')) <= ind:
             break
         yield j
         j += 1
@@ -296,7 +297,7 @@ def build_db(text, timestamp=0.0, firewalls=None, accesslists=None, log=None, na
     networkgroups, servicegroups, hostname = {}, {}, ''
     for line in file_lines:
         if line[:12] == 'object-group':
-            parts = line.split()
+            parts = py2_split(line)
             if len(parts) < 3:
                 continue
             if parts[1] == 'network':
@@ -304,9 +305,9 @@ def build_db(text, timestamp=0.0, firewalls=None, accesslists=None, log=None, na
             elif parts[1] == 'service':
                 servicegroups.setdefault(parts[3], {})[parts[2]] = []
         elif line[:8] == 'hostname':
-            hostname = line[9:].strip()
+            hostname = py2_strip(line[9:])
         elif line[:12] == 'access-group':
-            parts = line.split()
+            parts = py2_split(line)
             if hostname != '':
                 firewalls.setdefault(hostname, {}).setdefault(parts[4], {})[parts[2]] = parts[1]
             else:
@@ -316,14 +317,14 @@ def build_db(text, timestamp=0.0, firewalls=None, accesslists=None, log=None, na
         _exit(log, 'Config file does not contain hostname of firewall')
     for grp in networkgroups:
         for line in find_all_children(conf_lines, '^object-group network ' + grp + '$'):
-            line = line.strip()
+            line = py2_strip(line)
             if line.find('network-object') != -1:
                 address = line[15:]
                 networkgroups[grp].append(address[5:] if address[:4] == 'host' else address.replace(' ', '/'))
     for protocol in servicegroups:
         for grp in servicegroups[protocol]:
             for line in find_all_children(conf_lines, '^object-group service ' + grp + ' ' + protocol + '$'):
-                line = line.strip()
+                line = py2_strip(line)
                 if line.find('port-object') != -1:
                     obj = line[12:]
                     for p in (['tcp', 'udp'] if protocol == 'tcp-udp' else [protocol]):
@@ -338,7 +339,7 @@ def build_db(text, timestamp=0.0, firewalls=None, accesslists=None, log=None, na
     for line in file_lines:
         if line[:12] != 'access-list ':
             continue
-        parts = line.split()
+        parts = py2_split(line)
         acl = parts[1]
         if acl not in acls:
             acls[acl] = _Acl()
@@ -350,13 +351,13 @@ def build_db(text, timestamp=0.0, firewalls=None, accesslists=None, log=None, na
             raise TypeError('list indices must be integers or slices, not str')
         if parts[2] == 'remark':
             if comments_used:
-                comments, comments_used = [line.strip()], False
+                comments, comments_used = [py2_strip(line)], False
             else:
-                comments.append(line.strip())
+                comments.append(py2_strip(line))
         try:
             parsed = parse_acl_entry(line, name2num, icmptype2num, networkgroups, servicegroups)
         except ValueError:
-            _exit(log, 'Unable to parse one of the lines in the config, aborting.', 'The line is: {0}'.format(line.strip()))
+            _exit(log, 'Unable to parse one of the lines in the config, aborting.', 'The line is: {0}'.format(py2_strip(line)))
         if parsed:
             allow, protocol, original, src, dst, sport, dport = parsed
             try:

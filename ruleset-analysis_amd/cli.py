@@ -28,7 +28,8 @@ import numpy as np
 from . import acldb
 from .compile import CompiledRules, TUPLE_DTYPE, F_HIT, F_BUILT
 from .engine import DeviceBatch, Engine
-from .logparse import reducer_fields, reducer_timestamp, PY2_WS
+from .logparse import reducer_fields, reducer_timestamp
+from .py2text import PY2_WS, py2_int
 from .pipeline import analyze_text
 from .textparse import parse_text
 from .report import mapper_output, reducer_report
@@ -151,7 +152,7 @@ def reducer_main(argv=None):
         try:
             key, value = line.split('\t', 1)
             hostname, acl, ruleindex = key.split(';', 3)
-            rule = db.accesslists[hostname][acl]['rules'][int(ruleindex)]
+            rule = db.accesslists[hostname][acl]['rules'][py2_int(ruleindex)]
             rule.hostname = hostname
             rule.accesslist = acl
         except ValueError:

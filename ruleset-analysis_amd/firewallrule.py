@@ -10,6 +10,7 @@ rule to the integer predicate they evaluate.
 """
 
 from .ipaddr import IP
+from .py2text import py2_int
 
 __all__ = ['FirewallRule']
 
@@ -17,7 +18,7 @@ __all__ = ['FirewallRule']
 def _as_port_list(value, what):
     if isinstance(value, str):
         try:
-            value = [int(value)]
+            value = [py2_int(value)]
         except ValueError:
             raise ValueError('unable to convert either source or destination port to Integer')
     if not isinstance(value, list):

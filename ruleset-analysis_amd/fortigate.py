@@ -37,6 +37,7 @@ from .acldb import AclDB
 from .firewallrule import FirewallRule
 from .ipaddr import IP
 from .py2dict import iteration_order
+from .py2text import py2_int, py2_lower, py2_split, py2_strip
 from .rulecols import RuleColumns
 
 __all__ = ['parse_config', 'build_db', 'expand_addr', 'expand_service']
@@ -62,8 +63,8 @@ def parse_config(text):
     obj = {}
     section = False
     elem = False
-    for line in text.splitlines():
-        line = line.strip()
+    for line in text.split('\n'):             # readlines(): lines end at '\n' only
+        line = py2_strip(line)
         if line in SECTIONS:
             section = SECTIONS[line]
             obj[section] = {}
@@ -77,11 +78,11 @@ def parse_config(text):
                 elem = str(m.groups()[0])
                 obj[section][elem] = {}
         if section == 'router' and line[:12] == 'set hostname':
-            obj[section]['hostname'] = line.split()[2].replace("'", '').replace('"', '')
+            obj[section]['hostname'] = py2_split(line)[2].replace("'", '').replace('"', '')
         elif line == 'next':
             elem = False
         elif line[:3] == 'set' and elem:
-            words = line.split()
+            words = py2_split(line)
             title = None
             for title in TITLES[section]:
                 if words[1] == title:
@@ -126,12 +127,12 @@ def _port_values(spec):
     reference's order (range ascending, list in text order)."""
     if spec.find('-') != -1:
         start, end = spec.split('-')
-        if int(start) == 1 and int(end) == 65535:
+        if py2_int(start) == 1 and py2_int(end) == 65535:
             return np.array([FirewallRule.NO_PORT], np.int64)
-        return np.arange(int(start), int(end) + 1, dtype=np.int64)
+        return np.arange(py2_int(start), py2_int(end) + 1, dtype=np.int64)
     if spec.find(' ') != -1:
-        return np.array([int(p) for p in spec.split(' ')], np.int64)
-    return np.array([int(spec)], np.int64)
+        return np.array([py2_int(p) for p in spec.split(' ')], np.int64)
+    return np.array([py2_int(spec)], np.int64)
 
 
 def expand_service(entry, obj, log=None):
@@ -157,7 +158,7 @@ def expand_service(entry, obj, log=None):
                 else:
                     res.append((protocol, np.full(len(dst), FirewallRule.NO_PORT, np.int64), dst))
         elif o['protocol'] in ('ICMP', 'IP'):
-            res.append((o['protocol'].lower(), np.array([FirewallRule.NO_PORT], np.int64),
+            res.append((py2_lower(o['protocol']), np.array([FirewallRule.NO_PORT], np.int64),
                         np.array([FirewallRule.NO_PORT], np.int64)))
         elif log is not None:
             log('Unknown protocol {} in service object {}, skipping it.\n'.format(o['protocol'], entry))
@@ -185,13 +186,13 @@ class _AclBuilder(object):
         there, so a policy without rules never reads its fields."""
         if not srcs or not dsts or not svcs:
             return
-        original = 'access-list {}-in {} {} to {} service {}'.format(p['srcintf'].lower(), p['action'], p['srcaddr'],
+        original = 'access-list {}-in {} {} to {} service {}'.format(py2_lower(p['srcintf']), p['action'], p['srcaddr'],
                                                                     p['dstaddr'], p['service'])
         original = original.replace('"', '').replace('accept', 'permit')
         if p['comments'] != "''":
-            comment = 'access-list {}-in remark {}: {}'.format(p['srcintf'].lower(), p['global-label'], p['comments'])
+            comment = 'access-list {}-in remark {}: {}'.format(py2_lower(p['srcintf']), p['global-label'], p['comments'])
         else:
-            comment = 'access-list {}-in remark {}'.format(p['srcintf'].lower(), p['global-label'])
+            comment = 'access-list {}-in remark {}'.format(py2_lower(p['srcintf']), p['global-label'])
         comment = comment.replace('"', '')
         permit = p['action'] == 'accept'
         # per service segment: protocol id and ports; a segment of k rules

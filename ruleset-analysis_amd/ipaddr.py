@@ -12,6 +12,8 @@ host, ``addr/netmask``, object-group members), containment, length and
 
 import ipaddress
 
+from .py2text import py2_int, py2_isdigit, py2_strip
+
 __all__ = ['IP']
 
 _V4_BITS = 32
@@ -26,11 +28,11 @@ def _addr_value(text):
     """Address text without prefix -> (int value, version)."""
     if ':' in text:
         return int(ipaddress.IPv6Address(text)), 6
-    if text.isdigit():
+    if py2_isdigit(text):
         v = int(text)
         return v, (4 if v < (1 << 32) else 6)
     octets = text.split('.')
-    if len(octets) > 4 or not all(o.isdigit() and int(o) < 256 for o in octets):
+    if len(octets) > 4 or not all(py2_isdigit(o) and int(o) < 256 for o in octets):
         raise ValueError('invalid IPv4 address %r' % (text,))
     octets = octets + ['0'] * (4 - len(octets))
     value = 0
@@ -57,7 +59,7 @@ class IP(object):
             version = ipversion or (4 if 0 <= data < (1 << 32) else 6)
             self.ip, self._prefixlen, self._ipversion = data, _bits(version), version
             return
-        text = str(data).strip()
+        text = py2_strip(str(data))
         if '-' in text:
             first, last = text.split('-', 1)
             lo, version = _addr_value(first)
@@ -73,7 +75,7 @@ class IP(object):
             if '.' in pfx or ':' in pfx:
                 prefixlen = _mask_to_len(_addr_value(pfx)[0], _bits(version))
             else:
-                prefixlen = int(pfx)
+                prefixlen = py2_int(pfx)
         else:
             value, version = _addr_value(text)
             prefixlen = _bits(version)

@@ -27,18 +27,18 @@ import numpy as np
 from .compile import TUPLE_DTYPE, F_VALID, F_HIT, F_BUILT, F_SWAP
 from .firewallrule import FirewallRule
 from .ipaddr import IP
+from .py2text import PY2_WS, py2_int
 
 __all__ = ['ParsedLog', 'parse_logs', 'get_builtconn', 'BUILT', 'PY2_WS', 'reducer_fields',
            'D_IGNORE', 'D_NOACL', 'D_MISSING', 'D_CLASSIFY']
 
 D_IGNORE, D_NOACL, D_MISSING, D_CLASSIFY = 0, 1, 2, 3
-PY2_WS = ' \t\n\r\x0b\x0c'          # what Python 2's byte-string strip() removes
 
 _GB = re.compile(r'^(?P<rmon>[A-Z][a-z]{2}) +(?P<rday>\d{1,2}) (?P<rtime>\d\d:\d\d:\d\d) '
                  r'(?:(?P<mon>[A-Z][a-z]{2}) +(?P<day>\d{1,2}) (?P<year>\d{4}) (?P<time>\d\d:\d\d:\d\d): )?'
                  r'.*?%(?:ASA|FWSM|PIX)-\d-\d{6}: Built (?P<dir>inbound|outbound) (?P<proto>TCP|UDP) connection \d+ '
                  r'for (?P<if1>[A-Za-z0-9_-]+):(?P<ip1>[0-9.]+)/(?P<p1>[0-9]+) \([^)]*\) '
-                 r'to (?P<if2>[A-Za-z0-9_-]+):(?P<ip2>[0-9.]+)/(?P<p2>[0-9]+)')
+                 r'to (?P<if2>[A-Za-z0-9_-]+):(?P<ip2>[0-9.]+)/(?P<p2>[0-9]+)', re.ASCII)
 
 # connlist-reducer.py:25 (the reducer's own pattern, applied to the same line)
 BUILT = re.compile(r'[a-zA-Z]+ [0-9 ]?[0-9] ([0-9:]+) ([a-zA-Z]+) ([0-9]+) ([0-9]+) .* Built (out|in)bound '
@@ -172,7 +172,7 @@ def _parse_one(line, host, fw, acls, compiled, pspell, P, i):
         return zero, D_IGNORE, None
     proto = d['protocol'].lower()
     # Connection(...) -> FirewallRule.__init__ validation (firewallrule.py:47-93)
-    sport, dport = int(d['sport']), int(d['dport'])
+    sport, dport = py2_int(d['sport']), py2_int(d['dport'])
     src_ip = FirewallRule._address(d['src'], 'src')
     dst_ip = FirewallRule._address(d['dst'], 'dst')
     ifc = d['interface_in']

@@ -19,6 +19,7 @@ Host-side text work (the report is per rule, not per log line).
 import re
 
 from .py2dict import iteration_order
+from .py2text import py2_strip
 
 __all__ = ['hadoop_output', 'postprocess', 'SUPPORTED_PROTOCOLS']
 
@@ -82,7 +83,7 @@ def postprocess(accesslists, text):
                         nonehits = False
                 else:
                     if nonehits and current.protocol in SUPPORTED_PROTOCOLS and current.action in SUPPORTED_ACTIONS:
-                        out.extend(line.strip() for line in current.comments)
+                        out.extend(py2_strip(line) for line in current.comments)
                         out.append('{0}'.format(current.original))
                     current = rule
                     nonehits = False if hc[i] > 0 else True
