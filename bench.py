@@ -441,7 +441,7 @@ def rank_main(args, rank, world, local):
         return _cpu_model_rank(args, wl, lines, cap, rank, world, dist)
 
     from ruleset_analysis_amd import native
-    from ruleset_analysis_amd.dist import EngineBackend, merge
+    from ruleset_analysis_amd.dist import EngineBackend, ShardOverflow, merge
     from ruleset_analysis_amd.engine import Engine
     eng = Engine(local)
     eng.load_compiled(compiled, index=not args.no_index, prefix=args.prefix)
@@ -469,20 +469,25 @@ def rank_main(args, rank, world, local):
     # has 4x fewer regions and spans far fewer pages, so the slot traffic of
     # the region sort and reduction is cheaper.  A job whose
     # table overflows anyway fails with RSA_ERR_CAPACITY and is rerun at the
-    # bound (single GPU; the re-run is inside the timed step when it happens).
+    # bound (the re-run is inside the timed step when it happens; with several
+    # ranks the merge raises ShardOverflow on all of them and they rerun
+    # together, at the largest bound of any rank).
     bound = max(n_hb, 1)
+    if dist is not None:
+        tb = torch.tensor([bound], dtype=torch.int64, device=eng.device)
+        dist.all_reduce(tb, op=dist.ReduceOp.MAX)
+        bound = int(tb.item())
     sizing = {'capacity': args.capacity or bound, 'learn': not args.capacity, 'reruns': 0}
     pass1_launch_ms = []
     pass1_launches = []
     last = {}
 
     def step(timed):
-        if dist is not None:
-            return job(timed)
         n_t, n_l = len(pass1_launch_ms), len(pass1_launches)
         try:
             r = job(timed)
-        except native.NativeError as e:
+        except (native.NativeError, ShardOverflow) as e:
+            # multi-GPU: the merge raises ShardOverflow on every rank together
             if e.code != native.RSA_ERR_CAPACITY or sizing['capacity'] >= bound:
                 raise
             del pass1_launch_ms[n_t:], pass1_launches[n_l:]
@@ -495,7 +500,7 @@ def rank_main(args, rank, world, local):
         used = torch.tensor([eng.table_size()], dtype=torch.int64, device=eng.device)
         if dist is not None:
             dist.all_reduce(used, op=dist.ReduceOp.MAX)
-        sizing['capacity'] = min(bound, max(4 * int(used.item()), 1 << 20))
+        sizing['capacity'] = min(bound, max(4 * int(used.item()), args.capacity_floor))
         sizing['learn'] = False
 
     def job(timed):
@@ -840,6 +845,8 @@ def parse_args(argv=None):
     ap.add_argument('--opt', action='append', default=[], help='NAME=VALUE library option (e.g. FILTER_STEPS=3)')
     ap.add_argument('--no-index', action='store_true', help='classify with the plain linear scan')
     ap.add_argument('--capacity', type=int, default=0, help='EXPERIMENT: table capacity (default: hit+built lines)')
+    ap.add_argument('--capacity-floor', type=int, default=1 << 20,
+                    help='TESTING: smallest learned table capacity (default 2^20)')
     ap.add_argument('--prefix', type=int, default=0, help='entries per list scanned before the index')
     ap.add_argument('--text', action='store_true',
                     help='the fused job from log text in HBM (GPU parse + order keys + classify + aggregate)')

@@ -26,7 +26,7 @@ import numpy as np
 
 from .compile import RECORD_DTYPE
 
-__all__ = ['merge', 'merged_to_host', 'EngineBackend', 'route_records']
+__all__ = ['merge', 'merged_to_host', 'EngineBackend', 'route_records', 'ShardOverflow']
 
 REC = RECORD_DTYPE.itemsize
 NO_THRESHOLD = -1   # 0xFFFF_FFFF_FFFF_FFFF viewed as int64
@@ -119,8 +119,17 @@ def torch_empty_like_cpu(t):
     return torch.empty(t.shape, dtype=t.dtype)
 
 
-def route_records(buf, world, dist, group=None):
-    """all_to_all of record bytes to owner rank gid % world; returns received bytes."""
+class ShardOverflow(RuntimeError):
+    """Some rank's pass-1 table overflowed (RSA_ERR_CAPACITY): raised on every
+    rank together, so all of them can rerun the job with a larger table instead
+    of the healthy ranks waiting in the next collective."""
+    code = -4    # native.RSA_ERR_CAPACITY
+
+
+def route_records(buf, world, dist, group=None, flag=0):
+    """all_to_all of record bytes to owner rank gid % world; returns received
+    bytes.  ``flag`` (this rank's error flag) rides along with the counts: if
+    any rank sent a non-zero flag, every rank returns None instead."""
     import torch
     n = buf.numel() // REC
     rows = buf.view(-1, REC)
@@ -133,10 +142,15 @@ def route_records(buf, world, dist, group=None):
     perm = torch.argsort(okey, stable=True)
     send = rows[perm].contiguous().view(-1)
     counts = torch.bincount(owner, minlength=world).to(torch.int64)
-    recv_counts = torch.empty_like(counts)
-    _all_to_all(recv_counts, counts, dist, group)
-    sc = [int(c) * REC for c in counts.cpu().tolist()]
-    rc = [int(c) * REC for c in recv_counts.cpu().tolist()]
+    # (count, flag) per destination, one all_to_all and one host read for both
+    send_c = torch.stack([counts, torch.full_like(counts, int(flag))], 1).reshape(-1)
+    recv_c = torch.empty_like(send_c)
+    _all_to_all(recv_c, send_c, dist, group)
+    h = torch.cat([counts, recv_c]).cpu().tolist()
+    if any(h[world + 2 * r + 1] for r in range(world)):
+        return None
+    sc = [int(c) * REC for c in h[:world]]
+    rc = [int(h[world + 2 * r]) * REC for r in range(world)]
     out = torch.empty(sum(rc), dtype=torch.uint8, device=buf.device)
     _all_to_all(out, send, dist, group, rc, sc)
     return out
@@ -156,9 +170,18 @@ def merge(backend, dist, world, rank, group=None, to_host=True):
     _all_reduce(c['matches'], dist, group)
     _all_reduce(c['hits'], dist, group)
     tr('counters', dev)
-    exported = backend.export(0)
+    failed = 0
+    try:
+        exported = backend.export(0)
+    except Exception as e:  # noqa: BLE001 - a table overflow must not strand the other ranks
+        if getattr(e, 'code', None) != ShardOverflow.code:
+            raise
+        exported = torch.zeros(0, dtype=torch.uint8, device=dev)
+        failed = 1
     tr('export1', dev)
-    recv = route_records(exported, world, dist, group)
+    recv = route_records(exported, world, dist, group, flag=failed)
+    if recv is None:
+        raise ShardOverflow('distinct-connection table overflow on at least one rank')
     tr('route1', dev)
     backend.owner_reset(max(recv.numel() // REC, 1))
     backend.owner_import(recv, 0)

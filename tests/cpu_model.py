@@ -72,11 +72,29 @@ class NumpyTable(object):
         e[3] = min(e[3], order)
         return False
 
+    def local_thresh(self, n_rules, cap):
+        """Per rule the cap-th smallest min_order of this table (NO: fewer
+        than cap entries) -- the shard's own P (rsa_resolve_cap)."""
+        per = {}
+        for (gid, *_), e in self.t.items():
+            per.setdefault(gid, []).append(e[3])
+        th = np.full(n_rules, NO, np.uint64)
+        for gid, orders in per.items():
+            if cap > 0 and len(orders) >= cap:
+                th[gid] = sorted(orders)[cap - 1]
+        return th
+
     def records(self, which, thresh=None):
         rows = []
         for (gid, pspell, f, t, p), e in self.t.items():
             if which == 0:
                 rows.append((e[3], gid, f, t, p, pspell, 0, e[0], e[1], e[2], 0))
+            elif which == 3:
+                # pass1_kept (k_emit mode 3): entries that can still reach the
+                # report under the shard's own threshold
+                P = int(thresh[gid])
+                if P == NO or e[3] <= P:
+                    rows.append((e[3], gid, f, t, p, pspell, 0, e[0], e[1], e[2], 0))
             elif which == 1:
                 if e[4]:
                     rows.append((e[3], gid, f, t, p, pspell, 0, e[4], e[5], e[6], 0))
@@ -128,6 +146,14 @@ class NumpyBackend(object):
         return self.counters
 
     def export(self, which):
+        if which == 0:
+            # as EngineBackend.export(0): the shard resolves its own cap first
+            # and exports only the entries its threshold keeps (exact: a
+            # shard's P bounds the global P from above)
+            self.exported_all = len(self.local.t)
+            recs = self.local.records(3, self.local.local_thresh(self.n_rules, self.cap))
+            self.exported_kept = recs.numel() // RECORD_DTYPE.itemsize
+            return recs
         return self.local.records(which)
 
     def owner_reset(self, capacity):

@@ -31,9 +31,10 @@ def _worker(rank, world, port, payload, out_q):
     n = len(cols[0])
     cut = np.linspace(0, n, world + 1).astype(int)
     shard = tuple(c[cut[rank]:cut[rank + 1]] for c in cols)
-    out = merge(NumpyBackend(n_rules, cap, shard), dist, world, rank)
+    be = NumpyBackend(n_rules, cap, shard)
+    out = merge(be, dist, world, rank)
     if rank == 0:
-        out_q.put(out)
+        out_q.put((out, be.exported_all, be.exported_kept))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -76,7 +77,9 @@ def test_merge_world2_matches_oracle(cap):
     for p in procs:
         p.join(timeout=300)
         assert p.exitcode == 0
-    recs, matches, hits, distinct, thresh = out
+    (recs, matches, hits, distinct, thresh), n_all, n_kept = out
+    # the shard-side filter (export(0) = pass1_kept) engages when rules are capped
+    assert (n_kept < n_all) if cap == 15 else (n_kept == n_all)
     assert np.array_equal(matches, ref['matches'])
     assert np.array_equal(hits, ref['hits'])
     assert np.array_equal(thresh != NO, (ref['n_conns'] >= cap) & (cap > 0))
@@ -86,3 +89,65 @@ def test_merge_world2_matches_oracle(cap):
     want = sorted(zip(*(rows[k].astype(int).tolist() for k in ('gid', 'pspell', 'for_ip', 'to_ip', 'to_port',
                                                                   'count', 'first', 'last'))))
     assert got == want
+
+
+class _OverflowBackend(NumpyBackend):
+    """Rank 1's pass-1 table overflowed: export(0) fails with RSA_ERR_CAPACITY."""
+
+    def export(self, which):
+        if which == 0 and self.fail:
+            from ruleset_analysis_amd.native import NativeError, RSA_ERR_CAPACITY
+            raise NativeError(RSA_ERR_CAPACITY, 'distinct-connection table overflow')
+        return super().export(which)
+
+
+def _overflow_worker(rank, world, port, payload, out_q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from ruleset_analysis_amd.dist import ShardOverflow, merge
+    n_rules, cap, cols = payload
+    be = _OverflowBackend(n_rules, cap, cols)
+    be.fail = rank == 1
+    try:
+        merge(be, dist, world, rank)
+        out_q.put((rank, 'returned'))
+    except ShardOverflow as e:
+        out_q.put((rank, 'overflow %d' % e.code))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_merge_overflow_raises_on_every_rank():
+    """One rank's table overflow reaches every rank as ShardOverflow (code
+    RSA_ERR_CAPACITY) through the routing exchange, so bench.py reruns the job
+    on all ranks instead of the healthy rank waiting in a collective."""
+    dbj, info = synth.make_db(53, 100)
+    tr = synth.make_traffic((dbj, info), 2000, seed=54)
+    R = coracle.OracleRules(dbj)
+    cols, ts, order = coracle.inputs_from_traffic(R, tr)
+    gid, _ev = coracle.classify(R, cols['list'], cols['proto'], cols['src'], cols['dst'], cols['sport'],
+                                cols['dport'])
+    payload = (R.n_rules, 10, (gid, cols['flags'], cols['pspell'], cols['src'], cols['dst'], cols['sport'],
+                               cols['dport'], ts, order))
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_overflow_worker, args=(r, 2, port, payload, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {}
+    import queue
+    import time
+    deadline = time.time() + 120
+    while len(got) < 2:
+        try:
+            r, what = q.get(timeout=2)
+            got[r] = what
+        except queue.Empty:
+            if time.time() > deadline or any(p.exitcode not in (None, 0) for p in procs):
+                for p in procs:
+                    p.kill()
+                pytest.fail('overflow protocol stalled: %s' % got)
+    for p in procs:
+        p.join(timeout=60)
+    assert got == {0: 'overflow -4', 1: 'overflow -4'}
