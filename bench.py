@@ -444,7 +444,7 @@ def rank_main(args, rank, world, local):
     from ruleset_analysis_amd.dist import EngineBackend, ShardOverflow, merge
     from ruleset_analysis_amd.engine import Engine
     eng = Engine(local)
-    eng.load_compiled(compiled, index=not args.no_index, prefix=args.prefix)
+    eng.load_compiled(compiled, index=not args.no_index, prefix=args.prefix, kind=args.index)
     if args.filter_slice:
         eng.set_option(native.RSA_OPT_FILTER_SLICE, args.filter_slice)
     for kv in args.opt:
@@ -591,7 +591,7 @@ def rank_main(args, rank, world, local):
             'config': {'workload': '%s: %s (%d expanded rules, %d candidate-list entries), %d lines per GPU, cap %d'
                                    % (args.config, wl.describe, compiled.n_rules, len(ent), lines, cap),
                        'rules': compiled.n_rules, 'entries': len(ent), 'lines_per_gpu': lines, 'cap': cap,
-                       'parallelism': 'dp%d' % world,
+                       'parallelism': 'dp%d' % world, 'index': 'none' if args.no_index else args.index,
                        'backend': args.backend if dist is not None else 'none', 'records': n_rec,
                        'table_capacity': sizing['capacity'], 'capacity_bound': bound,
                        'capacity_reruns': sizing['reruns'],
@@ -663,7 +663,7 @@ def text_main(args):
     eng = Engine(0)
     ifcs, _names = textparse.interface_table(wl.db, compiled, wl.info['host'])
     spells = textparse.spell_table(list(textparse.DEFAULT_SPELLS))
-    eng.load_compiled(compiled, index=not args.no_index, prefix=args.prefix)
+    eng.load_compiled(compiled, index=not args.no_index, prefix=args.prefix, kind=args.index)
     dev = eng.device
     text = textparse._device_bytes(torch, data, dev)
     n = lines
@@ -844,6 +844,8 @@ def parse_args(argv=None):
     ap.add_argument('--filter-slice', type=int, default=0, help='override RSA_OPT_FILTER_SLICE')
     ap.add_argument('--opt', action='append', default=[], help='NAME=VALUE library option (e.g. FILTER_STEPS=3)')
     ap.add_argument('--no-index', action='store_true', help='classify with the plain linear scan')
+    ap.add_argument('--index', default='bucket', choices=('bucket', 'pht'),
+                    help='classification index: partial-key bucket index (default) or pruned perfect-hash index')
     ap.add_argument('--capacity', type=int, default=0, help='EXPERIMENT: table capacity (default: hit+built lines)')
     ap.add_argument('--capacity-floor', type=int, default=1 << 20,
                     help='TESTING: smallest learned table capacity (default 2^20)')

@@ -105,6 +105,27 @@ typedef struct rsa_rule_entry {
 #define RSA_PHT_MAGIC 0x34415352u
 #define RSA_PHT_NONE 0xFFFFFFFFu
 
+/* The partial-key bucket index (word 1 = RSA_BKT_MAGIC; ruleset-analysis_amd/
+ * bucketindex.py): the same header and list records (rsa_pht_list), where
+ * group_off / n_groups are the record's rsa_bkt_table descriptors (ascending
+ * min_gid) and mask_off / n_masks / bm_off / n_bitmaps are unused.  A table
+ * keys its entries on (src & src_mask, dst & dst_mask, ports & port_mask);
+ * its n_buckets buckets are two uint32 slots each at bucket_off (even),
+ * slot = tag8 << 24 | len8 << 16 | first16 (len 0: empty), the bucket's rows
+ * being residual rows entry_base + first .. + len - 1 (first-gid ascending).
+ * For key hash h = fmix32(ks ^ kd * 0x9E3779B1 ^ kp * 0x85EBCA77 ^ seed) the
+ * candidate buckets are ((h & 0xFFFF) * n_buckets) >> 16 and ((h >> 16) *
+ * n_buckets) >> 16, the tag ((h >> 16) ^ h) & 0xFF.  Exact: no deferred lines. */
+#define RSA_BKT_MAGIC 0x35415352u
+typedef struct rsa_bkt_table {   /* 32 B */
+  uint32_t src_mask, dst_mask, port_mask;
+  uint32_t bucket_off;           /* image word offset of the bucket slots (even)   */
+  uint32_t n_buckets;            /* 1 .. 65536                                     */
+  uint32_t seed;
+  uint32_t min_gid;              /* smallest first gid of the table's entries      */
+  uint32_t entry_base;           /* residual row of the table's first bucket row   */
+} rsa_bkt_table;
+
 typedef struct rsa_pht_table {
   uint32_t slot_off;   /* first slot word in the image                           */
   uint32_t disp_off;   /* first displacement, in uint16 units of the image       */

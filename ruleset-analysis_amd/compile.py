@@ -253,14 +253,23 @@ class CompiledRules(object):
     def n_lists(self):
         return len(self._lists)
 
-    def index(self, prefix=0, chunk=None):
-        """Perfect-hash tuple-space index of the current lists (cached until a list
-        is added); ``chunk``: entries per chained record (default PHT_CHUNK)."""
+    def index(self, prefix=0, chunk=None, kind='bucket'):
+        """Index of the current lists (cached until a list is added): ``kind``
+        'bucket' = the partial-key bucket index (bucketindex.py, image RSA5),
+        'pht' = the pruned perfect-hash tuple-space index (build_index, RSA4);
+        ``chunk``: entries per chained record (default PHT_CHUNK)."""
         ent, off = self.packed()
         chunk = chunk or PHT_CHUNK
-        if getattr(self, '_index', None) is None or self._index[0] is not self._packed or \
-                self._index[1] != (prefix, chunk):
-            self._index = (self._packed, (prefix, chunk), build_index(ent, off, prefix=prefix, chunk=chunk))
+        key = (prefix, chunk, kind)
+        if getattr(self, '_index', None) is None or self._index[0] is not self._packed or self._index[1] != key:
+            if kind == 'bucket':
+                from .bucketindex import build_bucket_index
+                built = build_bucket_index(ent, off, prefix=prefix, chunk=chunk)
+            elif kind == 'pht':
+                built = build_index(ent, off, prefix=prefix, chunk=chunk)
+            else:
+                raise ValueError('index kind must be bucket or pht')
+            self._index = (self._packed, key, built)
         return self._index[2]
 
     def ensure_lists(self, protos=('tcp', 'udp')):

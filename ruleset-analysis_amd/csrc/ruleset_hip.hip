@@ -100,6 +100,8 @@ struct Rules {
   int force_defer;              // testing: every index candidate takes the exact deferred path
   int group_tasks;              // RSA_OPT_GROUP_TASKS: candidate groups dealt out over the wave (index_lookup_wave)
   int prof;                     // RSA_OPT_PROFILE_CLASSIFY (results invalid): 1 no lookup, 2 pruning only, 4 no verification
+  int bkt;                      // the image is the partial-key bucket index (RSA_BKT_MAGIC): bucket_lookup
+  const v4u* residg;            // residual + bucket entries for per-lane (divergent) loads
 };
 
 struct Agg {
@@ -533,6 +535,74 @@ __device__ __forceinline__ uint32_t index_lookup_wave(const Rules& R, P32 img, u
   return index_verify(R, img, lw, cand0, bi, src, dst, ports);
 }
 
+// ---- partial-key bucket index (RSA_BKT_MAGIC, bucketindex.py) ---------------------
+// Per list record a few tables, each keyed on (src & sm, dst & dm, ports & pm)
+// of a template every one of its entries is exact on; a table is a bucketised
+// cuckoo hash (2 candidate buckets of 2 slots) whose slot holds tag8 << 24 |
+// len8 << 16 | first16: the bucket of entries with that key (rows entry_base
+// + first .. + len of the residual array, first-gid ascending).  A lane probes
+// every table (both buckets: independent LDS reads), checks the entries of the
+// slots whose tag matches with the full predicate; every entry containing the
+// connection is in a probed bucket, so the minimum is the linear scan's.
+constexpr uint32_t kBktTableWords = 8;
+constexpr uint32_t kBktMulD = 0x9E3779B1u, kBktMulP = 0x85EBCA77u;
+
+// must equal bucketindex.py bkt_hash / bkt_buckets
+__device__ __forceinline__ uint32_t bkt_hash(uint32_t ks, uint32_t kd, uint32_t kp, uint32_t seed) {
+  return fmix32(ks ^ (kd * kBktMulD) ^ (kp * kBktMulP) ^ seed);
+}
+
+// Entries [beg, end) of one bucket (first-gid ascending) for ONE lane: the
+// lane stops at the first entry whose first gid cannot beat its best.
+__device__ __forceinline__ uint32_t scan_bucket(const v4u* __restrict__ E, uint32_t beg, uint32_t end, uint32_t best,
+                                                uint32_t src, uint32_t dst, uint32_t ports) {
+  for (uint32_t e = beg; e < end; ++e) {
+    const v4u a = E[2 * (size_t)e], b = E[2 * (size_t)e + 1];
+    if (b.z >= best) break;
+    if (entry_match(a, b, src, dst, ports)) best = min(best, entry_gid(b, ports));
+  }
+  return best;
+}
+
+// One table (descriptor a = {src_mask, dst_mask, port_mask, bucket_off}, b =
+// {n_buckets, seed, min_gid, entry_base}): hash, both candidate buckets, the
+// slots whose tag matches.
+template <typename P32>
+__device__ __forceinline__ uint32_t bkt_table(const Rules& R, P32 img, v4u a, v4u b, uint32_t src, uint32_t dst,
+                                              uint32_t ports, uint32_t best) {
+  const uint32_t h = bkt_hash(src & a.x, dst & a.y, ports & a.z, b.y);
+  const uint32_t b1 = __umul24(h & 0xFFFFu, b.x) >> 16;   // n_buckets <= 2^16: 24-bit operands
+  const uint32_t b2 = __umul24(h >> 16, b.x) >> 16;
+  const uint32_t tag = ((h >> 16) ^ h) & 0xFFu;
+  const v2u s1 = rd2(img, a.w + 2 * b1), s2 = rd2(img, a.w + 2 * b2);
+  const uint32_t sl[4] = {s1.x, s1.y, s2.x, s2.y};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t w = sl[q];
+    const uint32_t len = (w >> 16) & 0xFFu;
+    if (len && (w >> 24) == tag) {
+      const uint32_t beg = b.w + (w & 0xFFFFu);
+      best = scan_bucket(R.residg, beg, beg + len, best, src, dst, ports);
+    }
+  }
+  return best;
+}
+
+// The tables of one list record for ONE lane (ascending min gid: stop once
+// the best beats a table's smallest gid).
+template <typename P32>
+__device__ __forceinline__ uint32_t bucket_lookup(const Rules& R, P32 img, uint32_t lw, uint32_t src, uint32_t dst,
+                                                  uint32_t ports, uint32_t best) {
+  const uint32_t toff = img[lw], nt = img[lw + 1];
+  for (uint32_t j = 0; j < nt; ++j) {
+    const uint32_t tw = toff + kBktTableWords * j;
+    const v4u a = rd4(img, tw), b = rd4(img, tw + 4);
+    if (best <= b.z) break;
+    best = bkt_table(R, img, a, b, src, dst, ports, best);
+  }
+  return best;
+}
+
 // First-match classification of one wave of tuples.  Linear scans (the whole
 // list without the index; the prefix and the residual entries with it) run as
 // a waterfall over the distinct lists present in the wave (list id broadcast
@@ -583,7 +653,16 @@ __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Ru
   while (__ballot(go)) {
     const bool ix = go && img[lw + 1] != 0;
     uint32_t c = kNoGid;
-    if (kTasks) {
+    if (R.bkt) {
+      // partial-key bucket index: exact, never deferred
+      if (ix && !(R.prof & 1)) {
+        if (R.force_defer) {
+          c = kDefer;
+        } else {
+          c = bucket_lookup(R, img, lw, t.x, t.y, t.z, best);
+        }
+      }
+    } else if (kTasks) {
       c = index_lookup_wave(R, img, lw, ix, t.x, t.y, t.z, scr);
     } else if (ix) {
       c = index_lookup(R, img, lw, t.x, t.y, t.z);
@@ -1997,6 +2076,7 @@ struct rsa_ctx {
   rsa_rule_entry* d_resid = nullptr;
   bool index_loaded = false;
   bool indexed = false;
+  bool bkt_index = false;               // the loaded image is the bucket index (RSA_BKT_MAGIC)
   bool force_defer = false;
   bool group_tasks = true;     // RSA_OPT_GROUP_TASKS
   uint32_t prof_classify = 0;  // RSA_OPT_PROFILE_CLASSIFY
@@ -2107,6 +2187,8 @@ Rules rules_of(const rsa_ctx* c) {
   r.force_defer = c->force_defer ? 1 : 0;
   r.group_tasks = c->group_tasks ? 1 : 0;
   r.prof = (int)c->prof_classify;
+  r.bkt = c->bkt_index ? 1 : 0;
+  r.residg = reinterpret_cast<const v4u*>(c->d_resid);
   return r;
 }
 
@@ -2714,8 +2796,9 @@ bool table_ok(const uint32_t* img, uint32_t words, const rsa_pht_table& t, uint3
 int rsa_load_index(rsa_ctx* c, const uint32_t* img, uint32_t words, const rsa_rule_entry* h_resid, uint32_t n_resid) {
   if (!c || !img || (n_resid && !h_resid)) return fail(c, RSA_ERR_ARG, "null argument");
   if (!c->rules_loaded) return fail(c, RSA_ERR_STATE, "load the candidate lists first");
-  if (words < 8 || img[0] != 0xFFFFFFFFu || img[1] != RSA_PHT_MAGIC)
-    return fail(c, RSA_ERR_ARG, "not an index image (word 0 must be empty, word 1 RSA_PHT_MAGIC)");
+  if (words < 8 || img[0] != 0xFFFFFFFFu || (img[1] != RSA_PHT_MAGIC && img[1] != RSA_BKT_MAGIC))
+    return fail(c, RSA_ERR_ARG, "not an index image (word 0 must be empty, word 1 RSA_PHT_MAGIC or RSA_BKT_MAGIC)");
+  const bool bkt = img[1] == RSA_BKT_MAGIC;
   if (words > (1u << 26)) return fail(c, RSA_ERR_ARG, "index image larger than 2^26 words");   // task words: gw << 6
   const uint32_t nl = c->n_lists;
   if (img[2] != nl) return fail(c, RSA_ERR_ARG, "image has %u lists, %u are loaded", img[2], nl);
@@ -2746,7 +2829,31 @@ int rsa_load_index(rsa_ctx* c, const uint32_t* img, uint32_t words, const rsa_ru
         if (e > h.resid_beg && h_resid[e].gid < h_resid[e - 1].gid)
           return fail(c, RSA_ERR_ARG, "list %u: residual not gid-ascending", l);
       }
-      if (h.n_groups != 0) {
+      if (bkt && h.n_groups != 0) {
+        // bucket index: table descriptors, bucket arrays and every slot's rows
+        const uint32_t tw = sizeof(rsa_bkt_table) / 4;
+        if (h.n_groups > 64 || h.group_off % 4 || (uint64_t)h.group_off + (uint64_t)tw * h.n_groups > words)
+          return fail(c, RSA_ERR_ARG, "list %u record %u: table descriptors outside the image", l, r);
+        uint32_t prev_min = 0;
+        for (uint32_t g = 0; g < h.n_groups; ++g) {
+          rsa_bkt_table T;
+          memcpy(&T, img + h.group_off + (size_t)tw * g, sizeof T);
+          if (T.n_buckets == 0 || T.n_buckets > 0x10000u || T.bucket_off % 2 ||
+              (uint64_t)T.bucket_off + 2ull * T.n_buckets > words)
+            return fail(c, RSA_ERR_ARG, "list %u table %u: buckets outside the image", l, g);
+          if (T.min_gid < prev_min) return fail(c, RSA_ERR_ARG, "list %u: tables not in ascending min gid", l);
+          prev_min = T.min_gid;
+          for (uint32_t s = 0; s < 2 * T.n_buckets; ++s) {
+            const uint32_t w = img[T.bucket_off + s], len = (w >> 16) & 0xFFu;
+            if (!len) continue;
+            const uint64_t beg = (uint64_t)T.entry_base + (w & 0xFFFFu);
+            if (beg + len > n_resid) return fail(c, RSA_ERR_ARG, "list %u table %u: bucket rows out of bounds", l, g);
+            for (uint64_t e = beg; e < beg + len; ++e)
+              if (h_resid[e].gid >= c->n_rules || (e > beg && h_resid[e].gid < h_resid[e - 1].gid))
+                return fail(c, RSA_ERR_ARG, "list %u table %u: bucket rows not gid-ascending or out of range", l, g);
+          }
+        }
+      } else if (h.n_groups != 0) {
         if (h.n_groups > 64) return fail(c, RSA_ERR_ARG, "list %u: more than 64 groups", l);
         if (len > 0xFFFEu) return fail(c, RSA_ERR_ARG, "list %u record %u: indexed chunk too long", l, r);
         if (h.group_off % 4 || (uint64_t)h.group_off + (uint64_t)gw * h.n_groups > words || h.mask_off % 4 ||
@@ -2795,6 +2902,7 @@ int rsa_load_index(rsa_ctx* c, const uint32_t* img, uint32_t words, const rsa_ru
   c->img_words = words;
   c->list_off = lo;
   c->index_loaded = true;
+  c->bkt_index = bkt;
   c->indexed = true;
   return RSA_OK;
 }

@@ -92,7 +92,8 @@ class Engine(object):
         self._bind(n_rules)
 
     def load_index(self, index):
-        """Upload a compile.build_index() result (image, residual entries)."""
+        """Upload an index (image, residual entries): compile.build_index() or
+        bucketindex.build_bucket_index()."""
         image, resid = (np.ascontiguousarray(a) for a in index)
         self._index_hold = (image, resid)
         v = lambda a: a.ctypes.data_as(ctypes.c_void_p)
@@ -124,14 +125,17 @@ class Engine(object):
         self.ctx.call('rsa_last_pass1_ms', ctypes.byref(ms))
         return float(ms.value)
 
-    def load_compiled(self, compiled, index=True, prefix=0, chunk=None):
-        """Upload a CompiledRules' lists (and its perfect-hash tuple-space index,
-        whose first ``prefix`` entries per list are scanned linearly and whose
+    def load_compiled(self, compiled, index=True, prefix=0, chunk=None, kind=None):
+        """Upload a CompiledRules' lists and its index (``kind``: 'bucket', the
+        default, or 'pht' -- the RSA_INDEX environment variable overrides the
+        default; the first ``prefix`` entries per list are scanned linearly,
         records hold at most ``chunk`` entries each, chained)."""
+        import os
         ent, off = compiled.packed()
         self.load_rules(ent, off, compiled.n_rules)
         if index:
-            self.load_index(compiled.index(prefix=prefix, chunk=chunk))
+            kind = kind or os.environ.get('RSA_INDEX', 'bucket')
+            self.load_index(compiled.index(prefix=prefix, chunk=chunk, kind=kind))
 
     def set_rule_count(self, n_rules):
         self.ctx.call('rsa_set_rule_count', ctypes.c_uint32(n_rules))

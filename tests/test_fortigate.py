@@ -145,7 +145,7 @@ def test_compressed_index_classifies_like_oracle(small_fg, chunk):
                                   cols['dport'])
     assert evals > 50 * len(tup)                     # long scans in the reference
     assert np.array_equal(classify_entries(ent, off, tup), ref)
-    index = comp.index(chunk=chunk)
+    index = comp.index(chunk=chunk, kind='pht')
     if chunk:
         assert int(index[0][4]) > int(index[0][2])     # chained records exist
     for i in range(0, len(tup), 3):

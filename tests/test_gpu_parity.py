@@ -47,7 +47,7 @@ def test_golden_mapper_stream(engine, case):
 
 
 def _gpu_vs_oracle(engine, n_rules, n_lines, cap, seed, zipf=None, interfaces=('outside',), batches=1,
-                   shuffle=False, index=True, broad=True, prefix=0):
+                   shuffle=False, index=True, broad=True, prefix=0, kind=None):
     dbj, info = synth.make_db(seed, n_rules, interfaces=interfaces, broad=broad)
     tr = synth.make_traffic((dbj, info), n_lines, seed=seed + 1, zipf=zipf)
     if shuffle:   # input order no longer follows the sort order
@@ -57,7 +57,7 @@ def _gpu_vs_oracle(engine, n_rules, n_lines, cap, seed, zipf=None, interfaces=('
     db = acldb.load_json(dbj)
     compiled = CompiledRules(db)
     tup, ts, order = synth.pack(tr, compiled)
-    engine.load_compiled(compiled, index=index, prefix=prefix)
+    engine.load_compiled(compiled, index=index, prefix=prefix, kind=kind)
     cuts = np.linspace(0, n_lines, batches + 1).astype(int)
     bs = [DeviceBatch.from_numpy(tup[a:b], ts[a:b], order[a:b], engine.device) for a, b in zip(cuts[:-1], cuts[1:])]
     res = engine.run(bs, cap, capacity=max(built_hit_count(tup), 1))
@@ -109,14 +109,20 @@ def test_synth_parity_linear_scan(engine):
     _gpu_vs_oracle(engine, 3000, 200000, 100, seed=18, index=False)
 
 
-def test_synth_parity_deferred_tail(engine):
-    """Every index candidate forced through the exact deferred-line kernel."""
+@pytest.mark.parametrize('kind', ['bucket', 'pht'])
+def test_synth_parity_deferred_tail(engine, kind):
+    """Every index lookup forced through the exact deferred-line kernel."""
     from ruleset_analysis_amd import native
     engine.set_option(native.RSA_OPT_FORCE_DEFER, 1)
     try:
-        _gpu_vs_oracle(engine, 2000, 300000, 50, seed=23, zipf=1.2, broad=False, prefix=0)
+        _gpu_vs_oracle(engine, 2000, 300000, 50, seed=23, zipf=1.2, broad=False, prefix=0, kind=kind)
     finally:
         engine.set_option(native.RSA_OPT_FORCE_DEFER, 0)
+
+
+def test_synth_parity_pht_index(engine):
+    """The pruned perfect-hash index (RSA4, the previous default) against the oracle."""
+    _gpu_vs_oracle(engine, 3000, 300000, 40, seed=61, zipf=1.2, broad=False, kind='pht')
 
 
 def test_synth_parity_wave_cap_scatter(engine):
@@ -130,16 +136,18 @@ def test_synth_parity_wave_cap_scatter(engine):
         engine.set_option(native.RSA_OPT_WAVE_CAP_SCATTER, 0)
 
 
+@pytest.mark.parametrize('kind', ['bucket', 'pht'])
 @pytest.mark.parametrize('broad,prefix', [(True, 64), (False, 64), (False, 0), (False, 4096)])
-def test_index_and_scan_agree_10k(engine, broad, prefix):
-    """The perfect-hash index (after a linear prefix) and the plain linear scan
-    classify identically, half of the lines unmatched (full-list scans)."""
+def test_index_and_scan_agree_10k(engine, broad, prefix, kind):
+    """Both indexes (the bucket index and the pruned perfect-hash index, after
+    a linear prefix) and the plain linear scan classify identically, half of
+    the lines unmatched (full-list scans)."""
     dbj, info = synth.make_db(19, 10000, broad=broad)
     tr = synth.make_traffic((dbj, info), 1_000_000, seed=20, p_unmatched=0.5)
     compiled = CompiledRules(acldb.load_json(dbj))
     tup, _ts, _order = synth.pack(tr, compiled)
     b = DeviceBatch.from_numpy(tup, _ts, _order, engine.device)
-    engine.load_compiled(compiled, index=True, prefix=prefix)
+    engine.load_compiled(compiled, index=True, prefix=prefix, kind=kind)
     g_idx = engine.classify_only(b).cpu().numpy()
     engine.use_index(False)
     g_scan = engine.classify_only(b).cpu().numpy()
