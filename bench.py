@@ -61,7 +61,8 @@ CONFIGS = {
                        broad=True),
     'cfg2': dict(kind='asa', rules=1000, lines=100_000_000, cap=1000, seed=2, zipf=None, ifcs=('outside',),
                  broad=False),
-    'cfg5': dict(kind='asa', rules=2500, lines=100_000_000, cap=1000, seed=5, zipf=1.1,
+    # 4 interfaces x 2.5k-rule ACLs; (src, dst, dport) Zipf s=1.1 over a population of 1e8 connections
+    'cfg5': dict(kind='asa', rules=2500, lines=100_000_000, cap=1000, seed=5, zipf=1.1, population=10 ** 8,
                  ifcs=('outside', 'partner', 'vpn', 'extranet'), broad=False),
     # FortiGate policy set (synth_fg.make_config): 160 policies, 3 with 1024-65535 ranges, >= 3M expanded rules,
     # traffic biased to late or no match (BASELINE config 4, the long-scan worst case)
@@ -77,6 +78,7 @@ class Workload(object):
         spec = dict(CONFIGS[name])
         self.name, self.kind = name, spec['kind']
         self.lines, self.seed, self.zipf = spec['lines'], spec['seed'], spec.get('zipf')
+        self.population = spec.get('population')
         self.cap = spec['cap'] if cap is None else cap
         if self.kind == 'asa':
             self.rules = rules or spec['rules']
@@ -96,6 +98,10 @@ class Workload(object):
         self.compiled.ensure_lists()
 
     def traffic(self, m, seed, t0, span, cid0):
+        if self.kind == 'asa' and self.population:
+            return synth.make_traffic_population((self.dbj, self.info), m, seed=seed, s=self.zipf,
+                                                 population=self.population, t0=t0, span=span, cid0=cid0,
+                                                 pop_seed=self.seed)
         if self.kind == 'asa':
             return synth.make_traffic((self.dbj, self.info), m, seed=seed, zipf=self.zipf, t0=t0, span=span,
                                       cid0=cid0)

@@ -588,11 +588,12 @@ __device__ __forceinline__ uint32_t bkt_table(const Rules& R, P32 img, v4u a, v4
   return best;
 }
 
-// The tables of one list record for ONE lane (ascending min gid: stop once
-// the best beats a table's smallest gid).
+// The tables of one list record for ONE lane, one after the other (ascending
+// min gid: stop once the best beats a table's smallest gid).  The general
+// form: every slot whose tag matches, in every table.
 template <typename P32>
-__device__ __forceinline__ uint32_t bucket_lookup(const Rules& R, P32 img, uint32_t lw, uint32_t src, uint32_t dst,
-                                                  uint32_t ports, uint32_t best) {
+__device__ __forceinline__ uint32_t bucket_lookup_serial(const Rules& R, P32 img, uint32_t lw, uint32_t src,
+                                                         uint32_t dst, uint32_t ports, uint32_t best) {
   const uint32_t toff = img[lw], nt = img[lw + 1];
   for (uint32_t j = 0; j < nt; ++j) {
     const uint32_t tw = toff + kBktTableWords * j;
@@ -601,6 +602,76 @@ __device__ __forceinline__ uint32_t bucket_lookup(const Rules& R, P32 img, uint3
     best = bkt_table(R, img, a, b, src, dst, ports, best);
   }
   return best;
+}
+
+#ifndef RSA_BKT_PHASED
+#define RSA_BKT_PHASED 1
+#endif
+constexpr int kBktMaxTables = 8;   // bucketindex.py MAX_TABLES
+
+// Phased form: (A) every table's probe -- LDS reads only, all independent --
+// keeping the first tag-matching slot of the first two tables with one; (B)
+// those two buckets' first entries loaded together, then the rest of the two
+// buckets.  A lane with a third hit table, or two tag-matching slots in one
+// table (a tag collision or a key over two slots), takes the serial form.
+template <typename P32>
+__device__ __forceinline__ uint32_t bucket_lookup(const Rules& R, P32 img, uint32_t lw, uint32_t src, uint32_t dst,
+                                                  uint32_t ports, uint32_t best) {
+#if !RSA_BKT_PHASED
+  return bucket_lookup_serial(R, img, lw, src, dst, ports, best);
+#else
+  const uint32_t toff = img[lw], nt = img[lw + 1];
+  uint32_t w0 = 0u, w1 = 0u, t0 = 0u, t1 = 0u;
+  bool slow = false;
+#pragma unroll
+  for (int j = 0; j < kBktMaxTables; ++j) {
+    if ((uint32_t)j < nt) {
+      const uint32_t tw = toff + kBktTableWords * j;
+      const v4u a = rd4(img, tw);
+      const v2u b = rd2(img, tw + 4);   // n_buckets, seed
+      const uint32_t h = bkt_hash(src & a.x, dst & a.y, ports & a.z, b.y);
+      const uint32_t b1 = __umul24(h & 0xFFFFu, b.x) >> 16;
+      const uint32_t b2 = __umul24(h >> 16, b.x) >> 16;
+      const uint32_t tag = ((h >> 16) ^ h) & 0xFFu;
+      const v2u s1 = rd2(img, a.w + 2 * b1), s2 = rd2(img, a.w + 2 * b2);
+      const uint32_t sl[4] = {s1.x, s1.y, s2.x, s2.y};
+      uint32_t f = 0u;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t w = sl[q];
+        const bool m = ((w >> 16) & 0xFFu) != 0u && (w >> 24) == tag && !(q >= 2 && b2 == b1);
+        slow |= m && f != 0u;
+        f = (m && f == 0u) ? w : f;
+      }
+      if (f) {
+        slow |= w1 != 0u;
+        t1 = w0 ? tw : t1;
+        w1 = w0 ? f : w1;
+        t0 = w0 ? t0 : tw;
+        w0 = w0 ? w0 : f;
+      }
+    }
+  }
+  if (slow) return bucket_lookup_serial(R, img, lw, src, dst, ports, best);
+  if (!w0) return best;
+  // (B) t0 < t1 in table order (ascending min gid)
+  const v2u m0 = rd2(img, t0 + 6);                // min_gid, entry_base
+  const v2u m1 = rd2(img, (w1 ? t1 : t0) + 6);
+  const uint32_t e0 = m0.y + (w0 & 0xFFFFu), e1 = m1.y + (w1 & 0xFFFFu);
+  const v4u a0 = R.residg[2 * (size_t)e0], c0 = R.residg[2 * (size_t)e0 + 1];
+  const v4u a1 = R.residg[2 * (size_t)e1], c1 = R.residg[2 * (size_t)e1 + 1];
+  if (best > m0.x) {
+    if (c0.z < best && entry_match(a0, c0, src, dst, ports)) best = min(best, entry_gid(c0, ports));
+    const uint32_t len0 = (w0 >> 16) & 0xFFu;
+    if (len0 > 1u) best = scan_bucket(R.residg, e0 + 1, e0 + len0, best, src, dst, ports);
+  }
+  if (w1 && best > m1.x) {
+    if (c1.z < best && entry_match(a1, c1, src, dst, ports)) best = min(best, entry_gid(c1, ports));
+    const uint32_t len1 = (w1 >> 16) & 0xFFu;
+    if (len1 > 1u) best = scan_bucket(R.residg, e1 + 1, e1 + len1, best, src, dst, ports);
+  }
+  return best;
+#endif
 }
 
 // First-match classification of one wave of tuples.  Linear scans (the whole
@@ -2832,7 +2903,8 @@ int rsa_load_index(rsa_ctx* c, const uint32_t* img, uint32_t words, const rsa_ru
       if (bkt && h.n_groups != 0) {
         // bucket index: table descriptors, bucket arrays and every slot's rows
         const uint32_t tw = sizeof(rsa_bkt_table) / 4;
-        if (h.n_groups > 64 || h.group_off % 4 || (uint64_t)h.group_off + (uint64_t)tw * h.n_groups > words)
+        if (h.n_groups > (uint32_t)kBktMaxTables || h.group_off % 4 ||
+            (uint64_t)h.group_off + (uint64_t)tw * h.n_groups > words)
           return fail(c, RSA_ERR_ARG, "list %u record %u: table descriptors outside the image", l, r);
         uint32_t prev_min = 0;
         for (uint32_t g = 0; g < h.n_groups; ++g) {

@@ -28,8 +28,8 @@ seconds.
 
 import numpy as np
 
-__all__ = ['make_db', 'make_traffic', 'render_lines', 'pack', 'order_keys', 'ts_decode', 'PSPELL', 'FORM_NAMES',
-           'COMMON_PORTS']
+__all__ = ['make_db', 'make_traffic', 'make_traffic_population', 'render_lines', 'pack', 'order_keys', 'ts_decode',
+           'PSPELL', 'FORM_NAMES', 'COMMON_PORTS']
 
 COMMON_PORTS = np.array([80, 443, 22, 25, 53, 123, 389, 445, 636, 993, 1433, 3306, 3389, 5432, 8080, 8443],
                         dtype=np.int64)
@@ -257,6 +257,107 @@ def make_traffic(db_and_info, n, seed, form_probs=(0.86, 0.04, 0.04, 0.03, 0.02,
     cid = cid0 + np.arange(n, dtype=np.int64)
     return {'src': src, 'dst': dst, 'sport': sport, 'dport': dport, 'proto': proto, 'ifc': ifc, 'form': form,
             't': t, 'cid': cid, 'interfaces': list(ifcs), 'host': info['host']}
+
+
+def _mix64(x, salt):
+    """splitmix64 finaliser of (x + salt) over uint64 arrays (per-rank streams)."""
+    with np.errstate(over='ignore'):
+        z = np.asarray(x, np.uint64) + np.uint64(salt) * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def zipf_ranks(rng, n, s, population):
+    """n ranks in [0, population) with P(rank = k) ~ (k + 1)^-s: numpy's
+    unbounded Zipf draws, those beyond the population drawn again."""
+    out = rng.zipf(s, size=n).astype(np.int64) - 1
+    bad = np.nonzero(out >= population)[0]
+    while len(bad):
+        out[bad] = rng.zipf(s, size=len(bad)).astype(np.int64) - 1
+        bad = bad[out[bad] >= population]
+    return out
+
+
+def make_traffic_population(db_and_info, n, seed, s=1.1, population=10 ** 8,
+                            form_probs=(0.86, 0.04, 0.04, 0.03, 0.02, 0.01), p_unmatched=0.10,
+                            t0=15 * 86400, span=3 * 3600, cid0=1000000, pop_seed=None):
+    """BASELINE config 5's traffic: every line's connection --
+    interface, protocol, (src, dst, dport) -- is connection number r of a
+    fixed population of ``population`` connections, r drawn Zipf(s) per line,
+    so hot connections repeat (the many-occurrences-of-one-key path of the
+    reducer dict, ``connlist-reducer.py:167-172``) while rules with a large
+    share of the population go far past the cap.  Connection r is a pure
+    function of r (splitmix64 streams): it lies inside a permit rule of the
+    ACL of its interface (one of ``p_unmatched`` of them is random noise);
+    the source port, message form and time stay per line.  Same dict layout
+    as ``make_traffic``.  ``pop_seed`` (default ``seed``) fixes the
+    population: chunks of one log drawn with different ``seed`` and the same
+    ``pop_seed`` share it."""
+    db, info = db_and_info
+    rng = np.random.default_rng(seed)
+    space = info['space']
+    ifcs = info['interfaces']
+    r = zipf_ranks(rng, n, s, population).astype(np.uint64)
+    seed = seed if pop_seed is None else pop_seed
+    u = lambda k: _mix64(r, seed * 64 + k)
+    form = rng.choice(len(form_probs), size=n, p=np.asarray(form_probs) / np.sum(form_probs))
+    if not info['with_inside']:
+        form[form == F_OUTBOUND] = F_BUILT
+    ifc = (u(0) % np.uint64(len(ifcs))).astype(np.int64)
+    src = np.zeros(n, np.int64)
+    dst = np.zeros(n, np.int64)
+    sport = rng.integers(1024, 65536, size=n)
+    dport = COMMON_PORTS[(u(1) % np.uint64(len(COMMON_PORTS))).astype(np.int64)]
+    proto = ((u(2) % np.uint64(10)) < np.uint64(3)).astype(np.int64)
+    unmatched = (u(3) % np.uint64(1000)) < np.uint64(int(p_unmatched * 1000))
+    for k, name in enumerate(ifcs):
+        meta = info['meta']['%s_access_in' % name]
+        permits = np.array([i for i, m in enumerate(meta) if m[0]], dtype=np.int64)
+        sel = np.nonzero((ifc == k) & (form != F_OUTBOUND))[0]
+        if len(sel) == 0 or len(permits) == 0:
+            continue
+        m = np.array(meta, dtype=object)
+        sn = np.array([int(x) for x in m[:, 2]], np.int64)
+        sl = np.array([int(x) for x in m[:, 3]], np.int64)
+        dn = np.array([int(x) for x in m[:, 4]], np.int64)
+        dl = np.array([int(x) for x in m[:, 5]], np.int64)
+        sp = np.array([int(x) for x in m[:, 6]], np.int64)
+        dp = np.array([int(x) for x in m[:, 7]], np.int64)
+        pr = np.array([{'tcp': 0, 'udp': 1}.get(x, -1) for x in m[:, 1]], np.int64)
+        rs = r[sel]
+        # the rule of a connection: skewed to the head of the ACL (a power law
+        # over the permit rules), so some rules collect far more distinct
+        # connections than the cap while others stay below it
+        q = (_mix64(rs, seed * 64 + 4) >> np.uint64(11)).astype(np.float64) / float(1 << 53)
+        rule = permits[np.minimum((len(permits) * q ** 3).astype(np.int64), len(permits) - 1)]
+        hs = _mix64(rs, seed * 64 + 5)
+        hd = _mix64(rs, seed * 64 + 6)
+        ssize = np.int64(1) << (32 - sl[rule])
+        s_off = (hs % np.minimum(ssize, 1 << 16).astype(np.uint64)).astype(np.int64)
+        src[sel] = np.where(sl[rule] == 0, 0x0B000000 + (hs % np.uint64(0xD4000000)).astype(np.int64), sn[rule] + s_off)
+        dsize = np.where(dl[rule] == 0, np.int64(1) << 24, np.int64(1) << (32 - dl[rule]))
+        d_off = (hd % np.minimum(dsize, 1 << 16).astype(np.uint64)).astype(np.int64)
+        dst[sel] = np.where(dl[rule] == 0, 0x0A000000 + d_off, dn[rule] + d_off)
+        has_sp = sp[rule] >= 0
+        sport[sel[has_sp]] = sp[rule][has_sp]
+        has_dp = dp[rule] >= 0
+        dport[sel[has_dp]] = dp[rule][has_dp]
+        fixed = pr[rule] >= 0
+        proto[sel[fixed]] = pr[rule][fixed]
+        un = sel[unmatched[sel]]
+        hu = _mix64(r[un], seed * 64 + 7)
+        src[un] = 0x0B000000 + (hu % np.uint64(0xD4000000)).astype(np.int64)
+        dst[un] = 0x0A000000 + ((hu >> np.uint64(32)) % np.uint64(1 << 24)).astype(np.int64)
+        dport[un] = 1 + ((hu >> np.uint64(8)) % np.uint64(65535)).astype(np.int64)
+    ob = np.nonzero(form == F_OUTBOUND)[0]
+    ho = _mix64(r[ob], seed * 64 + 8)
+    src[ob] = space.servers[(ho % np.uint64(len(space.servers))).astype(np.int64)]
+    dst[ob] = space.clients[((ho >> np.uint64(20)) % np.uint64(len(space.clients))).astype(np.int64)]
+    t = t0 + (np.arange(n, dtype=np.int64) * span) // max(n, 1)
+    cid = cid0 + np.arange(n, dtype=np.int64)
+    return {'src': src, 'dst': dst, 'sport': sport, 'dport': dport, 'proto': proto, 'ifc': ifc, 'form': form,
+            't': t, 'cid': cid, 'interfaces': list(ifcs), 'host': info['host'], 'rank': r.astype(np.int64)}
 
 
 def _clock(t):

@@ -47,9 +47,12 @@ def test_golden_mapper_stream(engine, case):
 
 
 def _gpu_vs_oracle(engine, n_rules, n_lines, cap, seed, zipf=None, interfaces=('outside',), batches=1,
-                   shuffle=False, index=True, broad=True, prefix=0, kind=None):
+                   shuffle=False, index=True, broad=True, prefix=0, kind=None, population=None):
     dbj, info = synth.make_db(seed, n_rules, interfaces=interfaces, broad=broad)
-    tr = synth.make_traffic((dbj, info), n_lines, seed=seed + 1, zipf=zipf)
+    if population:
+        tr = synth.make_traffic_population((dbj, info), n_lines, seed=seed + 1, s=zipf, population=population)
+    else:
+        tr = synth.make_traffic((dbj, info), n_lines, seed=seed + 1, zipf=zipf)
     if shuffle:   # input order no longer follows the sort order
         perm = np.random.default_rng(seed).permutation(n_lines)
         for k in ('src', 'dst', 'sport', 'dport', 'proto', 'ifc', 'form', 't', 'cid'):
@@ -276,7 +279,20 @@ def test_cfg2_shape_20m_lines(engine):
 
 def test_cfg5_shape_zipf_multi_acl_10m_lines(engine):
     """BASELINE config 5's shape: 4 interface ACLs x 2.5k rules, Zipf 1.1
-    traffic, cap 1000 engaged, 10M lines, shuffled input order."""
+    over rules, cap 1000 engaged, 10M lines, shuffled input order."""
     res, ref = _gpu_vs_oracle(engine, 2500, 10_000_000, 1000, seed=5, zipf=1.1,
                               interfaces=('outside', 'partner', 'vpn', 'extranet'), broad=False, shuffle=True)
     assert (ref['n_conns'] >= 1000).sum() > 20          # the cap is engaged on many rules
+
+
+@pytest.mark.parametrize('shuffle', [False, True])
+def test_cfg5_population_zipf_10m_lines(engine, shuffle):
+    """BASELINE config 5 as SURVEY.md 8d defines it: 4 interface ACLs x 2.5k
+    rules, every line's (src, dst, dport) drawn Zipf s=1.1 from a population
+    of 1e8 connections (hot connections repeat: the reducer's count/first/last
+    updates of one key, connlist-reducer.py:167-172), cap 1000 engaged,
+    10M lines, in time order and shuffled, against the C oracle."""
+    res, ref = _gpu_vs_oracle(engine, 2500, 10_000_000, 1000, seed=5, zipf=1.1, population=10 ** 8,
+                              interfaces=('outside', 'partner', 'vpn', 'extranet'), broad=False, shuffle=shuffle)
+    assert (ref['n_conns'] >= 1000).sum() > 20
+    assert int(ref['rows']['count'].max()) > 10000      # one connection seen many times
