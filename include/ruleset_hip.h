@@ -111,17 +111,21 @@ typedef struct rsa_rule_entry {
  * min_gid) and mask_off / n_masks / bm_off / n_bitmaps are unused.  A table
  * keys its entries on (src & src_mask, dst & dst_mask, ports & port_mask);
  * its n_buckets buckets are two uint32 slots each at bucket_off (even),
- * slot = tag8 << 24 | len8 << 16 | first16 (len 0: empty), the bucket's rows
+ * slot = tag11 << 21 | len5 << 16 | first16 (len 0: empty), the bucket's rows
  * being residual rows entry_base + first .. + len - 1 (first-gid ascending).
- * For key hash h = fmix32(ks ^ kd * 0x9E3779B1 ^ kp * 0x85EBCA77 ^ seed) the
+ * For key hash h = fmix32(ks ^ kd * 0x9E3779B1 ^ kp * 0x85EBCA77 ^ 0x2545F491) the
  * candidate buckets are ((h & 0xFFFF) * n_buckets) >> 16 and ((h >> 16) *
- * n_buckets) >> 16, the tag ((h >> 16) ^ h) & 0xFF.  Exact: no deferred lines. */
+ * n_buckets) >> 16, the tag ((h >> 16) ^ h) & 0x7FF.  Row filter words (one
+ * per bucket row at filter_off + first + i) are slen6 << 26 | dlen6 << 20 |
+ * pm2 << 18 | fp18: the low 18 bits of the same hash (seed 0x6A09E667) over
+ * the row's exact bits (src, dst under their prefix masks; sport if pm2 bit 0,
+ * dport if bit 1).  Exact: no deferred lines. */
 #define RSA_BKT_MAGIC 0x35415352u
 typedef struct rsa_bkt_table {   /* 32 B */
   uint32_t src_mask, dst_mask, port_mask;
   uint32_t bucket_off;           /* image word offset of the bucket slots (even)   */
   uint32_t n_buckets;            /* 1 .. 65536                                     */
-  uint32_t seed;
+  uint32_t filter_off;           /* image word offset of the row filters (one per bucket row) */
   uint32_t min_gid;              /* smallest first gid of the table's entries      */
   uint32_t entry_base;           /* residual row of the table's first bucket row   */
 } rsa_bkt_table;
@@ -176,7 +180,7 @@ typedef struct rsa_pht_list {    /* 80 B: one list (or one chained chunk of a li
 #define RSA_OPT_PRECHECK 9     /* pre-check monotone slot fields with a plain load before their atomics (default 1)       */
 #define RSA_OPT_WAVE_CAP_SCATTER 11 /* TESTING: cap scatter by wave grouping (the path for > 16384 capped rules) */
 #define RSA_OPT_GROUP_TASKS 12 /* index lookup: candidate groups dealt out over the wave (1, default) or per-lane loops (0) */
-#define RSA_OPT_PROFILE_CLASSIFY 13 /* PROFILING ONLY, results invalid: bit0 no index lookup, bit1 pruning only, bit2 no verification */
+#define RSA_OPT_PROFILE_CLASSIFY 13 /* PROFILING ONLY, results invalid: bit0 no index lookup, bit1 pruning only (bucket index: probes only), bit2 no verification (bucket: no serial fallback) */
 #define RSA_OPT_STATS 10       /* PROFILING: count table work into the rsa_stats counters (default 0)                 */
 
 /* One distinct (rule, connection) aggregate, 40 B (connlist-reducer.py:162-176). */

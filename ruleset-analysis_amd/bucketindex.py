@@ -10,7 +10,7 @@ is at least as long as the template's, its port is exact on every port side
 the template keys on).  Inside a table the entries are grouped into *buckets*
 by their masked key; a connection computes its key for each table, probes one
 bucketised cuckoo hash table per template (two independent 8-B bucket reads,
-two 4-B slots each: 8-bit tag, bucket length, first entry), and verifies every
+two 4-B slots each: 11-bit tag, bucket length, first entry), and verifies every
 entry of the buckets whose tag matches with the full predicate.  Every entry
 that contains the connection sits in exactly one probed bucket, so the minimum
 over the probed buckets (and the linear prefix and residual entries) is
@@ -34,8 +34,11 @@ Image layout (uint32 words; everything the GPU indexes is validated by
 0, 0, 0]``; list records (``rsa_pht_list``, 20 words: ``group_off`` = table
 descriptors, ``n_groups`` = tables, the other fields as for RSA4); table
 descriptors (8 words: src_mask, dst_mask, port_mask, bucket_off, n_buckets,
-seed, min_gid, entry_base); buckets (2 words: two slots ``tag8 << 24 | len8 <<
-16 | first16``, len 0 = empty; ``first`` relative to the table's entry_base).
+filter_off, min_gid, entry_base); buckets (2 words: two slots ``tag11 << 21 |
+len5 << 16 | first16``, len 0 = empty; ``first`` relative to the table's
+entry_base); row filters (one word per bucket row at filter_off + row:
+``row_filters``), checked in LDS before a row is loaded from the residual
+array.
 Bucket entries are rows of the residual entry array (the ``rsa_load_index``
 resid argument) after the record's linear residual rows.
 """
@@ -50,10 +53,13 @@ __all__ = ['BKT_MAGIC', 'build_bucket_index', 'bucket_lookup', 'bucket_stats', '
 BKT_MAGIC = 0x35415352                   # 'RSA5'
 BKT_TABLE_WORDS = 8
 MAX_TABLES = 8
-BKT_MAX_LEN = 0xFF                        # slot: tag8 << 24 | len8 << 16 | first16
+BKT_MAX_LEN = 31                          # slot: tag11 << 21 | len5 << 16 | first16
+TAG_BITS = 11
 LENGTHS = (0, 8, 16, 24, 32)
 PORT_CLASSES = (0x00000000, 0xFFFF0000, 0x0000FFFF, 0xFFFFFFFF)   # none, dport, sport, both
 MUL_D, MUL_P = 0x9E3779B1, 0x85EBCA77       # odd: each field's pre-mix is a bijection
+SEED_KEY, SEED_ROW = 0x2545F491, 0x6A09E667     # bucket-key hash, row-filter hash
+FP_BITS = 18
 BKT_LOAD = 0.85
 
 
@@ -68,17 +74,45 @@ def bkt_hash(ks, kd, kp, seed):
 def bkt_buckets(h, nb):
     """(b1, b2, tag) of hashes h for a table of nb <= 65536 buckets: each
     half of h picks a bucket by multiply-shift (full-rate 24-bit products on
-    the device), the tag is the xor of bytes 0 and 2 (independent of either
-    bucket's leading bits)."""
+    the device), the 11-bit tag is the xor of the low bits of both halves
+    (independent of either bucket's leading bits)."""
     h = np.asarray(h, np.uint32).astype(np.int64)
     b1 = ((h & 0xFFFF) * nb) >> 16
     b2 = ((h >> 16) * nb) >> 16
-    tag = ((h >> 16) ^ h) & 0xFF
+    tag = ((h >> 16) ^ h) & ((1 << TAG_BITS) - 1)
     return b1, b2, tag
 
 
 def _mask(length):
     return (M32 << (32 - length)) & M32 if length else 0
+
+
+def _masks(lengths):
+    ln = np.asarray(lengths, np.int64)
+    return np.where(ln > 0, (M32 << (32 - np.clip(ln, 1, 32))) & M32, 0).astype(np.uint32)
+
+
+def row_filters(rows):
+    """Per bucket row the 4-B LDS filter: slen6 << 26 | dlen6 << 20 | pm2 << 18
+    | fp18, fp = the low 18 bits of bkt_hash over the row's own exact bits
+    (src & its prefix mask, dst & its prefix mask, the exact port sides: pm2
+    bit 0 sport, bit 1 dport; range or run sides are not filtered).  A
+    connection the row contains always passes; most others do not."""
+    sl, dl, sx, dx = _entry_shape(rows)
+    pm2 = sx.astype(np.int64) | (dx.astype(np.int64) << 1)
+    pm = np.where(sx, 0xFFFF, 0) | np.where(dx, 0xFFFF0000, 0)
+    h = bkt_hash(rows['src_lo'] & _masks(sl), rows['dst_lo'] & _masks(dl),
+                 rows['port_lo'] & pm.astype(np.uint32), SEED_ROW)
+    return ((sl.astype(np.uint32) << np.uint32(26)) | (dl.astype(np.uint32) << np.uint32(20)) |
+            (pm2.astype(np.uint32) << np.uint32(18)) | (h & np.uint32((1 << FP_BITS) - 1)))
+
+
+def row_passes(f, src, dst, ports):
+    """The device's filter test of one row word f for a connection."""
+    sl, dl, pm2 = f >> 26, (f >> 20) & 63, (f >> 18) & 3
+    pm = (0xFFFF if pm2 & 1 else 0) | (0xFFFF0000 if pm2 & 2 else 0)
+    h = int(bkt_hash(np.uint32(src & _mask(sl)), np.uint32(dst & _mask(dl)), np.uint32(ports & pm), SEED_ROW))
+    return (h & ((1 << FP_BITS) - 1)) == (f & ((1 << FP_BITS) - 1))
 
 
 def _entry_shape(e):
@@ -229,20 +263,21 @@ def _record(img, rec, e, base_gid_order, pre, resid_rows):
         resid_rows.append(rows)
         base = pos
         pos += len(rows)
-        seed = 0x2545F491
+        seed = SEED_KEY
         rng = np.random.default_rng(len(tabs) + 7)
         h = bkt_hash(uk[:, 0], uk[:, 1], uk[:, 2], seed)
         nb, where = _cuckoo(h, rng)
         _b1, _b2, tag = bkt_buckets(h, nb)
         words = np.zeros(2 * nb, np.uint32)                         # bucket b = slots 2b, 2b + 1
-        words[where] = (tag.astype(np.uint32) << np.uint32(24)) | (counts.astype(np.uint32) << np.uint32(16)) | \
+        words[where] = (tag.astype(np.uint32) << np.uint32(21)) | (counts.astype(np.uint32) << np.uint32(16)) | \
             firsts.astype(np.uint32)
         boff, _ = img.alloc(words, align=2)
-        tabs.append((int(e['gid'][w].min()), _mask(ls), _mask(ld), pm, boff, nb, seed, base))
+        foff, _ = img.alloc(row_filters(rows))
+        tabs.append((int(e['gid'][w].min()), _mask(ls), _mask(ld), pm, boff, nb, foff, base))
     tabs.sort()
     toff, trec = img.alloc(np.zeros(BKT_TABLE_WORDS * len(tabs), np.uint32), align=4)
-    for j, (mg, sm, dm, pm, boff, nb, seed, base) in enumerate(tabs):
-        trec[BKT_TABLE_WORDS * j: BKT_TABLE_WORDS * (j + 1)] = (sm, dm, pm, boff, nb, seed, mg, base)
+    for j, (mg, sm, dm, pm, boff, nb, foff, base) in enumerate(tabs):
+        trec[BKT_TABLE_WORDS * j: BKT_TABLE_WORDS * (j + 1)] = (sm, dm, pm, boff, nb, foff, mg, base)
     rec[0], rec[1] = toff, len(tabs)
     return r_beg, r_end
 
@@ -309,7 +344,7 @@ def bucket_stats(index):
         for j in range(r[1]):
             t = image[r[0] + BKT_TABLE_WORDS * j: r[0] + BKT_TABLE_WORDS * (j + 1)]
             w = image[int(t[3]): int(t[3]) + 2 * int(t[4])]
-            nb += int(((w >> np.uint32(16)) & np.uint32(0xFF)).sum())
+            nb += int(((w >> np.uint32(16)) & np.uint32(0x1F)).sum())
         out.append((r[6], r[1], r[5] - r[4], nb))
     return out
 
@@ -328,17 +363,26 @@ def bucket_lookup(index, ent, off, L, src, dst, ports):
     while True:
         for j in range(r[1]):
             t = [int(v) for v in image[r[0] + BKT_TABLE_WORDS * j: r[0] + BKT_TABLE_WORDS * (j + 1)]]
-            sm, dm, pm, boff, nb, seed, mg, base = t
+            sm, dm, pm, boff, nb, foff, mg, base = t
             if best is not None and best <= mg:
                 break
-            h = bkt_hash(src & sm, dst & dm, ports & pm, seed)
+            h = bkt_hash(src & sm, dst & dm, ports & pm, SEED_KEY)
             b1, b2, tag = (int(x) for x in bkt_buckets(h, nb))
             for s in (2 * b1, 2 * b1 + 1, 2 * b2, 2 * b2 + 1):       # b2 == b1: the same slots twice
                 w = int(image[boff + s])
-                ln = (w >> 16) & 0xFF
-                if ln and (w >> 24) == tag:
-                    a = base + (w & 0xFFFF)
-                    best = _scan(resid[a:a + ln], src, dst, ports, best)
+                ln = (w >> 16) & 0x1F
+                if ln and (w >> 21) == tag:
+                    # the first row of the bucket that passes its filter is the
+                    # bucket's candidate (rows ascend in first gid)
+                    for k in range(w & 0xFFFF, (w & 0xFFFF) + ln):
+                        x = resid[base + k]
+                        if best is not None and int(x['gid']) >= best:
+                            break
+                        if row_passes(int(image[foff + k]), src, dst, ports) and \
+                                _scan(resid[base + k:base + k + 1], src, dst, ports, None) is not None:
+                            g = entry_gid(x, ports & 0xFFFF, ports >> 16)
+                            best = g if best is None else min(best, g)
+                            break
         best = _scan(resid[r[4]:r[5]], src, dst, ports, best)
         if r[16] == PHT_EMPTY or (best is not None and best <= r[17]):
             break

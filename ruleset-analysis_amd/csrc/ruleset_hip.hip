@@ -538,14 +538,28 @@ __device__ __forceinline__ uint32_t index_lookup_wave(const Rules& R, P32 img, u
 // ---- partial-key bucket index (RSA_BKT_MAGIC, bucketindex.py) ---------------------
 // Per list record a few tables, each keyed on (src & sm, dst & dm, ports & pm)
 // of a template every one of its entries is exact on; a table is a bucketised
-// cuckoo hash (2 candidate buckets of 2 slots) whose slot holds tag8 << 24 |
-// len8 << 16 | first16: the bucket of entries with that key (rows entry_base
-// + first .. + len of the residual array, first-gid ascending).  A lane probes
+// cuckoo hash (2 candidate buckets of 2 slots) whose slot locates the
+// bucket of entries with that key (rows entry_base
+// + first .. + len of the residual array, first-gid ascending; the slot is
+// tag11 << 21 | len5 << 16 | first16).  A lane probes
 // every table (both buckets: independent LDS reads), checks the entries of the
 // slots whose tag matches with the full predicate; every entry containing the
 // connection is in a probed bucket, so the minimum is the linear scan's.
 constexpr uint32_t kBktTableWords = 8;
+constexpr uint32_t kBktTagMask = 0x7FFu, kBktLenMask = 0x1Fu;   // slot = tag11 << 21 | len5 << 16 | first16
 constexpr uint32_t kBktMulD = 0x9E3779B1u, kBktMulP = 0x85EBCA77u;
+constexpr uint32_t kBktSeedKey = 0x2545F491u, kBktSeedRow = 0x6A09E667u, kBktFpMask = 0x3FFFFu;   // bucketindex.py
+
+// Row filter (bucketindex.py row_filters): f = slen6 << 26 | dlen6 << 20 |
+// pm2 << 18 | fp18 over the row's own exact bits; a row that contains the
+// connection always passes.
+__device__ __forceinline__ uint32_t len_mask(uint32_t l) { return l ? 0xFFFFFFFFu << (32u - l) : 0u; }
+__device__ __forceinline__ bool row_passes(uint32_t f, uint32_t src, uint32_t dst, uint32_t ports) {
+  const uint32_t pm = ((f >> 18) & 1u ? 0x0000FFFFu : 0u) | ((f >> 19) & 1u ? 0xFFFF0000u : 0u);
+  const uint32_t h = fmix32((src & len_mask(f >> 26)) ^ ((dst & len_mask((f >> 20) & 63u)) * kBktMulD) ^
+                            ((ports & pm) * kBktMulP) ^ kBktSeedRow);
+  return ((h ^ f) & kBktFpMask) == 0u;
+}
 
 // must equal bucketindex.py bkt_hash / bkt_buckets
 __device__ __forceinline__ uint32_t bkt_hash(uint32_t ks, uint32_t kd, uint32_t kp, uint32_t seed) {
@@ -565,22 +579,22 @@ __device__ __forceinline__ uint32_t scan_bucket(const v4u* __restrict__ E, uint3
 }
 
 // One table (descriptor a = {src_mask, dst_mask, port_mask, bucket_off}, b =
-// {n_buckets, seed, min_gid, entry_base}): hash, both candidate buckets, the
-// slots whose tag matches.
+// {n_buckets, filter_off, min_gid, entry_base}): hash, both candidate
+// buckets, every row of the slots whose tag matches (no row filters).
 template <typename P32>
 __device__ __forceinline__ uint32_t bkt_table(const Rules& R, P32 img, v4u a, v4u b, uint32_t src, uint32_t dst,
                                               uint32_t ports, uint32_t best) {
-  const uint32_t h = bkt_hash(src & a.x, dst & a.y, ports & a.z, b.y);
+  const uint32_t h = bkt_hash(src & a.x, dst & a.y, ports & a.z, kBktSeedKey);
   const uint32_t b1 = __umul24(h & 0xFFFFu, b.x) >> 16;   // n_buckets <= 2^16: 24-bit operands
   const uint32_t b2 = __umul24(h >> 16, b.x) >> 16;
-  const uint32_t tag = ((h >> 16) ^ h) & 0xFFu;
+  const uint32_t tag = ((h >> 16) ^ h) & kBktTagMask;
   const v2u s1 = rd2(img, a.w + 2 * b1), s2 = rd2(img, a.w + 2 * b2);
   const uint32_t sl[4] = {s1.x, s1.y, s2.x, s2.y};
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const uint32_t w = sl[q];
-    const uint32_t len = (w >> 16) & 0xFFu;
-    if (len && (w >> 24) == tag) {
+    const uint32_t len = (w >> 16) & kBktLenMask;
+    if (len && (w >> 21) == tag && !(q >= 2 && b2 == b1)) {
       const uint32_t beg = b.w + (w & 0xFFFFu);
       best = scan_bucket(R.residg, beg, beg + len, best, src, dst, ports);
     }
@@ -609,11 +623,16 @@ __device__ __forceinline__ uint32_t bucket_lookup_serial(const Rules& R, P32 img
 #endif
 constexpr int kBktMaxTables = 8;   // bucketindex.py MAX_TABLES
 
+
 // Phased form: (A) every table's probe -- LDS reads only, all independent --
-// keeping the first tag-matching slot of the first two tables with one; (B)
-// those two buckets' first entries loaded together, then the rest of the two
-// buckets.  A lane with a third hit table, or two tag-matching slots in one
-// table (a tag collision or a key over two slots), takes the serial form.
+// keeping the tag-matching slots of the (at most four) tables with one; (B)
+// per hit bucket the first row whose LDS filter the connection passes (LDS
+// only); (C) the (at most two) candidate rows loaded together and checked in
+// full; a candidate that fails (an 18-bit filter collision, or a side the
+// filter cannot check: port ranges, runs) continues its bucket's scan.  A
+// lane with more hit tables or candidates, or two tag-matching slots in one
+// table (an 11-bit tag collision), takes the serial form.  Typically one
+// global load per matched line, none for an unmatched one.
 template <typename P32>
 __device__ __forceinline__ uint32_t bucket_lookup(const Rules& R, P32 img, uint32_t lw, uint32_t src, uint32_t dst,
                                                   uint32_t ports, uint32_t best) {
@@ -621,54 +640,81 @@ __device__ __forceinline__ uint32_t bucket_lookup(const Rules& R, P32 img, uint3
   return bucket_lookup_serial(R, img, lw, src, dst, ports, best);
 #else
   const uint32_t toff = img[lw], nt = img[lw + 1];
-  uint32_t w0 = 0u, w1 = 0u, t0 = 0u, t1 = 0u;
+  uint32_t h0 = 0u, h1 = 0u, h2 = 0u, h3 = 0u;   // hit slot words, in table order
+  uint32_t tj = 0u;                              // their tables, 4 bits each (hit k at bits 4k)
+  uint32_t nh = 0u;
   bool slow = false;
 #pragma unroll
   for (int j = 0; j < kBktMaxTables; ++j) {
     if ((uint32_t)j < nt) {
       const uint32_t tw = toff + kBktTableWords * j;
       const v4u a = rd4(img, tw);
-      const v2u b = rd2(img, tw + 4);   // n_buckets, seed
-      const uint32_t h = bkt_hash(src & a.x, dst & a.y, ports & a.z, b.y);
-      const uint32_t b1 = __umul24(h & 0xFFFFu, b.x) >> 16;
-      const uint32_t b2 = __umul24(h >> 16, b.x) >> 16;
-      const uint32_t tag = ((h >> 16) ^ h) & 0xFFu;
+      const uint32_t nb = img[tw + 4];
+      const uint32_t h = bkt_hash(src & a.x, dst & a.y, ports & a.z, kBktSeedKey);
+      const uint32_t b1 = __umul24(h & 0xFFFFu, nb) >> 16;
+      const uint32_t b2 = __umul24(h >> 16, nb) >> 16;
+      const uint32_t tag = ((h >> 16) ^ h) & kBktTagMask;
       const v2u s1 = rd2(img, a.w + 2 * b1), s2 = rd2(img, a.w + 2 * b2);
       const uint32_t sl[4] = {s1.x, s1.y, s2.x, s2.y};
       uint32_t f = 0u;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const uint32_t w = sl[q];
-        const bool m = ((w >> 16) & 0xFFu) != 0u && (w >> 24) == tag && !(q >= 2 && b2 == b1);
+        const bool m = ((w >> 16) & kBktLenMask) != 0u && (w >> 21) == tag && !(q >= 2 && b2 == b1);
         slow |= m && f != 0u;
         f = (m && f == 0u) ? w : f;
       }
       if (f) {
-        slow |= w1 != 0u;
-        t1 = w0 ? tw : t1;
-        w1 = w0 ? f : w1;
-        t0 = w0 ? t0 : tw;
-        w0 = w0 ? w0 : f;
+        h0 = nh == 0u ? f : h0;
+        h1 = nh == 1u ? f : h1;
+        h2 = nh == 2u ? f : h2;
+        h3 = nh == 3u ? f : h3;
+        tj |= (uint32_t)j << (4 * (nh & 7u));
+        ++nh;
       }
     }
   }
-  if (slow) return bucket_lookup_serial(R, img, lw, src, dst, ports, best);
-  if (!w0) return best;
-  // (B) t0 < t1 in table order (ascending min gid)
-  const v2u m0 = rd2(img, t0 + 6);                // min_gid, entry_base
-  const v2u m1 = rd2(img, (w1 ? t1 : t0) + 6);
-  const uint32_t e0 = m0.y + (w0 & 0xFFFFu), e1 = m1.y + (w1 & 0xFFFFu);
-  const v4u a0 = R.residg[2 * (size_t)e0], c0 = R.residg[2 * (size_t)e0 + 1];
-  const v4u a1 = R.residg[2 * (size_t)e1], c1 = R.residg[2 * (size_t)e1 + 1];
-  if (best > m0.x) {
-    if (c0.z < best && entry_match(a0, c0, src, dst, ports)) best = min(best, entry_gid(c0, ports));
-    const uint32_t len0 = (w0 >> 16) & 0xFFu;
-    if (len0 > 1u) best = scan_bucket(R.residg, e0 + 1, e0 + len0, best, src, dst, ports);
+  if (R.prof & 2) return best ^ (nh & 0x80000000u);             // PROFILING: probes only (results invalid)
+  if ((slow || nh > 4u) && !(R.prof & 4)) return bucket_lookup_serial(R, img, lw, src, dst, ports, best);
+  if (nh > 4u) nh = 4u;                                          // (only under R.prof & 4)
+  // (B) candidate rows: absolute residual row and the rows left in its bucket
+  uint32_t r0 = 0u, n0 = 0u, r1 = 0u, n1 = 0u, nc = 0u;
+  for (uint32_t k = 0; k < nh; ++k) {
+    const uint32_t w = k == 0u ? h0 : k == 1u ? h1 : k == 2u ? h2 : h3;
+    const uint32_t j = (tj >> (4 * k)) & 0xFu;
+    const v4u d = rd4(img, toff + kBktTableWords * j + 4);     // n_buckets, filter_off, min_gid, entry_base
+    if (best <= d.z) break;                                    // tables ascend in min gid
+    const uint32_t first = w & 0xFFFFu, end = first + ((w >> 16) & kBktLenMask);
+    for (uint32_t r = first; r < end; ++r) {
+      if (row_passes(img[d.y + r], src, dst, ports)) {
+        r1 = nc == 1u ? d.w + r : r1;
+        n1 = nc == 1u ? end - r - 1u : n1;
+        r0 = nc == 0u ? d.w + r : r0;
+        n0 = nc == 0u ? end - r - 1u : n0;
+        ++nc;
+        break;
+      }
+    }
   }
-  if (w1 && best > m1.x) {
-    if (c1.z < best && entry_match(a1, c1, src, dst, ports)) best = min(best, entry_gid(c1, ports));
-    const uint32_t len1 = (w1 >> 16) & 0xFFu;
-    if (len1 > 1u) best = scan_bucket(R.residg, e1 + 1, e1 + len1, best, src, dst, ports);
+  if (nc > 2u) return bucket_lookup_serial(R, img, lw, src, dst, ports, best);
+  if (nc == 0u) return best;
+  // (C) the candidates' rows, both loads in flight
+  const uint32_t rb = nc > 1u ? r1 : r0;
+  const v4u a0 = R.residg[2 * (size_t)r0], c0 = R.residg[2 * (size_t)r0 + 1];
+  const v4u a1 = R.residg[2 * (size_t)rb], c1 = R.residg[2 * (size_t)rb + 1];
+  if (c0.z < best) {
+    if (entry_match(a0, c0, src, dst, ports)) {
+      best = min(best, entry_gid(c0, ports));
+    } else if (n0) {
+      best = scan_bucket(R.residg, r0 + 1u, r0 + 1u + n0, best, src, dst, ports);
+    }
+  }
+  if (nc > 1u && c1.z < best) {
+    if (entry_match(a1, c1, src, dst, ports)) {
+      best = min(best, entry_gid(c1, ports));
+    } else if (n1) {
+      best = scan_bucket(R.residg, r1 + 1u, r1 + 1u + n1, best, src, dst, ports);
+    }
   }
   return best;
 #endif
@@ -2916,10 +2962,12 @@ int rsa_load_index(rsa_ctx* c, const uint32_t* img, uint32_t words, const rsa_ru
           if (T.min_gid < prev_min) return fail(c, RSA_ERR_ARG, "list %u: tables not in ascending min gid", l);
           prev_min = T.min_gid;
           for (uint32_t s = 0; s < 2 * T.n_buckets; ++s) {
-            const uint32_t w = img[T.bucket_off + s], len = (w >> 16) & 0xFFu;
+            const uint32_t w = img[T.bucket_off + s], len = (w >> 16) & 0x1Fu;
             if (!len) continue;
             const uint64_t beg = (uint64_t)T.entry_base + (w & 0xFFFFu);
             if (beg + len > n_resid) return fail(c, RSA_ERR_ARG, "list %u table %u: bucket rows out of bounds", l, g);
+            if ((uint64_t)T.filter_off + (w & 0xFFFFu) + len > words)
+              return fail(c, RSA_ERR_ARG, "list %u table %u: row filters outside the image", l, g);
             for (uint64_t e = beg; e < beg + len; ++e)
               if (h_resid[e].gid >= c->n_rules || (e > beg && h_resid[e].gid < h_resid[e - 1].gid))
                 return fail(c, RSA_ERR_ARG, "list %u table %u: bucket rows not gid-ascending or out of range", l, g);
