@@ -597,7 +597,7 @@ def rank_main(args, rank, world, local):
             'config': {'workload': '%s: %s (%d expanded rules, %d candidate-list entries), %d lines per GPU, cap %d'
                                    % (args.config, wl.describe, compiled.n_rules, len(ent), lines, cap),
                        'rules': compiled.n_rules, 'entries': len(ent), 'lines_per_gpu': lines, 'cap': cap,
-                       'parallelism': 'dp%d' % world, 'index': 'none' if args.no_index else args.index,
+                       'parallelism': 'dp%d' % world, 'index': 'none' if args.no_index else getattr(eng, 'index_kind', args.index),
                        'backend': args.backend if dist is not None else 'none', 'records': n_rec,
                        'table_capacity': sizing['capacity'], 'capacity_bound': bound,
                        'capacity_reruns': sizing['reruns'],
@@ -850,8 +850,9 @@ def parse_args(argv=None):
     ap.add_argument('--filter-slice', type=int, default=0, help='override RSA_OPT_FILTER_SLICE')
     ap.add_argument('--opt', action='append', default=[], help='NAME=VALUE library option (e.g. FILTER_STEPS=3)')
     ap.add_argument('--no-index', action='store_true', help='classify with the plain linear scan')
-    ap.add_argument('--index', default='bucket', choices=('bucket', 'pht'),
-                    help='classification index: partial-key bucket index (default) or pruned perfect-hash index')
+    ap.add_argument('--index', default='auto', choices=('auto', 'pht', 'bucket', 'bucket-filtered'),
+                    help='classification index: auto (default: pht while its image fits LDS, else bucket), the '
+                         'pruned perfect-hash index or the partial-key bucket index (without / with LDS row filters)')
     ap.add_argument('--capacity', type=int, default=0, help='EXPERIMENT: table capacity (default: hit+built lines)')
     ap.add_argument('--capacity-floor', type=int, default=1 << 20,
                     help='TESTING: smallest learned table capacity (default 2^20)')

@@ -236,7 +236,7 @@ def _cuckoo(h, seed_rng, load=BKT_LOAD, kicks=1000):
         nb = nb + nb // 8 + 1
 
 
-def _record(img, rec, e, base_gid_order, pre, resid_rows):
+def _record(img, rec, e, base_gid_order, pre, resid_rows, filters=False):
     """Tables of one list record over entries e (record-local indices; [0, pre)
     is the linear prefix).  Appends residual rows then bucket rows to
     resid_rows (list of RULE_DTYPE arrays); returns (resid_beg, resid_end) of
@@ -272,7 +272,7 @@ def _record(img, rec, e, base_gid_order, pre, resid_rows):
         words[where] = (tag.astype(np.uint32) << np.uint32(21)) | (counts.astype(np.uint32) << np.uint32(16)) | \
             firsts.astype(np.uint32)
         boff, _ = img.alloc(words, align=2)
-        foff, _ = img.alloc(row_filters(rows))
+        foff = img.alloc(row_filters(rows))[0] if filters else 0
         tabs.append((int(e['gid'][w].min()), _mask(ls), _mask(ld), pm, boff, nb, foff, base))
     tabs.sort()
     toff, trec = img.alloc(np.zeros(BKT_TABLE_WORDS * len(tabs), np.uint32), align=4)
@@ -282,11 +282,12 @@ def _record(img, rec, e, base_gid_order, pre, resid_rows):
     return r_beg, r_end
 
 
-def build_bucket_index(ent, off, prefix=0, chunk=PHT_CHUNK, min_entries=32):
+def build_bucket_index(ent, off, prefix=0, chunk=PHT_CHUNK, min_entries=32, filters=False):
     """Bucket index over packed lists: (image uint32[], resid RULE_DTYPE[]),
     the rsa_load_index arguments.  Lists longer than ``chunk`` entries are
     chains of records as in the RSA4 index; a record with fewer than
-    ``min_entries`` entries after its prefix is all residual."""
+    ``min_entries`` entries after its prefix is all residual.  ``filters``:
+    LDS row filters (image word 5 bit 0; table filter_off)."""
     n_lists = len(off) - 1
     spans = []
     for L in range(n_lists):
@@ -299,6 +300,7 @@ def build_bucket_index(ent, off, prefix=0, chunk=PHT_CHUNK, min_entries=32):
     img.chunks[0][2] = n_lists
     img.chunks[0][3] = list_off
     img.chunks[0][4] = n_records
+    img.chunks[0][5] = 1 if filters else 0
     resid_rows = []
     next_virtual = n_lists
     for L in range(n_lists):
@@ -324,7 +326,7 @@ def build_bucket_index(ent, off, prefix=0, chunk=PHT_CHUNK, min_entries=32):
                 rec[16] = PHT_EMPTY
                 rec[17] = PHT_EMPTY
             if len(e) - p >= min_entries:
-                rb, re_ = _record(img, rec, e, None, p, resid_rows)
+                rb, re_ = _record(img, rec, e, None, p, resid_rows, filters)
             else:
                 n0 = sum(len(x) for x in resid_rows)
                 resid_rows.append(e[p:])
@@ -371,7 +373,10 @@ def bucket_lookup(index, ent, off, L, src, dst, ports):
             for s in (2 * b1, 2 * b1 + 1, 2 * b2, 2 * b2 + 1):       # b2 == b1: the same slots twice
                 w = int(image[boff + s])
                 ln = (w >> 16) & 0x1F
-                if ln and (w >> 21) == tag:
+                if ln and (w >> 21) == tag and not int(image[5]) & 1:
+                    a = base + (w & 0xFFFF)
+                    best = _scan(resid[a:a + ln], src, dst, ports, best)
+                elif ln and (w >> 21) == tag:
                     # the first row of the bucket that passes its filter is the
                     # bucket's candidate (rows ascend in first gid)
                     for k in range(w & 0xFFFF, (w & 0xFFFF) + ln):

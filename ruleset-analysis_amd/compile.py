@@ -253,18 +253,28 @@ class CompiledRules(object):
     def n_lists(self):
         return len(self._lists)
 
-    def index(self, prefix=0, chunk=None, kind='bucket'):
+    def index(self, prefix=0, chunk=None, kind='auto'):
         """Index of the current lists (cached until a list is added): ``kind``
-        'bucket' = the partial-key bucket index (bucketindex.py, image RSA5),
-        'pht' = the pruned perfect-hash tuple-space index (build_index, RSA4);
+        'pht' = the pruned perfect-hash tuple-space index (build_index, RSA4),
+        'bucket' / 'bucket-filtered' = the partial-key bucket index
+        (bucketindex.py, image RSA5) without / with LDS row filters, 'auto'
+        (default) = pht while its image fits the LDS of two classifier
+        workgroups per CU (AUTO_PHT_MAX_WORDS), else bucket -- from global
+        memory the bucket index's fewer dependent reads win (cfg4: 0.96 vs 4.48
+        ms per classification launch; at 10k rules in LDS pht 0.90 vs 1.06);
         ``chunk``: entries per chained record (default PHT_CHUNK)."""
         ent, off = self.packed()
         chunk = chunk or PHT_CHUNK
+        if kind == 'auto':
+            pht = self.index(prefix, chunk, 'pht')
+            if len(pht[0]) <= AUTO_PHT_MAX_WORDS:
+                return pht
+            kind = 'bucket'
         key = (prefix, chunk, kind)
         if getattr(self, '_index', None) is None or self._index[0] is not self._packed or self._index[1] != key:
-            if kind == 'bucket':
+            if kind in ('bucket', 'bucket-filtered'):
                 from .bucketindex import build_bucket_index
-                built = build_bucket_index(ent, off, prefix=prefix, chunk=chunk)
+                built = build_bucket_index(ent, off, prefix=prefix, chunk=chunk, filters=kind == 'bucket-filtered')
             elif kind == 'pht':
                 built = build_index(ent, off, prefix=prefix, chunk=chunk)
             else:
@@ -318,6 +328,7 @@ class CompiledRules(object):
 #   list records (PHT_LIST_WORDS each), group records, mask records, bitmaps
 #   (uint64, lo word first), CHD displacements (uint16) and slot words.
 PHT_MAGIC = 0x34415352              # 'RSA4'
+AUTO_PHT_MAX_WORDS = 19456          # csrc kImgSmallMax: the image of two 1024-thread classifier workgroups per CU
 PHT_LIST_WORDS, PHT_GROUP_WORDS, PHT_MASK_WORDS = 20, 20, 4
 PHT_HEADER_WORDS = 8
 PHT_CHUNK = 0xF000                  # entries per chained record: a table never needs > 2^16 slots

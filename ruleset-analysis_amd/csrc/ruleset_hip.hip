@@ -101,6 +101,7 @@ struct Rules {
   int group_tasks;              // RSA_OPT_GROUP_TASKS: candidate groups dealt out over the wave (index_lookup_wave)
   int prof;                     // RSA_OPT_PROFILE_CLASSIFY (results invalid): 1 no lookup, 2 pruning only, 4 no verification
   int bkt;                      // the image is the partial-key bucket index (RSA_BKT_MAGIC): bucket_lookup
+  int bkt_filters;              // ... with LDS row filters (image word 5 bit 0)
   const v4u* residg;            // residual + bucket entries for per-lane (divergent) loads
 };
 
@@ -625,9 +626,10 @@ constexpr int kBktMaxTables = 8;   // bucketindex.py MAX_TABLES
 
 
 // Phased form: (A) every table's probe -- LDS reads only, all independent --
-// keeping the tag-matching slots of the (at most four) tables with one; (B)
-// per hit bucket the first row whose LDS filter the connection passes (LDS
-// only); (C) the (at most two) candidate rows loaded together and checked in
+// keeping the tag-matching slots of the (at most four) tables with one;
+// without row filters (B') their buckets two at a time, both first rows
+// loaded together; with row filters (B) per hit bucket the first row whose
+// LDS filter the connection passes (LDS only); (C) the (at most two) candidate rows loaded together and checked in
 // full; a candidate that fails (an 18-bit filter collision, or a side the
 // filter cannot check: port ranges, runs) continues its bucket's scan.  A
 // lane with more hit tables or candidates, or two tag-matching slots in one
@@ -677,6 +679,31 @@ __device__ __forceinline__ uint32_t bucket_lookup(const Rules& R, P32 img, uint3
   if (R.prof & 2) return best ^ (nh & 0x80000000u);             // PROFILING: probes only (results invalid)
   if ((slow || nh > 4u) && !(R.prof & 4)) return bucket_lookup_serial(R, img, lw, src, dst, ports, best);
   if (nh > 4u) nh = 4u;                                          // (only under R.prof & 4)
+  if (!R.bkt_filters) {
+    // (B') no row filters: the hit buckets two at a time, both first rows in flight
+    for (uint32_t p = 0; p < nh; p += 2) {
+      const uint32_t wa = p ? h2 : h0, wb = p ? h3 : h1;
+      const uint32_t ja = (tj >> (4 * p)) & 0xFu;
+      const bool two = p + 1 < nh;
+      const uint32_t jb = two ? (tj >> (4 * p + 4)) & 0xFu : ja;
+      const v2u ma = rd2(img, toff + kBktTableWords * ja + 6);   // min_gid, entry_base
+      const v2u mb = rd2(img, toff + kBktTableWords * jb + 6);
+      const uint32_t ea = ma.y + (wa & 0xFFFFu), eb = mb.y + ((two ? wb : wa) & 0xFFFFu);
+      const v4u aa = R.residg[2 * (size_t)ea], ca = R.residg[2 * (size_t)ea + 1];
+      const v4u ab = R.residg[2 * (size_t)eb], cb = R.residg[2 * (size_t)eb + 1];
+      if (best > ma.x) {
+        if (ca.z < best && entry_match(aa, ca, src, dst, ports)) best = min(best, entry_gid(ca, ports));
+        const uint32_t la = (wa >> 16) & kBktLenMask;
+        if (la > 1u) best = scan_bucket(R.residg, ea + 1, ea + la, best, src, dst, ports);
+      }
+      if (two && best > mb.x) {
+        if (cb.z < best && entry_match(ab, cb, src, dst, ports)) best = min(best, entry_gid(cb, ports));
+        const uint32_t lb = (wb >> 16) & kBktLenMask;
+        if (lb > 1u) best = scan_bucket(R.residg, eb + 1, eb + lb, best, src, dst, ports);
+      }
+    }
+    return best;
+  }
   // (B) candidate rows: absolute residual row and the rows left in its bucket
   uint32_t r0 = 0u, n0 = 0u, r1 = 0u, n1 = 0u, nc = 0u;
   for (uint32_t k = 0; k < nh; ++k) {
@@ -725,7 +752,9 @@ __device__ __forceinline__ uint32_t bucket_lookup(const Rules& R, P32 img, uint3
 // a waterfall over the distinct lists present in the wave (list id broadcast
 // by readlane, so entries are wave-uniform scalar loads); the index lookup
 // runs per lane.  kExact: ignore the index (the deferred-line path).
-template <bool kExact, bool kTasks, typename P32>
+// kMode: 0 = pht index, per-lane group loops; 1 = pht index, candidate groups
+// dealt out over the wave (RSA_OPT_GROUP_TASKS); 2 = bucket index.
+template <bool kExact, int kMode, typename P32>
 __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Rules& R, P32 img, unsigned int* flags,
                                                   lds_w32* scr) {
   const uint32_t list = t.w & 0xFFFFu;
@@ -770,7 +799,7 @@ __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Ru
   while (__ballot(go)) {
     const bool ix = go && img[lw + 1] != 0;
     uint32_t c = kNoGid;
-    if (R.bkt) {
+    if (kMode == 2) {
       // partial-key bucket index: exact, never deferred
       if (ix && !(R.prof & 1)) {
         if (R.force_defer) {
@@ -779,7 +808,7 @@ __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Ru
           c = bucket_lookup(R, img, lw, t.x, t.y, t.z, best);
         }
       }
-    } else if (kTasks) {
+    } else if (kMode == 1) {
       c = index_lookup_wave(R, img, lw, ix, t.x, t.y, t.z, scr);
     } else if (ix) {
       c = index_lookup(R, img, lw, t.x, t.y, t.z);
@@ -1056,13 +1085,13 @@ __device__ __forceinline__ void emit_one(uint32_t i, uint4 t, uint32_t gid, cons
 // with kEmit the line's counter word and table record (emit_wave).  Lines
 // whose index candidate failed verification kAttempts times go to `tail`
 // (k_tail scans and emits them exactly).
-template <int kImg, bool kEmit, bool kTasks>
+template <int kImg, bool kEmit, int kMode>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kImgSmallMax ? 4 : 8, 8))) void k_classify(
     const uint4* __restrict__ T, unsigned long long n, int32_t* __restrict__ gout, Rules R, unsigned int* flags,
     uint32_t* tail, unsigned long long* tail_n, Agg A, Emit E) {
   __shared__ __attribute__((aligned(16))) uint32_t lds_img[kImg > 0 ? kImg : 4];
-  __shared__ uint32_t lds_task[kTasks ? 1024 : 64];   // 64 words per wave (index_lookup_wave)
-  lds_w32* scr = (lds_w32*)lds_task + (kTasks ? (threadIdx.x & ~63u) : 0u);
+  __shared__ uint32_t lds_task[kMode == 1 ? 1024 : 64];   // 64 words per wave (index_lookup_wave)
+  lds_w32* scr = (lds_w32*)lds_task + (kMode == 1 ? (threadIdx.x & ~63u) : 0u);
   if (kImg > 0 && R.indexed) {
     const uint4* src = reinterpret_cast<const uint4*>(R.img);
     uint4* dst = reinterpret_cast<uint4*>(lds_img);
@@ -1079,9 +1108,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kIm
     const bool valid = in && (((t.w >> 16) & 0xFFu) & RSA_F_VALID);
     uint32_t gid;
     if (kImg > 0) {
-      gid = classify_wave<false, kTasks>(t, valid, R, (const lds_u32*)lds_img, flags, scr);
+      gid = classify_wave<false, kMode>(t, valid, R, (const lds_u32*)lds_img, flags, scr);
     } else {
-      gid = classify_wave<false, kTasks>(t, valid, R, R.img, flags, scr);
+      gid = classify_wave<false, kMode>(t, valid, R, R.img, flags, scr);
     }
     const bool defer = gid == kDefer;
     const unsigned long long dm = __ballot(defer);
@@ -1111,7 +1140,7 @@ __global__ __launch_bounds__(kBlock) void k_tail(const uint4* __restrict__ T, in
     const unsigned long long i = in ? tail[j] : 0u;
     const uint4 t = in ? T[i] : make_uint4(0u, 0u, 0u, 0u);
     const bool valid = in && (((t.w >> 16) & 0xFFu) & RSA_F_VALID);
-    const uint32_t gid = classify_wave<true, false>(t, valid, R, R.img, flags, nullptr);
+    const uint32_t gid = classify_wave<true, 0>(t, valid, R, R.img, flags, nullptr);
     if (gout && in) gout[i] = (int32_t)gid;
     if (kEmit && in) emit_one((uint32_t)i, t, gid, A, E);
   }
@@ -2194,6 +2223,7 @@ struct rsa_ctx {
   bool index_loaded = false;
   bool indexed = false;
   bool bkt_index = false;               // the loaded image is the bucket index (RSA_BKT_MAGIC)
+  bool bkt_filters = false;             // ... with row filters
   bool force_defer = false;
   bool group_tasks = true;     // RSA_OPT_GROUP_TASKS
   uint32_t prof_classify = 0;  // RSA_OPT_PROFILE_CLASSIFY
@@ -2305,6 +2335,7 @@ Rules rules_of(const rsa_ctx* c) {
   r.group_tasks = c->group_tasks ? 1 : 0;
   r.prof = (int)c->prof_classify;
   r.bkt = c->bkt_index ? 1 : 0;
+  r.bkt_filters = c->bkt_filters ? 1 : 0;
   r.residg = reinterpret_cast<const v4u*>(c->d_resid);
   return r;
 }
@@ -2488,17 +2519,17 @@ int ensure_events(rsa_ctx* c) {
 constexpr int kImgSmall = kImgSmallMax;   // 76 KiB: two 1024-thread workgroups per CU (32 waves)
 constexpr int kImgLarge = 38912;   // 152 KiB: one workgroup per CU
 
-template <bool kEmit, bool kTasks>
+template <bool kEmit, int kMode>
 void launch_classify_img(rsa_ctx* c, const uint4* t, uint64_t m, int32_t* go, const Rules& r, const Agg& ag,
                          const Emit& e) {
   if (c->indexed && c->img_words <= (uint32_t)kImgSmall) {
-    k_classify<kImgSmall, kEmit, kTasks><<<grid_for_threads(c, m, 1024, 2), 1024, 0, c->stream>>>(
+    k_classify<kImgSmall, kEmit, kMode><<<grid_for_threads(c, m, 1024, 2), 1024, 0, c->stream>>>(
         t, m, go, r, c->d_flags, c->d_tail, c->d_tail_n, ag, e);
   } else if (c->indexed && c->img_words <= (uint32_t)kImgLarge) {
-    k_classify<kImgLarge, kEmit, kTasks><<<grid_for_threads(c, m, 1024, 1), 1024, 0, c->stream>>>(
+    k_classify<kImgLarge, kEmit, kMode><<<grid_for_threads(c, m, 1024, 1), 1024, 0, c->stream>>>(
         t, m, go, r, c->d_flags, c->d_tail, c->d_tail_n, ag, e);
   } else {
-    k_classify<0, kEmit, kTasks><<<grid_for_threads(c, m, 1024, 2), 1024, 0, c->stream>>>(t, m, go, r, c->d_flags, c->d_tail,
+    k_classify<0, kEmit, kMode><<<grid_for_threads(c, m, 1024, 2), 1024, 0, c->stream>>>(t, m, go, r, c->d_flags, c->d_tail,
                                                                                    c->d_tail_n, ag, e);
   }
 }
@@ -2509,10 +2540,12 @@ template <bool kEmit>
 int launch_classify_t(rsa_ctx* c, const uint4* t, uint64_t m, int32_t* go, const Emit& e) {
   const Rules r = rules_of(c);
   const Agg ag = agg_of(c);
-  if (c->group_tasks) {
-    launch_classify_img<kEmit, true>(c, t, m, go, r, ag, e);
+  if (c->bkt_index) {
+    launch_classify_img<kEmit, 2>(c, t, m, go, r, ag, e);
+  } else if (c->group_tasks) {
+    launch_classify_img<kEmit, 1>(c, t, m, go, r, ag, e);
   } else {
-    launch_classify_img<kEmit, false>(c, t, m, go, r, ag, e);
+    launch_classify_img<kEmit, 0>(c, t, m, go, r, ag, e);
   }
   HIPCHK(c, hipGetLastError());
   // deferred lines (their number is read on the device: no host sync)
@@ -2966,7 +2999,7 @@ int rsa_load_index(rsa_ctx* c, const uint32_t* img, uint32_t words, const rsa_ru
             if (!len) continue;
             const uint64_t beg = (uint64_t)T.entry_base + (w & 0xFFFFu);
             if (beg + len > n_resid) return fail(c, RSA_ERR_ARG, "list %u table %u: bucket rows out of bounds", l, g);
-            if ((uint64_t)T.filter_off + (w & 0xFFFFu) + len > words)
+            if ((img[5] & 1u) && (uint64_t)T.filter_off + (w & 0xFFFFu) + len > words)
               return fail(c, RSA_ERR_ARG, "list %u table %u: row filters outside the image", l, g);
             for (uint64_t e = beg; e < beg + len; ++e)
               if (h_resid[e].gid >= c->n_rules || (e > beg && h_resid[e].gid < h_resid[e - 1].gid))
@@ -3023,6 +3056,7 @@ int rsa_load_index(rsa_ctx* c, const uint32_t* img, uint32_t words, const rsa_ru
   c->list_off = lo;
   c->index_loaded = true;
   c->bkt_index = bkt;
+  c->bkt_filters = bkt && (img[5] & 1u);
   c->indexed = true;
   return RSA_OK;
 }

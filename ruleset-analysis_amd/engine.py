@@ -96,6 +96,9 @@ class Engine(object):
         bucketindex.build_bucket_index()."""
         image, resid = (np.ascontiguousarray(a) for a in index)
         self._index_hold = (image, resid)
+        # which index is loaded (reporting): RSA4 'pht', RSA5 'bucket' / 'bucket-filtered'
+        self.index_kind = 'pht' if int(image[1]) == 0x34415352 else (
+            'bucket-filtered' if int(image[5]) & 1 else 'bucket')
         v = lambda a: a.ctypes.data_as(ctypes.c_void_p)
         self.ctx.call('rsa_load_index', v(image), ctypes.c_uint32(len(image)), v(resid), ctypes.c_uint32(len(resid)))
 
@@ -126,15 +129,16 @@ class Engine(object):
         return float(ms.value)
 
     def load_compiled(self, compiled, index=True, prefix=0, chunk=None, kind=None):
-        """Upload a CompiledRules' lists and its index (``kind``: 'bucket', the
-        default, or 'pht' -- the RSA_INDEX environment variable overrides the
-        default; the first ``prefix`` entries per list are scanned linearly,
-        records hold at most ``chunk`` entries each, chained)."""
+        """Upload a CompiledRules' lists and its index (``kind``: 'auto', the
+        default (CompiledRules.index), 'pht', 'bucket' or 'bucket-filtered' --
+        the RSA_INDEX environment variable overrides the default; the first ``prefix`` entries per list
+        are scanned linearly, records hold at most ``chunk`` entries each,
+        chained)."""
         import os
         ent, off = compiled.packed()
         self.load_rules(ent, off, compiled.n_rules)
         if index:
-            kind = kind or os.environ.get('RSA_INDEX', 'bucket')
+            kind = kind or os.environ.get('RSA_INDEX', 'auto')
             self.load_index(compiled.index(prefix=prefix, chunk=chunk, kind=kind))
 
     def set_rule_count(self, n_rules):

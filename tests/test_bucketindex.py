@@ -24,13 +24,14 @@ def _check(index, ent, off, tup, every=1):
     return n
 
 
+@pytest.mark.parametrize('kind', ['bucket', 'bucket-filtered'])
 @pytest.mark.parametrize('broad,prefix', [(False, 0), (True, 0), (False, 16)])
-def test_lookup_equals_scan_asa(broad, prefix):
+def test_lookup_equals_scan_asa(broad, prefix, kind):
     dbj, info = synth.make_db(71, 3000, interfaces=('outside', 'partner'), broad=broad)
     comp = CompiledRules(acldb.load_json(dbj))
     comp.ensure_lists()
     ent, off = comp.packed()
-    index = comp.index(prefix=prefix, kind='bucket')
+    index = comp.index(prefix=prefix, kind=kind)
     assert int(index[0][1]) == bi.BKT_MAGIC
     st = bi.bucket_stats(index)
     assert sum(s[1] for s in st) >= 4 and sum(s[3] for s in st) > 0.9 * len(ent) - sum(s[2] for s in st) - 64
@@ -39,7 +40,8 @@ def test_lookup_equals_scan_asa(broad, prefix):
     assert _check(index, ent, off, tup) > 8000
 
 
-def test_lookup_equals_scan_fortigate_chained():
+@pytest.mark.parametrize('kind', ['bucket', 'bucket-filtered'])
+def test_lookup_equals_scan_fortigate_chained(kind):
     """Run-compressed stepped entries (gid depends on the port) and lists
     chained over records of 700 entries."""
     text, info = synth_fg.make_config(7, n_policies=30, n_wide=1, n_mid=1, n_syslog=2, wide_members=(2, 3))
@@ -47,7 +49,7 @@ def test_lookup_equals_scan_fortigate_chained():
     comp.ensure_lists()
     ent, off = comp.packed()
     assert (ent['step'] != 0).sum() > 5
-    index = comp.index(chunk=700, kind='bucket')
+    index = comp.index(chunk=700, kind=kind)
     recs = _records(index[0])
     assert len(recs) > len(off) - 1                       # chained records exist
     tr = synth_fg.make_traffic(info, 4000, seed=8)
@@ -63,7 +65,8 @@ def test_image_invariants():
     comp = CompiledRules(acldb.load_json(dbj))
     comp.ensure_lists()
     ent, off = comp.packed()
-    image, resid = comp.index(kind='bucket')
+    image, resid = comp.index(kind='bucket-filtered')
+    assert int(image[5]) == 1
     words = len(image)
     for r in _records(image):
         prev = 0

@@ -24,10 +24,10 @@ def cfg4():
     return text, info, db, comp, coracle.OracleRules.from_fortigate(text)
 
 
-def _job_vs_oracle(engine, text, info, comp, R, n, seed, cap, chunk=None, index=True):
+def _job_vs_oracle(engine, text, info, comp, R, n, seed, cap, chunk=None, index=True, kind=None):
     tr = synth_fg.make_traffic(info, n, seed=seed)
     tup, ts, order = synth.pack(tr, comp)
-    engine.load_compiled(comp, index=index, chunk=chunk)
+    engine.load_compiled(comp, index=index, chunk=chunk, kind=kind)
     b = DeviceBatch.from_numpy(tup, ts, order, engine.device)
     res = engine.run([b], cap, capacity=max(built_hit_count(tup), 1))
     gids = engine.last_gids[0].cpu().numpy()
@@ -54,10 +54,17 @@ def test_cfg4_parity_indexed(engine, cfg4):
     assert (ref['gid'] >= 0).mean() > 0.4
 
 
-def test_cfg4_parity_chained_index_capped(engine, cfg4):
+@pytest.mark.parametrize('kind', ['pht', 'bucket', 'bucket-filtered'])
+def test_cfg4_parity_chained_index_capped(engine, cfg4, kind):
     """Index records of at most 4096 entries (chained) and a small cap."""
     text, info, db, comp, R = cfg4
-    _job_vs_oracle(engine, text, info, comp, R, 12000, seed=42, cap=20, chunk=4096)
+    _job_vs_oracle(engine, text, info, comp, R, 12000, seed=42, cap=20, chunk=4096, kind=kind)
+
+
+@pytest.mark.parametrize('kind', ['bucket', 'bucket-filtered'])
+def test_cfg4_parity_bucket_index(engine, cfg4, kind):
+    text, info, db, comp, R = cfg4
+    _job_vs_oracle(engine, text, info, comp, R, 12000, seed=44, cap=1000, kind=kind)
 
 
 def test_cfg4_parity_linear_scan(engine, cfg4):

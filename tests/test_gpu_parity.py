@@ -112,7 +112,7 @@ def test_synth_parity_linear_scan(engine):
     _gpu_vs_oracle(engine, 3000, 200000, 100, seed=18, index=False)
 
 
-@pytest.mark.parametrize('kind', ['bucket', 'pht'])
+@pytest.mark.parametrize('kind', ['pht', 'bucket'])
 def test_synth_parity_deferred_tail(engine, kind):
     """Every index lookup forced through the exact deferred-line kernel."""
     from ruleset_analysis_amd import native
@@ -123,9 +123,10 @@ def test_synth_parity_deferred_tail(engine, kind):
         engine.set_option(native.RSA_OPT_FORCE_DEFER, 0)
 
 
-def test_synth_parity_pht_index(engine):
-    """The pruned perfect-hash index (RSA4, the previous default) against the oracle."""
-    _gpu_vs_oracle(engine, 3000, 300000, 40, seed=61, zipf=1.2, broad=False, kind='pht')
+@pytest.mark.parametrize('kind', ['bucket', 'bucket-filtered'])
+def test_synth_parity_bucket_index(engine, kind):
+    """The partial-key bucket index (RSA5, both forms) against the oracle."""
+    _gpu_vs_oracle(engine, 3000, 300000, 40, seed=61, zipf=1.2, broad=False, kind=kind)
 
 
 def test_synth_parity_wave_cap_scatter(engine):
@@ -139,7 +140,7 @@ def test_synth_parity_wave_cap_scatter(engine):
         engine.set_option(native.RSA_OPT_WAVE_CAP_SCATTER, 0)
 
 
-@pytest.mark.parametrize('kind', ['bucket', 'pht'])
+@pytest.mark.parametrize('kind', ['pht', 'bucket', 'bucket-filtered'])
 @pytest.mark.parametrize('broad,prefix', [(True, 64), (False, 64), (False, 0), (False, 4096)])
 def test_index_and_scan_agree_10k(engine, broad, prefix, kind):
     """Both indexes (the bucket index and the pruned perfect-hash index, after
