@@ -266,9 +266,12 @@ __device__ __forceinline__ uint32_t rd16(const uint32_t* img, uint32_t h) { retu
 // slot = (x * n_slots) >> 16.  All operands fit the 24-bit multiplier
 // (n_slots <= 2^16), so both products are full-rate v_mad/v_mul_u32_u24
 // (the 32-bit v_mul_lo/hi and v_mad_u64 they replace issue at quarter rate).
+// NB: HIP's __umul24 returns a SIGNED int: a product >= 2^31 (x * n_slots with
+// n_slots > 2^15) must be shifted as unsigned, or the slot index goes negative.
+__device__ __forceinline__ uint32_t umul24(uint32_t a, uint32_t b) { return (uint32_t)__umul24(a, b); }
 __device__ __forceinline__ uint32_t pht_slot(uint32_t H, uint32_t d, uint32_t n_slots) {
-  const uint32_t x = (__umul24(d, (H >> 16) | 1u) + H) & 0xFFFFu;
-  return __umul24(x, n_slots) >> 16;
+  const uint32_t x = (umul24(d, (H >> 16) | 1u) + H) & 0xFFFFu;
+  return umul24(x, n_slots) >> 16;
 }
 
 // One CHD probe (compile.py _probe): H -> the slot's 16-bit value, or kNoCand.
@@ -586,8 +589,8 @@ template <typename P32>
 __device__ __forceinline__ uint32_t bkt_table(const Rules& R, P32 img, v4u a, v4u b, uint32_t src, uint32_t dst,
                                               uint32_t ports, uint32_t best) {
   const uint32_t h = bkt_hash(src & a.x, dst & a.y, ports & a.z, kBktSeedKey);
-  const uint32_t b1 = __umul24(h & 0xFFFFu, b.x) >> 16;   // n_buckets <= 2^16: 24-bit operands
-  const uint32_t b2 = __umul24(h >> 16, b.x) >> 16;
+  const uint32_t b1 = umul24(h & 0xFFFFu, b.x) >> 16;   // n_buckets <= 2^16: 24-bit operands
+  const uint32_t b2 = umul24(h >> 16, b.x) >> 16;
   const uint32_t tag = ((h >> 16) ^ h) & kBktTagMask;
   const v2u s1 = rd2(img, a.w + 2 * b1), s2 = rd2(img, a.w + 2 * b2);
   const uint32_t sl[4] = {s1.x, s1.y, s2.x, s2.y};
@@ -653,8 +656,8 @@ __device__ __forceinline__ uint32_t bucket_lookup(const Rules& R, P32 img, uint3
       const v4u a = rd4(img, tw);
       const uint32_t nb = img[tw + 4];
       const uint32_t h = bkt_hash(src & a.x, dst & a.y, ports & a.z, kBktSeedKey);
-      const uint32_t b1 = __umul24(h & 0xFFFFu, nb) >> 16;
-      const uint32_t b2 = __umul24(h >> 16, nb) >> 16;
+      const uint32_t b1 = umul24(h & 0xFFFFu, nb) >> 16;
+      const uint32_t b2 = umul24(h >> 16, nb) >> 16;
       const uint32_t tag = ((h >> 16) ^ h) & kBktTagMask;
       const v2u s1 = rd2(img, a.w + 2 * b1), s2 = rd2(img, a.w + 2 * b2);
       const uint32_t sl[4] = {s1.x, s1.y, s2.x, s2.y};

@@ -43,3 +43,13 @@ def test_ctx_create_without_gpu_fails_cleanly():
     lib = native.load()
     h = ctypes.c_void_p()
     assert lib.rsa_ctx_create(0, ctypes.byref(h)) != 0
+
+
+def test_no_signed_mul24_shifts():
+    """HIP's __umul24 returns a signed int: shifting a product >= 2^31 right
+    sign-extends it (an index of a table with more than 2^15 slots or buckets
+    went negative and faulted).  Only the unsigned wrapper may call it."""
+    for name in ('ruleset_hip.hip', 'textparse.hip', 'textparse_line.h'):
+        with open(os.path.join(ROOT, 'ruleset-analysis_amd', 'csrc', name)) as f:
+            calls = [l for l in f if '__umul24(' in l and 'uint32_t umul24(' not in l and not l.lstrip().startswith('//')]
+        assert calls == [], (name, calls)
