@@ -526,8 +526,17 @@ def rank_main(args, rank, world, local):
         last['merged'] = out
         return 0 if out is None else out[0].numel() // RECORD_DTYPE.itemsize
 
+    cold_ms = None
     for w in range(max(args.warmup, 1 if sizing['learn'] else 0)):
+        if w == 0:
+            # a cold one-shot job: first table allocation + clear (k_table_init)
+            # at the exact bound, nothing learned yet
+            torch.cuda.synchronize()
+            tc = time.perf_counter()
         step(False)
+        if w == 0:
+            torch.cuda.synchronize()
+            cold_ms = (time.perf_counter() - tc) * 1e3
         if sizing['learn']:
             learn_capacity()
 
@@ -601,6 +610,9 @@ def rank_main(args, rank, world, local):
                        'backend': args.backend if dist is not None else 'none', 'records': n_rec,
                        'table_capacity': sizing['capacity'], 'capacity_bound': bound,
                        'capacity_reruns': sizing['reruns'],
+                       'cold_job_ms': cold_ms,
+                       'cold_job': 'rank-local wall time of the first (untimed) job: table allocated and cleared '
+                                   'at the exact bound, no learned size',
                        'capacity_policy': 'first warmup job at the bound (hit+BUILT lines), then 4x the distinct '
                                           'entries it used; rerun at the bound on overflow'},
             'roofline': roofline_block(lines, classify_ms, aggregate_ms, float(np.mean(pass1_launches)),

@@ -21,3 +21,12 @@ for c in $CFGS; do
     > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err" || { tail -30 "$OUT/bench_$c.err"; exit 1; }
   python3 -c "import json,sys;d=json.load(open(sys.argv[1]));r=d['roofline'];p=r['pass1'];print(sys.argv[2],'%.3f G lines/s  %.3f ms/step  classify %.3f  aggregate %.3f  checks %s'%(d['value']/1e9,d['ms_per_step'],p['classify_ms'],p['aggregate_ms'],(d.get('checks') or {}).get('ok')))" "$OUT/bench_$c.json" "$c"
 done
+# kernel traces (rocprofv3 --kernel-trace --stats) of the configs in $TRACE
+for c in $TRACE; do
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace_$c" -o run --output-format csv -- \
+    python3 bench.py --config "$c" --no-cpu-baseline --no-check --steps 3 --warmup 1 \
+    > "$OUT/trace_$c.json" 2> "$OUT/trace_$c.err" || { tail -20 "$OUT/trace_$c.err"; exit 1; }
+  f=$(find "$OUT/trace_$c" -name '*kernel_trace.csv' | head -1)
+  [ -n "$f" ] && python3 tools/ktrace_summary.py "$f" > "$OUT/trace_${c}_summary.txt" 2>&1
+  true
+done
