@@ -375,6 +375,25 @@ int rsa_parse_text(rsa_ctx *ctx, const uint8_t *d_text, const uint64_t *d_off, u
 int rsa_order_keys(rsa_ctx *ctx, const uint8_t *d_text, const uint64_t *d_off, uint64_t n_lines, uint64_t base,
                    uint64_t *d_order);
 
+/* ---- Reducer drop-in parse: the sorted mapper stream ("host;acl;idx\t<log line>"
+ * per line) resident in HBM -> the per-line inputs of rsa_aggregate_gids.
+ * Replaces the per-line Python of connlist-reducer.py:62-79,146-165: strip,
+ * split('\t', 1), the hit test and the BUILT regex on the value, key and
+ * timestamp.  Per line: d_disp = RSA_RED_KEYED (d_tuples: src = FROMIP, dst =
+ * TOIP, dport = TOPORT, pspell, flags RSA_F_HIT / RSA_F_BUILT; d_ts the code
+ * when hit+BUILT), RSA_RED_NOISE (no tab after strip: the reducer's "Unable to
+ * unpack" line), or RSA_LINE_HOST (outside the device grammar: non-canonical
+ * address/port text, an unknown protocol spelling, a timestamp outside the code
+ * range); | RSA_RED_SAME_KEY when the line's key bytes equal the previous
+ * line's (both keyed).  Key validity (split(';'), int(), DB lookup) is decided
+ * by the host once per run of equal keys. */
+#define RSA_RED_KEYED 0
+#define RSA_RED_NOISE 1
+#define RSA_RED_SAME_KEY 0x100u
+int rsa_parse_reduce(rsa_ctx *ctx, const uint8_t *d_text, const uint64_t *d_off, uint64_t n_lines,
+                     const rsa_parse_spell *h_spells, uint32_t n_spells, rsa_tuple *d_tuples, uint32_t *d_ts,
+                     uint32_t *d_disp);
+
 /* Synchronise the ctx stream (tests, host hand-off). */
 int rsa_sync(rsa_ctx *ctx);
 

@@ -48,8 +48,10 @@ def _block(out, rule, hits, conns, first, last, cap):
     return rows
 
 
-def reduce_lines(lines, accesslists, cap=1000):
-    out = []
+def reduce_lines(lines, accesslists, cap=1000, out=None):
+    """``out``: a list the printed lines are appended to (so a caller still
+    has them when the reference's KeyError / IndexError / ValueError escapes)."""
+    out = [] if out is None else out
     blocks = []
     conns, first, last = {}, {}, {}
     currentkey = ''

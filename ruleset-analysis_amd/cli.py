@@ -26,26 +26,11 @@ import sys
 import numpy as np
 
 from . import acldb
-from .compile import CompiledRules, TUPLE_DTYPE, F_HIT, F_BUILT
-from .engine import DeviceBatch, Engine
-from .logparse import reducer_fields, reducer_timestamp
-from .py2text import PY2_WS, py2_int
+from .compile import CompiledRules
+from .engine import Engine
 from .pipeline import analyze_text
 from .textparse import parse_text
-from .report import mapper_output, reducer_report
-
-
-def _stdin_lines():
-    data = sys.stdin.buffer.read().decode('latin-1')
-    out, start = [], 0
-    while True:
-        i = data.find('\n', start)
-        if i < 0:
-            if start < len(data):
-                out.append(data[start:])
-            return out
-        out.append(data[start:i + 1])
-        start = i + 1
+from .report import mapper_output
 
 
 def _write(text):
@@ -122,136 +107,30 @@ def mapper_main(argv=None):
     return 0
 
 
-class _Interner(object):
-    def __init__(self):
-        self.ids = {}
-        self.values = []
-
-    def __call__(self, v):
-        k = self.ids.get(v)
-        if k is None:
-            k = self.ids[v] = len(self.values)
-            self.values.append(v)
-        return k
-
-
 def reducer_main(argv=None):
-    import re  # noqa: F401 - BUILT lives in logparse
+    """connlist-reducer.py as a stdin -> stdout filter (reducer_stream: GPU
+    parse and aggregation per chunk of RSA_REDUCER_CHUNK bytes, runs of equal
+    keys decided once on the host, output as the runs complete)."""
+    from .reducer_stream import ReducerStream
     config = load_config()
     db = _open_db(os.path.basename(config['ACCESSLIST_DATABASE_FILENAME']), 'reducer')
     cap = int(config['MAX_NUMBER_OF_CONNECTIONS_PER_RULE'])
-    lines = _stdin_lines()
-    runs = []            # (key, host, acl, rule)
-    events = []          # ('noise', text) | ('run', run id)
-    rows = []            # per line with a key: (run, flags, for, to, port, pspell, ts string)
-    spell, ips, ports = _Interner(), _Interner(), _Interner()
-    current = None
-    error = None
-    for raw in lines:
-        line = raw.strip(PY2_WS)
-        try:
-            key, value = line.split('\t', 1)
-            hostname, acl, ruleindex = key.split(';', 3)
-            rule = db.accesslists[hostname][acl]['rules'][py2_int(ruleindex)]
-            rule.hostname = hostname
-            rule.accesslist = acl
-        except ValueError:
-            events.append(('noise', line))
-            continue
-        except (KeyError, IndexError) as exc:        # the reference dies here
-            error = exc
-            break
-        if current is None or key != current:
-            current = key
-            runs.append((key, hostname, acl, rule))
-            events.append(('run', len(runs) - 1))
-        hit, res = reducer_fields(value)
-        flags = F_HIT if hit else 0
-        f = t = p = ps = 0
-        ts = None
-        if res is not None:
-            flags |= F_BUILT
-            ps, f, t, p = spell(res[5]), ips(res[6]), ips(res[8]), ports(res[9])
-            if hit:
-                ts = reducer_timestamp(res)
-        rows.append((len(runs) - 1, flags, f, t, p, ps, ts))
-    if len(ports.values) > 65536 or len(spell.values) > 256:
-        raise NotImplementedError('more than 65536 distinct port strings or 256 protocol words')
-    n = len(rows)
-    tup = np.zeros(n, dtype=TUPLE_DTYPE)
-    gids = np.zeros(n, dtype=np.int32)
-    if n:
-        arr = np.array([r[:6] for r in rows], dtype=np.int64)
-        gids[:] = arr[:, 0]
-        tup['flags'] = arr[:, 1]
-        tup['src'] = arr[:, 2]
-        tup['dst'] = arr[:, 3]
-        tup['dport'] = arr[:, 4]
-        tup['pspell'] = arr[:, 5]
-    distinct_ts = sorted({r[6] for r in rows if r[6] is not None})
-    code = {s: k for k, s in enumerate(distinct_ts)}
-    ts = np.array([code.get(r[6], 0) for r in rows], dtype=np.uint32)
-    order = np.arange(n, dtype=np.uint64)          # the input is already in reducer order
+    chunk = max(int(os.environ.get('RSA_REDUCER_CHUNK', 64 << 20)), 1)
     eng = Engine(0)
-    eng.set_rule_count(len(runs))
-    b = DeviceBatch.from_numpy(tup, ts, order, eng.device, gids=gids)
-    both = F_HIT | F_BUILT
-    res = eng.run([b], cap, capacity=max(int(np.count_nonzero((tup['flags'] & both) == both)), 1))
-    # decode interned fields back to text through the record fields
-    out = _reduce_text(events, runs, res, cap, distinct_ts, spell.values, ips.values, ports.values,
-                       finished=error is None)
-    _write(''.join(l + '\n' for l in out))
-    sys.stdout.flush()
-    if error is not None:
-        raise error
+
+    def write(text):
+        _write(text)
+        sys.stdout.flush()
+
+    job = ReducerStream(eng, db, cap, write, chunk=chunk)
+    src = sys.stdin.buffer
+    while True:
+        block = src.read(min(chunk, 16 << 20))
+        if not block:
+            break
+        job.feed(block)
+    job.finish()
     return 0
-
-
-def _reduce_text(events, runs, res, cap, ts_table, spells, ips, ports, finished=True):
-    from .report import NOISE1, HEADER, table_order
-    by_run = {}
-    rec = res.records
-    for k in np.argsort(rec['gid'], kind='stable'):
-        by_run.setdefault(int(rec['gid'][k]), []).append(rec[k])
-    out = []
-
-    def block(r):
-        key, host, acl, rule = runs[r]
-        rws = by_run.get(r, [])
-        if rws:
-            rws = [rws[k] for k in table_order([spells[int(x['pspell'])] for x in rws],
-                                               [ips[int(x['for_ip'])] for x in rws],
-                                               [ips[int(x['to_ip'])] for x in rws],
-                                               [ports[int(x['to_port'])] for x in rws],
-                                               [int(x['min_order']) for x in rws])]
-        lines = ['{0}: access-list {1}, rule {2}: {3}'.format(host, acl, rule.ruleindex, str(rule)),
-                 '{0}'.format(rule.original), 'Total number of hits: {0}'.format(int(res.hits[r]))]
-        if cap == 0 or int(res.thresh[r]) != 0xFFFFFFFFFFFFFFFF:
-            lines.append('NOTE: Maximum number of connections ({0}) reached for this rule, additional connections '
-                         'not displayed.'.format(cap))
-        lines.append(HEADER)
-        for x in rws:
-            lines.append('%6d %4s %15s  %15s %-5s %19s  %19s' % (int(x['count']), spells[int(x['pspell'])],
-                                                                 ips[int(x['for_ip'])], ips[int(x['to_ip'])],
-                                                                 ports[int(x['to_port'])], ts_table[int(x['first'])],
-                                                                 ts_table[int(x['last'])]))
-        return lines
-
-    prev = None
-    for kind, v in events:
-        if kind == 'noise':
-            out.append(NOISE1)
-            out.append('The line was: {0}'.format(v))
-        else:
-            if prev is not None:
-                out.append('')
-                out.extend(block(prev))
-            prev = v
-    if finished:
-        out.append('')
-        if prev is not None:
-            out.extend(block(prev))
-    return out
 
 
 def _host_of(path):

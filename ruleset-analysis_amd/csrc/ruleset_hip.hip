@@ -108,6 +108,7 @@ struct Rules {
 struct Agg {
   unsigned long long* matches;
   unsigned long long* hits;
+  unsigned long long* packed;        // per rule, rules beyond the LDS histogram: hits << 32 | lines of one launch
   unsigned int* distinct;
   const unsigned long long* thresh;
   const unsigned long long* filter;  // per rule: lines with order > filter cannot matter
@@ -1149,23 +1150,35 @@ __global__ __launch_bounds__(kBlock) void k_tail(const uint4* __restrict__ T, in
   }
 }
 
-// matches[key] += 1 for lanes with `m`, hits[key] += 1 for lanes with `h` (h
-// implies m): one loop over the wave's distinct keys, one device atomic per
-// key and counter.  Wave-uniform control flow.
-__device__ __forceinline__ void wave_count2(bool m, bool h, uint32_t key, unsigned long long* matches,
-                                            unsigned long long* hits) {
-  unsigned long long pending = __ballot(m);
+// packed[key] += m | h << 32 for every lane with `m` (h implies m): one
+// 64-bit device atomic per line (the lanes sharing the key of the wave's
+// first one combined into one), where a per-key waterfall over the wave
+// serialises up to 64 rounds on waves whose rules all differ -- the common
+// case with millions of rules (BASELINE config 4).  Wave-uniform control flow.
+__device__ __forceinline__ void wave_count_packed(bool m, bool h, uint32_t key, unsigned long long* packed) {
+  const unsigned long long pending = __ballot(m);
+  if (!pending) return;
   const unsigned long long hm = __ballot(h);
-  while (pending) {
-    const int leader = __builtin_ctzll(pending);
-    const uint32_t k = __builtin_amdgcn_readlane(key, leader);
-    const unsigned long long peers = __ballot(m && key == k);
-    pending &= ~peers;
-    if ((int)__lane_id() == leader) {
-      atomicAdd(&matches[k], (unsigned long long)__popcll(peers));
-      const unsigned long long hp = peers & hm;
-      if (hp) atomicAdd(&hits[k], (unsigned long long)__popcll(hp));
-    }
+  const int leader = __builtin_ctzll(pending);
+  const uint32_t k = __builtin_amdgcn_readlane(key, leader);
+  const unsigned long long peers = __ballot(m && key == k);
+  if ((int)__lane_id() == leader)
+    atomicAdd(&packed[k], (unsigned long long)__popcll(peers) | ((unsigned long long)__popcll(peers & hm) << 32));
+  if (m && key != k) atomicAdd(&packed[key], 1ull | ((unsigned long long)(h ? 1u : 0u) << 32));
+}
+
+// matches/hits += the packed counts of one launch (< 2^31 lines, so neither
+// half overflows), packed cleared for the next launch.
+__global__ __launch_bounds__(kBlock) void k_count_flush(unsigned long long* __restrict__ packed, uint32_t n_rules,
+                                                       unsigned long long* __restrict__ matches,
+                                                       unsigned long long* __restrict__ hits) {
+  const uint32_t stride = gridDim.x * kBlock;
+  for (uint32_t r = blockIdx.x * kBlock + threadIdx.x; r < n_rules; r += stride) {
+    const unsigned long long v = packed[r];
+    if (!v) continue;
+    packed[r] = 0;
+    matches[r] += v & 0xFFFFFFFFull;
+    if (v >> 32) hits[r] += v >> 32;
   }
 }
 
@@ -1197,7 +1210,7 @@ __global__ __launch_bounds__(1024) void k_count(const uint32_t* __restrict__ gh,
         if (m) atomicAdd(&cnt[g], 1u);
         if (h) atomicAdd(&cnt[kLds + g], 1u);
       } else {
-        wave_count2(m, h, g, A.matches, A.hits);
+        wave_count_packed(m, h, g, A.packed);
       }
     }
   }
@@ -1269,7 +1282,7 @@ __global__ __launch_bounds__(1024) void k_aggregate(const uint4* __restrict__ T,
           if (matched) atomicAdd(&cnt[gid], 1u);
           if (hit) atomicAdd(&cnt[kLds + gid], 1u);
         } else {
-          wave_count2(matched, hit, gid, A.matches, A.hits);
+          wave_count_packed(matched, hit, gid, A.packed);
         }
       }
       bool need = table && hit && (flags & RSA_F_BUILT);
@@ -2248,6 +2261,7 @@ struct rsa_ctx {
   bool table_ready = false;
   unsigned long long* d_filter = nullptr;
   uint32_t filter_len = 0;
+  unsigned long long* d_packed = nullptr;   // k_count / k_aggregate packed counters (rules > kCnt)
   bool auto_tighten = true;
   bool tightened = false;
   uint32_t profile_skip = 0;
@@ -2350,6 +2364,7 @@ Agg agg_of(const rsa_ctx* c) {
   a.distinct = c->d_distinct;
   a.thresh = c->d_thresh;
   a.filter = c->d_filter;
+  a.packed = c->d_packed;
   a.slots = c->d_slots;
   a.mask = c->slot_cap ? c->slot_cap - 1 : 0;
   a.used = c->d_used;
@@ -2615,6 +2630,8 @@ int launch_aggregate(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsig
         k_count<kCnt><<<grid_for_threads(c, units, 1024, RSA_COUNT_PER_CU), 1024, 0, c->stream>>>(gh, m, c->n_rules, ag);
       } else {
         k_count<0><<<grid_for_threads(c, units, 1024, 8), 1024, 0, c->stream>>>(gh, m, c->n_rules, ag);
+        k_count_flush<<<grid_for(c, c->n_rules, 8), kBlock, 0, c->stream>>>(c->d_packed, c->n_rules, c->d_matches,
+                                                                            c->d_hits);
       }
     }
   } else {
@@ -2628,6 +2645,9 @@ int launch_aggregate(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsig
     } else {
       k_aggregate<0><<<grid_for_threads(c, units, 1024, 2), 1024, 0, c->stream>>>(t, ts, o, g, m, c->n_rules, ag,
                                                                                   recs, c->d_regs, c->d_wcnt);
+      if (!(ag.skip & 1u))
+        k_count_flush<<<grid_for(c, c->n_rules, 8), kBlock, 0, c->stream>>>(c->d_packed, c->n_rules, c->d_matches,
+                                                                            c->d_hits);
     }
   }
   HIPCHK(c, hipGetLastError());
@@ -2807,7 +2827,7 @@ int rsa_ctx_destroy(rsa_ctx* c) {
   void* bufs[] = {c->d_tail, c->d_tail_n, c->d_gscratch, c->d_gh, c->d_stats, c->d_recs, c->d_recs2, c->d_regs, c->d_wcnt, c->d_nrecs, c->d_starts, c->d_hist,
                   c->d_scan_sums, c->d_occ, c->d_entries, c->d_off,
                   c->d_img, c->d_resid,
-                  c->d_slots, c->d_used, c->d_used_n, c->d_filter, c->d_flags, c->d_cursor, c->d_cidx,
+                  c->d_slots, c->d_used, c->d_used_n, c->d_filter, c->d_packed, c->d_flags, c->d_cursor, c->d_cidx,
                   c->d_capped_gid, c->d_capped_cnt, c->d_capped_start, c->d_keys};
   for (void* b : bufs) (void)hipFree(b);
   for (int k = 0; k < kMaxEvents; ++k)
@@ -3150,10 +3170,14 @@ int rsa_reset(rsa_ctx* c, uint64_t capacity, uint32_t cap) {
     hipFree(c->d_filter);
     c->d_filter = nullptr;
     c->filter_len = 0;
+    hipFree(c->d_packed);
+    c->d_packed = nullptr;
     HIPCHK(c, hipMalloc(&c->d_filter, (nr ? nr : 1) * sizeof(unsigned long long)));
+    HIPCHK(c, hipMalloc(&c->d_packed, (nr ? nr : 1) * sizeof(unsigned long long)));
     c->filter_len = nr ? (uint32_t)nr : 1;
   }
   HIPCHK(c, hipMemsetAsync(c->d_filter, 0xFF, (nr ? nr : 1) * sizeof(unsigned long long), c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_packed, 0, (nr ? nr : 1) * sizeof(unsigned long long), c->stream));
   c->tightened = false;
   HIPCHK(c, hipMemsetAsync(c->d_flags, 0, 4 * sizeof(unsigned int), c->stream));
   c->table_ready = true;

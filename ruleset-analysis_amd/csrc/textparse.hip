@@ -152,6 +152,9 @@ __global__ void k_set_u64(uint64_t* p, uint64_t v) { *p = v; }
 // whose lines do not fit parses straight from HBM with byte loads.
 constexpr uint32_t kParseWG = 128, kStageBytes = 32768;
 
+// kReduce: the reducer drop-in's lines (rsa_text::reduce_line, plus the
+// same-key flag against the previous line of the batch).
+template <bool kReduce>
 __global__ __launch_bounds__(kParseWG) void k_parse(const uint8_t* __restrict__ text, const uint64_t* __restrict__ off,
                                                     uint64_t n_lines, const rsa_parse_ifc* __restrict__ ifcs,
                                                     uint32_t n_ifcs, const rsa_parse_spell* __restrict__ spells,
@@ -188,7 +191,33 @@ __global__ __launch_bounds__(kParseWG) void k_parse(const uint8_t* __restrict__ 
   rsa_tuple tup = {0u, 0u, 0, 0, 0, 0, 0};
   uint32_t ts = 0, d = RSA_LINE_HOST;
   if (len < 0xFFFFFFFFull) {
-    if (staged) {
+    if (kReduce) {
+      // the previous line: staged unless it is the workgroup's first line's predecessor
+      const uint64_t pa = i ? off[i - 1] : 0;
+      uint64_t plen = a - pa;
+      if (plen && text[a - 1] == '\n') --plen;
+      const bool pin = i > 0 && plen < 0xFFFFFFFFull;
+      if (staged) {
+        const rsa_text::WordLn s{sm, (uint32_t)(a - base), (uint32_t)len, 0xFFFFFFFFu, 0u};
+        rsa_text::reduce_line(s, spells, n_spells, tup, ts, d);
+        if (pin && d != RSA_RED_NOISE) {
+          bool same;
+          if (i > l0) {
+            const rsa_text::WordLn q{sm, (uint32_t)(pa - base), (uint32_t)plen, 0xFFFFFFFFu, 0u};
+            same = rsa_text::same_key(s, q);
+          } else {
+            const rsa_text::ByteLn q{text + pa, (uint32_t)plen};
+            same = rsa_text::same_key(s, q);
+          }
+          if (same) d |= RSA_RED_SAME_KEY;
+        }
+      } else {
+        const rsa_text::ByteLn s{text + a, (uint32_t)len};
+        rsa_text::reduce_line(s, spells, n_spells, tup, ts, d);
+        if (pin && d != RSA_RED_NOISE && rsa_text::same_key(s, rsa_text::ByteLn{text + pa, (uint32_t)plen}))
+          d |= RSA_RED_SAME_KEY;
+      }
+    } else if (staged) {
       const rsa_text::WordLn s{sm, (uint32_t)(a - base), (uint32_t)len, 0xFFFFFFFFu, 0u};
       rsa_text::parse_line(s, ifcs, n_ifcs, spells, n_spells, tup, ts, d);
     } else {
@@ -433,8 +462,34 @@ int rsa_parse_text(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_off, uin
     return rsa_internal_fail(c, RSA_ERR_ARG, "rsa_parse_text: d_text must be 4-byte aligned");
   const uint64_t nb = (n_lines + kParseWG - 1) / kParseWG;
   if (nb > 0x7FFFFFFFull) return rsa_internal_fail(c, RSA_ERR_ARG, "too many lines");
-  hipLaunchKernelGGL(k_parse, dim3((uint32_t)nb), dim3(kParseWG), 0, st, d_text, d_off, n_lines, d_ifcs, n_ifcs, d_spells,
+  hipLaunchKernelGGL(k_parse<false>, dim3((uint32_t)nb), dim3(kParseWG), 0, st, d_text, d_off, n_lines, d_ifcs, n_ifcs, d_spells,
                      n_spells, d_tuples, d_ts, d_disp);
+  TPCHK(c, hipGetLastError());
+  return RSA_OK;
+}
+
+int rsa_parse_reduce(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_off, uint64_t n_lines,
+                     const rsa_parse_spell* h_spells, uint32_t n_spells, rsa_tuple* d_tuples, uint32_t* d_ts,
+                     uint32_t* d_disp) {
+  if (!c || (n_lines && (!d_text || !d_off || !d_tuples || !d_ts || !d_disp))) return RSA_ERR_ARG;
+  if (n_spells > 64 || (n_spells && !h_spells))
+    return rsa_internal_fail(c, RSA_ERR_ARG, "rsa_parse_reduce: bad spelling table");
+  for (uint32_t k = 0; k < n_spells; ++k)
+    if (h_spells[k].len > 15) return rsa_internal_fail(c, RSA_ERR_ARG, "rsa_parse_reduce: spelling too long");
+  if (!n_lines) return RSA_OK;
+  if (reinterpret_cast<uintptr_t>(d_text) & 3u)
+    return rsa_internal_fail(c, RSA_ERR_ARG, "rsa_parse_reduce: d_text must be 4-byte aligned");
+  const uint64_t nb = (n_lines + kParseWG - 1) / kParseWG;
+  if (nb > 0x7FFFFFFFull) return rsa_internal_fail(c, RSA_ERR_ARG, "too many lines");
+  hipStream_t st = rsa_internal_stream(c);
+  Scratch S{c, st};
+  const size_t sb = (size_t)n_spells * sizeof(rsa_parse_spell);
+  TPCHK(c, hipMallocAsync(&S.base, sb + 64, st));
+  rsa_parse_spell* d_spells = static_cast<rsa_parse_spell*>(S.base);
+  if (sb) TPCHK(c, hipMemcpyAsync(d_spells, h_spells, sb, hipMemcpyHostToDevice, st));
+  TPCHK(c, hipStreamSynchronize(st));   // the host table may go away after return
+  hipLaunchKernelGGL(k_parse<true>, dim3((uint32_t)nb), dim3(kParseWG), 0, st, d_text, d_off, n_lines, nullptr, 0u,
+                     d_spells, n_spells, d_tuples, d_ts, d_disp);
   TPCHK(c, hipGetLastError());
   return RSA_OK;
 }

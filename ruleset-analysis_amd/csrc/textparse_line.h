@@ -456,6 +456,92 @@ RSA_HD void parse_line(const S& s, const rsa_parse_ifc* ifcs, uint32_t n_ifcs, c
   d_out = d;
 }
 
+// ---- the reducer drop-in: one line of the sorted mapper stream
+// (connlist-reducer.py:62-79,146-165)
+
+RSA_HD bool is_py2ws(uint32_t c) { return c == ' ' || c - 9u < 5u; }   // Python 2 str.strip(): ' \t\n\v\f\r'
+
+// The value of a mapper-stream line: byte i = byte o + i of the line.
+template <class S>
+struct SubLn {
+  const S& s;
+  uint32_t o;
+  uint32_t n;
+  RSA_HD uint32_t operator[](uint32_t i) const { return s[o + i]; }
+};
+
+// line.strip().split('\t', 1): the key is [a, t); false when the stripped
+// line [a, b) has no tab (the reducer's ValueError "Unable to unpack" line)
+template <class S>
+RSA_HD bool key_span(const S& s, uint32_t& a, uint32_t& t, uint32_t& b) {
+  a = 0;
+  b = s.n;
+  while (a < b && is_py2ws(s[a])) ++a;
+  while (b > a && is_py2ws(s[b - 1])) --b;
+  for (t = a; t < b; ++t)
+    if (s[t] == '\t') return true;
+  return false;
+}
+
+// The reducer's per-line fields: disposition (RSA_RED_* or RSA_LINE_HOST),
+// tuple (src = FROMIP, dst = TOIP, dport = TOPORT, pspell, flags) and the
+// timestamp code of a hit line whose value the BUILT regex matches.
+template <class S>
+RSA_HD void reduce_line(const S& s, const rsa_parse_spell* spells, uint32_t n_spells, rsa_tuple& tup_out,
+                        uint32_t& ts_out, uint32_t& d_out) {
+  rsa_tuple tup = {0u, 0u, 0, 0, 0, 0, 0};
+  uint32_t ts = 0, d = RSA_RED_NOISE;
+  uint32_t a, t, b;
+  if (key_span(s, a, t, b)) {
+    d = RSA_RED_KEYED;
+    const SubLn<S> v{s, t + 1, b - t - 1};
+    uint32_t flags = 0;
+    const bool hit = hit_test(v);
+    if (hit) flags |= RSA_F_HIT;
+    Reduced r;
+    if (built_search(v, r)) {
+      flags |= RSA_F_BUILT;
+      uint32_t vf = 0, vt = 0;
+      const uint32_t pv = port_val(v, r.to_port);
+      // the key is the text: canonical text <-> value is one to one
+      if (!ipv4_canon(v, r.for_ip, vf) || !ipv4_canon(v, r.to_ip, vt) || !port_canon(v, r.to_port) || pv > 65535u)
+        d = RSA_LINE_HOST;
+      if (hit && !ts_code(v, r, ts)) d = RSA_LINE_HOST;
+      int32_t sid = -1;
+      const uint32_t wl = r.word.b - r.word.a;
+      for (uint32_t k = 0; k < n_spells && sid < 0; ++k) {
+        if (spells[k].len != wl) continue;
+        bool eq = true;
+        for (uint32_t c = 0; c < wl && eq; ++c) eq = v[r.word.a + c] == (uint8_t)spells[k].word[c];
+        if (eq) sid = (int32_t)k;
+      }
+      if (sid < 0) d = RSA_LINE_HOST;
+      tup.src = vf;
+      tup.dst = vt;
+      tup.dport = (uint16_t)pv;
+      tup.pspell = (uint8_t)(sid < 0 ? 0 : sid);
+    }
+    tup.flags = (uint8_t)flags;
+  }
+  if (d != RSA_RED_KEYED) {
+    tup = rsa_tuple{0u, 0u, 0, 0, 0, 0, 0};
+    ts = 0;
+  }
+  tup_out = tup;
+  ts_out = ts;
+  d_out = d;
+}
+
+// Key bytes of two lines equal (both keyed): runs of equal keys.
+template <class S1, class S2>
+RSA_HD bool same_key(const S1& x, const S2& y) {
+  uint32_t xa, xt, xb, ya, yt, yb;
+  if (!key_span(x, xa, xt, xb) || !key_span(y, ya, yt, yb) || xt - xa != yt - ya) return false;
+  for (uint32_t i = 0; i < xt - xa; ++i)
+    if (x[xa + i] != y[ya + i]) return false;
+  return true;
+}
+
 #undef RSA_HD
 
 }  // namespace rsa_text

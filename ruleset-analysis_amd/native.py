@@ -76,6 +76,7 @@ SYMBOLS = {
     'rsa_text_line_offsets': (I32, [P, P, U64, P, U64]),
     'rsa_parse_text': (I32, [P, P, P, U64, P, U32, P, U32, P, P, P]),
     'rsa_order_keys': (I32, [P, P, P, U64, U64, P]),
+    'rsa_parse_reduce': (I32, [P, P, P, U64, P, U32, P, P, P]),
     'rsa_sync': (I32, [P]),
 }
 

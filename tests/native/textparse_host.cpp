@@ -23,3 +23,27 @@ extern "C" void parse_lines_host(const uint8_t* text, const uint64_t* off, uint6
     }
   }
 }
+
+// The reducer drop-in's per-line parse (textparse.hip k_parse<true>): each
+// line's fields and the same-key flag against the previous line.
+extern "C" void reduce_lines_host(const uint8_t* text, const uint64_t* off, uint64_t n, const rsa_parse_spell* spells,
+                                  uint32_t n_spells, rsa_tuple* tuples, uint32_t* ts, uint32_t* disp, int word) {
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t a = off[i], b = off[i + 1];
+    uint64_t len = b - a;
+    if (len && text[b - 1] == '\n') --len;
+    const rsa_text::ByteLn s{text + a, (uint32_t)len};
+    if (word) {
+      const rsa_text::WordLn w{reinterpret_cast<const uint32_t*>(text), (uint32_t)a, (uint32_t)len, 0xFFFFFFFFu, 0u};
+      rsa_text::reduce_line(w, spells, n_spells, tuples[i], ts[i], disp[i]);
+    } else {
+      rsa_text::reduce_line(s, spells, n_spells, tuples[i], ts[i], disp[i]);
+    }
+    if (i > 0 && disp[i] != RSA_RED_NOISE) {
+      const uint64_t pa = off[i - 1];
+      uint64_t plen = a - pa;
+      if (plen && text[a - 1] == '\n') --plen;
+      if (rsa_text::same_key(s, rsa_text::ByteLn{text + pa, (uint32_t)plen})) disp[i] |= RSA_RED_SAME_KEY;
+    }
+  }
+}

@@ -10,7 +10,7 @@ OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 if [ -z "$SKIP_TESTS" ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+  timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -x -q --timeout 300 --timeout-method thread \
     > "$OUT/pytest.log" 2>&1 || { tail -40 "$OUT/pytest.log"; exit 1; }
   tail -3 "$OUT/pytest.log"
 fi
@@ -21,6 +21,11 @@ for c in $CFGS; do
     > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err" || { tail -30 "$OUT/bench_$c.err"; exit 1; }
   python3 -c "import json,sys;d=json.load(open(sys.argv[1]));r=d['roofline'];p=r['pass1'];print(sys.argv[2],'%.3f G lines/s  %.3f ms/step  classify %.3f  aggregate %.3f  checks %s'%(d['value']/1e9,d['ms_per_step'],p['classify_ms'],p['aggregate_ms'],(d.get('checks') or {}).get('ok')))" "$OUT/bench_$c.json" "$c"
 done
+# extra GPU steps (each a command line, run under a time limit)
+if [ -n "$EXTRA" ]; then
+  timeout -k 10 600 bash -c "$EXTRA" > "$OUT/extra.log" 2>&1 || { tail -30 "$OUT/extra.log"; exit 1; }
+  tail -5 "$OUT/extra.log"
+fi
 # kernel traces (rocprofv3 --kernel-trace --stats) of the configs in $TRACE
 for c in $TRACE; do
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace_$c" -o run --output-format csv -- \
