@@ -40,12 +40,14 @@ def main():
     lines = stream.splitlines(True)
     lines.sort()                                   # LC_ALL=C sort: byte order
     data = b''.join(lines)
+    eng.close()
+    red = Engine(0)                                # the reducer's own ctx (no rule lists loaded)
     out = []
     best = None
     for rep in range(3):
         out = []
-        job = ReducerStream(eng, acldb.load_json(dbj), cap, out.append)
-        eng.torch.cuda.synchronize()
+        job = ReducerStream(red, acldb.load_json(dbj), cap, out.append)
+        red.torch.cuda.synchronize()
         t = time.perf_counter()
         for a in range(0, len(data), 16 << 20):
             job.feed(data[a:a + (16 << 20)])
