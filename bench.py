@@ -694,11 +694,14 @@ def text_main(args):
     v = lambda t: ctypes.c_void_p(t.data_ptr())
     hp = lambda a: a.ctypes.data_as(ctypes.c_void_p)
     ctx = eng.ctx
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
     phases = []
     last = {}
+    group = torch.empty(n, dtype=torch.int32, device=dev)
 
     def step(timed):
+        # split -> parse -> classify -> order keys within each rule (the reducer
+        # only compares one rule's lines: pipeline.analyze_text) -> aggregate
         ev[0].record()
         nl = ctypes.c_uint64(0)
         ctx.call('rsa_text_count_lines', v(text), ctypes.c_uint64(len(data)), ctypes.byref(nl))
@@ -709,24 +712,28 @@ def text_main(args):
         ctx.call('rsa_parse_text', v(text), v(off), ctypes.c_uint64(n), hp(ifcs), ctypes.c_uint32(len(ifcs)),
                  hp(spells), ctypes.c_uint32(len(spells)), v(tup), v(ts), v(disp))
         ev[2].record()
-        ctx.call('rsa_order_keys', v(text), v(off), ctypes.c_uint64(n), ctypes.c_uint64(0), v(order))
+        ctx.call('rsa_classify_only', v(tup), ctypes.c_uint64(n), v(gbuf))
+        flags = (tup[:, 3] >> 16) & 0xFF
+        both = 0x06
+        hb = (flags & both) == both
+        torch.where(hb & (gbuf >= 0), gbuf, torch.full_like(gbuf, -1), out=group)
         ev[3].record()
+        ctx.call('rsa_order_keys_grouped', v(text), v(off), ctypes.c_uint64(n), v(group), ctypes.c_uint64(0), v(order))
+        ev[4].record()
         n_host = int(((disp & 0xFF) == textparse.LINE_HOST).sum().item())
         if n_host:
             die('%d synthetic lines outside the device grammar' % n_host)
-        flags = (tup[:, 3] >> 16) & 0xFF
-        both = 0x06
-        n_hb = int(((flags & both) == both).sum().item())
-        b = DeviceBatch(tup, ts, order)
+        n_hb = int(hb.sum().item())
+        b = DeviceBatch(tup, ts, order, gbuf)
         eng.reset(max(n_hb, 1), wl.cap)
-        eng.pass1(b, gbuf)
+        eng.pass1(b)
         if eng.resolve_cap():
-            eng.pass2(b, gbuf)
+            eng.pass2(b)
         last['recs'] = eng.emit_device('final')
-        ev[4].record()
+        ev[5].record()
         if timed:
             torch.cuda.synchronize()
-            phases.append([ev[k].elapsed_time(ev[k + 1]) for k in range(4)])
+            phases.append([ev[k].elapsed_time(ev[k + 1]) for k in range(5)])
 
     for _ in range(args.warmup):
         step(False)
@@ -755,10 +762,13 @@ def text_main(args):
         same_tuples = bool(np.array_equal(gt[cls].view(np.uint8), pk[cls].view(np.uint8))) and \
             not pk['flags'][~cls].any()
         perm = torch.argsort(order).cpu().numpy()
+        grp = group.cpu().numpy()
         rng = np.random.default_rng(0)
         sample = rng.integers(0, n - 1, 100_000)
         line = lambda i: data[h_off[i]:h_off[i + 1] - 1]
-        sorted_pairs = all(line(perm[j]) <= line(perm[j + 1]) for j in sample)
+        # adjacent ranks of one rule's lines are in byte order (ranks are grouped by rule)
+        sorted_pairs = all(line(perm[j]) <= line(perm[j + 1]) for j in sample
+                           if grp[perm[j]] >= 0 and grp[perm[j]] == grp[perm[j + 1]])
         distinct = bool(torch.unique(order).numel() == n)
         c_text = record_checksum(last['recs'])
         b2 = DeviceBatch.from_numpy(pk, ts.cpu().numpy().view(np.uint32), order.cpu().numpy().view(np.uint64), dev)
@@ -774,7 +784,7 @@ def text_main(args):
     text_bytes = len(data)
     parse_gbs = (text_bytes + 32 * n) / (ph[1] * 1e-3) / 1e9
     res = {
-        'metric': 'log lines/sec from TEXT in HBM: line split + parse + order keys + classify + aggregate (1 GPU)',
+        'metric': 'log lines/sec from TEXT in HBM: line split + parse + classify + order keys + aggregate (1 GPU)',
         'value': n * args.steps / dt, 'unit': 'lines/s', 'n_gpus': 1, 'steps': args.steps, 'warmup': args.warmup,
         'ms_per_step': dt / args.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
         'dtype': 'u8',
@@ -782,7 +792,8 @@ def text_main(args):
         'config': {'workload': '%s text: %d lines, %.2f GB, %d expanded rules, cap %d'
                                % (args.config, n, text_bytes / 1e9, compiled.n_rules, wl.cap),
                    'lines': n, 'text_bytes': text_bytes, 'parallelism': 'dp1'},
-        'phases_ms': {'split': ph[0], 'parse': ph[1], 'order_keys': ph[2], 'classify_aggregate_job': ph[3]},
+        'phases_ms': {'split': ph[0], 'parse': ph[1], 'classify': ph[2], 'order_keys_within_rules': ph[3],
+                      'aggregate_job': ph[4]},
         'roofline': {'bound': 'hbm', 'kernel': 'k_parse', 'achieved': parse_gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': parse_gbs / HBM_PEAK_GBS, 'traffic': None,
                      'bytes': 'text bytes read + 32 B/line (off 8, tuple 16, ts 4, disp 4)'},

@@ -182,6 +182,8 @@ typedef struct rsa_pht_list {    /* 80 B: one list (or one chained chunk of a li
 #define RSA_OPT_GROUP_TASKS 12 /* index lookup: candidate groups dealt out over the wave (1, default) or per-lane loops (0) */
 #define RSA_OPT_PROFILE_CLASSIFY 13 /* PROFILING ONLY, results invalid: bit0 no index lookup, bit1 pruning only (bucket index: probes only), bit2 no verification (bucket: no serial fallback) */
 #define RSA_OPT_STATS 10       /* PROFILING: count table work into the rsa_stats counters (default 0)                 */
+#define RSA_OPT_HOT_SPLIT 14   /* pre-combine regions holding > max(RSA_OPT_HOT_MIN, 4 x mean) records on all CUs (default 1) */
+#define RSA_OPT_HOT_MIN 15     /* hot-region minimum in records (default 65536; below it TESTING: any region above it is hot) */
 
 /* One distinct (rule, connection) aggregate, 40 B (connlist-reducer.py:162-176). */
 typedef struct rsa_conn_record {
@@ -374,6 +376,14 @@ int rsa_parse_text(rsa_ctx *ctx, const uint8_t *d_text, const uint64_t *d_off, u
  * groups refined by radix sorts until every line is settled. */
 int rsa_order_keys(rsa_ctx *ctx, const uint8_t *d_text, const uint64_t *d_off, uint64_t n_lines, uint64_t base,
                    uint64_t *d_order);
+/* Order keys within groups: d_order[i] = base + rank of (d_group[i], line i's
+ * bytes), for the lines with d_group[i] >= 0 (the others get distinct ranks
+ * after them).  The reducer compares order keys of ONE rule's lines only (its
+ * cap point and first-seen order, connlist-reducer.py:151,167-176), so with the
+ * line's rule as its group the keys are exact, and lines of different rules
+ * are never compared: most groups are settled by the timestamp prefix. */
+int rsa_order_keys_grouped(rsa_ctx *ctx, const uint8_t *d_text, const uint64_t *d_off, uint64_t n_lines,
+                           const int32_t *d_group, uint64_t base, uint64_t *d_order);
 
 /* ---- Reducer drop-in parse: the sorted mapper stream ("host;acl;idx\t<log line>"
  * per line) resident in HBM -> the per-line inputs of rsa_aggregate_gids.

@@ -1485,6 +1485,88 @@ __device__ __forceinline__ unsigned long long readlane64(unsigned long long v, i
   return ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) |
          __builtin_amdgcn_readlane((uint32_t)v, l);
 }
+// One (possibly pre-combined) record per lane into a workgroup's LDS
+// aggregation table (open addressing; the caller keeps it below 3/4 load):
+// count summed, first/last min/max, first-seen order min (kMinOrder).  Hot
+// keys: a rule with one distinct connection puts all its records into one
+// region, so lanes sharing the key of one of the wave's first live lanes are
+// combined with wave reductions and enter the table as ONE insert (LDS atomics
+// on one address serialise over the lanes).  Wave-uniform call.
+template <int kE, bool kMinOrder>
+__device__ __forceinline__ void lds_agg_insert(unsigned long long (&e_kA)[kE], unsigned long long (&e_kB)[kE],
+                                               unsigned long long (&e_mo)[kE], uint32_t (&e_first)[kE],
+                                               uint32_t (&e_last)[kE], uint32_t (&e_cnt)[kE], uint32_t& used,
+                                               bool have, unsigned long long kA, unsigned long long kB,
+                                               unsigned long long mo, uint32_t first, uint32_t last, uint32_t cnt) {
+  unsigned long long pending = __ballot(have);
+  for (int att = 0; att < kHotTries && pending; ++att) {
+    const int l0 = __builtin_ctzll(pending);
+    const unsigned long long kA0 = readlane64(kA, l0), kB0 = readlane64(kB, l0);
+    const bool dom = have && kA == kA0 && kB == kB0;
+    const unsigned long long dm = __ballot(dom);
+    pending &= ~dm;
+    if (__popcll(dm) >= kHotMin) {
+      uint32_t f = dom ? first : 0xFFFFFFFFu, l = dom ? last : 0u, c = dom ? cnt : 0u;
+      unsigned long long o = dom ? mo : ~0ull;
+#pragma unroll
+      for (int sh = 32; sh; sh >>= 1) {
+        f = min(f, (uint32_t)__shfl_xor((int)f, sh));
+        l = max(l, (uint32_t)__shfl_xor((int)l, sh));
+        c += (uint32_t)__shfl_xor((int)c, sh);
+        const unsigned long long oo = __shfl_xor(o, sh);
+        o = oo < o ? oo : o;
+      }
+      if (dom) {
+        if ((int)__lane_id() == l0) {
+          cnt = c;
+          first = f;
+          last = l;
+          mo = o;
+        } else {
+          have = false;
+        }
+      }
+    }
+  }
+  if (!have) return;
+  const uint32_t h = (uint32_t)mix64(kA ^ (kB * 0x9e3779b97f4a7c15ull));
+  uint32_t e = (kE & (kE - 1)) == 0 ? (h & (kE - 1)) : __umulhi(h, (uint32_t)kE);
+  while (true) {
+    const unsigned long long cur = __hip_atomic_load(&e_kB[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (cur == kEmpty) {
+      if (atomicCAS(&e_kB[e], kEmpty, kBusy) == kEmpty) {
+        e_kA[e] = kA;
+        e_mo[e] = mo;
+        e_first[e] = first;
+        e_last[e] = last;
+        e_cnt[e] = cnt;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        atomicExch(&e_kB[e], kB);
+        atomicAdd(&used, 1u);
+        return;
+      }
+      continue;
+    }
+    if (cur == kBusy) continue;
+    if (cur == kB && __hip_atomic_load(&e_kA[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == kA) {
+      atomicAdd(&e_cnt[e], cnt);
+      atomicMin(&e_first[e], first);
+      atomicMax(&e_last[e], last);
+      if (kMinOrder) atomicMin(&e_mo[e], mo);
+      return;
+    }
+    e = e + 1 == (uint32_t)kE ? 0u : e + 1;
+  }
+}
+
+// A hot region's pre-combined records (k_hot_combine): one per key and
+// combining workgroup flush, 40 B.
+struct HRec {
+  unsigned long long kA, kB, mo;
+  uint32_t first, last, cnt, pad;
+};
+static_assert(sizeof(HRec) == 40, "hot record layout");
+
 #ifndef RSA_COUNT_PER_CU
 #define RSA_COUNT_PER_CU 1   // k_count workgroups per CU (one is resident: 104 KiB LDS); fewer workgroups, fewer histogram-flush atomics
 #endif
@@ -1494,7 +1576,8 @@ __device__ __forceinline__ unsigned long long readlane64(unsigned long long v, i
 template <int kPass>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2 ? RSA_RED2_WPE : 4, 8))) void k_reduce(const Rec* __restrict__ recs,
                                                  const unsigned long long* __restrict__ starts, uint32_t n_segs,
-                                                 Agg A) {
+                                                 Agg A, const unsigned long long* __restrict__ hot_base,
+                                                 const uint32_t* __restrict__ hot_fill, const HRec* __restrict__ hot) {
   __shared__ unsigned long long e_kA[kRedE<kPass>], e_kB[kRedE<kPass>], e_mo[kRedE<kPass>];
   __shared__ uint32_t e_first[kRedE<kPass>], e_last[kRedE<kPass>], e_cnt[kRedE<kPass>];
   __shared__ uint32_t occ[1u << (kRegionMaxBits - 5)];     // occupied before this flush
@@ -1504,9 +1587,16 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
   __shared__ unsigned long long sh_base;
   const uint32_t region = blockIdx.x;
   const uint32_t n_regions = 1u << A.np_bits;
+  // a hot region's records were pre-combined by k_hot_combine: read those
+  const bool is_hot = hot_base && hot_base[region] != kEmpty;   // workgroup-uniform
   unsigned long long total_recs = 0;
-  for (uint32_t sg = 0; sg < n_segs; ++sg)
-    total_recs += starts[(size_t)sg * (n_regions + 1) + region + 1] - starts[(size_t)sg * (n_regions + 1) + region];
+  if (is_hot) {
+    total_recs = hot_fill[region];
+    n_segs = 1;
+  } else {
+    for (uint32_t sg = 0; sg < n_segs; ++sg)
+      total_recs += starts[(size_t)sg * (n_regions + 1) + region + 1] - starts[(size_t)sg * (n_regions + 1) + region];
+  }
   if (total_recs == 0) return;   // workgroup-uniform
   const uint32_t rs = 1u << A.rs_bits, words = (rs + 31) / 32;
   const unsigned long long rbase = (unsigned long long)region << A.rs_bits;
@@ -1519,7 +1609,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
   if (threadIdx.x == 0) used = 0;
   __syncthreads();
   uint32_t sg = 0;
-  unsigned long long pos = starts[region], end = starts[region + 1];
+  unsigned long long pos = is_hot ? hot_base[region] : starts[region];
+  unsigned long long end = is_hot ? pos + total_recs : starts[region + 1];
   while (true) {
     while (pos >= end && sg + 1 < n_segs) {   // workgroup-uniform: next segment
       ++sg;
@@ -1534,76 +1625,33 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
       for (unsigned long long jb = 0; jb < take; jb += blockDim.x) {   // workgroup-uniform trip count
         const unsigned long long j = jb + threadIdx.x;
         bool have = j < take;
-        Rec r;
-        if (have) r = recs[pos + j];
-        if (kPass == 2 && have) {
-          const unsigned long long P = A.thresh[r.kB >> 32];
-          if (P == RSA_NO_THRESHOLD || r.order > P) have = false;
-        }
-        uint32_t cnt = 1u, first = r.ts, last = r.ts;
-        unsigned long long mo = r.order;
-        // hot keys: a rule with one distinct connection puts all its records
-        // into one region; lanes sharing the key of one of the wave's first
-        // live lanes are combined with wave reductions and enter the LDS table
-        // as ONE insert (LDS atomics on one address serialise over the lanes)
-        unsigned long long pending = __ballot(have);
-        for (int att = 0; att < kHotTries && pending; ++att) {
-          const int l0 = __builtin_ctzll(pending);
-          const unsigned long long kA0 = readlane64(r.kA, l0), kB0 = readlane64(r.kB, l0);
-          const bool dom = have && r.kA == kA0 && r.kB == kB0;
-          const unsigned long long dm = __ballot(dom);
-          pending &= ~dm;
-          if (__popcll(dm) >= kHotMin) {
-            uint32_t f = dom ? r.ts : 0xFFFFFFFFu, l = dom ? r.ts : 0u;
-            unsigned long long o = dom ? r.order : ~0ull;
-#pragma unroll
-            for (int sh = 32; sh; sh >>= 1) {
-              f = min(f, (uint32_t)__shfl_xor((int)f, sh));
-              l = max(l, (uint32_t)__shfl_xor((int)l, sh));
-              const unsigned long long oo = __shfl_xor(o, sh);
-              o = oo < o ? oo : o;
-            }
-            if (dom) {
-              if ((int)__lane_id() == l0) {
-                cnt = (uint32_t)__popcll(dm);
-                first = f;
-                last = l;
-                mo = o;
-              } else {
-                have = false;
-              }
-            }
+        unsigned long long kA = 0, kB = 0, mo = 0;
+        uint32_t first = 0, last = 0, cnt = 1;
+        if (is_hot) {
+          if (have) {
+            const HRec hr = hot[pos + j];
+            kA = hr.kA;
+            kB = hr.kB;
+            mo = hr.mo;
+            first = hr.first;
+            last = hr.last;
+            cnt = hr.cnt;
+          }
+        } else {
+          if (have) {
+            const Rec r = recs[pos + j];
+            kA = r.kA;
+            kB = r.kB;
+            mo = r.order;
+            first = last = r.ts;
+          }
+          if (kPass == 2 && have) {   // (hot records of pass 2 were filtered when combined)
+            const unsigned long long P = A.thresh[kB >> 32];
+            if (P == RSA_NO_THRESHOLD || mo > P) have = false;
           }
         }
-        if (!have) continue;
-        const uint32_t h = (uint32_t)mix64(r.kA ^ (r.kB * 0x9e3779b97f4a7c15ull));
-        uint32_t e = (kRedE<kPass> & (kRedE<kPass> - 1)) == 0 ? (h & (kRedE<kPass> - 1)) : __umulhi(h, (uint32_t)kRedE<kPass>);
-        while (true) {
-          const unsigned long long cur = __hip_atomic_load(&e_kB[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          if (cur == kEmpty) {
-            if (atomicCAS(&e_kB[e], kEmpty, kBusy) == kEmpty) {
-              e_kA[e] = r.kA;
-              e_mo[e] = mo;
-              e_first[e] = first;
-              e_last[e] = last;
-              e_cnt[e] = cnt;
-              __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-              atomicExch(&e_kB[e], r.kB);
-              atomicAdd(&used, 1u);
-              break;
-            }
-            continue;
-          }
-          if (cur == kBusy) continue;
-          if (cur == r.kB && __hip_atomic_load(&e_kA[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == r.kA) {
-            atomicAdd(&e_cnt[e], cnt);
-            atomicMin(&e_first[e], first);
-            atomicMax(&e_last[e], last);
-            if (kPass == 1) atomicMin(&e_mo[e], mo);
-            break;
-          }
-          e = e + 1 == (uint32_t)kRedE<kPass> ? 0u : e + 1;
-        }
+        lds_agg_insert<kRedE<kPass>, kPass == 1>(e_kA, e_kB, e_mo, e_first, e_last, e_cnt, used, have, kA, kB, mo,
+                                                 first, last, cnt);
       }
       pos += take;
       __syncthreads();
@@ -1749,6 +1797,137 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
   }
   if (kPass == 1)
     for (uint32_t w = threadIdx.x; w < words; w += blockDim.x) gocc[w] = occ[w];
+}
+
+// ---- hot regions (skewed traffic: a few connections on most lines, BASELINE
+// config 5's Zipf population).  Every record of one key lands in one region,
+// and one k_reduce workgroup per region would read a hot region's millions
+// of records alone.  k_hot_plan marks the regions holding more than
+// max(kHotMinRecs, kHotFactor x the mean) records of the segments and deals
+// their ranges out as slices; k_hot_combine (all CUs) aggregates each slice
+// in an LDS table and appends one HRec per key and flush to the region's
+// contiguous area of the hot buffer; k_reduce then merges that instead.  Pass
+// 2 does the same over its filtered records (capped rules, order <= P), so the
+// combined counts stay exact for the recount.
+constexpr uint32_t kHotSlice = 65536, kHotMinRecs = 65536, kHotFactor = 4;
+struct HotTask {
+  unsigned long long beg, end;
+  uint32_t region, pad;
+};
+// ctl[0] tasks planned, ctl[1] task cursor; *hot_total: hot buffer records reserved
+__global__ void k_hot_plan(const unsigned long long* __restrict__ starts, uint32_t n_segs, uint32_t n_regions,
+                           HotTask* __restrict__ tasks, uint32_t max_tasks, uint32_t* __restrict__ ctl,
+                           unsigned long long* __restrict__ hot_total, unsigned long long* __restrict__ hot_base,
+                           uint32_t* __restrict__ hot_fill, unsigned long long min_recs, uint32_t factor) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_regions) return;
+  unsigned long long all = 0, mine = 0;
+  for (uint32_t sg = 0; sg < n_segs; ++sg) {
+    const unsigned long long* st = starts + (size_t)sg * (n_regions + 1);
+    all += st[n_regions] - st[0];
+    mine += st[r + 1] - st[r];
+  }
+  const unsigned long long thr = max(min_recs, factor * (all / n_regions));
+  hot_fill[r] = 0;
+  if (mine <= thr) {
+    hot_base[r] = kEmpty;
+    return;
+  }
+  uint32_t nt = 0;
+  for (uint32_t sg = 0; sg < n_segs; ++sg) {
+    const unsigned long long* st = starts + (size_t)sg * (n_regions + 1);
+    nt += (uint32_t)((st[r + 1] - st[r] + kHotSlice - 1) / kHotSlice);
+  }
+  const uint32_t t0 = atomicAdd(&ctl[0], nt);
+  if (t0 + nt > max_tasks) {   // (cannot happen: max_tasks bounds every plan) leave the region to k_reduce
+    hot_base[r] = kEmpty;
+    return;
+  }
+  hot_base[r] = atomicAdd(hot_total, mine);
+  uint32_t t = t0;
+  for (uint32_t sg = 0; sg < n_segs; ++sg) {
+    const unsigned long long* st = starts + (size_t)sg * (n_regions + 1);
+    for (unsigned long long b = st[r]; b < st[r + 1]; b += kHotSlice)
+      tasks[t++] = HotTask{b, min(b + kHotSlice, st[r + 1]), r, 0u};
+  }
+}
+
+// Persistent grid: every workgroup takes slices until none is left (the
+// count planned is read on the device); per slice an LDS table, flushed when
+// it could overflow and at the slice end, one device atomic per flush.
+template <int kPass>
+__global__ __launch_bounds__(1024) void k_hot_combine(const Rec* __restrict__ recs, const HotTask* __restrict__ tasks,
+                                                      uint32_t* __restrict__ ctl, Agg A,
+                                                      const unsigned long long* __restrict__ hot_base,
+                                                      uint32_t* __restrict__ hot_fill, HRec* __restrict__ hot) {
+  constexpr int kE = RSA_RED1;
+  __shared__ unsigned long long e_kA[kE], e_kB[kE], e_mo[kE];
+  __shared__ uint32_t e_first[kE], e_last[kE], e_cnt[kE];
+  __shared__ uint32_t used, task;
+  __shared__ uint32_t sh[18];
+  __shared__ unsigned long long sh_base;
+  for (uint32_t e = threadIdx.x; e < (uint32_t)kE; e += blockDim.x) e_kB[e] = kEmpty;
+  if (threadIdx.x == 0) used = 0;
+  const uint32_t n_tasks = ctl[0];
+  while (true) {
+    __syncthreads();
+    if (threadIdx.x == 0) task = atomicAdd(&ctl[1], 1u);
+    __syncthreads();
+    const uint32_t t = task;
+    if (t >= n_tasks) break;   // workgroup-uniform: every workgroup drains here
+    const HotTask T = tasks[t];
+    unsigned long long pos = T.beg;
+    while (pos < T.end || used > 0) {   // workgroup-uniform (read after a barrier)
+      if (pos < T.end) {
+        const uint32_t room = (3u * kE) / 4 - used;
+        const unsigned long long take = T.end - pos < room ? T.end - pos : room;
+        __syncthreads();   // every thread has read `used` before any insert changes it
+        for (unsigned long long jb = 0; jb < take; jb += blockDim.x) {
+          const unsigned long long j = jb + threadIdx.x;
+          bool have = j < take;
+          Rec r;
+          if (have) r = recs[pos + j];
+          if (kPass == 2 && have) {
+            const unsigned long long P = A.thresh[r.kB >> 32];
+            if (P == RSA_NO_THRESHOLD || r.order > P) have = false;
+          }
+          lds_agg_insert<kE, kPass == 1>(e_kA, e_kB, e_mo, e_first, e_last, e_cnt, used, have, r.kA, r.kB, r.order,
+                                         r.ts, r.ts, 1u);
+        }
+        pos += take;
+        __syncthreads();
+        if (pos < T.end && used + 1024u <= (3u * kE) / 4) continue;   // room for more of this slice
+      }
+      // flush: the table's entries to the region's hot area
+      constexpr int kPer = kE / 1024;
+      uint32_t n_mine = 0;
+#pragma unroll
+      for (int q = 0; q < kPer; ++q) n_mine += e_kB[threadIdx.x + q * 1024] != kEmpty ? 1u : 0u;
+      uint32_t total;
+      const uint32_t off = block_exscan(n_mine, sh, &total);
+      if (threadIdx.x == 0) sh_base = total ? hot_base[T.region] + atomicAdd(&hot_fill[T.region], total) : 0ull;
+      __syncthreads();
+      unsigned long long at = sh_base + off;
+#pragma unroll
+      for (int q = 0; q < kPer; ++q) {
+        const uint32_t e = threadIdx.x + q * 1024;
+        if (e_kB[e] == kEmpty) continue;
+        HRec h;
+        h.kA = e_kA[e];
+        h.kB = e_kB[e];
+        h.mo = e_mo[e];
+        h.first = e_first[e];
+        h.last = e_last[e];
+        h.cnt = e_cnt[e];
+        h.pad = 0;
+        hot[at++] = h;
+        e_kB[e] = kEmpty;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) used = 0;
+      __syncthreads();
+    }
+  }
 }
 
 // Segment starts of one pass-1 launch: starts[r] = base + offs[r * n_tiles],
@@ -2262,6 +2441,18 @@ struct rsa_ctx {
   unsigned long long* d_filter = nullptr;
   uint32_t filter_len = 0;
   unsigned long long* d_packed = nullptr;   // k_count / k_aggregate packed counters (rules > kCnt)
+  // hot-region split (k_hot_plan / k_hot_combine)
+  bool hot_split = true;                    // RSA_OPT_HOT_SPLIT
+  unsigned long long hot_min = kHotMinRecs; // RSA_OPT_HOT_MIN: a hot region holds more than max(hot_min,
+  uint32_t hot_factor = kHotFactor;         //   hot_factor x the mean region) records
+  void* d_hot = nullptr;                    // HRec[hot_alloc]
+  size_t hot_alloc = 0;
+  void* d_hot_tasks = nullptr;              // HotTask[tasks_alloc]
+  size_t tasks_alloc = 0;
+  unsigned long long* d_hot_base = nullptr; // [kMaxRegions]
+  uint32_t* d_hot_fill = nullptr;           // [kMaxRegions]
+  uint32_t* d_hot_ctl = nullptr;            // [4]: tasks planned, task cursor
+  unsigned long long* d_hot_total = nullptr;
   bool auto_tighten = true;
   bool tightened = false;
   uint32_t profile_skip = 0;
@@ -2604,6 +2795,56 @@ int exclusive_scan(rsa_ctx* c, uint32_t* d, unsigned long long n, uint32_t** tot
   return RSA_OK;
 }
 
+// The hot-region split for the records of segments [seg0, seg0 + n_segs) of
+// d_starts (at most `records` records): plan, combine; returns the hot
+// descriptors for k_reduce in *base / *fill / *hot (nullptr: split off).
+template <int kPass>
+int hot_split(rsa_ctx* c, uint32_t seg0, uint32_t n_segs, unsigned long long records,
+              const unsigned long long** base, const uint32_t** fill, const HRec** hot) {
+  *base = nullptr;
+  *fill = nullptr;
+  *hot = nullptr;
+  if (!c->hot_split || records == 0) return RSA_OK;
+  const uint32_t n_regions = 1u << c->np_bits;
+  if (!c->d_hot_base) {
+    HIPCHK(c, hipMalloc(&c->d_hot_base, kMaxRegions * sizeof(unsigned long long)));
+    HIPCHK(c, hipMalloc(&c->d_hot_fill, kMaxRegions * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(&c->d_hot_ctl, 4 * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(&c->d_hot_total, sizeof(unsigned long long)));
+  }
+  const size_t max_tasks = records / kHotSlice + (size_t)n_segs * n_regions + 1;
+  if (max_tasks > c->tasks_alloc || records > c->hot_alloc) HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (max_tasks > c->tasks_alloc) {
+    hipFree(c->d_hot_tasks);
+    c->d_hot_tasks = nullptr;
+    c->tasks_alloc = 0;
+    HIPCHK(c, hipMalloc(&c->d_hot_tasks, max_tasks * sizeof(HotTask)));
+    c->tasks_alloc = max_tasks;
+  }
+  if (records > c->hot_alloc) {
+    hipFree(c->d_hot);
+    c->d_hot = nullptr;
+    c->hot_alloc = 0;
+    HIPCHK(c, hipMalloc(&c->d_hot, records * sizeof(HRec)));
+    c->hot_alloc = records;
+  }
+  HIPCHK(c, hipMemsetAsync(c->d_hot_ctl, 0, 4 * sizeof(uint32_t), c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_hot_total, 0, sizeof(unsigned long long), c->stream));
+  HotTask* tasks = static_cast<HotTask*>(c->d_hot_tasks);
+  k_hot_plan<<<(n_regions + 255) / 256, 256, 0, c->stream>>>(c->d_starts + (size_t)seg0 * (n_regions + 1), n_segs,
+                                                             n_regions, tasks, (uint32_t)max_tasks, c->d_hot_ctl,
+                                                             c->d_hot_total, c->d_hot_base, c->d_hot_fill, c->hot_min,
+                                                             c->hot_factor);
+  k_hot_combine<kPass><<<c->cu_count, 1024, 0, c->stream>>>(reinterpret_cast<const Rec*>(c->d_recs2), tasks,
+                                                             c->d_hot_ctl, agg_of(c), c->d_hot_base, c->d_hot_fill,
+                                                             static_cast<HRec*>(c->d_hot));
+  HIPCHK(c, hipGetLastError());
+  *base = c->d_hot_base;
+  *fill = c->d_hot_fill;
+  *hot = static_cast<const HRec*>(c->d_hot);
+  return RSA_OK;
+}
+
 // Window-compacted record buffers of a pass-1 launch over m lines.
 int prepare_records(rsa_ctx* c, uint64_t m) {
   const uint64_t mw = (m + kWin - 1) / kWin * kWin;
@@ -2680,7 +2921,12 @@ int launch_aggregate(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsig
   HIPCHK(c, hipGetLastError());
   unsigned long long* st = c->d_starts + (size_t)c->n_segs * (n_regions + 1);
   k_seg_starts<<<(n_regions + 1 + 255) / 256, 256, 0, c->stream>>>(c->d_hist, n_tiles, n_regions, seg_base, total, st);
-  k_reduce<1><<<n_regions, 1024, 0, c->stream>>>(reinterpret_cast<const Rec*>(c->d_recs2), st, 1, ag);
+  const unsigned long long* hb = nullptr;
+  const uint32_t* hf = nullptr;
+  const HRec* hr = nullptr;
+  rc = hot_split<1>(c, c->n_segs, 1, m, &hb, &hf, &hr);
+  if (rc) return rc;
+  k_reduce<1><<<n_regions, 1024, 0, c->stream>>>(reinterpret_cast<const Rec*>(c->d_recs2), st, 1, ag, hb, hf, hr);
   HIPCHK(c, hipGetLastError());
   if (c->rec_cache) ++c->n_segs;
   if (c->debug) {
@@ -2827,7 +3073,8 @@ int rsa_ctx_destroy(rsa_ctx* c) {
   void* bufs[] = {c->d_tail, c->d_tail_n, c->d_gscratch, c->d_gh, c->d_stats, c->d_recs, c->d_recs2, c->d_regs, c->d_wcnt, c->d_nrecs, c->d_starts, c->d_hist,
                   c->d_scan_sums, c->d_occ, c->d_entries, c->d_off,
                   c->d_img, c->d_resid,
-                  c->d_slots, c->d_used, c->d_used_n, c->d_filter, c->d_packed, c->d_flags, c->d_cursor, c->d_cidx,
+                  c->d_slots, c->d_used, c->d_used_n, c->d_filter, c->d_packed, c->d_hot, c->d_hot_tasks, c->d_hot_base,
+                  c->d_hot_fill, c->d_hot_ctl, c->d_hot_total, c->d_flags, c->d_cursor, c->d_cidx,
                   c->d_capped_gid, c->d_capped_cnt, c->d_capped_start, c->d_keys};
   for (void* b : bufs) (void)hipFree(b);
   for (int k = 0; k < kMaxEvents; ++k)
@@ -2875,6 +3122,14 @@ int rsa_set_option(rsa_ctx* c, int option, int64_t value) {
       return RSA_OK;
     case RSA_OPT_PRECHECK:
       c->precheck = value != 0;
+      return RSA_OK;
+    case RSA_OPT_HOT_SPLIT:
+      c->hot_split = value != 0;
+      return RSA_OK;
+    case RSA_OPT_HOT_MIN:
+      if (value < 1) return fail(c, RSA_ERR_ARG, "hot-region minimum must be >= 1 record");
+      c->hot_min = (unsigned long long)value;
+      c->hot_factor = value < (int64_t)kHotMinRecs ? 0u : kHotFactor;   // testing: any region above the minimum
       return RSA_OK;
     case RSA_OPT_STATS:
       if (value && !c->d_stats) {
@@ -3262,8 +3517,13 @@ int rsa_recount(rsa_ctx* c, const rsa_tuple* T, const uint32_t* TS, const uint64
   if (c->rec_cache && c->cache_T == (const void*)T && c->cache_n == n && c->n_segs > 0) {
     // every occurrence with order <= P of a capped rule produced a pass-1
     // record (P <= the filter bound in force when its line was aggregated)
+    const unsigned long long* hb = nullptr;
+    const uint32_t* hf = nullptr;
+    const HRec* hr = nullptr;
+    int rc2 = hot_split<2>(c, 0, c->n_segs, n, &hb, &hf, &hr);
+    if (rc2) return rc2;
     k_reduce<2><<<1u << c->np_bits, 1024, 0, c->stream>>>(reinterpret_cast<const Rec*>(c->d_recs2), c->d_starts,
-                                                         c->n_segs, agg_of(c));
+                                                         c->n_segs, agg_of(c), hb, hf, hr);
     HIPCHK(c, hipGetLastError());
     return RSA_OK;
   }

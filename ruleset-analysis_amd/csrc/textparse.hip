@@ -275,6 +275,42 @@ __global__ void k_keys0(const uint8_t* __restrict__ text, const uint64_t* __rest
   ids[j] = j;
 }
 
+// Grouped order keys, round -1: per line its length, its group as a 32-bit
+// sort key (a negative group -- a line no rank is asked for -- sorts last as
+// 0xFFFFFFFF) and its id.
+__global__ void k_grp0(const int32_t* __restrict__ group, const uint8_t* __restrict__ text,
+                       const uint64_t* __restrict__ off, uint32_t n, uint32_t* __restrict__ lens,
+                       uint32_t* __restrict__ keys, uint32_t* __restrict__ ids) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint64_t a = off[j], b = off[j + 1];
+  uint64_t len = b - a;
+  if (len && text[b - 1] == '\n') --len;
+  lens[j] = len < 0xFFFFFFFFull ? (uint32_t)len : 0xFFFFFFFFu;
+  const int32_t g = group[j];
+  keys[j] = g < 0 ? 0xFFFFFFFFu : (uint32_t)g;
+  ids[j] = j;
+}
+
+// after the sort by group: group starts (+1, max-scanned by the caller)
+__global__ void k_grp_bounds(const uint32_t* __restrict__ keys, uint32_t m, uint32_t* __restrict__ bstart) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  bstart[j] = (j == 0 || keys[j] != keys[j - 1]) ? j + 1 : 0u;
+}
+
+// a line alone in its group, or without a group, is settled at its position
+__global__ void k_grp_settle(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ ids,
+                             const uint32_t* __restrict__ first, uint32_t m, uint64_t base, uint64_t* __restrict__ order,
+                             uint32_t* __restrict__ keep) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const bool last_in_group = j + 1 == m || keys[j + 1] != keys[j];
+  const bool settled = keys[j] == 0xFFFFFFFFu || (first[j] == j + 1 && last_in_group);
+  if (settled) order[ids[j]] = base + j;
+  keep[j] = settled ? 0u : 1u;
+}
+
 struct Act {               // an unsettled line: its id and the position its group starts at
   uint32_t id, gs;
 };
@@ -496,6 +532,11 @@ int rsa_parse_reduce(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_off, u
 
 int rsa_order_keys(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_off, uint64_t n_lines, uint64_t base,
                    uint64_t* d_order) {
+  return rsa_order_keys_grouped(c, d_text, d_off, n_lines, nullptr, base, d_order);
+}
+
+int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_off, uint64_t n_lines,
+                           const int32_t* d_group, uint64_t base, uint64_t* d_order) {
   if (!c || (n_lines && (!d_text || !d_off || !d_order))) return RSA_ERR_ARG;
   if (n_lines >= 0x7FFFFFFFull) return rsa_internal_fail(c, RSA_ERR_ARG, "rsa_order_keys: too many lines");
   if (reinterpret_cast<uintptr_t>(d_text) & 3u)
@@ -548,19 +589,37 @@ int rsa_order_keys(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_off, uin
   uint32_t* idsA = reinterpret_cast<uint32_t*>(valsA);   // round 0 reuses the value arrays as u32 ids
   uint32_t* idsB = reinterpret_cast<uint32_t*>(valsB);
 
-  // round 0: all lines
   uint64_t n_bytes = 0;
   TPCHK(c, hipMemcpyAsync(&n_bytes, d_off + n, 8, hipMemcpyDeviceToHost, st));
   TPCHK(c, hipStreamSynchronize(st));
-  hipLaunchKernelGGL(k_keys0, dim3(blocks(n, 256)), dim3(256), 0, st, d_text, d_off, n, n_bytes, lens, keysA, idsA);
   size_t tt = tmp;
-  TPCHK(c, rocprim::radix_sort_pairs(t, tt, keysA, keysB, idsA, idsB, (size_t)n, 0, 64, st));
-  hipLaunchKernelGGL(k_bounds, dim3(blocks(n, 256)), dim3(256), 0, st, keysB, (const uint32_t*)nullptr,
-                     (const uint32_t*)nullptr, n, pos, bstart);
-  tt = tmp;
-  TPCHK(c, rocprim::inclusive_scan(t, tt, bstart, first, (size_t)n, rocprim::maximum<uint32_t>(), st));
-  hipLaunchKernelGGL(k_settle, dim3(blocks(n, 256)), dim3(256), 0, st, keysB, (const uint32_t*)nullptr, idsB, pos,
-                     first, n, base, d_order, keep);
+  uint32_t round0 = 1;
+  if (d_group) {
+    // grouped: ranks of (group, line bytes); the groups come first (one sort of
+    // 32-bit keys), so only lines of one group are ever compared (the reducer
+    // compares order keys of one rule's lines only), and a group of one line
+    // is settled at once.  Then the byte rounds from round 0.
+    uint32_t* gkA = reinterpret_cast<uint32_t*>(keysA);
+    uint32_t* gkB = reinterpret_cast<uint32_t*>(keysB);
+    hipLaunchKernelGGL(k_grp0, dim3(blocks(n, 256)), dim3(256), 0, st, d_group, d_text, d_off, n, lens, gkA, idsA);
+    TPCHK(c, rocprim::radix_sort_pairs(t, tt, gkA, gkB, idsA, idsB, (size_t)n, 0, 32, st));
+    hipLaunchKernelGGL(k_grp_bounds, dim3(blocks(n, 256)), dim3(256), 0, st, gkB, n, bstart);
+    tt = tmp;
+    TPCHK(c, rocprim::inclusive_scan(t, tt, bstart, first, (size_t)n, rocprim::maximum<uint32_t>(), st));
+    hipLaunchKernelGGL(k_grp_settle, dim3(blocks(n, 256)), dim3(256), 0, st, gkB, idsB, first, n, base, d_order,
+                       keep);
+    round0 = 0;
+  } else {
+    // round 0: all lines
+    hipLaunchKernelGGL(k_keys0, dim3(blocks(n, 256)), dim3(256), 0, st, d_text, d_off, n, n_bytes, lens, keysA, idsA);
+    TPCHK(c, rocprim::radix_sort_pairs(t, tt, keysA, keysB, idsA, idsB, (size_t)n, 0, 64, st));
+    hipLaunchKernelGGL(k_bounds, dim3(blocks(n, 256)), dim3(256), 0, st, keysB, (const uint32_t*)nullptr,
+                       (const uint32_t*)nullptr, n, pos, bstart);
+    tt = tmp;
+    TPCHK(c, rocprim::inclusive_scan(t, tt, bstart, first, (size_t)n, rocprim::maximum<uint32_t>(), st));
+    hipLaunchKernelGGL(k_settle, dim3(blocks(n, 256)), dim3(256), 0, st, keysB, (const uint32_t*)nullptr, idsB, pos,
+                       first, n, base, d_order, keep);
+  }
   tt = tmp;
   TPCHK(c, rocprim::exclusive_scan(t, tt, keep, slot, 0u, (size_t)n, rocprim::plus<uint32_t>(), st));
   hipLaunchKernelGGL(k_compact, dim3(blocks(n, 256)), dim3(256), 0, st, idsB, first, keep, slot, n, act);
@@ -570,7 +629,7 @@ int rsa_order_keys(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_off, uin
   TPCHK(c, hipStreamSynchronize(st));
   m += lastk;
   uint32_t* live = reinterpret_cast<uint32_t*>(act2);   // act2 is spare: one flag word
-  for (uint32_t round = 1; m > 0; ++round) {
+  for (uint32_t round = round0; m > 0; ++round) {
     hipLaunchKernelGGL(k_keys, dim3(blocks(m, 256)), dim3(256), 0, st, d_text, d_off, lens, n_bytes, act, m, round,
                        keysA, valsA);
     // rounds inside a shared prefix (e.g. lines of one second share ~90 bytes)

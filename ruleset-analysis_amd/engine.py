@@ -47,7 +47,7 @@ class DeviceBatch(object):
         self.ts = ts            # int32 [n]  (uint32 codes)
         self.order = order      # int64 [n]  (uint64 keys)
         self.gids = gids        # int32 [n] or None
-        self.n = int(ts.numel())
+        self.n = int(ts.numel()) if ts is not None else int(tuples.shape[0])
 
     @classmethod
     def from_numpy(cls, tuples, ts, order, device, gids=None):

@@ -37,6 +37,7 @@ RSA_OPT_STATS = 10
 RSA_OPT_WAVE_CAP_SCATTER = 11
 RSA_OPT_GROUP_TASKS = 12
 RSA_OPT_PROFILE_CLASSIFY = 13
+RSA_OPT_HOT_SPLIT, RSA_OPT_HOT_MIN = 14, 15
 
 P = ctypes.c_void_p
 U32 = ctypes.c_uint32
@@ -76,6 +77,7 @@ SYMBOLS = {
     'rsa_text_line_offsets': (I32, [P, P, U64, P, U64]),
     'rsa_parse_text': (I32, [P, P, P, U64, P, U32, P, U32, P, P, P]),
     'rsa_order_keys': (I32, [P, P, P, U64, U64, P]),
+    'rsa_order_keys_grouped': (I32, [P, P, P, U64, P, U64, P]),
     'rsa_parse_reduce': (I32, [P, P, P, U64, P, U32, P, P, P]),
     'rsa_sync': (I32, [P]),
 }

@@ -73,35 +73,42 @@ def analyze(inputs, db, cap=1000, device=0, engine=None):
 
 def analyze_text(inputs, db, cap=1000, device=0, engine=None):
     """The fused job from raw log bytes: inputs = iterable of (host, bytes).
-    The text is parsed on the GPU (textparse); returns (report lines, results)."""
+    The text is parsed on the GPU (textparse), the lines classified, then
+    ranked for the reducer's order: by their bytes within each rule (grouped
+    order keys over all inputs together, as ``cat f1 f2 | mapper | sort`` orders
+    a key's lines across files -- the reducer only ever compares one rule's
+    lines), and aggregated with their gids; returns (report lines, results)."""
     from . import textparse
     compiled = CompiledRules(db)
     compiled.ensure_lists()
     eng = engine if engine is not None else Engine(device)
-    inputs = list(inputs)
-    single = len(inputs) == 1
+    torch = eng.torch
     parts, pspell = [], {}
     for host, data in inputs:
-        # one input: its order keys come with the parse; several: ranked together
-        # below, as ``cat f1 f2 | mapper | sort`` orders a key's lines across files
-        p = textparse.parse_text(eng, host, data, db, compiled, pspell=pspell, need_order=single,
-                                 keep_text=not single)
+        p = textparse.parse_text(eng, host, data, db, compiled, pspell=pspell, need_order=False, keep_text=True)
         parts.append(p)
         if p.error is not None:
             break
-    if not single:
-        textparse.order_keys_global(eng, parts)
-    parsed = textparse.concat(parts, eng.torch)
-    if parsed.error is not None:
+    if any(p.error is not None for p in parts):
+        for p in parts:
+            p._d_text = p._d_off = None
+        parsed = textparse.concat(parts, torch)
         raise parsed.error[1]
     eng.load_compiled(compiled)
-    if parsed.n == 0:
+    n = sum(p.n for p in parts)
+    if n == 0:
+        for p in parts:
+            p._d_text = p._d_off = None
+        parsed = textparse.concat(parts, torch)
         results = eng.run([], cap, capacity=1)
         return assemble_report(parsed, np.zeros(0, np.int32), results, compiled, cap), results
-    batch = parsed.batch()
-    flags = (batch.tuples[:, 3] >> 16) & 0xFF
+    tuples = torch.cat([p.tuples for p in parts if p.n])
+    gids = eng.classify_only(DeviceBatch(tuples, None, None))
+    flags = (tuples[:, 3] >> 16) & 0xFF
     both = F_HIT | F_BUILT
-    n_hb = int(((flags & both) == both).sum().item())
-    results = eng.run([batch], cap, capacity=max(n_hb, 1))
-    gids = eng.last_gids[0].cpu().numpy()
-    return assemble_report(parsed, gids, results, compiled, cap), results
+    hb = (flags & both) == both
+    textparse.order_keys_global(eng, parts, group=torch.where(hb & (gids >= 0), gids, torch.full_like(gids, -1)))
+    parsed = textparse.concat(parts, torch)
+    batch = DeviceBatch(parsed.tuples, parsed.ts, parsed.order, gids)
+    results = eng.run([batch], cap, capacity=max(int(hb.sum().item()), 1))
+    return assemble_report(parsed, gids.cpu().numpy(), results, compiled, cap), results

@@ -304,14 +304,18 @@ def parse_text(engine, host, data, db, compiled, pspell=None, order_base=0, need
     return P
 
 
-def order_keys_global(engine, parts):
+def order_keys_global(engine, parts, group=None):
     """Order keys of all lines of several inputs ranked together: the
     reference's ``cat f1 f2 ... | mapper | LC_ALL=C sort`` (or Hadoop's shuffle
     sort over every split, ``runAnalysis.sh:42-56``) orders a key group's lines
     by their bytes across all inputs, and the cap freeze follows that order
     (``connlist-reducer.py:151``).  ``parts``: ParsedText from ``parse_text(...,
     keep_text=True)``; each part's ``order`` is replaced by its lines' global
-    ranks (lines past a part's error are left out), the device text released."""
+    ranks (lines past a part's error are left out), the device text released.
+    ``group`` (int32 tensor over the parts' lines, in order): rank within
+    groups (``rsa_order_keys_grouped``) -- with each line's rule as its group
+    (-1: a line the reducer never orders) the keys are what the reducer
+    compares, and lines of different rules are never compared."""
     torch = engine.torch
     live = [p for p in parts if p.n and p._d_text is not None]
     if live:
@@ -327,7 +331,13 @@ def order_keys_global(engine, parts):
         total = int(off.numel()) - 1
         order = torch.empty(total, dtype=torch.int64, device=dev)
         v = lambda t: ctypes.c_void_p(t.data_ptr())
-        engine.ctx.call('rsa_order_keys', v(text), v(off), ctypes.c_uint64(total), ctypes.c_uint64(0), v(order))
+        if group is None:
+            engine.ctx.call('rsa_order_keys', v(text), v(off), ctypes.c_uint64(total), ctypes.c_uint64(0), v(order))
+        else:
+            g = group.to(torch.int32).contiguous()
+            assert g.numel() == total
+            engine.ctx.call('rsa_order_keys_grouped', v(text), v(off), ctypes.c_uint64(total), v(g),
+                            ctypes.c_uint64(0), v(order))
         a = 0
         for p in live:
             p.order = order[a:a + p.n]

@@ -14,7 +14,7 @@ import pytest
 from conftest import golden_cases
 from golden_io import load_case, split_lines
 from oracle import coracle
-from ruleset_analysis_amd import acldb, synth
+from ruleset_analysis_amd import acldb, native, synth
 from ruleset_analysis_amd.compile import CompiledRules
 from ruleset_analysis_amd.engine import DeviceBatch
 from ruleset_analysis_amd.logparse import parse_logs
@@ -297,3 +297,28 @@ def test_cfg5_population_zipf_10m_lines(engine, shuffle):
                               interfaces=('outside', 'partner', 'vpn', 'extranet'), broad=False, shuffle=shuffle)
     assert (ref['n_conns'] >= 1000).sum() > 20
     assert int(ref['rows']['count'].max()) > 10000      # one connection seen many times
+
+
+@pytest.mark.parametrize('n_lines,cap,shuffle', [(600_000, 1000, False), (600_000, 20, True), (5_000_000, 40, False)])
+def test_hot_split_every_region(engine, n_lines, cap, shuffle):
+    """Every region holding a record takes the hot-region path
+    (RSA_OPT_HOT_MIN=1): its segment is cut into slices pre-combined on all
+    CUs (k_hot_combine), pass 1 and the pass-2 recount, then merged by its
+    k_reduce workgroup -- per-rule results equal the C oracle's; the 5M-line
+    case runs the filter slices (four segments per region in pass 2)."""
+    engine.set_option(native.RSA_OPT_HOT_MIN, 1)
+    try:
+        _gpu_vs_oracle(engine, 800, n_lines, cap, seed=21, zipf=1.1, population=10 ** 6, shuffle=shuffle)
+    finally:
+        engine.set_option(native.RSA_OPT_HOT_MIN, 65536)
+
+
+def test_hot_split_off_equals_on(engine):
+    """The skewed 10M-line shape with the hot split off (one workgroup reads a
+    hot region alone) gives the same records as with it on."""
+    engine.set_option(native.RSA_OPT_HOT_SPLIT, 0)
+    try:
+        _gpu_vs_oracle(engine, 2500, 3_000_000, 1000, seed=5, zipf=1.1, population=10 ** 8,
+                       interfaces=('outside', 'partner'), broad=False)
+    finally:
+        engine.set_option(native.RSA_OPT_HOT_SPLIT, 1)

@@ -354,6 +354,19 @@ def test_gpu_order_keys_adversarial(engine):
     want = np.empty(len(lines), np.int64)
     want[np.array(perm)] = np.arange(len(lines)) + 77
     assert np.array_equal(order.cpu().numpy(), want)
+    # grouped: ranks of (group, bytes) among the lines with a group (few
+    # groups, many, singletons), the others ranked after them
+    for n_groups in (1, 7, 5000):
+        grp = np.array([rng.randrange(-1, n_groups) for _ in lines], np.int32)
+        g = torch.from_numpy(grp).to(dev)
+        engine.ctx.call('rsa_order_keys_grouped', v(text), v(off), ctypes.c_uint64(len(lines)), v(g),
+                        ctypes.c_uint64(5), v(order))
+        got = order.cpu().numpy()
+        idx = [i for i in range(len(lines)) if grp[i] >= 0]
+        perm = sorted(idx, key=lambda i: (int(grp[i]), lines[i]))
+        assert np.array_equal(got[np.array(perm)], np.arange(len(perm)) + 5)
+        rest = got[grp < 0]
+        assert len(set(rest.tolist())) == len(rest) and (rest >= 5 + len(perm)).all()
 
 
 @pytest.mark.gpu
