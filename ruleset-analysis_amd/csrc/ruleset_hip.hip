@@ -2442,6 +2442,7 @@ struct rsa_ctx {
   uint32_t filter_len = 0;
   unsigned long long* d_packed = nullptr;   // k_count / k_aggregate packed counters (rules > kCnt)
   // hot-region split (k_hot_plan / k_hot_combine)
+  int parse_mode = 0;                       // RSA_OPT_PARSE_MODE (textparse.hip)
   bool hot_split = true;                    // RSA_OPT_HOT_SPLIT
   unsigned long long hot_min = kHotMinRecs; // RSA_OPT_HOT_MIN: a hot region holds more than max(hot_min,
   uint32_t hot_factor = kHotFactor;         //   hot_factor x the mean region) records
@@ -3123,6 +3124,10 @@ int rsa_set_option(rsa_ctx* c, int option, int64_t value) {
     case RSA_OPT_PRECHECK:
       c->precheck = value != 0;
       return RSA_OK;
+    case RSA_OPT_PARSE_MODE:
+      if (value < 0 || value > 1) return fail(c, RSA_ERR_ARG, "parse mode must be 0 (LDS staged) or 1 (direct)");
+      c->parse_mode = (int)value;
+      return RSA_OK;
     case RSA_OPT_HOT_SPLIT:
       c->hot_split = value != 0;
       return RSA_OK;
@@ -3149,6 +3154,7 @@ int rsa_set_option(rsa_ctx* c, int option, int64_t value) {
 
 hipStream_t rsa_internal_stream(rsa_ctx* c) { return c->stream; }
 int rsa_internal_fail(rsa_ctx* c, int code, const char* msg) { return fail(c, code, "%s", msg); }
+int rsa_internal_parse_mode(rsa_ctx* c) { return c->parse_mode; }
 
 int rsa_sync(rsa_ctx* c) {
   if (!c) return RSA_ERR_ARG;

@@ -154,16 +154,47 @@ constexpr uint32_t kParseWG = 128, kStageBytes = 32768;
 
 // kReduce: the reducer drop-in's lines (rsa_text::reduce_line, plus the
 // same-key flag against the previous line of the batch).
-template <bool kReduce>
+// kDirect: no staging, every lane reads its line from HBM through 4-byte
+// loads (no LDS: occupancy bound by registers only).
+template <bool kReduce, bool kDirect>
 __global__ __launch_bounds__(kParseWG) void k_parse(const uint8_t* __restrict__ text, const uint64_t* __restrict__ off,
                                                     uint64_t n_lines, const rsa_parse_ifc* __restrict__ ifcs,
                                                     uint32_t n_ifcs, const rsa_parse_spell* __restrict__ spells,
                                                     uint32_t n_spells, rsa_tuple* __restrict__ tuples,
                                                     uint32_t* __restrict__ ts_out, uint32_t* __restrict__ disp) {
-  __shared__ uint32_t sm[kStageBytes / 4];
+  __shared__ uint32_t sm[kDirect ? 1 : kStageBytes / 4];
   const uint64_t l0 = (uint64_t)blockIdx.x * kParseWG;
   const uint64_t l1 = l0 + kParseWG < n_lines ? l0 + kParseWG : n_lines;
   const uint64_t n_bytes = off[n_lines];
+  if (kDirect) {
+    const uint64_t i = l0 + threadIdx.x;
+    if (i >= l1) return;
+    const uint64_t a = off[i], b = off[i + 1];
+    uint64_t len = b - a;
+    if (len && text[b - 1] == '\n') --len;
+    rsa_tuple tup = {0u, 0u, 0, 0, 0, 0, 0};
+    uint32_t ts = 0, d = kReduce ? (uint32_t)RSA_LINE_HOST : (uint32_t)RSA_LINE_HOST;
+    if (len < 0xFFFFFFFFull) {
+      const rsa_text::GWordLn s{reinterpret_cast<const uint32_t*>(text), text, a, n_bytes, (uint32_t)len, ~0ull, 0u};
+      if (kReduce) {
+        rsa_text::reduce_line(s, spells, n_spells, tup, ts, d);
+        if (i > 0 && d != RSA_RED_NOISE) {
+          const uint64_t pa = off[i - 1];
+          uint64_t plen = a - pa;
+          if (plen && text[a - 1] == '\n') --plen;
+          const rsa_text::GWordLn q{reinterpret_cast<const uint32_t*>(text), text, pa, n_bytes, (uint32_t)plen, ~0ull,
+                                    0u};
+          if (plen < 0xFFFFFFFFull && rsa_text::same_key(s, q)) d |= RSA_RED_SAME_KEY;
+        }
+      } else {
+        rsa_text::parse_line(s, ifcs, n_ifcs, spells, n_spells, tup, ts, d);
+      }
+    }
+    tuples[i] = tup;
+    ts_out[i] = ts;
+    disp[i] = d;
+    return;
+  }
   const uint64_t base = off[l0] & ~3ull, span = off[l1] - base;
   const bool staged = span <= kStageBytes;   // workgroup-uniform
   if (staged) {
@@ -498,8 +529,12 @@ int rsa_parse_text(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_off, uin
     return rsa_internal_fail(c, RSA_ERR_ARG, "rsa_parse_text: d_text must be 4-byte aligned");
   const uint64_t nb = (n_lines + kParseWG - 1) / kParseWG;
   if (nb > 0x7FFFFFFFull) return rsa_internal_fail(c, RSA_ERR_ARG, "too many lines");
-  hipLaunchKernelGGL(k_parse<false>, dim3((uint32_t)nb), dim3(kParseWG), 0, st, d_text, d_off, n_lines, d_ifcs, n_ifcs, d_spells,
-                     n_spells, d_tuples, d_ts, d_disp);
+  if (rsa_internal_parse_mode(c) == 1)
+    hipLaunchKernelGGL((k_parse<false, true>), dim3((uint32_t)nb), dim3(kParseWG), 0, st, d_text, d_off, n_lines, d_ifcs,
+                       n_ifcs, d_spells, n_spells, d_tuples, d_ts, d_disp);
+  else
+    hipLaunchKernelGGL((k_parse<false, false>), dim3((uint32_t)nb), dim3(kParseWG), 0, st, d_text, d_off, n_lines, d_ifcs,
+                       n_ifcs, d_spells, n_spells, d_tuples, d_ts, d_disp);
   TPCHK(c, hipGetLastError());
   return RSA_OK;
 }
@@ -524,8 +559,12 @@ int rsa_parse_reduce(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_off, u
   rsa_parse_spell* d_spells = static_cast<rsa_parse_spell*>(S.base);
   if (sb) TPCHK(c, hipMemcpyAsync(d_spells, h_spells, sb, hipMemcpyHostToDevice, st));
   TPCHK(c, hipStreamSynchronize(st));   // the host table may go away after return
-  hipLaunchKernelGGL(k_parse<true>, dim3((uint32_t)nb), dim3(kParseWG), 0, st, d_text, d_off, n_lines, nullptr, 0u,
-                     d_spells, n_spells, d_tuples, d_ts, d_disp);
+  if (rsa_internal_parse_mode(c) == 1)
+    hipLaunchKernelGGL((k_parse<true, true>), dim3((uint32_t)nb), dim3(kParseWG), 0, st, d_text, d_off, n_lines, nullptr,
+                       0u, d_spells, n_spells, d_tuples, d_ts, d_disp);
+  else
+    hipLaunchKernelGGL((k_parse<true, false>), dim3((uint32_t)nb), dim3(kParseWG), 0, st, d_text, d_off, n_lines, nullptr,
+                       0u, d_spells, n_spells, d_tuples, d_ts, d_disp);
   TPCHK(c, hipGetLastError());
   return RSA_OK;
 }

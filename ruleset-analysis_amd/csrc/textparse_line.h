@@ -40,6 +40,30 @@ struct WordLn {              // 4-byte loads with a one-word cache: a scan reads
   }
 };
 
+struct GWordLn {             // global 4-byte loads with a one-word cache (no staging); bytes of the
+  const uint32_t* w32;       // buffer's last, partial word are read one by one
+  const uint8_t* b8;         // the same buffer, as bytes
+  uint64_t o;                // byte offset of the line
+  uint64_t nb;               // bytes in the buffer
+  uint32_t n;
+  mutable uint64_t ci;
+  mutable uint32_t cw;
+  RSA_HD uint32_t operator[](uint32_t i) const {
+    const uint64_t pos = o + i, wi = pos >> 2;
+    if (wi != ci) {
+      ci = wi;
+      if (4 * wi + 4 <= nb) {
+        cw = w32[wi];
+      } else {
+        cw = 0;
+        for (uint32_t k = 0; k < 4; ++k)
+          if (4 * wi + k < nb) cw |= (uint32_t)b8[4 * wi + k] << (8 * k);
+      }
+    }
+    return (cw >> ((uint32_t)(pos & 3u) * 8u)) & 0xFFu;
+  }
+};
+
 RSA_HD bool is_dig(uint32_t c) { return c - '0' < 10u; }
 RSA_HD bool is_upper(uint32_t c) { return c - 'A' < 26u; }
 RSA_HD bool is_lower(uint32_t c) { return c - 'a' < 26u; }

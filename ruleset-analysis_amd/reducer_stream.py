@@ -39,7 +39,7 @@ from . import textparse
 from .compile import F_BUILT, F_HIT, TUPLE_DTYPE
 from .logparse import reducer_fields, reducer_timestamp, _canonical_v4
 from .py2text import PY2_WS, py2_int
-from .report import HEADER, NOISE1, dotted, table_order
+from .report import HEADER, NOISE1, MemoDecode, _rows_by_gid, dotted_list, table_rows
 
 __all__ = ['ReducerStream']
 
@@ -266,12 +266,23 @@ class ReducerStream(object):
         res = eng.run([b], self.cap, capacity=max(int(hb.sum()), 1))
         return res, ts_decode
 
-    def _strings(self, x):
-        ps = int(x['pspell'])
-        if ps & INTERNED:
-            s = self.istr.values
-            return self.spells[ps & ~INTERNED], s[int(x['for_ip'])], s[int(x['to_ip'])], s[int(x['to_port'])]
-        return self.spells[ps], dotted(x['for_ip']), dotted(x['to_ip']), str(int(x['to_port']))
+    def _strings(self, rows):
+        """The key strings (PROTO, FROMIP, TOIP, TOPORT) of one rule's records:
+        canonical values printed back, interned text looked up."""
+        ps = rows['pspell'].tolist()
+        if not any(p & INTERNED for p in ps):
+            return ([self.spells[p] for p in ps], dotted_list(rows['for_ip']), dotted_list(rows['to_ip']),
+                    [str(p) for p in rows['to_port'].tolist()])
+        s = self.istr.values
+        out = ([], [], [], [])
+        for p, f, t, q in zip(ps, rows['for_ip'].tolist(), rows['to_ip'].tolist(), rows['to_port'].tolist()):
+            if p & INTERNED:
+                vals = (self.spells[p & ~INTERNED], s[f], s[t], s[q])
+            else:
+                vals = (self.spells[p], dotted_list([f])[0], dotted_list([t])[0], str(q))
+            for col, x in zip(out, vals):
+                col.append(x)
+        return out
 
     def _report(self, events, runs, res, ts_decode, mode):
         """connlist-reducer.py's stdout for these events: noise pairs at their
@@ -279,31 +290,22 @@ class ReducerStream(object):
         ended): the blank line and the last block; 'carry': the last block too
         (the carried run's key follows); 'error': the reference died at the
         next line, before printing the last block."""
-        rec = res.records
-        by_run = {}
-        for k in np.argsort(rec['gid'], kind='stable'):
-            by_run.setdefault(int(rec['gid'][k]), []).append(rec[k])
+        by_run = _rows_by_gid(res.records)
         out = []
         cap = self.cap
+        ts_decode = MemoDecode(ts_decode)
 
         def block(r):
             _key, host, acl, rule, _first = runs[r]
-            rws = by_run.get(r, [])
-            strs = [self._strings(x) for x in rws]
-            if rws:
-                order = table_order([s[0] for s in strs], [s[1] for s in strs], [s[2] for s in strs],
-                                    [s[3] for s in strs], [int(x['min_order']) for x in rws])
-                rws = [rws[k] for k in order]
-                strs = [strs[k] for k in order]
             lines = ['{0}: access-list {1}, rule {2}: {3}'.format(host, acl, rule.ruleindex, str(rule)),
                      '{0}'.format(rule.original), 'Total number of hits: {0}'.format(int(res.hits[r]))]
             if cap == 0 or int(res.thresh[r]) != 0xFFFFFFFFFFFFFFFF:
                 lines.append('NOTE: Maximum number of connections ({0}) reached for this rule, additional '
                              'connections not displayed.'.format(cap))
             lines.append(HEADER)
-            for x, s in zip(rws, strs):
-                lines.append('%6d %4s %15s  %15s %-5s %19s  %19s' % (int(x['count']), s[0], s[1], s[2], s[3],
-                                                                     ts_decode(x['first']), ts_decode(x['last'])))
+            rows = by_run.get(r)
+            if rows is not None and len(rows):
+                lines.extend(table_rows(rows, *self._strings(rows), ts_decode))
             return lines
 
         prev = None

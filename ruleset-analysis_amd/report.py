@@ -67,12 +67,49 @@ def table_order(spell, from_ip, to_ip, to_port, first_seen):
     first-seen order, stable-sorted by ``"TOIP TOPORT"``."""
     n = len(to_ip)
     sort_key = [to_ip[k] + ' ' + to_port[k] for k in range(n)]
-    ins = sorted(range(n), key=lambda k: int(first_seen[k]))
     if len(set(sort_key)) == n:            # no ties: dict order cannot show
         return sorted(range(n), key=sort_key.__getitem__)
+    fs = first_seen.tolist() if hasattr(first_seen, 'tolist') else list(first_seen)
+    ins = sorted(range(n), key=fs.__getitem__)
     keys = [';'.join((spell[k], from_ip[k], to_ip[k], to_port[k])) for k in ins]
     py2 = [ins[j] for j in iteration_order(keys)]
     return sorted(py2, key=sort_key.__getitem__)
+
+
+_OCTET = [str(k) for k in range(256)]
+
+
+def dotted_list(values):
+    """dotted() of a sequence of IPv4 values (one list pass)."""
+    o = _OCTET
+    return [o[v >> 24] + '.' + o[(v >> 16) & 255] + '.' + o[(v >> 8) & 255] + '.' + o[v & 255]
+            for v in (values.tolist() if hasattr(values, 'tolist') else values)]
+
+
+class MemoDecode(object):
+    """A timestamp decoder with a memo: a report's rows share few distinct codes."""
+
+    def __init__(self, decode):
+        self.decode, self.memo = decode, {}
+
+    def __call__(self, code):
+        s = self.memo.get(code)
+        if s is None:
+            s = self.memo[code] = self.decode(code)
+        return s
+
+
+def table_rows(rows, spell, from_ip, to_ip, to_port, ts_decode):
+    """The connection-table lines of one rule (connlist-reducer.py:119-126):
+    ``rows`` its records, the key strings per record, ordered by table_order."""
+    cnt = rows['count'].tolist()
+    first = rows['first'].tolist()
+    last = rows['last'].tolist()
+    if not isinstance(ts_decode, MemoDecode):
+        ts_decode = MemoDecode(ts_decode)
+    return ['%6d %4s %15s  %15s %-5s %19s  %19s' % (cnt[k], spell[k], from_ip[k], to_ip[k], to_port[k],
+                                                     ts_decode(first[k]), ts_decode(last[k]))
+            for k in table_order(spell, from_ip, to_ip, to_port, rows['min_order'])]
 
 
 def block_lines(host, acl, rule, hits, rows, capped, cap, ts_decode, pspell_table):
@@ -84,15 +121,9 @@ def block_lines(host, acl, rule, hits, rows, capped, cap, ts_decode, pspell_tabl
                    'displayed.'.format(cap))
     out.append(HEADER)
     if rows is not None and len(rows):
-        spell = [pspell_table[int(p)] for p in rows['pspell']]
-        from_ip = [dotted(v) for v in rows['for_ip']]
-        to_ip = [dotted(v) for v in rows['to_ip']]
-        to_port = [str(int(p)) for p in rows['to_port']]
-        for k in table_order(spell, from_ip, to_ip, to_port, rows['min_order']):
-            r = rows[k]
-            out.append('%6d %4s %15s  %15s %-5s %19s  %19s' % (int(r['count']), spell[k], from_ip[k], to_ip[k],
-                                                                 to_port[k], ts_decode(int(r['first'])),
-                                                                 ts_decode(int(r['last']))))
+        spell = [pspell_table[p] for p in rows['pspell'].tolist()]
+        out.extend(table_rows(rows, spell, dotted_list(rows['for_ip']), dotted_list(rows['to_ip']),
+                              [str(p) for p in rows['to_port'].tolist()], ts_decode))
     return out
 
 
@@ -106,6 +137,7 @@ def reducer_report(results, groups, noise, cap, ts_decode, pspell_table, n_blank
     records (the mapper's doubled newlines) sort before everything else.
     """
     rows = _rows_by_gid(results.records)
+    ts_decode = MemoDecode(ts_decode)
     out = [NOISE1, 'The line was: '] * int(n_blank)
     ni = 0
     noise = sorted(noise, key=lambda t: t[0])

@@ -88,7 +88,7 @@ def _key_of(line):
     return s.split('\t', 1)[0] if '\t' in s else None
 
 
-@pytest.mark.parametrize('case,seed,word', [('small_200r', 1, 1), ('cap5_zipf', 2, 0), ('multi_acl', 3, 1)])
+@pytest.mark.parametrize('case,seed,word', [('small_200r', 1, 1), ('cap5_zipf', 2, 0), ('multi_acl', 3, 2)])
 def test_device_reducer_fields_on_cpu_equal_reference_regex(case, seed, word):
     """Every line the device decides (not RSA_LINE_HOST) has the reducer's own
     hit flag, BUILT match, key strings and timestamp; noise is exactly the

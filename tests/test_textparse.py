@@ -199,7 +199,7 @@ def _device_stage_on_cpu(lib, host, lines, db, compiled, spells, word=1):
     return tup, ts, disp, names
 
 
-@pytest.mark.parametrize('seed,word', [(1, 1), (2, 1), (3, 0)])
+@pytest.mark.parametrize('seed,word', [(1, 1), (2, 1), (3, 0), (4, 2)])
 def test_device_line_parser_on_cpu_equals_host_parser(seed, word):
     """Every line the device parser decides itself (not RSA_LINE_HOST) gets
     exactly the host parser's disposition, tuple, list, spelling and
@@ -289,12 +289,18 @@ def test_gpu_parse_golden_equals_host(engine, case):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('seed', [1, 2])
-def test_gpu_parse_fuzz_equals_host(engine, seed):
+@pytest.mark.parametrize('seed,mode', [(1, 0), (2, 0), (1, 1)])
+def test_gpu_parse_fuzz_equals_host(engine, seed, mode):
+    """mode: RSA_OPT_PARSE_MODE (0 LDS-staged lines, 1 direct HBM reads)."""
+    from ruleset_analysis_amd import native
     db, lines = _fuzz_lines(seed, 6000)
     good = [l for l in lines if _host_ok('fw1', l, db)]
     assert len(good) > 4000
-    got = _compare(engine, 'fw1', good, db)
+    engine.set_option(native.RSA_OPT_PARSE_MODE, mode)
+    try:
+        got = _compare(engine, 'fw1', good, db)
+    finally:
+        engine.set_option(native.RSA_OPT_PARSE_MODE, 0)
     d = got.disposition
     # the fuzz reaches every outcome, and most lines stay on the device
     for k in (logparse.D_IGNORE, logparse.D_NOACL, logparse.D_MISSING, logparse.D_CLASSIFY):
