@@ -16,7 +16,7 @@ import numpy as np
 
 from . import native
 from .native import RSA_ERR_CAPACITY, NativeError
-from .compile import RECORD_DTYPE, TUPLE_DTYPE
+from .compile import RECORD_DTYPE, RULE_DTYPE, TUPLE_DTYPE
 
 __all__ = ['Engine', 'Results', 'DeviceBatch']
 
@@ -142,8 +142,10 @@ class Engine(object):
             self.load_index(compiled.index(prefix=prefix, chunk=chunk, kind=kind))
 
     def set_rule_count(self, n_rules):
-        self.ctx.call('rsa_set_rule_count', ctypes.c_uint32(n_rules))
-        self._bind(n_rules)
+        """Rule count of jobs over given gids (rsa_aggregate_gids: the reducer
+        drop-in's runs, the merge owners): any loaded candidate lists are
+        replaced by none, so the count may change between jobs."""
+        self.load_rules(np.zeros(0, RULE_DTYPE), np.zeros(1, np.uint32), n_rules)
 
     def _bind(self, n_rules):
         torch = self.torch
