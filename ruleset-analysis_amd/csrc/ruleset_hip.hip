@@ -2306,6 +2306,84 @@ __global__ __launch_bounds__(1024) void k_emit(const Slot* S, const unsigned lon
   }
 }
 
+// ---- Owner import (multi-GPU merge): received rsa_conn_records are merged
+// into this ctx's table the way pass 1 merges its records -- counting-sorted
+// by table region into HRecs (k_imp_hist, a scan, k_imp_scatter), then one
+// k_reduce workgroup per region (LDS aggregation, plain loads and stores on the
+// region's own slots) -- instead of device atomics per record on the slots.
+constexpr uint32_t kImpChunk = 16384;   // records per workgroup chunk (16 per thread)
+
+__device__ __forceinline__ void imp_key(const rsa_conn_record& r, unsigned long long& kA, unsigned long long& kB) {
+  kA = ((unsigned long long)r.for_ip << 32) | r.to_ip;
+  kB = ((unsigned long long)r.gid << 32) | ((unsigned long long)r.pspell << 16) | r.to_port;
+}
+
+__global__ __launch_bounds__(1024) void k_imp_hist(const rsa_conn_record* __restrict__ in, unsigned long long n, Agg A,
+                                                   uint32_t n_regions, uint32_t* __restrict__ counts) {
+  __shared__ uint32_t h[kMaxRegions];
+  for (uint32_t r = threadIdx.x; r < n_regions; r += blockDim.x) h[r] = 0;
+  __syncthreads();
+  for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (unsigned long long)gridDim.x * blockDim.x) {
+    unsigned long long kA, kB;
+    imp_key(in[i], kA, kB);
+    atomicAdd(&h[key_region(A, slot_hash(kA, kB))], 1u);
+  }
+  __syncthreads();
+  for (uint32_t r = threadIdx.x; r < n_regions; r += blockDim.x)
+    if (h[r]) atomicAdd(&counts[r], h[r]);
+}
+
+// base: exclusive scan of the region counts; cursor: zeroed.  One device
+// atomic per (chunk, region) reserves the chunk's run of each region.
+__global__ __launch_bounds__(1024) void k_imp_scatter(const rsa_conn_record* __restrict__ in, unsigned long long n,
+                                                      Agg A, uint32_t n_regions, const uint32_t* __restrict__ base,
+                                                      uint32_t* __restrict__ cursor, HRec* __restrict__ out) {
+  __shared__ uint32_t cnt[kMaxRegions], at[kMaxRegions];
+  for (unsigned long long c0 = (unsigned long long)blockIdx.x * kImpChunk; c0 < n;
+       c0 += (unsigned long long)gridDim.x * kImpChunk) {
+    const unsigned long long c1 = c0 + kImpChunk < n ? c0 + kImpChunk : n;
+    for (uint32_t r = threadIdx.x; r < n_regions; r += blockDim.x) cnt[r] = 0;
+    __syncthreads();
+    for (unsigned long long i = c0 + threadIdx.x; i < c1; i += blockDim.x) {
+      unsigned long long kA, kB;
+      imp_key(in[i], kA, kB);
+      atomicAdd(&cnt[key_region(A, slot_hash(kA, kB))], 1u);
+    }
+    __syncthreads();
+    for (uint32_t r = threadIdx.x; r < n_regions; r += blockDim.x) {
+      at[r] = cnt[r] ? base[r] + atomicAdd(&cursor[r], cnt[r]) : 0u;
+      cnt[r] = 0;
+    }
+    __syncthreads();
+    for (unsigned long long i = c0 + threadIdx.x; i < c1; i += blockDim.x) {
+      const rsa_conn_record r = in[i];
+      unsigned long long kA, kB;
+      imp_key(r, kA, kB);
+      const uint32_t g = key_region(A, slot_hash(kA, kB));
+      HRec h;
+      h.kA = kA;
+      h.kB = kB;
+      h.mo = r.min_order;
+      h.first = r.first;
+      h.last = r.last;
+      h.cnt = r.count;
+      h.pad = 0;
+      out[at[g] + atomicAdd(&cnt[g], 1u)] = h;
+    }
+    __syncthreads();
+  }
+}
+
+// every region reads its HRecs: hot_base = base, hot_fill = counts
+__global__ void k_imp_desc(const uint32_t* __restrict__ base, const uint32_t* __restrict__ counts, uint32_t n_regions,
+                           unsigned long long* __restrict__ hot_base, uint32_t* __restrict__ hot_fill) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_regions) return;
+  hot_base[r] = base[r];
+  hot_fill[r] = counts[r];
+}
+
 // New slots are appended to the used list with one device atomic per 1024
 // records (workgroup scan), not one per wave: every import record of a fresh
 // owner table is new, and per-wave appends serialise on the one cursor word.
@@ -2443,6 +2521,7 @@ struct rsa_ctx {
   unsigned long long* d_packed = nullptr;   // k_count / k_aggregate packed counters (rules > kCnt)
   // hot-region split (k_hot_plan / k_hot_combine)
   int parse_mode = 0;                       // RSA_OPT_PARSE_MODE (textparse.hip)
+  bool region_import = true;                // RSA_OPT_REGION_IMPORT: rsa_import by region sort + k_reduce
   bool hot_split = true;                    // RSA_OPT_HOT_SPLIT
   unsigned long long hot_min = kHotMinRecs; // RSA_OPT_HOT_MIN: a hot region holds more than max(hot_min,
   uint32_t hot_factor = kHotFactor;         //   hot_factor x the mean region) records
@@ -3128,6 +3207,9 @@ int rsa_set_option(rsa_ctx* c, int option, int64_t value) {
       if (value < 0 || value > 1) return fail(c, RSA_ERR_ARG, "parse mode must be 0 (LDS staged) or 1 (direct)");
       c->parse_mode = (int)value;
       return RSA_OK;
+    case RSA_OPT_REGION_IMPORT:
+      c->region_import = value != 0;
+      return RSA_OK;
     case RSA_OPT_HOT_SPLIT:
       c->hot_split = value != 0;
       return RSA_OK;
@@ -3565,7 +3647,46 @@ int rsa_import(rsa_ctx* c, int which, const rsa_conn_record* in, uint64_t n) {
   if (n == 0) return RSA_OK;
   if (!in) return fail(c, RSA_ERR_ARG, "null input records");
   c->table_dirty = true;
-  k_import<<<grid_for_threads(c, n, 1024, 4), 1024, 0, c->stream>>>(in, n, which, agg_of(c));
+  if (!c->region_import) {
+    k_import<<<grid_for_threads(c, n, 1024, 4), 1024, 0, c->stream>>>(in, n, which, agg_of(c));
+    HIPCHK(c, hipGetLastError());
+    return RSA_OK;
+  }
+  if (n > 0xFFFFFFFFull) return fail(c, RSA_ERR_ARG, "more than 2^32 records in one import");
+  const uint32_t n_regions = 1u << c->np_bits;
+  if (!c->d_hot_base) {
+    HIPCHK(c, hipMalloc(&c->d_hot_base, kMaxRegions * sizeof(unsigned long long)));
+    HIPCHK(c, hipMalloc(&c->d_hot_fill, kMaxRegions * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(&c->d_hot_ctl, 4 * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(&c->d_hot_total, sizeof(unsigned long long)));
+  }
+  if (n > c->hot_alloc) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    hipFree(c->d_hot);
+    c->d_hot = nullptr;
+    c->hot_alloc = 0;
+    HIPCHK(c, hipMalloc(&c->d_hot, n * sizeof(HRec)));
+    c->hot_alloc = n;
+  }
+  // counts [0, n_regions], scanned in place (k_scan_sums writes the total at
+  // [n_regions]); cursors behind them
+  int rc2 = ensure_buf(c, &c->d_scan_sums, &c->scan_sums_alloc, 2ull * (kMaxRegions + 1));
+  if (rc2) return rc2;
+  uint32_t* counts = c->d_scan_sums;
+  uint32_t* cursor = c->d_scan_sums + kMaxRegions + 1;
+  HIPCHK(c, hipMemsetAsync(counts, 0, 2ull * (kMaxRegions + 1) * sizeof(uint32_t), c->stream));
+  const Agg ag = agg_of(c);
+  k_imp_hist<<<grid_for_threads(c, n, 1024, 2), 1024, 0, c->stream>>>(in, n, ag, n_regions, counts);
+  k_scan_sums<<<1, 1024, 0, c->stream>>>(counts, n_regions);
+  k_imp_scatter<<<grid_for_threads(c, (n + kImpChunk - 1) / kImpChunk * 1024, 1024, 2), 1024, 0, c->stream>>>(
+      in, n, ag, n_regions, counts, cursor, static_cast<HRec*>(c->d_hot));
+  k_imp_desc<<<(n_regions + 255) / 256, 256, 0, c->stream>>>(counts, cursor, n_regions, c->d_hot_base, c->d_hot_fill);
+  if (which == 0)
+    k_reduce<1><<<n_regions, 1024, 0, c->stream>>>(nullptr, c->d_starts, 0, ag, c->d_hot_base, c->d_hot_fill,
+                                                   static_cast<const HRec*>(c->d_hot));
+  else
+    k_reduce<2><<<n_regions, 1024, 0, c->stream>>>(nullptr, c->d_starts, 0, ag, c->d_hot_base, c->d_hot_fill,
+                                                   static_cast<const HRec*>(c->d_hot));
   HIPCHK(c, hipGetLastError());
   return RSA_OK;
 }

@@ -54,6 +54,17 @@ def main():
         job.finish()
         dt = time.perf_counter() - t
         best = dt if best is None else min(best, dt)
+    if os.environ.get('RSA_PROFILE_HOST'):
+        import cProfile
+        import pstats
+        pr = cProfile.Profile()
+        job = ReducerStream(red, acldb.load_json(dbj), cap, lambda t: None)
+        pr.enable()
+        for a in range(0, len(data), 16 << 20):
+            job.feed(data[a:a + (16 << 20)])
+        job.finish()
+        pr.disable()
+        pstats.Stats(pr, stream=sys.stderr).sort_stats('cumulative').print_stats(25)
     got = ''.join(out)
     from oracle.crosscheck_2to3 import oracle_db
     from oracle.reducer import reduce_lines
