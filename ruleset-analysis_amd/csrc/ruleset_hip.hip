@@ -3475,8 +3475,12 @@ int rsa_reset(rsa_ctx* c, uint64_t capacity, uint32_t cap) {
   {
     uint32_t bits = 0;
     while ((1ull << bits) < want) ++bits;
-    c->rs_bits = bits < (uint32_t)kRegionMaxBits ? bits : (uint32_t)kRegionMaxBits;
-    c->np_bits = bits - c->rs_bits;
+    // regions of at most 2^16 slots, and at least 256 of them (one k_reduce
+    // workgroup each: every CU busy) while they keep >= 1024 slots
+    uint32_t rs = bits < (uint32_t)kRegionMaxBits ? bits : (uint32_t)kRegionMaxBits;
+    while (rs > 10 && bits - rs < 8) --rs;
+    c->rs_bits = rs;
+    c->np_bits = bits - rs;
   }
   if (want > c->slot_alloc) {
     HIPCHK(c, hipStreamSynchronize(c->stream));

@@ -112,6 +112,9 @@ class ReducerStream(object):
         d = disp.cpu().numpy().view(np.uint32)
         kind, same = d & 0xFF, (d & RED_SAME) != 0
         line = lambda i: data[int(h_off[i]):int(h_off[i + 1])].decode('latin-1')
+        # empty lines (the mapper's blank records, all sorted to the front) are
+        # "Unable to unpack" noise with nothing to parse: handled as runs
+        blank = (kind == RED_NOISE) & (np.diff(h_off.astype(np.int64)) <= 1) if n else np.zeros(0, bool)
 
         # runs: the host decides each line that does not repeat its predecessor's key
         status = np.full(n, -1, np.int64)       # run id of the line, -1 noise
@@ -119,7 +122,7 @@ class ReducerStream(object):
         events = []                             # (line, 'noise', text) | (line, 'run', id)
         current = None
         stop, error = n, None
-        decide = np.nonzero(~same)[0]
+        decide = np.nonzero(~same & ~blank)[0]
         for i in decide:
             i = int(i)
             if kind[i] == RED_NOISE:
@@ -219,6 +222,12 @@ class ReducerStream(object):
                     res, ts_decode = self._aggregate(tuples[:stop], ts[:stop], status[:stop], kind[:stop], odd_ts,
                                                      len(runs))
                     break
+        if blank[:stop].any():   # runs of empty lines: one event per run
+            b = np.concatenate([[False], blank[:stop], [False]]).astype(np.int8)
+            edges = np.diff(b)
+            for a, e in zip(np.nonzero(edges == 1)[0].tolist(), np.nonzero(edges == -1)[0].tolist()):
+                events.append((a, 'blanks', e - a))
+            events.sort(key=lambda e: e[0])
         mode = 'error' if error is not None else 'final' if final else 'carry'
         self.write(self._report(events, runs, res, ts_decode, mode))
         self.lines_done += stop
@@ -293,6 +302,7 @@ class ReducerStream(object):
         by_run = _rows_by_gid(res.records)
         out = []
         cap = self.cap
+        parts = []      # text already joined (runs of blank-line noise pairs)
         ts_decode = MemoDecode(ts_decode)
 
         def block(r):
@@ -310,7 +320,12 @@ class ReducerStream(object):
 
         prev = None
         for _i, what, val in events:
-            if what == 'noise':
+            if what == 'blanks':
+                if out:
+                    parts.append(''.join(l + '\n' for l in out))
+                    out = []
+                parts.append((NOISE1 + '\nThe line was: \n') * val)
+            elif what == 'noise':
                 out.append(NOISE1)
                 out.append('The line was: {0}'.format(val))
             else:
@@ -327,4 +342,5 @@ class ReducerStream(object):
             # run's key arrives (always the next chunk's first run)
             out.append('')
             out.extend(block(prev))
-        return ''.join(l + '\n' for l in out)
+        parts.append(''.join(l + '\n' for l in out))
+        return ''.join(parts)
