@@ -314,13 +314,18 @@ int rsa_stats(rsa_ctx *ctx, uint64_t *h_out4, int reset);
 typedef struct rsa_shadow_rule {
   uint32_t src_lo, src_span;  /* IPv4 network [lo, lo + span]                      */
   uint32_t dst_lo, dst_span;
-  int32_t sport, dport;       /* one port, or -1 = NO_PORT                         */
+  int32_t sport, dport;       /* one port, -1 = NO_PORT, <= -2 a list (rsa_shadowed_ports) */
   uint16_t proto;             /* protocol id, 0 = 'ip'                              */
   uint8_t action;             /* 1 permit, 0 deny                                   */
   uint8_t v4;                 /* 1: both addresses IPv4 (else never contains/contained) */
   uint32_t reserved;
 } rsa_shadow_rule;
 int rsa_shadowed(rsa_ctx *ctx, const rsa_shadow_rule *h_rules, uint32_t n, int32_t *h_cover);
+/* The same for rules whose port sides may be lists: a side <= -2 names the list
+ * h_ports[-side - 2] = count, followed by its ports (firewallrule.py:162-171:
+ * every port of the other rule's list must be in this rule's list). */
+int rsa_shadowed_ports(rsa_ctx *ctx, const rsa_shadow_rule *h_rules, uint32_t n, const int32_t *h_ports,
+                       uint32_t n_ports, int32_t *h_cover);
 
 /* ---- Text parse: one firewall's log text resident in
  * HBM -> the packed inputs of rsa_classify.  Replaces the per-line Python of

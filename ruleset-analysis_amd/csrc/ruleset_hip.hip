@@ -2433,20 +2433,42 @@ __global__ __launch_bounds__(1024) void k_import(const rsa_conn_record* __restri
 constexpr int kShadowTile = 1024;
 static_assert(sizeof(rsa_shadow_rule) == 32, "shadow rule layout");
 
-__device__ __forceinline__ bool rule_contains(const rsa_shadow_rule& a, const rsa_shadow_rule& b) {
+// One port side of FirewallRule.__contains__ (firewallrule.py:162-171): self
+// "any" ([NO_PORT]) contains every list, else every port of the other list
+// must be in self's list.  A side is one port (>= 0), -1 (any) or a list
+// (<= -2: ports[-v - 2] = count, the ports after it; rsa_shadowed_ports).
+__device__ __forceinline__ bool side_contains(int32_t a, int32_t b, const int32_t* __restrict__ ports) {
+  if (a == -1) return true;
+  if (a >= 0 && b >= -1) return b == a;
+  const int32_t* al = a <= -2 ? ports + (-a - 2) : nullptr;
+  const int32_t* bl = b <= -2 ? ports + (-b - 2) : nullptr;
+  const int32_t na = al ? al[0] : 1, nb = bl ? bl[0] : 1;
+  for (int32_t x = 0; x < nb; ++x) {
+    const int32_t q = bl ? bl[1 + x] : b;
+    bool in = false;
+    for (int32_t y = 0; y < na && !in; ++y) in = (al ? al[1 + y] : a) == q;
+    if (!in) return false;
+  }
+  return true;
+}
+
+__device__ __forceinline__ bool rule_contains(const rsa_shadow_rule& a, const rsa_shadow_rule& b,
+                                              const int32_t* __restrict__ ports) {
   if (a.action != b.action) return false;                         // :146
   if (a.proto != 0 && a.proto != b.proto) return false;           // :150
   if (!a.v4 || !b.v4) return false;                               // IPy: another version is never contained
   const unsigned long long as = a.src_lo, bs = b.src_lo, ad = a.dst_lo, bd = b.dst_lo;
   if (bs < as || bs + b.src_span > as + a.src_span) return false;   // :154 other.src in self.src
   if (bd < ad || bd + b.dst_span > ad + a.dst_span) return false;   // :158
-  if (a.sport != -1 && b.sport != a.sport) return false;          // :162-165
-  if (a.dport != -1 && b.dport != a.dport) return false;          // :168-171
+  if (a.sport != b.sport || a.sport < -1 || b.sport < -1)         // :162-165
+    if (!side_contains(a.sport, b.sport, ports)) return false;
+  if (a.dport != b.dport || a.dport < -1 || b.dport < -1)         // :168-171
+    if (!side_contains(a.dport, b.dport, ports)) return false;
   return true;
 }
 
 __global__ __launch_bounds__(1024) void k_shadow(const rsa_shadow_rule* __restrict__ rules, uint32_t n,
-                                                 int32_t* __restrict__ cover) {
+                                                 const int32_t* __restrict__ ports, int32_t* __restrict__ cover) {
   __shared__ rsa_shadow_rule tile[kShadowTile];
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const bool in = i < n;
@@ -2462,7 +2484,7 @@ __global__ __launch_bounds__(1024) void k_shadow(const rsa_shadow_rule* __restri
     if (in && found < 0) {
       const uint32_t lim = min((uint32_t)kShadowTile, i > t0 ? i - t0 : 0u);
       for (uint32_t q = 0; q < lim; ++q) {
-        if (rule_contains(tile[q], me)) {
+        if (rule_contains(tile[q], me, ports)) {
           found = (int32_t)(t0 + q);
           break;
         }
@@ -3696,20 +3718,39 @@ int rsa_import(rsa_ctx* c, int which, const rsa_conn_record* in, uint64_t n) {
 }
 
 int rsa_shadowed(rsa_ctx* c, const rsa_shadow_rule* h_rules, uint32_t n, int32_t* h_cover) {
-  if (!c || (n && (!h_rules || !h_cover))) return fail(c, RSA_ERR_ARG, "null argument");
+  return rsa_shadowed_ports(c, h_rules, n, nullptr, 0, h_cover);
+}
+
+int rsa_shadowed_ports(rsa_ctx* c, const rsa_shadow_rule* h_rules, uint32_t n, const int32_t* h_ports,
+                       uint32_t n_ports, int32_t* h_cover) {
+  if (!c || (n && (!h_rules || !h_cover)) || (n_ports && !h_ports)) return fail(c, RSA_ERR_ARG, "null argument");
   if (n == 0) return RSA_OK;
+  // every list a rule names lies inside the port array (the kernel trusts them)
+  for (uint32_t k = 0; k < n; ++k) {
+    for (int32_t v : {h_rules[k].sport, h_rules[k].dport}) {
+      if (v >= -1) continue;
+      const uint64_t at = (uint64_t)(-(int64_t)v - 2);
+      if (at >= n_ports || h_ports[at] < 1 || at + 1 + (uint64_t)h_ports[at] > n_ports)
+        return fail(c, RSA_ERR_ARG, "rule %u: port list outside the port array", k);
+    }
+  }
   HIPCHK(c, hipSetDevice(c->device));
   rsa_shadow_rule* d_rules = nullptr;
   int32_t* d_cover = nullptr;
+  int32_t* d_ports = nullptr;
   HIPCHK(c, hipMalloc(&d_rules, (size_t)n * sizeof(rsa_shadow_rule)));
-  if (hipMalloc(&d_cover, (size_t)n * sizeof(int32_t)) != hipSuccess) {
+  if (hipMalloc(&d_cover, (size_t)n * sizeof(int32_t)) != hipSuccess ||
+      hipMalloc(&d_ports, (size_t)(n_ports ? n_ports : 1) * sizeof(int32_t)) != hipSuccess) {
     hipFree(d_rules);
-    return fail(c, RSA_ERR_HIP, "hipMalloc of the cover array failed");
+    hipFree(d_cover);
+    return fail(c, RSA_ERR_HIP, "hipMalloc of the shadow buffers failed");
   }
   int rc = RSA_OK;
   hipError_t e = hipMemcpyAsync(d_rules, h_rules, (size_t)n * sizeof(rsa_shadow_rule), hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess && n_ports)
+    e = hipMemcpyAsync(d_ports, h_ports, (size_t)n_ports * sizeof(int32_t), hipMemcpyHostToDevice, c->stream);
   if (e == hipSuccess) {
-    k_shadow<<<(n + 1023) / 1024, 1024, 0, c->stream>>>(d_rules, n, d_cover);
+    k_shadow<<<(n + 1023) / 1024, 1024, 0, c->stream>>>(d_rules, n, d_ports, d_cover);
     e = hipGetLastError();
   }
   if (e == hipSuccess) e = hipMemcpyAsync(h_cover, d_cover, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream);
@@ -3717,6 +3758,7 @@ int rsa_shadowed(rsa_ctx* c, const rsa_shadow_rule* h_rules, uint32_t n, int32_t
   if (e != hipSuccess) rc = fail(c, RSA_ERR_HIP, "rsa_shadowed: %s", hipGetErrorString(e));
   hipFree(d_rules);
   hipFree(d_cover);
+  hipFree(d_ports);
   return rc;
 }
 

@@ -73,6 +73,7 @@ SYMBOLS = {
     'rsa_export': (I32, [P, I32, P, U64, PU64]),
     'rsa_import': (I32, [P, I32, P, U64]),
     'rsa_shadowed': (I32, [P, P, U32, P]),
+    'rsa_shadowed_ports': (I32, [P, P, U32, P, U32, P]),
     'rsa_text_count_lines': (I32, [P, P, U64, PU64]),
     'rsa_text_line_offsets': (I32, [P, P, U64, P, U64]),
     'rsa_parse_text': (I32, [P, P, P, U64, P, U32, P, U32, P, P, P]),

@@ -8,8 +8,11 @@ candidate rules staged in LDS tiles) and the host prints the reference's
 three log messages per shadowed rule.
 
 ``shadow_table`` lowers a rule list (objects or ``RuleColumns``) to the 32-B
-``rsa_shadow_rule`` rows; every rule holds one port per side (SURVEY.md trap
-3) — a multi-port list raises ``NotImplementedError``.
+``rsa_shadow_rule`` rows: a port side is one port, ``-1`` (``[NO_PORT]``,
+any) or -- for a rule whose side is a list of several ports -- a reference
+``<= -2`` into a port array (``ShadowTable.ports``: count, then the ports),
+where the kernel tests list containment as ``__contains__`` does
+(``firewallrule.py:162-171``).
 """
 
 import ctypes
@@ -26,16 +29,26 @@ SHADOW_DTYPE = np.dtype([('src_lo', '<u4'), ('src_span', '<u4'), ('dst_lo', '<u4
 assert SHADOW_DTYPE.itemsize == 32
 
 
-def _one_port(ports):
-    if len(ports) != 1:
-        raise NotImplementedError('shadow analysis needs one port per rule side, got %r' % (ports,))
-    return int(ports[0])
+class ShadowTable(np.ndarray):
+    """rsa_shadow_rule rows with the port array their list sides refer to."""
+    ports = None
+
+
+def _side(ports, arr):
+    """One port side: the port (or -1 for [NO_PORT]), or a list reference."""
+    if len(ports) == 1:
+        return int(ports[0])
+    at = len(arr)
+    arr.append(len(ports))
+    arr.extend(int(p) for p in ports)
+    return -(at + 2)
 
 
 def shadow_table(rules):
     """rsa_shadow_rule rows of a rule list, protocol ids with 0 = 'ip'."""
     n = len(rules)
-    out = np.zeros(n, SHADOW_DTYPE)
+    out = np.zeros(n, SHADOW_DTYPE).view(ShadowTable)
+    out.ports = np.zeros(0, np.int32)
     names = {'ip': 0}
     cols = getattr(rules, 'proto_names', None)
     if cols is not None:                       # rulecols.RuleColumns
@@ -50,6 +63,7 @@ def shadow_table(rules):
         out['sport'] = rules.sport
         out['dport'] = rules.dport
         return out
+    plist = []
     for i, r in enumerate(rules):
         v4 = r.src._ipversion == 4 and r.dst._ipversion == 4
         out[i]['proto'] = names.setdefault(r.protocol, len(names))
@@ -58,17 +72,21 @@ def shadow_table(rules):
         if v4:
             out[i]['src_lo'], out[i]['src_span'] = r.src.ip, r.src.len() - 1
             out[i]['dst_lo'], out[i]['dst_span'] = r.dst.ip, r.dst.len() - 1
-        out[i]['sport'] = _one_port(r.sport)
-        out[i]['dport'] = _one_port(r.dport)
+        out[i]['sport'] = _side(r.sport, plist)
+        out[i]['dport'] = _side(r.dport, plist)
+    out.ports = np.array(plist, np.int32)
     return out
 
 
 def shadowed(engine, table):
     """cover[i] = smallest j < i whose rule contains rule i, or -1 (GPU)."""
-    table = np.ascontiguousarray(table, SHADOW_DTYPE)
+    ports = getattr(table, 'ports', None)
+    ports = np.ascontiguousarray(ports if ports is not None else np.zeros(0, np.int32), np.int32)
+    table = np.ascontiguousarray(np.asarray(table).view(np.ndarray), SHADOW_DTYPE)
     cover = np.empty(len(table), np.int32)
     if len(table):
-        engine.ctx.call('rsa_shadowed', table.ctypes.data_as(ctypes.c_void_p), ctypes.c_uint32(len(table)),
+        engine.ctx.call('rsa_shadowed_ports', table.ctypes.data_as(ctypes.c_void_p), ctypes.c_uint32(len(table)),
+                        ports.ctypes.data_as(ctypes.c_void_p), ctypes.c_uint32(len(ports)),
                         cover.ctypes.data_as(ctypes.c_void_p))
     return cover
 
