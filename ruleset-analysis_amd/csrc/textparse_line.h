@@ -32,11 +32,15 @@ struct WordLn {              // 4-byte loads with a one-word cache: a scan reads
   mutable uint32_t ci, cw;
   RSA_HD uint32_t operator[](uint32_t i) const {
     const uint32_t pos = o + i, wi = pos >> 2;
+#ifdef RSA_TP_NOCACHE
+    return (w32[wi] >> ((pos & 3u) * 8u)) & 0xFFu;   // EXPERIMENT: no branch, one read per byte
+#else
     if (wi != ci) {
       ci = wi;
       cw = w32[wi];
     }
     return (cw >> ((pos & 3u) * 8u)) & 0xFFu;
+#endif
   }
 };
 

@@ -15,4 +15,12 @@ done
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace_dist" -o run --output-format csv -- \
   python3 bench.py --gpus 1 --force-dist --no-cpu-baseline --no-check --steps 3 --warmup 1 \
   > "$OUT/trace_dist.json" 2> "$OUT/trace_dist.err" || { tail -20 "$OUT/trace_dist.err"; exit 1; }
+# text parse A/B: the word-cached LDS accessor vs one LDS read per byte
+for v in base nocache; do
+  lib=ruleset-analysis_amd/_build/libruleset_hip.so
+  [ "$v" = nocache ] && lib=ruleset-analysis_amd/_build/var/libruleset_hip_nocache.so
+  RSA_HIP_LIB=$lib timeout -k 10 300 python3 bench.py --text --lines 8000000 --steps 3 --warmup 1 --no-cpu-baseline \
+    --no-check > "$OUT/text_$v.json" 2> "$OUT/text_$v.err" || { tail -5 "$OUT/text_$v.err"; exit 1; }
+  python3 -c "import json,sys;d=json.load(open(sys.argv[1]));print(sys.argv[2], d['phases_ms'])" "$OUT/text_$v.json" $v
+done
 echo done
