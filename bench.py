@@ -215,7 +215,10 @@ def reference_pipeline_baseline(n_lines=1_000_000, rules=200, seed=1, procs=None
     import shutil
     import subprocess
     import tempfile
-    procs = procs or min(os.cpu_count() or 1, 16)
+    # nproc mappers: the CPUs this job may use -- on the GPU box the job of one
+    # GPU gets 16 of the host's CPUs (OMP_NUM_THREADS=16 there), although
+    # os.cpu_count() shows the whole machine
+    procs = procs or int(os.environ.get('OMP_NUM_THREADS') or len(os.sched_getaffinity(0)) or 1)
     dbj, info = synth.make_db(seed, rules)
     tr = synth.make_traffic((dbj, info), n_lines, seed=seed + 100)
     text = ''.join(l + '\n' for l in synth.render_lines(tr))

@@ -229,12 +229,12 @@ __global__ __launch_bounds__(kParseWG) void k_parse(const uint8_t* __restrict__ 
       if (plen && text[a - 1] == '\n') --plen;
       const bool pin = i > 0 && plen < 0xFFFFFFFFull;
       if (staged) {
-        const rsa_text::WordLn s{sm, (uint32_t)(a - base), (uint32_t)len, 0xFFFFFFFFu, 0u};
+        const rsa_text::WordLn s{sm, (uint32_t)(a - base), (uint32_t)len};
         rsa_text::reduce_line(s, spells, n_spells, tup, ts, d);
         if (pin && d != RSA_RED_NOISE) {
           bool same;
           if (i > l0) {
-            const rsa_text::WordLn q{sm, (uint32_t)(pa - base), (uint32_t)plen, 0xFFFFFFFFu, 0u};
+            const rsa_text::WordLn q{sm, (uint32_t)(pa - base), (uint32_t)plen};
             same = rsa_text::same_key(s, q);
           } else {
             const rsa_text::ByteLn q{text + pa, (uint32_t)plen};
@@ -249,7 +249,7 @@ __global__ __launch_bounds__(kParseWG) void k_parse(const uint8_t* __restrict__ 
           d |= RSA_RED_SAME_KEY;
       }
     } else if (staged) {
-      const rsa_text::WordLn s{sm, (uint32_t)(a - base), (uint32_t)len, 0xFFFFFFFFu, 0u};
+      const rsa_text::WordLn s{sm, (uint32_t)(a - base), (uint32_t)len};
       rsa_text::parse_line(s, ifcs, n_ifcs, spells, n_spells, tup, ts, d);
     } else {
       const rsa_text::ByteLn s{text + a, (uint32_t)len};

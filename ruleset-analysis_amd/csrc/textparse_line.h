@@ -25,22 +25,13 @@ struct ByteLn {              // plain byte loads (any buffer)
   uint32_t n;
   RSA_HD uint32_t operator[](uint32_t i) const { return p[i]; }
 };
-struct WordLn {              // 4-byte loads with a one-word cache: a scan reads each word once
-  const uint32_t* w32;       // 4-byte aligned buffer, readable up to the word holding the line's last byte
-  uint32_t o;                // byte offset of the line in it
-  uint32_t n;
-  mutable uint32_t ci, cw;
+struct WordLn {              // one 4-byte load per byte read (LDS staging): no per-lane word cache, whose
+  const uint32_t* w32;       // compare-and-branch cost more than the extra LDS reads (8 % on k_parse,
+  uint32_t o;                // profiles/r03l_text_8M_*.json); buffer readable up to the line's last word;
+  uint32_t n;                // o = byte offset of the line in it
   RSA_HD uint32_t operator[](uint32_t i) const {
-    const uint32_t pos = o + i, wi = pos >> 2;
-#ifdef RSA_TP_NOCACHE
-    return (w32[wi] >> ((pos & 3u) * 8u)) & 0xFFu;   // EXPERIMENT: no branch, one read per byte
-#else
-    if (wi != ci) {
-      ci = wi;
-      cw = w32[wi];
-    }
-    return (cw >> ((pos & 3u) * 8u)) & 0xFFu;
-#endif
+    const uint32_t pos = o + i;
+    return (w32[pos >> 2] >> ((pos & 3u) * 8u)) & 0xFFu;
   }
 };
 

@@ -18,7 +18,7 @@ extern "C" void parse_lines_host(const uint8_t* text, const uint64_t* off, uint6
       const rsa_text::GWordLn s{reinterpret_cast<const uint32_t*>(text), text, a, off[n], (uint32_t)len, ~0ull, 0u};
       rsa_text::parse_line(s, ifcs, n_ifcs, spells, n_spells, tuples[i], ts[i], disp[i]);
     } else if (word) {
-      const rsa_text::WordLn s{reinterpret_cast<const uint32_t*>(text), (uint32_t)a, (uint32_t)len, 0xFFFFFFFFu, 0u};
+      const rsa_text::WordLn s{reinterpret_cast<const uint32_t*>(text), (uint32_t)a, (uint32_t)len};
       rsa_text::parse_line(s, ifcs, n_ifcs, spells, n_spells, tuples[i], ts[i], disp[i]);
     } else {
       const rsa_text::ByteLn s{text + a, (uint32_t)len};
@@ -40,7 +40,7 @@ extern "C" void reduce_lines_host(const uint8_t* text, const uint64_t* off, uint
       const rsa_text::GWordLn w{reinterpret_cast<const uint32_t*>(text), text, a, off[n], (uint32_t)len, ~0ull, 0u};
       rsa_text::reduce_line(w, spells, n_spells, tuples[i], ts[i], disp[i]);
     } else if (word) {
-      const rsa_text::WordLn w{reinterpret_cast<const uint32_t*>(text), (uint32_t)a, (uint32_t)len, 0xFFFFFFFFu, 0u};
+      const rsa_text::WordLn w{reinterpret_cast<const uint32_t*>(text), (uint32_t)a, (uint32_t)len};
       rsa_text::reduce_line(w, spells, n_spells, tuples[i], ts[i], disp[i]);
     } else {
       rsa_text::reduce_line(s, spells, n_spells, tuples[i], ts[i], disp[i]);

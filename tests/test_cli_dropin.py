@@ -86,3 +86,29 @@ def test_fused_run_postprocess_cli(tmp_path, case):
     with open(os.path.join(ROOT, 'tests', 'golden', case, 'postprocess.txt'), encoding='latin-1', newline='') as f:
         assert r.stdout.decode('latin-1') == f.read()
     assert b'INFO - Found rule which never gets hits' in r.stderr
+
+
+def test_config1_rsa_run_equals_oracle_pipeline(tmp_path):
+    """BASELINE config 1 exactly as bench.py's CPU baseline builds it (a
+    200-rule ACL and 1M synthetic ASA lines, seed 1): the fused rsa_run.py
+    report is byte-identical to ``oracle.cli map | LC_ALL=C sort | oracle.cli
+    reduce`` -- the pipeline the CPU baseline times -- over the same bytes."""
+    from ruleset_analysis_amd import synth
+    dbj, info = synth.make_db(1, 200)
+    tr = synth.make_traffic((dbj, info), 1_000_000, seed=101)
+    text = ''.join(l + '\n' for l in synth.render_lines(tr)).encode('latin-1')
+    (tmp_path / 'db.json').write_text(json.dumps(dbj))
+    logdir = tmp_path / 'logs' / 'fw1'
+    logdir.mkdir(parents=True)
+    (logdir / 'part-00000').write_bytes(text)
+    env = dict(os.environ, LC_ALL='C', mapred_input_dir=str(logdir) + '/part-00000', PYTHONPATH=ROOT)
+    py = sys.executable
+    want = subprocess.run('%s -m oracle.cli map db.json < logs/fw1/part-00000 | LC_ALL=C sort | '
+                          '%s -m oracle.cli reduce db.json 1000' % (py, py), shell=True, cwd=tmp_path, env=env,
+                          stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=600, check=True).stdout
+    r = subprocess.run([py, os.path.join(ROOT, 'rsa_run.py'), '--db', 'db.json', '--cap', '1000',
+                        str(logdir / 'part-00000')], cwd=tmp_path, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr.decode()[-2000:]
+    assert r.stdout == want
+    assert want.count(b'Total number of hits') > 100

@@ -1,15 +1,19 @@
 #!/usr/bin/env python3
 """Turn rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE counter CSVs of a bench run into
-profiles/<config>_pass1_pmc.json: HBM bytes per step of the pass-1 kernel.
+profiles/<config>_pass1_pmc.json: HBM bytes per step of the pass-1 kernels.
 
-Correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE is in KiB and on gfx950 reads
-1/2 of the bytes of wide coalesced streaming reads, so read bytes =
-2 * FETCH_SIZE * 1024; WRITE_SIZE * 1024 is taken as is.  The pass-1 kernel
-also issues scattered atomics whose accounting is uncalibrated, so the figure
-is a best estimate (it is reported beside, not instead of, the algorithmic
-bytes).  Usage: pmc_summary.py FETCH_CSV WRITE_CSV OUT_JSON LINES STEPS_TOTAL
-(STEPS_TOTAL = warmup + timed steps + 1 untimed stats step of the profiled
-bench run)."""
+FETCH_SIZE is in KiB and tallies 64 B per memory request.  Calibrated on the
+box with tools/fetch_calib.hip against known byte counts
+(profiles/r03l_fetch_calibration.json): 16-B-per-lane streaming reads and
+consecutive 32-B records per lane report 0.50 of their bytes (x2, as
+MI355X_MICROARCH.md §HBM says for wide streaming reads), random 32-B reads
+2.0x and random 64-B reads 1.04x (one 64-B tally per read).  Each kernel is
+converted with the factor of its dominant read pattern: the streaming
+kernels (k_classify, k_count, k_part_hist, k_part_scatter, the scans) x2,
+k_reduce (segment reads plus random 64-B slot read-modify-writes) x1.
+WRITE_SIZE * 1024 is taken as is.  Usage: pmc_summary.py FETCH_CSV WRITE_CSV
+OUT_JSON LINES STEPS_TOTAL (STEPS_TOTAL = warmup + timed steps of the profiled
+bench run, + 1 untimed stats step when the run had one)."""
 import csv
 import json
 import sys
@@ -36,25 +40,27 @@ def main():
     # every pass-1 launch of every slice: classification, deferred tails,
     # aggregation (record append, region histogram, region scatter, per-region
     # reduction) -- the kernels bracketed by the pass-1 HIP events
-    kinds = ('k_classify', 'k_tail', 'k_count', 'k_aggregate', 'k_part_hist', 'k_scan_blocks', 'k_scan_sums',
-             'k_scan_add', 'k_part_scatter', 'k_seg_starts', 'k_reduce<1>')
+    kinds = ('k_classify', 'k_tail', 'k_count<', 'k_count_flush', 'k_aggregate', 'k_part_hist', 'k_scan_blocks',
+             'k_scan_sums', 'k_scan_add', 'k_part_scatter', 'k_seg_starts', 'k_hot_plan', 'k_hot_combine<1>',
+             'k_reduce<1>', 'k_cap_mark', 'k_cap_scatter', 'k_cap_select')
     # pass-1 launches only: the classifier instantiated with emission (the
     # classify-only launches of bench's untimed checks are excluded)
     pick = lambda name: any(k in name for k in kinds) and not ('k_classify' in name and 'false>' in name) and \
         not ('k_tail' in name and 'false>' in name)
-    fk = [v for d, v in sorted(f.items()) if pick(fn[d])]
-    wk = [v for d, v in sorted(w.items()) if pick(wn[d])]
-    read = 2 * 1024 * sum(fk) / steps
-    write = 1024 * sum(wk) / steps
+    factor = lambda name: 1.0 if 'k_reduce' in name else 2.0
+    read = 1024 * sum(v * factor(fn[d]) for d, v in f.items() if pick(fn[d])) / steps
+    write = 1024 * sum(v for d, v in w.items() if pick(wn[d])) / steps
     split = {}
     for k in kinds:
-        split[k] = {'read_bytes_per_step': 2 * 1024 * sum(v for d, v in f.items() if k in fn[d] and pick(fn[d])) / steps,
+        split[k] = {'read_bytes_per_step': 1024 * sum(v * factor(fn[d]) for d, v in f.items()
+                                                      if k in fn[d] and pick(fn[d])) / steps,
                     'write_bytes_per_step': 1024 * sum(v for d, v in w.items() if k in wn[d] and pick(wn[d])) / steps}
     res = {'hbm_bytes_per_step': read + write, 'read_bytes_per_step': read, 'write_bytes_per_step': write,
            'lines_per_step': lines, 'steps_seen': steps, 'bytes_per_line': (read + write) / lines,
            'kernels': split,
            'method': 'rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes), pass-1 launches, '
-                     'FETCH_SIZE x2 gfx950 correction'}
+                     'FETCH_SIZE x2 for the streaming kernels and x1 for k_reduce (calibrated: '
+                     'profiles/r03l_fetch_calibration.json)'}
     json.dump(res, open(out, 'w'), indent=1)
     print(json.dumps(res))
 
