@@ -371,7 +371,7 @@ def roofline_block(lines, classify_ms, aggregate_ms, launches, step_ms, pmc, sq,
     return {
         'bound': 'hbm', 'kernel': 'k_classify', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
         'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
-        'traffic_unit': 'HBM bytes per k_classify launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)',
+        'traffic_unit': 'HBM bytes per k_classify launch (rocprofv3 FETCH_SIZE x2, calibrated for its streaming reads in profiles/r03l_fetch_calibration.json, + WRITE_SIZE)',
         'traffic_source': 'profiles/%s_pass1_pmc.json' % config if traffic is not None else None,
         'launches_per_step': launches, 'ms_per_launch': ms_launch, 'algorithmic_bytes_per_launch': per_launch_bytes,
         'bytes_per_line': BYTES_PER_LINE,

@@ -1224,6 +1224,181 @@ __global__ __launch_bounds__(1024) void k_count(const uint32_t* __restrict__ gh,
   }
 }
 
+// ---- Per-rule counters past the LDS histogram (rule sets > kCnt, BASELINE
+// config 4's 3.45M rules): one device atomic per line (k_count<0>) runs at
+// ~13 G lines/s against memory-side atomics, so the gid|hit words are instead
+// counting-sorted by rule block (kCntBlock consecutive rules) and every block
+// counted in LDS:
+//   k_cnt_hist / exclusive scan / k_cnt_scatter   words grouped by block
+//   k_seg_starts / k_cnt_plan                      block segments cut into tasks
+//                                                  of <= kCntChunk words
+//   k_cnt_reduce                                   one LDS histogram per task,
+//                                                  added to matches/hits (plain
+//                                                  read-modify-write when the task
+//                                                  is its block's only one)
+// 16 B of streaming traffic per line instead of one scattered atomic.
+constexpr int kMaxRegions = 4096;   // table regions (and count blocks) per partition
+constexpr uint32_t kCntBits = 13, kCntBlock = 1u << kCntBits;
+constexpr uint32_t kCntChunk = 1u << 18;
+
+struct CntTask {
+  unsigned long long beg, end;
+  uint32_t block, single;
+};
+
+// lanes whose key equals the first active lane's: that lane adds their count
+// (one LDS atomic instead of up to 64 on one address); returns whether this
+// lane's own add is still due
+__device__ __forceinline__ bool wave_peer_add(bool act, uint32_t key, uint32_t* cnt, uint32_t add_hits,
+                                              bool h, uint32_t* hcnt) {
+  const unsigned long long pending = __ballot(act);
+  if (!pending) return false;
+  const int leader = __builtin_ctzll(pending);
+  const uint32_t k = __builtin_amdgcn_readlane(key, leader);
+  const unsigned long long peers = __ballot(act && key == k);
+  const unsigned long long hm = add_hits ? __ballot(act && h) : 0ull;
+  if ((int)__lane_id() == leader) {
+    atomicAdd(&cnt[k], (uint32_t)__popcll(peers));
+    const uint32_t hh = (uint32_t)__popcll(peers & hm);
+    if (hh) atomicAdd(&hcnt[k], hh);
+  }
+  return act && key != k;
+}
+
+__global__ __launch_bounds__(1024) void k_cnt_hist(const uint32_t* __restrict__ gh, unsigned long long n,
+                                                   uint32_t n_blocks, uint32_t n_tiles, uint32_t tile_len,
+                                                   uint32_t* __restrict__ hist) {
+  __shared__ uint32_t hc[kMaxRegions];
+  const uint32_t tile = blockIdx.x;
+  for (uint32_t b = threadIdx.x; b < n_blocks; b += blockDim.x) hc[b] = 0;
+  __syncthreads();
+  const unsigned long long beg = (unsigned long long)tile * tile_len;
+  const unsigned long long end = beg + tile_len < n ? beg + tile_len : n;
+  for (unsigned long long base = beg; base < end; base += 4ull * blockDim.x) {   // block-uniform trip count
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const unsigned long long i = base + (unsigned long long)k * blockDim.x + threadIdx.x;
+      w[k] = i < end ? gh[i] : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool act = w[k] != 0xFFFFFFFFu;
+      const uint32_t b = (w[k] & 0x7FFFFFFFu) >> kCntBits;
+      if (wave_peer_add(act, b, hc, 0, false, nullptr)) atomicAdd(&hc[b], 1u);
+    }
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < n_blocks; b += blockDim.x) hist[(size_t)b * n_tiles + tile] = hc[b];
+}
+
+__global__ __launch_bounds__(1024) void k_cnt_scatter(const uint32_t* __restrict__ gh, unsigned long long n,
+                                                      uint32_t n_blocks, uint32_t n_tiles, uint32_t tile_len,
+                                                      const uint32_t* __restrict__ offs, uint32_t* __restrict__ out) {
+  __shared__ uint32_t cur[kMaxRegions];
+  const uint32_t tile = blockIdx.x;
+  for (uint32_t b = threadIdx.x; b < n_blocks; b += blockDim.x) cur[b] = offs[(size_t)b * n_tiles + tile];
+  __syncthreads();
+  const unsigned long long beg = (unsigned long long)tile * tile_len;
+  const unsigned long long end = beg + tile_len < n ? beg + tile_len : n;
+  const uint32_t lane = __lane_id();
+  for (unsigned long long base = beg; base < end; base += 4ull * blockDim.x) {
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const unsigned long long i = base + (unsigned long long)k * blockDim.x + threadIdx.x;
+      w[k] = i < end ? gh[i] : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool act = w[k] != 0xFFFFFFFFu;
+      const uint32_t b = (w[k] & 0x7FFFFFFFu) >> kCntBits;
+      // the first active lane's block: one cursor bump for all its peers
+      const unsigned long long pending = __ballot(act);
+      if (!pending) continue;
+      const int leader = __builtin_ctzll(pending);
+      const uint32_t bl = __builtin_amdgcn_readlane(b, leader);
+      const unsigned long long peers = __ballot(act && b == bl);
+      uint32_t at = 0;
+      if ((int)lane == leader) at = atomicAdd(&cur[bl], (uint32_t)__popcll(peers));
+      at = __builtin_amdgcn_readlane(at, leader);
+      if (act && b == bl) {
+        out[at + (uint32_t)__popcll(peers & ((1ull << lane) - 1ull))] = w[k];
+      } else if (act) {
+        out[atomicAdd(&cur[b], 1u)] = w[k];
+      }
+    }
+  }
+}
+
+// One workgroup: block segments [starts[b], starts[b+1]) cut into tasks of at
+// most `chunk` words; ctl[0] = the task count.
+__global__ __launch_bounds__(1024) void k_cnt_plan(const unsigned long long* __restrict__ starts, uint32_t n_blocks,
+                                                   uint32_t chunk, CntTask* __restrict__ tasks, uint32_t max_tasks,
+                                                   uint32_t* __restrict__ ctl) {
+  __shared__ uint32_t sh[18];
+  uint32_t carry = 0;
+  for (uint32_t b0 = 0; b0 < n_blocks; b0 += blockDim.x) {
+    const uint32_t b = b0 + threadIdx.x;
+    const unsigned long long s = b < n_blocks ? starts[b] : 0, e = b < n_blocks ? starts[b + 1] : 0;
+    const uint32_t k = (uint32_t)((e - s + chunk - 1) / chunk);
+    uint32_t total;
+    const uint32_t off = carry + block_exscan(k, sh, &total);
+    for (uint32_t q = 0; q < k && off + q < max_tasks; ++q) {
+      CntTask t;
+      t.beg = s + (unsigned long long)q * chunk;
+      t.end = t.beg + chunk < e ? t.beg + chunk : e;
+      t.block = b;
+      t.single = k == 1;
+      tasks[off + q] = t;
+    }
+    carry += total;
+  }
+  if (threadIdx.x == 0) ctl[0] = carry < max_tasks ? carry : max_tasks;
+}
+
+__global__ __launch_bounds__(1024) void k_cnt_reduce(const uint32_t* __restrict__ words,
+                                                     const CntTask* __restrict__ tasks, const uint32_t* __restrict__ ctl,
+                                                     uint32_t n_rules, unsigned long long* __restrict__ matches,
+                                                     unsigned long long* __restrict__ hits) {
+  __shared__ uint32_t cm[kCntBlock], ch[kCntBlock];
+  if (blockIdx.x >= ctl[0]) return;   // workgroup-uniform
+  const CntTask t = tasks[blockIdx.x];
+  for (uint32_t r = threadIdx.x; r < kCntBlock; r += blockDim.x) cm[r] = ch[r] = 0;
+  __syncthreads();
+  for (unsigned long long base = t.beg; base < t.end; base += 4ull * blockDim.x) {
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const unsigned long long i = base + (unsigned long long)k * blockDim.x + threadIdx.x;
+      w[k] = i < t.end ? words[i] : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool act = w[k] != 0xFFFFFFFFu;
+      const uint32_t r = w[k] & (kCntBlock - 1u);
+      const bool h = act && (w[k] >> 31);
+      if (wave_peer_add(act, r, cm, 1, h, ch)) {
+        atomicAdd(&cm[r], 1u);
+        if (h) atomicAdd(&ch[r], 1u);
+      }
+    }
+  }
+  __syncthreads();
+  const uint32_t r0 = t.block << kCntBits;
+  for (uint32_t r = threadIdx.x; r < kCntBlock && r0 + r < n_rules; r += blockDim.x) {
+    const uint32_t m = cm[r], h = ch[r];
+    if (!m) continue;
+    if (t.single) {
+      matches[r0 + r] += m;
+      if (h) hits[r0 + r] += h;
+    } else {
+      atomicAdd(&matches[r0 + r], (unsigned long long)m);
+      if (h) atomicAdd(&hits[r0 + r], (unsigned long long)h);
+    }
+  }
+}
+
 // ---- Pass 1b — the reducer's aggregation of classified lines
 // (connlist-reducer.py:62-79,146-176), as an on-chip shuffle.
 //
@@ -1326,7 +1501,6 @@ __global__ __launch_bounds__(1024) void k_aggregate(const uint4* __restrict__ T,
 // tile]) so that its exclusive scan gives every (region, tile) run its output
 // offset.
 constexpr uint32_t kPartTileMin = 8192, kPartTileMax = 262144, kPartTilesWant = 384;
-constexpr int kMaxRegions = 4096;
 
 // Both partition kernels walk their tile as groups of kPartW windows per wave:
 // the group's window counts are wave-uniform (scalar) loads, and the live
@@ -2555,6 +2729,16 @@ struct rsa_ctx {
   uint32_t* d_hot_fill = nullptr;           // [kMaxRegions]
   uint32_t* d_hot_ctl = nullptr;            // [4]: tasks planned, task cursor
   unsigned long long* d_hot_total = nullptr;
+  // per-rule counters by rule block (k_cnt_*), rule sets > kCnt
+  bool count_sort = true;                   // RSA_OPT_COUNT_SORT
+  uint32_t* d_cnt_words = nullptr;          // gid|hit words grouped by rule block
+  unsigned long long cnt_words_alloc = 0;
+  unsigned long long* d_cnt_starts = nullptr;
+  unsigned long long cnt_starts_alloc = 0;
+  CntTask* d_cnt_tasks = nullptr;
+  unsigned long long cnt_tasks_alloc = 0;
+  uint32_t* d_cnt_ctl = nullptr;
+  unsigned long long cnt_ctl_alloc = 0;
   bool auto_tighten = true;
   bool tightened = false;
   uint32_t profile_skip = 0;
@@ -2956,6 +3140,37 @@ int prepare_records(rsa_ctx* c, uint64_t m) {
   return rc;
 }
 
+// Per-rule counters of m gid|hit words by rule block (rule sets > kCnt, at
+// most kMaxRegions blocks): see k_cnt_hist.
+int count_by_block(rsa_ctx* c, const uint32_t* gh, uint64_t m) {
+  const uint32_t n_blocks = (c->n_rules + kCntBlock - 1) >> kCntBits;
+  uint32_t tile_len = kPartTileMin;
+  while (tile_len < kPartTileMax && (unsigned long long)tile_len * 2 * kPartTilesWant <= m) tile_len <<= 1;
+  const uint32_t n_tiles = (uint32_t)((m + tile_len - 1) / tile_len);
+  const unsigned long long hl = (unsigned long long)n_blocks * n_tiles;
+  const unsigned long long max_tasks = m / kCntChunk + n_blocks + 1;
+  int rc = ensure_buf(c, &c->d_hist, &c->hist_alloc, hl);
+  if (!rc) rc = ensure_buf(c, &c->d_cnt_words, &c->cnt_words_alloc, m);
+  if (!rc) rc = ensure_buf(c, &c->d_cnt_starts, &c->cnt_starts_alloc, n_blocks + 1);
+  if (!rc) rc = ensure_buf(c, &c->d_cnt_tasks, &c->cnt_tasks_alloc, max_tasks);
+  if (!rc) rc = ensure_buf(c, &c->d_cnt_ctl, &c->cnt_ctl_alloc, 4);
+  if (rc) return rc;
+  k_cnt_hist<<<n_tiles, 1024, 0, c->stream>>>(gh, m, n_blocks, n_tiles, tile_len, c->d_hist);
+  HIPCHK(c, hipGetLastError());
+  uint32_t* total = nullptr;
+  rc = exclusive_scan(c, c->d_hist, hl, &total);
+  if (rc) return rc;
+  k_cnt_scatter<<<n_tiles, 1024, 0, c->stream>>>(gh, m, n_blocks, n_tiles, tile_len, c->d_hist, c->d_cnt_words);
+  k_seg_starts<<<(n_blocks + 1 + 255) / 256, 256, 0, c->stream>>>(c->d_hist, n_tiles, n_blocks, 0, total,
+                                                                  c->d_cnt_starts);
+  k_cnt_plan<<<1, 1024, 0, c->stream>>>(c->d_cnt_starts, n_blocks, kCntChunk, c->d_cnt_tasks, (uint32_t)max_tasks,
+                                        c->d_cnt_ctl);
+  k_cnt_reduce<<<(unsigned)max_tasks, 1024, 0, c->stream>>>(c->d_cnt_words, c->d_cnt_tasks, c->d_cnt_ctl, c->n_rules,
+                                                            c->d_matches, c->d_hits);
+  HIPCHK(c, hipGetLastError());
+  return RSA_OK;
+}
+
 // Pass 1b over lines [a, a + m) of the batch: the per-rule counters (k_count
 // over the gid|hit words `gh` of a classifying pass 1a, or k_aggregate over
 // given gids, which also writes the line-indexed records), then the counting
@@ -2971,6 +3186,9 @@ int launch_aggregate(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsig
       const uint64_t units = (m + 3) / 4;
       if (c->n_rules <= (uint32_t)kCnt) {
         k_count<kCnt><<<grid_for_threads(c, units, 1024, RSA_COUNT_PER_CU), 1024, 0, c->stream>>>(gh, m, c->n_rules, ag);
+      } else if (c->count_sort && ((c->n_rules + kCntBlock - 1) >> kCntBits) <= (uint32_t)kMaxRegions) {
+        const int rc2 = count_by_block(c, gh, m);
+        if (rc2) return rc2;
       } else {
         k_count<0><<<grid_for_threads(c, units, 1024, 8), 1024, 0, c->stream>>>(gh, m, c->n_rules, ag);
         k_count_flush<<<grid_for(c, c->n_rules, 8), kBlock, 0, c->stream>>>(c->d_packed, c->n_rules, c->d_matches,
@@ -3176,7 +3394,8 @@ int rsa_ctx_destroy(rsa_ctx* c) {
                   c->d_scan_sums, c->d_occ, c->d_entries, c->d_off,
                   c->d_img, c->d_resid,
                   c->d_slots, c->d_used, c->d_used_n, c->d_filter, c->d_packed, c->d_hot, c->d_hot_tasks, c->d_hot_base,
-                  c->d_hot_fill, c->d_hot_ctl, c->d_hot_total, c->d_flags, c->d_cursor, c->d_cidx,
+                  c->d_hot_fill, c->d_hot_ctl, c->d_hot_total, c->d_cnt_words, c->d_cnt_starts,
+                  c->d_cnt_tasks, c->d_cnt_ctl, c->d_flags, c->d_cursor, c->d_cidx,
                   c->d_capped_gid, c->d_capped_cnt, c->d_capped_start, c->d_keys};
   for (void* b : bufs) (void)hipFree(b);
   for (int k = 0; k < kMaxEvents; ++k)
@@ -3231,6 +3450,9 @@ int rsa_set_option(rsa_ctx* c, int option, int64_t value) {
       return RSA_OK;
     case RSA_OPT_REGION_IMPORT:
       c->region_import = value != 0;
+      return RSA_OK;
+    case RSA_OPT_COUNT_SORT:
+      c->count_sort = value != 0;
       return RSA_OK;
     case RSA_OPT_HOT_SPLIT:
       c->hot_split = value != 0;

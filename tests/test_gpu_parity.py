@@ -322,3 +322,35 @@ def test_hot_split_off_equals_on(engine):
                        interfaces=('outside', 'partner'), broad=False)
     finally:
         engine.set_option(native.RSA_OPT_HOT_SPLIT, 1)
+
+
+@pytest.mark.parametrize('zipf,n_lines', [(None, 2_000_000), (1.2, 3_000_000)])
+def test_count_by_rule_block_past_lds(engine, zipf, n_lines):
+    """20000 rules (past the 13312 LDS counters): the per-rule line and hit
+    counters by rule-block counting sort (k_cnt_*; >2^18 lines in a block, so
+    blocks split into several tasks) equal one device atomic per
+    line (RSA_OPT_COUNT_SORT=0) and the host's bincount of the pass-1 gids."""
+    from ruleset_analysis_amd.compile import F_HIT
+    dbj, info = synth.make_db(71, 20000, broad=False)
+    tr = synth.make_traffic((dbj, info), n_lines, seed=72, zipf=zipf)
+    compiled = CompiledRules(acldb.load_json(dbj))
+    tup, ts, order = synth.pack(tr, compiled)
+    engine.load_compiled(compiled)
+    out = []
+    for on in (1, 0):
+        engine.set_option(native.RSA_OPT_COUNT_SORT, on)
+        try:
+            b = DeviceBatch.from_numpy(tup, ts, order, engine.device)
+            res = engine.run([b], 1000, capacity=max(built_hit_count(tup), 1))
+            out.append((res.matches.copy(), res.hits.copy(), engine.last_gids[0].cpu().numpy()))
+        finally:
+            engine.set_option(native.RSA_OPT_COUNT_SORT, 1)
+    (m1, h1, g1), (m0, h0, g0) = out
+    assert np.array_equal(g1, g0)
+    assert np.array_equal(m1, m0) and np.array_equal(h1, h0)
+    nr = len(m1)
+    ok = g1 >= 0
+    assert np.array_equal(m1, np.bincount(g1[ok], minlength=nr))
+    hit = ok & ((tup['flags'] & F_HIT) != 0)
+    assert np.array_equal(h1, np.bincount(g1[hit], minlength=nr))
+    assert np.bincount(g1[ok] >> 13).max() > 1 << 18          # a block of several tasks
