@@ -28,6 +28,7 @@ from .compile import TUPLE_DTYPE, F_VALID, F_HIT, F_BUILT, F_SWAP
 from .firewallrule import FirewallRule
 from .ipaddr import IP
 from .py2text import PY2_WS, py2_int
+from .keytext import INTERNED, KeyText
 
 __all__ = ['ParsedLog', 'parse_logs', 'get_builtconn', 'BUILT', 'PY2_WS', 'reducer_fields',
            'D_IGNORE', 'D_NOACL', 'D_MISSING', 'D_CLASSIFY']
@@ -107,15 +108,19 @@ class ParsedLog(object):
         self.pspell_table = []
         self.error = None          # (line index, exception) — the mapper dies there
         self.n = 0
+        self.keytext = None        # report.KeyText of the interned (non-canonical) reducer keys
+        self.keyx = {}             # line index -> (pspell | INTERNED, from id, to id, port id)
 
 
-def parse_logs(inputs, db, compiled, pspell_table=None, need_order=True):
+def parse_logs(inputs, db, compiled, pspell_table=None, need_order=True, keytext=None):
     """inputs: iterable of (host, list_of_lines).  Lines keep their '\\n'.
+    ``keytext``: a report.KeyText shared with other parses (a new one if None).
 
     Stops at the first line where the reference mapper would raise; the
     exception and line index are kept in ``.error`` and everything before it is
     parsed (the drop-in mapper prints that prefix and then re-raises)."""
     P = ParsedLog()
+    P.keytext = keytext if keytext is not None else KeyText()
     pspell = {} if pspell_table is None else {s: i for i, s in enumerate(pspell_table)}
     rows = []
     disp = []
@@ -197,20 +202,56 @@ def _parse_one(line, host, fw, acls, compiled, pspell, P, i):
     if res is not None:
         flags |= F_BUILT
         for_ip, to_ip, to_port = res[6], res[8], res[9]
+        if hit:
+            ts = reducer_timestamp(res)
+        word = res[5]
+        if word not in pspell:
+            if len(pspell) >= INTERNED:
+                raise NotImplementedError('more than %d protocol spellings' % INTERNED)
+            pspell[word] = len(pspell)
+        ps = pspell[word]
+        # the reducer keys its dict by the strings (connlist-reducer.py:167):
+        # canonical text that names the tuple's own fields is carried as the
+        # tuple's values, anything else as interned text
         if (for_ip, to_ip, to_port) == (d['src'], d['dst'], d['dport']):
             pass
         elif (for_ip, to_ip, to_port) == (d['dst'], d['src'], d['sport']):
             flags |= F_SWAP
         else:
-            raise NotImplementedError('reducer key does not map onto the connection tuple: %r' % line)
-        if _canonical_v4(for_ip) is None or _canonical_v4(to_ip) is None or str(int(to_port)) != to_port:
-            raise NotImplementedError('non-canonical address/port text in BUILT message: %r' % line)
-        if hit:
-            ts = reducer_timestamp(res)
-        word = res[5]
-        if word not in pspell:
-            if len(pspell) >= 256:
-                raise NotImplementedError('more than 256 protocol spellings')
-            pspell[word] = len(pspell)
-        ps = pspell[word]
+            for_ip = None
+        if for_ip is None or not _canonical_key(for_ip, to_ip, to_port):
+            kt = P.keytext
+            P.keyx[i] = (ps | INTERNED, kt(res[6]), kt(res[8]), kt(res[9]))
+            if len(kt.values) > 0xFFFF:
+                raise NotImplementedError('more than 65536 distinct non-canonical key strings')
     return (src_ip.ip, dst_ip.ip, sport, dport, lid, flags, ps), D_CLASSIFY, ts
+
+
+def _canonical_key(for_ip, to_ip, to_port):
+    try:
+        return _canonical_v4(for_ip) is not None and _canonical_v4(to_ip) is not None and \
+            str(int(to_port)) == to_port
+    except ValueError:
+        return False
+
+
+def key_tuples(torch, tuples, keyx):
+    """The aggregation tuples (int32 [n, 4] tensor) of classified lines: rows
+    of lines with interned keys (``keyx``) carry the key ids in place of the
+    connection (src = from id, dst = to id, dport = port id, no swap) -- what
+    the device aggregates given the gids.  Returns ``tuples`` itself when
+    there are none."""
+    if not keyx:
+        return tuples
+    idx = np.fromiter(keyx.keys(), np.int64, len(keyx))
+    rows = np.zeros(len(idx), TUPLE_DTYPE)
+    vals = np.array(list(keyx.values()), np.int64).reshape(-1, 4)
+    old = tuples[torch.from_numpy(idx).to(tuples.device)].cpu().numpy().view(TUPLE_DTYPE).reshape(-1)
+    rows['src'], rows['dst'], rows['sport'], rows['dport'] = vals[:, 1], vals[:, 2], 0, vals[:, 3]
+    rows['list'] = old['list']
+    rows['flags'] = old['flags'] & np.uint8(0xFF ^ F_SWAP)
+    rows['pspell'] = vals[:, 0]
+    out = tuples.clone()
+    out[torch.from_numpy(idx).to(tuples.device)] = torch.from_numpy(rows.view(np.int32).reshape(-1, 4)).to(
+        tuples.device)
+    return out

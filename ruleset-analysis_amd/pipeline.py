@@ -12,7 +12,8 @@ import numpy as np
 
 from .compile import CompiledRules, F_HIT, F_BUILT
 from .engine import Engine, DeviceBatch
-from .logparse import parse_logs, D_CLASSIFY, D_MISSING
+from .keytext import KeyText
+from .logparse import parse_logs, key_tuples, D_CLASSIFY, D_MISSING
 from .report import reducer_report
 
 __all__ = ['analyze', 'analyze_text', 'assemble_report', 'built_hit_count']
@@ -54,7 +55,8 @@ def assemble_report(parsed, gids, results, compiled, cap, ts_decode=None, pspell
         ts_decode = getattr(parsed, 'ts_decode', None) or parsed.ts_table.__getitem__
     if pspell_table is None:
         pspell_table = parsed.pspell_table
-    return reducer_report(results, groups, noise, cap, ts_decode, pspell_table, n_blank=n_blank)
+    return reducer_report(results, groups, noise, cap, ts_decode, pspell_table, n_blank=n_blank,
+                          keytext=getattr(parsed, 'keytext', None))
 
 
 def analyze(inputs, db, cap=1000, device=0, engine=None):
@@ -66,8 +68,17 @@ def analyze(inputs, db, cap=1000, device=0, engine=None):
     eng = engine if engine is not None else Engine(device)
     eng.load_compiled(compiled)
     batch = DeviceBatch.from_numpy(parsed.tuples, parsed.ts, parsed.order, eng.device)
-    results = eng.run([batch], cap, capacity=max(built_hit_count(parsed.tuples), 1))
-    gids = eng.last_gids[0].cpu().numpy() if parsed.n else np.zeros(0, np.int32)
+    cap_n = max(built_hit_count(parsed.tuples), 1)
+    if parsed.keyx:
+        # lines with interned reducer keys: classified on their tuples,
+        # aggregated under their key ids (logparse.key_tuples)
+        g = eng.classify_only(batch)
+        agg = DeviceBatch(key_tuples(eng.torch, batch.tuples, parsed.keyx), batch.ts, batch.order, g)
+        results = eng.run([agg], cap, capacity=cap_n)
+        gids = g.cpu().numpy()
+    else:
+        results = eng.run([batch], cap, capacity=cap_n)
+        gids = eng.last_gids[0].cpu().numpy() if parsed.n else np.zeros(0, np.int32)
     return assemble_report(parsed, gids, results, compiled, cap), results
 
 
@@ -83,9 +94,10 @@ def analyze_text(inputs, db, cap=1000, device=0, engine=None):
     compiled.ensure_lists()
     eng = engine if engine is not None else Engine(device)
     torch = eng.torch
-    parts, pspell = [], {}
+    parts, pspell, keytext = [], {}, KeyText()
     for host, data in inputs:
-        p = textparse.parse_text(eng, host, data, db, compiled, pspell=pspell, need_order=False, keep_text=True)
+        p = textparse.parse_text(eng, host, data, db, compiled, pspell=pspell, need_order=False, keep_text=True,
+                                 keytext=keytext)
         parts.append(p)
         if p.error is not None:
             break
@@ -109,6 +121,6 @@ def analyze_text(inputs, db, cap=1000, device=0, engine=None):
     hb = (flags & both) == both
     textparse.order_keys_global(eng, parts, group=torch.where(hb & (gids >= 0), gids, torch.full_like(gids, -1)))
     parsed = textparse.concat(parts, torch)
-    batch = DeviceBatch(parsed.tuples, parsed.ts, parsed.order, gids)
+    batch = DeviceBatch(key_tuples(torch, parsed.tuples, parsed.keyx), parsed.ts, parsed.order, gids)
     results = eng.run([batch], cap, capacity=max(int(hb.sum().item()), 1))
     return assemble_report(parsed, gids.cpu().numpy(), results, compiled, cap), results

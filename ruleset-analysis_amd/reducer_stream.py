@@ -39,24 +39,11 @@ from . import textparse
 from .compile import F_BUILT, F_HIT, TUPLE_DTYPE
 from .logparse import reducer_fields, reducer_timestamp, _canonical_v4
 from .py2text import PY2_WS, py2_int
-from .report import HEADER, NOISE1, MemoDecode, _rows_by_gid, dotted_list, table_rows
+from .report import HEADER, INTERNED, NOISE1, KeyText, MemoDecode, _rows_by_gid, key_strings, table_rows
 
 __all__ = ['ReducerStream']
 
 RED_KEYED, RED_NOISE, RED_SAME = 0, 1, 0x100
-INTERNED = 0x80
-
-
-class _Interner(object):
-    def __init__(self):
-        self.ids, self.values = {}, []
-
-    def __call__(self, v):
-        k = self.ids.get(v)
-        if k is None:
-            k = self.ids[v] = len(self.values)
-            self.values.append(v)
-        return k
 
 
 class ReducerStream(object):
@@ -68,7 +55,7 @@ class ReducerStream(object):
         self.chunk = max(int(chunk), 1)
         self.pending = b''
         self.spells = list(textparse.DEFAULT_SPELLS)      # device spelling ids (<= 64, < 0x80)
-        self.istr = _Interner()                           # interned text of non-canonical keys
+        self.istr = KeyText()                             # interned text of non-canonical keys
         self.need = self.chunk                            # bytes to gather before the next chunk is processed
         self.lines_done = 0
 
@@ -275,24 +262,6 @@ class ReducerStream(object):
         res = eng.run([b], self.cap, capacity=max(int(hb.sum()), 1))
         return res, ts_decode
 
-    def _strings(self, rows):
-        """The key strings (PROTO, FROMIP, TOIP, TOPORT) of one rule's records:
-        canonical values printed back, interned text looked up."""
-        ps = rows['pspell'].tolist()
-        if not any(p & INTERNED for p in ps):
-            return ([self.spells[p] for p in ps], dotted_list(rows['for_ip']), dotted_list(rows['to_ip']),
-                    [str(p) for p in rows['to_port'].tolist()])
-        s = self.istr.values
-        out = ([], [], [], [])
-        for p, f, t, q in zip(ps, rows['for_ip'].tolist(), rows['to_ip'].tolist(), rows['to_port'].tolist()):
-            if p & INTERNED:
-                vals = (self.spells[p & ~INTERNED], s[f], s[t], s[q])
-            else:
-                vals = (self.spells[p], dotted_list([f])[0], dotted_list([t])[0], str(q))
-            for col, x in zip(out, vals):
-                col.append(x)
-        return out
-
     def _report(self, events, runs, res, ts_decode, mode):
         """connlist-reducer.py's stdout for these events: noise pairs at their
         lines, a block per run when the next one starts; mode 'final' (input
@@ -315,7 +284,7 @@ class ReducerStream(object):
             lines.append(HEADER)
             rows = by_run.get(r)
             if rows is not None and len(rows):
-                lines.extend(table_rows(rows, *self._strings(rows), ts_decode))
+                lines.extend(table_rows(rows, *key_strings(rows, self.spells, self.istr), ts_decode))
             return lines
 
         prev = None

@@ -17,9 +17,10 @@
 import numpy as np
 
 from .logparse import PY2_WS, D_CLASSIFY, D_MISSING
+from .keytext import INTERNED, KeyText
 from .py2dict import iteration_order
 
-__all__ = ['mapper_output', 'reducer_report', 'block_lines', 'HEADER', 'dotted']
+__all__ = ['mapper_output', 'reducer_report', 'block_lines', 'HEADER', 'dotted', 'KeyText', 'INTERNED']
 
 HEADER = '%6s %4s  %-15s %-14s %-5s %-19s  %-19s' % ('COUNT', 'PROTO', 'FROM IP', 'TO IP', 'PORT', 'FIRST SEEN',
                                                      'LAST SEEN')
@@ -86,6 +87,14 @@ def dotted_list(values):
             for v in (values.tolist() if hasattr(values, 'tolist') else values)]
 
 
+def key_strings(rows, spells, keytext=None):
+    """(PROTO, FROMIP, TOIP, TOPORT) strings of one rule's records."""
+    if keytext is None or not (rows['pspell'] & INTERNED).any():
+        return ([spells[p] for p in rows['pspell'].tolist()], dotted_list(rows['for_ip']),
+                dotted_list(rows['to_ip']), [str(p) for p in rows['to_port'].tolist()])
+    return keytext.strings(rows, spells)
+
+
 class MemoDecode(object):
     """A timestamp decoder with a memo: a report's rows share few distinct codes."""
 
@@ -112,7 +121,7 @@ def table_rows(rows, spell, from_ip, to_ip, to_port, ts_decode):
             for k in table_order(spell, from_ip, to_ip, to_port, rows['min_order'])]
 
 
-def block_lines(host, acl, rule, hits, rows, capped, cap, ts_decode, pspell_table):
+def block_lines(host, acl, rule, hits, rows, capped, cap, ts_decode, pspell_table, keytext=None):
     """One rule block without the leading blank line (connlist-reducer.py:113-126)."""
     out = ['{0}: access-list {1}, rule {2}: {3}'.format(host, acl, rule.ruleindex, str(rule)),
            '{0}'.format(rule.original), 'Total number of hits: {0}'.format(int(hits))]
@@ -121,13 +130,11 @@ def block_lines(host, acl, rule, hits, rows, capped, cap, ts_decode, pspell_tabl
                    'displayed.'.format(cap))
     out.append(HEADER)
     if rows is not None and len(rows):
-        spell = [pspell_table[p] for p in rows['pspell'].tolist()]
-        out.extend(table_rows(rows, spell, dotted_list(rows['for_ip']), dotted_list(rows['to_ip']),
-                              [str(p) for p in rows['to_port'].tolist()], ts_decode))
+        out.extend(table_rows(rows, *key_strings(rows, pspell_table, keytext), ts_decode))
     return out
 
 
-def reducer_report(results, groups, noise, cap, ts_decode, pspell_table, n_blank=0):
+def reducer_report(results, groups, noise, cap, ts_decode, pspell_table, n_blank=0, keytext=None):
     """Reducer stdout lines.
 
     ``groups``: list of (sort_key, gid, host, acl, rule) for every aggregation
@@ -135,6 +142,7 @@ def reducer_report(results, groups, noise, cap, ts_decode, pspell_table, n_blank
     ``noise``: list of (position_key, raw_text) non-key records; a record is
     emitted before group g iff position_key < g's sort_key.  ``n_blank`` empty
     records (the mapper's doubled newlines) sort before everything else.
+    ``keytext``: the KeyText of records with interned keys.
     """
     rows = _rows_by_gid(results.records)
     ts_decode = MemoDecode(ts_decode)
@@ -149,7 +157,7 @@ def reducer_report(results, groups, noise, cap, ts_decode, pspell_table, n_blank
             ni += 1
         if prev is not None:
             out.append('')
-            out.extend(_block(prev, results, rows, cap, ts_decode, pspell_table))
+            out.extend(_block(prev, results, rows, cap, ts_decode, pspell_table, keytext))
         prev = (gid, host, acl, rule)
     while ni < len(noise):
         out.append(NOISE1)
@@ -157,11 +165,12 @@ def reducer_report(results, groups, noise, cap, ts_decode, pspell_table, n_blank
         ni += 1
     out.append('')
     if prev is not None:
-        out.extend(_block(prev, results, rows, cap, ts_decode, pspell_table))
+        out.extend(_block(prev, results, rows, cap, ts_decode, pspell_table, keytext))
     return out
 
 
-def _block(prev, results, rows, cap, ts_decode, pspell_table):
+def _block(prev, results, rows, cap, ts_decode, pspell_table, keytext=None):
     gid, host, acl, rule = prev
     capped = cap == 0 or int(results.thresh[gid]) != 0xFFFFFFFFFFFFFFFF
-    return block_lines(host, acl, rule, results.hits[gid], rows.get(gid), capped, cap, ts_decode, pspell_table)
+    return block_lines(host, acl, rule, results.hits[gid], rows.get(gid), capped, cap, ts_decode, pspell_table,
+                       keytext)

@@ -22,6 +22,7 @@ import numpy as np
 
 from . import logparse
 from .compile import F_BUILT, F_HIT, TUPLE_DTYPE
+from .keytext import INTERNED, KeyText
 
 __all__ = ['IFC_DTYPE', 'SPELL_DTYPE', 'LINE_IGNORE', 'LINE_NOACL', 'LINE_MISSING', 'LINE_CLASSIFY', 'LINE_HOST',
            'DEFAULT_SPELLS', 'ts_pack', 'ts_unpack', 'interface_table', 'spell_table', 'ParsedText', 'parse_text',
@@ -190,6 +191,8 @@ class ParsedText(object):
         self.ts_table = None
         self.error = None
         self.n_host = 0               # lines the host parser decided
+        self.keytext = None           # keytext.KeyText of interned reducer keys (host-parsed lines)
+        self.keyx = {}                # line -> interned key (logparse._parse_one)
         self._d_text = self._d_off = None   # device text / line offsets (parse_text keep_text=True)
 
     def batch(self):
@@ -206,14 +209,17 @@ def _device_bytes(torch, data, device):
     return t
 
 
-def parse_text(engine, host, data, db, compiled, pspell=None, order_base=0, need_order=True, keep_text=False):
+def parse_text(engine, host, data, db, compiled, pspell=None, order_base=0, need_order=True, keep_text=False,
+               keytext=None):
     """Parse one firewall's log bytes on the GPU.  ``pspell``: the spelling ->
-    id dict shared across calls (ids of new spellings are appended).
+    id dict shared across calls (ids of new spellings are appended);
+    ``keytext``: the KeyText of non-canonical reducer keys, likewise shared.
     ``keep_text``: keep the device text and line offsets on the result
     (``_d_text``/``_d_off``) for ``order_keys_global`` over several inputs."""
     torch = engine.torch
     ctx = engine.ctx
     P = ParsedText()
+    P.keytext = keytext if keytext is not None else KeyText()
     if pspell is None:
         pspell = {}
     for w in DEFAULT_SPELLS:
@@ -290,6 +296,7 @@ def parse_text(engine, host, data, db, compiled, pspell=None, order_base=0, need
     P.n = n
     P.disposition = kind[:n]
     P.acl_of = {i: a for i, a in P.acl_of.items() if i < n}
+    P.keyx = {i: k for i, k in P.keyx.items() if i < n}
     P.nl = np.zeros(n, bool)
     if n:
         P.nl[:] = True
@@ -299,8 +306,8 @@ def parse_text(engine, host, data, db, compiled, pspell=None, order_base=0, need
     if keep_text:
         P._d_text, P._d_off = text, off
     P.pspell_table = [w for w, _ in sorted(pspell.items(), key=lambda kv: kv[1])]
-    if len(P.pspell_table) > 256:
-        raise NotImplementedError('more than 256 protocol spellings')
+    if len(P.pspell_table) > INTERNED:
+        raise NotImplementedError('more than %d protocol spellings' % INTERNED)
     return P
 
 
@@ -353,7 +360,7 @@ def concat(parts, torch):
     if len(parts) == 1:
         return parts[0]
     P = ParsedText()
-    starts, hosts, acl_of = [], [], {}
+    starts, hosts, acl_of, keyx = [], [], {}, {}
     base = 0
     kept = []
     for p in parts:
@@ -362,6 +369,8 @@ def concat(parts, torch):
         hosts.append(p.host_of.hosts[0])
         for i, a in p.acl_of.items():
             acl_of[base + i] = a
+        for i, k in p.keyx.items():
+            keyx[base + i] = k
         if p.error is not None:
             P.error = (base + p.error[0], p.error[1])
             base += p.n
@@ -376,6 +385,9 @@ def concat(parts, torch):
     P.lines = _Lines(b''.join(datas), np.concatenate(off))
     P.host_of = _HostOf(starts, hosts)
     P.acl_of = acl_of
+    P.keyx = keyx
+    P.keytext = kept[0].keytext
+    assert all(p.keytext is P.keytext for p in kept), 'parts parsed with different KeyText'
     P.n = base
     P.disposition = np.concatenate([p.disposition for p in kept])
     P.nl = np.concatenate([p.nl for p in kept])
