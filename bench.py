@@ -461,10 +461,6 @@ def rank_main(args, rank, world, local):
         eng.set_option(getattr(native, 'RSA_OPT_' + k), int(v))
     ent, _off = compiled.packed()
     batch, n_hb = build_shard(wl, lines, rank, eng.device, world=world)
-    owner = None
-    if dist is not None:
-        owner = Engine(local)
-        owner.set_rule_count(compiled.n_rules)
     gbuf = torch.empty(lines, dtype=torch.int32, device=eng.device)
     torch.cuda.synchronize()
     log('rank %d setup %.1fs: %d rules, %d lists, %d entries, %d lines, %d hit+built' % (
@@ -525,7 +521,7 @@ def rank_main(args, rank, world, local):
             last['recs'] = recs
             return recs.numel() // RECORD_DTYPE.itemsize
         # the merged records stay in rank 0's HBM, like the single-GPU result
-        out = merge(EngineBackend(eng, owner, [batch], [gbuf], cap), dist, world, rank, to_host=False)
+        out = merge(EngineBackend(eng, [batch], [gbuf], cap), dist, world, rank, to_host=False)
         last['merged'] = out
         return 0 if out is None else out[0].numel() // RECORD_DTYPE.itemsize
 
@@ -581,16 +577,16 @@ def rank_main(args, rank, world, local):
         dist.all_reduce(n_cls)
         if rank == 0:
             mrecs, mmatches = last['merged'][0], last['merged'][1]
+            c_merged = record_checksum(mrecs)
             checks = {'merged_sum_matches_eq_classified_lines':
                       int(mmatches[:compiled.n_rules].sum().item()) == int(n_cls.item()),
-                      'merged_record_checksum': '%016x' % record_checksum(mrecs)}
+                      'merged_record_checksum': '%016x' % c_merged}
             if world == 1:
                 eng.reset(sizing['capacity'], cap)
                 eng.pass1(batch, gbuf)
                 if eng.resolve_cap():
                     eng.pass2(batch, gbuf)
-                checks['merged_eq_single_gpu_records'] = record_checksum(eng.emit_device('final')) == \
-                    record_checksum(mrecs)
+                checks['merged_eq_single_gpu_records'] = record_checksum(eng.emit_device('final')) == c_merged
             checks['ok'] = all(v for k, v in checks.items() if k != 'merged_record_checksum')
             log('checks: %s' % json.dumps(checks))
     sum_e = scan_work(compiled, batch, gbuf) if rank == 0 else 0

@@ -2425,6 +2425,10 @@ __device__ __forceinline__ rsa_conn_record make_record(const Slot& s, int which)
 // mode 3: export the pass-1 aggregates of the entries that can still matter
 // under this table's own thresholds (rsa_resolve_cap): no threshold, or
 // min_order <= P (a shard's P bounds the global one from above).
+// With owner_world > 0 (the multi-GPU merge, RSA_OPT_OWNER_WORLD) the table
+// is this rank's shard table AND the merged table of the rules it owns (gid %
+// owner_world == owner_rank): exports (modes 1-3) leave the owned entries at
+// home, the final rows (mode 0) are the owned entries only.
 // Each thread takes kEmitU entries per iteration; one device atomic per
 // workgroup iteration reserves the output rows (a per-wave append on the one
 // cursor word serialises there).
@@ -2432,7 +2436,8 @@ constexpr int kEmitU = 4;
 __global__ __launch_bounds__(1024) void k_emit(const Slot* S, const unsigned long long* used,
                                                const unsigned long long* n_used_p, unsigned long long slot_cap,
                                                const unsigned long long* thresh, int mode, rsa_conn_record* out,
-                                               unsigned long long max_out, unsigned long long* cursor) {
+                                               unsigned long long max_out, unsigned long long* cursor,
+                                               uint32_t owner_world, uint32_t owner_rank) {
   __shared__ uint32_t sh[18];
   __shared__ unsigned long long sh_base;
   // the used-slot count is read on the device (persistent grid): no host
@@ -2462,6 +2467,7 @@ __global__ __launch_bounds__(1024) void k_emit(const Slot* S, const unsigned lon
         } else if (sl[k].count2 != 0) {
           which[k] = 1;
         }
+        if (owner_world && ((uint32_t)(sl[k].kB >> 32) % owner_world == owner_rank) != (mode == 0)) which[k] = -1;
       }
       c += which[k] >= 0 ? 1u : 0u;
     }
@@ -2731,6 +2737,7 @@ struct rsa_ctx {
   unsigned long long* d_hot_total = nullptr;
   // per-rule counters by rule block (k_cnt_*), rule sets > kCnt
   bool count_sort = true;                   // RSA_OPT_COUNT_SORT
+  uint32_t owner_world = 0, owner_rank = 0; // RSA_OPT_OWNER_WORLD / _RANK (k_emit)
   uint32_t* d_cnt_words = nullptr;          // gid|hit words grouped by rule block
   unsigned long long cnt_words_alloc = 0;
   unsigned long long* d_cnt_starts = nullptr;
@@ -3343,7 +3350,7 @@ int emit_mode(rsa_ctx* c, int mode, rsa_conn_record* out, uint64_t max_out, uint
   // persistent grid (two 1024-thread workgroups per CU) over the device-side
   // used count; one round trip for the emitted count and the error flags
   k_emit<<<c->cu_count * 2, 1024, 0, c->stream>>>(c->d_slots, c->d_used, c->d_used_n, c->slot_cap, c->d_thresh, mode,
-                                                  out, max_out, c->d_cursor);
+                                                  out, max_out, c->d_cursor, c->owner_world, c->owner_rank);
   HIPCHK(c, hipGetLastError());
   unsigned long long n = 0;
   unsigned int f[4];
@@ -3453,6 +3460,14 @@ int rsa_set_option(rsa_ctx* c, int option, int64_t value) {
       return RSA_OK;
     case RSA_OPT_COUNT_SORT:
       c->count_sort = value != 0;
+      return RSA_OK;
+    case RSA_OPT_OWNER_WORLD:
+      if (value < 0) return fail(c, RSA_ERR_ARG, "owner world must be >= 0");
+      c->owner_world = (uint32_t)value;
+      return RSA_OK;
+    case RSA_OPT_OWNER_RANK:
+      if (value < 0) return fail(c, RSA_ERR_ARG, "owner rank must be >= 0");
+      c->owner_rank = (uint32_t)value;
       return RSA_OK;
     case RSA_OPT_HOT_SPLIT:
       c->hot_split = value != 0;

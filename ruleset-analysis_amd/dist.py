@@ -4,22 +4,26 @@
 One process per GPU (``torch.distributed``; backend ``nccl`` = RCCL over xGMI
 on the GPU box, ``gloo`` in the CPU tests).  Every rank classifies and
 aggregates its own contiguous shard of the log (pass 1, rule tables
-replicated).  Then:
+replicated).  Rank r owns the rules with ``gid % world == r`` (the reducer
+partitioning), and its pass-1 table doubles as the merged table of those
+rules: their entries stay where pass 1 put them.  Then:
 
 1. ``all_reduce(SUM)`` of the per-rule line and hit counters;
-2. ``all_to_all`` of the compacted (rule, connection) pass-1 records to the
-   owner rank ``gid % world`` (the reducer partitioning), where they are merged
-   (count sum, first-seen min, last-seen max, min order key);
-3. each owner resolves the cap for its rules; ``all_reduce(MAX)`` of the
-   threshold vector gives every rank every rule's threshold P;
+2. each rank resolves its shard's own cap thresholds and sends the entries of
+   rules owned elsewhere that can still reach the report (no threshold, or
+   min_order <= the shard's P, which bounds the global P from above) to their
+   owners (``all_to_all``); owners merge them into their table (count sum,
+   first-seen min, last-seen max, min order key);
+3. owners resolve the cap of their rules; ``all_reduce(MAX)`` of the threshold
+   vector (other ranks' rules at "none") gives every rank every rule's P;
 4. if any rule is capped: every rank recounts its shard's occurrences with
-   order <= P (pass 2), the pass-2 records go to the owners by ``all_to_all``
-   and are summed there;
-5. the owners' final records are gathered to rank 0 for emission.
+   order <= P (pass 2 from its kept pass-1 records), sends the pass-2 sums of
+   rules owned elsewhere to their owners, which add them;
+5. the owners' final rows are gathered to rank 0.
 
-The order keys are global, so the cap logic is shard-agnostic.  Records are
-40-byte ``rsa_conn_record`` rows moved as uint8 tensors; routing uses torch
-index ops only.
+At world 1 nothing moves: the merge is the single-GPU job.  The order keys
+are global, so the cap logic is shard-agnostic.  Records are 40-byte
+``rsa_conn_record`` rows moved as uint8 tensors; routing uses torch index ops.
 """
 
 import numpy as np
@@ -156,6 +160,10 @@ def route_records(buf, world, dist, group=None, flag=0):
     return out
 
 
+def _overflow(e):
+    return getattr(e, 'code', None) == ShardOverflow.code
+
+
 def merge(backend, dist, world, rank, group=None, to_host=True):
     """Run the protocol; returns (records, matches, hits, distinct, thresh) on
     rank 0 and None elsewhere: numpy arrays (records as RECORD_DTYPE rows), or
@@ -164,50 +172,71 @@ def merge(backend, dist, world, rank, group=None, to_host=True):
     single-GPU job leaves its result too."""
     import torch
     tr = _Trace(rank)
-    c = backend.local_counters()
+    c = backend.counters()
     dev = c['matches'].device
     tr('start', dev)
     _all_reduce(c['matches'], dist, group)
     _all_reduce(c['hits'], dist, group)
     tr('counters', dev)
-    failed = 0
+    n_rules = c['thresh'].numel()
+    others = (torch.arange(n_rules, device=dev) % world) != rank    # rules owned elsewhere
+    backend.set_owner(world, rank)
     try:
-        exported = backend.export(0)
-    except Exception as e:  # noqa: BLE001 - a table overflow must not strand the other ranks
-        if getattr(e, 'code', None) != ShardOverflow.code:
-            raise
-        exported = torch.zeros(0, dtype=torch.uint8, device=dev)
-        failed = 1
-    tr('export1', dev)
-    recv = route_records(exported, world, dist, group, flag=failed)
-    if recv is None:
-        raise ShardOverflow('distinct-connection table overflow on at least one rank')
-    tr('route1', dev)
-    backend.owner_reset(max(recv.numel() // REC, 1))
-    backend.owner_import(recv, 0)
-    tr('import1', dev)
-    backend.owner_resolve_cap()
-    oc = backend.owner_counters()
-    thresh = oc['thresh'].clone()
-    _all_reduce(thresh, dist, group, op=dist.ReduceOp.MAX)
-    capped_any = bool((thresh != NO_THRESHOLD).any().item())
-    tr('cap', dev)
-    if capped_any:
-        backend.set_local_thresh(thresh)
-        backend.local_recount()
-        recv2 = route_records(backend.export(1), world, dist, group)
-        backend.owner_import(recv2, 1)
-        backend.set_owner_thresh(thresh)
-        tr('pass2', dev)
-    final = backend.owner_emit()
-    distinct = oc['distinct'].clone()
-    _all_reduce(distinct, dist, group)
-    tr('emit', dev)
+        failed = 0
+        try:
+            exported = backend.export(0)
+        except Exception as e:  # noqa: BLE001 - a table overflow must not strand the other ranks
+            if not _overflow(e):
+                raise
+            exported = torch.zeros(0, dtype=torch.uint8, device=dev)
+            failed = 1
+        tr('export1', dev)
+        recv = route_records(exported, world, dist, group, flag=failed)
+        if recv is None:
+            raise ShardOverflow('distinct-connection table overflow on at least one rank')
+        tr('route1', dev)
+        failed = 0
+        if recv.numel():
+            # the received entries join the owned ones: the thresholds of the
+            # owned rules are resolved again over the merged entries (with
+            # nothing received, the shard's own resolution already is that)
+            try:
+                backend.import_records(recv, 0)
+                backend.resolve_cap()
+            except Exception as e:  # noqa: BLE001
+                if not _overflow(e):
+                    raise
+                failed = 1
+        tr('import1', dev)
+        # thresholds of the owned rules (MAX: the others say "none" = -1),
+        # with the overflow flag riding along as one more element
+        thresh = torch.cat([c['thresh'].masked_fill(others, NO_THRESHOLD),
+                            torch.tensor([failed], dtype=torch.int64, device=dev)])
+        _all_reduce(thresh, dist, group, op=dist.ReduceOp.MAX)
+        capped_any, failed_any = (bool(x) for x in torch.stack([(thresh[:-1] != NO_THRESHOLD).any(),
+                                                               thresh[-1] != 0]).cpu().tolist())
+        if failed_any:
+            raise ShardOverflow('distinct-connection table overflow on at least one rank')
+        thresh = thresh[:-1]
+        tr('cap', dev)
+        if capped_any:
+            backend.set_thresh(thresh)
+            backend.recount()
+            recv2 = route_records(backend.export(1), world, dist, group)
+            if recv2.numel():
+                backend.import_records(recv2, 1)
+            tr('pass2', dev)
+        final = backend.emit_final()
+        distinct = c['distinct'].masked_fill(others, 0)
+        _all_reduce(distinct, dist, group)
+        tr('emit', dev)
+    finally:
+        backend.set_owner(0, 0)
     # the owners' rows to rank 0 (sizes first: one int per rank)
     size = torch.tensor([final.numel()], dtype=torch.int64, device=final.device)
     sizes = [torch.zeros_like(size) for _ in range(world)]
     _all_gather(sizes, size, dist, group)
-    sizes = [int(s.item()) for s in sizes]
+    sizes = [int(s) for s in torch.cat(sizes).cpu().tolist()]
     parts = _gather0(final, sizes, rank, world, dist, group)
     tr('gather', dev)
     if rank != 0:
@@ -232,51 +261,45 @@ def merged_to_host(out):
 
 
 class EngineBackend(object):
-    """Binds the protocol to two HIP contexts on this rank's GPU: ``local`` holds
-    the shard's pass-1 table, ``owner`` the merged table of the rules this rank
-    owns."""
+    """Binds the protocol to this rank's HIP context: ``eng`` holds the
+    shard's pass-1 table (and, during the merge, the merged entries of the
+    rules this rank owns)."""
 
-    def __init__(self, local, owner, batches, gid_bufs, cap):
-        self.local = local
-        self.owner = owner
+    def __init__(self, eng, batches, gid_bufs, cap):
+        self.eng = eng
         self.batches = batches
         self.gid_bufs = gid_bufs
         self.cap = cap
 
-    def local_counters(self):
-        return self.local.counters
+    def counters(self):
+        return self.eng.counters
+
+    def set_owner(self, world, rank):
+        from . import native
+        self.eng.set_option(native.RSA_OPT_OWNER_WORLD, world)
+        self.eng.set_option(native.RSA_OPT_OWNER_RANK, rank)
 
     def export(self, which):
+        """Entries of rules owned elsewhere: which 0 = the pass-1 aggregates
+        that can still reach the report (after the shard's own cap
+        resolution), 1 = the pass-2 sums."""
         if which == 0:
-            # the shard's own cap resolution first: its P bounds the global P
-            # from above, so only entries with min_order <= P (or of rules
-            # without a threshold) can reach the report; the rest stay home
-            # (exact; fewer records over xGMI and into the owners' tables)
-            self.local.resolve_cap()
-            return self.local.emit_device('pass1_kept')
-        return self.local.emit_device('pass2')
+            self.eng.resolve_cap()
+            return self.eng.emit_device('pass1_kept')
+        return self.eng.emit_device('pass2')
 
-    def owner_reset(self, capacity):
-        self.owner.reset(capacity, self.cap)
+    def import_records(self, buf, which):
+        self.eng.import_records(buf, which)
 
-    def owner_import(self, buf, which):
-        self.owner.import_records(buf, which)
+    def resolve_cap(self):
+        return self.eng.resolve_cap()
 
-    def owner_resolve_cap(self):
-        return self.owner.resolve_cap()
+    def set_thresh(self, thresh):
+        self.eng.counters['thresh'].copy_(thresh)
 
-    def owner_counters(self):
-        return self.owner.counters
-
-    def set_local_thresh(self, thresh):
-        self.local.counters['thresh'].copy_(thresh)
-
-    def set_owner_thresh(self, thresh):
-        self.owner.counters['thresh'].copy_(thresh)
-
-    def local_recount(self):
+    def recount(self):
         for b, g in zip(self.batches, self.gid_bufs):
-            self.local.pass2(b, g)
+            self.eng.pass2(b, g)
 
-    def owner_emit(self):
-        return self.owner.emit_device('final')
+    def emit_final(self):
+        return self.eng.emit_device('final')

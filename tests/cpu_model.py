@@ -84,9 +84,18 @@ class NumpyTable(object):
                 th[gid] = sorted(orders)[cap - 1]
         return th
 
-    def records(self, which, thresh=None):
+    def distinct(self, n_rules):
+        d = np.zeros(n_rules, np.int32)
+        for (gid, *_) in self.t:
+            d[gid] += 1
+        return d
+
+    def records(self, which, thresh=None, keep=None):
+        """Rows of the k_emit mode ``which``; ``keep(gid)``: the owner filter."""
         rows = []
         for (gid, pspell, f, t, p), e in self.t.items():
+            if keep is not None and not keep(gid):
+                continue
             if which == 0:
                 rows.append((e[3], gid, f, t, p, pspell, 0, e[0], e[1], e[2], 0))
             elif which == 3:
@@ -110,12 +119,14 @@ class NumpyTable(object):
 
 class NumpyBackend(object):
     """``dist.merge`` backend over one rank's shard: ``shard`` = (gid, flags,
-    pspell, src, dst, sport, dport, ts, order) numpy columns."""
+    pspell, src, dst, sport, dport, ts, order) numpy columns.  One table, as
+    the HIP ctx: the shard's pass-1 entries, joined during the merge by the
+    received entries of the rules this rank owns."""
 
     def __init__(self, n_rules, cap, shard):
         self.n_rules, self.cap, self.shard = n_rules, cap, shard
         self.local = NumpyTable()
-        self.owner = NumpyTable()
+        self.world, self.rank = 0, 0
         gid, flags, pspell, src, dst, sport, dport, ts, order = shard
         m = np.zeros(n_rules, np.int64)
         h = np.zeros(n_rules, np.int64)
@@ -128,8 +139,9 @@ class NumpyBackend(object):
                 h[g] += 1
                 if flags[i] & 4:
                     self.local.combine(self._key(i), 1, int(ts[i]), int(ts[i]), int(order[i]))
-        self.counters = {'matches': torch.from_numpy(m), 'hits': torch.from_numpy(h)}
-        self.thresh = torch.full((n_rules,), -1, dtype=torch.int64)
+        self._counters = {'matches': torch.from_numpy(m), 'hits': torch.from_numpy(h),
+                          'distinct': torch.from_numpy(self.local.distinct(n_rules)),
+                          'thresh': torch.full((n_rules,), -1, dtype=torch.int64)}
 
     @classmethod
     def from_packed(cls, n_rules, cap, gids, tup, ts, order):
@@ -142,61 +154,54 @@ class NumpyBackend(object):
             return (int(gid[i]), int(pspell[i]), int(dst[i]), int(src[i]), int(sport[i]))
         return (int(gid[i]), int(pspell[i]), int(src[i]), int(dst[i]), int(dport[i]))
 
-    def local_counters(self):
-        return self.counters
+    def _owned(self, gid):
+        return self.world == 0 or gid % self.world == self.rank
+
+    def counters(self):
+        return self._counters
+
+    def set_owner(self, world, rank):
+        self.world, self.rank = world, rank
+
+    def _thresh_np(self):
+        return self._counters['thresh'].numpy().view(np.uint64)
 
     def export(self, which):
+        foreign = lambda g: not self._owned(g)
         if which == 0:
             # as EngineBackend.export(0): the shard resolves its own cap first
             # and exports only the entries its threshold keeps (exact: a
             # shard's P bounds the global P from above)
-            self.exported_all = len(self.local.t)
-            recs = self.local.records(3, self.local.local_thresh(self.n_rules, self.cap))
+            self.resolve_cap()
+            self.exported_all = sum(1 for (g, *_) in self.local.t if foreign(g))
+            recs = self.local.records(3, self._thresh_np(), keep=foreign)
             self.exported_kept = recs.numel() // RECORD_DTYPE.itemsize
             return recs
-        return self.local.records(which)
+        return self.local.records(1, keep=foreign)
 
-    def owner_reset(self, capacity):
-        self.owner = NumpyTable()
-
-    def owner_import(self, buf, which):
+    def import_records(self, buf, which):
         for r in buf.numpy().view(RECORD_DTYPE):
             k = (int(r['gid']), int(r['pspell']), int(r['for_ip']), int(r['to_ip']), int(r['to_port']))
             if which == 0:
-                self.owner.combine(k, int(r['count']), int(r['first']), int(r['last']), int(r['min_order']))
+                if self.local.combine(k, int(r['count']), int(r['first']), int(r['last']), int(r['min_order'])):
+                    self._counters['distinct'][k[0]] += 1
             else:
-                e = self.owner.t[k]
+                e = self.local.t[k]
                 e[4] += int(r['count'])
                 e[5] = min(e[5], int(r['first']))
                 e[6] = max(e[6], int(r['last']))
 
-    def owner_resolve_cap(self):
-        per = {}
-        for (gid, *_), e in self.owner.t.items():
-            per.setdefault(gid, []).append(e[3])
-        th = np.full(self.n_rules, NO, np.uint64)
-        for gid, orders in per.items():
-            if self.cap > 0 and len(orders) >= self.cap:
-                th[gid] = sorted(orders)[self.cap - 1]
-        self.owner_thresh = torch.from_numpy(th.view(np.int64).copy())
-        d = np.zeros(self.n_rules, np.int32)
-        for gid, orders in per.items():
-            d[gid] = len(orders)
-        self.owner_distinct = torch.from_numpy(d)
+    def resolve_cap(self):
+        th = self.local.local_thresh(self.n_rules, self.cap)
+        self._counters['thresh'].copy_(torch.from_numpy(th.view(np.int64).copy()))
         return int((th != NO).sum())
 
-    def owner_counters(self):
-        return {'thresh': self.owner_thresh, 'distinct': self.owner_distinct}
+    def set_thresh(self, thresh):
+        self._counters['thresh'].copy_(thresh)
 
-    def set_local_thresh(self, thresh):
-        self.thresh = thresh.clone()
-
-    def set_owner_thresh(self, thresh):
-        self.owner_thresh = thresh.clone()
-
-    def local_recount(self):
+    def recount(self):
         gid, flags, pspell, src, dst, sport, dport, ts, order = self.shard
-        th = self.thresh.numpy().view(np.uint64)
+        th = self._thresh_np()
         for i in range(len(gid)):
             g = int(gid[i])
             if g < 0 or (flags[i] & 6) != 6 or int(th[g]) == NO or int(order[i]) > int(th[g]):
@@ -206,5 +211,5 @@ class NumpyBackend(object):
             e[5] = min(e[5], int(ts[i]))
             e[6] = max(e[6], int(ts[i]))
 
-    def owner_emit(self):
-        return self.owner.records(2, self.owner_thresh.numpy().view(np.uint64))
+    def emit_final(self):
+        return self.local.records(2, self._thresh_np(), keep=self._owned)

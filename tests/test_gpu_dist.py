@@ -38,13 +38,11 @@ def _worker(rank, world, port, args, out_q):
     a, b = cut[rank], cut[rank + 1]
     local = Engine(0)
     local.load_compiled(compiled)
-    owner = Engine(0)
-    owner.set_rule_count(compiled.n_rules)
     batch = DeviceBatch.from_numpy(tup[a:b], ts[a:b], order[a:b], local.device)
     local.reset(max(built_hit_count(tup[a:b]), 1), cap)
     g = torch.empty(batch.n, dtype=torch.int32, device=local.device)
     local.pass1(batch, g)
-    out = merge(EngineBackend(local, owner, [batch], [g], cap), dist, world, rank)
+    out = merge(EngineBackend(local, [batch], [g], cap), dist, world, rank)
     if rank == 0:
         out_q.put(out)
     dist.barrier()
