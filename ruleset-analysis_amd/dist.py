@@ -135,6 +135,8 @@ def route_records(buf, world, dist, group=None, flag=0):
     bytes.  ``flag`` (this rank's error flag) rides along with the counts: if
     any rank sent a non-zero flag, every rank returns None instead."""
     import torch
+    if world == 1:       # every record is already at its owner
+        return None if flag else buf
     n = buf.numel() // REC
     rows = buf.view(-1, REC)
     gid = rows[:, 8:12].contiguous().view(torch.int32).view(-1).to(torch.int64) if n else \
@@ -233,11 +235,14 @@ def merge(backend, dist, world, rank, group=None, to_host=True):
     finally:
         backend.set_owner(0, 0)
     # the owners' rows to rank 0 (sizes first: one int per rank)
-    size = torch.tensor([final.numel()], dtype=torch.int64, device=final.device)
-    sizes = [torch.zeros_like(size) for _ in range(world)]
-    _all_gather(sizes, size, dist, group)
-    sizes = [int(s) for s in torch.cat(sizes).cpu().tolist()]
-    parts = _gather0(final, sizes, rank, world, dist, group)
+    if world == 1:
+        parts = [final]
+    else:
+        size = torch.tensor([final.numel()], dtype=torch.int64, device=final.device)
+        sizes = [torch.zeros_like(size) for _ in range(world)]
+        _all_gather(sizes, size, dist, group)
+        sizes = [int(s) for s in torch.cat(sizes).cpu().tolist()]
+        parts = _gather0(final, sizes, rank, world, dist, group)
     tr('gather', dev)
     if rank != 0:
         tr('end')
@@ -267,6 +272,7 @@ class EngineBackend(object):
 
     def __init__(self, eng, batches, gid_bufs, cap):
         self.eng = eng
+        self.world = 0
         self.batches = batches
         self.gid_bufs = gid_bufs
         self.cap = cap
@@ -276,17 +282,20 @@ class EngineBackend(object):
 
     def set_owner(self, world, rank):
         from . import native
+        self.world = world
         self.eng.set_option(native.RSA_OPT_OWNER_WORLD, world)
         self.eng.set_option(native.RSA_OPT_OWNER_RANK, rank)
 
     def export(self, which):
         """Entries of rules owned elsewhere: which 0 = the pass-1 aggregates
         that can still reach the report (after the shard's own cap
-        resolution), 1 = the pass-2 sums."""
+        resolution), 1 = the pass-2 sums.  A single rank owns every rule:
+        nothing to scan for."""
         if which == 0:
             self.eng.resolve_cap()
-            return self.eng.emit_device('pass1_kept')
-        return self.eng.emit_device('pass2')
+        if self.world == 1:
+            return self.eng.torch.zeros(0, dtype=self.eng.torch.uint8, device=self.eng.device)
+        return self.eng.emit_device('pass1_kept' if which == 0 else 'pass2')
 
     def import_records(self, buf, which):
         self.eng.import_records(buf, which)
