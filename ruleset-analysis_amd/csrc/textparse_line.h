@@ -109,6 +109,14 @@ struct Span {
 struct Mapped {             // get_builtconn's fields
   bool inbound, udp;
   Span if1, ip1, p1, if2, ip2, p2;
+  Span par1;                // the text of the first \([^)]*\)
+  uint32_t tag_d, proto;    // positions of the severity digit and of TCP/UDP
+};
+
+// Where gb_match found the header (parse_line's template fast path).
+struct Hdr {
+  uint32_t hms1, m2, d2a, d2b, ya, q, k;   // k: the '%' whose rest matched
+  bool single, opt;                        // single spaces after both months; device date present
 };
 
 // The rest of logparse._GB after `.*?`, at the '%' + 1 position p.
@@ -119,6 +127,7 @@ RSA_HD bool gb_rest(const S& s, uint32_t p, Mapped& m) {
   else if (lit(s, p, "PIX")) p += 3;
   else return false;
   if (p + 3 > s.n || s[p] != '-' || !is_dig(s[p + 1]) || s[p + 2] != '-') return false;
+  m.tag_d = p + 1;
   p += 3;
   if (p + 6 > s.n) return false;
   for (int i = 0; i < 6; ++i)
@@ -138,6 +147,7 @@ RSA_HD bool gb_rest(const S& s, uint32_t p, Mapped& m) {
   if (lit(s, p, "TCP")) m.udp = false;
   else if (lit(s, p, "UDP")) m.udp = true;
   else return false;
+  m.proto = p;
   p += 3;
   if (!lit(s, p, " connection ")) return false;
   p += 12;
@@ -158,8 +168,10 @@ RSA_HD bool gb_rest(const S& s, uint32_t p, Mapped& m) {
   if (e == p || !lit(s, e, " (")) return false;
   m.p1 = {p, e};
   p = e + 2;
+  m.par1.a = p;
   while (p < s.n && s[p] != ')') ++p;   // [^)]*
   if (p >= s.n) return false;
+  m.par1.b = p;
   ++p;
   if (!lit(s, p, " to ")) return false;
   p += 4;
@@ -182,36 +194,57 @@ RSA_HD bool gb_rest(const S& s, uint32_t p, Mapped& m) {
 // is taken when it matches: skipping it cannot change the outcome, since its
 // text holds no '%'.
 template <class S>
-RSA_HD bool gb_match(const S& s, Mapped& m) {
+RSA_HD bool gb_match(const S& s, Mapped& m, Hdr& h) {
   if (s.n < 3 || !is_upper(s[0]) || !is_lower(s[1]) || !is_lower(s[2])) return false;
   uint32_t p = 3;
   if (p >= s.n || s[p] != ' ') return false;
   while (p < s.n && s[p] == ' ') ++p;
+  h.single = p == 4;
   uint32_t e = run<kDig>(s, p);
   if (e - p < 1 || e - p > 2 || e >= s.n || s[e] != ' ') return false;
   p = e + 1;
   if (!hms(s, p) || p + 8 >= s.n || s[p + 8] != ' ') return false;
+  h.hms1 = p;
   p += 9;
   uint32_t q = p;
+  h.opt = false;
   {
     uint32_t t = p;
     if (t + 3 <= s.n && is_upper(s[t]) && is_lower(s[t + 1]) && is_lower(s[t + 2]) && t + 3 < s.n && s[t + 3] == ' ') {
+      h.m2 = t;
       t += 3;
       while (t < s.n && s[t] == ' ') ++t;
+      h.single = h.single && t == h.m2 + 4;
       e = run<kDig>(s, t);
       if (e - t >= 1 && e - t <= 2 && e < s.n && s[e] == ' ') {
+        h.d2a = t;
+        h.d2b = e;
         t = e + 1;
         e = run<kDig>(s, t);
         if (e - t == 4 && e < s.n && s[e] == ' ') {
+          h.ya = t;
           t = e + 1;
-          if (hms(s, t) && t + 10 <= s.n && s[t + 8] == ':' && s[t + 9] == ' ') q = t + 10;
+          if (hms(s, t) && t + 10 <= s.n && s[t + 8] == ':' && s[t + 9] == ' ') {
+            q = t + 10;
+            h.opt = true;
+          }
         }
       }
     }
   }
+  h.q = q;
   for (uint32_t k = q; k < s.n; ++k)
-    if (s[k] == '%' && gb_rest(s, k + 1, m)) return true;
+    if (s[k] == '%' && gb_rest(s, k + 1, m)) {
+      h.k = k;
+      return true;
+    }
   return false;
+}
+
+template <class S>
+RSA_HD bool gb_match(const S& s, Mapped& m) {
+  Hdr h;
+  return gb_match(s, m, h);
 }
 
 struct Reduced {            // connlist-reducer.py:25 BUILT captures used downstream
@@ -388,6 +421,54 @@ RSA_HD bool ts_code(const S& s, const Reduced& r, uint32_t& code) {
   return true;
 }
 
+RSA_HD bool is_parch(uint32_t c) { return is_dig(c) || c == '.' || c == '/'; }
+
+template <class S>
+RSA_HD bool no_dash(const S& s, Span x) {
+  for (uint32_t i = x.a; i < x.b; ++i)
+    if (s[i] == '-') return false;
+  return true;
+}
+
+// The template fast path of parse_line.  A line of exactly the form
+//   Mmm D HH:MM:SS Mmm D YYYY HH:MM:SS: %TAG-d-dddddd: Built DIR PROTO
+//   connection N for IF:IP/P (IP/P) to IF:IP/P (IP/P)
+// (single spaces; D one or two digits; the parenthesised texts [0-9./]*; the
+// line ends at the last ')') has one ' Built ', one ' for ' and one ' to '
+// after the device date, so connlist-reducer.py:25's BUILT.search matches at
+// the line's start with groups (HH:MM:SS of the syslog header, the device
+// date's month, day and year, PROTO, the first IP, the second IP and P) --
+// what built_search returns after its backtracking, read off gb_match's
+// positions instead.  The hit test needs no scan either when no interface
+// name holds a '-': the only '-' are then the tag's.  False: not the
+// template, the general path decides.
+template <class S>
+RSA_HD bool built_template(const S& s, const Mapped& m, const Hdr& h, Reduced& r, bool& hit) {
+  if (!h.opt || !h.single || h.k != h.q) return false;
+  for (uint32_t i = m.par1.a; i < m.par1.b; ++i)
+    if (!is_parch(s[i])) return false;
+  uint32_t p = m.p2.b;
+  if (!lit(s, p, " (")) return false;
+  p += 2;
+  while (p < s.n && is_parch(s[p])) ++p;
+  if (p + 1 != s.n || s[p] != ')') return false;
+  r.time = {h.hms1, h.hms1 + 8};
+  r.mon = {h.m2, h.m2 + 3};
+  r.day = {h.d2a, h.d2b};
+  r.year = {h.ya, h.ya + 4};
+  r.word = {m.proto, m.proto + 3};
+  r.for_ip = m.ip1;
+  r.to_ip = m.ip2;
+  r.to_port = m.p2;
+  if (no_dash(s, m.if1) && no_dash(s, m.if2)) {
+    const uint32_t t = m.tag_d;
+    hit = s[t] == '6' && lit(s, t + 2, "30201") && (s[t + 7] == '3' || s[t + 7] == '5');
+  } else {
+    hit = hit_test(s);
+  }
+  return true;
+}
+
 // The whole line: disposition (RSA_LINE_* | interface << 8), tuple, timestamp code.
 template <class S>
 RSA_HD void parse_line(const S& s, const rsa_parse_ifc* ifcs, uint32_t n_ifcs, const rsa_parse_spell* spells,
@@ -396,7 +477,8 @@ RSA_HD void parse_line(const S& s, const rsa_parse_ifc* ifcs, uint32_t n_ifcs, c
   uint32_t ts = 0, d = RSA_LINE_IGNORE;
   {
     Mapped m;
-    if (gb_match(s, m)) {
+    Hdr h;
+    if (gb_match(s, m, h)) {
       d = RSA_LINE_CLASSIFY;
       const Span src = m.inbound ? m.ip1 : m.ip2, dst = m.inbound ? m.ip2 : m.ip1;
       const Span sp = m.inbound ? m.p1 : m.p2, dp = m.inbound ? m.p2 : m.p1;
@@ -436,10 +518,12 @@ RSA_HD void parse_line(const S& s, const rsa_parse_ifc* ifcs, uint32_t n_ifcs, c
         tup.dport = (uint16_t)pd;
         tup.list = (uint16_t)lid;
         uint32_t flags = RSA_F_VALID;
-        const bool hit = hit_test(s);
-        if (hit) flags |= RSA_F_HIT;
         Reduced r;
-        if (d == RSA_LINE_CLASSIFY && built_search(s, r)) {
+        bool hit = false;
+        const bool fast = built_template(s, m, h, r, hit);
+        if (!fast) hit = hit_test(s);
+        if (hit) flags |= RSA_F_HIT;
+        if (d == RSA_LINE_CLASSIFY && (fast || built_search(s, r))) {
           flags |= RSA_F_BUILT;
           uint32_t vf = 0, vt = 0;
           if (span_eq(s, r.for_ip, src) && span_eq(s, r.to_ip, dst) && span_eq(s, r.to_port, dp)) {
@@ -515,10 +599,14 @@ RSA_HD void reduce_line(const S& s, const rsa_parse_spell* spells, uint32_t n_sp
     d = RSA_RED_KEYED;
     const SubLn<S> v{s, t + 1, b - t - 1};
     uint32_t flags = 0;
-    const bool hit = hit_test(v);
-    if (hit) flags |= RSA_F_HIT;
     Reduced r;
-    if (built_search(v, r)) {
+    Mapped m;
+    Hdr h;
+    bool hit = false;
+    const bool fast = gb_match(v, m, h) && built_template(v, m, h, r, hit);   // the canonical form
+    if (!fast) hit = hit_test(v);
+    if (hit) flags |= RSA_F_HIT;
+    if (fast || built_search(v, r)) {
       flags |= RSA_F_BUILT;
       uint32_t vf = 0, vt = 0;
       const uint32_t pv = port_val(v, r.to_port);

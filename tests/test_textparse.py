@@ -423,3 +423,37 @@ def test_gpu_analyze_text_equals_host_parse_fuzzed(engine):
     want, _ = analyze([('fw1', good)], db, cap=7, engine=engine)
     got, _ = analyze_text([('fw1', ''.join(good).encode('latin-1'))], db, cap=7, engine=engine)
     assert got == want
+
+
+def test_template_fast_path_equals_general_parse():
+    """textparse_line.h built_template (the fast path for the canonical ASA
+    form) gives exactly built_search's groups and hit_test's flag on every
+    line it takes: rendered lines (nearly all taken), fuzzed lines, and lines
+    aimed at its conditions (one-digit days, double spaces, '-' in interface
+    names, a second ' to ' after the last address, other message ids)."""
+    lib = _harness()
+    _db, fuzz = _fuzz_lines(7, 6000)
+    dbj, info = synth.make_db(11, 300, interfaces=('outside', 'partner'))
+    clean = [l + '\n' for l in synth.render_lines(synth.make_traffic((dbj, info), 3000, seed=8))]
+    head = 'Jul 15 00:00:01 Jul 15 2013 00:00:01: %ASA-6-302013: '
+    body = 'Built inbound TCP connection 5 for outside:10.0.0.1/1234 (10.0.0.1/1234) to inside:10.0.0.2/80 (10.0.0.2/80)'
+    aimed = [head + body, head.replace('Jul 15 2013', 'Jul 5 2013') + body, head.replace('Jul 15 00', 'Jul 5 00') + body,
+             head.replace('Jul 15 2013', 'Jul  5 2013') + body, head.replace('6-302013', '6-302015') + body,
+             head.replace('6-302013', '6-302014') + body, head.replace('ASA-6', 'ASA-5') + body,
+             head + body.replace('outside:', 'out-6-302013:'), head + body.replace('inside:', 'in-side:'),
+             head.replace('ASA-6-302013', 'ASA-5-302014') + body.replace('outside:', 'x-6-302015:'),
+             head + body + ' to dmz:1.2.3.4/5', head + body + ' ', head + body.replace('(10.0.0.1/1234)', '(x y)'),
+             head.replace(': %ASA', ':  %ASA') + body, head + body.replace('inbound', 'outbound'),
+             head.replace('%ASA', 'x %ASA') + body, head + body.replace('(10.0.0.2/80)', '(10.0.0.2/80) ')]
+    lines = clean + fuzz + [a + '\n' for a in aimed]
+    data = ''.join(lines).encode('latin-1')
+    off = np.cumsum([0] + [len(l.encode('latin-1')) for l in lines]).astype(np.uint64)
+    out = np.zeros(len(lines), np.uint8)
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    buf = np.frombuffer(data, np.uint8).copy()
+    lib.template_check_host(p(buf), p(off), ctypes.c_uint64(len(lines)), p(out))
+    assert not (out == 2).any(), [lines[i] for i in np.nonzero(out == 2)[0][:3]]
+    assert (out[:len(clean)] == 1).mean() > 0.9        # the rendered BUILT lines take the fast path
+    a = out[len(clean) + len(fuzz):]
+    assert a[0] == a[1] == a[2] == a[4] == a[5] == a[6] == a[7] == a[8] == a[9] == a[14] == 1
+    assert [a[k] for k in (3, 10, 11, 12, 13, 15, 16)] == [0] * 7, a.tolist()
