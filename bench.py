@@ -681,6 +681,10 @@ def text_main(args):
     ifcs, _names = textparse.interface_table(wl.db, compiled, wl.info['host'])
     spells = textparse.spell_table(list(textparse.DEFAULT_SPELLS))
     eng.load_compiled(compiled, index=not args.no_index, prefix=args.prefix, kind=args.index)
+    from ruleset_analysis_amd import native
+    for kv in args.opt:
+        k, v = kv.split('=')
+        eng.set_option(getattr(native, 'RSA_OPT_' + k), int(v))
     dev = eng.device
     text = textparse._device_bytes(torch, data, dev)
     n = lines

@@ -152,16 +152,33 @@ __global__ void k_set_u64(uint64_t* p, uint64_t v) { *p = v; }
 // whose lines do not fit parses straight from HBM with byte loads.
 constexpr uint32_t kParseWG = 128, kStageBytes = 32768;
 
+// A line the template pass defers (rsa_text::kLineDefer): its index is
+// appended to the slow list (one device atomic per wave).
+__device__ __forceinline__ void defer_append(bool defer, uint64_t i, uint32_t* __restrict__ slow_idx,
+                                             unsigned int* __restrict__ slow_n) {
+  const unsigned long long b = __ballot(defer);
+  if (!b) return;
+  const int leader = __builtin_ctzll(b);
+  const uint32_t lane = __lane_id();
+  uint32_t at = 0;
+  if ((int)lane == leader) at = atomicAdd(slow_n, (unsigned int)__popcll(b));
+  at = __builtin_amdgcn_readlane(at, leader);
+  if (defer) slow_idx[at + (uint32_t)__popcll(b & ((1ull << lane) - 1ull))] = (uint32_t)i;
+}
+
 // kReduce: the reducer drop-in's lines (rsa_text::reduce_line, plus the
 // same-key flag against the previous line of the batch).
 // kDirect: no staging, every lane reads its line from HBM through 4-byte
 // loads (no LDS: occupancy bound by registers only).
+// Both parse the template form only (kDefer): other classified lines go to
+// the slow list for k_parse_slow.
 template <bool kReduce, bool kDirect>
 __global__ __launch_bounds__(kParseWG) void k_parse(const uint8_t* __restrict__ text, const uint64_t* __restrict__ off,
                                                     uint64_t n_lines, const rsa_parse_ifc* __restrict__ ifcs,
                                                     uint32_t n_ifcs, const rsa_parse_spell* __restrict__ spells,
                                                     uint32_t n_spells, rsa_tuple* __restrict__ tuples,
-                                                    uint32_t* __restrict__ ts_out, uint32_t* __restrict__ disp) {
+                                                    uint32_t* __restrict__ ts_out, uint32_t* __restrict__ disp,
+                                                    uint32_t* __restrict__ slow_idx, unsigned int* __restrict__ slow_n) {
   __shared__ uint32_t sm[kDirect ? 1 : kStageBytes / 4];
   const uint64_t l0 = (uint64_t)blockIdx.x * kParseWG;
   const uint64_t l1 = l0 + kParseWG < n_lines ? l0 + kParseWG : n_lines;
@@ -173,12 +190,12 @@ __global__ __launch_bounds__(kParseWG) void k_parse(const uint8_t* __restrict__ 
     uint64_t len = b - a;
     if (len && text[b - 1] == '\n') --len;
     rsa_tuple tup = {0u, 0u, 0, 0, 0, 0, 0};
-    uint32_t ts = 0, d = kReduce ? (uint32_t)RSA_LINE_HOST : (uint32_t)RSA_LINE_HOST;
+    uint32_t ts = 0, d = RSA_LINE_HOST;
     if (len < 0xFFFFFFFFull) {
       const rsa_text::GWordLn s{reinterpret_cast<const uint32_t*>(text), text, a, n_bytes, (uint32_t)len, ~0ull, 0u};
       if (kReduce) {
-        rsa_text::reduce_line(s, spells, n_spells, tup, ts, d);
-        if (i > 0 && d != RSA_RED_NOISE) {
+        rsa_text::reduce_line<true>(s, spells, n_spells, tup, ts, d);
+        if (i > 0 && d != RSA_RED_NOISE && d != rsa_text::kLineDefer) {
           const uint64_t pa = off[i - 1];
           uint64_t plen = a - pa;
           if (plen && text[a - 1] == '\n') --plen;
@@ -187,9 +204,10 @@ __global__ __launch_bounds__(kParseWG) void k_parse(const uint8_t* __restrict__ 
           if (plen < 0xFFFFFFFFull && rsa_text::same_key(s, q)) d |= RSA_RED_SAME_KEY;
         }
       } else {
-        rsa_text::parse_line(s, ifcs, n_ifcs, spells, n_spells, tup, ts, d);
+        rsa_text::parse_line<true>(s, ifcs, n_ifcs, spells, n_spells, tup, ts, d);
       }
     }
+    defer_append(d == rsa_text::kLineDefer, i, slow_idx, slow_n);
     tuples[i] = tup;
     ts_out[i] = ts;
     disp[i] = d;
@@ -230,8 +248,8 @@ __global__ __launch_bounds__(kParseWG) void k_parse(const uint8_t* __restrict__ 
       const bool pin = i > 0 && plen < 0xFFFFFFFFull;
       if (staged) {
         const rsa_text::WordLn s{sm, (uint32_t)(a - base), (uint32_t)len};
-        rsa_text::reduce_line(s, spells, n_spells, tup, ts, d);
-        if (pin && d != RSA_RED_NOISE) {
+        rsa_text::reduce_line<true>(s, spells, n_spells, tup, ts, d);
+        if (pin && d != RSA_RED_NOISE && d != rsa_text::kLineDefer) {
           bool same;
           if (i > l0) {
             const rsa_text::WordLn q{sm, (uint32_t)(pa - base), (uint32_t)plen};
@@ -244,21 +262,65 @@ __global__ __launch_bounds__(kParseWG) void k_parse(const uint8_t* __restrict__ 
         }
       } else {
         const rsa_text::ByteLn s{text + a, (uint32_t)len};
-        rsa_text::reduce_line(s, spells, n_spells, tup, ts, d);
-        if (pin && d != RSA_RED_NOISE && rsa_text::same_key(s, rsa_text::ByteLn{text + pa, (uint32_t)plen}))
+        rsa_text::reduce_line<true>(s, spells, n_spells, tup, ts, d);
+        if (pin && d != RSA_RED_NOISE && d != rsa_text::kLineDefer &&
+            rsa_text::same_key(s, rsa_text::ByteLn{text + pa, (uint32_t)plen}))
           d |= RSA_RED_SAME_KEY;
       }
     } else if (staged) {
       const rsa_text::WordLn s{sm, (uint32_t)(a - base), (uint32_t)len};
-      rsa_text::parse_line(s, ifcs, n_ifcs, spells, n_spells, tup, ts, d);
+      rsa_text::parse_line<true>(s, ifcs, n_ifcs, spells, n_spells, tup, ts, d);
     } else {
       const rsa_text::ByteLn s{text + a, (uint32_t)len};
-      rsa_text::parse_line(s, ifcs, n_ifcs, spells, n_spells, tup, ts, d);
+      rsa_text::parse_line<true>(s, ifcs, n_ifcs, spells, n_spells, tup, ts, d);
     }
   }
+  defer_append(d == rsa_text::kLineDefer, i, slow_idx, slow_n);
   tuples[i] = tup;
   ts_out[i] = ts;
   disp[i] = d;
+}
+
+// The deferred lines, densely packed: the general parse (the regexes'
+// backtracking restated), reading from HBM.  Persistent grid over the
+// device-side count.
+constexpr uint32_t kSlowGrid = 2048;
+template <bool kReduce>
+__global__ __launch_bounds__(kParseWG) void k_parse_slow(const uint8_t* __restrict__ text,
+                                                         const uint64_t* __restrict__ off, uint64_t n_lines,
+                                                         const rsa_parse_ifc* __restrict__ ifcs, uint32_t n_ifcs,
+                                                         const rsa_parse_spell* __restrict__ spells, uint32_t n_spells,
+                                                         const uint32_t* __restrict__ slow_idx,
+                                                         const unsigned int* __restrict__ slow_n,
+                                                         rsa_tuple* __restrict__ tuples, uint32_t* __restrict__ ts_out,
+                                                         uint32_t* __restrict__ disp) {
+  const uint32_t ns = *slow_n;
+  const uint64_t n_bytes = off[n_lines];
+  const uint32_t* w32 = reinterpret_cast<const uint32_t*>(text);
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < ns; j += gridDim.x * blockDim.x) {
+    const uint64_t i = slow_idx[j];
+    const uint64_t a = off[i], b = off[i + 1];
+    uint64_t len = b - a;
+    if (len && text[b - 1] == '\n') --len;
+    rsa_tuple tup = {0u, 0u, 0, 0, 0, 0, 0};
+    uint32_t ts = 0, d = RSA_LINE_HOST;
+    const rsa_text::GWordLn s{w32, text, a, n_bytes, (uint32_t)len, ~0ull, 0u};
+    if (kReduce) {
+      rsa_text::reduce_line(s, spells, n_spells, tup, ts, d);
+      if (i > 0 && d != RSA_RED_NOISE) {
+        const uint64_t pa = off[i - 1];
+        uint64_t plen = a - pa;
+        if (plen && text[a - 1] == '\n') --plen;
+        const rsa_text::GWordLn q{w32, text, pa, n_bytes, (uint32_t)plen, ~0ull, 0u};
+        if (rsa_text::same_key(s, q)) d |= RSA_RED_SAME_KEY;
+      }
+    } else {
+      rsa_text::parse_line(s, ifcs, n_ifcs, spells, n_spells, tup, ts, d);
+    }
+    tuples[i] = tup;
+    ts_out[i] = ts;
+    disp[i] = d;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -528,15 +590,23 @@ int rsa_parse_text(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_off, uin
   if (reinterpret_cast<uintptr_t>(d_text) & 3u)
     return rsa_internal_fail(c, RSA_ERR_ARG, "rsa_parse_text: d_text must be 4-byte aligned");
   const uint64_t nb = (n_lines + kParseWG - 1) / kParseWG;
-  if (nb > 0x7FFFFFFFull) return rsa_internal_fail(c, RSA_ERR_ARG, "too many lines");
+  if (nb > 0x7FFFFFFFull || n_lines > 0xFFFFFFFFull) return rsa_internal_fail(c, RSA_ERR_ARG, "too many lines");
+  Scratch L{c, st};   // slow list: count, then the deferred line indices
+  TPCHK(c, hipMallocAsync(&L.base, 16 + n_lines * 4, st));
+  unsigned int* slow_n = static_cast<unsigned int*>(L.base);
+  uint32_t* slow_idx = reinterpret_cast<uint32_t*>(static_cast<char*>(L.base) + 16);
+  TPCHK(c, hipMemsetAsync(slow_n, 0, 4, st));
   if (rsa_internal_parse_mode(c) == 1)
     hipLaunchKernelGGL((k_parse<false, true>), dim3((uint32_t)nb), dim3(kParseWG), 0, st, d_text, d_off, n_lines, d_ifcs,
-                       n_ifcs, d_spells, n_spells, d_tuples, d_ts, d_disp);
+                       n_ifcs, d_spells, n_spells, d_tuples, d_ts, d_disp, slow_idx, slow_n);
   else
     hipLaunchKernelGGL((k_parse<false, false>), dim3((uint32_t)nb), dim3(kParseWG), 0, st, d_text, d_off, n_lines, d_ifcs,
-                       n_ifcs, d_spells, n_spells, d_tuples, d_ts, d_disp);
+                       n_ifcs, d_spells, n_spells, d_tuples, d_ts, d_disp, slow_idx, slow_n);
+  hipLaunchKernelGGL((k_parse_slow<false>), dim3((uint32_t)(nb < kSlowGrid ? nb : kSlowGrid)), dim3(kParseWG), 0, st,
+                     d_text, d_off, n_lines, d_ifcs, n_ifcs, d_spells, n_spells, slow_idx, slow_n, d_tuples, d_ts,
+                     d_disp);
   TPCHK(c, hipGetLastError());
-  return RSA_OK;
+  return RSA_OK;   // (the arenas are freed in stream order)
 }
 
 int rsa_parse_reduce(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_off, uint64_t n_lines,
@@ -559,14 +629,22 @@ int rsa_parse_reduce(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_off, u
   rsa_parse_spell* d_spells = static_cast<rsa_parse_spell*>(S.base);
   if (sb) TPCHK(c, hipMemcpyAsync(d_spells, h_spells, sb, hipMemcpyHostToDevice, st));
   TPCHK(c, hipStreamSynchronize(st));   // the host table may go away after return
+  if (n_lines > 0xFFFFFFFFull) return rsa_internal_fail(c, RSA_ERR_ARG, "too many lines");
+  Scratch L{c, st};   // slow list: count, then the deferred line indices
+  TPCHK(c, hipMallocAsync(&L.base, 16 + n_lines * 4, st));
+  unsigned int* slow_n = static_cast<unsigned int*>(L.base);
+  uint32_t* slow_idx = reinterpret_cast<uint32_t*>(static_cast<char*>(L.base) + 16);
+  TPCHK(c, hipMemsetAsync(slow_n, 0, 4, st));
   if (rsa_internal_parse_mode(c) == 1)
     hipLaunchKernelGGL((k_parse<true, true>), dim3((uint32_t)nb), dim3(kParseWG), 0, st, d_text, d_off, n_lines, nullptr,
-                       0u, d_spells, n_spells, d_tuples, d_ts, d_disp);
+                       0u, d_spells, n_spells, d_tuples, d_ts, d_disp, slow_idx, slow_n);
   else
     hipLaunchKernelGGL((k_parse<true, false>), dim3((uint32_t)nb), dim3(kParseWG), 0, st, d_text, d_off, n_lines, nullptr,
-                       0u, d_spells, n_spells, d_tuples, d_ts, d_disp);
+                       0u, d_spells, n_spells, d_tuples, d_ts, d_disp, slow_idx, slow_n);
+  hipLaunchKernelGGL((k_parse_slow<true>), dim3((uint32_t)(nb < kSlowGrid ? nb : kSlowGrid)), dim3(kParseWG), 0, st,
+                     d_text, d_off, n_lines, nullptr, 0u, d_spells, n_spells, slow_idx, slow_n, d_tuples, d_ts, d_disp);
   TPCHK(c, hipGetLastError());
-  return RSA_OK;
+  return RSA_OK;   // (the arenas are freed in stream order)
 }
 
 int rsa_order_keys(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_off, uint64_t n_lines, uint64_t base,

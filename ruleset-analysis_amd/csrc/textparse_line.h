@@ -469,8 +469,15 @@ RSA_HD bool built_template(const S& s, const Mapped& m, const Hdr& h, Reduced& r
   return true;
 }
 
-// The whole line: disposition (RSA_LINE_* | interface << 8), tuple, timestamp code.
-template <class S>
+// Disposition of a line the template pass left to the general one (k_parse
+// with kDefer; never leaves the library).
+constexpr uint32_t kLineDefer = 0xFEu;
+
+// The whole line: disposition (RSA_LINE_* | interface << 8), tuple, timestamp
+// code.  kDefer: a classified line outside the template form is not parsed
+// further (disposition kLineDefer): the general path, whose backtracking
+// searches cost a whole wave for one such lane, runs on those lines alone.
+template <bool kDefer = false, class S>
 RSA_HD void parse_line(const S& s, const rsa_parse_ifc* ifcs, uint32_t n_ifcs, const rsa_parse_spell* spells,
                        uint32_t n_spells, rsa_tuple& tup_out, uint32_t& ts_out, uint32_t& d_out) {
   rsa_tuple tup = {0u, 0u, 0, 0, 0, 0, 0};
@@ -521,6 +528,12 @@ RSA_HD void parse_line(const S& s, const rsa_parse_ifc* ifcs, uint32_t n_ifcs, c
         Reduced r;
         bool hit = false;
         const bool fast = built_template(s, m, h, r, hit);
+        if (kDefer && !fast && d == RSA_LINE_CLASSIFY) {
+          tup_out = rsa_tuple{0u, 0u, 0, 0, 0, 0, 0};
+          ts_out = 0;
+          d_out = kLineDefer;
+          return;
+        }
         if (!fast) hit = hit_test(s);
         if (hit) flags |= RSA_F_HIT;
         if (d == RSA_LINE_CLASSIFY && (fast || built_search(s, r))) {
@@ -589,7 +602,7 @@ RSA_HD bool key_span(const S& s, uint32_t& a, uint32_t& t, uint32_t& b) {
 // The reducer's per-line fields: disposition (RSA_RED_* or RSA_LINE_HOST),
 // tuple (src = FROMIP, dst = TOIP, dport = TOPORT, pspell, flags) and the
 // timestamp code of a hit line whose value the BUILT regex matches.
-template <class S>
+template <bool kDefer = false, class S>
 RSA_HD void reduce_line(const S& s, const rsa_parse_spell* spells, uint32_t n_spells, rsa_tuple& tup_out,
                         uint32_t& ts_out, uint32_t& d_out) {
   rsa_tuple tup = {0u, 0u, 0, 0, 0, 0, 0};
@@ -604,6 +617,12 @@ RSA_HD void reduce_line(const S& s, const rsa_parse_spell* spells, uint32_t n_sp
     Hdr h;
     bool hit = false;
     const bool fast = gb_match(v, m, h) && built_template(v, m, h, r, hit);   // the canonical form
+    if (kDefer && !fast) {
+      tup_out = rsa_tuple{0u, 0u, 0, 0, 0, 0, 0};
+      ts_out = 0;
+      d_out = kLineDefer;
+      return;
+    }
     if (!fast) hit = hit_test(v);
     if (hit) flags |= RSA_F_HIT;
     if (fast || built_search(v, r)) {
