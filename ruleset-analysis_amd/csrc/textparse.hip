@@ -180,6 +180,11 @@ __global__ __launch_bounds__(kParseWG) void k_parse(const uint8_t* __restrict__ 
                                                     uint32_t* __restrict__ ts_out, uint32_t* __restrict__ disp,
                                                     uint32_t* __restrict__ slow_idx, unsigned int* __restrict__ slow_n) {
   __shared__ uint32_t sm[kDirect ? 1 : kStageBytes / 4];
+  constexpr bool kScan = !kDirect && !kReduce;   // the template scan (rsa_text::tpl)
+  __shared__ uint32_t tprog[kScan ? rsa_text::tpl::kProgLen : 1];
+  __shared__ uint32_t tslot[kScan ? kParseWG * rsa_text::tpl::kSlotWords : 1];
+  if (kScan)
+    for (uint32_t k = threadIdx.x; k < rsa_text::tpl::kProgLen; k += blockDim.x) tprog[k] = rsa_text::tpl::kProg[k];
   const uint64_t l0 = (uint64_t)blockIdx.x * kParseWG;
   const uint64_t l1 = l0 + kParseWG < n_lines ? l0 + kParseWG : n_lines;
   const uint64_t n_bytes = off[n_lines];
@@ -238,7 +243,7 @@ __global__ __launch_bounds__(kParseWG) void k_parse(const uint8_t* __restrict__ 
   uint64_t len = b - a;
   if (len && text[b - 1] == '\n') --len;
   rsa_tuple tup = {0u, 0u, 0, 0, 0, 0, 0};
-  uint32_t ts = 0, d = RSA_LINE_HOST;
+  uint32_t ts = 0, d = rsa_text::kLineDefer;
   if (len < 0xFFFFFFFFull) {
     if (kReduce) {
       // the previous line: staged unless it is the workgroup's first line's predecessor
@@ -255,24 +260,26 @@ __global__ __launch_bounds__(kParseWG) void k_parse(const uint8_t* __restrict__ 
             const rsa_text::WordLn q{sm, (uint32_t)(pa - base), (uint32_t)plen};
             same = rsa_text::same_key(s, q);
           } else {
-            const rsa_text::ByteLn q{text + pa, (uint32_t)plen};
+            const rsa_text::GWordLn q{reinterpret_cast<const uint32_t*>(text), text, pa, n_bytes, (uint32_t)plen, ~0ull,
+                                      0u};
             same = rsa_text::same_key(s, q);
           }
           if (same) d |= RSA_RED_SAME_KEY;
         }
       } else {
-        const rsa_text::ByteLn s{text + a, (uint32_t)len};
-        rsa_text::reduce_line<true>(s, spells, n_spells, tup, ts, d);
-        if (pin && d != RSA_RED_NOISE && d != rsa_text::kLineDefer &&
-            rsa_text::same_key(s, rsa_text::ByteLn{text + pa, (uint32_t)plen}))
-          d |= RSA_RED_SAME_KEY;
+        d = rsa_text::kLineDefer;   // lines too long to stage: the slow pass reads them from HBM
       }
     } else if (staged) {
       const rsa_text::WordLn s{sm, (uint32_t)(a - base), (uint32_t)len};
-      rsa_text::parse_line<true>(s, ifcs, n_ifcs, spells, n_spells, tup, ts, d);
+      uint32_t* slot = tslot + threadIdx.x * rsa_text::tpl::kSlotWords;
+      if (!(rsa_text::tpl::scan(s, tprog, slot) &&
+            rsa_text::tpl_finish(s, slot, ifcs, n_ifcs, spells, n_spells, tup, ts, d))) {
+        tup = rsa_tuple{0u, 0u, 0, 0, 0, 0, 0};
+        ts = 0;
+        d = rsa_text::kLineDefer;
+      }
     } else {
-      const rsa_text::ByteLn s{text + a, (uint32_t)len};
-      rsa_text::parse_line<true>(s, ifcs, n_ifcs, spells, n_spells, tup, ts, d);
+      d = rsa_text::kLineDefer;
     }
   }
   defer_append(d == rsa_text::kLineDefer, i, slow_idx, slow_n);
@@ -305,7 +312,9 @@ __global__ __launch_bounds__(kParseWG) void k_parse_slow(const uint8_t* __restri
     rsa_tuple tup = {0u, 0u, 0, 0, 0, 0, 0};
     uint32_t ts = 0, d = RSA_LINE_HOST;
     const rsa_text::GWordLn s{w32, text, a, n_bytes, (uint32_t)len, ~0ull, 0u};
-    if (kReduce) {
+    if (len >= 0xFFFFFFFFull) {
+      // (a line of 4 GiB: the host parser's)
+    } else if (kReduce) {
       rsa_text::reduce_line(s, spells, n_spells, tup, ts, d);
       if (i > 0 && d != RSA_RED_NOISE) {
         const uint64_t pa = off[i - 1];

@@ -442,7 +442,7 @@ RSA_HD bool no_dash(const S& s, Span x) {
 // positions instead.  The hit test needs no scan either when no interface
 // name holds a '-': the only '-' are then the tag's.  False: not the
 // template, the general path decides.
-template <class S>
+template <bool kScan = true, class S>
 RSA_HD bool built_template(const S& s, const Mapped& m, const Hdr& h, Reduced& r, bool& hit) {
   if (!h.opt || !h.single || h.k != h.q) return false;
   for (uint32_t i = m.par1.a; i < m.par1.b; ++i)
@@ -464,6 +464,7 @@ RSA_HD bool built_template(const S& s, const Mapped& m, const Hdr& h, Reduced& r
     const uint32_t t = m.tag_d;
     hit = s[t] == '6' && lit(s, t + 2, "30201") && (s[t + 7] == '3' || s[t + 7] == '5');
   } else {
+    if constexpr (!kScan) return false;   // (kScan false: no scanning code in the caller's kernel)
     hit = hit_test(s);
   }
   return true;
@@ -482,9 +483,30 @@ RSA_HD void parse_line(const S& s, const rsa_parse_ifc* ifcs, uint32_t n_ifcs, c
                        uint32_t n_spells, rsa_tuple& tup_out, uint32_t& ts_out, uint32_t& d_out) {
   rsa_tuple tup = {0u, 0u, 0, 0, 0, 0, 0};
   uint32_t ts = 0, d = RSA_LINE_IGNORE;
+#if defined(RSA_TP_PROF) && RSA_TP_PROF == 1   // timing experiment: no parse
+  tup.src = s.n;
+  tup_out = tup;
+  ts_out = ts;
+  d_out = d;
+  return;
+#endif
   {
     Mapped m;
     Hdr h;
+#if defined(RSA_TP_PROF) && RSA_TP_PROF >= 2   // timing experiment: the mapper regex (+ template) only
+    {
+      const bool g = gb_match(s, m, h);
+      Reduced r;
+      bool hit = false;
+      const bool f = RSA_TP_PROF == 3 && g && built_template(s, m, h, r, hit);
+      tup.src = g ? m.ip1.b + m.p2.b : 0u;
+      tup.dst = f ? r.year.a + r.time.b + hit : 0u;
+      tup_out = tup;
+      ts_out = ts;
+      d_out = d;
+      return;
+    }
+#endif
     if (gb_match(s, m, h)) {
       d = RSA_LINE_CLASSIFY;
       const Span src = m.inbound ? m.ip1 : m.ip2, dst = m.inbound ? m.ip2 : m.ip1;
@@ -527,16 +549,25 @@ RSA_HD void parse_line(const S& s, const rsa_parse_ifc* ifcs, uint32_t n_ifcs, c
         uint32_t flags = RSA_F_VALID;
         Reduced r;
         bool hit = false;
-        const bool fast = built_template(s, m, h, r, hit);
-        if (kDefer && !fast && d == RSA_LINE_CLASSIFY) {
-          tup_out = rsa_tuple{0u, 0u, 0, 0, 0, 0, 0};
-          ts_out = 0;
-          d_out = kLineDefer;
-          return;
+        const bool fast = built_template<!kDefer>(s, m, h, r, hit);
+        bool built = fast;
+        if constexpr (kDefer) {
+          // the general searches are not even compiled into the template
+          // pass (code size: the kernel stays in the instruction cache)
+          if (!fast && d == RSA_LINE_CLASSIFY) {
+            tup_out = rsa_tuple{0u, 0u, 0, 0, 0, 0, 0};
+            ts_out = 0;
+            d_out = kLineDefer;
+            return;
+          }
+        } else {
+          if (!fast) {
+            hit = hit_test(s);
+            built = d == RSA_LINE_CLASSIFY && built_search(s, r);
+          }
         }
-        if (!fast) hit = hit_test(s);
         if (hit) flags |= RSA_F_HIT;
-        if (d == RSA_LINE_CLASSIFY && (fast || built_search(s, r))) {
+        if (d == RSA_LINE_CLASSIFY && built) {
           flags |= RSA_F_BUILT;
           uint32_t vf = 0, vt = 0;
           if (span_eq(s, r.for_ip, src) && span_eq(s, r.to_ip, dst) && span_eq(s, r.to_port, dp)) {
@@ -570,6 +601,229 @@ RSA_HD void parse_line(const S& s, const rsa_parse_ifc* ifcs, uint32_t n_ifcs, c
   tup_out = tup;
   ts_out = ts;
   d_out = d;
+}
+
+// ---- The template pass as one position-synchronous scan (k_parse).
+//
+// parse_line's sequential form runs data-dependent loops per lane (runs of
+// digits, literals, searches): a wave pays for every loop of every lane, and
+// the exec-mask bookkeeping of that divergence is scalar work the CU's one
+// scalar unit serialises over its four SIMDs (~16K SALU per 64-line wave).
+// Here every lane steps through its line one byte per iteration, all lanes on
+// the same byte index, through a fixed program of segments (literal bytes, or
+// runs of a character class with length bounds, each followed by one literal
+// byte), with branch-free updates of running values: the decimal value of the
+// current digit group, the dotted-quad value, the last eight letters, the run
+// start, and at each run end the field's value into a per-lane slot.  Only
+// the canonical form is accepted (exactly built_template's lines, plus the
+// device's canonical-text conditions); anything else is left to the general
+// parse.  Every accepted line gets parse_line's own disposition, tuple and
+// timestamp code (tests/test_textparse.py checks that on the CPU).
+namespace tpl {
+
+enum Field : uint32_t {
+  fM1, fHH, fMM, fSS, fM2, fD2, fY, fTAG, fSEV, fMSG, fDIR, fPROTO, fIF1, fIP1, fP1, fIF2, fIP2, fP2, kFields,
+  fNone = 31
+};
+enum Kind : uint32_t { kNum = 0, kIp = 1, kAlpha = 2, kIfcK = 3 };
+constexpr uint32_t kind_of(uint32_t f) {
+  return (f == fIP1 || f == fIP2) ? kIp
+         : (f == fM1 || f == fM2 || f == fTAG || f == fDIR || f == fPROTO) ? kAlpha
+         : (f == fIF1 || f == fIF2) ? kIfcK
+                                    : kNum;
+}
+constexpr unsigned long long kinds_word() {
+  unsigned long long w = 0;
+  for (uint32_t f = 0; f < 32; ++f) w |= (unsigned long long)kind_of(f) << (2 * f);
+  return w;
+}
+constexpr unsigned long long kKinds = kinds_word();
+
+// character classes
+constexpr uint32_t cD = 1, cU = 2, cL = 4, cDot = 8, cSl = 16, cDash = 32, cUnd = 64;
+RSA_HD uint32_t cls_of(uint32_t c) {
+  return (c - '0' < 10u ? cD : 0u) | (c - 'A' < 26u ? cU : 0u) | (c - 'a' < 26u ? cL : 0u) | (c == '.' ? cDot : 0u) |
+         (c == '/' ? cSl : 0u) | (c == '-' ? cDash : 0u) | (c == '_' ? cUnd : 0u);
+}
+
+// segment: literal / follow byte 8 | class mask 8 (0: a literal) | min 3 | max 8 | field 5
+constexpr uint32_t R(uint32_t msk, uint32_t mn, uint32_t mx, char follow, uint32_t fld) {
+  return (uint32_t)(uint8_t)follow | msk << 8 | mn << 16 | mx << 19 | fld << 27;
+}
+constexpr uint32_t L(char ch) { return (uint32_t)(uint8_t)ch | (uint32_t)fNone << 27; }
+constexpr uint32_t kEndSeg = 7u << 16 | (uint32_t)fNone << 27;   // a literal that matches nothing
+constexpr uint32_t cIfc = cD | cU | cL | cDash | cUnd;
+
+// Mmm D HH:MM:SS Mmm D YYYY HH:MM:SS: %TAG-d-dddddd: Built DIR PROTO connection N
+// for IF:IP/P (IP/P) to IF:IP/P (IP/P)
+constexpr uint32_t kProg[] = {
+    R(cU | cL, 3, 3, ' ', fM1), R(cD, 1, 2, ' ', fNone), R(cD, 2, 2, ':', fHH), R(cD, 2, 2, ':', fMM),
+    R(cD, 2, 2, ' ', fSS), R(cU | cL, 3, 3, ' ', fM2), R(cD, 1, 2, ' ', fD2), R(cD, 4, 4, ' ', fY),
+    R(cD, 2, 2, ':', fNone), R(cD, 2, 2, ':', fNone), R(cD, 2, 2, ':', fNone), L(' '), L('%'),
+    R(cU, 3, 4, '-', fTAG), R(cD, 1, 1, '-', fSEV), R(cD, 6, 6, ':', fMSG), L(' '), L('B'), L('u'), L('i'), L('l'),
+    L('t'), L(' '), R(cL, 7, 8, ' ', fDIR), R(cU, 3, 3, ' ', fPROTO), L('c'), L('o'), L('n'), L('n'), L('e'),
+    L('c'), L('t'), L('i'), L('o'), L('n'), L(' '), R(cD, 1, 255, ' ', fNone), L('f'), L('o'), L('r'), L(' '),
+    R(cIfc, 1, 255, ':', fIF1), R(cD | cDot, 1, 255, '/', fIP1), R(cD, 1, 255, ' ', fP1), L('('),
+    R(cD | cDot | cSl, 0, 255, ')', fNone), L(' '), L('t'), L('o'), L(' '), R(cIfc, 1, 255, ':', fIF2),
+    R(cD | cDot, 1, 255, '/', fIP2), R(cD, 1, 255, ' ', fP2), L('('), R(cD | cDot | cSl, 0, 255, ')', fNone),
+    kEndSeg};
+constexpr uint32_t kProgLen = sizeof(kProg) / sizeof(kProg[0]);
+constexpr uint32_t kSlotWords = 2 * (kFields + 1);   // v0, v1 per field + a dummy slot
+
+constexpr uint32_t pack3(char a, char b, char c) { return (uint32_t)(uint8_t)a << 16 | (uint32_t)(uint8_t)b << 8 | (uint8_t)c; }
+
+// The scan.  P: the program (LDS copy on the device), Q: the lane's kSlotWords
+// slot words.  True: the line has the template form (slots hold its fields).
+template <class S, class P, class Q>
+RSA_HD bool scan(const S& s, P prog, Q slot) {
+  uint32_t seg = 0, cnt = 0, num = 0, ng = 0, ipv = 0, dots = 0, bad = 0, fz = 0, aw_lo = 0, aw_hi = 0, pos0 = 0,
+           dash = 0;
+  bool ok = true;
+  for (uint32_t i = 0; i < s.n; ++i) {
+    const uint32_t c = s[i];
+    const uint32_t desc = prog[seg];
+    const uint32_t lit = desc & 0xFFu, msk = (desc >> 8) & 0xFFu, mn = (desc >> 16) & 7u, mx = (desc >> 19) & 0xFFu,
+                   fld = desc >> 27;
+    const bool is_run = msk != 0;
+    const uint32_t cl = cls_of(c);
+    const bool start = is_run && cnt == 0;
+    num = start ? 0u : num;
+    ng = start ? 0u : ng;
+    ipv = start ? 0u : ipv;
+    dots = start ? 0u : dots;
+    bad = start ? 0u : bad;
+    fz = start ? 0u : fz;
+    aw_lo = start ? 0u : aw_lo;
+    aw_hi = start ? 0u : aw_hi;
+    dash = start ? 0u : dash;
+    pos0 = start ? i : pos0;
+    const bool cont = is_run && (cl & msk) != 0 && cnt < mx;
+    // a run ends at this byte: its field's value into the slot (dummy slot otherwise)
+    const bool rend = ok && is_run && !cont;
+    const uint32_t kind = (uint32_t)(kKinds >> (2 * fld)) & 3u;
+    const uint32_t lz = (fz && ng > 1) ? 1u : 0u;   // a multi-digit group with a leading zero
+    const uint32_t ipbad = bad | (ng == 0 ? 1u : 0u) | (num > 255 ? 1u : 0u) | (ng > 3 ? 1u : 0u) | lz;
+    const uint32_t v0 = kind == kIp ? (ipv << 8 | num) : kind == kNum ? num : kind == kAlpha ? aw_lo : pos0;
+    const uint32_t v1 = kind == kIp ? (dots | ipbad << 8) : kind == kNum ? (ng | lz << 8)
+                        : kind == kAlpha                  ? aw_hi
+                                                          : (cnt | dash << 8);
+    const uint32_t at = (rend && fld < kFields) ? 2 * fld : 2 * kFields;
+    slot[at] = v0;
+    slot[at + 1] = v1;
+    // the byte joins the run
+    const bool isd = (cl & cD) != 0, isdot = c == '.';
+    const uint32_t dv = c - '0';
+    if (cont) {
+      aw_hi = aw_hi << 8 | aw_lo >> 24;
+      aw_lo = aw_lo << 8 | c;
+      dash |= c == '-' ? 1u : 0u;
+      const uint32_t nn = num * 10u + dv;
+      fz = isd ? (ng == 0 ? (dv == 0 ? 1u : 0u) : fz) : (isdot ? 0u : fz);
+      bad |= isdot ? ipbad : 0u;
+      ipv = isdot ? (ipv << 8 | num) : ipv;
+      dots += isdot ? 1u : 0u;
+      num = isd ? (nn > 0xFFFFFu ? 0xFFFFFu : nn) : (isdot ? 0u : num);
+      ng = isd ? ng + 1 : (isdot ? 0u : ng);
+    }
+    const bool step_ok = is_run ? (cont || (cnt >= mn && c == lit)) : (c == lit && desc != kEndSeg);
+    ok = ok && step_ok;
+    seg = (ok && !cont) ? seg + 1 : seg;
+    seg = seg < kProgLen ? seg : kProgLen - 1;
+    cnt = cont ? cnt + 1 : 0u;
+  }
+  return ok && prog[seg] == kEndSeg;
+}
+
+}  // namespace tpl
+
+// parse_line for a line tpl::scan accepted, from its slots; false: leave the
+// line to the general parse (everything parse_line would send to the host,
+// and a '-' in an interface name, where the hit test must scan).
+template <class S, class Q>
+RSA_HD bool tpl_finish(const S& s, Q slot, const rsa_parse_ifc* ifcs, uint32_t n_ifcs, const rsa_parse_spell* spells,
+                       uint32_t n_spells, rsa_tuple& tup, uint32_t& ts, uint32_t& d) {
+  using namespace tpl;
+  auto v0 = [&](uint32_t f) { return (uint32_t)slot[2 * f]; };
+  auto v1 = [&](uint32_t f) { return (uint32_t)slot[2 * f + 1]; };
+  auto ulll = [](uint32_t w) {   // [A-Z][a-z]{2}, packed big-endian in 24 bits
+    return is_upper(w >> 16 & 0xFFu) && is_lower(w >> 8 & 0xFFu) && is_lower(w & 0xFFu);
+  };
+  if (!ulll(v0(fM1)) || !ulll(v0(fM2))) return false;
+  const uint32_t tag = v0(fTAG);
+  if (!(tag == pack3('A', 'S', 'A') || tag == pack3('P', 'I', 'X') ||
+        (tag == ('F' << 24 | 'W' << 16 | 'S' << 8 | 'M') && v1(fTAG) == 0)))
+    return false;
+  const uint32_t dl = v0(fDIR), dh = v1(fDIR);   // last eight letters
+  const bool inbound = dh == ('i' << 16 | 'n' << 8 | 'b') && dl == ('o' << 24 | 'u' << 16 | 'n' << 8 | 'd');
+  const bool outbound = dh == ('o' << 24 | 'u' << 16 | 't' << 8 | 'b') && dl == ('o' << 24 | 'u' << 16 | 'n' << 8 | 'd');
+  if (!inbound && !outbound) return false;
+  const uint32_t proto = v0(fPROTO);
+  const bool udp = proto == pack3('U', 'D', 'P');
+  if (!udp && proto != pack3('T', 'C', 'P')) return false;
+  if ((v1(fIF1) >> 8) | (v1(fIF2) >> 8)) return false;          // '-' in an interface name
+  if (v1(fIP1) != 3 || v1(fIP2) != 3) return false;             // not canonical dotted quads
+  const uint32_t p1 = v0(fP1), p2 = v0(fP2);
+  if (p1 > 65535u || p2 > 65535u || (v1(fP2) >> 8)) return false;   // long ports; TOPORT text not canonical
+  const uint32_t ip1 = v0(fIP1), ip2 = v0(fIP2);
+  const uint32_t src = inbound ? ip1 : ip2, dst = inbound ? ip2 : ip1;
+  const uint32_t sp = inbound ? p1 : p2, dp = inbound ? p2 : p1;
+  // the interface of the ingress side
+  const uint32_t ia = inbound ? v0(fIF1) : v0(fIF2), il = (inbound ? v1(fIF1) : v1(fIF2)) & 0xFFu;
+  int32_t found = -1;
+  if (il > RSA_IFC_NAME_MAX) return false;
+  for (uint32_t k = 0; k < n_ifcs && found < 0; ++k) {
+    if (ifcs[k].len != il) continue;
+    bool eq = true;
+    for (uint32_t c = 0; c < il && eq; ++c) eq = s[ia + c] == (uint8_t)ifcs[k].name[c];
+    if (eq) found = (int32_t)k;
+  }
+  tup = rsa_tuple{0u, 0u, 0, 0, 0, 0, 0};
+  ts = 0;
+  if (found < 0) {
+    d = RSA_LINE_NOACL;
+    return true;
+  }
+  if (ifcs[found].kind == RSA_LINE_MISSING) {
+    d = RSA_LINE_MISSING | ((uint32_t)found << 8);
+    return true;
+  }
+  if (ifcs[found].kind != RSA_LINE_CLASSIFY) return false;
+  const uint32_t lid = udp ? ifcs[found].list_udp : ifcs[found].list_tcp;
+  if (lid == RSA_LIST_HOST) return false;
+  // the reducer's fields: FROMIP = the first address, TOIP = the second, TOPORT = P2
+  const uint32_t sev = v0(fSEV), msg = v0(fMSG);
+  const bool hit = sev == 6 && (msg == 302013 || msg == 302015);
+  uint32_t flags = RSA_F_VALID | RSA_F_BUILT | (hit ? RSA_F_HIT : 0u);
+  // outbound: the reducer key is (IP1, IP2, P2) = (dst, src, sport) -- unless its
+  // text equals the (src, dst, dport) one, which parse_line's first test takes
+  if (outbound && !(ip1 == ip2 && p1 == p2 && (v1(fP1) & 0xFFu) == (v1(fP2) & 0xFFu) && !(v1(fP1) >> 8)))
+    flags |= RSA_F_SWAP;
+  if (hit) {
+    // ts_code: HH:MM:SS of the syslog header, the device date's month, day, year
+    const char* const months = "JanFebMarAprMayJunJulAugSepOctNovDec";
+    const uint32_t mw = v0(fM2);
+    int mo = -1;
+    for (int k = 0; k < 12; ++k)
+      if (mw == pack3(months[3 * k], months[3 * k + 1], months[3 * k + 2])) mo = k;
+    const uint32_t y = v0(fY), day = v0(fD2), hh = v0(fHH), mm = v0(fMM), ss = v0(fSS);
+    if (mo < 0 || y < RSA_TS_YEAR0 || y >= RSA_TS_YEAR0 + 128 || day > 31 || hh > 23 || mm > 59 || ss > 59)
+      return false;
+    ts = ((((y - RSA_TS_YEAR0) * 12u + (uint32_t)mo) * 32u + day) * 86400u) + hh * 3600u + mm * 60u + ss;
+  }
+  int32_t sid = -1;
+  for (uint32_t k = 0; k < n_spells && sid < 0; ++k)
+    if (spells[k].len == 3 && pack3(spells[k].word[0], spells[k].word[1], spells[k].word[2]) == proto)
+      sid = (int32_t)k;
+  if (sid < 0) return false;
+  tup.src = src;
+  tup.dst = dst;
+  tup.sport = (uint16_t)sp;
+  tup.dport = (uint16_t)dp;
+  tup.list = (uint16_t)lid;
+  tup.flags = (uint8_t)flags;
+  tup.pspell = (uint8_t)sid;
+  d = RSA_LINE_CLASSIFY;
+  return true;
 }
 
 // ---- the reducer drop-in: one line of the sorted mapper stream
@@ -616,16 +870,23 @@ RSA_HD void reduce_line(const S& s, const rsa_parse_spell* spells, uint32_t n_sp
     Mapped m;
     Hdr h;
     bool hit = false;
-    const bool fast = gb_match(v, m, h) && built_template(v, m, h, r, hit);   // the canonical form
-    if (kDefer && !fast) {
-      tup_out = rsa_tuple{0u, 0u, 0, 0, 0, 0, 0};
-      ts_out = 0;
-      d_out = kLineDefer;
-      return;
+    const bool fast = gb_match(v, m, h) && built_template<!kDefer>(v, m, h, r, hit);   // the canonical form
+    bool built = fast;
+    if constexpr (kDefer) {
+      if (!fast) {
+        tup_out = rsa_tuple{0u, 0u, 0, 0, 0, 0, 0};
+        ts_out = 0;
+        d_out = kLineDefer;
+        return;
+      }
+    } else {
+      if (!fast) {
+        hit = hit_test(v);
+        built = built_search(v, r);
+      }
     }
-    if (!fast) hit = hit_test(v);
     if (hit) flags |= RSA_F_HIT;
-    if (fast || built_search(v, r)) {
+    if (built) {
       flags |= RSA_F_BUILT;
       uint32_t vf = 0, vt = 0;
       const uint32_t pv = port_val(v, r.to_port);

@@ -457,3 +457,47 @@ def test_template_fast_path_equals_general_parse():
     a = out[len(clean) + len(fuzz):]
     assert a[0] == a[1] == a[2] == a[4] == a[5] == a[6] == a[7] == a[8] == a[9] == a[14] == 1
     assert [a[k] for k in (3, 10, 11, 12, 13, 15, 16)] == [0] * 7, a.tolist()
+
+
+@pytest.mark.parametrize('seed', [1, 2, 3])
+def test_template_scan_equals_general_parse(seed):
+    """textparse_line.h tpl::scan + tpl_finish (k_parse's branch-free pass)
+    give parse_line's exact disposition, tuple and timestamp code on every
+    line they accept: rendered lines (nearly all accepted), fuzzed lines,
+    lines aimed at the scan's bounds, with missing and host-decided ACLs."""
+    lib = _harness()
+    db, fuzz = _fuzz_lines(seed, 6000)
+    dbj, info = synth.make_db(11, 300, interfaces=('outside', 'partner'))
+    dbj['firewalls']['fw1']['dmz'] = {'in': 'dmz_missing_acl'}
+    clean = [l + '\n' for l in synth.render_lines(synth.make_traffic((dbj, info), 4000, seed=seed + 10))]
+    head = 'Jul 15 00:00:01 Jul 15 2013 00:00:01: %ASA-6-302013: '
+    body = 'Built inbound TCP connection 5 for outside:10.0.0.1/1234 (10.0.0.1/1234) to inside:10.0.0.2/80 (10.0.0.2/80)'
+    aimed = [head + body, head.replace('Jul 15 2013', 'Jul 5 2013') + body, head.replace('2013', '1999') + body,
+             head.replace('2013', '2128') + body, head.replace('00:00:01 Jul', '24:00:01 Jul') + body,
+             head.replace('Jul 15 2013', 'Jux 15 2013') + body, head.replace('Jul 15 2013', 'Jul 32 2013') + body,
+             head + body.replace('/80 ', '/080 '), head + body.replace('/1234 (', '/01234 ('),
+             head + body.replace('10.0.0.1/', '10.0.0.01/'), head + body.replace('10.0.0.2/', '10.0.0.256/'),
+             head + body.replace('/80 ', '/65536 '), head + body.replace('outside:', 'dmz:'),
+             head + body.replace('outside:', 'nowhere:'), head.replace('ASA', 'FWSM') + body,
+             head.replace('ASA', 'PIXX') + body, head + body.replace('TCP', 'ICMP'),
+             head + body.replace('inbound', 'outbound'),
+             head + body.replace('inbound', 'outbound').replace('/1234 (10.0.0.1/1234)', '/80 (10.0.0.1/80)')
+             .replace('10.0.0.1', '10.0.0.2'),
+             head + body.replace('inbound', 'outbound').replace('/1234 (10.0.0.1/1234)', '/080 (x)')
+             .replace('10.0.0.1', '10.0.0.2'),
+             head.replace('6-302013', '6-302015') + body.replace('TCP', 'UDP'), head.replace('-6-', '-5-') + body]
+    lines = clean + fuzz + [a + '\n' for a in aimed]
+    data = ''.join(lines).encode('latin-1')
+    off = np.cumsum([0] + [len(l.encode('latin-1')) for l in lines]).astype(np.uint64)
+    cg = CompiledRules(acldb.load_json(dbj))
+    ifcs, _names = textparse.interface_table(acldb.load_json(dbj), cg, 'fw1')
+    sp = textparse.spell_table(list(textparse.DEFAULT_SPELLS))
+    out = np.zeros(len(lines), np.uint8)
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    buf = np.frombuffer(data, np.uint8).copy()
+    lib.tpl_check_host(p(buf), p(off), ctypes.c_uint64(len(lines)), p(ifcs), ctypes.c_uint32(len(ifcs)), p(sp),
+                       ctypes.c_uint32(len(sp)), p(out))
+    assert not (out == 2).any(), [lines[i] for i in np.nonzero(out == 2)[0][:3]]
+    assert (out[:len(clean)] == 1).mean() > 0.88
+    a = out[len(clean) + len(fuzz):].tolist()
+    assert a[0] == a[1] == a[12] == a[13] == a[14] == a[17] == a[18] == a[20] == a[21] == 1, a
