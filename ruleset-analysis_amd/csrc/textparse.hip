@@ -182,9 +182,13 @@ __global__ __launch_bounds__(kParseWG) void k_parse(const uint8_t* __restrict__ 
   __shared__ uint32_t sm[kDirect ? 1 : kStageBytes / 4];
   constexpr bool kScan = !kDirect && !kReduce;   // the template scan (rsa_text::tpl)
   __shared__ uint32_t tprog[kScan ? rsa_text::tpl::kProgLen : 1];
+  __shared__ uint8_t tcls[kScan ? 256 : 1];
   __shared__ uint32_t tslot[kScan ? kParseWG * rsa_text::tpl::kSlotWords : 1];
-  if (kScan)
+  if (kScan) {
+    constexpr rsa_text::tpl::ClsTable kCls = rsa_text::tpl::cls_table();
     for (uint32_t k = threadIdx.x; k < rsa_text::tpl::kProgLen; k += blockDim.x) tprog[k] = rsa_text::tpl::kProg[k];
+    for (uint32_t k = threadIdx.x; k < 256; k += blockDim.x) tcls[k] = kCls.t[k];
+  }
   const uint64_t l0 = (uint64_t)blockIdx.x * kParseWG;
   const uint64_t l1 = l0 + kParseWG < n_lines ? l0 + kParseWG : n_lines;
   const uint64_t n_bytes = off[n_lines];
@@ -272,7 +276,7 @@ __global__ __launch_bounds__(kParseWG) void k_parse(const uint8_t* __restrict__ 
     } else if (staged) {
       const rsa_text::WordLn s{sm, (uint32_t)(a - base), (uint32_t)len};
       uint32_t* slot = tslot + threadIdx.x * rsa_text::tpl::kSlotWords;
-      if (!(rsa_text::tpl::scan(s, tprog, slot) &&
+      if (!(rsa_text::tpl::scan(s, tprog, tcls, slot) &&
             rsa_text::tpl_finish(s, slot, ifcs, n_ifcs, spells, n_spells, tup, ts, d))) {
         tup = rsa_tuple{0u, 0u, 0, 0, 0, 0, 0};
         ts = 0;

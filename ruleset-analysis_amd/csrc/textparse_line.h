@@ -625,23 +625,9 @@ enum Field : uint32_t {
   fM1, fHH, fMM, fSS, fM2, fD2, fY, fTAG, fSEV, fMSG, fDIR, fPROTO, fIF1, fIP1, fP1, fIF2, fIP2, fP2, kFields,
   fNone = 31
 };
-enum Kind : uint32_t { kNum = 0, kIp = 1, kAlpha = 2, kIfcK = 3 };
-constexpr uint32_t kind_of(uint32_t f) {
-  return (f == fIP1 || f == fIP2) ? kIp
-         : (f == fM1 || f == fM2 || f == fTAG || f == fDIR || f == fPROTO) ? kAlpha
-         : (f == fIF1 || f == fIF2) ? kIfcK
-                                    : kNum;
-}
-constexpr unsigned long long kinds_word() {
-  unsigned long long w = 0;
-  for (uint32_t f = 0; f < 32; ++f) w |= (unsigned long long)kind_of(f) << (2 * f);
-  return w;
-}
-constexpr unsigned long long kKinds = kinds_word();
-
 // character classes
 constexpr uint32_t cD = 1, cU = 2, cL = 4, cDot = 8, cSl = 16, cDash = 32, cUnd = 64;
-RSA_HD uint32_t cls_of(uint32_t c) {
+constexpr uint32_t cls_of(uint32_t c) {
   return (c - '0' < 10u ? cD : 0u) | (c - 'A' < 26u ? cU : 0u) | (c - 'a' < 26u ? cL : 0u) | (c == '.' ? cDot : 0u) |
          (c == '/' ? cSl : 0u) | (c == '-' ? cDash : 0u) | (c == '_' ? cUnd : 0u);
 }
@@ -668,16 +654,19 @@ constexpr uint32_t kProg[] = {
     R(cD | cDot, 1, 255, '/', fIP2), R(cD, 1, 255, ' ', fP2), L('('), R(cD | cDot | cSl, 0, 255, ')', fNone),
     kEndSeg};
 constexpr uint32_t kProgLen = sizeof(kProg) / sizeof(kProg[0]);
-constexpr uint32_t kSlotWords = 2 * (kFields + 1);   // v0, v1 per field + a dummy slot
+constexpr uint32_t kSlotWords = kFields + 1;   // one span per field + a dummy slot
 
 constexpr uint32_t pack3(char a, char b, char c) { return (uint32_t)(uint8_t)a << 16 | (uint32_t)(uint8_t)b << 8 | (uint8_t)c; }
 
-// The scan.  P: the program (LDS copy on the device), Q: the lane's kSlotWords
-// slot words.  True: the line has the template form (slots hold its fields).
-template <class S, class P, class Q>
-RSA_HD bool scan(const S& s, P prog, Q slot) {
-  uint32_t seg = 0, cnt = 0, num = 0, ng = 0, ipv = 0, dots = 0, bad = 0, fz = 0, aw_lo = 0, aw_hi = 0, pos0 = 0,
-           dash = 0;
+// The scan.  P: the program (LDS copy on the device), C: the class of each
+// byte value (cls_of, an LDS table on the device), Q: the lane's kSlotWords
+// slot words, each field's span as start | length << 16.  True: the line has
+// the template form.  All lanes step together (the loop runs to the longest
+// line of the wave); the body is selects only.
+template <class S, class P, class C, class Q>
+RSA_HD bool scan(const S& s, P prog, C cls, Q slot) {
+  if (s.n > 0xFFFFu) return false;
+  uint32_t seg = 0, cnt = 0, pos0 = 0;
   bool ok = true;
   for (uint32_t i = 0; i < s.n; ++i) {
     const uint32_t c = s[i];
@@ -685,53 +674,26 @@ RSA_HD bool scan(const S& s, P prog, Q slot) {
     const uint32_t lit = desc & 0xFFu, msk = (desc >> 8) & 0xFFu, mn = (desc >> 16) & 7u, mx = (desc >> 19) & 0xFFu,
                    fld = desc >> 27;
     const bool is_run = msk != 0;
-    const uint32_t cl = cls_of(c);
-    const bool start = is_run && cnt == 0;
-    num = start ? 0u : num;
-    ng = start ? 0u : ng;
-    ipv = start ? 0u : ipv;
-    dots = start ? 0u : dots;
-    bad = start ? 0u : bad;
-    fz = start ? 0u : fz;
-    aw_lo = start ? 0u : aw_lo;
-    aw_hi = start ? 0u : aw_hi;
-    dash = start ? 0u : dash;
-    pos0 = start ? i : pos0;
-    const bool cont = is_run && (cl & msk) != 0 && cnt < mx;
-    // a run ends at this byte: its field's value into the slot (dummy slot otherwise)
-    const bool rend = ok && is_run && !cont;
-    const uint32_t kind = (uint32_t)(kKinds >> (2 * fld)) & 3u;
-    const uint32_t lz = (fz && ng > 1) ? 1u : 0u;   // a multi-digit group with a leading zero
-    const uint32_t ipbad = bad | (ng == 0 ? 1u : 0u) | (num > 255 ? 1u : 0u) | (ng > 3 ? 1u : 0u) | lz;
-    const uint32_t v0 = kind == kIp ? (ipv << 8 | num) : kind == kNum ? num : kind == kAlpha ? aw_lo : pos0;
-    const uint32_t v1 = kind == kIp ? (dots | ipbad << 8) : kind == kNum ? (ng | lz << 8)
-                        : kind == kAlpha                  ? aw_hi
-                                                          : (cnt | dash << 8);
-    const uint32_t at = (rend && fld < kFields) ? 2 * fld : 2 * kFields;
-    slot[at] = v0;
-    slot[at + 1] = v1;
-    // the byte joins the run
-    const bool isd = (cl & cD) != 0, isdot = c == '.';
-    const uint32_t dv = c - '0';
-    if (cont) {
-      aw_hi = aw_hi << 8 | aw_lo >> 24;
-      aw_lo = aw_lo << 8 | c;
-      dash |= c == '-' ? 1u : 0u;
-      const uint32_t nn = num * 10u + dv;
-      fz = isd ? (ng == 0 ? (dv == 0 ? 1u : 0u) : fz) : (isdot ? 0u : fz);
-      bad |= isdot ? ipbad : 0u;
-      ipv = isdot ? (ipv << 8 | num) : ipv;
-      dots += isdot ? 1u : 0u;
-      num = isd ? (nn > 0xFFFFFu ? 0xFFFFFu : nn) : (isdot ? 0u : num);
-      ng = isd ? ng + 1 : (isdot ? 0u : ng);
-    }
-    const bool step_ok = is_run ? (cont || (cnt >= mn && c == lit)) : (c == lit && desc != kEndSeg);
+    pos0 = cnt == 0 ? i : pos0;
+    const bool cont = (cls[c] & msk) != 0 && cnt < mx;   // (msk 0: a literal, never a run byte)
+    const bool rend = ok && is_run && !cont;               // a run ends here: its span into the slot
+    slot[(rend && fld < kFields) ? fld : kFields] = pos0 | cnt << 16;
+    const bool step_ok = cont || ((cnt >= mn || !is_run) && c == lit && desc != kEndSeg);
     ok = ok && step_ok;
-    seg = (ok && !cont) ? seg + 1 : seg;
-    seg = seg < kProgLen ? seg : kProgLen - 1;
+    seg = (ok && !cont && seg + 1 < kProgLen) ? seg + 1 : seg;
     cnt = cont ? cnt + 1 : 0u;
   }
   return ok && prog[seg] == kEndSeg;
+}
+
+// the byte classes as a table (the device copies it to LDS)
+struct ClsTable {
+  uint8_t t[256];
+};
+constexpr ClsTable cls_table() {
+  ClsTable x{};
+  for (uint32_t c = 0; c < 256; ++c) x.t[c] = (uint8_t)cls_of(c);
+  return x;
 }
 
 }  // namespace tpl
@@ -743,32 +705,35 @@ template <class S, class Q>
 RSA_HD bool tpl_finish(const S& s, Q slot, const rsa_parse_ifc* ifcs, uint32_t n_ifcs, const rsa_parse_spell* spells,
                        uint32_t n_spells, rsa_tuple& tup, uint32_t& ts, uint32_t& d) {
   using namespace tpl;
-  auto v0 = [&](uint32_t f) { return (uint32_t)slot[2 * f]; };
-  auto v1 = [&](uint32_t f) { return (uint32_t)slot[2 * f + 1]; };
+  auto at = [&](uint32_t f) { return (uint32_t)slot[f] & 0xFFFFu; };
+  auto len = [&](uint32_t f) { return ((uint32_t)slot[f] >> 16) & 0xFFu; };
+  auto span = [&](uint32_t f) { return Span{at(f), at(f) + len(f)}; };
+  auto num = [&](uint32_t f) { return small_num(s, span(f)); };   // <= 6 digits here
+  auto word3 = [&](uint32_t f) { const uint32_t a = at(f); return (uint32_t)(s[a] << 16 | s[a + 1] << 8 | s[a + 2]); };
   auto ulll = [](uint32_t w) {   // [A-Z][a-z]{2}, packed big-endian in 24 bits
     return is_upper(w >> 16 & 0xFFu) && is_lower(w >> 8 & 0xFFu) && is_lower(w & 0xFFu);
   };
-  if (!ulll(v0(fM1)) || !ulll(v0(fM2))) return false;
-  const uint32_t tag = v0(fTAG);
-  if (!(tag == pack3('A', 'S', 'A') || tag == pack3('P', 'I', 'X') ||
-        (tag == ('F' << 24 | 'W' << 16 | 'S' << 8 | 'M') && v1(fTAG) == 0)))
+  const uint32_t m2 = word3(fM2);
+  if (!ulll(word3(fM1)) || !ulll(m2)) return false;
+  const uint32_t tag = word3(fTAG);
+  if (len(fTAG) == 3 ? !(tag == pack3('A', 'S', 'A') || tag == pack3('P', 'I', 'X'))
+                     : !(tag == pack3('F', 'W', 'S') && s[at(fTAG) + 3] == 'M'))
     return false;
-  const uint32_t dl = v0(fDIR), dh = v1(fDIR);   // last eight letters
-  const bool inbound = dh == ('i' << 16 | 'n' << 8 | 'b') && dl == ('o' << 24 | 'u' << 16 | 'n' << 8 | 'd');
-  const bool outbound = dh == ('o' << 24 | 'u' << 16 | 't' << 8 | 'b') && dl == ('o' << 24 | 'u' << 16 | 'n' << 8 | 'd');
+  const bool inbound = len(fDIR) == 7 && lit(s, at(fDIR), "inbound");
+  const bool outbound = len(fDIR) == 8 && lit(s, at(fDIR), "outbound");
   if (!inbound && !outbound) return false;
-  const uint32_t proto = v0(fPROTO);
+  const uint32_t proto = word3(fPROTO);
   const bool udp = proto == pack3('U', 'D', 'P');
   if (!udp && proto != pack3('T', 'C', 'P')) return false;
-  if ((v1(fIF1) >> 8) | (v1(fIF2) >> 8)) return false;          // '-' in an interface name
-  if (v1(fIP1) != 3 || v1(fIP2) != 3) return false;             // not canonical dotted quads
-  const uint32_t p1 = v0(fP1), p2 = v0(fP2);
-  if (p1 > 65535u || p2 > 65535u || (v1(fP2) >> 8)) return false;   // long ports; TOPORT text not canonical
-  const uint32_t ip1 = v0(fIP1), ip2 = v0(fIP2);
+  if (!no_dash(s, span(fIF1)) || !no_dash(s, span(fIF2))) return false;   // '-' in an interface name
+  uint32_t ip1 = 0, ip2 = 0;
+  if (!ipv4_canon(s, span(fIP1), ip1) || !ipv4_canon(s, span(fIP2), ip2)) return false;   // not canonical quads
+  const uint32_t p1 = port_val(s, span(fP1)), p2 = port_val(s, span(fP2));
+  if (p1 > 65535u || p2 > 65535u || !port_canon(s, span(fP2))) return false;   // long ports; TOPORT not canonical
   const uint32_t src = inbound ? ip1 : ip2, dst = inbound ? ip2 : ip1;
   const uint32_t sp = inbound ? p1 : p2, dp = inbound ? p2 : p1;
   // the interface of the ingress side
-  const uint32_t ia = inbound ? v0(fIF1) : v0(fIF2), il = (inbound ? v1(fIF1) : v1(fIF2)) & 0xFFu;
+  const uint32_t ia = inbound ? at(fIF1) : at(fIF2), il = inbound ? len(fIF1) : len(fIF2);
   int32_t found = -1;
   if (il > RSA_IFC_NAME_MAX) return false;
   for (uint32_t k = 0; k < n_ifcs && found < 0; ++k) {
@@ -791,21 +756,19 @@ RSA_HD bool tpl_finish(const S& s, Q slot, const rsa_parse_ifc* ifcs, uint32_t n
   const uint32_t lid = udp ? ifcs[found].list_udp : ifcs[found].list_tcp;
   if (lid == RSA_LIST_HOST) return false;
   // the reducer's fields: FROMIP = the first address, TOIP = the second, TOPORT = P2
-  const uint32_t sev = v0(fSEV), msg = v0(fMSG);
+  const uint32_t sev = s[at(fSEV)] - '0', msg = num(fMSG);
   const bool hit = sev == 6 && (msg == 302013 || msg == 302015);
   uint32_t flags = RSA_F_VALID | RSA_F_BUILT | (hit ? RSA_F_HIT : 0u);
   // outbound: the reducer key is (IP1, IP2, P2) = (dst, src, sport) -- unless its
   // text equals the (src, dst, dport) one, which parse_line's first test takes
-  if (outbound && !(ip1 == ip2 && p1 == p2 && (v1(fP1) & 0xFFu) == (v1(fP2) & 0xFFu) && !(v1(fP1) >> 8)))
-    flags |= RSA_F_SWAP;
+  if (outbound && !(ip1 == ip2 && span_eq(s, span(fP1), span(fP2)))) flags |= RSA_F_SWAP;
   if (hit) {
     // ts_code: HH:MM:SS of the syslog header, the device date's month, day, year
     const char* const months = "JanFebMarAprMayJunJulAugSepOctNovDec";
-    const uint32_t mw = v0(fM2);
     int mo = -1;
     for (int k = 0; k < 12; ++k)
-      if (mw == pack3(months[3 * k], months[3 * k + 1], months[3 * k + 2])) mo = k;
-    const uint32_t y = v0(fY), day = v0(fD2), hh = v0(fHH), mm = v0(fMM), ss = v0(fSS);
+      if (m2 == pack3(months[3 * k], months[3 * k + 1], months[3 * k + 2])) mo = k;
+    const uint32_t y = num(fY), day = num(fD2), hh = num(fHH), mm = num(fMM), ss = num(fSS);
     if (mo < 0 || y < RSA_TS_YEAR0 || y >= RSA_TS_YEAR0 + 128 || day > 31 || hh > 23 || mm > 59 || ss > 59)
       return false;
     ts = ((((y - RSA_TS_YEAR0) * 12u + (uint32_t)mo) * 32u + day) * 86400u) + hh * 3600u + mm * 60u + ss;

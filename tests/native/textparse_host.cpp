@@ -88,6 +88,7 @@ extern "C" void tpl_check_host(const uint8_t* text, const uint64_t* off, uint64_
                                uint32_t n_ifcs, const rsa_parse_spell* spells, uint32_t n_spells, uint8_t* out) {
   using namespace rsa_text;
   uint32_t slot[tpl::kSlotWords];
+  static constexpr tpl::ClsTable kCls = tpl::cls_table();
   for (uint64_t i = 0; i < n; ++i) {
     const uint64_t a = off[i], b = off[i + 1];
     uint64_t len = b - a;
@@ -96,7 +97,8 @@ extern "C" void tpl_check_host(const uint8_t* text, const uint64_t* off, uint64_
     rsa_tuple t1, t2;
     uint32_t ts1 = 0, ts2 = 0, d1 = 0, d2 = 0;
     out[i] = 0;
-    if (!tpl::scan(s, tpl::kProg, slot) || !tpl_finish(s, slot, ifcs, n_ifcs, spells, n_spells, t1, ts1, d1)) continue;
+    if (!tpl::scan(s, tpl::kProg, kCls.t, slot) || !tpl_finish(s, slot, ifcs, n_ifcs, spells, n_spells, t1, ts1, d1))
+      continue;
     parse_line(s, ifcs, n_ifcs, spells, n_spells, t2, ts2, d2);
     const bool same = d1 == d2 && ts1 == ts2 && t1.src == t2.src && t1.dst == t2.dst && t1.sport == t2.sport &&
                       t1.dport == t2.dport && t1.list == t2.list && t1.flags == t2.flags && t1.pspell == t2.pspell;
