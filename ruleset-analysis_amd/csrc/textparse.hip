@@ -180,7 +180,7 @@ __global__ __launch_bounds__(kParseWG) void k_parse(const uint8_t* __restrict__ 
                                                     uint32_t* __restrict__ ts_out, uint32_t* __restrict__ disp,
                                                     uint32_t* __restrict__ slow_idx, unsigned int* __restrict__ slow_n) {
   __shared__ uint32_t sm[kDirect ? 1 : kStageBytes / 4];
-  constexpr bool kScan = !kDirect && !kReduce;   // the template scan (rsa_text::tpl)
+  constexpr bool kScan = !kReduce;   // the template scan (rsa_text::tpl)
   __shared__ uint32_t tprog[kScan ? rsa_text::tpl::kProgLen : 1];
   __shared__ uint8_t tcls[kScan ? 256 : 1];
   __shared__ uint32_t tslot[kScan ? kParseWG * rsa_text::tpl::kSlotWords : 1];
@@ -193,6 +193,7 @@ __global__ __launch_bounds__(kParseWG) void k_parse(const uint8_t* __restrict__ 
   const uint64_t l1 = l0 + kParseWG < n_lines ? l0 + kParseWG : n_lines;
   const uint64_t n_bytes = off[n_lines];
   if (kDirect) {
+    if (kScan) __syncthreads();   // the scan tables (before any lane leaves)
     const uint64_t i = l0 + threadIdx.x;
     if (i >= l1) return;
     const uint64_t a = off[i], b = off[i + 1];
@@ -200,7 +201,22 @@ __global__ __launch_bounds__(kParseWG) void k_parse(const uint8_t* __restrict__ 
     if (len && text[b - 1] == '\n') --len;
     rsa_tuple tup = {0u, 0u, 0, 0, 0, 0, 0};
     uint32_t ts = 0, d = RSA_LINE_HOST;
-    if (len < 0xFFFFFFFFull) {
+    if (kScan) {
+      d = rsa_text::kLineDefer;
+      if (len < 0xFFFFu) {
+        const uint64_t nw = n_bytes >> 2;
+        uint32_t tail = 0;
+        for (uint32_t k = 0; k < (uint32_t)(n_bytes & 3u); ++k) tail |= (uint32_t)text[4 * nw + k] << (8 * k);
+        const rsa_text::GWordU s{reinterpret_cast<const uint32_t*>(text), a, nw, tail, (uint32_t)len};
+        uint32_t* slot = tslot + threadIdx.x * rsa_text::tpl::kSlotWords;
+        if (!(rsa_text::tpl::scan(s, tprog, tcls, slot) &&
+              rsa_text::tpl_finish(s, slot, ifcs, n_ifcs, spells, n_spells, tup, ts, d))) {
+          tup = rsa_tuple{0u, 0u, 0, 0, 0, 0, 0};
+          ts = 0;
+          d = rsa_text::kLineDefer;
+        }
+      }
+    } else if (len < 0xFFFFFFFFull) {
       const rsa_text::GWordLn s{reinterpret_cast<const uint32_t*>(text), text, a, n_bytes, (uint32_t)len, ~0ull, 0u};
       if (kReduce) {
         rsa_text::reduce_line<true>(s, spells, n_spells, tup, ts, d);

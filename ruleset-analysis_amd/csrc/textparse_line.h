@@ -59,6 +59,19 @@ struct GWordLn {             // global 4-byte loads with a one-word cache (no st
   }
 };
 
+struct GWordU {              // global 4-byte loads, one per byte read, no per-lane branch: the word of
+  const uint32_t* w32;       // the buffer's last, partial bytes comes from `tail`
+  uint64_t o;                // byte offset of the line
+  uint64_t nw;               // whole words in the buffer
+  uint32_t tail;             // the partial last word (zero padded)
+  uint32_t n;
+  RSA_HD uint32_t operator[](uint32_t i) const {
+    const uint64_t pos = o + i, wi = pos >> 2;
+    const uint32_t w = wi < nw ? w32[wi] : tail;
+    return (w >> ((uint32_t)(pos & 3u) * 8u)) & 0xFFu;
+  }
+};
+
 RSA_HD bool is_dig(uint32_t c) { return c - '0' < 10u; }
 RSA_HD bool is_upper(uint32_t c) { return c - 'A' < 26u; }
 RSA_HD bool is_lower(uint32_t c) { return c - 'a' < 26u; }
