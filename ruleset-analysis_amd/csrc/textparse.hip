@@ -180,7 +180,10 @@ __global__ __launch_bounds__(kParseWG) void k_parse(const uint8_t* __restrict__ 
                                                     uint32_t* __restrict__ ts_out, uint32_t* __restrict__ disp,
                                                     uint32_t* __restrict__ slow_idx, unsigned int* __restrict__ slow_n) {
   __shared__ uint32_t sm[kDirect ? 1 : kStageBytes / 4];
-  constexpr bool kScan = !kReduce;   // the template scan (rsa_text::tpl)
+  // the template scan (rsa_text::tpl) over the staged lines; the direct mode
+  // keeps the per-lane template path (the scan's byte-per-step HBM loads were
+  // 2.3x slower there: profiles/r03y_text_parse_modes.txt)
+  constexpr bool kScan = !kReduce && !kDirect;
   __shared__ uint32_t tprog[kScan ? rsa_text::tpl::kProgLen : 1];
   __shared__ uint8_t tcls[kScan ? 256 : 1];
   __shared__ uint32_t tslot[kScan ? kParseWG * rsa_text::tpl::kSlotWords : 1];
