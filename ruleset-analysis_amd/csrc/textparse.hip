@@ -150,7 +150,9 @@ __global__ void k_set_u64(uint64_t* p, uint64_t v) { *p = v; }
 // coalesced 4-byte loads, then every lane parses its line from LDS through
 // the word-cached accessor (one LDS read per 4 bytes scanned).  A workgroup
 // whose lines do not fit parses straight from HBM with byte loads.
-constexpr uint32_t kParseWG = 128, kStageBytes = 32768;
+// 28 KB of staged text + the scan's slots and tables: four workgroups per CU
+// (a workgroup whose lines average more than 224 B defers them to the slow pass)
+constexpr uint32_t kParseWG = 128, kStageBytes = 28672;
 
 // A line the template pass defers (rsa_text::kLineDefer): its index is
 // appended to the slow list (one device atomic per wave).
