@@ -474,21 +474,29 @@ __global__ void k_skip(const uint8_t* __restrict__ text, const uint64_t* __restr
                        const uint32_t* __restrict__ lens, uint64_t n_bytes, const Act* __restrict__ act, uint32_t m,
                        uint32_t round, unsigned int* __restrict__ next_round) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= m) return;
-  const Act x = act[j];
-  const uint32_t L = lens[x.id];
-  uint32_t best = L == 0 ? 0u : (L + 6) / 7 - 1;   // the window holding the line's last byte
-  if (j > 0 && act[j - 1].gs == x.gs) {
-    const Act y = act[j - 1];
-    const uint32_t Ly = lens[y.id];
-    const uint64_t ax = off[x.id], ay = off[y.id];
-    for (uint32_t r = round; r < best; ++r)
-      if (chunk_key(text, n_bytes, ax, L, r) != chunk_key(text, n_bytes, ay, Ly, r)) {
-        best = r;
-        break;
-      }
+  uint32_t best = 0xFFFFFFFFu;
+  if (j < m) {
+    const Act x = act[j];
+    const uint32_t L = lens[x.id];
+    best = L == 0 ? 0u : (L + 6) / 7 - 1;   // the window holding the line's last byte
+    if (j > 0 && act[j - 1].gs == x.gs) {
+      const Act y = act[j - 1];
+      const uint32_t Ly = lens[y.id];
+      const uint64_t ax = off[x.id], ay = off[y.id];
+      for (uint32_t r = round; r < best; ++r)
+        if (chunk_key(text, n_bytes, ax, L, r) != chunk_key(text, n_bytes, ay, Ly, r)) {
+          best = r;
+          break;
+        }
+    }
+    best = best > round ? best : round;
   }
-  atomicMin(next_round, best > round ? best : round);
+  // the wave's minimum, one device atomic per wave
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t t = (uint32_t)__shfl_xor((int)best, o);
+    best = t < best ? t : best;
+  }
+  if (__lane_id() == 0 && best != 0xFFFFFFFFu) atomicMin(next_round, best);
 }
 
 __global__ void k_gs_iota(const uint64_t* __restrict__ vals, uint32_t m, uint32_t* __restrict__ gs,
