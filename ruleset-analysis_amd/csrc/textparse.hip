@@ -463,42 +463,6 @@ __global__ void k_round_live(const uint64_t* __restrict__ keys, const Act* __res
   if (ended || split) *live = 1u;
 }
 
-// After a dead round: the next round that can change anything, for all the
-// unsettled lines at once.  A round is live when a line ends in its window or
-// two neighbours of one group (groups are contiguous in `act`) differ there;
-// each line reports the first such round from `round` on (its own end, or its
-// first window that differs from its predecessor's), and the rounds before
-// the minimum are skipped without keys, checks or host reads (lines of one
-// second share ~80 bytes: eight dead rounds in a row).
-__global__ void k_skip(const uint8_t* __restrict__ text, const uint64_t* __restrict__ off,
-                       const uint32_t* __restrict__ lens, uint64_t n_bytes, const Act* __restrict__ act, uint32_t m,
-                       uint32_t round, unsigned int* __restrict__ next_round) {
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t best = 0xFFFFFFFFu;
-  if (j < m) {
-    const Act x = act[j];
-    const uint32_t L = lens[x.id];
-    best = L == 0 ? 0u : (L + 6) / 7 - 1;   // the window holding the line's last byte
-    if (j > 0 && act[j - 1].gs == x.gs) {
-      const Act y = act[j - 1];
-      const uint32_t Ly = lens[y.id];
-      const uint64_t ax = off[x.id], ay = off[y.id];
-      for (uint32_t r = round; r < best; ++r)
-        if (chunk_key(text, n_bytes, ax, L, r) != chunk_key(text, n_bytes, ay, Ly, r)) {
-          best = r;
-          break;
-        }
-    }
-    best = best > round ? best : round;
-  }
-  // the wave's minimum, one device atomic per wave
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint32_t t = (uint32_t)__shfl_xor((int)best, o);
-    best = t < best ? t : best;
-  }
-  if (__lane_id() == 0 && best != 0xFFFFFFFFu) atomicMin(next_round, best);
-}
-
 __global__ void k_gs_iota(const uint64_t* __restrict__ vals, uint32_t m, uint32_t* __restrict__ gs,
                           uint32_t* __restrict__ idx) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -826,17 +790,7 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
     uint32_t h_live = 0;
     TPCHK(c, hipMemcpyAsync(&h_live, live, 4, hipMemcpyDeviceToHost, st));
     TPCHK(c, hipStreamSynchronize(st));
-    if (!h_live) {
-      // jump over the following dead rounds too
-      TPCHK(c, hipMemsetAsync(live, 0xFF, 4, st));
-      hipLaunchKernelGGL(k_skip, dim3(blocks(m, 256)), dim3(256), 0, st, d_text, d_off, lens, n_bytes, act, m,
-                         round + 1, live);
-      uint32_t nxt = 0;
-      TPCHK(c, hipMemcpyAsync(&nxt, live, 4, hipMemcpyDeviceToHost, st));
-      TPCHK(c, hipStreamSynchronize(st));
-      if (nxt > round + 1) round = nxt - 1;   // (the loop's ++ lands on nxt)
-      continue;
-    }
+    if (!h_live) continue;
     tt = tmp;   // stable LSD: by the chunk key, then by the group start
     TPCHK(c, rocprim::radix_sort_pairs(t, tt, keysA, keysB, valsA, valsB, (size_t)m, 0, 64, st));
     hipLaunchKernelGGL(k_gs_iota, dim3(blocks(m, 256)), dim3(256), 0, st, valsB, m, gs, ids);
