@@ -53,3 +53,19 @@ def test_no_signed_mul24_shifts():
         with open(os.path.join(ROOT, 'ruleset-analysis_amd', 'csrc', name)) as f:
             calls = [l for l in f if '__umul24(' in l and 'uint32_t umul24(' not in l and not l.lstrip().startswith('//')]
         assert calls == [], (name, calls)
+
+
+def test_header_constants_equal_binding():
+    """Every RSA_OPT_* / RSA_ERR_* / RSA_LINE_* / RSA_F_* / RSA_RED_* value the
+    binding names equals the header's #define (the options are plain ints on
+    the ctypes side)."""
+    with open(os.path.join(ROOT, 'include', 'ruleset_hip.h')) as f:
+        text = f.read()
+    defs = {m.group(1): int(m.group(2), 0) for m in
+            re.finditer(r'^#define\s+(RSA_(?:OPT|ERR|LINE|F|RED)_[A-Z0-9_]+)\s+\(?(-?(?:0x)?[0-9A-Fa-f]+)u?\)?', text,
+                        re.M)}
+    bound = {k: getattr(native, k) for k in dir(native) if k in defs}
+    assert len(bound) >= 20
+    for k, v in bound.items():
+        assert v == defs[k], k
+    assert {'RSA_OPT_COUNT_SORT', 'RSA_OPT_OWNER_WORLD', 'RSA_OPT_OWNER_RANK'} <= set(bound)
