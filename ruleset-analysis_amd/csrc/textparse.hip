@@ -456,28 +456,13 @@ __global__ void k_keys(const uint8_t* __restrict__ text, const uint64_t* __restr
 
 // 1 if this round can change anything: a group whose keys differ, or a line
 // that ends in this window (else the round is skipped: no sort, no settle)
-// live[1..2]: the OR over all keys of (key ^ keys[0]) -- the bits that vary
-// this round; the sort then runs over those bits only (a round of lines of one
-// second varies in ~20 of the 64 key bits: 3 radix passes instead of 8)
 __global__ void k_round_live(const uint64_t* __restrict__ keys, const Act* __restrict__ act, uint32_t m,
                              uint32_t* __restrict__ live) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  uint64_t d = 0;
-  if (j < m) {
-    const bool ended = (keys[j] & 0xFFu) < 8u;
-    const bool split = j > 0 && act[j].gs == act[j - 1].gs && keys[j] != keys[j - 1];
-    if (ended || split) live[0] = 1u;
-    d = keys[j] ^ keys[0];
-  }
-  uint32_t lo = (uint32_t)d, hi = (uint32_t)(d >> 32);
-  for (int o = 32; o > 0; o >>= 1) {
-    lo |= (uint32_t)__shfl_xor((int)lo, o);
-    hi |= (uint32_t)__shfl_xor((int)hi, o);
-  }
-  if (__lane_id() == 0) {
-    if (lo) atomicOr(&live[1], lo);
-    if (hi) atomicOr(&live[2], hi);
-  }
+  if (j >= m) return;
+  const bool ended = (keys[j] & 0xFFu) < 8u;
+  const bool split = j > 0 && act[j].gs == act[j - 1].gs && keys[j] != keys[j - 1];
+  if (ended || split) *live = 1u;
 }
 
 __global__ void k_gs_iota(const uint64_t* __restrict__ vals, uint32_t m, uint32_t* __restrict__ gs,
@@ -803,24 +788,20 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
   TPCHK(c, hipMemcpyAsync(&lastk, keep + n - 1, 4, hipMemcpyDeviceToHost, st));
   TPCHK(c, hipStreamSynchronize(st));
   m += lastk;
-  uint32_t* live = reinterpret_cast<uint32_t*>(act2);   // act2 is spare: the live flag + the varying key bits
+  uint32_t* live = reinterpret_cast<uint32_t*>(act2);   // act2 is spare: one flag word
   for (uint32_t round = round0; m > 0; ++round) {
     hipLaunchKernelGGL(k_keys, dim3(blocks(m, 256)), dim3(256), 0, st, d_text, act_a, act_l, n_bytes, act, m, round,
                        keysA, valsA);
     // rounds inside a shared prefix (e.g. lines of one second share ~90 bytes)
     // change nothing: detect them with one pass and skip the sorts
-    TPCHK(c, hipMemsetAsync(live, 0, 12, st));
+    TPCHK(c, hipMemsetAsync(live, 0, 4, st));
     hipLaunchKernelGGL(k_round_live, dim3(blocks(m, 256)), dim3(256), 0, st, keysA, act, m, live);
-    uint32_t h_live[3] = {0, 0, 0};
-    TPCHK(c, hipMemcpyAsync(h_live, live, 12, hipMemcpyDeviceToHost, st));
+    uint32_t h_live = 0;
+    TPCHK(c, hipMemcpyAsync(&h_live, live, 4, hipMemcpyDeviceToHost, st));
     TPCHK(c, hipStreamSynchronize(st));
-    if (!h_live[0]) continue;
-    // the key bits that vary this round (the others are equal in every key)
-    const uint64_t vary = (uint64_t)h_live[2] << 32 | h_live[1];
-    const unsigned b0 = vary ? (unsigned)__builtin_ctzll(vary) : 0u;
-    const unsigned b1 = vary ? 64u - (unsigned)__builtin_clzll(vary) : 8u;
+    if (!h_live) continue;
     tt = tmp;   // stable LSD: by the chunk key, then by the group start
-    TPCHK(c, rocprim::radix_sort_pairs(t, tt, keysA, keysB, valsA, valsB, (size_t)m, b0, b1, st));
+    TPCHK(c, rocprim::radix_sort_pairs(t, tt, keysA, keysB, valsA, valsB, (size_t)m, 0, 64, st));
     hipLaunchKernelGGL(k_gs_iota, dim3(blocks(m, 256)), dim3(256), 0, st, valsB, m, gs, ids);
     tt = tmp;   // by group start (only the bits a position can have), carrying the index
     TPCHK(c, rocprim::radix_sort_pairs(t, tt, gs, first, ids, pos, (size_t)m, 0, gbits, st));
