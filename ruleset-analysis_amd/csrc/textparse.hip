@@ -442,15 +442,13 @@ struct Act {               // an unsettled line: its id and the position its gro
   uint32_t id, gs;
 };
 
-// (act_a / act_l: the unsettled lines' offsets and lengths beside `act`, so
-// that a round reads them coalesced instead of gathering off[] / lens[])
-__global__ void k_keys(const uint8_t* __restrict__ text, const uint64_t* __restrict__ act_a,
-                       const uint32_t* __restrict__ act_l, uint64_t n_bytes, const Act* __restrict__ act, uint32_t m,
+__global__ void k_keys(const uint8_t* __restrict__ text, const uint64_t* __restrict__ off,
+                       const uint32_t* __restrict__ lens, uint64_t n_bytes, const Act* __restrict__ act, uint32_t m,
                        uint32_t round, uint64_t* __restrict__ keys, uint64_t* __restrict__ vals) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= m) return;
   const Act x = act[j];
-  keys[j] = chunk_key(text, n_bytes, act_a[j], act_l[j], round);
+  keys[j] = chunk_key(text, n_bytes, off[x.id], lens[x.id], round);
   vals[j] = (uint64_t)x.gs << 32 | x.id;
 }
 
@@ -524,14 +522,10 @@ __global__ void k_settle(const uint64_t* __restrict__ keys, const uint32_t* __re
 
 __global__ void k_compact(const uint32_t* __restrict__ ids, const uint32_t* __restrict__ ngs1,
                           const uint32_t* __restrict__ keep, const uint32_t* __restrict__ slot, uint32_t m,
-                          const uint64_t* __restrict__ off, const uint32_t* __restrict__ lens, Act* __restrict__ out,
-                          uint64_t* __restrict__ out_a, uint32_t* __restrict__ out_l) {
+                          Act* __restrict__ out) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= m || !keep[j]) return;
-  const uint32_t id = ids[j], at = slot[j];
-  out[at] = Act{id, ngs1[j] - 1};
-  out_a[at] = off[id];
-  out_l[at] = lens[id];
+  out[slot[j]] = Act{ids[j], ngs1[j] - 1};
 }
 
 inline uint32_t blocks(uint64_t n, uint32_t t) { return (uint32_t)((n + t - 1) / t); }
@@ -723,7 +717,7 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
   tmp = (tmp + 255) / 256 * 256;
   const size_t N = ((size_t)n + 63) / 64 * 64;
   // keysA/keysB u64, valsA/valsB u64, gs/ids/first/pos/bstart/keep/slot u32, act/act2 Act, count
-  const size_t bytes = tmp + N * (8 * 4 + 4 * 8 + 8 * 2 + 12) + 256;
+  const size_t bytes = tmp + N * (8 * 4 + 4 * 8 + 8 * 2) + 256;
   Scratch S{c, st};
   TPCHK(c, hipMallocAsync(&S.base, bytes, st));
   char* p = static_cast<char*>(S.base);
@@ -743,8 +737,6 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
   Act* act = reinterpret_cast<Act*>(p); p += N * 8;
   Act* act2 = reinterpret_cast<Act*>(p); p += N * 8;
   uint32_t* lens = reinterpret_cast<uint32_t*>(p); p += N * 4;
-  uint64_t* act_a = reinterpret_cast<uint64_t*>(p); p += N * 8;   // offsets / lengths beside act
-  uint32_t* act_l = reinterpret_cast<uint32_t*>(p); p += N * 4;
   uint32_t* idsA = reinterpret_cast<uint32_t*>(valsA);   // round 0 reuses the value arrays as u32 ids
   uint32_t* idsB = reinterpret_cast<uint32_t*>(valsB);
 
@@ -781,8 +773,7 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
   }
   tt = tmp;
   TPCHK(c, rocprim::exclusive_scan(t, tt, keep, slot, 0u, (size_t)n, rocprim::plus<uint32_t>(), st));
-  hipLaunchKernelGGL(k_compact, dim3(blocks(n, 256)), dim3(256), 0, st, idsB, first, keep, slot, n, d_off, lens, act,
-                     act_a, act_l);
+  hipLaunchKernelGGL(k_compact, dim3(blocks(n, 256)), dim3(256), 0, st, idsB, first, keep, slot, n, act);
   uint32_t m = 0, lastk = 0;
   TPCHK(c, hipMemcpyAsync(&m, slot + n - 1, 4, hipMemcpyDeviceToHost, st));
   TPCHK(c, hipMemcpyAsync(&lastk, keep + n - 1, 4, hipMemcpyDeviceToHost, st));
@@ -790,7 +781,7 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
   m += lastk;
   uint32_t* live = reinterpret_cast<uint32_t*>(act2);   // act2 is spare: one flag word
   for (uint32_t round = round0; m > 0; ++round) {
-    hipLaunchKernelGGL(k_keys, dim3(blocks(m, 256)), dim3(256), 0, st, d_text, act_a, act_l, n_bytes, act, m, round,
+    hipLaunchKernelGGL(k_keys, dim3(blocks(m, 256)), dim3(256), 0, st, d_text, d_off, lens, n_bytes, act, m, round,
                        keysA, valsA);
     // rounds inside a shared prefix (e.g. lines of one second share ~90 bytes)
     // change nothing: detect them with one pass and skip the sorts
@@ -818,8 +809,7 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
     // slot (new group start + 1) is still needed by k_compact: scan the keep flags into `first`
     tt = tmp;
     TPCHK(c, rocprim::exclusive_scan(t, tt, keep, first, 0u, (size_t)m, rocprim::plus<uint32_t>(), st));
-    hipLaunchKernelGGL(k_compact, dim3(blocks(m, 256)), dim3(256), 0, st, ids, slot, keep, first, m, d_off, lens, act,
-                       act_a, act_l);
+    hipLaunchKernelGGL(k_compact, dim3(blocks(m, 256)), dim3(256), 0, st, ids, slot, keep, first, m, act);
     uint32_t nm = 0;
     TPCHK(c, hipMemcpyAsync(&nm, first + m - 1, 4, hipMemcpyDeviceToHost, st));
     TPCHK(c, hipMemcpyAsync(&lastk, keep + m - 1, 4, hipMemcpyDeviceToHost, st));
