@@ -28,24 +28,35 @@ def main(argv=None):
     acls, fws = _db(db_path)
     stdin = io.TextIOWrapper(sys.stdin.buffer, encoding='latin-1', newline='\n')
     stdout = io.TextIOWrapper(sys.stdout.buffer, encoding='latin-1', newline='\n', write_through=False)
+    # a Python 2 script that dies still flushes what it printed: the partial
+    # output is written before the exception propagates (exit status 1)
     if mode == 'map':
-        from .mapper import map_lines
+        from .mapper import HostMissing, map_lines
         host = os.environ['mapred_input_dir'].split('/')[-2]
         out = []
         chunk = []
-        for line in stdin:
-            chunk.append(line)
-            if len(chunk) >= 65536:
-                map_lines(chunk, host, acls, fws, out)
-                stdout.write(''.join(out))
-                out, chunk = [], []
-        map_lines(chunk, host, acls, fws, out)
-        stdout.write(''.join(out))
+        try:
+            for line in stdin:
+                chunk.append(line)
+                if len(chunk) >= 65536:
+                    map_lines(chunk, host, acls, fws, out)
+                    stdout.write(''.join(out))
+                    out, chunk = [], []
+            map_lines(chunk, host, acls, fws, out)
+        except HostMissing:
+            sys.exit(1)                                   # mapper.py:115-117 (the message is in out)
+        finally:
+            stdout.write(''.join(out))
+            stdout.flush()
     elif mode == 'reduce':
         from .reducer import reduce_lines
         cap = int(argv[2]) if len(argv) > 2 else 1000
-        lines, _blocks = reduce_lines(stdin, acls, cap)
-        stdout.write(''.join(l + '\n' for l in lines))
+        lines = []
+        try:
+            reduce_lines(stdin, acls, cap, out=lines)
+        finally:
+            stdout.write(''.join(l + '\n' for l in lines))
+            stdout.flush()
     else:
         raise SystemExit('usage: python -m oracle.cli map|reduce DB.json [CAP]')
     stdout.flush()

@@ -39,7 +39,10 @@ class FirewallRule(object):
             sport = [self.NO_PORT]
         if not dport:
             dport = [self.NO_PORT]
-        if any(not isinstance(p, int) for p in sport) or any(not isinstance(p, int) for p in dport):
+        # Python 2: int() of a literal past sys.maxint (2^63 - 1) is a long, which
+        # isinstance(p, int) rejects (firewallrule.py:67-75)
+        py2int = lambda p: isinstance(p, int) and -(1 << 63) <= p < (1 << 63)
+        if any(not py2int(p) for p in sport) or any(not py2int(p) for p in dport):
             raise ValueError('Source port must be an integer or -1 for "No port"')
         self.src = self._addr(src, 'src')
         self.dst = self._addr(dst, 'dst')

@@ -16,8 +16,11 @@
 
 Error behaviour follows the reference: the same exception classes at the same
 validation points (``KeyError`` for a missing ``'in'`` binding or protocol
-list, ``ValueError`` for malformed addresses), config/DB problems reported on
-stderr with exit status 1.
+list, ``ValueError`` for malformed addresses or ports past a 64-bit int),
+config/DB problems reported on stderr with exit status 1.  The mapper never
+validates the month (``mapper.py:127-131``); the fused job dies where
+``mapper | sort | reducer`` would under ``set -o pipefail``, after printing
+what the reducer printed (``pipeline.finish_job``).
 """
 
 import os
@@ -97,6 +100,7 @@ def mapper_main(argv=None):
         else:
             carry = b''
         parsed = parse_text(eng, hostname, data, db, compiled, need_order=False)
+        eng.refresh_compiled(compiled)     # lists derived for ports past 65535 (compile.list_id_oor)
         gids = eng.classify_only(parsed.batch()).cpu().numpy() if parsed.n else np.zeros(0, np.int32)
         _write(mapper_output(parsed, gids, compiled))
         sys.stdout.flush()
@@ -187,7 +191,16 @@ def run_main(argv=None):
                 sys.stderr.write('INFO - ' + m + '\n')
     if not inputs:
         return 0
-    out, _res = analyze_text(inputs, db, cap=args.cap, engine=engine)
+    try:
+        out, _res = analyze_text(inputs, db, cap=args.cap, engine=engine)
+    except BaseException as exc:
+        # the pipeline died (pipeline.finish_job): the reducer's stdout up to
+        # there, then the exception; a failed Hadoop job stores no output
+        part = getattr(exc, 'rsa_report', None)
+        if part is not None and not (args.postprocess or args.hadoop_output):
+            _write(''.join(l + '\n' for l in part))
+            sys.stdout.flush()
+        raise
     if args.postprocess or args.hadoop_output:
         from .postprocess import hadoop_output, postprocess
         k = out.index('') if '' in out else len(out)   # the noise records of the empty mapper records

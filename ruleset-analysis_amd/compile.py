@@ -53,6 +53,14 @@ def _port_ranges(ports):
     return [tuple(r) for r in out]
 
 
+def _oor_side(ports, value):
+    """A rule side against a connection port past 65535: None ('no check') if
+    the side is NO_PORT or names the value, else [] (never matches)."""
+    if ports == [FirewallRule.NO_PORT] or value in ports:
+        return None
+    return []
+
+
 def _addr_range(ip):
     """(lo, span) for an IPv4 network, None for IPv6 (never contains an IPv4 tuple)."""
     if ip._ipversion != 4:
@@ -196,6 +204,47 @@ class CompiledRules(object):
         rows = self._lower(entry['rules'], idxs, proto, self.base[(host, acl)])
         if self.run_min:
             rows = compress_runs(rows, self.run_min)
+        return self._add_list(k, rows)
+
+    def list_id_oor(self, host, acl, proto, sport=None, dport=None):
+        """Candidate list of a connection whose source and/or destination port
+        is past 65535: the mapper builds the ``Connection`` from ``int()`` of
+        the log's digits with no range check (``mapper.py:139``,
+        ``firewallrule.py:47-53``), and a rule side with ports contains it only
+        if that value is in its list (``:162-171``) while a NO_PORT side always
+        does.  ``sport``/``dport``: the out-of-range values (None for a side in
+        range).  The derived list keeps the entries whose out-of-range sides
+        can match, widened to any port there; the line's tuple carries port 0
+        on such a side.  Values no rule of the list names share one list."""
+        if sport is None and dport is None:
+            return self.list_id(host, acl, proto)
+        entry = self.db.accesslists[host][acl]
+        idxs = candidate_indices(entry['protocols'], proto)        # mapper.py:159-166 KeyError first
+        named = self._named_oor(host, acl)
+        fold = lambda v: None if v is None else (v if v in named else -2)
+        k = (host, acl, proto, fold(sport), fold(dport))
+        lid = self.list_ids.get(k)
+        if lid is not None:
+            return lid
+        rows = self._lower(entry['rules'], idxs, proto, self.base[(host, acl)], oor=(sport, dport))
+        if self.run_min:
+            rows = compress_runs(rows, self.run_min)
+        return self._add_list(k, rows)
+
+    def _named_oor(self, host, acl):
+        """Port values past 65535 that rules of (host, acl) name."""
+        cache = self.__dict__.setdefault('_oor_named', {})
+        got = cache.get((host, acl))
+        if got is None:
+            rules = self.db.accesslists[host][acl]['rules']
+            if hasattr(rules, 'sport') and hasattr(rules, 'lower'):
+                got = {int(v) for col in (rules.sport, rules.dport) for v in np.unique(col) if v > 65535}
+            else:
+                got = {int(p) for r in rules for p in list(r.sport) + list(r.dport) if p > 65535}
+            cache[(host, acl)] = got
+        return got
+
+    def _add_list(self, k, rows):
         if len(self._lists) >= MAX_LISTS:
             raise OverflowError('more than %d (host, acl, protocol) candidate lists' % MAX_LISTS)
         lid = len(self._lists)
@@ -206,10 +255,10 @@ class CompiledRules(object):
         return lid
 
     @staticmethod
-    def _lower(rules, idxs, proto, base):
+    def _lower(rules, idxs, proto, base, oor=(None, None)):
         lower_cols = getattr(rules, 'lower', None)
         if lower_cols is not None:          # columnar rule store (rulecols.RuleColumns)
-            return lower_cols(idxs, proto, base)
+            return lower_cols(idxs, proto, base, oor=oor)
         rows = []
         seen = set()
         for i in idxs:
@@ -226,8 +275,8 @@ class CompiledRules(object):
             d = _addr_range(rule.dst)
             if s is None or d is None:
                 continue
-            sps = _port_ranges(rule.sport)
-            dps = _port_ranges(rule.dport)
+            sps = _port_ranges(rule.sport) if oor[0] is None else _oor_side(rule.sport, oor[0])
+            dps = _port_ranges(rule.dport) if oor[1] is None else _oor_side(rule.dport, oor[1])
             if sps == [] or dps == []:
                 continue
             for slo, shi in (sps or [(0, 65535)]):

@@ -135,17 +135,30 @@ class Engine(object):
         are scanned linearly, records hold at most ``chunk`` entries each,
         chained)."""
         import os
-        ent, off = compiled.packed()
+        packed = compiled.packed()
+        ent, off = packed
         self.load_rules(ent, off, compiled.n_rules)
         if index:
             kind = kind or os.environ.get('RSA_INDEX', 'auto')
             self.load_index(compiled.index(prefix=prefix, chunk=chunk, kind=kind))
+        self._loaded = (compiled, packed, index, prefix, chunk, kind)
+
+    def refresh_compiled(self, compiled):
+        """Re-upload ``compiled`` if lists were added since load_compiled (the
+        host parse derives lists for lines with ports past 65535,
+        CompiledRules.list_id_oor); a no-op otherwise."""
+        held = getattr(self, '_loaded', None)
+        if held is None or held[0] is not compiled:
+            self.load_compiled(compiled)
+        elif held[1] is not compiled.packed():
+            self.load_compiled(compiled, *held[2:])
 
     def set_rule_count(self, n_rules):
         """Rule count of jobs over given gids (rsa_aggregate_gids: the reducer
         drop-in's runs, the merge owners): any loaded candidate lists are
         replaced by none, so the count may change between jobs."""
         self.load_rules(np.zeros(0, RULE_DTYPE), np.zeros(1, np.uint32), n_rules)
+        self._loaded = None
 
     def _bind(self, n_rules):
         torch = self.torch

@@ -10,7 +10,7 @@ rule to the integer predicate they evaluate.
 """
 
 from .ipaddr import IP
-from .py2text import py2_int
+from .py2text import py2_int, py2_is_int
 
 __all__ = ['FirewallRule']
 
@@ -26,7 +26,7 @@ def _as_port_list(value, what):
     if not value:
         value = [FirewallRule.NO_PORT]
     for p in value:
-        if not isinstance(p, int):
+        if not py2_is_int(p):              # a Python 2 long (|p| > sys.maxint) is not an int either
             raise ValueError('%s port must be an integer or -1 for "No port"' % what)
     return value
 

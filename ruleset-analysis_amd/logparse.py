@@ -27,8 +27,8 @@ import numpy as np
 from .compile import TUPLE_DTYPE, F_VALID, F_HIT, F_BUILT, F_SWAP
 from .firewallrule import FirewallRule
 from .ipaddr import IP
-from .py2text import PY2_WS, py2_int
-from .keytext import INTERNED, KeyText
+from .py2text import PY2_WS, py2_int, py2_is_int
+from .keytext import INTERNED, MAX_SPELL_ID, KeyText
 
 __all__ = ['ParsedLog', 'parse_logs', 'get_builtconn', 'BUILT', 'PY2_WS', 'reducer_fields',
            'D_IGNORE', 'D_NOACL', 'D_MISSING', 'D_CLASSIFY']
@@ -108,8 +108,9 @@ class ParsedLog(object):
         self.pspell_table = []
         self.error = None          # (line index, exception) — the mapper dies there
         self.n = 0
-        self.keytext = None        # report.KeyText of the interned (non-canonical) reducer keys
-        self.keyx = {}             # line index -> (pspell | INTERNED, from id, to id, port id)
+        self.keytext = None        # keytext.KeyText of the interned (non-canonical) reducer keys
+        self.keyx = {}             # line index -> KeyText id of its interned reducer key
+        self.bad_month = {}        # line index -> the ValueError months.index raises for its hit, BUILT line
 
 
 def parse_logs(inputs, db, compiled, pspell_table=None, need_order=True, keytext=None):
@@ -118,7 +119,12 @@ def parse_logs(inputs, db, compiled, pspell_table=None, need_order=True, keytext
 
     Stops at the first line where the reference mapper would raise; the
     exception and line index are kept in ``.error`` and everything before it is
-    parsed (the drop-in mapper prints that prefix and then re-raises)."""
+    parsed (the drop-in mapper prints that prefix and then re-raises).  A hit,
+    BUILT line whose month ``months.index`` rejects is NOT an error here: the
+    mapper never looks at the month (``mapper.py:127-131``) and the reducer
+    only for a line it still inserts (``connlist-reducer.py:151-164``); such
+    lines are kept in ``.bad_month`` (flag F_BUILT cleared: a hit, never a
+    record) for the job to decide after aggregation."""
     P = ParsedLog()
     P.keytext = keytext if keytext is not None else KeyText()
     pspell = {} if pspell_table is None else {s: i for i, s in enumerate(pspell_table)}
@@ -178,6 +184,8 @@ def _parse_one(line, host, fw, acls, compiled, pspell, P, i):
     proto = d['protocol'].lower()
     # Connection(...) -> FirewallRule.__init__ validation (firewallrule.py:47-93)
     sport, dport = py2_int(d['sport']), py2_int(d['dport'])
+    if not py2_is_int(sport) or not py2_is_int(dport):         # a Python 2 long (firewallrule.py:67-75)
+        raise ValueError('Source port must be an integer or -1 for "No port"')
     src_ip = FirewallRule._address(d['src'], 'src')
     dst_ip = FirewallRule._address(d['dst'], 'dst')
     ifc = d['interface_in']
@@ -191,7 +199,11 @@ def _parse_one(line, host, fw, acls, compiled, pspell, P, i):
     if src_ip._ipversion != 4 or dst_ip._ipversion != 4 or src_ip._prefixlen != 32 or dst_ip._prefixlen != 32:
         raise NotImplementedError('only IPv4 host addresses are supported in connection tuples: %r' % line)
     if sport > 65535 or dport > 65535:
-        raise NotImplementedError('port out of 16-bit range in %r' % line)
+        # int() of the log's digits is never range-checked: such a side matches
+        # only rule sides that are NO_PORT or name the value (compile.list_id_oor)
+        lid = compiled.list_id_oor(host, acl, proto, sport if sport > 65535 else None,
+                                   dport if dport > 65535 else None)
+        sport, dport = sport if sport <= 65535 else 0, dport if dport <= 65535 else 0
     flags = F_VALID
     stripped = line.strip(PY2_WS)
     hit, res = reducer_fields(stripped)
@@ -203,13 +215,16 @@ def _parse_one(line, host, fw, acls, compiled, pspell, P, i):
         flags |= F_BUILT
         for_ip, to_ip, to_port = res[6], res[8], res[9]
         if hit:
-            ts = reducer_timestamp(res)
+            try:
+                ts = reducer_timestamp(res)
+            except ValueError as exc:
+                # months.index fails: decided after aggregation (parse_logs)
+                P.bad_month[i] = exc
+                return (src_ip.ip, dst_ip.ip, sport, dport, lid, flags & ~F_BUILT, 0), D_CLASSIFY, None
         word = res[5]
-        if word not in pspell:
-            if len(pspell) >= INTERNED:
-                raise NotImplementedError('more than %d protocol spellings' % INTERNED)
+        if word not in pspell and len(pspell) < MAX_SPELL_ID:
             pspell[word] = len(pspell)
-        ps = pspell[word]
+        ps = pspell.get(word)
         # the reducer keys its dict by the strings (connlist-reducer.py:167):
         # canonical text that names the tuple's own fields is carried as the
         # tuple's values, anything else as interned text
@@ -219,38 +234,35 @@ def _parse_one(line, host, fw, acls, compiled, pspell, P, i):
             flags |= F_SWAP
         else:
             for_ip = None
-        if for_ip is None or not _canonical_key(for_ip, to_ip, to_port):
-            kt = P.keytext
-            P.keyx[i] = (ps | INTERNED, kt(res[6]), kt(res[8]), kt(res[9]))
-            if len(kt.values) > 0xFFFF:
-                raise NotImplementedError('more than 65536 distinct non-canonical key strings')
+        if ps is None or for_ip is None or not _canonical_key(for_ip, to_ip, to_port):
+            P.keyx[i] = P.keytext((word, res[6], res[8], res[9]))
+            ps = 0
     return (src_ip.ip, dst_ip.ip, sport, dport, lid, flags, ps), D_CLASSIFY, ts
 
 
 def _canonical_key(for_ip, to_ip, to_port):
     try:
         return _canonical_v4(for_ip) is not None and _canonical_v4(to_ip) is not None and \
-            str(int(to_port)) == to_port
+            str(int(to_port)) == to_port and int(to_port) <= 65535
     except ValueError:
         return False
 
 
 def key_tuples(torch, tuples, keyx):
     """The aggregation tuples (int32 [n, 4] tensor) of classified lines: rows
-    of lines with interned keys (``keyx``) carry the key ids in place of the
-    connection (src = from id, dst = to id, dport = port id, no swap) -- what
-    the device aggregates given the gids.  Returns ``tuples`` itself when
-    there are none."""
+    of lines with interned keys (``keyx``: line -> KeyText id) carry the id in
+    place of the connection (src = id, dst = sport = dport = 0, pspell =
+    INTERNED, no swap) -- what the device aggregates given the gids.  Returns
+    ``tuples`` itself when there are none."""
     if not keyx:
         return tuples
     idx = np.fromiter(keyx.keys(), np.int64, len(keyx))
     rows = np.zeros(len(idx), TUPLE_DTYPE)
-    vals = np.array(list(keyx.values()), np.int64).reshape(-1, 4)
     old = tuples[torch.from_numpy(idx).to(tuples.device)].cpu().numpy().view(TUPLE_DTYPE).reshape(-1)
-    rows['src'], rows['dst'], rows['sport'], rows['dport'] = vals[:, 1], vals[:, 2], 0, vals[:, 3]
+    rows['src'] = np.fromiter(keyx.values(), np.int64, len(keyx))
     rows['list'] = old['list']
     rows['flags'] = old['flags'] & np.uint8(0xFF ^ F_SWAP)
-    rows['pspell'] = vals[:, 0]
+    rows['pspell'] = INTERNED
     out = tuples.clone()
     out[torch.from_numpy(idx).to(tuples.device)] = torch.from_numpy(rows.view(np.int32).reshape(-1, 4)).to(
         tuples.device)

@@ -12,9 +12,10 @@ reference text handling goes through these helpers instead.
 
 import re
 
-__all__ = ['PY2_WS', 'py2_strip', 'py2_split', 'py2_lower', 'py2_int', 'py2_isdigit']
+__all__ = ['PY2_WS', 'PY2_MAXINT', 'py2_strip', 'py2_split', 'py2_lower', 'py2_int', 'py2_isdigit', 'py2_is_int']
 
 PY2_WS = ' \t\n\r\x0b\x0c'          # what Python 2's byte-string strip()/split() treat as whitespace
+PY2_MAXINT = (1 << 63) - 1          # sys.maxint of a 64-bit Python 2: int() of a larger literal is a long
 _SPLIT = re.compile('[' + re.escape(PY2_WS) + ']+')
 _LOWER = str.maketrans('ABCDEFGHIJKLMNOPQRSTUVWXYZ', 'abcdefghijklmnopqrstuvwxyz')
 _INT = re.compile(r'[ \t\n\r\x0b\x0c]*[+-]?[0-9]+[ \t\n\r\x0b\x0c]*\Z')
@@ -49,3 +50,10 @@ def py2_int(s):
     if not _INT.match(s):
         raise ValueError('invalid literal for int() with base 10: %r' % (s,))
     return int(s.strip(PY2_WS))
+
+
+def py2_is_int(v):
+    """``isinstance(v, int)`` under Python 2 for a number ``int()`` produced:
+    values outside a 64-bit machine word are ``long``, not ``int``
+    (``firewallrule.py:67-75`` rejects them as ports)."""
+    return isinstance(v, int) and -PY2_MAXINT - 1 <= v <= PY2_MAXINT

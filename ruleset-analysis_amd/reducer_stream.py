@@ -27,7 +27,7 @@ rule's cap threshold after aggregation, and the job is redone up to it.
 Keys are the reducer's strings (``PROTO;FROMIP;TOIP;TOPORT``): canonical
 dotted quads and ports are carried as values (one to one with their text);
 a line whose address or port text is not canonical is parsed on the host and
-its three fields are interned (``pspell | 0x80`` marks such keys), so two
+its whole key text is interned (``pspell == 0x80`` marks such keys), so two
 spellings of one address stay two connections, as in the reference.
 """
 
@@ -39,6 +39,7 @@ from . import textparse
 from .compile import F_BUILT, F_HIT, TUPLE_DTYPE
 from .logparse import reducer_fields, reducer_timestamp, _canonical_v4
 from .py2text import PY2_WS, py2_int
+from .keytext import MAX_SPELL_ID
 from .report import HEADER, INTERNED, NOISE1, KeyText, MemoDecode, _rows_by_gid, key_strings, table_rows
 
 __all__ = ['ReducerStream']
@@ -54,7 +55,8 @@ class ReducerStream(object):
         self.eng, self.db, self.cap, self.write = engine, db, int(cap), write
         self.chunk = max(int(chunk), 1)
         self.pending = b''
-        self.spells = list(textparse.DEFAULT_SPELLS)      # device spelling ids (<= 64, < 0x80)
+        self.spells = list(textparse.DEFAULT_SPELLS)      # spelling ids (the device table holds the first 64)
+        self.spell_ids = {w: k for k, w in enumerate(self.spells)}
         self.istr = KeyText()                             # interned text of non-canonical keys
         self.need = self.chunk                            # bytes to gather before the next chunk is processed
         self.lines_done = 0
@@ -197,7 +199,7 @@ class ReducerStream(object):
             thresh = res.thresh
             for i, exc in bad_month:
                 r = int(status[i])
-                if int(thresh[r]) == 0xFFFFFFFFFFFFFFFF or i < int(thresh[r]):
+                if self.cap > 0 and (int(thresh[r]) == 0xFFFFFFFFFFFFFFFF or i < int(thresh[r])):
                     # the reference reaches months.index at this line: redo the job up to it
                     # (the key test of this line already ran: a run starting here
                     # printed the block before it, as the reference does)
@@ -223,23 +225,21 @@ class ReducerStream(object):
         return carry
 
     def _conn(self, res):
-        """(pspell, from, to, port) fields of a host-parsed BUILT match."""
+        """(pspell, from, to, port) fields of a host-parsed BUILT match: the
+        values of a canonical key, else (INTERNED, id of the key text, 0, 0)."""
         word, f, t, p = res[5], res[6], res[8], res[9]
         try:
             vf, vt = _canonical_v4(f), _canonical_v4(t)
         except ValueError:
             vf = vt = None
         canon = vf is not None and vt is not None and p.isdigit() and (len(p) == 1 or p[0] != '0') and int(p) < 65536
-        if word in self.spells[:64]:
-            sid = self.spells.index(word)
-        else:
+        sid = self.spell_ids.get(word)
+        if sid is None and len(self.spells) < MAX_SPELL_ID:
+            sid = self.spell_ids[word] = len(self.spells)
             self.spells.append(word)
-            sid = len(self.spells) - 1
-            if sid >= INTERNED:
-                raise NotImplementedError('more than 128 protocol spellings')
-        if canon:
+        if canon and sid is not None:
             return sid, vf, vt, int(p)
-        return sid | INTERNED, self.istr(f), self.istr(t), self.istr(p)
+        return INTERNED, self.istr((word, f, t, p)), 0, 0
 
     def _aggregate(self, tuples, ts, status, kind, odd_ts, n_runs):
         eng, torch = self.eng, self.eng.torch

@@ -134,7 +134,7 @@ def block_lines(host, acl, rule, hits, rows, capped, cap, ts_decode, pspell_tabl
     return out
 
 
-def reducer_report(results, groups, noise, cap, ts_decode, pspell_table, n_blank=0, keytext=None):
+def reducer_report(results, groups, noise, cap, ts_decode, pspell_table, n_blank=0, keytext=None, stop=None):
     """Reducer stdout lines.
 
     ``groups``: list of (sort_key, gid, host, acl, rule) for every aggregation
@@ -142,7 +142,11 @@ def reducer_report(results, groups, noise, cap, ts_decode, pspell_table, n_blank
     ``noise``: list of (position_key, raw_text) non-key records; a record is
     emitted before group g iff position_key < g's sort_key.  ``n_blank`` empty
     records (the mapper's doubled newlines) sort before everything else.
-    ``keytext``: the KeyText of records with interned keys.
+    ``keytext``: the KeyText of records with interned keys.  ``stop``: (gid,
+    sorted line text) of the line the reducer dies at (``months.index``,
+    ``connlist-reducer.py:164``): the lines end with what it printed before --
+    every earlier group's block (the key test of the dying line already ran)
+    and the noise sorted before that line -- and no final blank line.
     """
     rows = _rows_by_gid(results.records)
     ts_decode = MemoDecode(ts_decode)
@@ -158,6 +162,12 @@ def reducer_report(results, groups, noise, cap, ts_decode, pspell_table, n_blank
         if prev is not None:
             out.append('')
             out.extend(_block(prev, results, rows, cap, ts_decode, pspell_table, keytext))
+        if stop is not None and gid == stop[0]:
+            while ni < len(noise) and noise[ni][0] < stop[1]:
+                out.append(NOISE1)
+                out.append('The line was: {0}'.format(noise[ni][1].strip(PY2_WS)))
+                ni += 1
+            return out
         prev = (gid, host, acl, rule)
     while ni < len(noise):
         out.append(NOISE1)

@@ -94,11 +94,15 @@ class RuleColumns(object):
         return {name: np.flatnonzero(self.proto == k).astype(np.int64) for k, name in enumerate(self.proto_names)
                 if (self.proto == k).any()}
 
-    def lower(self, idxs, proto, base):
+    def lower(self, idxs, proto, base, oor=(None, None)):
         """Candidate-list entries (compile.RULE_DTYPE) of the rules ``idxs`` for a
         connection of protocol ``proto``: the connection-independent part of
         ``FirewallRule.__contains__`` (firewallrule.py:146-150: permit, protocol
-        'ip' or equal) filters, the rest lowers to integer ranges."""
+        'ip' or equal) filters, the rest lowers to integer ranges.  ``oor``:
+        (sport, dport) of a connection whose port on that side is past 65535
+        (None: in range); such a side matches only a NO_PORT rule side or one
+        naming that port (``:162-171``) and is lowered to "any port" (the
+        tuple carries 0 there, ``CompiledRules.list_id_oor``)."""
         from .compile import RULE_DTYPE
         idx = np.unique(np.asarray(idxs, np.int64))
         if len(idx) and (idx[0] < 0 or idx[-1] >= len(self)):
@@ -108,7 +112,12 @@ class RuleColumns(object):
         keep = self.action[idx] & ok_proto[self.proto[idx]]
         sp = self.sport[idx].astype(np.int64)
         dp = self.dport[idx].astype(np.int64)
-        keep &= ((sp == -1) | ((sp >= 0) & (sp <= 65535))) & ((dp == -1) | ((dp >= 0) & (dp <= 65535)))
+        for col, v in ((sp, oor[0]), (dp, oor[1])):
+            if v is None:
+                keep &= (col == -1) | ((col >= 0) & (col <= 65535))
+            else:
+                keep &= (col == -1) | (col == v)
+                col[:] = -1
         idx, sp, dp = idx[keep], sp[keep], dp[keep]
         out = np.zeros(len(idx), RULE_DTYPE)
         slen = self.src_len[idx].astype(np.int64)

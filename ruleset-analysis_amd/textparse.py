@@ -22,7 +22,7 @@ import numpy as np
 
 from . import logparse
 from .compile import F_BUILT, F_HIT, TUPLE_DTYPE
-from .keytext import INTERNED, KeyText
+from .keytext import KeyText
 
 __all__ = ['IFC_DTYPE', 'SPELL_DTYPE', 'LINE_IGNORE', 'LINE_NOACL', 'LINE_MISSING', 'LINE_CLASSIFY', 'LINE_HOST',
            'DEFAULT_SPELLS', 'ts_pack', 'ts_unpack', 'interface_table', 'spell_table', 'ParsedText', 'parse_text',
@@ -192,7 +192,8 @@ class ParsedText(object):
         self.error = None
         self.n_host = 0               # lines the host parser decided
         self.keytext = None           # keytext.KeyText of interned reducer keys (host-parsed lines)
-        self.keyx = {}                # line -> interned key (logparse._parse_one)
+        self.keyx = {}                # line -> KeyText id of its interned key (logparse._parse_one)
+        self.bad_month = {}           # line -> ValueError of months.index (logparse.parse_logs)
         self._d_text = self._d_off = None   # device text / line offsets (parse_text keep_text=True)
 
     def batch(self):
@@ -297,6 +298,7 @@ def parse_text(engine, host, data, db, compiled, pspell=None, order_base=0, need
     P.disposition = kind[:n]
     P.acl_of = {i: a for i, a in P.acl_of.items() if i < n}
     P.keyx = {i: k for i, k in P.keyx.items() if i < n}
+    P.bad_month = {i: e for i, e in P.bad_month.items() if i < n}
     P.nl = np.zeros(n, bool)
     if n:
         P.nl[:] = True
@@ -306,8 +308,6 @@ def parse_text(engine, host, data, db, compiled, pspell=None, order_base=0, need
     if keep_text:
         P._d_text, P._d_off = text, off
     P.pspell_table = [w for w, _ in sorted(pspell.items(), key=lambda kv: kv[1])]
-    if len(P.pspell_table) > INTERNED:
-        raise NotImplementedError('more than %d protocol spellings' % INTERNED)
     return P
 
 
@@ -360,7 +360,7 @@ def concat(parts, torch):
     if len(parts) == 1:
         return parts[0]
     P = ParsedText()
-    starts, hosts, acl_of, keyx = [], [], {}, {}
+    starts, hosts, acl_of, keyx, bad = [], [], {}, {}, {}
     base = 0
     kept = []
     for p in parts:
@@ -371,6 +371,8 @@ def concat(parts, torch):
             acl_of[base + i] = a
         for i, k in p.keyx.items():
             keyx[base + i] = k
+        for i, e in p.bad_month.items():
+            bad[base + i] = e
         if p.error is not None:
             P.error = (base + p.error[0], p.error[1])
             base += p.n
@@ -386,6 +388,7 @@ def concat(parts, torch):
     P.host_of = _HostOf(starts, hosts)
     P.acl_of = acl_of
     P.keyx = keyx
+    P.bad_month = bad
     P.keytext = kept[0].keytext
     assert all(p.keytext is P.keytext for p in kept), 'parts parsed with different KeyText'
     P.n = base

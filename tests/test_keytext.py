@@ -46,10 +46,9 @@ def test_host_parse_interns_noncanonical_keys():
     # the connection tuples (what the classifier sees) do not change
     for f in ('src', 'dst', 'sport', 'dport', 'list', 'flags'):
         assert np.array_equal(P.tuples[f], Q.tuples[f]), f
-    for i, (ps, f, t, p) in P.keyx.items():
-        assert ps & INTERNED
+    for i, k in P.keyx.items():
         res = logparse.reducer_fields(lines[i].strip(logparse.PY2_WS))[1]
-        assert (P.keytext.values[f], P.keytext.values[t], P.keytext.values[p]) == (res[6], res[8], res[9])
+        assert P.keytext.values[k] == (res[5], res[6], res[8], res[9])
 
 
 def test_key_tuples_rewrites_only_interned_rows():
@@ -59,12 +58,13 @@ def test_key_tuples_rewrites_only_interned_rows():
     tup['flags'] = 0x07 | F_SWAP
     tup['list'] = 9
     t = torch.from_numpy(tup.view(np.int32).reshape(-1, 4).copy())
-    out = logparse.key_tuples(torch, t, {1: (INTERNED | 2, 5, 6, 7), 3: (INTERNED, 0, 1, 2)})
+    out = logparse.key_tuples(torch, t, {1: 5, 3: 0x89ABCDEF})
     assert out is not t
     o = out.numpy().reshape(-1).view(TUPLE_DTYPE)
     assert np.array_equal(o[[0, 2, 4]], tup[[0, 2, 4]])
     assert tuple(o[1][['src', 'dst', 'sport', 'dport', 'list', 'flags', 'pspell']].tolist()) == \
-        (5, 6, 0, 7, 9, 0x07, INTERNED | 2)
+        (5, 0, 0, 0, 9, 0x07, INTERNED)
+    assert int(o[3]['src']) == 0x89ABCDEF
     assert logparse.key_tuples(torch, t, {}) is t
 
 
