@@ -492,11 +492,14 @@ def rank_main(args, rank, world, local):
         try:
             r = job(timed)
         except (native.NativeError, ShardOverflow) as e:
-            # multi-GPU: the merge raises ShardOverflow on every rank together
-            if e.code != native.RSA_ERR_CAPACITY or sizing['capacity'] >= bound:
+            # multi-GPU: the merge raises ShardOverflow on every rank together,
+            # with the entries the fullest owner table needs (its shard's plus
+            # the imported ones: the per-shard bound does not cover those)
+            need = max(bound, getattr(e, 'needed', 0))
+            if e.code != native.RSA_ERR_CAPACITY or sizing['capacity'] >= need:
                 raise
             del pass1_launch_ms[n_t:], pass1_launches[n_l:]
-            sizing['capacity'] = bound
+            sizing['capacity'] = need
             sizing['reruns'] += 1
             r = job(timed)
         return r

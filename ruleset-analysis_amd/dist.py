@@ -126,8 +126,14 @@ def torch_empty_like_cpu(t):
 class ShardOverflow(RuntimeError):
     """Some rank's pass-1 table overflowed (RSA_ERR_CAPACITY): raised on every
     rank together, so all of them can rerun the job with a larger table instead
-    of the healthy ranks waiting in the next collective."""
+    of the healthy ranks waiting in the next collective.  ``needed``: the
+    entries the largest failing table must hold (its own entries plus the
+    records it received for the rules it owns; 0 if unknown)."""
     code = -4    # native.RSA_ERR_CAPACITY
+
+    def __init__(self, msg, needed=0):
+        RuntimeError.__init__(self, msg)
+        self.needed = int(needed)
 
 
 def route_records(buf, world, dist, group=None, flag=0):
@@ -208,17 +214,19 @@ def merge(backend, dist, world, rank, group=None, to_host=True):
             except Exception as e:  # noqa: BLE001
                 if not _overflow(e):
                     raise
-                failed = 1
+                # the table must hold the shard's entries and every received one
+                failed = max(backend.table_need(recv.numel() // REC), 1)
         tr('import1', dev)
         # thresholds of the owned rules (MAX: the others say "none" = -1),
-        # with the overflow flag riding along as one more element
+        # with the overflow flag (the entries a failed table needs) riding along
         thresh = torch.cat([c['thresh'].masked_fill(others, NO_THRESHOLD),
                             torch.tensor([failed], dtype=torch.int64, device=dev)])
         _all_reduce(thresh, dist, group, op=dist.ReduceOp.MAX)
-        capped_any, failed_any = (bool(x) for x in torch.stack([(thresh[:-1] != NO_THRESHOLD).any(),
-                                                               thresh[-1] != 0]).cpu().tolist())
-        if failed_any:
-            raise ShardOverflow('distinct-connection table overflow on at least one rank')
+        capped_any, need = (int(x) for x in torch.stack([(thresh[:-1] != NO_THRESHOLD).any().to(torch.int64),
+                                                         thresh[-1]]).cpu().tolist())
+        capped_any = bool(capped_any)
+        if need:
+            raise ShardOverflow('distinct-connection table overflow on at least one rank (merge import)', needed=need)
         thresh = thresh[:-1]
         tr('cap', dev)
         if capped_any:
@@ -299,6 +307,11 @@ class EngineBackend(object):
 
     def import_records(self, buf, which):
         self.eng.import_records(buf, which)
+
+    def table_need(self, n_received):
+        """Entries the table needs to hold this shard's pass-1 entries and
+        n_received imported records (each possibly new)."""
+        return self.eng.table_size() + int(n_received)
 
     def resolve_cap(self):
         return self.eng.resolve_cap()

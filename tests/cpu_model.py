@@ -191,6 +191,9 @@ class NumpyBackend(object):
                 e[5] = min(e[5], int(r['first']))
                 e[6] = max(e[6], int(r['last']))
 
+    def table_need(self, n_received):
+        return len(self.local.t) + int(n_received)
+
     def resolve_cap(self):
         th = self.local.local_thresh(self.n_rules, self.cap)
         self._counters['thresh'].copy_(torch.from_numpy(th.view(np.int64).copy()))

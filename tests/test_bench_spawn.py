@@ -58,8 +58,10 @@ def check_dump_against_oracle(got, world, rules, lines, cap, seed=3):
     return ref
 
 
-@pytest.mark.parametrize('world,cap', [(2, 15), (3, 100000)])
+@pytest.mark.parametrize('world,cap', [(2, 15), (3, 100000), (8, 12)])
 def test_bench_spawn_cpu_model_matches_oracle(tmp_path, world, cap):
+    """World 8 is the driver's scaling run (one node): eight rank processes,
+    the all_to_all routing to eight owners, the cap engaged."""
     rules, lines = 300, 12000
     line, got = run_bench(tmp_path, ['--backend', 'gloo', '--cpu-model', '--gpus', str(world), '--rules', str(rules),
                                      '--lines', str(lines), '--cap', str(cap)])
