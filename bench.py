@@ -542,6 +542,11 @@ def rank_main(args, rank, world, local):
         if sizing['learn']:
             learn_capacity()
 
+    phase_prof = os.environ.get('RSA_PHASE_PROF') == '1'   # PROFILING: a -DRSA_PHASE_PROF library variant
+    if phase_prof:
+        import ctypes
+        ph = (ctypes.c_uint64 * 9)()
+        eng.ctx.call('rsa_phase_prof', ph, ctypes.c_int(1))
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -549,6 +554,12 @@ def rank_main(args, rank, world, local):
     for _ in range(args.steps):
         n_rec = step(True)
     torch.cuda.synchronize()
+    if phase_prof:
+        eng.ctx.call('rsa_phase_prof', ph, ctypes.c_int(1))
+        v = [int(x) for x in ph]
+        names = ['tuple+list', 'prefix', 'pruning', 'group0', 'tasks', 'verify', 'resid+chain', 'emit']
+        log('phase_prof cycles/wave-iteration: ' + json.dumps(
+            {nm: round(v[k] / max(v[8], 1), 1) for k, nm in enumerate(names)}) + ' iterations %d' % v[8])
     if dist is not None:
         dist.barrier()
     dt = time.perf_counter() - t0

@@ -87,8 +87,9 @@ typedef struct rsa_rule_entry {
  *          point there with n_slots = 1)
  * holding the smallest entry index with that key.  Pruning: per non-zero src
  * (dst) mask of a record, a CHD table over H = fmix32((src & mask) ^ 0x9E3779B9)
- * (dst: ^ 0x7F4A7C15) whose word value indexes a uint64 bitmap of the groups
- * holding a rule on that prefix; groups with mask 0 are in src_any (dst_any).
+ * (dst: ^ 0x7F4A7C15) whose slot value indexes a uint64 bitmap of the groups
+ * holding a rule on that prefix (bitmap 0 is empty: an empty slot, 0, and a
+ * tag mismatch both read it); groups with mask 0 are in src_any (dst_any).
  * A tuple probes only the groups in (src bitmap & dst bitmap).  All other
  * entries are residual (a first-gid-ascending list scanned linearly).
  *
@@ -100,8 +101,9 @@ typedef struct rsa_rule_entry {
  *
  * Everything lives in ONE uint32 image: word 0 = 0xFFFFFFFF, word 1 =
  * RSA_PHT_MAGIC, word 2 = n_lists, word 3 = list_off (word offset of n_records
- * rsa_pht_list records), word 4 = n_records, words 5..7 = 0; records sit at
- * 4-word aligned offsets, bitmaps at even offsets (low word first). */
+ * rsa_pht_list records), word 4 = n_records, word 5 = flags (bit 1: every
+ * pruning table has 16-bit slots), words 6..7 = 0; records sit at 4-word
+ * aligned offsets, bitmaps at even offsets (low word first). */
 #define RSA_PHT_MAGIC 0x34415352u
 #define RSA_PHT_NONE 0xFFFFFFFFu
 
@@ -148,8 +150,8 @@ typedef struct rsa_pht_group {   /* 80 B */
 typedef struct rsa_pht_mask {    /* 16 B: one pruning table (src tables first: rsa_pht_list.n_src_masks) */
   uint32_t mask;             /* address mask (non-zero)                           */
   uint32_t slot;             /* slot_off | RSA_PHT_NARROW: uint16 slots (H & 0xFF) << 8 | value,
-                                0xFFFF empty, slot_off in uint16 units, values < 255;
-                                else 32-bit slots as above                        */
+                                slot_off in uint16 units, values 1..255; else uint32
+                                slots (H & 0xFFFF) << 16 | value; 0 = empty (value 0) */
   uint32_t disp_off;         /* first displacement, uint16 units                  */
   uint32_t size;             /* n_slots | disp_mask << 17; slot value = bitmap index */
 } rsa_pht_mask;

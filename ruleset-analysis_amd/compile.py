@@ -391,6 +391,7 @@ PHT_NONE = 0xFFFF
 PHT_MAX_IDX = 0xFFFE
 PHT_MAX_SLOTS = 0x10000              # slot index * n_slots must fit the 24-bit multiplier
 MASK_NARROW = 0x80000000            # pruning record word 1: 16-bit slots (offset in uint16 units)
+HDR_ALL_NARROW = 0x2                # image word 5: every pruning table has 16-bit slots
 SALT_S, SALT_D, SALT_P = 0x9E3779B9, 0x7F4A7C15, 0x2545F491
 
 
@@ -505,6 +506,7 @@ class _Image(object):
     def __init__(self):
         self.chunks = [np.array([PHT_EMPTY, PHT_MAGIC, 0, 0, 0, 0, 0, 0], dtype=np.uint32)]
         self.n = PHT_HEADER_WORDS
+        self.all_narrow = True      # header word 5 bit 1: every pruning table has 16-bit slots
 
     def alloc(self, arr, align=1):
         pad = (-self.n) % align
@@ -529,17 +531,30 @@ class _Image(object):
         return (soff, 2 * doff, nslots, dmask)
 
     def table16(self, H, vals):
-        """CHD table with 16-bit slots (8-bit tag << 8 | 8-bit value, 0xFFFF
-        empty) for values < 255; offsets in uint16 units of the image."""
+        """Pruning CHD table with 16-bit slots (8-bit tag << 8 | 8-bit value,
+        values 1..255; 0 = empty, which reads as value 0 = the empty bitmap);
+        offsets in uint16 units of the image."""
         nslots, dmask, disp, slot_of = _chd(H)
         dwords = np.zeros(((dmask + 2) // 2) * 2, dtype=np.uint16)
         dwords[:dmask + 1] = disp
         doff, _ = self.alloc(dwords.view(np.uint32))
-        slots = np.full(nslots + (nslots & 1), 0xFFFF, dtype=np.uint16)
+        slots = np.zeros(nslots + (nslots & 1), dtype=np.uint16)
         slots[slot_of] = ((H.astype(np.uint32) & np.uint32(0xFF)) << np.uint32(8)).astype(np.uint16) | \
             np.asarray(vals, np.uint16)
         soff, _ = self.alloc(slots.view(np.uint32))
         return (2 * soff, 2 * doff, nslots, dmask)
+
+    def table_prune(self, H, vals):
+        """Pruning CHD table with 32-bit slots (16-bit tag << 16 | value, 0 =
+        empty = value 0, the empty bitmap)."""
+        nslots, dmask, disp, slot_of = _chd(H)
+        dwords = np.zeros(((dmask + 2) // 2) * 2, dtype=np.uint16)
+        dwords[:dmask + 1] = disp
+        doff, _ = self.alloc(dwords.view(np.uint32))
+        slots = np.zeros(nslots, dtype=np.uint32)
+        slots[slot_of] = ((H.astype(np.uint32) & np.uint32(0xFFFF)) << np.uint32(16)) | np.asarray(vals, np.uint32)
+        soff, _ = self.alloc(slots)
+        return (soff, 2 * doff, nslots, dmask)
 
     def build(self):
         return np.concatenate(self.chunks)
@@ -643,22 +658,25 @@ def _index_record(img, rec, e, pre, min_entries, max_groups):
                 for h, k in zip(H.tolist(), keys.tolist()):   # full-hash collision: OR (a superset is safe)
                     merged[h] = merged.get(h, 0) | by_mask[m][k]
                 tables.append((m, side, merged))
+        # bitmap 0 is the empty one: an empty slot or a tag mismatch reads it
         distinct = sorted({b for _m, _s, mg in tables for b in mg.values()})
-        bm_index = {b: i for i, b in enumerate(distinct)}
-        if len(distinct) > PHT_MAX_IDX:
+        bm_index = {b: i + 1 for i, b in enumerate(distinct)}
+        if len(distinct) + 1 > PHT_MAX_IDX:
             raise OverflowError('too many distinct group bitmaps in one list')
-        bm_words = np.zeros(2 * max(len(distinct), 1), dtype=np.uint32)
-        for i, b in enumerate(distinct):
+        bm_words = np.zeros(2 * (len(distinct) + 1), dtype=np.uint32)
+        for b, i in bm_index.items():
             bm_words[2 * i] = b & M32
             bm_words[2 * i + 1] = b >> 32
         bm_off, _ = img.alloc(bm_words, align=2)
         moff, mrec = img.alloc(np.zeros(PHT_MASK_WORDS * max(len(tables), 1), dtype=np.uint32), align=4)
+        narrow = len(distinct) + 1 <= 0x100      # 16-bit slots: half the LDS of the pruning tables
+        if not narrow:
+            img.all_narrow = False
         for q, (m, side, merged) in enumerate(tables):
             H = np.array(list(merged.keys()), dtype=np.uint32)
             vals = np.array([bm_index[b] for b in merged.values()], dtype=np.uint32)
             r = mrec[PHT_MASK_WORDS * q: PHT_MASK_WORDS * (q + 1)]
-            narrow = len(distinct) < 0xFF     # 16-bit slots: half the LDS of the pruning tables
-            soff, doff, nslots, dmask = img.table16(H, vals) if narrow else img.table(H, vals)
+            soff, doff, nslots, dmask = img.table16(H, vals) if narrow else img.table_prune(H, vals)
             r[0] = m
             r[1] = soff | (MASK_NARROW if narrow else 0)
             r[2] = doff
@@ -668,7 +686,7 @@ def _index_record(img, rec, e, pre, min_entries, max_groups):
         rec[7] = bm_off
         rec[8], rec[9] = src_any & M32, src_any >> 32
         rec[10], rec[11] = dst_any & M32, dst_any >> 32
-        rec[14] = len(distinct)
+        rec[14] = len(distinct) + 1
     return sorted(set(resid_idx))
 
 
@@ -720,6 +738,8 @@ def build_index(ent, off, prefix=0, min_entries=96, max_groups=PHT_MAX_GROUPS, c
             resid_parts.append(e[resid_idx])
             n_resid += len(resid_idx)
             rec[5] = n_resid
+    if img.all_narrow:
+        img.chunks[0][5] |= HDR_ALL_NARROW
     image = img.build()
     resid = np.concatenate(resid_parts) if resid_parts else np.zeros(0, RULE_DTYPE)
     return image, resid
@@ -745,14 +765,19 @@ def _probe(image, H, t):
     return (w & 0xFFFF) if (w >> 16) == (H & 0xFFFF) else PHT_NONE
 
 
-def _probe16(image, H, t):
-    """One probe of a 16-bit-slot CHD table (csrc: pht_probe16): value or PHT_NONE."""
+def _prune_probe(image, H, t, narrow):
+    """One pruning-table probe (csrc: prune_side): the bitmap index of the
+    slot, 0 (the empty bitmap) on an empty slot or a tag mismatch."""
     slot_off, disp_off, n_slots, disp_mask = (int(v) for v in t)
     H = int(H)
     h16 = image.view(np.uint16)
     d = int(h16[disp_off + ((H >> 16) & disp_mask)])
-    w = int(h16[slot_off + int(pht_slot(H, d, n_slots))])
-    return (w & 0xFF) if w != 0xFFFF and (w >> 8) == (H & 0xFF) else PHT_NONE
+    slot = int(pht_slot(H, d, n_slots))
+    if narrow:
+        w = int(h16[slot_off + slot])
+        return (w & 0xFF) if (w >> 8) == (H & 0xFF) else 0
+    w = int(image[slot_off + slot])
+    return (w & 0xFFFF) if (w >> 16) == (H & 0xFFFF) else 0
 
 
 def _match(x, src, dst, ports):
@@ -799,13 +824,12 @@ def pht_lookup(index, ent, off, L, src, dst, ports):
                 side = 0 if q < n_src else 1
                 key = (dst if side else src) & mr[0]
                 t = (mr[1] & ~MASK_NARROW, mr[2], mr[3] & 0x1FFFF, mr[3] >> 17)
-                v = (_probe16 if mr[1] & MASK_NARROW else _probe)(image, field_hash(key, side), t)
-                if v != PHT_NONE:
-                    bits = int(image[r[7] + 2 * v]) | (int(image[r[7] + 2 * v + 1]) << 32)
-                    if side:
-                        D |= bits
-                    else:
-                        S |= bits
+                v = _prune_probe(image, field_hash(key, side), t, bool(mr[1] & MASK_NARROW))
+                bits = int(image[r[7] + 2 * v]) | (int(image[r[7] + 2 * v + 1]) << 32)
+                if side:
+                    D |= bits
+                else:
+                    S |= bits
             cand0 = S & D
             floor = 0
             found = None

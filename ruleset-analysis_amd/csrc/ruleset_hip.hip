@@ -284,23 +284,31 @@ __device__ __forceinline__ uint32_t pht_probe(P32 img, uint32_t H, v4u b) {
   return ((w >> 16) == (H & 0xFFFFu)) ? (w & 0xFFFFu) : kNoCand;
 }
 
-// A pruning-table probe (compile.py _probe/_probe16 by the record's
-// MASK_NARROW bit), branch-free: the slot is read through the dword that holds
-// it.  m = the packed record {mask, slot_off | narrow << 31, disp_off,
-// n_slots | disp_mask << 17}; 16-bit slots hold tag << 8 | value (0xFFFF
-// empty, values < 255), 32-bit slots tag << 16 | value.
-template <typename P32>
-__device__ __forceinline__ uint32_t mask_probe(P32 img, uint32_t H, v4u m) {
-  const uint32_t d = rd16(img, m.z + ((H >> 16) & (m.w >> 17)));
-  const uint32_t narrow = m.y >> 31;
-  const uint32_t hidx = (m.y & 0x7FFFFFFFu) + pht_slot(H, d, m.w & 0x1FFFFu);   // in units of the slot width
-  const uint32_t w32 = img[hidx >> narrow];
-  const uint32_t sh = 16u >> narrow;                                  // tag shift: 16 (wide) or 8 (narrow)
-  const uint32_t u = narrow ? (w32 >> ((hidx & 1u) << 4)) & 0xFFFFu : w32;
-  const uint32_t fm = (1u << sh) - 1u;
-  const uint32_t val = u & fm;
-  return ((u >> sh) == (H & fm) && val != fm) ? val : kNoCand;
-}
+// PROFILING BUILD ONLY (make variant DEFS=-DRSA_PHASE_PROF=1): per-wave wall
+// cycles (s_memtime) of the classifier's phases, summed over all waves into
+// g_phase and read by rsa_phase_prof.  The markers wait for outstanding LDS
+// and scalar loads (lgkmcnt), so the timed kernel is slower than the real one
+// and the split is indicative only.
+#ifdef RSA_PHASE_PROF
+struct PhaseAcc {
+  unsigned long long last, acc[8];
+};
+__device__ unsigned long long g_phase[9];
+#define RSA_PH_PARAM , PhaseAcc& ph
+#define RSA_PH_ARG , ph
+#define PH(k)                                                      \
+  do {                                                             \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();    \
+    ph.acc[k] += t_ - ph.last;                                     \
+    ph.last = t_;                                                  \
+  } while (0)
+#else
+#define RSA_PH_PARAM
+#define RSA_PH_ARG
+#define PH(k) \
+  do {        \
+  } while (0)
+#endif
 
 constexpr int kAttempts = 4;   // compile.py PHT_ATTEMPTS
 constexpr uint32_t kListWords = 20, kGroupWords = 20, kMaskWords = 4;
@@ -308,10 +316,60 @@ constexpr uint32_t kListWords = 20, kGroupWords = 20, kMaskWords = 4;
 // Pruning stage of the index lookup for ONE lane (compile.py pht_lookup): each
 // src/dst mask table maps the masked address to a bitmap of the groups holding
 // a rule on that prefix; the candidate groups are those in both the src and
-// the dst bitmap.  Masks are probed two at a time, branch-free (an odd count
-// probes its last mask twice: OR is idempotent).  lw: the lane's list record
-// {group_off, n_groups, mask_off, n_masks}, {…, bm_off}, {src_any, dst_any}.
-template <typename P32>
+// the dst bitmap.  A pruning slot holds tag << 8 | value (16-bit slots, tag =
+// H & 0xFF) or tag << 16 | value (32-bit, tag = H & 0xFFFF); value indexes
+// the record's uint64 bitmaps, where bitmap 0 is empty: an empty slot (0) or
+// a tag mismatch reads bitmap 0, so every probe ORs a bitmap in, branch-free.
+// The src tables come first (n_src_masks), then the dst tables: each side is
+// its own loop with its address and salt fixed, kU masks per iteration phase
+// by phase (all reads of a phase in flight before the first is waited for; a
+// short last batch repeats its last mask: OR is idempotent).  kNarrow: every
+// table of the image has 16-bit slots (image word 5 bit 1, wave-uniform), so
+// the slot width is not decided per table.
+template <bool kNarrow, int kPruneU, typename P32>
+__device__ __forceinline__ unsigned long long prune_side(P32 img, uint32_t moff, uint32_t k0, uint32_t k1, uint32_t key,
+                                                         uint32_t salt, uint32_t bm_off) {
+  unsigned long long acc = 0ull;
+  for (uint32_t k = k0; k < k1; k += kPruneU) {
+    v4u m[kPruneU];
+    uint32_t H[kPruneU], w[kPruneU];
+#pragma unroll
+    for (int u = 0; u < kPruneU; ++u) m[u] = rd4(img, moff + kMaskWords * min(k + u, k1 - 1));
+#pragma unroll
+    for (int u = 0; u < kPruneU; ++u) {
+      H[u] = fmix32((key & m[u].x) ^ salt);
+      w[u] = rd16(img, m[u].z + ((H[u] >> 16) & (m[u].w >> 17)));   // displacement
+    }
+#pragma unroll
+    for (int u = 0; u < kPruneU; ++u) {
+      const uint32_t hidx = (m[u].y & 0x7FFFFFFFu) + pht_slot(H[u], w[u], m[u].w & 0x1FFFFu);
+      if (kNarrow) {
+        w[u] = rd16(img, hidx);
+      } else {
+        const uint32_t narrow = m[u].y >> 31;
+        const uint32_t w32 = img[hidx >> narrow];
+        w[u] = narrow ? (w32 >> ((hidx & 1u) << 4)) & 0xFFFFu : w32;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kPruneU; ++u) {
+      uint32_t v;
+      if (kNarrow) {
+        v = (w[u] >> 8) == (H[u] & 0xFFu) ? (w[u] & 0xFFu) : 0u;
+      } else {
+        const uint32_t sh = (m[u].y >> 31) ? 8u : 16u, fm = (1u << sh) - 1u;
+        v = (w[u] >> sh) == (H[u] & fm) ? (w[u] & fm) : 0u;
+      }
+      const v2u bb = rd2(img, bm_off + 2 * v);   // bm_off is even (compile.py: alloc align=2)
+      acc |= ((unsigned long long)bb.y << 32) | bb.x;
+    }
+  }
+  return acc;
+}
+
+// lw: the lane's list record {group_off, n_groups, mask_off, n_masks}, {…,
+// bm_off}, {src_any, dst_any}, n_src_masks at word 18.
+template <bool kNarrow, typename P32>
 __device__ __forceinline__ unsigned long long index_candidates(P32 img, uint32_t lw, uint32_t src, uint32_t dst) {
   const v4u h0 = rd4(img, lw);
   const v4u h2 = rd4(img, lw + 8);
@@ -319,50 +377,12 @@ __device__ __forceinline__ unsigned long long index_candidates(P32 img, uint32_t
   unsigned long long D = ((unsigned long long)h2.w << 32) | h2.z;
   const uint32_t bm_off = img[lw + 7];
   const uint32_t nm = h0.w, ns = img[lw + 18];   // the first ns records are the src tables
-  constexpr int kU = 4;   // masks in flight per iteration (each a chain of dependent LDS reads)
-  for (uint32_t k = 0; k < nm; k += kU) {
-    // phase by phase over the kU masks, so that the reads of one phase are all
-    // in flight before the first is waited for (a short last batch repeats
-    // its last mask: OR is idempotent)
-    v4u m[kU];
-    uint32_t H[kU], w[kU];
-    bool side[kU];
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const uint32_t kk = min(k + u, nm - 1);
-      m[u] = rd4(img, h0.z + kMaskWords * kk);
-      side[u] = kk >= ns;
-    }
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      H[u] = fmix32(((side[u] ? dst : src) & m[u].x) ^ (side[u] ? kSaltD : kSaltS));
-      w[u] = rd16(img, m[u].z + ((H[u] >> 16) & (m[u].w >> 17)));   // displacement
-    }
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const uint32_t narrow = m[u].y >> 31;
-      const uint32_t hidx = (m[u].y & 0x7FFFFFFFu) + pht_slot(H[u], w[u], m[u].w & 0x1FFFFu);
-      m[u].z = hidx;                                   // (reused: slot index in units of the slot width)
-      w[u] = img[hidx >> narrow];
-    }
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const uint32_t narrow = m[u].y >> 31, hidx = m[u].z;
-      const uint32_t sh = 16u >> narrow, fm = (1u << sh) - 1u;
-      const uint32_t uu = narrow ? (w[u] >> ((hidx & 1u) << 4)) & 0xFFFFu : w[u];
-      const uint32_t val = uu & fm;
-      w[u] = ((uu >> sh) == (H[u] & fm) && val != fm) ? val : kNoCand;   // (mask_probe)
-      const uint32_t bw = bm_off + 2 * (w[u] == kNoCand ? 0u : w[u]);
-      const v2u bb = rd2(img, bw);   // bm_off is even (compile.py: alloc align=2)
-      m[u].x = bb.x;
-      m[u].y = bb.y;
-    }
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const unsigned long long b = w[u] == kNoCand ? 0ull : (((unsigned long long)m[u].y << 32) | m[u].x);
-      D |= side[u] ? b : 0ull;
-      S |= side[u] ? 0ull : b;
-    }
+  if (kNarrow) {
+    S |= prune_side<true, 4>(img, h0.z, 0u, ns, src, kSaltS, bm_off);
+    D |= prune_side<true, 4>(img, h0.z, ns, nm, dst, kSaltD, bm_off);
+  } else {   // (rare: a list with more than 255 distinct group bitmaps) one mask at a time
+    S |= prune_side<false, 1>(img, h0.z, 0u, ns, src, kSaltS, bm_off);
+    D |= prune_side<false, 1>(img, h0.z, ns, nm, dst, kSaltD, bm_off);
   }
   return S & D;
 }
@@ -440,11 +460,11 @@ __device__ __forceinline__ uint32_t index_verify(const Rules& R, P32 img, uint32
 // Index lookup for ONE lane, all in the lane's own control flow (the
 // RSA_OPT_GROUP_TASKS=0 form): pruning, the candidate groups in ascending
 // min index with early exit, verification.
-template <typename P32>
+template <bool kNarrow, typename P32>
 __device__ __forceinline__ uint32_t index_lookup(const Rules& R, P32 img, uint32_t lw, uint32_t src, uint32_t dst,
                                                  uint32_t ports) {
   if (R.prof & 1) return kNoGid;
-  const unsigned long long cand0 = index_candidates(img, lw, src, dst);
+  const unsigned long long cand0 = index_candidates<kNarrow>(img, lw, src, dst);
   if (!cand0 || (R.prof & 2)) return kNoGid;
   const uint32_t group_off = img[lw];
   const PortHash hp = port_hash(ports);
@@ -483,11 +503,12 @@ __device__ __forceinline__ void wave_lds_fence() {
 // the serial loop's first attempt.  scr: this wave's 64 LDS words (the task
 // list {group word << 6 | owner lane}, then per-owner minima via ds_min).
 // Returns gid, kNoGid or kDefer for the ix lanes.
-template <typename P32>
+template <bool kNarrow, typename P32>
 __device__ __forceinline__ uint32_t index_lookup_wave(const Rules& R, P32 img, uint32_t lw, bool ix, uint32_t src,
-                                                      uint32_t dst, uint32_t ports, lds_w32* scr) {
+                                                      uint32_t dst, uint32_t ports, lds_w32* scr RSA_PH_PARAM) {
   if (R.prof & 1) return kNoGid;
-  const unsigned long long cand0 = ix ? index_candidates(img, lw, src, dst) : 0ull;
+  const unsigned long long cand0 = ix ? index_candidates<kNarrow>(img, lw, src, dst) : 0ull;
+  PH(2);
   if (__ballot(cand0 != 0ull) == 0ull || (R.prof & 2)) return kNoGid;
   const uint32_t lane = __lane_id();
   const uint32_t group_off = ix ? img[lw] : 0u;
@@ -498,6 +519,7 @@ __device__ __forceinline__ uint32_t index_lookup_wave(const Rules& R, P32 img, u
     const uint32_t g = (uint32_t)__builtin_ctzll(cand0);
     bi = group_probe(img, group_rec(img, group_off + kGroupWords * g), src, dst, hp, 0u);
   }
+  PH(3);
   unsigned long long rem = cand0 & (cand0 - 1ull);   // this lane's groups not yet probed
   if (__ballot(rem != 0ull) != 0ull) {
     // exclusive prefix of the remaining counts over the wave, by bit planes
@@ -535,9 +557,12 @@ __device__ __forceinline__ uint32_t index_lookup_wave(const Rules& R, P32 img, u
       wave_lds_fence();
     }
   }
+  PH(4);
   if (!ix || cand0 == 0ull) return kNoGid;
   if (R.prof & 4) return bi == kNoCand ? kNoGid : bi;
-  return index_verify(R, img, lw, cand0, bi, src, dst, ports);
+  const uint32_t v = index_verify(R, img, lw, cand0, bi, src, dst, ports);
+  PH(5);
+  return v;
 }
 
 // ---- partial-key bucket index (RSA_BKT_MAGIC, bucketindex.py) ---------------------
@@ -758,9 +783,9 @@ __device__ __forceinline__ uint32_t bucket_lookup(const Rules& R, P32 img, uint3
 // runs per lane.  kExact: ignore the index (the deferred-line path).
 // kMode: 0 = pht index, per-lane group loops; 1 = pht index, candidate groups
 // dealt out over the wave (RSA_OPT_GROUP_TASKS); 2 = bucket index.
-template <bool kExact, int kMode, typename P32>
+template <bool kExact, int kMode, bool kNarrow, typename P32>
 __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Rules& R, P32 img, unsigned int* flags,
-                                                  lds_w32* scr) {
+                                                  lds_w32* scr RSA_PH_PARAM) {
   const uint32_t list = t.w & 0xFFFFu;
   if (active && list >= R.n_lists) {
     atomicOr(&flags[1], 1u);
@@ -784,6 +809,7 @@ __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Ru
   uint32_t lw = R.list_off + kListWords * (active ? list : 0u);
   // 1. prefix scans
   const uint32_t pre_n = active ? img[lw + 6] : 0u;
+  PH(0);
   unsigned long long pending = __ballot(active && pre_n != 0);
   while (pending) {
     const int leader = __builtin_ctzll(pending);
@@ -800,6 +826,7 @@ __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Ru
   // lane's best exceeds its smallest gid
   bool go = active && best > img[lw + 15];
   bool deferred = false;
+  PH(1);
   while (__ballot(go)) {
     const bool ix = go && img[lw + 1] != 0;
     uint32_t c = kNoGid;
@@ -813,9 +840,9 @@ __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Ru
         }
       }
     } else if (kMode == 1) {
-      c = index_lookup_wave(R, img, lw, ix, t.x, t.y, t.z, scr);
+      c = index_lookup_wave<kNarrow>(R, img, lw, ix, t.x, t.y, t.z, scr RSA_PH_ARG);
     } else if (ix) {
-      c = index_lookup(R, img, lw, t.x, t.y, t.z);
+      c = index_lookup<kNarrow>(R, img, lw, t.x, t.y, t.z);
     }
     if (ix) {
       if (c == kDefer) {
@@ -842,6 +869,7 @@ __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Ru
       go = next != RSA_PHT_NONE && best > img[lw + 17];
       if (go) lw = R.list_off + kListWords * next;
     }
+    PH(6);
   }
   if (deferred) return kDefer;
   return active ? best : kNoGid;
@@ -1089,7 +1117,7 @@ __device__ __forceinline__ void emit_one(uint32_t i, uint4 t, uint32_t gid, cons
 // with kEmit the line's counter word and table record (emit_wave).  Lines
 // whose index candidate failed verification kAttempts times go to `tail`
 // (k_tail scans and emits them exactly).
-template <int kImg, bool kEmit, int kMode>
+template <int kImg, bool kEmit, int kMode, bool kNarrow>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kImgSmallMax ? 4 : 8, 8))) void k_classify(
     const uint4* __restrict__ T, unsigned long long n, int32_t* __restrict__ gout, Rules R, unsigned int* flags,
     uint32_t* tail, unsigned long long* tail_n, Agg A, Emit E) {
@@ -1105,16 +1133,24 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kIm
   // 32-bit line indices: batches are < 2^31 lines (run_pass1, rsa_classify_only)
   const uint32_t n32 = (uint32_t)n;
   const uint32_t stride = gridDim.x * blockDim.x;
+#ifdef RSA_PHASE_PROF
+  PhaseAcc ph = {};
+  unsigned long long waves_seen = 0;
+#endif
   for (uint32_t base = blockIdx.x * blockDim.x; base < n32; base += stride) {
+#ifdef RSA_PHASE_PROF
+    ph.last = __builtin_amdgcn_s_memtime();
+    ++waves_seen;
+#endif
     const uint32_t i = base + threadIdx.x;
     const bool in = i < n32;
     const uint4 t = in ? T[i] : make_uint4(0u, 0u, 0u, 0u);
     const bool valid = in && (((t.w >> 16) & 0xFFu) & RSA_F_VALID);
     uint32_t gid;
     if (kImg > 0) {
-      gid = classify_wave<false, kMode>(t, valid, R, (const lds_u32*)lds_img, flags, scr);
+      gid = classify_wave<false, kMode, kNarrow>(t, valid, R, (const lds_u32*)lds_img, flags, scr RSA_PH_ARG);
     } else {
-      gid = classify_wave<false, kMode>(t, valid, R, R.img, flags, scr);
+      gid = classify_wave<false, kMode, kNarrow>(t, valid, R, R.img, flags, scr RSA_PH_ARG);
     }
     const bool defer = gid == kDefer;
     const unsigned long long dm = __ballot(defer);
@@ -1128,7 +1164,14 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kIm
     }
     if (gout && in && !defer) gout[i] = (int32_t)gid;
     if (kEmit) emit_wave(i, n32, in && !defer, t, gid, A, E);
+    PH(7);
   }
+#ifdef RSA_PHASE_PROF
+  if (__lane_id() == 0) {
+    for (int k = 0; k < 8; ++k) atomicAdd(&g_phase[k], ph.acc[k]);
+    atomicAdd(&g_phase[8], waves_seen);
+  }
+#endif
 }
 
 // Pass 1a, deferred lines: exact linear scan of their whole list (+ emission).
@@ -1144,7 +1187,10 @@ __global__ __launch_bounds__(kBlock) void k_tail(const uint4* __restrict__ T, in
     const unsigned long long i = in ? tail[j] : 0u;
     const uint4 t = in ? T[i] : make_uint4(0u, 0u, 0u, 0u);
     const bool valid = in && (((t.w >> 16) & 0xFFu) & RSA_F_VALID);
-    const uint32_t gid = classify_wave<true, 0>(t, valid, R, R.img, flags, nullptr);
+#ifdef RSA_PHASE_PROF
+    PhaseAcc ph = {};   // (the exact tail is not profiled)
+#endif
+    const uint32_t gid = classify_wave<true, 0, false>(t, valid, R, R.img, flags, nullptr RSA_PH_ARG);
     if (gout && in) gout[i] = (int32_t)gid;
     if (kEmit && in) emit_one((uint32_t)i, t, gid, A, E);
   }
@@ -2699,6 +2745,7 @@ struct rsa_ctx {
   bool indexed = false;
   bool bkt_index = false;               // the loaded image is the bucket index (RSA_BKT_MAGIC)
   bool bkt_filters = false;             // ... with row filters
+  bool prune_narrow = false;            // pht index: all pruning tables narrow (image word 5 bit 1)
   bool force_defer = false;
   bool group_tasks = true;     // RSA_OPT_GROUP_TASKS
   uint32_t prof_classify = 0;  // RSA_OPT_PROFILE_CLASSIFY
@@ -3021,18 +3068,18 @@ int ensure_events(rsa_ctx* c) {
 constexpr int kImgSmall = kImgSmallMax;   // 76 KiB: two 1024-thread workgroups per CU (32 waves)
 constexpr int kImgLarge = 38912;   // 152 KiB: one workgroup per CU
 
-template <bool kEmit, int kMode>
+template <bool kEmit, int kMode, bool kNarrow>
 void launch_classify_img(rsa_ctx* c, const uint4* t, uint64_t m, int32_t* go, const Rules& r, const Agg& ag,
                          const Emit& e) {
   if (c->indexed && c->img_words <= (uint32_t)kImgSmall) {
-    k_classify<kImgSmall, kEmit, kMode><<<grid_for_threads(c, m, 1024, 2), 1024, 0, c->stream>>>(
+    k_classify<kImgSmall, kEmit, kMode, kNarrow><<<grid_for_threads(c, m, 1024, 2), 1024, 0, c->stream>>>(
         t, m, go, r, c->d_flags, c->d_tail, c->d_tail_n, ag, e);
   } else if (c->indexed && c->img_words <= (uint32_t)kImgLarge) {
-    k_classify<kImgLarge, kEmit, kMode><<<grid_for_threads(c, m, 1024, 1), 1024, 0, c->stream>>>(
+    k_classify<kImgLarge, kEmit, kMode, kNarrow><<<grid_for_threads(c, m, 1024, 1), 1024, 0, c->stream>>>(
         t, m, go, r, c->d_flags, c->d_tail, c->d_tail_n, ag, e);
   } else {
-    k_classify<0, kEmit, kMode><<<grid_for_threads(c, m, 1024, 2), 1024, 0, c->stream>>>(t, m, go, r, c->d_flags, c->d_tail,
-                                                                                   c->d_tail_n, ag, e);
+    k_classify<0, kEmit, kMode, kNarrow><<<grid_for_threads(c, m, 1024, 2), 1024, 0, c->stream>>>(
+        t, m, go, r, c->d_flags, c->d_tail, c->d_tail_n, ag, e);
   }
 }
 
@@ -3042,12 +3089,18 @@ template <bool kEmit>
 int launch_classify_t(rsa_ctx* c, const uint4* t, uint64_t m, int32_t* go, const Emit& e) {
   const Rules r = rules_of(c);
   const Agg ag = agg_of(c);
+  // the pruning tables' slot width is a kernel variant: every table narrow
+  // (the common case) or each table deciding its own
   if (c->bkt_index) {
-    launch_classify_img<kEmit, 2>(c, t, m, go, r, ag, e);
+    launch_classify_img<kEmit, 2, false>(c, t, m, go, r, ag, e);
+  } else if (c->group_tasks && c->prune_narrow) {
+    launch_classify_img<kEmit, 1, true>(c, t, m, go, r, ag, e);
   } else if (c->group_tasks) {
-    launch_classify_img<kEmit, 1>(c, t, m, go, r, ag, e);
+    launch_classify_img<kEmit, 1, false>(c, t, m, go, r, ag, e);
+  } else if (c->prune_narrow) {
+    launch_classify_img<kEmit, 0, true>(c, t, m, go, r, ag, e);
   } else {
-    launch_classify_img<kEmit, 0>(c, t, m, go, r, ag, e);
+    launch_classify_img<kEmit, 0, false>(c, t, m, go, r, ag, e);
   }
   HIPCHK(c, hipGetLastError());
   // deferred lines (their number is read on the device: no host sync)
@@ -3541,27 +3594,29 @@ int rsa_load_rules(rsa_ctx* c, const rsa_rule_entry* h_entries, uint32_t n_entri
 
 namespace {
 
-// A 16-bit-slot CHD table inside the image whose slot values are all < `limit`.
+// A 16-bit-slot pruning table inside the image whose slot values are all <
+// `limit` (the record's bitmap count; an empty slot is 0, bitmap 0).
 bool table16_ok(const uint32_t* img, uint32_t words, const rsa_pht_table& t, uint32_t limit) {
   if (t.n_slots == 0 || t.n_slots > 0x10000u || (uint64_t)t.slot_off + t.n_slots > 2ull * words || (t.disp_mask & (t.disp_mask + 1)) != 0 ||
-      (uint64_t)t.disp_off + t.disp_mask + 1 > 2ull * words || limit > 0xFFu)
+      (uint64_t)t.disp_off + t.disp_mask + 1 > 2ull * words || limit == 0 || limit > 0x100u)
     return false;
   const uint16_t* h = reinterpret_cast<const uint16_t*>(img);
-  for (uint32_t q = 0; q < t.n_slots; ++q) {
-    const uint32_t w = h[t.slot_off + q];
-    if (w != 0xFFFFu && (w & 0xFFu) >= limit) return false;
-  }
+  for (uint32_t q = 0; q < t.n_slots; ++q)
+    if ((h[t.slot_off + q] & 0xFFu) >= limit) return false;
   return true;
 }
 
-// A CHD table inside the image whose slot values are all < `limit`.
-bool table_ok(const uint32_t* img, uint32_t words, const rsa_pht_table& t, uint32_t limit) {
+// A CHD table inside the image whose slot values are all < `limit`; `empty`:
+// the empty slot word (0xFFFFFFFF in the group tables, 0 in the pruning
+// tables, whose value 0 is a valid index: bitmap 0).
+bool table_ok(const uint32_t* img, uint32_t words, const rsa_pht_table& t, uint32_t limit,
+              uint32_t empty = 0xFFFFFFFFu) {
   if (t.n_slots == 0 || t.n_slots > 0x10000u || (uint64_t)t.slot_off + t.n_slots > words || (t.disp_mask & (t.disp_mask + 1)) != 0 ||
-      (uint64_t)t.disp_off + t.disp_mask + 1 > 2ull * words)
+      (uint64_t)t.disp_off + t.disp_mask + 1 > 2ull * words || limit == 0)
     return false;
   for (uint32_t q = 0; q < t.n_slots; ++q) {
     const uint32_t w = img[t.slot_off + q];
-    if (w != 0xFFFFFFFFu && (w & 0xFFFFu) >= limit) return false;
+    if (w != empty && (w & 0xFFFFu) >= limit) return false;
   }
   return true;
 }
@@ -3657,7 +3712,10 @@ int rsa_load_index(rsa_ctx* c, const uint32_t* img, uint32_t words, const rsa_ru
           rsa_pht_mask M;
           memcpy(&M, img + h.mask_off + (size_t)mw * m, sizeof M);
           const rsa_pht_table T = {M.slot & ~RSA_PHT_NARROW, M.disp_off, M.size & 0x1FFFFu, M.size >> 17};
-          if ((M.slot & RSA_PHT_NARROW) ? !table16_ok(img, words, T, h.n_bitmaps) : !table_ok(img, words, T, h.n_bitmaps))
+          if (!(M.slot & RSA_PHT_NARROW) && (img[5] & 2u))
+            return fail(c, RSA_ERR_ARG, "list %u mask %u: 32-bit slots in an image flagged all-narrow", l, m);
+          if ((M.slot & RSA_PHT_NARROW) ? !table16_ok(img, words, T, h.n_bitmaps)
+                                        : !table_ok(img, words, T, h.n_bitmaps, 0u))
             return fail(c, RSA_ERR_ARG, "list %u mask %u: table outside the image or bitmap out of range", l, m);
         }
       }
@@ -3682,6 +3740,7 @@ int rsa_load_index(rsa_ctx* c, const uint32_t* img, uint32_t words, const rsa_ru
   c->index_loaded = true;
   c->bkt_index = bkt;
   c->bkt_filters = bkt && (img[5] & 1u);
+  c->prune_narrow = !bkt && (img[5] & 2u);
   c->indexed = true;
   return RSA_OK;
 }
@@ -3998,6 +4057,21 @@ int rsa_shadowed_ports(rsa_ctx* c, const rsa_shadow_rule* h_rules, uint32_t n, c
   hipFree(d_ports);
   return rc;
 }
+
+#ifdef RSA_PHASE_PROF
+// PROFILING BUILD ONLY: the classifier's phase cycles (see PhaseAcc): out[0..7]
+// summed wave cycles per phase, out[8] wave iterations.
+int rsa_phase_prof(rsa_ctx* c, uint64_t* h_out, int reset) {
+  if (!c || !h_out) return RSA_ERR_ARG;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpyFromSymbol(h_out, HIP_SYMBOL(g_phase), 9 * sizeof(uint64_t)));
+  if (reset) {
+    const uint64_t z[9] = {};
+    HIPCHK(c, hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof z));
+  }
+  return RSA_OK;
+}
+#endif
 
 int rsa_stats(rsa_ctx* c, uint64_t* h_out, int reset) {
   if (!c || !h_out) return RSA_ERR_ARG;
