@@ -312,6 +312,9 @@ __device__ unsigned long long g_phase[9];
 
 constexpr int kAttempts = 4;   // compile.py PHT_ATTEMPTS
 constexpr uint32_t kListWords = 20, kGroupWords = 20, kMaskWords = 4;
+#ifndef RSA_PREFETCH_T
+#define RSA_PREFETCH_T 0   // A/B builds: load the next tuple one iteration ahead
+#endif
 
 // Pruning stage of the index lookup for ONE lane (compile.py pht_lookup): each
 // src/dst mask table maps the masked address to a bitmap of the groups holding
@@ -1068,11 +1071,14 @@ __device__ __forceinline__ bool make_rec(uint32_t i, uint4 t, uint32_t gid, cons
   const uint32_t flags = (t.w >> 16) & 0xFFu;
   bool need = gid != kNoGid && (flags & RSA_F_HIT) && (flags & RSA_F_BUILT) && A.cap > 0 && !(A.skip & 2u);
   if (!need) return false;
+  // the three loads in flight together (one memory round trip, not two)
   const unsigned long long o = E.ord[i];
-  if (o > A.filter[gid]) return false;   // exact skip: capped with threshold <= filter < order
+  const uint32_t ts = __builtin_nontemporal_load(&E.ts[i]);
+  const unsigned long long f = A.filter[gid];
+  r.ts = ts;
+  if (o > f) return false;   // exact skip: capped with threshold <= filter < order
   conn_key(t, gid, r.kA, r.kB);
   r.order = o;
-  r.ts = E.ts[i];
   r.region = key_region(A, slot_hash(r.kA, r.kB));
   return true;
 }
@@ -1137,6 +1143,12 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kIm
   PhaseAcc ph = {};
   unsigned long long waves_seen = 0;
 #endif
+#if RSA_PREFETCH_T
+  // the next iteration's tuple is loaded before this iteration's stores, so
+  // waiting for it does not wait for them (vmcnt counts stores too)
+  uint4 t_next = blockIdx.x * blockDim.x + threadIdx.x < n32 ? T[blockIdx.x * blockDim.x + threadIdx.x]
+                                                             : make_uint4(0u, 0u, 0u, 0u);
+#endif
   for (uint32_t base = blockIdx.x * blockDim.x; base < n32; base += stride) {
 #ifdef RSA_PHASE_PROF
     ph.last = __builtin_amdgcn_s_memtime();
@@ -1144,7 +1156,12 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kIm
 #endif
     const uint32_t i = base + threadIdx.x;
     const bool in = i < n32;
+#if RSA_PREFETCH_T
+    const uint4 t = t_next;
+    t_next = i + stride < n32 ? T[i + stride] : make_uint4(0u, 0u, 0u, 0u);
+#else
     const uint4 t = in ? T[i] : make_uint4(0u, 0u, 0u, 0u);
+#endif
     const bool valid = in && (((t.w >> 16) & 0xFFu) & RSA_F_VALID);
     uint32_t gid;
     if (kImg > 0) {
@@ -3068,10 +3085,13 @@ int ensure_events(rsa_ctx* c) {
 constexpr int kImgSmall = kImgSmallMax;   // 76 KiB: two 1024-thread workgroups per CU (32 waves)
 constexpr int kImgLarge = 38912;   // 152 KiB: one workgroup per CU
 
+#ifndef RSA_FORCE_LARGE
+#define RSA_FORCE_LARGE 0   // A/B builds: every indexed launch takes the one-workgroup-per-CU image variant
+#endif
 template <bool kEmit, int kMode, bool kNarrow>
 void launch_classify_img(rsa_ctx* c, const uint4* t, uint64_t m, int32_t* go, const Rules& r, const Agg& ag,
                          const Emit& e) {
-  if (c->indexed && c->img_words <= (uint32_t)kImgSmall) {
+  if (c->indexed && c->img_words <= (uint32_t)kImgSmall && !RSA_FORCE_LARGE) {
     k_classify<kImgSmall, kEmit, kMode, kNarrow><<<grid_for_threads(c, m, 1024, 2), 1024, 0, c->stream>>>(
         t, m, go, r, c->d_flags, c->d_tail, c->d_tail_n, ag, e);
   } else if (c->indexed && c->img_words <= (uint32_t)kImgLarge) {
