@@ -1565,49 +1565,36 @@ __global__ __launch_bounds__(1024) void k_aggregate(const uint4* __restrict__ T,
 // offset.
 constexpr uint32_t kPartTileMin = 8192, kPartTileMax = 262144, kPartTilesWant = 384;
 
-// Both partition kernels walk their tile as groups of kPartW windows per wave
-// iteration: lanes 0..kPartW-1 read the window counts (one coalesced load),
-// their prefix sums are broadcast as scalars, and the group's live records
-// are dealt densely to the lanes (record q -> window k = #{prefix <= q}, slot
-// q - prefix[k]), up to kPartU records per lane with every load issued before
-// the first is used: a wave keeps ~kPartU x 64 record loads in flight instead
-// of one dependent load/atomic/store chain per 64 records (the kernels are
-// memory-latency bound, not VALU bound: the window search is ~3 VALU per
-// window and record).  Tiles are multiples of 8192 lines, so a tile's first
-// window is a multiple of kPartW.
-constexpr int kPartW = 16, kPartU = 6;
+// Both partition kernels walk their tile as groups of kPartW windows per wave:
+// the group's window counts are wave-uniform (scalar) loads, and the live
+// records of the group are dealt to the lanes densely (record q of the group ->
+// window k = #{prefix <= q}, slot q - prefix[k]), so a wave does ~one pass per
+// 64 records instead of one per 64 window slots (windows are ~1/3 full).
+// Tiles are multiples of 8192 lines, so a tile's first window is a multiple of
+// kPartW.
+constexpr int kPartW = 4;
 
 struct WinGroup {
-  uint32_t pre[kPartW];   // exclusive prefix of the window counts (wave-uniform)
-  uint32_t tot;
+  uint32_t p1, p2, p3, tot;
 };
 
 __device__ __forceinline__ WinGroup win_group(const uint32_t* __restrict__ wcnt, unsigned long long w0,
                                               unsigned long long wend) {
-  const uint32_t lane = __lane_id();
-  const uint32_t c = lane < (uint32_t)kPartW && w0 + lane < wend ? wcnt[w0 + lane] : 0u;
-  uint32_t x = c;
+  uint32_t c[kPartW];
 #pragma unroll
-  for (int o = 1; o < kPartW; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o);
-    if ((int)lane >= o) x += y;
-  }
+  for (int k = 0; k < kPartW; ++k) c[k] = w0 + k < wend ? wcnt[w0 + k] : 0u;
   WinGroup g;
-#pragma unroll
-  for (int k = 0; k < kPartW; ++k) g.pre[k] = __builtin_amdgcn_readlane(x - c, k);
-  g.tot = __builtin_amdgcn_readlane(x, kPartW - 1);
+  g.p1 = c[0];
+  g.p2 = g.p1 + c[1];
+  g.p3 = g.p2 + c[2];
+  g.tot = g.p3 + c[3];
   return g;
 }
 
 // line-slot index of record q (< g.tot) of the window group starting at w0
 __device__ __forceinline__ unsigned long long win_slot(const WinGroup& g, unsigned long long w0, uint32_t q) {
-  uint32_t k = 0, pre = 0;
-#pragma unroll
-  for (int m = 1; m < kPartW; ++m) {
-    const bool ge = q >= g.pre[m];
-    k += ge ? 1u : 0u;
-    pre = ge ? g.pre[m] : pre;
-  }
+  const uint32_t k = (uint32_t)(q >= g.p1) + (uint32_t)(q >= g.p2) + (uint32_t)(q >= g.p3);
+  const uint32_t pre = k == 0 ? 0u : k == 1 ? g.p1 : k == 2 ? g.p2 : g.p3;
   return (w0 + k) * kWin + (q - pre);
 }
 
@@ -1624,16 +1611,12 @@ __global__ __launch_bounds__(1024) void k_part_hist(const uint16_t* __restrict__
   const uint32_t lane = __lane_id(), nwv = blockDim.x >> 6;
   for (unsigned long long w0 = beg / kWin + (threadIdx.x >> 6) * kPartW; w0 < wend; w0 += (unsigned long long)nwv * kPartW) {
     const WinGroup g = win_group(wcnt, w0, wend);
-    for (uint32_t q0 = 0; q0 < g.tot; q0 += kPartU * kWin) {
-      uint32_t rg[kPartU];
-#pragma unroll
-      for (int u = 0; u < kPartU; ++u) {
-        const uint32_t q = q0 + lane + u * kWin;
-        rg[u] = q < g.tot ? regs[win_slot(g, w0, q)] : 0xFFFFFFFFu;
-      }
-#pragma unroll
-      for (int u = 0; u < kPartU; ++u)
-        if (rg[u] != 0xFFFFFFFFu) atomicAdd(&hcount[rg[u]], 1u);
+    for (uint32_t q = lane; q < g.tot; q += 2 * kWin) {   // two records per lane in flight
+      const bool two = q + kWin < g.tot;
+      const uint32_t r0 = regs[win_slot(g, w0, q)];
+      const uint32_t r1 = two ? regs[win_slot(g, w0, q + kWin)] : 0u;
+      atomicAdd(&hcount[r0], 1u);
+      if (two) atomicAdd(&hcount[r1], 1u);
     }
   }
   __syncthreads();
@@ -1654,22 +1637,11 @@ __global__ __launch_bounds__(1024) void k_part_scatter(const Rec* __restrict__ r
   const uint32_t lane = __lane_id(), nwv = blockDim.x >> 6;
   for (unsigned long long w0 = beg / kWin + (threadIdx.x >> 6) * kPartW; w0 < wend; w0 += (unsigned long long)nwv * kPartW) {
     const WinGroup g = win_group(wcnt, w0, wend);
-    for (uint32_t q0 = 0; q0 < g.tot; q0 += kPartU * kWin) {
-      Rec r[kPartU];
-      uint32_t rg[kPartU];
-#pragma unroll
-      for (int u = 0; u < kPartU; ++u) {
-        const uint32_t q = q0 + lane + u * kWin;
-        rg[u] = 0xFFFFFFFFu;
-        if (q < g.tot) {
-          const unsigned long long j = win_slot(g, w0, q);
-          rg[u] = regs[j];
-          r[u] = recs[j];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < kPartU; ++u)
-        if (rg[u] != 0xFFFFFFFFu) out[atomicAdd(&cur[rg[u]], 1u)] = r[u];
+    for (uint32_t q = lane; q < g.tot; q += kWin) {
+      const unsigned long long j = win_slot(g, w0, q);
+      const uint32_t rg = regs[j];
+      const Rec r = recs[j];
+      out[atomicAdd(&cur[rg], 1u)] = r;
     }
   }
 }
