@@ -1004,11 +1004,14 @@ __device__ __forceinline__ unsigned long long table_combine(const Agg& A, unsign
 }
 
 // Find an existing key (after pass 1 completed: plain loads are coherent across
-// the kernel boundary).
+// the kernel boundary).  A slot is live only if its occupancy bit is set: the
+// slots are not cleared between jobs (rsa_reset clears the bitmap), so an
+// unoccupied slot may hold a key of an earlier job.
 __device__ __forceinline__ Slot* table_find(const Agg& A, unsigned long long kA, unsigned long long kB) {
   unsigned long long h = slot_home(A, slot_hash(kA, kB));
   for (unsigned long long probes = 0; probes < (1ull << A.rs_bits); ++probes) {
     Slot* c = &A.slots[h];
+    if (!((A.occ[h >> 5] >> (h & 31)) & 1u)) return nullptr;
     const unsigned long long cb = c->kB;
     if (cb == kEmpty) return nullptr;
     if (cb == kB && c->kA == kA) return c;
@@ -2788,6 +2791,7 @@ struct rsa_ctx {
   // hot-region split (k_hot_plan / k_hot_combine)
   int parse_mode = 0;                       // RSA_OPT_PARSE_MODE (textparse.hip)
   bool region_import = true;                // RSA_OPT_REGION_IMPORT: rsa_import by region sort + k_reduce
+  bool slots_clean = true;                  // no slot holds a key of an earlier job (k_import's CAS claims need it)
   bool hot_split = true;                    // RSA_OPT_HOT_SPLIT
   unsigned long long hot_min = kHotMinRecs; // RSA_OPT_HOT_MIN: a hot region holds more than max(hot_min,
   uint32_t hot_factor = kHotFactor;         //   hot_factor x the mean region) records
@@ -3833,13 +3837,18 @@ int rsa_reset(rsa_ctx* c, uint64_t capacity, uint32_t cap) {
     HIPCHK(c, hipGetLastError());
     c->slot_alloc = want;
     c->table_dirty = false;
-  } else if (c->table_dirty) {
-    // clear exactly the slots the previous job used (they may lie anywhere in
-    // the allocation; their number is read on the device)
+  } else if (c->table_dirty && !c->region_import) {
+    // the per-record atomic import (RSA_OPT_REGION_IMPORT=0) claims slots by
+    // CAS on an empty key: clear exactly the slots the previous job used
+    // (they may lie anywhere in the allocation; their number is read on the
+    // device).  Every other path decides occupancy by the bitmap cleared
+    // below and writes a whole slot when it claims one, so the slots keep
+    // the previous job's contents (no 64 B write per used slot per job).
     k_table_clear<<<c->cu_count * 8, kBlock, 0, c->stream>>>(c->d_slots, c->d_used, c->d_used_n, c->slot_alloc);
     HIPCHK(c, hipGetLastError());
     c->table_dirty = false;
   }
+  c->slots_clean = !c->table_dirty;
   c->slot_cap = want;
   c->cap = cap;
   HIPCHK(c, hipMemsetAsync(c->d_used_n, 0, sizeof(unsigned long long), c->stream));
@@ -3990,6 +3999,8 @@ int rsa_import(rsa_ctx* c, int which, const rsa_conn_record* in, uint64_t n) {
   if (!in) return fail(c, RSA_ERR_ARG, "null input records");
   c->table_dirty = true;
   if (!c->region_import) {
+    if (which == 0 && !c->slots_clean)
+      return fail(c, RSA_ERR_STATE, "RSA_OPT_REGION_IMPORT=0 imports need the table cleared: set it before rsa_reset");
     k_import<<<grid_for_threads(c, n, 1024, 4), 1024, 0, c->stream>>>(in, n, which, agg_of(c));
     HIPCHK(c, hipGetLastError());
     return RSA_OK;
