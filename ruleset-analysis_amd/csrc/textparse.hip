@@ -528,6 +528,97 @@ __global__ void k_compact(const uint32_t* __restrict__ ids, const uint32_t* __re
   out[slot[j]] = Act{ids[j], ngs1[j] - 1};
 }
 
+// ---- small-class finish: a class (lines equal in their first `depth` bytes,
+// contiguous in act) of at most kSmallClass lines is ranked directly: each
+// lane counts the members that sort before its line (bytes from `depth` on,
+// a prefix first, equal strings by line index), so its position is the class
+// start + that count -- no further rounds of sorts for it.  After the first
+// live window nearly every class is small (lines of one rule that share a
+// second), so the global rounds stop early.
+constexpr uint32_t kSmallClass = 64;
+
+// 8 bytes of a line from byte p of the text, big-endian, zero past `rem`
+// (rem >= 1 bytes of the line remain at p); text is 4-byte aligned.
+__device__ __forceinline__ uint64_t line_chunk8(const uint8_t* __restrict__ text, uint64_t n_bytes, uint64_t p,
+                                                uint32_t rem) {
+  uint64_t k;
+  if (p + 12 <= n_bytes) {
+    const uint32_t* t32 = reinterpret_cast<const uint32_t*>(text);
+    const uint64_t q = p >> 2;
+    const uint32_t sh = (uint32_t)(p & 3) * 8;
+    const uint64_t lo = (uint64_t)t32[q] | ((uint64_t)t32[q + 1] << 32);
+    const uint64_t x = sh ? (lo >> sh) | ((uint64_t)t32[q + 2] << (64 - sh)) : lo;
+    k = __builtin_bswap64(x);
+  } else {
+    k = 0;
+    for (uint32_t j = 0; j < 8; ++j) k = k << 8 | (p + j < n_bytes ? text[p + j] : 0u);
+  }
+  if (rem < 8) k &= ~0ull << (64 - 8 * rem);
+  return k;
+}
+
+// <0, 0, >0: line a vs line b from byte `depth` (LC_ALL=C order: bytes, then length)
+__device__ __forceinline__ int cmp_lines(const uint8_t* __restrict__ text, uint64_t n_bytes, uint64_t a, uint32_t la,
+                                         uint64_t b, uint32_t lb, uint32_t depth) {
+  for (uint32_t p = depth;; p += 8) {
+    const uint32_t ra = la > p ? la - p : 0u, rb = lb > p ? lb - p : 0u;
+    if (!ra || !rb) return (int)(ra != 0) - (int)(rb != 0);
+    const uint64_t ka = line_chunk8(text, n_bytes, a + p, ra), kb = line_chunk8(text, n_bytes, b + p, rb);
+    if (ka != kb) return ka < kb ? -1 : 1;
+    if (ra <= 8 || rb <= 8) return (int)(ra > rb) - (int)(ra < rb);
+  }
+}
+
+// per element of act: 1 + index of its class's first element at class starts, else 0
+__global__ void k_cls_first(const Act* __restrict__ act, uint32_t m, uint32_t* __restrict__ out) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  out[j] = (j == 0 || act[j].gs != act[j - 1].gs) ? j + 1 : 0u;
+}
+
+// (after the max-scan of k_cls_first): the class size, stored at its first element
+__global__ void k_cls_size(const Act* __restrict__ act, const uint32_t* __restrict__ first1, uint32_t m,
+                           uint32_t* __restrict__ size) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  if (j + 1 == m || act[j + 1].gs != act[j].gs) size[first1[j] - 1] = j + 2 - first1[j];
+}
+
+// rank every element of a small class; keep[j] = 1 for the elements of large classes
+__global__ void k_finish_small(const uint8_t* __restrict__ text, uint64_t n_bytes, const uint64_t* __restrict__ off,
+                               const uint32_t* __restrict__ lens, const Act* __restrict__ act,
+                               const uint32_t* __restrict__ first1, const uint32_t* __restrict__ size, uint32_t m,
+                               uint32_t depth, uint64_t base, uint64_t* __restrict__ order,
+                               uint32_t* __restrict__ keep) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const uint32_t cs = first1[j] - 1, cn = size[cs];
+  if (cn > kSmallClass) {
+    keep[j] = 1u;
+    return;
+  }
+  keep[j] = 0u;
+  const Act x = act[j];
+  const uint64_t a = off[x.id];
+  const uint32_t la = lens[x.id];
+  uint32_t rank = 0;
+  for (uint32_t k = cs; k < cs + cn; ++k) {
+    if (k == j) continue;
+    const uint32_t y = act[k].id;
+    const int c = cmp_lines(text, n_bytes, off[y], lens[y], a, la, depth);
+    rank += (c < 0 || (c == 0 && y < x.id)) ? 1u : 0u;
+  }
+  order[x.id] = base + x.gs + rank;
+}
+
+// compaction of the kept elements (slot: exclusive scan of keep)
+__global__ void k_compact_act(const Act* __restrict__ in, const uint32_t* __restrict__ keep,
+                              const uint32_t* __restrict__ slot, uint32_t m, Act* __restrict__ out) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m || !keep[j]) return;
+  out[slot[j]] = in[j];
+}
+
 inline uint32_t blocks(uint64_t n, uint32_t t) { return (uint32_t)((n + t - 1) / t); }
 
 struct Scratch {           // one hipMallocAsync'd arena, freed on the stream at the end
@@ -716,8 +807,8 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
   if (t_exscan > tmp) tmp = t_exscan;
   tmp = (tmp + 255) / 256 * 256;
   const size_t N = ((size_t)n + 63) / 64 * 64;
-  // keysA/keysB u64, valsA/valsB u64, gs/ids/first/pos/bstart/keep/slot u32, act/act2 Act, count
-  const size_t bytes = tmp + N * (8 * 4 + 4 * 8 + 8 * 2) + 256;
+  // keysA/keysB u64, valsA/valsB u64, gs/ids/first/pos/bstart/keep/slot u32, act/act2/act3 Act, count
+  const size_t bytes = tmp + N * (8 * 4 + 4 * 8 + 8 * 3) + 256;
   Scratch S{c, st};
   TPCHK(c, hipMallocAsync(&S.base, bytes, st));
   char* p = static_cast<char*>(S.base);
@@ -736,6 +827,7 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
   uint32_t* slot = reinterpret_cast<uint32_t*>(p); p += N * 4;
   Act* act = reinterpret_cast<Act*>(p); p += N * 8;
   Act* act2 = reinterpret_cast<Act*>(p); p += N * 8;
+  Act* act3 = reinterpret_cast<Act*>(p); p += N * 8;
   uint32_t* lens = reinterpret_cast<uint32_t*>(p); p += N * 4;
   uint32_t* idsA = reinterpret_cast<uint32_t*>(valsA);   // round 0 reuses the value arrays as u32 ids
   uint32_t* idsB = reinterpret_cast<uint32_t*>(valsB);
@@ -781,6 +873,28 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
   m += lastk;
   uint32_t* live = reinterpret_cast<uint32_t*>(act2);   // act2 is spare: one flag word
   for (uint32_t round = round0; m > 0; ++round) {
+    // the classes of at most kSmallClass lines are ranked here (their lines
+    // agree on bytes [0, 7 * round)); the others go on to the next round
+    hipLaunchKernelGGL(k_cls_first, dim3(blocks(m, 256)), dim3(256), 0, st, act, m, bstart);
+    tt = tmp;
+    TPCHK(c, rocprim::inclusive_scan(t, tt, bstart, first, (size_t)m, rocprim::maximum<uint32_t>(), st));
+    hipLaunchKernelGGL(k_cls_size, dim3(blocks(m, 256)), dim3(256), 0, st, act, first, m, pos);
+    hipLaunchKernelGGL(k_finish_small, dim3(blocks(m, 256)), dim3(256), 0, st, d_text, n_bytes, d_off, lens, act,
+                       first, pos, m, 7u * round, base, d_order, keep);
+    tt = tmp;
+    TPCHK(c, rocprim::exclusive_scan(t, tt, keep, slot, 0u, (size_t)m, rocprim::plus<uint32_t>(), st));
+    hipLaunchKernelGGL(k_compact_act, dim3(blocks(m, 256)), dim3(256), 0, st, act, keep, slot, m, act3);
+    {
+      uint32_t nm = 0;
+      TPCHK(c, hipMemcpyAsync(&nm, slot + m - 1, 4, hipMemcpyDeviceToHost, st));
+      TPCHK(c, hipMemcpyAsync(&lastk, keep + m - 1, 4, hipMemcpyDeviceToHost, st));
+      TPCHK(c, hipStreamSynchronize(st));
+      m = nm + lastk;
+      Act* sw = act;
+      act = act3;
+      act3 = sw;
+    }
+    if (m == 0) break;
     hipLaunchKernelGGL(k_keys, dim3(blocks(m, 256)), dim3(256), 0, st, d_text, d_off, lens, n_bytes, act, m, round,
                        keysA, valsA);
     // rounds inside a shared prefix (e.g. lines of one second share ~90 bytes)
