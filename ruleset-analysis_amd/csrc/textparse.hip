@@ -16,8 +16,10 @@
 //   order keys                the rank of each line's bytes (LC_ALL=C sort of
 //                             the mapper stream, runAnalysis.sh:42-56): 7-byte
 //                             big-endian chunks + a length field, groups of
-//                             equal prefixes refined by stable radix sorts
-//                             (rocPRIM) until every line is settled.
+//                             equal prefixes refined by stable LSD radix sorts
+//                             (k_rs_*, hand-written) over the key bits that
+//                             vary; classes of <= 64 lines ranked directly
+//                             by string comparison (k_finish_small).
 //
 // Anything outside the canonical grammar is marked RSA_LINE_HOST: the host
 // parser (logparse._parse_one) decides those lines, so every error the
@@ -28,9 +30,6 @@
 #include <cstring>
 #include <string>
 
-#include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/device/device_reduce.hpp>
-#include <rocprim/device/device_scan.hpp>
 
 #include "../../include/ruleset_hip.h"
 #include "rsa_internal.h"
@@ -406,7 +405,7 @@ __global__ void k_keys0(const uint8_t* __restrict__ text, const uint64_t* __rest
 // sort key (a negative group -- a line no rank is asked for -- sorts last as
 // 0xFFFFFFFF) and its id.
 __global__ void k_grp0(const int32_t* __restrict__ group, const uint8_t* __restrict__ text,
-                       const uint64_t* __restrict__ off, uint32_t n, uint32_t* __restrict__ lens,
+                       const uint64_t* __restrict__ off, uint32_t n, uint32_t none, uint32_t* __restrict__ lens,
                        uint32_t* __restrict__ keys, uint32_t* __restrict__ ids) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
@@ -415,8 +414,19 @@ __global__ void k_grp0(const int32_t* __restrict__ group, const uint8_t* __restr
   if (len && text[b - 1] == '\n') --len;
   lens[j] = len < 0xFFFFFFFFull ? (uint32_t)len : 0xFFFFFFFFu;
   const int32_t g = group[j];
-  keys[j] = g < 0 ? 0xFFFFFFFFu : (uint32_t)g;
+  keys[j] = g < 0 ? none : (uint32_t)g;
   ids[j] = j;
+}
+
+// the largest group (atomicMax into *mx, zeroed by the caller)
+__global__ void k_grp_max(const int32_t* __restrict__ group, uint32_t n, uint32_t* __restrict__ mx) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  int32_t g = j < n ? group[j] : 0;
+  for (int o = 32; o > 0; o >>= 1) {
+    const int32_t y = __shfl_xor(g, o);
+    g = y > g ? y : g;
+  }
+  if (__lane_id() == 0 && g > 0) atomicMax(mx, (uint32_t)g);
 }
 
 // after the sort by group: group starts (+1, max-scanned by the caller)
@@ -428,12 +438,12 @@ __global__ void k_grp_bounds(const uint32_t* __restrict__ keys, uint32_t m, uint
 
 // a line alone in its group, or without a group, is settled at its position
 __global__ void k_grp_settle(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ ids,
-                             const uint32_t* __restrict__ first, uint32_t m, uint64_t base, uint64_t* __restrict__ order,
-                             uint32_t* __restrict__ keep) {
+                             const uint32_t* __restrict__ first, uint32_t m, uint32_t none, uint64_t base,
+                             uint64_t* __restrict__ order, uint32_t* __restrict__ keep) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= m) return;
   const bool last_in_group = j + 1 == m || keys[j + 1] != keys[j];
-  const bool settled = keys[j] == 0xFFFFFFFFu || (first[j] == j + 1 && last_in_group);
+  const bool settled = keys[j] == none || (first[j] == j + 1 && last_in_group);
   if (settled) order[ids[j]] = base + j;
   keep[j] = settled ? 0u : 1u;
 }
@@ -454,13 +464,27 @@ __global__ void k_keys(const uint8_t* __restrict__ text, const uint64_t* __restr
 
 // 1 if this round can change anything: a group whose keys differ, or a line
 // that ends in this window (else the round is skipped: no sort, no settle)
+// live[1..2]: the OR over all keys of (key ^ keys[0]) -- the bits that vary
+// this round; the sort then runs over those bits only
 __global__ void k_round_live(const uint64_t* __restrict__ keys, const Act* __restrict__ act, uint32_t m,
                              uint32_t* __restrict__ live) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= m) return;
-  const bool ended = (keys[j] & 0xFFu) < 8u;
-  const bool split = j > 0 && act[j].gs == act[j - 1].gs && keys[j] != keys[j - 1];
-  if (ended || split) *live = 1u;
+  uint64_t d = 0;
+  if (j < m) {
+    const bool ended = (keys[j] & 0xFFu) < 8u;
+    const bool split = j > 0 && act[j].gs == act[j - 1].gs && keys[j] != keys[j - 1];
+    if (ended || split) live[0] = 1u;
+    d = keys[j] ^ keys[0];
+  }
+  uint32_t lo = (uint32_t)d, hi = (uint32_t)(d >> 32);
+  for (int o = 32; o > 0; o >>= 1) {
+    lo |= (uint32_t)__shfl_xor((int)lo, o);
+    hi |= (uint32_t)__shfl_xor((int)hi, o);
+  }
+  if (__lane_id() == 0) {
+    if (lo) atomicOr(&live[1], lo);
+    if (hi) atomicOr(&live[2], hi);
+  }
 }
 
 __global__ void k_gs_iota(const uint64_t* __restrict__ vals, uint32_t m, uint32_t* __restrict__ gs,
@@ -621,6 +645,244 @@ __global__ void k_compact_act(const Act* __restrict__ in, const uint32_t* __rest
 
 inline uint32_t blocks(uint64_t n, uint32_t t) { return (uint32_t)((n + t - 1) / t); }
 
+// ---- scans and the LSD radix sort of the order keys (hand-written) ----------
+// Scans: kScanTile elements per workgroup (1024 threads x 4), the tile sums
+// scanned by one workgroup, then added back.  Max-scans are inclusive (group
+// starts), plus-scans inclusive or exclusive.
+constexpr uint32_t kScanThreads = 1024, kScanPer = 4, kScanTile = kScanThreads * kScanPer;
+
+struct OpPlus {
+  template <typename T>
+  __device__ static T f(T a, T b) { return a + b; }
+  template <typename T>
+  __device__ static T id() { return 0; }
+};
+struct OpMax {
+  template <typename T>
+  __device__ static T f(T a, T b) { return a > b ? a : b; }
+  template <typename T>
+  __device__ static T id() { return 0; }
+};
+
+// workgroup scan of one value per thread (Op commutative: + or max): this
+// thread's exclusive and inclusive values and the workgroup total
+template <typename Op, typename T>
+__device__ __forceinline__ void wg_scan(T v, T* sh, T& excl, T& incl, T& total) {
+  const uint32_t lane = __lane_id(), w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  T x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const T y = __shfl_up(x, o);
+    if ((int)lane >= o) x = Op::f(x, y);
+  }
+  T xe = __shfl_up(x, 1);
+  if (lane == 0) xe = Op::template id<T>();
+  if (lane == 63) sh[w] = x;
+  __syncthreads();
+  T before = Op::template id<T>(), all = Op::template id<T>();
+  for (uint32_t q = 0; q < nw; ++q) {
+    const T t = sh[q];
+    if (q < w) before = Op::f(before, t);
+    all = Op::f(all, t);
+  }
+  __syncthreads();
+  incl = Op::f(before, x);
+  excl = Op::f(before, xe);
+  total = all;
+}
+
+// pass 1: per tile, the scan inside the tile (out) and the tile's total
+template <typename Op, bool kIncl, typename Tin, typename Tout>
+__global__ __launch_bounds__(kScanThreads) void k_scan_tiles(const Tin* __restrict__ in, Tout* __restrict__ out,
+                                                             uint64_t n, Tout* __restrict__ sums) {
+  __shared__ Tout sh[16];
+  const uint64_t beg = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanPer;
+  Tout v[kScanPer];
+  Tout c = Op::template id<Tout>();
+#pragma unroll
+  for (uint32_t k = 0; k < kScanPer; ++k) {
+    v[k] = beg + k < n ? (Tout)in[beg + k] : Op::template id<Tout>();
+    c = Op::f(c, v[k]);
+  }
+  Tout ex, inc, total;
+  wg_scan<Op>(c, sh, ex, inc, total);
+  Tout run = ex;
+#pragma unroll
+  for (uint32_t k = 0; k < kScanPer; ++k) {
+    const Tout nx = Op::f(run, v[k]);
+    if (beg + k < n) out[beg + k] = kIncl ? nx : run;
+    run = nx;
+  }
+  if (threadIdx.x == 0) sums[blockIdx.x] = total;
+}
+
+// pass 2: one workgroup scans the tile totals in place (exclusive), the
+// grand total into sums[nb]
+template <typename Op, typename T>
+__global__ __launch_bounds__(kScanThreads) void k_scan_tile_sums(T* __restrict__ sums, uint32_t nb) {
+  __shared__ T sh[16];
+  T carry = Op::template id<T>();
+  for (uint32_t b0 = 0; b0 < nb; b0 += blockDim.x) {
+    const uint32_t j = b0 + threadIdx.x;
+    const T v = j < nb ? sums[j] : Op::template id<T>();
+    T ex, inc, total;
+    wg_scan<Op>(v, sh, ex, inc, total);
+    if (j < nb) sums[j] = Op::f(carry, ex);
+    carry = Op::f(carry, total);
+  }
+  if (threadIdx.x == 0) sums[nb] = carry;
+}
+
+// pass 3: add each tile's exclusive prefix
+template <typename Op, typename Tout>
+__global__ __launch_bounds__(kScanThreads) void k_scan_tiles_add(Tout* __restrict__ out, uint64_t n,
+                                                                 const Tout* __restrict__ sums) {
+  const uint64_t beg = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanPer;
+  const Tout add = sums[blockIdx.x];
+#pragma unroll
+  for (uint32_t k = 0; k < kScanPer; ++k)
+    if (beg + k < n) out[beg + k] = Op::f(add, out[beg + k]);
+}
+
+// sum of n uint32 into *total (uint64, zeroed by the caller): one device atomic per workgroup
+__global__ __launch_bounds__(kScanThreads) void k_sum_u32(const uint32_t* __restrict__ in, uint64_t n,
+                                                          unsigned long long* __restrict__ total) {
+  __shared__ unsigned long long sh[16];
+  const uint64_t beg = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanPer;
+  unsigned long long c = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kScanPer; ++k) c += beg + k < n ? in[beg + k] : 0u;
+  unsigned long long ex, inc, all;
+  wg_scan<OpPlus>(c, sh, ex, inc, all);
+  if (threadIdx.x == 0 && all) atomicAdd(total, all);
+}
+
+// LSD radix sort of (key, value) pairs, 8-bit digits: per pass a digit
+// histogram per tile of kRsTile elements (bin-major, so its exclusive scan is
+// every (digit, tile) run's output offset), then a stable scatter: a tile is
+// walked row by row (one element per thread), each lane ranked among the
+// earlier lanes of its wave with the same digit (eight ballots), the waves'
+// digit counts turned into output bases in LDS.  Only the bits [b0, b1) the
+// caller asks for are sorted (bits outside them must be equal in every key,
+// or be allowed to order ties).
+constexpr uint32_t kRsThreads = 1024, kRsRows = 8, kRsTile = kRsThreads * kRsRows;
+
+__device__ __forceinline__ unsigned long long match_digit(uint32_t d, bool valid) {
+  unsigned long long peers = __ballot(valid);
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    const unsigned long long bb = __ballot(valid && ((d >> b) & 1u));
+    peers &= ((d >> b) & 1u) ? bb : ~bb;
+  }
+  return valid ? peers : 0ull;
+}
+
+template <typename K>
+__global__ __launch_bounds__(kRsThreads) void k_rs_hist(const K* __restrict__ keys, uint32_t n, uint32_t shift,
+                                                        uint32_t n_tiles, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[256];
+  if (threadIdx.x < 256) h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x * kRsTile;
+  const uint32_t lane = __lane_id();
+  for (uint32_t r = 0; r < kRsRows; ++r) {
+    const uint64_t i = base + (uint64_t)r * kRsThreads + threadIdx.x;
+    const bool valid = i < n;
+    const uint32_t d = valid ? (uint32_t)(keys[i] >> shift) & 255u : 0u;
+    const unsigned long long peers = match_digit(d, valid);   // one LDS atomic per distinct digit of the wave
+    if (valid && __popcll(peers & ((1ull << lane) - 1ull)) == 0) atomicAdd(&h[d], (uint32_t)__popcll(peers));
+  }
+  __syncthreads();
+  if (threadIdx.x < 256) hist[(size_t)threadIdx.x * n_tiles + blockIdx.x] = h[threadIdx.x];
+}
+
+template <typename K, typename V>
+__global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const K* __restrict__ kin, const V* __restrict__ vin,
+                                                           K* __restrict__ kout, V* __restrict__ vout, uint32_t n,
+                                                           uint32_t shift, uint32_t n_tiles,
+                                                           const uint32_t* __restrict__ offs) {
+  __shared__ uint32_t run[256];                       // next output position per digit
+  __shared__ uint32_t wc[kRsThreads / 64][256];       // the row's per-wave digit counts, then their output bases
+  const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
+  if (threadIdx.x < 256) run[threadIdx.x] = offs[(size_t)threadIdx.x * n_tiles + blockIdx.x];
+  const uint64_t base = (uint64_t)blockIdx.x * kRsTile;
+  for (uint32_t r = 0; r < kRsRows; ++r) {
+    for (uint32_t q = threadIdx.x; q < (kRsThreads / 64) * 256; q += kRsThreads) (&wc[0][0])[q] = 0;
+    __syncthreads();
+    const uint64_t i = base + (uint64_t)r * kRsThreads + threadIdx.x;
+    const bool valid = i < n;
+    const K k = valid ? kin[i] : K(0);
+    const V v = valid ? vin[i] : V(0);
+    const uint32_t d = (uint32_t)(k >> shift) & 255u;
+    const unsigned long long peers = match_digit(d, valid);
+    const uint32_t rank = __popcll(peers & ((1ull << lane) - 1ull));
+    if (valid && rank == 0) wc[w][d] = __popcll(peers);
+    __syncthreads();
+    if (threadIdx.x < 256) {
+      uint32_t x = run[threadIdx.x];
+      for (uint32_t q = 0; q < kRsThreads / 64; ++q) {
+        const uint32_t cnt = wc[q][threadIdx.x];
+        wc[q][threadIdx.x] = x;
+        x += cnt;
+      }
+      run[threadIdx.x] = x;
+    }
+    __syncthreads();
+    if (valid) {
+      const uint32_t pos = wc[w][d] + rank;
+      kout[pos] = k;
+      vout[pos] = v;
+    }
+    __syncthreads();   // wc is cleared for the next row
+  }
+}
+
+// host: scan of n elements (sums: >= n / kScanTile + 2 elements of Tout; the
+// plus-scans leave the grand total in sums[n_tiles])
+template <typename Op, bool kIncl, typename Tin, typename Tout>
+void scan(hipStream_t st, const Tin* in, Tout* out, uint64_t n, Tout* sums) {
+  if (!n) return;
+  const uint32_t nb = (uint32_t)((n + kScanTile - 1) / kScanTile);
+  hipLaunchKernelGGL((k_scan_tiles<Op, kIncl, Tin, Tout>), dim3(nb), dim3(kScanThreads), 0, st, in, out, n, sums);
+  hipLaunchKernelGGL((k_scan_tile_sums<Op, Tout>), dim3(1), dim3(kScanThreads), 0, st, sums, nb);
+  hipLaunchKernelGGL((k_scan_tiles_add<Op, Tout>), dim3(nb), dim3(kScanThreads), 0, st, out, n, sums);
+}
+
+inline size_t scan_sums_len(uint64_t n) { return (size_t)((n + kScanTile - 1) / kScanTile) + 2; }
+
+// scratch of radix_pairs for n elements: hist (256 per tile) and its scan sums
+inline size_t rs_hist_len(uint64_t n) { return (size_t)256 * ((n + kRsTile - 1) / kRsTile); }
+
+// host: stable sort of (kA, vA) by key bits [b0, b1) into (kB, vB); (kT, vT)
+// is ping-pong space, hist / sums scratch (rs_hist_len, scan_sums_len of it)
+template <typename K, typename V>
+void radix_pairs(hipStream_t st, const K* kA, K* kB, const V* vA, V* vB, uint32_t n, uint32_t b0, uint32_t b1,
+                 K* kT, V* vT, uint32_t* hist, uint32_t* sums) {
+  if (!n) return;
+  const uint32_t passes = b1 > b0 ? (b1 - b0 + 7) / 8 : 0u;
+  if (!passes) {
+    (void)hipMemcpyAsync(kB, kA, (size_t)n * sizeof(K), hipMemcpyDeviceToDevice, st);
+    (void)hipMemcpyAsync(vB, vA, (size_t)n * sizeof(V), hipMemcpyDeviceToDevice, st);
+    return;
+  }
+  const uint32_t n_tiles = (n + kRsTile - 1) / kRsTile;
+  const K* ks = kA;
+  const V* vs = vA;
+  for (uint32_t p = 0; p < passes; ++p) {
+    const bool to_b = ((passes - 1 - p) & 1u) == 0u;   // the last pass writes (kB, vB)
+    K* kd = to_b ? kB : kT;
+    V* vd = to_b ? vB : vT;
+    const uint32_t shift = b0 + 8 * p;
+    hipLaunchKernelGGL((k_rs_hist<K>), dim3(n_tiles), dim3(kRsThreads), 0, st, ks, n, shift, n_tiles, hist);
+    scan<OpPlus, false, uint32_t, uint32_t>(st, hist, hist, (uint64_t)256 * n_tiles, sums);
+    hipLaunchKernelGGL((k_rs_scatter<K, V>), dim3(n_tiles), dim3(kRsThreads), 0, st, ks, vs, kd, vd, n, shift, n_tiles,
+                       hist);
+    ks = kd;
+    vs = vd;
+  }
+}
+
+
+
 struct Scratch {           // one hipMallocAsync'd arena, freed on the stream at the end
   rsa_ctx* c;
   hipStream_t st;
@@ -643,17 +905,16 @@ int rsa_text_count_lines(rsa_ctx* c, const uint8_t* d_text, uint64_t n, uint64_t
   if (nb > 0xFFFFFFFFull) return rsa_internal_fail(c, RSA_ERR_ARG, "text too large");
   const int aligned = (reinterpret_cast<uintptr_t>(d_text) & 15u) == 0;
   Scratch S{c, st};
-  size_t tmp = 0;
-  TPCHK(c, rocprim::reduce(nullptr, tmp, (uint32_t*)nullptr, (uint64_t*)nullptr, (uint64_t)0, (size_t)nb,
-                           rocprim::plus<uint64_t>(), st));
-  const size_t need = nb * 4 + 16 + tmp + 256;
+  const size_t need = nb * 4 + 16 + 256;
   TPCHK(c, hipMallocAsync(&S.base, need, st));
   uint32_t* counts = static_cast<uint32_t*>(S.base);
-  uint64_t* total = reinterpret_cast<uint64_t*>(static_cast<char*>(S.base) + ((nb * 4 + 15) / 16) * 16);
-  void* t = reinterpret_cast<char*>(total) + 16;
+  unsigned long long* total =
+      reinterpret_cast<unsigned long long*>(static_cast<char*>(S.base) + ((nb * 4 + 15) / 16) * 16);
+  TPCHK(c, hipMemsetAsync(total, 0, 8, st));
   hipLaunchKernelGGL(k_nl_count, dim3((uint32_t)nb), dim3(kSplitThreads), 0, st, d_text, n, aligned, counts);
+  hipLaunchKernelGGL(k_sum_u32, dim3((uint32_t)((nb + kScanTile - 1) / kScanTile)), dim3(kScanThreads), 0, st,
+                     counts, nb, total);
   TPCHK(c, hipGetLastError());
-  TPCHK(c, rocprim::reduce(t, tmp, counts, total, (uint64_t)0, (size_t)nb, rocprim::plus<uint64_t>(), st));
   uint64_t h_total = 0;
   uint8_t last = 0;
   TPCHK(c, hipMemcpyAsync(&h_total, total, 8, hipMemcpyDeviceToHost, st));
@@ -672,16 +933,13 @@ int rsa_text_line_offsets(rsa_ctx* c, const uint8_t* d_text, uint64_t n, uint64_
     if (nb > 0xFFFFFFFFull) return rsa_internal_fail(c, RSA_ERR_ARG, "text too large");
     const int aligned = (reinterpret_cast<uintptr_t>(d_text) & 15u) == 0;
     Scratch S{c, st};
-    size_t tmp = 0;
-    TPCHK(c, rocprim::inclusive_scan(nullptr, tmp, (uint32_t*)nullptr, (uint64_t*)nullptr, (size_t)nb,
-                                     rocprim::plus<uint64_t>(), st));
     const size_t cnt_bytes = ((nb * 4 + 15) / 16) * 16;
-    TPCHK(c, hipMallocAsync(&S.base, cnt_bytes + nb * 8 + tmp + 256, st));
+    TPCHK(c, hipMallocAsync(&S.base, cnt_bytes + nb * 8 + scan_sums_len(nb) * 8 + 256, st));
     uint32_t* counts = static_cast<uint32_t*>(S.base);
     uint64_t* incl = reinterpret_cast<uint64_t*>(static_cast<char*>(S.base) + cnt_bytes);
-    void* t = incl + nb;
+    uint64_t* sums = incl + nb;
     hipLaunchKernelGGL(k_nl_count, dim3((uint32_t)nb), dim3(kSplitThreads), 0, st, d_text, n, aligned, counts);
-    TPCHK(c, rocprim::inclusive_scan(t, tmp, counts, incl, (size_t)nb, rocprim::plus<uint64_t>(), st));
+    scan<OpPlus, true, uint32_t, uint64_t>(st, counts, incl, nb, sums);
     hipLaunchKernelGGL(k_nl_write, dim3((uint32_t)nb), dim3(kSplitThreads), 0, st, d_text, n, aligned, counts, incl,
                        d_off, n_lines);
     TPCHK(c, hipGetLastError());
@@ -786,38 +1044,22 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
   if (!n_lines) return RSA_OK;
   hipStream_t st = rsa_internal_stream(c);
   const uint32_t n = (uint32_t)n_lines;
-  // temp sizes of every primitive at the largest size
-  size_t t_sort64 = 0, t_sort0 = 0, t_sort32 = 0, t_scan = 0, t_exscan = 0;
-  unsigned gbits = 1;
+  unsigned gbits = 1;   // bits of a position (< n)
   while (gbits < 32 && (1ull << gbits) < (uint64_t)n) ++gbits;
-  TPCHK(c, rocprim::radix_sort_pairs(nullptr, t_sort0, (uint64_t*)nullptr, (uint64_t*)nullptr, (uint32_t*)nullptr,
-                                     (uint32_t*)nullptr, (size_t)n, 0, 64, st));
-  TPCHK(c, rocprim::radix_sort_pairs(nullptr, t_sort64, (uint64_t*)nullptr, (uint64_t*)nullptr, (uint64_t*)nullptr,
-                                     (uint64_t*)nullptr, (size_t)n, 0, 64, st));
-  TPCHK(c, rocprim::radix_sort_pairs(nullptr, t_sort32, (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                     (uint32_t*)nullptr, (size_t)n, 0, 32, st));
-  TPCHK(c, rocprim::inclusive_scan(nullptr, t_scan, (uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)n,
-                                   rocprim::maximum<uint32_t>(), st));
-  TPCHK(c, rocprim::exclusive_scan(nullptr, t_exscan, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u, (size_t)n,
-                                   rocprim::plus<uint32_t>(), st));
-  size_t tmp = t_sort64;
-  if (t_sort0 > tmp) tmp = t_sort0;
-  if (t_sort32 > tmp) tmp = t_sort32;
-  if (t_scan > tmp) tmp = t_scan;
-  if (t_exscan > tmp) tmp = t_exscan;
-  tmp = (tmp + 255) / 256 * 256;
   const size_t N = ((size_t)n + 63) / 64 * 64;
-  // keysA/keysB u64, valsA/valsB u64, gs/ids/first/pos/bstart/keep/slot u32, act/act2/act3 Act, count
-  const size_t bytes = tmp + N * (8 * 4 + 4 * 8 + 8 * 3) + 256;
+  const size_t H = rs_hist_len(N), SL = scan_sums_len(H > N ? H : N);
+  // keysA/keysB/keysT u64, valsA/valsB/valsT u64, gs/ids/first/pos/bstart/keep/slot/lens u32,
+  // act/act3 Act (and a spare), radix histogram + scan sums, flag words
+  const size_t bytes = N * (8 * 6 + 4 * 8 + 8 * 3) + (H + SL) * 4 + 512;
   Scratch S{c, st};
   TPCHK(c, hipMallocAsync(&S.base, bytes, st));
   char* p = static_cast<char*>(S.base);
-  void* t = p;
-  p += tmp;
   uint64_t* keysA = reinterpret_cast<uint64_t*>(p); p += N * 8;
   uint64_t* keysB = reinterpret_cast<uint64_t*>(p); p += N * 8;
+  uint64_t* keysT = reinterpret_cast<uint64_t*>(p); p += N * 8;
   uint64_t* valsA = reinterpret_cast<uint64_t*>(p); p += N * 8;
   uint64_t* valsB = reinterpret_cast<uint64_t*>(p); p += N * 8;
+  uint64_t* valsT = reinterpret_cast<uint64_t*>(p); p += N * 8;
   uint32_t* gs = reinterpret_cast<uint32_t*>(p); p += N * 4;
   uint32_t* ids = reinterpret_cast<uint32_t*>(p); p += N * 4;
   uint32_t* first = reinterpret_cast<uint32_t*>(p); p += N * 4;
@@ -825,64 +1067,78 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
   uint32_t* bstart = reinterpret_cast<uint32_t*>(p); p += N * 4;
   uint32_t* keep = reinterpret_cast<uint32_t*>(p); p += N * 4;
   uint32_t* slot = reinterpret_cast<uint32_t*>(p); p += N * 4;
-  Act* act = reinterpret_cast<Act*>(p); p += N * 8;
-  Act* act2 = reinterpret_cast<Act*>(p); p += N * 8;
-  Act* act3 = reinterpret_cast<Act*>(p); p += N * 8;
   uint32_t* lens = reinterpret_cast<uint32_t*>(p); p += N * 4;
-  uint32_t* idsA = reinterpret_cast<uint32_t*>(valsA);   // round 0 reuses the value arrays as u32 ids
+  Act* act = reinterpret_cast<Act*>(p); p += N * 8;
+  Act* act3 = reinterpret_cast<Act*>(p); p += N * 8;
+  uint32_t* hist = reinterpret_cast<uint32_t*>(p); p += H * 4;
+  uint32_t* sums = reinterpret_cast<uint32_t*>(p); p += SL * 4;
+  uint32_t* flags = reinterpret_cast<uint32_t*>((reinterpret_cast<uintptr_t>(p) + 63) & ~(uintptr_t)63);
+  uint32_t* idsA = reinterpret_cast<uint32_t*>(valsA);   // the first sort's values are u32 line ids
   uint32_t* idsB = reinterpret_cast<uint32_t*>(valsB);
+  uint32_t* idsT = reinterpret_cast<uint32_t*>(valsT);
+  // exclusive plus-scan of m flags (u32) into out; the count of set flags is out[m-1] + in[m-1]
+  auto exscan = [&](const uint32_t* in, uint32_t* out, uint32_t m) {
+    scan<OpPlus, false, uint32_t, uint32_t>(st, in, out, m, sums);
+  };
+  auto maxscan = [&](const uint32_t* in, uint32_t* out, uint32_t m) {
+    scan<OpMax, true, uint32_t, uint32_t>(st, in, out, m, sums);
+  };
 
   uint64_t n_bytes = 0;
   TPCHK(c, hipMemcpyAsync(&n_bytes, d_off + n, 8, hipMemcpyDeviceToHost, st));
   TPCHK(c, hipStreamSynchronize(st));
-  size_t tt = tmp;
   uint32_t round0 = 1;
   if (d_group) {
-    // grouped: ranks of (group, line bytes); the groups come first (one sort of
-    // 32-bit keys), so only lines of one group are ever compared (the reducer
-    // compares order keys of one rule's lines only), and a group of one line
-    // is settled at once.  Then the byte rounds from round 0.
+    // grouped: ranks of (group, line bytes); the groups come first (one sort
+    // over the bits a group key has), so only lines of one group are ever
+    // compared (the reducer compares order keys of one rule's lines only), and
+    // a group of one line is settled at once.  Then the byte rounds from round 0.
+    TPCHK(c, hipMemsetAsync(flags, 0, 4, st));
+    hipLaunchKernelGGL(k_grp_max, dim3(blocks(n, 256)), dim3(256), 0, st, d_group, n, flags);
+    uint32_t gmax = 0;
+    TPCHK(c, hipMemcpyAsync(&gmax, flags, 4, hipMemcpyDeviceToHost, st));
+    TPCHK(c, hipStreamSynchronize(st));
+    // group keys 0 .. gmax, a line without a group (-1) gmax + 1: last
+    unsigned kbits = 1;
+    while (kbits < 32 && (1ull << kbits) <= (uint64_t)gmax + 1) ++kbits;
     uint32_t* gkA = reinterpret_cast<uint32_t*>(keysA);
     uint32_t* gkB = reinterpret_cast<uint32_t*>(keysB);
-    hipLaunchKernelGGL(k_grp0, dim3(blocks(n, 256)), dim3(256), 0, st, d_group, d_text, d_off, n, lens, gkA, idsA);
-    TPCHK(c, rocprim::radix_sort_pairs(t, tt, gkA, gkB, idsA, idsB, (size_t)n, 0, 32, st));
+    uint32_t* gkT = reinterpret_cast<uint32_t*>(keysT);
+    hipLaunchKernelGGL(k_grp0, dim3(blocks(n, 256)), dim3(256), 0, st, d_group, d_text, d_off, n, gmax + 1, lens,
+                       gkA, idsA);
+    radix_pairs<uint32_t, uint32_t>(st, gkA, gkB, idsA, idsB, n, 0, kbits, gkT, idsT, hist, sums);
     hipLaunchKernelGGL(k_grp_bounds, dim3(blocks(n, 256)), dim3(256), 0, st, gkB, n, bstart);
-    tt = tmp;
-    TPCHK(c, rocprim::inclusive_scan(t, tt, bstart, first, (size_t)n, rocprim::maximum<uint32_t>(), st));
-    hipLaunchKernelGGL(k_grp_settle, dim3(blocks(n, 256)), dim3(256), 0, st, gkB, idsB, first, n, base, d_order,
-                       keep);
+    maxscan(bstart, first, n);
+    hipLaunchKernelGGL(k_grp_settle, dim3(blocks(n, 256)), dim3(256), 0, st, gkB, idsB, first, n, gmax + 1, base,
+                       d_order, keep);
     round0 = 0;
   } else {
     // round 0: all lines
     hipLaunchKernelGGL(k_keys0, dim3(blocks(n, 256)), dim3(256), 0, st, d_text, d_off, n, n_bytes, lens, keysA, idsA);
-    TPCHK(c, rocprim::radix_sort_pairs(t, tt, keysA, keysB, idsA, idsB, (size_t)n, 0, 64, st));
+    radix_pairs<uint64_t, uint32_t>(st, keysA, keysB, idsA, idsB, n, 0, 64, keysT, idsT, hist, sums);
     hipLaunchKernelGGL(k_bounds, dim3(blocks(n, 256)), dim3(256), 0, st, keysB, (const uint32_t*)nullptr,
                        (const uint32_t*)nullptr, n, pos, bstart);
-    tt = tmp;
-    TPCHK(c, rocprim::inclusive_scan(t, tt, bstart, first, (size_t)n, rocprim::maximum<uint32_t>(), st));
+    maxscan(bstart, first, n);
     hipLaunchKernelGGL(k_settle, dim3(blocks(n, 256)), dim3(256), 0, st, keysB, (const uint32_t*)nullptr, idsB, pos,
                        first, n, base, d_order, keep);
   }
-  tt = tmp;
-  TPCHK(c, rocprim::exclusive_scan(t, tt, keep, slot, 0u, (size_t)n, rocprim::plus<uint32_t>(), st));
+  exscan(keep, slot, n);
   hipLaunchKernelGGL(k_compact, dim3(blocks(n, 256)), dim3(256), 0, st, idsB, first, keep, slot, n, act);
   uint32_t m = 0, lastk = 0;
   TPCHK(c, hipMemcpyAsync(&m, slot + n - 1, 4, hipMemcpyDeviceToHost, st));
   TPCHK(c, hipMemcpyAsync(&lastk, keep + n - 1, 4, hipMemcpyDeviceToHost, st));
   TPCHK(c, hipStreamSynchronize(st));
   m += lastk;
-  uint32_t* live = reinterpret_cast<uint32_t*>(act2);   // act2 is spare: one flag word
+  uint32_t* live = flags;   // [0] the round splits something, [1..2] the key bits that vary
   for (uint32_t round = round0; m > 0; ++round) {
     // the classes of at most kSmallClass lines are ranked here (their lines
     // agree on bytes [0, 7 * round)); the others go on to the next round
     hipLaunchKernelGGL(k_cls_first, dim3(blocks(m, 256)), dim3(256), 0, st, act, m, bstart);
-    tt = tmp;
-    TPCHK(c, rocprim::inclusive_scan(t, tt, bstart, first, (size_t)m, rocprim::maximum<uint32_t>(), st));
+    maxscan(bstart, first, m);
     hipLaunchKernelGGL(k_cls_size, dim3(blocks(m, 256)), dim3(256), 0, st, act, first, m, pos);
     hipLaunchKernelGGL(k_finish_small, dim3(blocks(m, 256)), dim3(256), 0, st, d_text, n_bytes, d_off, lens, act,
                        first, pos, m, 7u * round, base, d_order, keep);
-    tt = tmp;
-    TPCHK(c, rocprim::exclusive_scan(t, tt, keep, slot, 0u, (size_t)m, rocprim::plus<uint32_t>(), st));
+    exscan(keep, slot, m);
     hipLaunchKernelGGL(k_compact_act, dim3(blocks(m, 256)), dim3(256), 0, st, act, keep, slot, m, act3);
     {
       uint32_t nm = 0;
@@ -898,31 +1154,33 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
     hipLaunchKernelGGL(k_keys, dim3(blocks(m, 256)), dim3(256), 0, st, d_text, d_off, lens, n_bytes, act, m, round,
                        keysA, valsA);
     // rounds inside a shared prefix (e.g. lines of one second share ~90 bytes)
-    // change nothing: detect them with one pass and skip the sorts
-    TPCHK(c, hipMemsetAsync(live, 0, 4, st));
+    // change nothing: detect them with one pass and skip the sorts; the sort
+    // of a live round runs over the key bits that vary only
+    TPCHK(c, hipMemsetAsync(live, 0, 12, st));
     hipLaunchKernelGGL(k_round_live, dim3(blocks(m, 256)), dim3(256), 0, st, keysA, act, m, live);
-    uint32_t h_live = 0;
-    TPCHK(c, hipMemcpyAsync(&h_live, live, 4, hipMemcpyDeviceToHost, st));
+    uint32_t h_live[3] = {0, 0, 0};
+    TPCHK(c, hipMemcpyAsync(h_live, live, 12, hipMemcpyDeviceToHost, st));
     TPCHK(c, hipStreamSynchronize(st));
-    if (!h_live) continue;
-    tt = tmp;   // stable LSD: by the chunk key, then by the group start
-    TPCHK(c, rocprim::radix_sort_pairs(t, tt, keysA, keysB, valsA, valsB, (size_t)m, 0, 64, st));
+    if (!h_live[0]) continue;
+    const uint64_t vary = (uint64_t)h_live[2] << 32 | h_live[1];
+    const unsigned b0 = vary ? (unsigned)__builtin_ctzll(vary) : 0u;
+    const unsigned b1 = vary ? 64u - (unsigned)__builtin_clzll(vary) : 0u;
+    // stable LSD: by the chunk key, then by the group start
+    radix_pairs<uint64_t, uint64_t>(st, keysA, keysB, valsA, valsB, m, b0, b1, keysT, valsT, hist, sums);
     hipLaunchKernelGGL(k_gs_iota, dim3(blocks(m, 256)), dim3(256), 0, st, valsB, m, gs, ids);
-    tt = tmp;   // by group start (only the bits a position can have), carrying the index
-    TPCHK(c, rocprim::radix_sort_pairs(t, tt, gs, first, ids, pos, (size_t)m, 0, gbits, st));
+    // by group start (only the bits a position can have), carrying the index
+    radix_pairs<uint32_t, uint32_t>(st, gs, first, ids, pos, m, 0, gbits, reinterpret_cast<uint32_t*>(keysT), idsT,
+                                    hist, sums);
     hipLaunchKernelGGL(k_gather, dim3(blocks(m, 256)), dim3(256), 0, st, keysB, valsB, pos, m, keysA, gs, ids);
     // now keysA / gs / ids are in (group start, chunk key) order
     hipLaunchKernelGGL(k_run_first, dim3(blocks(m, 256)), dim3(256), 0, st, gs, m, bstart);
-    tt = tmp;
-    TPCHK(c, rocprim::inclusive_scan(t, tt, bstart, first, (size_t)m, rocprim::maximum<uint32_t>(), st));
+    maxscan(bstart, first, m);
     hipLaunchKernelGGL(k_bounds, dim3(blocks(m, 256)), dim3(256), 0, st, keysA, gs, first, m, pos, bstart);
-    tt = tmp;
-    TPCHK(c, rocprim::inclusive_scan(t, tt, bstart, slot, (size_t)m, rocprim::maximum<uint32_t>(), st));
+    maxscan(bstart, slot, m);
     hipLaunchKernelGGL(k_settle, dim3(blocks(m, 256)), dim3(256), 0, st, keysA, gs, ids, pos, slot, m, base, d_order,
                        keep);
     // slot (new group start + 1) is still needed by k_compact: scan the keep flags into `first`
-    tt = tmp;
-    TPCHK(c, rocprim::exclusive_scan(t, tt, keep, first, 0u, (size_t)m, rocprim::plus<uint32_t>(), st));
+    exscan(keep, first, m);
     hipLaunchKernelGGL(k_compact, dim3(blocks(m, 256)), dim3(256), 0, st, ids, slot, keep, first, m, act);
     uint32_t nm = 0;
     TPCHK(c, hipMemcpyAsync(&nm, first + m - 1, 4, hipMemcpyDeviceToHost, st));
