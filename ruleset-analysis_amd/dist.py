@@ -177,17 +177,28 @@ def merge(backend, dist, world, rank, group=None, to_host=True):
     rank 0 and None elsewhere: numpy arrays (records as RECORD_DTYPE rows), or
     with to_host=False the device tensors as they stand in rank 0's HBM
     (records as uint8 rows; see merged_to_host), which is where the
-    single-GPU job leaves its result too."""
+    single-GPU job leaves its result too.
+
+    One host read per phase: the route counts (with the overflow flag), the
+    thresholds (with the import overflow need), the pass-2 route counts, and
+    the gather sizes (riding on the distinct-count all_reduce).  At world 1
+    there is no collective and no extra read: the shard's own cap resolution
+    says whether pass 2 runs, as in the single-GPU job."""
     import torch
     tr = _Trace(rank)
     c = backend.counters()
     dev = c['matches'].device
     tr('start', dev)
-    _all_reduce(c['matches'], dist, group)
-    _all_reduce(c['hits'], dist, group)
-    tr('counters', dev)
     n_rules = c['thresh'].numel()
-    others = (torch.arange(n_rules, device=dev) % world) != rank    # rules owned elsewhere
+    multi = world > 1
+    if multi:
+        # line and hit counters in one all_reduce
+        mh = torch.cat([c['matches'], c['hits']])
+        _all_reduce(mh, dist, group)
+        c['matches'].copy_(mh[:n_rules])
+        c['hits'].copy_(mh[n_rules:])
+        others = (torch.arange(n_rules, device=dev) % world) != rank    # rules owned elsewhere
+    tr('counters', dev)
     backend.set_owner(world, rank)
     try:
         failed = 0
@@ -199,58 +210,70 @@ def merge(backend, dist, world, rank, group=None, to_host=True):
             exported = torch.zeros(0, dtype=torch.uint8, device=dev)
             failed = 1
         tr('export1', dev)
-        recv = route_records(exported, world, dist, group, flag=failed)
-        if recv is None:
-            raise ShardOverflow('distinct-connection table overflow on at least one rank')
-        tr('route1', dev)
-        failed = 0
-        if recv.numel():
-            # the received entries join the owned ones: the thresholds of the
-            # owned rules are resolved again over the merged entries (with
-            # nothing received, the shard's own resolution already is that)
-            try:
-                backend.import_records(recv, 0)
-                backend.resolve_cap()
-            except Exception as e:  # noqa: BLE001
-                if not _overflow(e):
-                    raise
-                # the table must hold the shard's entries and every received one
-                failed = max(backend.table_need(recv.numel() // REC), 1)
-        tr('import1', dev)
-        # thresholds of the owned rules (MAX: the others say "none" = -1),
-        # with the overflow flag (the entries a failed table needs) riding along
-        thresh = torch.cat([c['thresh'].masked_fill(others, NO_THRESHOLD),
-                            torch.tensor([failed], dtype=torch.int64, device=dev)])
-        _all_reduce(thresh, dist, group, op=dist.ReduceOp.MAX)
-        capped_any, need = (int(x) for x in torch.stack([(thresh[:-1] != NO_THRESHOLD).any().to(torch.int64),
-                                                         thresh[-1]]).cpu().tolist())
-        capped_any = bool(capped_any)
-        if need:
-            raise ShardOverflow('distinct-connection table overflow on at least one rank (merge import)', needed=need)
-        thresh = thresh[:-1]
+        if multi:
+            recv = route_records(exported, world, dist, group, flag=failed)
+            if recv is None:
+                raise ShardOverflow('distinct-connection table overflow on at least one rank')
+            tr('route1', dev)
+            failed = 0
+            if recv.numel():
+                # the received entries join the owned ones: the thresholds of the
+                # owned rules are resolved again over the merged entries (with
+                # nothing received, the shard's own resolution already is that)
+                try:
+                    backend.import_records(recv, 0)
+                    backend.resolve_cap()
+                except Exception as e:  # noqa: BLE001
+                    if not _overflow(e):
+                        raise
+                    # the table must hold the shard's entries and every received one
+                    failed = max(backend.table_need(recv.numel() // REC), 1)
+            tr('import1', dev)
+            # thresholds of the owned rules (MAX: the others say "none" = -1),
+            # with the overflow flag (the entries a failed table needs) riding along
+            thresh = torch.cat([c['thresh'].masked_fill(others, NO_THRESHOLD),
+                                torch.tensor([failed], dtype=torch.int64, device=dev)])
+            _all_reduce(thresh, dist, group, op=dist.ReduceOp.MAX)
+            capped_any, need = (int(x) for x in torch.stack([(thresh[:-1] != NO_THRESHOLD).any().to(torch.int64),
+                                                             thresh[-1]]).cpu().tolist())
+            if need:
+                raise ShardOverflow('distinct-connection table overflow on at least one rank (merge import)',
+                                    needed=need)
+            thresh = thresh[:-1]
+        else:
+            if failed:
+                raise ShardOverflow('distinct-connection table overflow')
+            capped_any, thresh = backend.capped, c['thresh']
         tr('cap', dev)
         if capped_any:
-            backend.set_thresh(thresh)
+            if multi:
+                backend.set_thresh(thresh)
             backend.recount()
-            recv2 = route_records(backend.export(1), world, dist, group)
-            if recv2.numel():
-                backend.import_records(recv2, 1)
+            if multi:
+                recv2 = route_records(backend.export(1), world, dist, group)
+                if recv2.numel():
+                    backend.import_records(recv2, 1)
             tr('pass2', dev)
         final = backend.emit_final()
-        distinct = c['distinct'].masked_fill(others, 0)
-        _all_reduce(distinct, dist, group)
+        if multi:
+            # the distinct counts of the owned rules and every rank's row
+            # bytes (for the gather) in one all_reduce, one host read
+            dsz = torch.zeros(n_rules + world, dtype=torch.int64, device=dev)
+            dsz[:n_rules] = c['distinct'].masked_fill(others, 0).to(torch.int64)
+            dsz[n_rules + rank] = final.numel()
+            _all_reduce(dsz, dist, group)
+            distinct = dsz[:n_rules].to(c['distinct'].dtype)
+        else:
+            distinct = c['distinct']
         tr('emit', dev)
     finally:
         backend.set_owner(0, 0)
-    # the owners' rows to rank 0 (sizes first: one int per rank)
-    if world == 1:
-        parts = [final]
-    else:
-        size = torch.tensor([final.numel()], dtype=torch.int64, device=final.device)
-        sizes = [torch.zeros_like(size) for _ in range(world)]
-        _all_gather(sizes, size, dist, group)
-        sizes = [int(s) for s in torch.cat(sizes).cpu().tolist()]
+    # the owners' rows to rank 0
+    if multi:
+        sizes = [int(s) for s in dsz[n_rules:].cpu().tolist()]
         parts = _gather0(final, sizes, rank, world, dist, group)
+    else:
+        parts = [final]
     tr('gather', dev)
     if rank != 0:
         tr('end')
@@ -284,6 +307,7 @@ class EngineBackend(object):
         self.batches = batches
         self.gid_bufs = gid_bufs
         self.cap = cap
+        self.capped = 0     # rules the shard's own cap resolution (export(0)) found capped
 
     def counters(self):
         return self.eng.counters
@@ -300,7 +324,7 @@ class EngineBackend(object):
         resolution), 1 = the pass-2 sums.  A single rank owns every rule:
         nothing to scan for."""
         if which == 0:
-            self.eng.resolve_cap()
+            self.capped = self.eng.resolve_cap()
         if self.world == 1:
             return self.eng.torch.zeros(0, dtype=self.eng.torch.uint8, device=self.eng.device)
         return self.eng.emit_device('pass1_kept' if which == 0 else 'pass2')

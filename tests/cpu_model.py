@@ -172,7 +172,7 @@ class NumpyBackend(object):
             # as EngineBackend.export(0): the shard resolves its own cap first
             # and exports only the entries its threshold keeps (exact: a
             # shard's P bounds the global P from above)
-            self.resolve_cap()
+            self.capped = self.resolve_cap()
             self.exported_all = sum(1 for (g, *_) in self.local.t if foreign(g))
             recs = self.local.records(3, self._thresh_np(), keep=foreign)
             self.exported_kept = recs.numel() // RECORD_DTYPE.itemsize
