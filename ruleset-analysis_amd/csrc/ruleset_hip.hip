@@ -65,7 +65,7 @@ struct alignas(64) Slot {
   unsigned int first, last;      // pass-1 timestamp range
   unsigned int count;            // pass-1 occurrences
   unsigned int count2, first2, last2;   // pass-2 aggregates (order <= P only)
-  unsigned int pad[4];
+  unsigned int pad[4];           // pad[0]: the entry's used-list index (region path)
 };
 static_assert(sizeof(Slot) == 64, "slot layout");
 static_assert(offsetof(Slot, first) % 8 == 0 && offsetof(Slot, last) == offsetof(Slot, first) + 4,
@@ -116,6 +116,8 @@ struct Agg {
   unsigned long long mask;           // capacity - 1 (power of two)
   unsigned long long* used;          // used-slot list: gid << 32 | slot
   unsigned long long* used_n;
+  unsigned long long* ukey;          // per used-list index: the entry's current min_order (kept by k_reduce<1>;
+                                     // the slot's pad[0] holds its used-list index)
   unsigned int* flags;               // [0] overflow, [1] bad gid/list/state
   uint32_t cap;
   uint32_t skip;                     // profiling only (RSA_OPT_PROFILE_SKIP): 1 counters, 2 table, 4 table updates
@@ -312,6 +314,9 @@ __device__ unsigned long long g_phase[9];
 
 constexpr int kAttempts = 4;   // compile.py PHT_ATTEMPTS
 constexpr uint32_t kListWords = 20, kGroupWords = 20, kMaskWords = 4;
+#ifndef RSA_CAP_FULLSCAN
+#define RSA_CAP_FULLSCAN 0   // A/B builds: cap resolution gathers every capped entry's key from its slot
+#endif
 #ifndef RSA_PREFETCH_T
 #define RSA_PREFETCH_T 0   // A/B builds: load the next tuple one iteration ahead
 #endif
@@ -1950,6 +1955,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
             nm.z = min(m.z, e_first[e]);
             nm.w = max(m.w, e_last[e]);
             *reinterpret_cast<v4u*>(&sl->min_order) = nm;
+            if (nmo < mo) A.ukey[sl->pad[0]] = nmo;   // the cap resolution's copy of the key
             c.x += e_cnt[e];
           } else {
             c.y += e_cnt[e];
@@ -1977,6 +1983,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
                 nm.z = min(m.z, e_first[e]);
                 nm.w = max(m.w, e_last[e]);
                 *reinterpret_cast<v4u*>(&sl->min_order) = nm;
+                if (nmo < mo) A.ukey[sl->pad[0]] = nmo;
                 sl->count += e_cnt[e];
               } else {
                 sl->count2 += e_cnt[e];
@@ -1988,24 +1995,14 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
             }
             if (kPass == 2) break;   // every pass-2 key was inserted in pass 1
             if (atomicOr(&claim[loc >> 5], bit) & bit) continue;   // claimed in this flush by another key
-            Slot ns;
-            ns.kA = kA;
-            ns.kB = kB;
-            ns.min_order = e_mo[e];
-            ns.first = e_first[e];
-            ns.last = e_last[e];
-            ns.count = e_cnt[e];
-            ns.count2 = 0;
-            ns.first2 = 0xFFFFFFFFu;
-            ns.last2 = 0;
-            ns.pad[0] = ns.pad[1] = ns.pad[2] = ns.pad[3] = 0;
-            A.slots[rbase + loc] = ns;
+            // the slot is written below, once its used-list index is known
+            // (no other key of this flush reads a claimed slot)
             slot = rbase + loc;
             fresh = true;
             break;
           }
           if (slot == kEmpty) atomicOr(&A.flags[kPass == 1 ? 0 : 1], kPass == 1 ? 1u : 4u);
-          e_kB[e] = kEmpty;
+          if (!fresh) e_kB[e] = kEmpty;
         }
         if (kPass == 1) {
           wave_count_hot(fresh, gid, A.distinct);
@@ -2022,8 +2019,27 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
         __syncthreads();
         uint32_t k = 0;
 #pragma unroll
-        for (int q = 0; q < kPer; ++q)
-          if (is_new[q]) A.used[sh_base + off + k++] = new_slot[q];
+        for (int q = 0; q < kPer; ++q) {
+          if (!is_new[q]) continue;
+          const uint32_t e = threadIdx.x + q * blockDim.x;
+          const unsigned long long ui = sh_base + off + k++;
+          Slot ns;
+          ns.kA = e_kA[e];
+          ns.kB = e_kB[e];
+          ns.min_order = e_mo[e];
+          ns.first = e_first[e];
+          ns.last = e_last[e];
+          ns.count = e_cnt[e];
+          ns.count2 = 0;
+          ns.first2 = 0xFFFFFFFFu;
+          ns.last2 = 0;
+          ns.pad[0] = (uint32_t)ui;
+          ns.pad[1] = ns.pad[2] = ns.pad[3] = 0;
+          A.slots[(uint32_t)new_slot[q]] = ns;
+          A.used[ui] = new_slot[q];
+          A.ukey[ui] = e_mo[e];
+          e_kB[e] = kEmpty;
+        }
       }
       __syncthreads();
       for (uint32_t w = threadIdx.x; w < words; w += blockDim.x) {
@@ -2247,16 +2263,25 @@ __global__ void k_table_clear(Slot* S, const unsigned long long* used, const uns
 // atomic cursor, so no scan is needed); the entries' min_order keys are
 // scattered into it and one workgroup per rule radix-selects the cap-th
 // smallest key, 8 bits at a time from the top (keys are unique order keys).
-__global__ void k_cap_mark(const unsigned int* distinct, uint32_t n_rules, uint32_t cap, uint32_t* cidx,
-                           uint32_t* capped_gid, uint32_t* capped_start, uint32_t* capped_fill,
+//
+// prev[g] is an earlier selection of this job (the last filter slice, or "none"):
+// an upper bound of the rule's P now, since a rule's entries only gain members
+// and their min_orders only decrease.  The cap entries at or below it then
+// still are, so the cap-th smallest key now is among the keys <= prev[g]: only
+// those are scattered (prev may alias out).
+__global__ void k_cap_mark(const unsigned int* distinct, uint32_t n_rules, uint32_t cap,
+                           const unsigned long long* prev, uint32_t* cidx, uint32_t* capped_gid,
+                           uint32_t* capped_start, uint32_t* capped_fill, unsigned long long* capped_prev,
                            unsigned int* n_capped, unsigned long long* total, unsigned long long* out) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= n_rules) return;
+  const unsigned long long pv = prev[g];
   out[g] = RSA_NO_THRESHOLD;
   if (cap > 0 && distinct[g] >= cap) {
     const unsigned int c = atomicAdd(n_capped, 1u);
     cidx[g] = c;
     capped_gid[c] = g;
+    capped_prev[c] = pv;
     capped_start[c] = (uint32_t)atomicAdd(total, (unsigned long long)distinct[g]);
     capped_fill[c] = 0;
   } else {
@@ -2271,7 +2296,8 @@ __global__ __launch_bounds__(kBlock) void k_cap_scatter(const Slot* S, const uns
                                                         const unsigned long long* n_used_p, const unsigned int* n_capped_p,
                                                         uint32_t lds_max,
                                                         const uint32_t* cidx, const uint32_t* capped_start,
-                                                        uint32_t* capped_fill, unsigned long long* keys,
+                                                        uint32_t* capped_fill, const unsigned long long* ukey,
+                                                        const unsigned long long* cprev, unsigned long long* keys,
                                                         unsigned long long max_keys, unsigned int* flags) {
   const unsigned int n_capped = *n_capped_p;
   if (n_capped == 0 || n_capped <= lds_max) return;   // the LDS variant's case (workgroup-uniform)
@@ -2284,7 +2310,10 @@ __global__ __launch_bounds__(kBlock) void k_cap_scatter(const Slot* S, const uns
     if (i < n_used) {
       const unsigned long long u = used[i];
       c = cidx[u >> 32];   // only the capped rules' entries are read
-      if (c != 0xFFFFFFFFu) key = S[(uint32_t)u].min_order;
+      if (c != 0xFFFFFFFFu) {
+        key = ukey ? ukey[i] : S[(uint32_t)u].min_order;
+        if (key > cprev[c]) c = 0xFFFFFFFFu;
+      }
     }
     const bool ok = c != 0xFFFFFFFFu;
     // lanes that share a rule are grouped first (ballots only, no memory
@@ -2326,7 +2355,8 @@ __global__ __launch_bounds__(1024) void k_cap_scatter_lds(const Slot* S, const u
                                                           const unsigned long long* n_used_p,
                                                           const unsigned int* n_capped_p, uint32_t lds_max,
                                                           const uint32_t* cidx, const uint32_t* capped_start,
-                                                          uint32_t* capped_fill, unsigned long long* keys,
+                                                          uint32_t* capped_fill, const unsigned long long* ukey,
+                                                          const unsigned long long* cprev, unsigned long long* keys,
                                                           unsigned long long max_keys, unsigned int* flags) {
   __shared__ uint32_t cnt[kCapLds];
   // counts are read on the device (no host round trip): a persistent grid
@@ -2348,7 +2378,10 @@ __global__ __launch_bounds__(1024) void k_cap_scatter_lds(const Slot* S, const u
     if (i < n_used) {
       const unsigned long long u = used[i];
       cc[k] = cidx[u >> 32];
-      if (cc[k] != 0xFFFFFFFFu) key[k] = S[(uint32_t)u].min_order;
+      if (cc[k] != 0xFFFFFFFFu) {
+        key[k] = ukey ? ukey[i] : S[(uint32_t)u].min_order;
+        if (key[k] > cprev[cc[k]]) cc[k] = 0xFFFFFFFFu;
+      }
     }
   }
 #pragma unroll
@@ -2780,6 +2813,8 @@ struct rsa_ctx {
   unsigned long long slot_cap = 0;    // power of two in use
   unsigned long long slot_alloc = 0;  // allocated (and initialised) slots
   unsigned long long* d_used = nullptr;
+  unsigned long long* d_ukey = nullptr;   // per used-list index: the entry's min_order (k_reduce<1> keeps it)
+  bool ukey_ok = true;                    // every entry of this job came through k_reduce<1> (no CAS import)
   unsigned long long* d_used_n = nullptr;
   unsigned long long used_last = 0;   // used slots at the last host read (upper bound for clearing)
   bool table_dirty = false;           // used list may be non-empty
@@ -2861,6 +2896,7 @@ struct rsa_ctx {
   uint32_t* d_capped_gid = nullptr;
   uint32_t* d_capped_cnt = nullptr;
   uint32_t* d_capped_start = nullptr;
+  unsigned long long* d_capped_prev = nullptr;   // per capped rule: the earlier selection bounding it
   uint32_t cidx_len = 0;
   unsigned long long* d_keys = nullptr;   // capped rules' min_order keys, one segment per rule
   unsigned long long sort_alloc = 0;
@@ -2920,6 +2956,7 @@ Agg agg_of(const rsa_ctx* c) {
   a.slots = c->d_slots;
   a.mask = c->slot_cap ? c->slot_cap - 1 : 0;
   a.used = c->d_used;
+  a.ukey = c->d_ukey;
   a.used_n = c->d_used_n;
   a.flags = c->d_flags;
   a.cap = c->cap;
@@ -3002,12 +3039,15 @@ int cap_select(rsa_ctx* c, unsigned long long* out, uint32_t* h_n_capped) {
     hipFree(c->d_capped_gid);
     hipFree(c->d_capped_cnt);
     hipFree(c->d_capped_start);
+    hipFree(c->d_capped_prev);
     c->d_cidx = c->d_capped_gid = c->d_capped_cnt = c->d_capped_start = nullptr;
+    c->d_capped_prev = nullptr;
     c->cidx_len = 0;
     HIPCHK(c, hipMalloc(&c->d_cidx, (size_t)nr * sizeof(uint32_t)));
     HIPCHK(c, hipMalloc(&c->d_capped_gid, (size_t)nr * sizeof(uint32_t)));
     HIPCHK(c, hipMalloc(&c->d_capped_cnt, (size_t)nr * sizeof(uint32_t)));
     HIPCHK(c, hipMalloc(&c->d_capped_start, (size_t)nr * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(&c->d_capped_prev, (size_t)nr * sizeof(unsigned long long)));
     c->cidx_len = nr;
   }
   if (c->sort_alloc < c->slot_cap) {   // a key per slot at most: sized once per table size
@@ -3021,19 +3061,32 @@ int cap_select(rsa_ctx* c, unsigned long long* out, uint32_t* h_n_capped) {
   unsigned int* d_ncap = c->d_flags + 2;
   HIPCHK(c, hipMemsetAsync(d_ncap, 0, sizeof(unsigned int), c->stream));
   HIPCHK(c, hipMemsetAsync(c->d_cursor, 0, sizeof(unsigned long long), c->stream));
-  k_cap_mark<<<(nr + kBlock - 1) / kBlock, kBlock, 0, c->stream>>>(c->d_distinct, nr, c->cap, c->d_cidx,
+  // the keys: read from the used-list-ordered copy k_reduce<1> keeps
+  // (16 B per used entry, coalesced) unless an entry was claimed by the CAS
+  // import; only keys at or below the rule's earlier selection (the job's last
+  // filter slice) are scattered and selected over
+#if RSA_CAP_FULLSCAN   // A/B build switch: slot gathers, every key of a capped rule
+  const unsigned long long* ukey = nullptr;
+  const unsigned long long* prev = out;
+  HIPCHK(c, hipMemsetAsync(out, 0xFF, nr * sizeof(unsigned long long), c->stream));
+#else
+  const unsigned long long* ukey = c->ukey_ok ? c->d_ukey : nullptr;
+  const unsigned long long* prev = c->d_filter;
+#endif
+  k_cap_mark<<<(nr + kBlock - 1) / kBlock, kBlock, 0, c->stream>>>(c->d_distinct, nr, c->cap, prev, c->d_cidx,
                                                                    c->d_capped_gid, c->d_capped_start,
-                                                                   c->d_capped_cnt, d_ncap, c->d_cursor, out);
+                                                                   c->d_capped_cnt, c->d_capped_prev, d_ncap,
+                                                                   c->d_cursor, out);
   HIPCHK(c, hipGetLastError());
   // both scatter variants are launched; each exits unless the device-side
   // count of capped rules is its case (LDS counters for <= kCapLds rules)
   const uint32_t lds_max = c->wave_cap_scatter ? 0u : (uint32_t)kCapLds;
   k_cap_scatter_lds<<<c->cu_count * 2, 1024, 0, c->stream>>>(c->d_slots, c->d_used, c->d_used_n, d_ncap, lds_max,
-                                                             c->d_cidx, c->d_capped_start, c->d_capped_cnt, c->d_keys,
-                                                             c->sort_alloc, c->d_flags);
+                                                             c->d_cidx, c->d_capped_start, c->d_capped_cnt, ukey,
+                                                             c->d_capped_prev, c->d_keys, c->sort_alloc, c->d_flags);
   k_cap_scatter<<<c->cu_count * 8, kBlock, 0, c->stream>>>(c->d_slots, c->d_used, c->d_used_n, d_ncap, lds_max,
-                                                          c->d_cidx, c->d_capped_start, c->d_capped_cnt, c->d_keys,
-                                                          c->sort_alloc, c->d_flags);
+                                                          c->d_cidx, c->d_capped_start, c->d_capped_cnt, ukey,
+                                                          c->d_capped_prev, c->d_keys, c->sort_alloc, c->d_flags);
   HIPCHK(c, hipGetLastError());
   const unsigned sel_grid = nr < (uint32_t)c->cu_count * 2 ? nr : (unsigned)c->cu_count * 2;
   k_cap_select<<<sel_grid, kSelThreads, 0, c->stream>>>(c->d_keys, c->d_capped_start, c->d_capped_cnt, c->d_capped_gid,
@@ -3477,10 +3530,10 @@ int rsa_ctx_destroy(rsa_ctx* c) {
   void* bufs[] = {c->d_tail, c->d_tail_n, c->d_gscratch, c->d_gh, c->d_stats, c->d_recs, c->d_recs2, c->d_regs, c->d_wcnt, c->d_nrecs, c->d_starts, c->d_hist,
                   c->d_scan_sums, c->d_occ, c->d_entries, c->d_off,
                   c->d_img, c->d_resid,
-                  c->d_slots, c->d_used, c->d_used_n, c->d_filter, c->d_packed, c->d_hot, c->d_hot_tasks, c->d_hot_base,
+                  c->d_slots, c->d_used, c->d_ukey, c->d_used_n, c->d_filter, c->d_packed, c->d_hot, c->d_hot_tasks, c->d_hot_base,
                   c->d_hot_fill, c->d_hot_ctl, c->d_hot_total, c->d_cnt_words, c->d_cnt_starts,
                   c->d_cnt_tasks, c->d_cnt_ctl, c->d_flags, c->d_cursor, c->d_cidx,
-                  c->d_capped_gid, c->d_capped_cnt, c->d_capped_start, c->d_keys};
+                  c->d_capped_gid, c->d_capped_cnt, c->d_capped_start, c->d_capped_prev, c->d_keys};
   for (void* b : bufs) (void)hipFree(b);
   for (int k = 0; k < kMaxEvents; ++k)
     if (c->ev[k]) (void)hipEventDestroy(c->ev[k]);
@@ -3828,11 +3881,14 @@ int rsa_reset(rsa_ctx* c, uint64_t capacity, uint32_t cap) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     hipFree(c->d_slots);
     hipFree(c->d_used);
+    hipFree(c->d_ukey);
     c->d_slots = nullptr;
     c->d_used = nullptr;
+    c->d_ukey = nullptr;
     c->slot_alloc = 0;
     HIPCHK(c, hipMalloc(&c->d_slots, want * sizeof(Slot)));
     HIPCHK(c, hipMalloc(&c->d_used, want * sizeof(unsigned long long)));
+    HIPCHK(c, hipMalloc(&c->d_ukey, want * sizeof(unsigned long long)));
     k_table_init<<<grid_for(c, want, 8), kBlock, 0, c->stream>>>(c->d_slots, want);
     HIPCHK(c, hipGetLastError());
     c->slot_alloc = want;
@@ -3849,6 +3905,7 @@ int rsa_reset(rsa_ctx* c, uint64_t capacity, uint32_t cap) {
     c->table_dirty = false;
   }
   c->slots_clean = !c->table_dirty;
+  c->ukey_ok = true;
   c->slot_cap = want;
   c->cap = cap;
   HIPCHK(c, hipMemsetAsync(c->d_used_n, 0, sizeof(unsigned long long), c->stream));
@@ -4001,6 +4058,7 @@ int rsa_import(rsa_ctx* c, int which, const rsa_conn_record* in, uint64_t n) {
   if (!c->region_import) {
     if (which == 0 && !c->slots_clean)
       return fail(c, RSA_ERR_STATE, "RSA_OPT_REGION_IMPORT=0 imports need the table cleared: set it before rsa_reset");
+    if (which == 0) c->ukey_ok = false;   // CAS claims do not know their used-list index: cap resolution reads slots
     k_import<<<grid_for_threads(c, n, 1024, 4), 1024, 0, c->stream>>>(in, n, which, agg_of(c));
     HIPCHK(c, hipGetLastError());
     return RSA_OK;
