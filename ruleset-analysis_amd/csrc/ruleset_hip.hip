@@ -3582,7 +3582,8 @@ int rsa_set_option(rsa_ctx* c, int option, int64_t value) {
       c->precheck = value != 0;
       return RSA_OK;
     case RSA_OPT_PARSE_MODE:
-      if (value < 0 || value > 1) return fail(c, RSA_ERR_ARG, "parse mode must be 0 (LDS staged) or 1 (direct)");
+      if (value < 0 || value > 2)
+        return fail(c, RSA_ERR_ARG, "parse mode must be 0 (LDS staged), 1 (direct) or 2 (register window)");
       c->parse_mode = (int)value;
       return RSA_OK;
     case RSA_OPT_REGION_IMPORT:

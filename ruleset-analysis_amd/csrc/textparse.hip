@@ -312,6 +312,104 @@ __global__ __launch_bounds__(kParseWG) void k_parse(const uint8_t* __restrict__ 
   disp[i] = d;
 }
 
+// k_parse_win: the template pass without staging.  Every lane reads its own
+// line straight from HBM through a register window: two aligned 16-B chunks,
+// funnel-shifted once per 16 bytes so that the line's next 16 bytes sit at
+// fixed register positions (the shift is the line's start modulo 16, the
+// same every round), the chunk after them loaded one round ahead.  LDS holds
+// only the program, the class table and the slots (~10 KB per workgroup,
+// where staging the text took 38 KB and held a CU to eight waves), so
+// occupancy is set by registers.  tpl_finish reads its few fields through
+// 4-byte loads (the line is in L2 by then).  The text must be 16-B aligned
+// (the host checks).
+__device__ __forceinline__ uint4 text_chunk(const uint4* __restrict__ t16, const uint8_t* __restrict__ text,
+                                            uint64_t ci, uint64_t n_full, uint64_t n_bytes) {
+  if (ci < n_full) return t16[ci];
+  uint32_t w[4] = {0u, 0u, 0u, 0u};   // the buffer's last, partial chunk (or past the end: zeros)
+  for (uint32_t k = 0; k < 16; ++k)
+    if (16 * ci + k < n_bytes) w[k >> 2] |= (uint32_t)text[16 * ci + k] << (8 * (k & 3));
+  return uint4{w[0], w[1], w[2], w[3]};
+}
+
+__global__ __launch_bounds__(kParseWG) void k_parse_win(const uint8_t* __restrict__ text,
+                                                       const uint64_t* __restrict__ off, uint64_t n_lines,
+                                                       const rsa_parse_ifc* __restrict__ ifcs, uint32_t n_ifcs,
+                                                       const rsa_parse_spell* __restrict__ spells, uint32_t n_spells,
+                                                       rsa_tuple* __restrict__ tuples, uint32_t* __restrict__ ts_out,
+                                                       uint32_t* __restrict__ disp, uint32_t* __restrict__ slow_idx,
+                                                       unsigned int* __restrict__ slow_n) {
+  using namespace rsa_text::tpl;
+  __shared__ uint32_t tprog[kProgLen];
+  __shared__ uint8_t tcls[256];
+  __shared__ uint32_t tslot[kParseWG * kSlotWords];
+  {
+    constexpr ClsTable kCls = cls_table();
+    for (uint32_t k = threadIdx.x; k < kProgLen; k += blockDim.x) tprog[k] = kProg[k];
+    for (uint32_t k = threadIdx.x; k < 256; k += blockDim.x) tcls[k] = kCls.t[k];
+  }
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * kParseWG + threadIdx.x;
+  const bool have = i < n_lines;
+  const uint64_t n_bytes = off[n_lines];
+  uint64_t a = 0, len = 0;
+  if (have) {
+    a = off[i];
+    const uint64_t b = off[i + 1];
+    len = b - a;
+    if (len && text[b - 1] == '\n') --len;
+  }
+  const bool scannable = have && len < 0xFFFFu;
+  const uint32_t n = scannable ? (uint32_t)len : 0u;
+  uint32_t nmax = n;   // the wave's longest line: the trip count of every lane
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t y = (uint32_t)__shfl_xor((int)nmax, o);
+    nmax = y > nmax ? y : nmax;
+  }
+  uint32_t* slot = tslot + threadIdx.x * kSlotWords;
+  const uint4* t16 = reinterpret_cast<const uint4*>(text);
+  const uint64_t n_full = n_bytes >> 4;
+  uint64_t ci = a >> 4;
+  const uint32_t q = (uint32_t)(a >> 2) & 3u, r = ((uint32_t)a & 3u) * 8u;
+  uint4 w0 = text_chunk(t16, text, ci, n_full, n_bytes), w1 = text_chunk(t16, text, ci + 1, n_full, n_bytes);
+  State st;
+  for (uint32_t base = 0; base < nmax; base += 16) {
+    const uint4 w2 = text_chunk(t16, text, ci + 2, n_full, n_bytes);   // the next round's second chunk
+    const uint32_t W[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+    uint32_t X[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) X[j] = q == 0 ? W[j] : q == 1 ? W[j + 1] : q == 2 ? W[j + 2] : W[j + 3];
+    uint32_t B[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) B[k] = __builtin_amdgcn_alignbit(X[k + 1], X[k], r);
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k) {
+      const uint32_t idx = base + k;
+      step(st, idx, (B[k >> 2] >> (8 * (k & 3))) & 0xFFu, lt01(idx, n), tprog, tcls, slot);
+    }
+    w0 = w1;
+    w1 = w2;
+    ++ci;
+  }
+  if (!have) return;
+  rsa_tuple tup = {0u, 0u, 0, 0, 0, 0, 0};
+  uint32_t ts = 0, d = rsa_text::kLineDefer;
+  if (scannable && st.ok && tprog[st.seg] == kEndSeg) {
+    const uint64_t nw = n_bytes >> 2;
+    uint32_t tail = 0;
+    for (uint32_t k = 0; k < (uint32_t)(n_bytes & 3u); ++k) tail |= (uint32_t)text[4 * nw + k] << (8 * k);
+    const rsa_text::GWordU s{reinterpret_cast<const uint32_t*>(text), a, nw, tail, (uint32_t)len};
+    if (!rsa_text::tpl_finish(s, slot, ifcs, n_ifcs, spells, n_spells, tup, ts, d)) {
+      tup = rsa_tuple{0u, 0u, 0, 0, 0, 0, 0};
+      ts = 0;
+      d = rsa_text::kLineDefer;
+    }
+  }
+  defer_append(d == rsa_text::kLineDefer, i, slow_idx, slow_n);
+  tuples[i] = tup;
+  ts_out[i] = ts;
+  disp[i] = d;
+}
+
 // The deferred lines, densely packed: the general parse (the regexes'
 // backtracking restated), reading from HBM.  Persistent grid over the
 // device-side count.
@@ -979,7 +1077,11 @@ int rsa_parse_text(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_off, uin
   unsigned int* slow_n = static_cast<unsigned int*>(L.base);
   uint32_t* slow_idx = reinterpret_cast<uint32_t*>(static_cast<char*>(L.base) + 16);
   TPCHK(c, hipMemsetAsync(slow_n, 0, 4, st));
-  if (rsa_internal_parse_mode(c) == 1)
+  const int mode = rsa_internal_parse_mode(c);
+  if (mode == 2 && !(reinterpret_cast<uintptr_t>(d_text) & 15u))
+    hipLaunchKernelGGL(k_parse_win, dim3((uint32_t)nb), dim3(kParseWG), 0, st, d_text, d_off, n_lines, d_ifcs, n_ifcs,
+                       d_spells, n_spells, d_tuples, d_ts, d_disp, slow_idx, slow_n);
+  else if (mode == 1)
     hipLaunchKernelGGL((k_parse<false, true>), dim3((uint32_t)nb), dim3(kParseWG), 0, st, d_text, d_off, n_lines, d_ifcs,
                        n_ifcs, d_spells, n_spells, d_tuples, d_ts, d_disp, slow_idx, slow_n);
   else

@@ -671,32 +671,50 @@ constexpr uint32_t kSlotWords = kFields + 1;   // one span per field + a dummy s
 
 constexpr uint32_t pack3(char a, char b, char c) { return (uint32_t)(uint8_t)a << 16 | (uint32_t)(uint8_t)b << 8 | (uint8_t)c; }
 
-// The scan.  P: the program (LDS copy on the device), C: the class of each
-// byte value (cls_of, an LDS table on the device), Q: the lane's kSlotWords
-// slot words, each field's span as start | length << 16.  True: the line has
-// the template form.  All lanes step together (the loop runs to the longest
-// line of the wave); the body is selects only.
+// One byte of the scan: byte c at index i of the line.  P: the program (LDS
+// copy on the device), C: the class of each byte value (cls_of, an LDS table
+// on the device), Q: the lane's kSlotWords slot words, each field's span as
+// start | length << 16.  act 0 (the line already ended): no state changes,
+// the slot write goes to the dummy slot.  The conditions are 0/1 integers
+// combined with integer ops and bit selects (v_bfi): booleans would live in
+// scalar lane masks, and their and/or/select bookkeeping is scalar work that
+// the CU's one scalar unit serialises over its four SIMDs.
+struct State {
+  uint32_t seg = 0, cnt = 0, pos0 = 0, ok = 1;
+};
+RSA_HD uint32_t lt01(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a - b) >> 63); }   // a < b
+RSA_HD uint32_t nz01(uint32_t a) { return a ? 1u : 0u; }
+RSA_HD uint32_t sel(uint32_t m01, uint32_t a, uint32_t b) {   // m01 ? a : b, as a bit select
+  const uint32_t m = 0u - m01;
+  return (a & m) | (b & ~m);
+}
+template <class P, class C, class Q>
+RSA_HD void step(State& st, uint32_t i, uint32_t c, uint32_t act, P prog, C cls, Q slot) {
+  const uint32_t desc = prog[st.seg];
+  const uint32_t lit = desc & 0xFFu, msk = (desc >> 8) & 0xFFu, mn = (desc >> 16) & 7u, mx = (desc >> 19) & 0xFFu,
+                 fld = desc >> 27;
+  const uint32_t is_run = nz01(msk);
+  const uint32_t cnt = st.cnt;
+  st.pos0 = sel(1u - nz01(cnt), i, st.pos0);
+  const uint32_t cont = nz01((uint32_t)cls[c] & msk) & lt01(cnt, mx);   // (msk 0: a literal, never a run byte)
+  const uint32_t rend = act & st.ok & is_run & (cont ^ 1u);              // a run ends here: its span into the slot
+  slot[sel(rend & lt01(fld, kFields), fld, kFields)] = st.pos0 | cnt << 16;
+  const uint32_t step_ok = cont | (((lt01(cnt, mn) ^ 1u) | (is_run ^ 1u)) & (1u - nz01(c ^ lit)) &
+                                   nz01(desc ^ kEndSeg));
+  const uint32_t nok = st.ok & step_ok;
+  st.seg += act & nok & (cont ^ 1u) & lt01(st.seg + 1, kProgLen);
+  st.ok = sel(act, nok, st.ok);
+  st.cnt = sel(act, (cnt + 1) & (0u - cont), cnt);
+}
+
+// The scan of a whole line.  True: the line has the template form.  All
+// lanes step together (the loop runs to the longest line of the wave).
 template <class S, class P, class C, class Q>
 RSA_HD bool scan(const S& s, P prog, C cls, Q slot) {
   if (s.n > 0xFFFFu) return false;
-  uint32_t seg = 0, cnt = 0, pos0 = 0;
-  bool ok = true;
-  for (uint32_t i = 0; i < s.n; ++i) {
-    const uint32_t c = s[i];
-    const uint32_t desc = prog[seg];
-    const uint32_t lit = desc & 0xFFu, msk = (desc >> 8) & 0xFFu, mn = (desc >> 16) & 7u, mx = (desc >> 19) & 0xFFu,
-                   fld = desc >> 27;
-    const bool is_run = msk != 0;
-    pos0 = cnt == 0 ? i : pos0;
-    const bool cont = (cls[c] & msk) != 0 && cnt < mx;   // (msk 0: a literal, never a run byte)
-    const bool rend = ok && is_run && !cont;               // a run ends here: its span into the slot
-    slot[(rend && fld < kFields) ? fld : kFields] = pos0 | cnt << 16;
-    const bool step_ok = cont || ((cnt >= mn || !is_run) && c == lit && desc != kEndSeg);
-    ok = ok && step_ok;
-    seg = (ok && !cont && seg + 1 < kProgLen) ? seg + 1 : seg;
-    cnt = cont ? cnt + 1 : 0u;
-  }
-  return ok && prog[seg] == kEndSeg;
+  State st;
+  for (uint32_t i = 0; i < s.n; ++i) step(st, i, s[i], 1u, prog, cls, slot);
+  return st.ok && prog[st.seg] == kEndSeg;
 }
 
 // the byte classes as a table (the device copies it to LDS)

@@ -292,9 +292,10 @@ def test_gpu_parse_golden_equals_host(engine, case):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('seed,mode', [(1, 0), (2, 0), (1, 1)])
+@pytest.mark.parametrize('seed,mode', [(1, 0), (2, 0), (1, 1), (1, 2), (2, 2)])
 def test_gpu_parse_fuzz_equals_host(engine, seed, mode):
-    """mode: RSA_OPT_PARSE_MODE (0 LDS-staged lines, 1 direct HBM reads)."""
+    """mode: RSA_OPT_PARSE_MODE (0 LDS-staged lines, 1 direct HBM reads,
+    2 register-window reads)."""
     from ruleset_analysis_amd import native
     db, lines = _fuzz_lines(seed, 6000)
     good = [l for l in lines if _host_ok('fw1', l, db)]
