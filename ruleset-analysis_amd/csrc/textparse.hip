@@ -462,8 +462,7 @@ __global__ __launch_bounds__(kParseWG) void k_parse_slow(const uint8_t* __restri
 // or its bytes ended in this window (then the whole group is equal strings,
 // already in line-index order: the sorts are stable).
 __device__ __forceinline__ uint64_t chunk_key(const uint8_t* __restrict__ text, uint64_t n_bytes, uint64_t a,
-                                              uint32_t len, uint32_t round) {
-  const uint64_t pos = (uint64_t)round * 7;
+                                              uint32_t len, uint64_t pos) {
   const uint32_t rem = len > pos ? (uint32_t)(len - pos) : 0u;
   if (!rem) return 0;
   const uint64_t p = a + pos;
@@ -484,6 +483,26 @@ __device__ __forceinline__ uint64_t chunk_key(const uint8_t* __restrict__ text, 
   return k | (rem < 8 ? rem : 8u);
 }
 
+// 8 bytes of a line from byte p of the text, big-endian, zero past `rem`
+// (rem >= 1 bytes of the line remain at p); text is 4-byte aligned.
+__device__ __forceinline__ uint64_t line_chunk8(const uint8_t* __restrict__ text, uint64_t n_bytes, uint64_t p,
+                                                uint32_t rem) {
+  uint64_t k;
+  if (p + 12 <= n_bytes) {
+    const uint32_t* t32 = reinterpret_cast<const uint32_t*>(text);
+    const uint64_t q = p >> 2;
+    const uint32_t sh = (uint32_t)(p & 3) * 8;
+    const uint64_t lo = (uint64_t)t32[q] | ((uint64_t)t32[q + 1] << 32);
+    const uint64_t x = sh ? (lo >> sh) | ((uint64_t)t32[q + 2] << (64 - sh)) : lo;
+    k = __builtin_bswap64(x);
+  } else {
+    k = 0;
+    for (uint32_t j = 0; j < 8; ++j) k = k << 8 | (p + j < n_bytes ? text[p + j] : 0u);
+  }
+  if (rem < 8) k &= ~0ull << (64 - 8 * rem);
+  return k;
+}
+
 // round 0: every line's length without '\n' (kept for the later rounds) and its first key
 __global__ void k_keys0(const uint8_t* __restrict__ text, const uint64_t* __restrict__ off, uint32_t n,
                         uint64_t n_bytes, uint32_t* __restrict__ lens, uint64_t* __restrict__ keys,
@@ -495,7 +514,7 @@ __global__ void k_keys0(const uint8_t* __restrict__ text, const uint64_t* __rest
   if (len && text[b - 1] == '\n') --len;
   const uint32_t l32 = len < 0xFFFFFFFFull ? (uint32_t)len : 0xFFFFFFFFu;
   lens[j] = l32;
-  keys[j] = chunk_key(text, n_bytes, a, l32, 0);
+  keys[j] = chunk_key(text, n_bytes, a, l32, 0u);
   ids[j] = j;
 }
 
@@ -550,14 +569,71 @@ struct Act {               // an unsettled line: its id and the position its gro
   uint32_t id, gs;
 };
 
+// the window of a class: its depth (bytes all its lines share, cdep) plus the
+// further common prefix k_lcp found (cmin), both indexed by the class start
 __global__ void k_keys(const uint8_t* __restrict__ text, const uint64_t* __restrict__ off,
                        const uint32_t* __restrict__ lens, uint64_t n_bytes, const Act* __restrict__ act, uint32_t m,
-                       uint32_t round, uint64_t* __restrict__ keys, uint64_t* __restrict__ vals) {
+                       const uint32_t* __restrict__ cdep, const uint32_t* __restrict__ cmin,
+                       uint64_t* __restrict__ keys, uint64_t* __restrict__ vals) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= m) return;
   const Act x = act[j];
-  keys[j] = chunk_key(text, n_bytes, off[x.id], lens[x.id], round);
+  keys[j] = chunk_key(text, n_bytes, off[x.id], lens[x.id], (uint64_t)cdep[x.gs] + cmin[x.gs]);
   vals[j] = (uint64_t)x.gs << 32 | x.id;
+}
+
+// Common-prefix skip: every line of a class is compared with the class's
+// first line from the class depth on; the class minimum of those lengths
+// (segmented over the wave, one atomicMin per class and wave into cmin[gs],
+// set to ~0 by k_cls_first) is where the class's lines first differ, so the
+// next window starts there -- the bytes all of them share (a syslog header,
+// "Built inbound TCP connection ...") cost one pass instead of a round per 7
+// bytes.  Capped at kLcpMax bytes per pass (the window then starts there).
+constexpr uint32_t kLcpMax = 4096;
+__global__ void k_lcp(const uint8_t* __restrict__ text, uint64_t n_bytes, const uint64_t* __restrict__ off,
+                      const uint32_t* __restrict__ lens, const Act* __restrict__ act,
+                      const uint32_t* __restrict__ first1, uint32_t m, const uint32_t* __restrict__ cdep,
+                      uint32_t* __restrict__ cmin) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t e = 0xFFFFFFFFu, gs = 0xFFFFFFFFu;
+  if (j < m) {
+    const Act x = act[j];
+    gs = x.gs;
+    const uint32_t y = act[first1[j] - 1].id;
+    const uint32_t d = cdep[gs], la = lens[x.id], lb = lens[y];
+    const uint32_t ra = la > d ? la - d : 0u, rb = lb > d ? lb - d : 0u;
+    const uint32_t lim = (ra < rb ? ra : rb) < kLcpMax ? (ra < rb ? ra : rb) : kLcpMax;
+    e = lim;
+    if (y != x.id) {
+      const uint64_t pa = off[x.id] + d, pb = off[y] + d;
+      for (uint32_t p = 0; p < lim; p += 8) {
+        const uint64_t ka = line_chunk8(text, n_bytes, pa + p, la - d - p),
+                       kb = line_chunk8(text, n_bytes, pb + p, lb - d - p);
+        if (ka != kb) {
+          const uint32_t q = p + (uint32_t)__builtin_clzll(ka ^ kb) / 8u;
+          e = q < lim ? q : lim;
+          break;
+        }
+      }
+    }
+  }
+  // segmented min over the wave (a class's elements are contiguous)
+  const uint32_t lane = __lane_id();
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t ye = (uint32_t)__shfl_down((int)e, o), yg = (uint32_t)__shfl_down((int)gs, o);
+    if (lane + o < 64 && yg == gs && ye < e) e = ye;
+  }
+  const uint32_t pg = (uint32_t)__shfl_up((int)gs, 1);
+  if (j < m && (lane == 0 || pg != gs)) atomicMin(&cmin[gs], e);
+}
+
+// a window that split nothing (only after a capped k_lcp): the classes move on by 7 bytes
+__global__ void k_dep_adv(const Act* __restrict__ act, uint32_t m, const uint32_t* __restrict__ cdep,
+                          const uint32_t* __restrict__ cmin, uint32_t* __restrict__ cnext) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const uint32_t g = act[j].gs;
+  cnext[g] = cdep[g] + cmin[g] + 7u;   // (every element writes its class's one value)
 }
 
 // 1 if this round can change anything: a group whose keys differ, or a line
@@ -642,12 +718,18 @@ __global__ void k_settle(const uint64_t* __restrict__ keys, const uint32_t* __re
   keep[j] = settled ? 0u : 1u;
 }
 
+// the kept elements into act; their new classes' depth into cnext[new start]:
+// the old class's window end (cdep + cmin of the old start gs_old, 0 when
+// gs_old is null) + adv (7: the window matched; 0: the group stage)
 __global__ void k_compact(const uint32_t* __restrict__ ids, const uint32_t* __restrict__ ngs1,
                           const uint32_t* __restrict__ keep, const uint32_t* __restrict__ slot, uint32_t m,
-                          Act* __restrict__ out) {
+                          Act* __restrict__ out, const uint32_t* __restrict__ gs_old, const uint32_t* __restrict__ cdep,
+                          const uint32_t* __restrict__ cmin, uint32_t* __restrict__ cnext, uint32_t adv) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= m || !keep[j]) return;
-  out[slot[j]] = Act{ids[j], ngs1[j] - 1};
+  const uint32_t g = ngs1[j] - 1;
+  out[slot[j]] = Act{ids[j], g};
+  cnext[g] = (gs_old ? cdep[gs_old[j]] + cmin[gs_old[j]] : 0u) + adv;   // (the same value from every member)
 }
 
 // ---- small-class finish: a class (lines equal in their first `depth` bytes,
@@ -658,26 +740,6 @@ __global__ void k_compact(const uint32_t* __restrict__ ids, const uint32_t* __re
 // live window nearly every class is small (lines of one rule that share a
 // second), so the global rounds stop early.
 constexpr uint32_t kSmallClass = 64;
-
-// 8 bytes of a line from byte p of the text, big-endian, zero past `rem`
-// (rem >= 1 bytes of the line remain at p); text is 4-byte aligned.
-__device__ __forceinline__ uint64_t line_chunk8(const uint8_t* __restrict__ text, uint64_t n_bytes, uint64_t p,
-                                                uint32_t rem) {
-  uint64_t k;
-  if (p + 12 <= n_bytes) {
-    const uint32_t* t32 = reinterpret_cast<const uint32_t*>(text);
-    const uint64_t q = p >> 2;
-    const uint32_t sh = (uint32_t)(p & 3) * 8;
-    const uint64_t lo = (uint64_t)t32[q] | ((uint64_t)t32[q + 1] << 32);
-    const uint64_t x = sh ? (lo >> sh) | ((uint64_t)t32[q + 2] << (64 - sh)) : lo;
-    k = __builtin_bswap64(x);
-  } else {
-    k = 0;
-    for (uint32_t j = 0; j < 8; ++j) k = k << 8 | (p + j < n_bytes ? text[p + j] : 0u);
-  }
-  if (rem < 8) k &= ~0ull << (64 - 8 * rem);
-  return k;
-}
 
 // <0, 0, >0: line a vs line b from byte `depth` (LC_ALL=C order: bytes, then length)
 __device__ __forceinline__ int cmp_lines(const uint8_t* __restrict__ text, uint64_t n_bytes, uint64_t a, uint32_t la,
@@ -692,10 +754,14 @@ __device__ __forceinline__ int cmp_lines(const uint8_t* __restrict__ text, uint6
 }
 
 // per element of act: 1 + index of its class's first element at class starts, else 0
-__global__ void k_cls_first(const Act* __restrict__ act, uint32_t m, uint32_t* __restrict__ out) {
+// (cmin non-null: the class's k_lcp minimum is reset to ~0 at its first element)
+__global__ void k_cls_first(const Act* __restrict__ act, uint32_t m, uint32_t* __restrict__ out,
+                            uint32_t* __restrict__ cmin) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= m) return;
-  out[j] = (j == 0 || act[j].gs != act[j - 1].gs) ? j + 1 : 0u;
+  const bool f = j == 0 || act[j].gs != act[j - 1].gs;
+  out[j] = f ? j + 1 : 0u;
+  if (f && cmin) cmin[act[j].gs] = 0xFFFFFFFFu;
 }
 
 // (after the max-scan of k_cls_first): the class size, stored at its first element
@@ -710,7 +776,7 @@ __global__ void k_cls_size(const Act* __restrict__ act, const uint32_t* __restri
 __global__ void k_finish_small(const uint8_t* __restrict__ text, uint64_t n_bytes, const uint64_t* __restrict__ off,
                                const uint32_t* __restrict__ lens, const Act* __restrict__ act,
                                const uint32_t* __restrict__ first1, const uint32_t* __restrict__ size, uint32_t m,
-                               uint32_t depth, uint64_t base, uint64_t* __restrict__ order,
+                               const uint32_t* __restrict__ cdep, uint64_t base, uint64_t* __restrict__ order,
                                uint32_t* __restrict__ keep) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= m) return;
@@ -722,7 +788,7 @@ __global__ void k_finish_small(const uint8_t* __restrict__ text, uint64_t n_byte
   keep[j] = 0u;
   const Act x = act[j];
   const uint64_t a = off[x.id];
-  const uint32_t la = lens[x.id];
+  const uint32_t la = lens[x.id], depth = cdep[x.gs];
   uint32_t rank = 0;
   for (uint32_t k = cs; k < cs + cn; ++k) {
     if (k == j) continue;
@@ -1151,8 +1217,8 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
   const size_t N = ((size_t)n + 63) / 64 * 64;
   const size_t H = rs_hist_len(N), SL = scan_sums_len(H > N ? H : N);
   // keysA/keysB/keysT u64, valsA/valsB/valsT u64, gs/ids/first/pos/bstart/keep/slot/lens u32,
-  // act/act3 Act (and a spare), radix histogram + scan sums, flag words
-  const size_t bytes = N * (8 * 6 + 4 * 8 + 8 * 3) + (H + SL) * 4 + 512;
+  // act/act3 Act (and a spare), class depths cdep/cnext/cmin u32, radix histogram + scan sums, flag words
+  const size_t bytes = N * (8 * 6 + 4 * 8 + 8 * 3 + 4 * 3) + (H + SL) * 4 + 512;
   Scratch S{c, st};
   TPCHK(c, hipMallocAsync(&S.base, bytes, st));
   char* p = static_cast<char*>(S.base);
@@ -1172,6 +1238,10 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
   uint32_t* lens = reinterpret_cast<uint32_t*>(p); p += N * 4;
   Act* act = reinterpret_cast<Act*>(p); p += N * 8;
   Act* act3 = reinterpret_cast<Act*>(p); p += N * 8;
+  p += N * 8;   // (spare)
+  uint32_t* cdep = reinterpret_cast<uint32_t*>(p); p += N * 4;    // per class start: bytes its lines share
+  uint32_t* cnext = reinterpret_cast<uint32_t*>(p); p += N * 4;   // ... of the classes the next round forms
+  uint32_t* cmin = reinterpret_cast<uint32_t*>(p); p += N * 4;    // per class start: k_lcp's further common bytes
   uint32_t* hist = reinterpret_cast<uint32_t*>(p); p += H * 4;
   uint32_t* sums = reinterpret_cast<uint32_t*>(p); p += SL * 4;
   uint32_t* flags = reinterpret_cast<uint32_t*>((reinterpret_cast<uintptr_t>(p) + 63) & ~(uintptr_t)63);
@@ -1189,7 +1259,7 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
   uint64_t n_bytes = 0;
   TPCHK(c, hipMemcpyAsync(&n_bytes, d_off + n, 8, hipMemcpyDeviceToHost, st));
   TPCHK(c, hipStreamSynchronize(st));
-  uint32_t round0 = 1;
+  uint32_t adv0 = 7;   // the depth of the classes the first stage leaves
   if (d_group) {
     // grouped: ranks of (group, line bytes); the groups come first (one sort
     // over the bits a group key has), so only lines of one group are ever
@@ -1213,7 +1283,7 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
     maxscan(bstart, first, n);
     hipLaunchKernelGGL(k_grp_settle, dim3(blocks(n, 256)), dim3(256), 0, st, gkB, idsB, first, n, gmax + 1, base,
                        d_order, keep);
-    round0 = 0;
+    adv0 = 0;
   } else {
     // round 0: all lines
     hipLaunchKernelGGL(k_keys0, dim3(blocks(n, 256)), dim3(256), 0, st, d_text, d_off, n, n_bytes, lens, keysA, idsA);
@@ -1225,21 +1295,22 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
                        first, n, base, d_order, keep);
   }
   exscan(keep, slot, n);
-  hipLaunchKernelGGL(k_compact, dim3(blocks(n, 256)), dim3(256), 0, st, idsB, first, keep, slot, n, act);
+  hipLaunchKernelGGL(k_compact, dim3(blocks(n, 256)), dim3(256), 0, st, idsB, first, keep, slot, n, act,
+                     (const uint32_t*)nullptr, (const uint32_t*)nullptr, (const uint32_t*)nullptr, cdep, adv0);
   uint32_t m = 0, lastk = 0;
   TPCHK(c, hipMemcpyAsync(&m, slot + n - 1, 4, hipMemcpyDeviceToHost, st));
   TPCHK(c, hipMemcpyAsync(&lastk, keep + n - 1, 4, hipMemcpyDeviceToHost, st));
   TPCHK(c, hipStreamSynchronize(st));
   m += lastk;
   uint32_t* live = flags;   // [0] the round splits something, [1..2] the key bits that vary
-  for (uint32_t round = round0; m > 0; ++round) {
+  while (m > 0) {
     // the classes of at most kSmallClass lines are ranked here (their lines
-    // agree on bytes [0, 7 * round)); the others go on to the next round
-    hipLaunchKernelGGL(k_cls_first, dim3(blocks(m, 256)), dim3(256), 0, st, act, m, bstart);
+    // agree on bytes [0, cdep[class])); the others go on
+    hipLaunchKernelGGL(k_cls_first, dim3(blocks(m, 256)), dim3(256), 0, st, act, m, bstart, (uint32_t*)nullptr);
     maxscan(bstart, first, m);
     hipLaunchKernelGGL(k_cls_size, dim3(blocks(m, 256)), dim3(256), 0, st, act, first, m, pos);
     hipLaunchKernelGGL(k_finish_small, dim3(blocks(m, 256)), dim3(256), 0, st, d_text, n_bytes, d_off, lens, act,
-                       first, pos, m, 7u * round, base, d_order, keep);
+                       first, pos, m, cdep, base, d_order, keep);
     exscan(keep, slot, m);
     hipLaunchKernelGGL(k_compact_act, dim3(blocks(m, 256)), dim3(256), 0, st, act, keep, slot, m, act3);
     {
@@ -1253,17 +1324,28 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
       act3 = sw;
     }
     if (m == 0) break;
-    hipLaunchKernelGGL(k_keys, dim3(blocks(m, 256)), dim3(256), 0, st, d_text, d_off, lens, n_bytes, act, m, round,
-                       keysA, valsA);
-    // rounds inside a shared prefix (e.g. lines of one second share ~90 bytes)
-    // change nothing: detect them with one pass and skip the sorts; the sort
-    // of a live round runs over the key bits that vary only
+    // the bytes every line of a class shares past its depth are skipped:
+    // the window starts at the class's first differing byte
+    hipLaunchKernelGGL(k_cls_first, dim3(blocks(m, 256)), dim3(256), 0, st, act, m, bstart, cmin);
+    maxscan(bstart, first, m);
+    hipLaunchKernelGGL(k_lcp, dim3(blocks(m, 256)), dim3(256), 0, st, d_text, n_bytes, d_off, lens, act, first, m,
+                       cdep, cmin);
+    hipLaunchKernelGGL(k_keys, dim3(blocks(m, 256)), dim3(256), 0, st, d_text, d_off, lens, n_bytes, act, m, cdep,
+                       cmin, keysA, valsA);
+    // a window that splits nothing (only after a k_lcp capped at kLcpMax):
+    // no sort; the sort of a live window runs over the key bits that vary only
     TPCHK(c, hipMemsetAsync(live, 0, 12, st));
     hipLaunchKernelGGL(k_round_live, dim3(blocks(m, 256)), dim3(256), 0, st, keysA, act, m, live);
     uint32_t h_live[3] = {0, 0, 0};
     TPCHK(c, hipMemcpyAsync(h_live, live, 12, hipMemcpyDeviceToHost, st));
     TPCHK(c, hipStreamSynchronize(st));
-    if (!h_live[0]) continue;
+    if (!h_live[0]) {
+      hipLaunchKernelGGL(k_dep_adv, dim3(blocks(m, 256)), dim3(256), 0, st, act, m, cdep, cmin, cnext);
+      uint32_t* sw = cdep;
+      cdep = cnext;
+      cnext = sw;
+      continue;
+    }
     const uint64_t vary = (uint64_t)h_live[2] << 32 | h_live[1];
     const unsigned b0 = vary ? (unsigned)__builtin_ctzll(vary) : 0u;
     const unsigned b1 = vary ? 64u - (unsigned)__builtin_clzll(vary) : 0u;
@@ -1283,7 +1365,11 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
                        keep);
     // slot (new group start + 1) is still needed by k_compact: scan the keep flags into `first`
     exscan(keep, first, m);
-    hipLaunchKernelGGL(k_compact, dim3(blocks(m, 256)), dim3(256), 0, st, ids, slot, keep, first, m, act);
+    hipLaunchKernelGGL(k_compact, dim3(blocks(m, 256)), dim3(256), 0, st, ids, slot, keep, first, m, act,
+                       (const uint32_t*)gs, (const uint32_t*)cdep, (const uint32_t*)cmin, cnext, 7u);
+    uint32_t* sw = cdep;
+    cdep = cnext;
+    cnext = sw;
     uint32_t nm = 0;
     TPCHK(c, hipMemcpyAsync(&nm, first + m - 1, 4, hipMemcpyDeviceToHost, st));
     TPCHK(c, hipMemcpyAsync(&lastk, keep + m - 1, 4, hipMemcpyDeviceToHost, st));

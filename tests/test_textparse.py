@@ -344,6 +344,13 @@ def test_gpu_order_keys_adversarial(engine):
             lines.append(long_prefix + bytes(rng.choice(b'0123\x00\xff') for _ in range(rng.randrange(0, 12))))
         else:
             lines.append(bytes(rng.randrange(0, 256) for _ in range(rng.randrange(0, 30))).replace(b'\n', b' '))
+    # classes past the small-class finisher (> 64 lines): a common prefix past
+    # one common-prefix pass (> 4096 bytes), identical long lines, a prefix
+    # that ends inside another line's shared run
+    huge = b'x' * 5000
+    lines += [huge + bytes(rng.choice(b'01\x00') for _ in range(rng.randrange(0, 5))) for _ in range(150)]
+    lines += [b'y' * 300] * 100 + [b'y' * 299] * 70 + [b'y' * 301 + b'z'] * 70
+    rng.shuffle(lines)
     data = b''.join(l + b'\n' for l in lines)
     import torch
     from ruleset_analysis_amd import native  # noqa: F401
