@@ -152,6 +152,9 @@ __global__ void k_set_u64(uint64_t* p, uint64_t v) { *p = v; }
 // 28 KB of staged text + the scan's slots and tables: four workgroups per CU
 // (a workgroup whose lines average more than 224 B defers them to the slow pass)
 constexpr uint32_t kParseWG = 128, kStageBytes = 28672;
+#ifndef RSA_TP_PROF
+#define RSA_TP_PROF 0   // PROFILING builds only (results invalid): 1 template scan without tpl_finish, 2 no scan either
+#endif
 
 // A line the template pass defers (rsa_text::kLineDefer): its index is
 // appended to the slow list (one device atomic per wave).
@@ -296,8 +299,12 @@ __global__ __launch_bounds__(kParseWG) void k_parse(const uint8_t* __restrict__ 
     } else if (staged) {
       const rsa_text::WordLn s{sm, (uint32_t)(a - base), (uint32_t)len};
       uint32_t* slot = tslot + threadIdx.x * rsa_text::tpl::kSlotWords;
-      if (!(rsa_text::tpl::scan(s, tprog, tcls, slot) &&
-            rsa_text::tpl_finish(s, slot, ifcs, n_ifcs, spells, n_spells, tup, ts, d))) {
+      if (RSA_TP_PROF == 2) {
+        d = RSA_LINE_NOACL + (s[len > 1 ? 1 : 0] == 0xFFu);
+      } else if (RSA_TP_PROF == 1) {
+        d = RSA_LINE_NOACL + !rsa_text::tpl::scan(s, tprog, tcls, slot);
+      } else if (!(rsa_text::tpl::scan(s, tprog, tcls, slot) &&
+                   rsa_text::tpl_finish(s, slot, ifcs, n_ifcs, spells, n_spells, tup, ts, d))) {
         tup = rsa_tuple{0u, 0u, 0, 0, 0, 0, 0};
         ts = 0;
         d = rsa_text::kLineDefer;
@@ -381,10 +388,14 @@ __global__ __launch_bounds__(kParseWG) void k_parse_win(const uint8_t* __restric
     uint32_t B[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) B[k] = __builtin_amdgcn_alignbit(X[k + 1], X[k], r);
+    if (RSA_TP_PROF == 2) {
+      st.ok ^= B[0] ^ B[1] ^ B[2] ^ B[3];   // (the loads only)
+    } else {
 #pragma unroll
-    for (uint32_t k = 0; k < 16; ++k) {
-      const uint32_t idx = base + k;
-      step(st, idx, (B[k >> 2] >> (8 * (k & 3))) & 0xFFu, lt01(idx, n), tprog, tcls, slot);
+      for (uint32_t k = 0; k < 16; ++k) {
+        const uint32_t idx = base + k;
+        step(st, idx, (B[k >> 2] >> (8 * (k & 3))) & 0xFFu, lt01(idx, n), tprog, tcls, slot);
+      }
     }
     w0 = w1;
     w1 = w2;
@@ -393,7 +404,9 @@ __global__ __launch_bounds__(kParseWG) void k_parse_win(const uint8_t* __restric
   if (!have) return;
   rsa_tuple tup = {0u, 0u, 0, 0, 0, 0, 0};
   uint32_t ts = 0, d = rsa_text::kLineDefer;
-  if (scannable && st.ok && tprog[st.seg] == kEndSeg) {
+  if (RSA_TP_PROF) {
+    d = RSA_LINE_NOACL + (st.ok == 7u);
+  } else if (scannable && st.ok && tprog[st.seg] == kEndSeg) {
     const uint64_t nw = n_bytes >> 2;
     uint32_t tail = 0;
     for (uint32_t k = 0; k < (uint32_t)(n_bytes & 3u); ++k) tail |= (uint32_t)text[4 * nw + k] << (8 * k);
