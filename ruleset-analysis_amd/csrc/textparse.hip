@@ -652,15 +652,19 @@ __global__ void k_dep_adv(const Act* __restrict__ act, uint32_t m, const uint32_
 // 1 if this round can change anything: a group whose keys differ, or a line
 // that ends in this window (else the round is skipped: no sort, no settle)
 // live[1..2]: the OR over all keys of (key ^ keys[0]) -- the bits that vary
-// this round; the sort then runs over those bits only
+// this round; the sort then runs over those bits only.  live[3]: some class
+// has a key below its predecessor's -- else every class is already in key
+// order (time-ordered logs: the header windows) and the round needs no sort
 __global__ void k_round_live(const uint64_t* __restrict__ keys, const Act* __restrict__ act, uint32_t m,
                              uint32_t* __restrict__ live) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t d = 0;
   if (j < m) {
     const bool ended = (keys[j] & 0xFFu) < 8u;
-    const bool split = j > 0 && act[j].gs == act[j - 1].gs && keys[j] != keys[j - 1];
+    const bool same = j > 0 && act[j].gs == act[j - 1].gs;
+    const bool split = same && keys[j] != keys[j - 1];
     if (ended || split) live[0] = 1u;
+    if (same && keys[j] < keys[j - 1]) live[3] = 1u;
     d = keys[j] ^ keys[0];
   }
   uint32_t lo = (uint32_t)d, hi = (uint32_t)(d >> 32);
@@ -672,6 +676,16 @@ __global__ void k_round_live(const uint64_t* __restrict__ keys, const Act* __res
     if (lo) atomicOr(&live[1], lo);
     if (hi) atomicOr(&live[2], hi);
   }
+}
+
+// a round already in (class, key) order: the values split into gs / ids in place
+__global__ void k_split_vals(const uint64_t* __restrict__ vals, uint32_t m, uint32_t* __restrict__ gs,
+                             uint32_t* __restrict__ ids) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const uint64_t v = vals[j];
+  gs[j] = (uint32_t)(v >> 32);
+  ids[j] = (uint32_t)v;
 }
 
 __global__ void k_gs_iota(const uint64_t* __restrict__ vals, uint32_t m, uint32_t* __restrict__ gs,
@@ -1347,10 +1361,10 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
                        cmin, keysA, valsA);
     // a window that splits nothing (only after a k_lcp capped at kLcpMax):
     // no sort; the sort of a live window runs over the key bits that vary only
-    TPCHK(c, hipMemsetAsync(live, 0, 12, st));
+    TPCHK(c, hipMemsetAsync(live, 0, 16, st));
     hipLaunchKernelGGL(k_round_live, dim3(blocks(m, 256)), dim3(256), 0, st, keysA, act, m, live);
-    uint32_t h_live[3] = {0, 0, 0};
-    TPCHK(c, hipMemcpyAsync(h_live, live, 12, hipMemcpyDeviceToHost, st));
+    uint32_t h_live[4] = {0, 0, 0, 0};
+    TPCHK(c, hipMemcpyAsync(h_live, live, 16, hipMemcpyDeviceToHost, st));
     TPCHK(c, hipStreamSynchronize(st));
     if (!h_live[0]) {
       hipLaunchKernelGGL(k_dep_adv, dim3(blocks(m, 256)), dim3(256), 0, st, act, m, cdep, cmin, cnext);
@@ -1359,16 +1373,21 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
       cnext = sw;
       continue;
     }
-    const uint64_t vary = (uint64_t)h_live[2] << 32 | h_live[1];
-    const unsigned b0 = vary ? (unsigned)__builtin_ctzll(vary) : 0u;
-    const unsigned b1 = vary ? 64u - (unsigned)__builtin_clzll(vary) : 0u;
-    // stable LSD: by the chunk key, then by the group start
-    radix_pairs<uint64_t, uint64_t>(st, keysA, keysB, valsA, valsB, m, b0, b1, keysT, valsT, hist, sums);
-    hipLaunchKernelGGL(k_gs_iota, dim3(blocks(m, 256)), dim3(256), 0, st, valsB, m, gs, ids);
-    // by group start (only the bits a position can have), carrying the index
-    radix_pairs<uint32_t, uint32_t>(st, gs, first, ids, pos, m, 0, gbits, reinterpret_cast<uint32_t*>(keysT), idsT,
-                                    hist, sums);
-    hipLaunchKernelGGL(k_gather, dim3(blocks(m, 256)), dim3(256), 0, st, keysB, valsB, pos, m, keysA, gs, ids);
+    if (!h_live[3]) {
+      // every class already in key order: no sort
+      hipLaunchKernelGGL(k_split_vals, dim3(blocks(m, 256)), dim3(256), 0, st, valsA, m, gs, ids);
+    } else {
+      const uint64_t vary = (uint64_t)h_live[2] << 32 | h_live[1];
+      const unsigned b0 = vary ? (unsigned)__builtin_ctzll(vary) : 0u;
+      const unsigned b1 = vary ? 64u - (unsigned)__builtin_clzll(vary) : 0u;
+      // stable LSD: by the chunk key, then by the group start
+      radix_pairs<uint64_t, uint64_t>(st, keysA, keysB, valsA, valsB, m, b0, b1, keysT, valsT, hist, sums);
+      hipLaunchKernelGGL(k_gs_iota, dim3(blocks(m, 256)), dim3(256), 0, st, valsB, m, gs, ids);
+      // by group start (only the bits a position can have), carrying the index
+      radix_pairs<uint32_t, uint32_t>(st, gs, first, ids, pos, m, 0, gbits, reinterpret_cast<uint32_t*>(keysT), idsT,
+                                      hist, sums);
+      hipLaunchKernelGGL(k_gather, dim3(blocks(m, 256)), dim3(256), 0, st, keysB, valsB, pos, m, keysA, gs, ids);
+    }
     // now keysA / gs / ids are in (group start, chunk key) order
     hipLaunchKernelGGL(k_run_first, dim3(blocks(m, 256)), dim3(256), 0, st, gs, m, bstart);
     maxscan(bstart, first, m);
