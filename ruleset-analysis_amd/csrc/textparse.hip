@@ -183,7 +183,7 @@ __global__ __launch_bounds__(kParseWG) void k_parse(const uint8_t* __restrict__ 
                                                     uint32_t n_spells, rsa_tuple* __restrict__ tuples,
                                                     uint32_t* __restrict__ ts_out, uint32_t* __restrict__ disp,
                                                     uint32_t* __restrict__ slow_idx, unsigned int* __restrict__ slow_n) {
-  __shared__ uint32_t sm[kDirect ? 1 : kStageBytes / 4];
+  __shared__ uint32_t sm[kDirect ? 1 : kStageBytes / 4 + 8];   // (+8: tpl_finish's 16-B field reads past a line)
   // the template scan (rsa_text::tpl) over the staged lines; the direct mode
   // keeps the per-lane template path (the scan's byte-per-step HBM loads were
   // 2.3x slower there: profiles/r03y_text_parse_modes.txt)

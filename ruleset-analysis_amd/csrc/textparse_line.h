@@ -729,50 +729,169 @@ constexpr ClsTable cls_table() {
 
 }  // namespace tpl
 
+// ---- 16 bytes of a line in registers (tpl_finish).  Each field is read as
+// one block (a few independent word loads, all issued before any test) and
+// decoded with selects, instead of one dependent byte load per step of a
+// per-field loop.  Bytes past the line are unspecified: callers mask by the
+// field's length.
+struct B16 {
+  uint32_t w[4];
+  RSA_HD uint32_t b(uint32_t i) const { return (w[i >> 2] >> (8u * (i & 3u))) & 0xFFu; }   // i static
+};
+RSA_HD uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t r) {   // (hi:lo) >> r, r < 32
+  return r ? (lo >> r) | (hi << (32u - r)) : lo;
+}
+RSA_HD B16 funnel5(const uint32_t (&x)[5], uint32_t r) {
+  return B16{{funnel(x[1], x[0], r), funnel(x[2], x[1], r), funnel(x[3], x[2], r), funnel(x[4], x[3], r)}};
+}
+template <class S>
+RSA_HD B16 bytes16(const S& s, uint32_t p) {   // any accessor: byte reads, zero past the line
+  B16 r{{0u, 0u, 0u, 0u}};
+  for (uint32_t i = 0; i < 16; ++i)
+    if (p + i < s.n) r.w[i >> 2] |= (uint32_t)s[p + i] << (8u * (i & 3u));
+  return r;
+}
+// LDS-staged words: the buffer must stay readable 20 bytes past the line
+RSA_HD B16 bytes16(const WordLn& s, uint32_t p) {
+  const uint32_t pos = s.o + p, q = pos >> 2;
+  const uint32_t x[5] = {s.w32[q], s.w32[q + 1], s.w32[q + 2], s.w32[q + 3], s.w32[q + 4]};
+  return funnel5(x, (pos & 3u) * 8u);
+}
+RSA_HD B16 bytes16(const GWordU& s, uint32_t p) {
+  const uint64_t pos = s.o + p, q = pos >> 2;
+  uint32_t x[5];
+  for (uint32_t k = 0; k < 5; ++k) x[k] = q + k < s.nw ? s.w32[q + k] : (q + k == s.nw ? s.tail : 0u);
+  return funnel5(x, (uint32_t)(pos & 3u) * 8u);
+}
+// bytes [0, n) of a block as a little-endian mask per word
+RSA_HD uint32_t lmask(uint32_t word, uint32_t n) {
+  const uint32_t lo = 4u * word;
+  return n >= lo + 4 ? 0xFFFFFFFFu : (n <= lo ? 0u : (1u << (8u * (n - lo))) - 1u);
+}
+RSA_HD bool b16_eq(const B16& x, const B16& y, uint32_t n) {   // first n (<= 16) bytes equal
+  uint32_t d = 0;
+  for (uint32_t k = 0; k < 4; ++k) d |= (x.w[k] ^ y.w[k]) & lmask(k, n);
+  return d == 0;
+}
+RSA_HD bool b16_has(const B16& x, uint32_t n, uint32_t c) {   // byte c among the first n
+  uint32_t hit = 0;
+  for (uint32_t i = 0; i < 16; ++i) hit |= (uint32_t)(i < n) & (uint32_t)(x.b(i) == c);
+  return hit != 0;
+}
+// decimal value of the digits [o, o + n) of a block (n <= N, the text is digits)
+template <uint32_t N>
+RSA_HD uint32_t b16_num(const B16& x, uint32_t o, uint32_t n) {
+  uint32_t v = 0;
+  for (uint32_t i = 0; i < N; ++i) {
+    const uint32_t c = x.b(o + i) - '0';
+    v = i < n ? v * 10u + c : v;
+  }
+  return v;
+}
+// port_val of a digit field: saturating at 65536 (fields past 16 bytes: 65536, the general parse decides)
+RSA_HD uint32_t b16_port(const B16& x, uint32_t n) {
+  uint32_t v = n > 16u ? 65536u : 0u;
+  for (uint32_t i = 0; i < 16; ++i) {
+    const uint32_t t = v * 10u + (x.b(i) - '0');
+    v = (i < n && v < 65536u) ? (t > 65535u ? 65536u : t) : v;
+  }
+  return v;
+}
+RSA_HD B16 b16_shr(const B16& x, uint32_t nb) {   // drop the first nb (< 4) bytes
+  const uint32_t r = 8u * nb;
+  return B16{{funnel(x.w[1], x.w[0], r), funnel(x.w[2], x.w[1], r), funnel(x.w[3], x.w[2], r), funnel(0u, x.w[3], r)}};
+}
+// ipv4_canon over a block: d{1,3}(.d{1,3}){3}, no leading zeros, octets <= 255
+RSA_HD bool b16_ipv4(const B16& x, uint32_t n, uint32_t& v) {
+  uint32_t val = 0, oct = 0, olen = 0, nd = 0, bad = (uint32_t)(n > 15u), lz = 0;
+  for (uint32_t i = 0; i < 15; ++i) {
+    const uint32_t c = x.b(i), in = (uint32_t)(i < n), dot = (uint32_t)(c == '.'), dig = (uint32_t)(c - '0' < 10u);
+    const uint32_t ind = in & dot, ing = in & dig;
+    bad |= (in & (dot | dig)) ^ in;
+    bad |= ind & ((uint32_t)(olen == 0) | (uint32_t)(oct > 255u) | (uint32_t)(nd == 3));
+    bad |= ing & ((uint32_t)(olen == 3) | ((uint32_t)(olen >= 1) & lz));
+    lz = (ing & (uint32_t)(olen == 0)) ? (uint32_t)(c == '0') : lz;
+    val = ind ? (val << 8) | oct : val;
+    nd += ind;
+    oct = ind ? 0u : (ing ? oct * 10u + (c - '0') : oct);
+    olen = ind ? 0u : olen + ing;
+  }
+  bad |= (uint32_t)(olen == 0) | (uint32_t)(oct > 255u) | (uint32_t)(nd != 3);
+  v = (val << 8) | oct;
+  return !bad;
+}
+RSA_HD uint32_t b16_pack3(const B16& x) { return x.b(0) << 16 | x.b(1) << 8 | x.b(2); }
+RSA_HD bool b16_ulll(const B16& x) { return is_upper(x.b(0)) && is_lower(x.b(1)) && is_lower(x.b(2)); }
+constexpr uint32_t le4(char a, char b, char c, char d) {
+  return (uint32_t)(uint8_t)a | (uint32_t)(uint8_t)b << 8 | (uint32_t)(uint8_t)c << 16 | (uint32_t)(uint8_t)d << 24;
+}
+// a name field [a, a + n): no '-' in it
+template <class S>
+RSA_HD bool name_no_dash(const S& s, uint32_t a, uint32_t n, const B16& first) {
+  bool ok = !b16_has(first, n < 16 ? n : 16, '-');
+  for (uint32_t o = 16; o < n && ok; o += 16) ok = !b16_has(bytes16(s, a + o), n - o < 16 ? n - o : 16, '-');
+  return ok;
+}
+// a name field equal to an interface name (n <= RSA_IFC_NAME_MAX)
+template <class S>
+RSA_HD bool name_eq(const S& s, uint32_t a, uint32_t n, const B16& first, const char* name) {
+  bool eq = true;
+  for (uint32_t o = 0; o < n && eq; o += 16) {
+    const B16 x = o ? bytes16(s, a + o) : first;
+    B16 y{{0u, 0u, 0u, 0u}};
+    for (uint32_t i = 0; i < 16; ++i) y.w[i >> 2] |= (o + i < n ? (uint32_t)(uint8_t)name[o + i] : 0u) << (8u * (i & 3u));
+    eq = b16_eq(x, y, n - o < 16 ? n - o : 16);
+  }
+  return eq;
+}
+
 // parse_line for a line tpl::scan accepted, from its slots; false: leave the
 // line to the general parse (everything parse_line would send to the host,
-// and a '-' in an interface name, where the hit test must scan).
+// and a '-' in an interface name, where the hit test must scan).  The fields
+// are read as blocks (bytes16), all before the first test.
 template <class S, class Q>
 RSA_HD bool tpl_finish(const S& s, Q slot, const rsa_parse_ifc* ifcs, uint32_t n_ifcs, const rsa_parse_spell* spells,
                        uint32_t n_spells, rsa_tuple& tup, uint32_t& ts, uint32_t& d) {
   using namespace tpl;
   auto at = [&](uint32_t f) { return (uint32_t)slot[f] & 0xFFFFu; };
   auto len = [&](uint32_t f) { return ((uint32_t)slot[f] >> 16) & 0xFFu; };
-  auto span = [&](uint32_t f) { return Span{at(f), at(f) + len(f)}; };
-  auto num = [&](uint32_t f) { return small_num(s, span(f)); };   // <= 6 digits here
-  auto word3 = [&](uint32_t f) { const uint32_t a = at(f); return (uint32_t)(s[a] << 16 | s[a + 1] << 8 | s[a + 2]); };
-  auto ulll = [](uint32_t w) {   // [A-Z][a-z]{2}, packed big-endian in 24 bits
-    return is_upper(w >> 16 & 0xFFu) && is_lower(w >> 8 & 0xFFu) && is_lower(w & 0xFFu);
-  };
-  const uint32_t m2 = word3(fM2);
-  if (!ulll(word3(fM1)) || !ulll(m2)) return false;
-  const uint32_t tag = word3(fTAG);
-  if (len(fTAG) == 3 ? !(tag == pack3('A', 'S', 'A') || tag == pack3('P', 'I', 'X'))
-                     : !(tag == pack3('F', 'W', 'S') && s[at(fTAG) + 3] == 'M'))
-    return false;
-  const bool inbound = len(fDIR) == 7 && lit(s, at(fDIR), "inbound");
-  const bool outbound = len(fDIR) == 8 && lit(s, at(fDIR), "outbound");
-  if (!inbound && !outbound) return false;
-  const uint32_t proto = word3(fPROTO);
+  // Mmm ... HH:MM:SS | Mmm D YYYY | TAG-d-dddddd | DIR PROTO | IF:IP/P twice
+  const B16 bM1 = bytes16(s, at(fM1)), bHMS = bytes16(s, at(fHH)), bM2 = bytes16(s, at(fM2)),
+            bTag = bytes16(s, at(fTAG)), bDir = bytes16(s, at(fDIR)), bIf1 = bytes16(s, at(fIF1)),
+            bIp1 = bytes16(s, at(fIP1)), bP1 = bytes16(s, at(fP1)), bIf2 = bytes16(s, at(fIF2)),
+            bIp2 = bytes16(s, at(fIP2)), bP2 = bytes16(s, at(fP2));
+  const uint32_t m2 = b16_pack3(bM2);
+  const uint32_t ltag = len(fTAG), tag = b16_pack3(bTag);
+  bool ok = b16_ulll(bM1) && b16_ulll(bM2);
+  ok = ok && (ltag == 3 ? (tag == pack3('A', 'S', 'A') || tag == pack3('P', 'I', 'X'))
+                        : (tag == pack3('F', 'W', 'S') && bTag.b(3) == 'M'));
+  const uint32_t ldir = len(fDIR);
+  const bool inbound = ldir == 7 && bDir.w[0] == le4('i', 'n', 'b', 'o') && (bDir.w[1] & 0xFFFFFFu) == le4('u', 'n', 'd', 0);
+  const bool outbound = ldir == 8 && bDir.w[0] == le4('o', 'u', 't', 'b') && bDir.w[1] == le4('o', 'u', 'n', 'd');
+  ok = ok && (inbound || outbound);
+  // PROTO follows DIR and one space
+  const B16 bPr = outbound ? B16{{bDir.w[2] >> 8 | bDir.w[3] << 24, bDir.w[3] >> 8, 0u, 0u}}
+                           : B16{{bDir.w[2], bDir.w[3], 0u, 0u}};
+  const uint32_t proto = b16_pack3(bPr);
   const bool udp = proto == pack3('U', 'D', 'P');
-  if (!udp && proto != pack3('T', 'C', 'P')) return false;
-  if (!no_dash(s, span(fIF1)) || !no_dash(s, span(fIF2))) return false;   // '-' in an interface name
+  ok = ok && (udp || proto == pack3('T', 'C', 'P'));
+  const uint32_t l1 = len(fIF1), l2 = len(fIF2);
+  ok = ok && name_no_dash(s, at(fIF1), l1, bIf1) && name_no_dash(s, at(fIF2), l2, bIf2);   // '-' in a name
   uint32_t ip1 = 0, ip2 = 0;
-  if (!ipv4_canon(s, span(fIP1), ip1) || !ipv4_canon(s, span(fIP2), ip2)) return false;   // not canonical quads
-  const uint32_t p1 = port_val(s, span(fP1)), p2 = port_val(s, span(fP2));
-  if (p1 > 65535u || p2 > 65535u || !port_canon(s, span(fP2))) return false;   // long ports; TOPORT not canonical
+  ok = ok && b16_ipv4(bIp1, len(fIP1), ip1) && b16_ipv4(bIp2, len(fIP2), ip2);   // not canonical quads
+  const uint32_t lp1 = len(fP1), lp2 = len(fP2);
+  const uint32_t p1 = b16_port(bP1, lp1), p2 = b16_port(bP2, lp2);
+  ok = ok && p1 <= 65535u && p2 <= 65535u && (lp2 == 1 || bP2.b(0) != '0');   // long ports; TOPORT not canonical
+  if (!ok) return false;
   const uint32_t src = inbound ? ip1 : ip2, dst = inbound ? ip2 : ip1;
   const uint32_t sp = inbound ? p1 : p2, dp = inbound ? p2 : p1;
   // the interface of the ingress side
-  const uint32_t ia = inbound ? at(fIF1) : at(fIF2), il = inbound ? len(fIF1) : len(fIF2);
+  const uint32_t ia = inbound ? at(fIF1) : at(fIF2), il = inbound ? l1 : l2;
+  const B16 bIf = inbound ? bIf1 : bIf2;
   int32_t found = -1;
   if (il > RSA_IFC_NAME_MAX) return false;
-  for (uint32_t k = 0; k < n_ifcs && found < 0; ++k) {
-    if (ifcs[k].len != il) continue;
-    bool eq = true;
-    for (uint32_t c = 0; c < il && eq; ++c) eq = s[ia + c] == (uint8_t)ifcs[k].name[c];
-    if (eq) found = (int32_t)k;
-  }
+  for (uint32_t k = 0; k < n_ifcs && found < 0; ++k)
+    if (ifcs[k].len == il && name_eq(s, ia, il, bIf, ifcs[k].name)) found = (int32_t)k;
   tup = rsa_tuple{0u, 0u, 0, 0, 0, 0, 0};
   ts = 0;
   if (found < 0) {
@@ -787,19 +906,23 @@ RSA_HD bool tpl_finish(const S& s, Q slot, const rsa_parse_ifc* ifcs, uint32_t n
   const uint32_t lid = udp ? ifcs[found].list_udp : ifcs[found].list_tcp;
   if (lid == RSA_LIST_HOST) return false;
   // the reducer's fields: FROMIP = the first address, TOIP = the second, TOPORT = P2
-  const uint32_t sev = s[at(fSEV)] - '0', msg = num(fMSG);
+  const B16 bSm = b16_shr(bTag, ltag - 3);   // "TAG-d-dddddd" from the tag's last 3 bytes: d at 4, dddddd at 6
+  const uint32_t sev = bSm.b(4) - '0', msg = b16_num<6>(bSm, 6, 6);
   const bool hit = sev == 6 && (msg == 302013 || msg == 302015);
   uint32_t flags = RSA_F_VALID | RSA_F_BUILT | (hit ? RSA_F_HIT : 0u);
   // outbound: the reducer key is (IP1, IP2, P2) = (dst, src, sport) -- unless its
   // text equals the (src, dst, dport) one, which parse_line's first test takes
-  if (outbound && !(ip1 == ip2 && span_eq(s, span(fP1), span(fP2)))) flags |= RSA_F_SWAP;
+  if (outbound && !(ip1 == ip2 && lp1 == lp2 && b16_eq(bP1, bP2, lp1))) flags |= RSA_F_SWAP;
   if (hit) {
     // ts_code: HH:MM:SS of the syslog header, the device date's month, day, year
     const char* const months = "JanFebMarAprMayJunJulAugSepOctNovDec";
     int mo = -1;
     for (int k = 0; k < 12; ++k)
       if (m2 == pack3(months[3 * k], months[3 * k + 1], months[3 * k + 2])) mo = k;
-    const uint32_t y = num(fY), day = num(fD2), hh = num(fHH), mm = num(fMM), ss = num(fSS);
+    const uint32_t ld = len(fD2);   // "Mmm D YYYY" / "Mmm DD YYYY"
+    const uint32_t day = b16_num<2>(bM2, 4, ld);
+    const uint32_t y = ld == 1 ? b16_num<4>(bM2, 6, 4) : b16_num<4>(bM2, 7, 4);
+    const uint32_t hh = b16_num<2>(bHMS, 0, 2), mm = b16_num<2>(bHMS, 3, 2), ss = b16_num<2>(bHMS, 6, 2);
     if (mo < 0 || y < RSA_TS_YEAR0 || y >= RSA_TS_YEAR0 + 128 || day > 31 || hh > 23 || mm > 59 || ss > 59)
       return false;
     ts = ((((y - RSA_TS_YEAR0) * 12u + (uint32_t)mo) * 32u + day) * 86400u) + hh * 3600u + mm * 60u + ss;

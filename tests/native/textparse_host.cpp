@@ -84,8 +84,11 @@ extern "C" void template_check_host(const uint8_t* text, const uint64_t* off, ui
 // out[i] = 0 (not accepted: the slow pass decides), 1 (accepted, same
 // disposition / tuple / timestamp code as parse_line), 2 (accepted but
 // different -- a bug).
+// word = 1: tpl_finish reads through the LDS-staged word accessor (the buffer
+// must stay readable 20 bytes past off[n]), 0: byte reads.
 extern "C" void tpl_check_host(const uint8_t* text, const uint64_t* off, uint64_t n, const rsa_parse_ifc* ifcs,
-                               uint32_t n_ifcs, const rsa_parse_spell* spells, uint32_t n_spells, uint8_t* out) {
+                               uint32_t n_ifcs, const rsa_parse_spell* spells, uint32_t n_spells, uint8_t* out,
+                               int word) {
   using namespace rsa_text;
   uint32_t slot[tpl::kSlotWords];
   static constexpr tpl::ClsTable kCls = tpl::cls_table();
@@ -97,7 +100,10 @@ extern "C" void tpl_check_host(const uint8_t* text, const uint64_t* off, uint64_
     rsa_tuple t1, t2;
     uint32_t ts1 = 0, ts2 = 0, d1 = 0, d2 = 0;
     out[i] = 0;
-    if (!tpl::scan(s, tpl::kProg, kCls.t, slot) || !tpl_finish(s, slot, ifcs, n_ifcs, spells, n_spells, t1, ts1, d1))
+    if (!tpl::scan(s, tpl::kProg, kCls.t, slot)) continue;
+    const WordLn w{reinterpret_cast<const uint32_t*>(text), (uint32_t)a, (uint32_t)len};
+    if (!(word ? tpl_finish(w, slot, ifcs, n_ifcs, spells, n_spells, t1, ts1, d1)
+               : tpl_finish(s, slot, ifcs, n_ifcs, spells, n_spells, t1, ts1, d1)))
       continue;
     parse_line(s, ifcs, n_ifcs, spells, n_spells, t2, ts2, d2);
     const bool same = d1 == d2 && ts1 == ts2 && t1.src == t2.src && t1.dst == t2.dst && t1.sport == t2.sport &&

@@ -478,8 +478,8 @@ def test_template_fast_path_equals_general_parse():
     assert [a[k] for k in (3, 10, 11, 12, 13, 15, 16)] == [0] * 7, a.tolist()
 
 
-@pytest.mark.parametrize('seed', [1, 2, 3])
-def test_template_scan_equals_general_parse(seed):
+@pytest.mark.parametrize('seed,word', [(1, 0), (2, 0), (3, 0), (1, 1), (2, 1)])
+def test_template_scan_equals_general_parse(seed, word):
     """textparse_line.h tpl::scan + tpl_finish (k_parse's branch-free pass)
     give parse_line's exact disposition, tuple and timestamp code on every
     line they accept: rendered lines (nearly all accepted), fuzzed lines,
@@ -513,9 +513,10 @@ def test_template_scan_equals_general_parse(seed):
     sp = textparse.spell_table(list(textparse.DEFAULT_SPELLS))
     out = np.zeros(len(lines), np.uint8)
     p = lambda a: a.ctypes.data_as(ctypes.c_void_p)
-    buf = np.frombuffer(data, np.uint8).copy()
+    buf = np.zeros(len(data) + 64, np.uint32).view(np.uint8)   # 4-byte aligned, readable past the end
+    buf[:len(data)] = np.frombuffer(data, np.uint8)
     lib.tpl_check_host(p(buf), p(off), ctypes.c_uint64(len(lines)), p(ifcs), ctypes.c_uint32(len(ifcs)), p(sp),
-                       ctypes.c_uint32(len(sp)), p(out))
+                       ctypes.c_uint32(len(sp)), p(out), ctypes.c_int(word))
     assert not (out == 2).any(), [lines[i] for i in np.nonzero(out == 2)[0][:3]]
     assert (out[:len(clean)] == 1).mean() > 0.88
     a = out[len(clean) + len(fuzz):].tolist()
