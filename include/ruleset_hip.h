@@ -186,7 +186,8 @@ typedef struct rsa_pht_list {    /* 80 B: one list (or one chained chunk of a li
 #define RSA_OPT_STATS 10       /* PROFILING: count table work into the rsa_stats counters (default 0)                 */
 #define RSA_OPT_HOT_SPLIT 14   /* pre-combine regions holding > max(RSA_OPT_HOT_MIN, 4 x mean) records on all CUs (default 1) */
 #define RSA_OPT_HOT_MIN 15     /* hot-region minimum in records (default 65536; below it TESTING: any region above it is hot) */
-#define RSA_OPT_PARSE_MODE 16  /* text parse: 0 = each workgroup's lines staged in LDS (default), 1 = direct 4-byte HBM reads */
+#define RSA_OPT_PARSE_MODE 16  /* text parse: 0 = each workgroup's lines staged in LDS, 1 = direct 4-byte HBM reads,
+                                  2 = register-window 16-byte HBM reads (default; text not 16-byte aligned: 0) */
 #define RSA_OPT_REGION_IMPORT 17 /* rsa_import: records sorted by table region, merged per region in LDS (1, default) or device atomics per record (0) */
 #define RSA_OPT_OWNER_WORLD 19   /* multi-GPU merge (0 = off): the ctx's table also holds the merged entries of the rules it owns (gid % world == rank); rsa_export leaves those at home, rsa_emit returns only those */
 #define RSA_OPT_OWNER_RANK 20    /* this ctx's rank for RSA_OPT_OWNER_WORLD */

@@ -2455,6 +2455,14 @@ __global__ __launch_bounds__(kSelThreads) void k_cap_select(const unsigned long 
   const int top = range ? 63 - __builtin_clzll(range) : 0;     // highest set bit of the range
   int shift = top >= 8 ? top - 7 : 0;
   unsigned long long hi_mask = 0;                                // bits above the current digit, fixed so far
+  // exactly cap keys (the common case after a filter slice: the cap entries
+  // at or below the earlier selection, nothing new below it): the largest;
+  // cap 1: the smallest (workgroup-uniform: n, cap)
+  if (n == cap || cap == 1) {
+    if (threadIdx.x == 0) out[capped_gid[c]] = n == cap ? mx : mn;
+    __syncthreads();
+    continue;
+  }
   while (true) {
     for (int q = threadIdx.x; q < kWaves * 256; q += kSelThreads) (&hist[0][0])[q] = 0;
     __syncthreads();
@@ -2824,7 +2832,7 @@ struct rsa_ctx {
   uint32_t filter_len = 0;
   unsigned long long* d_packed = nullptr;   // k_count / k_aggregate packed counters (rules > kCnt)
   // hot-region split (k_hot_plan / k_hot_combine)
-  int parse_mode = 0;                       // RSA_OPT_PARSE_MODE (textparse.hip)
+  int parse_mode = 2;                       // RSA_OPT_PARSE_MODE (textparse.hip): register-window reads
   bool region_import = true;                // RSA_OPT_REGION_IMPORT: rsa_import by region sort + k_reduce
   bool slots_clean = true;                  // no slot holds a key of an earlier job (k_import's CAS claims need it)
   bool hot_split = true;                    // RSA_OPT_HOT_SPLIT

@@ -548,15 +548,30 @@ __global__ void k_grp0(const int32_t* __restrict__ group, const uint8_t* __restr
   ids[j] = j;
 }
 
+// Reductions to a few device words: a persistent grid (kRedGrid workgroups)
+// reduces in registers, waves and LDS, then one atomic per workgroup -- one
+// atomic per wave on the same word serialises ~n/64 atomics at one L2 address.
+constexpr uint32_t kRedGrid = 1024, kRedThreads = 256;
+
 // the largest group (atomicMax into *mx, zeroed by the caller)
-__global__ void k_grp_max(const int32_t* __restrict__ group, uint32_t n, uint32_t* __restrict__ mx) {
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  int32_t g = j < n ? group[j] : 0;
+__global__ __launch_bounds__(kRedThreads) void k_grp_max(const int32_t* __restrict__ group, uint32_t n,
+                                                         uint32_t* __restrict__ mx) {
+  __shared__ int32_t sh[kRedThreads / 64];
+  int32_t g = 0;
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+    const int32_t y = group[j];
+    g = y > g ? y : g;
+  }
   for (int o = 32; o > 0; o >>= 1) {
     const int32_t y = __shfl_xor(g, o);
     g = y > g ? y : g;
   }
-  if (__lane_id() == 0 && g > 0) atomicMax(mx, (uint32_t)g);
+  if (__lane_id() == 0) sh[threadIdx.x >> 6] = g;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (uint32_t w = 1; w < blockDim.x / 64; ++w) g = sh[w] > g ? sh[w] : g;
+    if (g > 0) atomicMax(mx, (uint32_t)g);
+  }
 }
 
 // after the sort by group: group starts (+1, max-scanned by the caller)
@@ -655,26 +670,33 @@ __global__ void k_dep_adv(const Act* __restrict__ act, uint32_t m, const uint32_
 // this round; the sort then runs over those bits only.  live[3]: some class
 // has a key below its predecessor's -- else every class is already in key
 // order (time-ordered logs: the header windows) and the round needs no sort
-__global__ void k_round_live(const uint64_t* __restrict__ keys, const Act* __restrict__ act, uint32_t m,
-                             uint32_t* __restrict__ live) {
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  uint64_t d = 0;
-  if (j < m) {
-    const bool ended = (keys[j] & 0xFFu) < 8u;
+// (persistent grid of kRedGrid x kRedThreads; one atomic per word and workgroup)
+__global__ __launch_bounds__(kRedThreads) void k_round_live(const uint64_t* __restrict__ keys,
+                                                            const Act* __restrict__ act, uint32_t m,
+                                                            uint32_t* __restrict__ live) {
+  __shared__ uint32_t sh[kRedThreads / 64][4];
+  uint32_t v[4] = {0u, 0u, 0u, 0u};
+  const uint64_t k0 = keys[0];
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m; j += gridDim.x * blockDim.x) {
+    const uint64_t k = keys[j];
+    const bool ended = (k & 0xFFu) < 8u;
     const bool same = j > 0 && act[j].gs == act[j - 1].gs;
-    const bool split = same && keys[j] != keys[j - 1];
-    if (ended || split) live[0] = 1u;
-    if (same && keys[j] < keys[j - 1]) live[3] = 1u;
-    d = keys[j] ^ keys[0];
+    const uint64_t kp = same ? keys[j - 1] : k;
+    v[0] |= (ended || kp != k) ? 1u : 0u;
+    v[3] |= k < kp ? 1u : 0u;
+    const uint64_t d = k ^ k0;
+    v[1] |= (uint32_t)d;
+    v[2] |= (uint32_t)(d >> 32);
   }
-  uint32_t lo = (uint32_t)d, hi = (uint32_t)(d >> 32);
-  for (int o = 32; o > 0; o >>= 1) {
-    lo |= (uint32_t)__shfl_xor((int)lo, o);
-    hi |= (uint32_t)__shfl_xor((int)hi, o);
-  }
-  if (__lane_id() == 0) {
-    if (lo) atomicOr(&live[1], lo);
-    if (hi) atomicOr(&live[2], hi);
+  for (int o = 32; o > 0; o >>= 1)
+    for (int q = 0; q < 4; ++q) v[q] |= (uint32_t)__shfl_xor((int)v[q], o);
+  if (__lane_id() == 0)
+    for (int q = 0; q < 4; ++q) sh[threadIdx.x >> 6][q] = v[q];
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    uint32_t x = 0;
+    for (uint32_t w = 0; w < blockDim.x / 64; ++w) x |= sh[w][threadIdx.x];
+    if (x) atomicOr(&live[threadIdx.x], x);
   }
 }
 
@@ -1293,7 +1315,8 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
     // compared (the reducer compares order keys of one rule's lines only), and
     // a group of one line is settled at once.  Then the byte rounds from round 0.
     TPCHK(c, hipMemsetAsync(flags, 0, 4, st));
-    hipLaunchKernelGGL(k_grp_max, dim3(blocks(n, 256)), dim3(256), 0, st, d_group, n, flags);
+    hipLaunchKernelGGL(k_grp_max, dim3(blocks(n, kRedThreads) < kRedGrid ? blocks(n, kRedThreads) : kRedGrid),
+                       dim3(kRedThreads), 0, st, d_group, n, flags);
     uint32_t gmax = 0;
     TPCHK(c, hipMemcpyAsync(&gmax, flags, 4, hipMemcpyDeviceToHost, st));
     TPCHK(c, hipStreamSynchronize(st));
@@ -1362,7 +1385,8 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
     // a window that splits nothing (only after a k_lcp capped at kLcpMax):
     // no sort; the sort of a live window runs over the key bits that vary only
     TPCHK(c, hipMemsetAsync(live, 0, 16, st));
-    hipLaunchKernelGGL(k_round_live, dim3(blocks(m, 256)), dim3(256), 0, st, keysA, act, m, live);
+    hipLaunchKernelGGL(k_round_live, dim3(blocks(m, kRedThreads) < kRedGrid ? blocks(m, kRedThreads) : kRedGrid),
+                       dim3(kRedThreads), 0, st, keysA, act, m, live);
     uint32_t h_live[4] = {0, 0, 0, 0};
     TPCHK(c, hipMemcpyAsync(h_live, live, 16, hipMemcpyDeviceToHost, st));
     TPCHK(c, hipStreamSynchronize(st));

@@ -304,7 +304,7 @@ def test_gpu_parse_fuzz_equals_host(engine, seed, mode):
     try:
         got = _compare(engine, 'fw1', good, db)
     finally:
-        engine.set_option(native.RSA_OPT_PARSE_MODE, 0)
+        engine.set_option(native.RSA_OPT_PARSE_MODE, 2)
     d = got.disposition
     # the fuzz reaches every outcome, and most lines stay on the device
     for k in (logparse.D_IGNORE, logparse.D_NOACL, logparse.D_MISSING, logparse.D_CLASSIFY):
