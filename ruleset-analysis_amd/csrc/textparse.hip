@@ -821,11 +821,15 @@ __global__ void k_cls_size(const Act* __restrict__ act, const uint32_t* __restri
   if (j + 1 == m || act[j + 1].gs != act[j].gs) size[first1[j] - 1] = j + 2 - first1[j];
 }
 
-// rank every element of a small class; keep[j] = 1 for the elements of large classes
+// rank every element of a small class; keep[j] = 1 for the elements of large
+// classes.  keys[j]: the element's window key at its class's window start
+// (k_keys): members are compared by key, and only members with equal keys
+// that both go on past the window by their bytes from the window's end.
 __global__ void k_finish_small(const uint8_t* __restrict__ text, uint64_t n_bytes, const uint64_t* __restrict__ off,
                                const uint32_t* __restrict__ lens, const Act* __restrict__ act,
-                               const uint32_t* __restrict__ first1, const uint32_t* __restrict__ size, uint32_t m,
-                               const uint32_t* __restrict__ cdep, uint64_t base, uint64_t* __restrict__ order,
+                               const uint64_t* __restrict__ keys, const uint32_t* __restrict__ first1,
+                               const uint32_t* __restrict__ size, uint32_t m, const uint32_t* __restrict__ cdep,
+                               const uint32_t* __restrict__ cmin, uint64_t base, uint64_t* __restrict__ order,
                                uint32_t* __restrict__ keep) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= m) return;
@@ -836,24 +840,39 @@ __global__ void k_finish_small(const uint8_t* __restrict__ text, uint64_t n_byte
   }
   keep[j] = 0u;
   const Act x = act[j];
-  const uint64_t a = off[x.id];
-  const uint32_t la = lens[x.id], depth = cdep[x.gs];
+  const uint64_t kx = keys[j];
+  const bool deeper = (kx & 0xFFu) == 8u;   // 8: the line goes on past the 7-byte window
+  const uint32_t depth = cdep[x.gs] + cmin[x.gs] + 7u;
   uint32_t rank = 0;
   for (uint32_t k = cs; k < cs + cn; ++k) {
     if (k == j) continue;
+    const uint64_t ky = keys[k];
     const uint32_t y = act[k].id;
-    const int c = cmp_lines(text, n_bytes, off[y], lens[y], a, la, depth);
-    rank += (c < 0 || (c == 0 && y < x.id)) ? 1u : 0u;
+    bool before;
+    if (ky != kx) {
+      before = ky < kx;
+    } else if (deeper) {   // equal windows, both longer: the bytes after the window
+      const int c = cmp_lines(text, n_bytes, off[y], lens[y], off[x.id], lens[x.id], depth);
+      before = c < 0 || (c == 0 && y < x.id);
+    } else {               // equal strings
+      before = y < x.id;
+    }
+    rank += before ? 1u : 0u;
   }
   order[x.id] = base + x.gs + rank;
 }
 
 // compaction of the kept elements (slot: exclusive scan of keep)
 __global__ void k_compact_act(const Act* __restrict__ in, const uint32_t* __restrict__ keep,
-                              const uint32_t* __restrict__ slot, uint32_t m, Act* __restrict__ out) {
+                              const uint32_t* __restrict__ slot, uint32_t m, Act* __restrict__ out,
+                              const uint64_t* __restrict__ kin, const uint64_t* __restrict__ vin,
+                              uint64_t* __restrict__ kout, uint64_t* __restrict__ vout) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= m || !keep[j]) return;
-  out[slot[j]] = in[j];
+  const uint32_t q = slot[j];
+  out[q] = in[j];
+  kout[q] = kin[j];
+  vout[q] = vin[j];
 }
 
 inline uint32_t blocks(uint64_t n, uint32_t t) { return (uint32_t)((n + t - 1) / t); }
@@ -1354,15 +1373,22 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
   m += lastk;
   uint32_t* live = flags;   // [0] the round splits something, [1..2] the key bits that vary
   while (m > 0) {
-    // the classes of at most kSmallClass lines are ranked here (their lines
-    // agree on bytes [0, cdep[class])); the others go on
-    hipLaunchKernelGGL(k_cls_first, dim3(blocks(m, 256)), dim3(256), 0, st, act, m, bstart, (uint32_t*)nullptr);
+    // the bytes every line of a class shares past its depth are skipped: the
+    // window starts at the class's first differing byte (k_lcp); the window
+    // keys; then the classes of at most kSmallClass lines are ranked here
+    // (k_finish_small) and the others go on to the sort of their windows
+    hipLaunchKernelGGL(k_cls_first, dim3(blocks(m, 256)), dim3(256), 0, st, act, m, bstart, cmin);
     maxscan(bstart, first, m);
+    hipLaunchKernelGGL(k_lcp, dim3(blocks(m, 256)), dim3(256), 0, st, d_text, n_bytes, d_off, lens, act, first, m,
+                       cdep, cmin);
+    hipLaunchKernelGGL(k_keys, dim3(blocks(m, 256)), dim3(256), 0, st, d_text, d_off, lens, n_bytes, act, m, cdep,
+                       cmin, keysB, valsB);
     hipLaunchKernelGGL(k_cls_size, dim3(blocks(m, 256)), dim3(256), 0, st, act, first, m, pos);
     hipLaunchKernelGGL(k_finish_small, dim3(blocks(m, 256)), dim3(256), 0, st, d_text, n_bytes, d_off, lens, act,
-                       first, pos, m, cdep, base, d_order, keep);
+                       keysB, first, pos, m, cdep, cmin, base, d_order, keep);
     exscan(keep, slot, m);
-    hipLaunchKernelGGL(k_compact_act, dim3(blocks(m, 256)), dim3(256), 0, st, act, keep, slot, m, act3);
+    hipLaunchKernelGGL(k_compact_act, dim3(blocks(m, 256)), dim3(256), 0, st, act, keep, slot, m, act3, keysB, valsB,
+                       keysA, valsA);
     {
       uint32_t nm = 0;
       TPCHK(c, hipMemcpyAsync(&nm, slot + m - 1, 4, hipMemcpyDeviceToHost, st));
@@ -1374,14 +1400,6 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
       act3 = sw;
     }
     if (m == 0) break;
-    // the bytes every line of a class shares past its depth are skipped:
-    // the window starts at the class's first differing byte
-    hipLaunchKernelGGL(k_cls_first, dim3(blocks(m, 256)), dim3(256), 0, st, act, m, bstart, cmin);
-    maxscan(bstart, first, m);
-    hipLaunchKernelGGL(k_lcp, dim3(blocks(m, 256)), dim3(256), 0, st, d_text, n_bytes, d_off, lens, act, first, m,
-                       cdep, cmin);
-    hipLaunchKernelGGL(k_keys, dim3(blocks(m, 256)), dim3(256), 0, st, d_text, d_off, lens, n_bytes, act, m, cdep,
-                       cmin, keysA, valsA);
     // a window that splits nothing (only after a k_lcp capped at kLcpMax):
     // no sort; the sort of a live window runs over the key bits that vary only
     TPCHK(c, hipMemsetAsync(live, 0, 16, st));
