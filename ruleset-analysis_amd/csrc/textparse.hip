@@ -2,9 +2,10 @@
 // SURVEY.md §8f row 1, the step before the hot path.  Text of one firewall
 // sits in HBM; the kernels here produce what rsa_classify consumes.
 //
-//   k_nl_count / k_nl_write   line split: '\n' bytes counted per 64-KiB block
-//                             (16-B loads, exact zero-byte test), block offsets
-//                             by a device scan, line starts written in order;
+//   k_nl_count / k_nl_offsets line split: '\n' bytes counted per 64-KiB block
+//                             (16-B loads, exact zero-byte test); the line
+//                             starts in one pass (decoupled look-back over the
+//                             block counts, bytes held in registers);
 //   k_parse                   one lane per line: the mapper's message parse
 //                             (get_builtconn, mapper.py:124-142 — restated by
 //                             logparse._GB), the ACL of the
@@ -108,30 +109,82 @@ __global__ __launch_bounds__(kSplitThreads) void k_nl_count(const uint8_t* __res
   if (threadIdx.x == 0) counts[blockIdx.x] = total;
 }
 
-// incl = inclusive scan of the block counts; line k + 1 starts after the k-th '\n'
-__global__ __launch_bounds__(kSplitThreads) void k_nl_write(const uint8_t* __restrict__ text, uint64_t n, int aligned,
-                                                             const uint32_t* __restrict__ counts,
-                                                             const uint64_t* __restrict__ incl, uint64_t* __restrict__ off,
-                                                             uint64_t n_lines) {
+// Line starts in one pass (decoupled look-back): workgroups take the 64-KiB
+// blocks in launch order (an atomic ticket, so a block only ever waits on
+// blocks already running), count their '\n's with their bytes held in
+// registers, publish the count, add the predecessors' counts walking back to
+// the first published inclusive prefix, publish their own inclusive prefix,
+// and write the line starts from the registers: the text is read once.
+constexpr unsigned long long kLbAgg = 1ull << 62, kLbIncl = 1ull << 63, kLbVal = kLbAgg - 1;
+constexpr uint32_t kLbSpinMax = 1u << 26;   // a wait this long is a bug: flagged, never a hang
+__global__ __launch_bounds__(kSplitThreads) void k_nl_offsets(const uint8_t* __restrict__ text, uint64_t n, int aligned,
+                                                               uint64_t* __restrict__ off, uint64_t n_lines,
+                                                               unsigned long long* __restrict__ state,
+                                                               unsigned int* __restrict__ ticket) {
   __shared__ uint32_t sh[17];
-  const uint64_t a = (uint64_t)blockIdx.x * kSplitBlock + (uint64_t)threadIdx.x * kSplitPer;
-  uint32_t total;
-  const uint32_t mine = seg_count(text, a, n, aligned != 0);
-  uint64_t k = incl[blockIdx.x] - counts[blockIdx.x] + block_exscan(mine, sh, &total);
-  if (!mine) return;
-  if (aligned && a + kSplitPer <= n) {
+  __shared__ uint32_t sh_b;
+  __shared__ unsigned long long sh_prefix;
+  if (threadIdx.x == 0) sh_b = atomicAdd(&ticket[0], 1u);
+  __syncthreads();
+  const uint32_t b = sh_b;
+  const uint64_t a = (uint64_t)b * kSplitBlock + (uint64_t)threadIdx.x * kSplitPer;
+  const bool vec = aligned && a + kSplitPer <= n;
+  uint32_t w[16];
+  uint32_t mine = 0;
+  if (vec) {
     const uint4* q = reinterpret_cast<const uint4*>(text + a);
-    for (int c = 0; c < 4; ++c) {
-      const uint4 v = q[c];
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-      for (int e = 0; e < 4; ++e) {
-        uint32_t bits = nl_bits(w[e]);
-        while (bits) {
-          const uint32_t byte = (uint32_t)__builtin_ctz(bits) >> 3;
-          bits &= bits - 1;
-          if (k + 1 <= n_lines) off[k + 1] = a + 16 * c + 4 * e + byte + 1;
-          ++k;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint4 v = q[k];
+      w[4 * k] = v.x;
+      w[4 * k + 1] = v.y;
+      w[4 * k + 2] = v.z;
+      w[4 * k + 3] = v.w;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) mine += __popc(nl_bits(w[k]));
+  } else {
+    for (uint64_t i = a; i < a + kSplitPer && i < n; ++i) mine += text[i] == '\n';
+  }
+  uint32_t total;
+  const uint32_t excl = block_exscan(mine, sh, &total);
+  if (threadIdx.x == 0) {
+    unsigned long long run = 0;
+    if (b == 0) {
+      __hip_atomic_store(&state[0], kLbIncl | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_store(&state[b], kLbAgg | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      uint32_t p = b - 1, spins = 0;
+      while (true) {
+        const unsigned long long v = __hip_atomic_load(&state[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v & kLbIncl) {
+          run += v & kLbVal;
+          break;
         }
+        if (v & kLbAgg) {
+          run += v & kLbVal;
+          --p;   // (block 0 always publishes an inclusive prefix)
+        } else if (++spins > kLbSpinMax) {
+          atomicOr(&ticket[1], 1u);
+          break;
+        }
+      }
+      __hip_atomic_store(&state[b], kLbIncl | (run + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    sh_prefix = run;
+  }
+  __syncthreads();
+  uint64_t k = sh_prefix + excl;
+  if (!mine) return;
+  if (vec) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      uint32_t bits = nl_bits(w[e]);
+      while (bits) {
+        const uint32_t byte = (uint32_t)__builtin_ctz(bits) >> 3;
+        bits &= bits - 1;
+        if (k + 1 <= n_lines) off[k + 1] = a + 4 * e + byte + 1;
+        ++k;
       }
     }
     return;
@@ -1165,16 +1218,17 @@ int rsa_text_line_offsets(rsa_ctx* c, const uint8_t* d_text, uint64_t n, uint64_
     if (nb > 0xFFFFFFFFull) return rsa_internal_fail(c, RSA_ERR_ARG, "text too large");
     const int aligned = (reinterpret_cast<uintptr_t>(d_text) & 15u) == 0;
     Scratch S{c, st};
-    const size_t cnt_bytes = ((nb * 4 + 15) / 16) * 16;
-    TPCHK(c, hipMallocAsync(&S.base, cnt_bytes + nb * 8 + scan_sums_len(nb) * 8 + 256, st));
-    uint32_t* counts = static_cast<uint32_t*>(S.base);
-    uint64_t* incl = reinterpret_cast<uint64_t*>(static_cast<char*>(S.base) + cnt_bytes);
-    uint64_t* sums = incl + nb;
-    hipLaunchKernelGGL(k_nl_count, dim3((uint32_t)nb), dim3(kSplitThreads), 0, st, d_text, n, aligned, counts);
-    scan<OpPlus, true, uint32_t, uint64_t>(st, counts, incl, nb, sums);
-    hipLaunchKernelGGL(k_nl_write, dim3((uint32_t)nb), dim3(kSplitThreads), 0, st, d_text, n, aligned, counts, incl,
-                       d_off, n_lines);
+    TPCHK(c, hipMallocAsync(&S.base, nb * 8 + 64, st));
+    unsigned long long* state = static_cast<unsigned long long*>(S.base);   // per block: look-back word
+    unsigned int* ticket = reinterpret_cast<unsigned int*>(state + nb);     // [0] ticket, [1] error flag
+    TPCHK(c, hipMemsetAsync(S.base, 0, nb * 8 + 64, st));
+    hipLaunchKernelGGL(k_nl_offsets, dim3((uint32_t)nb), dim3(kSplitThreads), 0, st, d_text, n, aligned, d_off, n_lines,
+                       state, ticket);
     TPCHK(c, hipGetLastError());
+    unsigned int err = 0;
+    TPCHK(c, hipMemcpyAsync(&err, ticket + 1, 4, hipMemcpyDeviceToHost, st));
+    TPCHK(c, hipStreamSynchronize(st));
+    if (err) return rsa_internal_fail(c, RSA_ERR_HIP, "rsa_text_line_offsets: look-back did not resolve");
   }
   hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(1), 0, st, d_off + n_lines, n);
   TPCHK(c, hipGetLastError());
