@@ -148,30 +148,44 @@ __global__ __launch_bounds__(kSplitThreads) void k_nl_offsets(const uint8_t* __r
   }
   uint32_t total;
   const uint32_t excl = block_exscan(mine, sh, &total);
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < 64) {
+    // wave 0 looks back 64 blocks at a time: the nearest published inclusive
+    // prefix among them and the aggregates after it; an unpublished block
+    // after the last inclusive one means another look
     unsigned long long run = 0;
+    const uint32_t lane = threadIdx.x;
     if (b == 0) {
-      __hip_atomic_store(&state[0], kLbIncl | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) __hip_atomic_store(&state[0], kLbIncl | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
-      __hip_atomic_store(&state[b], kLbAgg | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      uint32_t p = b - 1, spins = 0;
+      if (lane == 0) __hip_atomic_store(&state[b], kLbAgg | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int64_t top = (int64_t)b - 1;   // the window is blocks (top - 63, top]
+      uint32_t spins = 0;
       while (true) {
-        const unsigned long long v = __hip_atomic_load(&state[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (v & kLbIncl) {
-          run += v & kLbVal;
-          break;
+        const int64_t p = top - (int64_t)lane;
+        const unsigned long long v =
+            p >= 0 ? __hip_atomic_load(&state[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbIncl;
+        // lanes in order of distance: the first inclusive one ends the walk
+        const unsigned long long incl = __ballot((v & kLbIncl) != 0);
+        const int stop = incl ? __builtin_ctzll(incl) : 64;   // lanes [0, stop) must be aggregates
+        const unsigned long long ready = __ballot((v & (kLbIncl | kLbAgg)) != 0);
+        const unsigned long long need = stop >= 64 ? ~0ull : ((2ull << stop) - 1ull);
+        if ((ready & need) != need) {   // someone in the window not published yet: look again
+          if (++spins > kLbSpinMax) {
+            if (lane == 0) atomicOr(&ticket[1], 1u);
+            break;
+          }
+          continue;
         }
-        if (v & kLbAgg) {
-          run += v & kLbVal;
-          --p;   // (block 0 always publishes an inclusive prefix)
-        } else if (++spins > kLbSpinMax) {
-          atomicOr(&ticket[1], 1u);
-          break;
-        }
+        unsigned long long x = ((int)lane <= stop && p >= 0) ? (v & kLbVal) : 0ull;
+        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+        run += x;
+        if (stop < 64) break;
+        top -= 64;
       }
-      __hip_atomic_store(&state[b], kLbIncl | (run + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0)
+        __hip_atomic_store(&state[b], kLbIncl | (run + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    sh_prefix = run;
+    if (lane == 0) sh_prefix = run;
   }
   __syncthreads();
   uint64_t k = sh_prefix + excl;
