@@ -2832,6 +2832,7 @@ struct rsa_ctx {
   uint32_t filter_len = 0;
   unsigned long long* d_packed = nullptr;   // k_count / k_aggregate packed counters (rules > kCnt)
   // hot-region split (k_hot_plan / k_hot_combine)
+  uint32_t min_regions_log2 = 8;            // RSA_OPT_MIN_REGIONS_LOG2
   int parse_mode = 2;                       // RSA_OPT_PARSE_MODE (textparse.hip): register-window reads
   bool region_import = true;                // RSA_OPT_REGION_IMPORT: rsa_import by region sort + k_reduce
   bool slots_clean = true;                  // no slot holds a key of an earlier job (k_import's CAS claims need it)
@@ -3594,6 +3595,10 @@ int rsa_set_option(rsa_ctx* c, int option, int64_t value) {
         return fail(c, RSA_ERR_ARG, "parse mode must be 0 (LDS staged), 1 (direct) or 2 (register window)");
       c->parse_mode = (int)value;
       return RSA_OK;
+    case RSA_OPT_MIN_REGIONS_LOG2:
+      if (value < 0 || value > 12) return fail(c, RSA_ERR_ARG, "RSA_OPT_MIN_REGIONS_LOG2 must be 0..12");
+      c->min_regions_log2 = (uint32_t)value;
+      return RSA_OK;
     case RSA_OPT_REGION_IMPORT:
       c->region_import = value != 0;
       return RSA_OK;
@@ -3882,7 +3887,7 @@ int rsa_reset(rsa_ctx* c, uint64_t capacity, uint32_t cap) {
     // regions of at most 2^16 slots, and at least 256 of them (one k_reduce
     // workgroup each: every CU busy) while they keep >= 1024 slots
     uint32_t rs = bits < (uint32_t)kRegionMaxBits ? bits : (uint32_t)kRegionMaxBits;
-    while (rs > 10 && bits - rs < 8) --rs;
+    while (rs > 10 && bits - rs < c->min_regions_log2) --rs;
     c->rs_bits = rs;
     c->np_bits = bits - rs;
   }

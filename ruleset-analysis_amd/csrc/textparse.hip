@@ -666,14 +666,31 @@ struct Act {               // an unsettled line: its id and the position its gro
 
 // the window of a class: its depth (bytes all its lines share, cdep) plus the
 // further common prefix k_lcp found (cmin), both indexed by the class start
+// (preH / preL: the line's 16 bytes from the class depth, big-endian, as k_lcp
+// read them: a window inside them needs no text read -- text reads by line
+// are one HBM transaction each, the staged bytes are coalesced)
 __global__ void k_keys(const uint8_t* __restrict__ text, const uint64_t* __restrict__ off,
                        const uint32_t* __restrict__ lens, uint64_t n_bytes, const Act* __restrict__ act, uint32_t m,
                        const uint32_t* __restrict__ cdep, const uint32_t* __restrict__ cmin,
+                       const uint64_t* __restrict__ preH, const uint64_t* __restrict__ preL,
                        uint64_t* __restrict__ keys, uint64_t* __restrict__ vals) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= m) return;
   const Act x = act[j];
-  keys[j] = chunk_key(text, n_bytes, off[x.id], lens[x.id], (uint64_t)cdep[x.gs] + cmin[x.gs]);
+  const uint32_t e = cmin[x.gs], len = lens[x.id];
+  const uint64_t pos = (uint64_t)cdep[x.gs] + e;
+  uint64_t key;
+  if (e <= 9u) {
+    const uint32_t rem = len > pos ? (uint32_t)(len - pos) : 0u;
+    const uint64_t H = preH[j], L = preL[j];
+    const uint64_t w = e ? (H << (8u * e)) | (L >> (64u - 8u * e)) : H;   // bytes e .. e + 7
+    uint64_t k = w & ~0xFFull;
+    if (rem && rem < 7) k &= ~0ull << (64u - 8u * rem);
+    key = rem ? (k | (rem < 8 ? rem : 8u)) : 0ull;
+  } else {
+    key = chunk_key(text, n_bytes, off[x.id], len, pos);
+  }
+  keys[j] = key;
   vals[j] = (uint64_t)x.gs << 32 | x.id;
 }
 
@@ -685,10 +702,11 @@ __global__ void k_keys(const uint8_t* __restrict__ text, const uint64_t* __restr
 // "Built inbound TCP connection ...") cost one pass instead of a round per 7
 // bytes.  Capped at kLcpMax bytes per pass (the window then starts there).
 constexpr uint32_t kLcpMax = 4096;
+// (the line's first 16 bytes from the depth go to preH / preL for k_keys)
 __global__ void k_lcp(const uint8_t* __restrict__ text, uint64_t n_bytes, const uint64_t* __restrict__ off,
                       const uint32_t* __restrict__ lens, const Act* __restrict__ act,
                       const uint32_t* __restrict__ first1, uint32_t m, const uint32_t* __restrict__ cdep,
-                      uint32_t* __restrict__ cmin) {
+                      uint32_t* __restrict__ cmin, uint64_t* __restrict__ preH, uint64_t* __restrict__ preL) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t e = 0xFFFFFFFFu, gs = 0xFFFFFFFFu;
   if (j < m) {
@@ -698,11 +716,16 @@ __global__ void k_lcp(const uint8_t* __restrict__ text, uint64_t n_bytes, const 
     const uint32_t d = cdep[gs], la = lens[x.id], lb = lens[y];
     const uint32_t ra = la > d ? la - d : 0u, rb = lb > d ? lb - d : 0u;
     const uint32_t lim = (ra < rb ? ra : rb) < kLcpMax ? (ra < rb ? ra : rb) : kLcpMax;
+    const uint64_t pa = off[x.id] + d;
+    const uint64_t H = ra ? line_chunk8(text, n_bytes, pa, ra) : 0ull;
+    const uint64_t L = ra > 8 ? line_chunk8(text, n_bytes, pa + 8, ra - 8) : 0ull;
+    preH[j] = H;
+    preL[j] = L;
     e = lim;
     if (y != x.id) {
-      const uint64_t pa = off[x.id] + d, pb = off[y] + d;
+      const uint64_t pb = off[y] + d;
       for (uint32_t p = 0; p < lim; p += 8) {
-        const uint64_t ka = line_chunk8(text, n_bytes, pa + p, la - d - p),
+        const uint64_t ka = p == 0 ? H : p == 8 ? L : line_chunk8(text, n_bytes, pa + p, la - d - p),
                        kb = line_chunk8(text, n_bytes, pb + p, lb - d - p);
         if (ka != kb) {
           const uint32_t q = p + (uint32_t)__builtin_clzll(ka ^ kb) / 8u;
@@ -892,12 +915,26 @@ __global__ void k_cls_size(const Act* __restrict__ act, const uint32_t* __restri
 // classes.  keys[j]: the element's window key at its class's window start
 // (k_keys): members are compared by key, and only members with equal keys
 // that both go on past the window by their bytes from the window's end.
-__global__ void k_finish_small(const uint8_t* __restrict__ text, uint64_t n_bytes, const uint64_t* __restrict__ off,
-                               const uint32_t* __restrict__ lens, const Act* __restrict__ act,
-                               const uint64_t* __restrict__ keys, const uint32_t* __restrict__ first1,
-                               const uint32_t* __restrict__ size, uint32_t m, const uint32_t* __restrict__ cdep,
-                               const uint32_t* __restrict__ cmin, uint64_t base, uint64_t* __restrict__ order,
-                               uint32_t* __restrict__ keep) {
+// The members' keys and ids are staged in LDS: a workgroup's elements
+// [b0, b0 + 256) have their small classes inside [b0 - 64, b0 + 320).
+constexpr uint32_t kFinThreads = 256, kFinSpan = kFinThreads + 2 * kSmallClass;
+__global__ __launch_bounds__(kFinThreads) void k_finish_small(
+    const uint8_t* __restrict__ text, uint64_t n_bytes, const uint64_t* __restrict__ off,
+    const uint32_t* __restrict__ lens, const Act* __restrict__ act, const uint64_t* __restrict__ keys,
+    const uint32_t* __restrict__ first1, const uint32_t* __restrict__ size, uint32_t m,
+    const uint32_t* __restrict__ cdep, const uint32_t* __restrict__ cmin, uint64_t base, uint64_t* __restrict__ order,
+    uint32_t* __restrict__ keep) {
+  __shared__ uint64_t skey[kFinSpan];
+  __shared__ uint32_t sid[kFinSpan];
+  const int64_t lo = (int64_t)blockIdx.x * kFinThreads - (int64_t)kSmallClass;
+  for (uint32_t q = threadIdx.x; q < kFinSpan; q += blockDim.x) {
+    const int64_t k = lo + (int64_t)q;
+    if (k >= 0 && k < (int64_t)m) {
+      skey[q] = keys[k];
+      sid[q] = act[k].id;
+    }
+  }
+  __syncthreads();
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= m) return;
   const uint32_t cs = first1[j] - 1, cn = size[cs];
@@ -913,8 +950,9 @@ __global__ void k_finish_small(const uint8_t* __restrict__ text, uint64_t n_byte
   uint32_t rank = 0;
   for (uint32_t k = cs; k < cs + cn; ++k) {
     if (k == j) continue;
-    const uint64_t ky = keys[k];
-    const uint32_t y = act[k].id;
+    const uint32_t q = (uint32_t)((int64_t)k - lo);   // inside the staged span
+    const uint64_t ky = skey[q];
+    const uint32_t y = sid[q];
     bool before;
     if (ky != kx) {
       before = ky < kx;
@@ -1448,12 +1486,12 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
     hipLaunchKernelGGL(k_cls_first, dim3(blocks(m, 256)), dim3(256), 0, st, act, m, bstart, cmin);
     maxscan(bstart, first, m);
     hipLaunchKernelGGL(k_lcp, dim3(blocks(m, 256)), dim3(256), 0, st, d_text, n_bytes, d_off, lens, act, first, m,
-                       cdep, cmin);
+                       cdep, cmin, keysT, valsT);
     hipLaunchKernelGGL(k_keys, dim3(blocks(m, 256)), dim3(256), 0, st, d_text, d_off, lens, n_bytes, act, m, cdep,
-                       cmin, keysB, valsB);
+                       cmin, (const uint64_t*)keysT, (const uint64_t*)valsT, keysB, valsB);
     hipLaunchKernelGGL(k_cls_size, dim3(blocks(m, 256)), dim3(256), 0, st, act, first, m, pos);
-    hipLaunchKernelGGL(k_finish_small, dim3(blocks(m, 256)), dim3(256), 0, st, d_text, n_bytes, d_off, lens, act,
-                       keysB, first, pos, m, cdep, cmin, base, d_order, keep);
+    hipLaunchKernelGGL(k_finish_small, dim3(blocks(m, kFinThreads)), dim3(kFinThreads), 0, st, d_text, n_bytes, d_off,
+                       lens, act, keysB, first, pos, m, cdep, cmin, base, d_order, keep);
     exscan(keep, slot, m);
     hipLaunchKernelGGL(k_compact_act, dim3(blocks(m, 256)), dim3(256), 0, st, act, keep, slot, m, act3, keysB, valsB,
                        keysA, valsA);
