@@ -683,7 +683,8 @@ __global__ void k_keys(const uint8_t* __restrict__ text, const uint64_t* __restr
   if (e <= 9u) {
     const uint32_t rem = len > pos ? (uint32_t)(len - pos) : 0u;
     const uint64_t H = preH[j], L = preL[j];
-    const uint64_t w = e ? (H << (8u * e)) | (L >> (64u - 8u * e)) : H;   // bytes e .. e + 7
+    // bytes e .. e + 6 at the top (shifts stay below 64)
+    const uint64_t w = e == 0 ? H : e < 8 ? (H << (8u * e)) | (L >> (64u - 8u * e)) : L << (8u * (e - 8u));
     uint64_t k = w & ~0xFFull;
     if (rem && rem < 7) k &= ~0ull << (64u - 8u * rem);
     key = rem ? (k | (rem < 8 ? rem : 8u)) : 0ull;
