@@ -219,6 +219,9 @@ __global__ void k_set_u64(uint64_t* p, uint64_t v) { *p = v; }
 // 28 KB of staged text + the scan's slots and tables: four workgroups per CU
 // (a workgroup whose lines average more than 224 B defers them to the slow pass)
 constexpr uint32_t kParseWG = 128, kStageBytes = 28672;
+#ifndef RSA_OK_FULLBITS
+#define RSA_OK_FULLBITS 0   // A/B builds: order-key window sorts over all 64 key bits, not only the bits that vary
+#endif
 #ifndef RSA_TP_PROF
 #define RSA_TP_PROF 0   // PROFILING builds only (results invalid): 1 template scan without tpl_finish, 2 no scan either
 #endif
@@ -1526,7 +1529,7 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
       // every class already in key order: no sort
       hipLaunchKernelGGL(k_split_vals, dim3(blocks(m, 256)), dim3(256), 0, st, valsA, m, gs, ids);
     } else {
-      const uint64_t vary = (uint64_t)h_live[2] << 32 | h_live[1];
+      const uint64_t vary = RSA_OK_FULLBITS ? ~0ull : (uint64_t)h_live[2] << 32 | h_live[1];
       const unsigned b0 = vary ? (unsigned)__builtin_ctzll(vary) : 0u;
       const unsigned b1 = vary ? 64u - (unsigned)__builtin_clzll(vary) : 0u;
       // stable LSD: by the chunk key, then by the group start
