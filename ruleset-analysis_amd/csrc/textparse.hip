@@ -408,7 +408,15 @@ __device__ __forceinline__ uint4 text_chunk(const uint4* __restrict__ t16, const
   return uint4{w[0], w[1], w[2], w[3]};
 }
 
-__global__ __launch_bounds__(kParseWG) void k_parse_win(const uint8_t* __restrict__ text,
+#ifndef RSA_PARSE_WIN_WAVES
+#define RSA_PARSE_WIN_WAVES 0   // A/B builds: minimum waves per SIMD for k_parse_win (register cap; 0 = compiler's choice)
+#endif
+#if RSA_PARSE_WIN_WAVES
+#define RSA_PARSE_WIN_ATTR __attribute__((amdgpu_waves_per_eu(RSA_PARSE_WIN_WAVES, 8)))
+#else
+#define RSA_PARSE_WIN_ATTR
+#endif
+__global__ __launch_bounds__(kParseWG) RSA_PARSE_WIN_ATTR void k_parse_win(const uint8_t* __restrict__ text,
                                                        const uint64_t* __restrict__ off, uint64_t n_lines,
                                                        const rsa_parse_ifc* __restrict__ ifcs, uint32_t n_ifcs,
                                                        const rsa_parse_spell* __restrict__ spells, uint32_t n_spells,

@@ -855,11 +855,10 @@ RSA_HD bool tpl_finish(const S& s, Q slot, const rsa_parse_ifc* ifcs, uint32_t n
   using namespace tpl;
   auto at = [&](uint32_t f) { return (uint32_t)slot[f] & 0xFFFFu; };
   auto len = [&](uint32_t f) { return ((uint32_t)slot[f] >> 16) & 0xFFu; };
-  // Mmm ... HH:MM:SS | Mmm D YYYY | TAG-d-dddddd | DIR PROTO | IF:IP/P twice
-  const B16 bM1 = bytes16(s, at(fM1)), bHMS = bytes16(s, at(fHH)), bM2 = bytes16(s, at(fM2)),
-            bTag = bytes16(s, at(fTAG)), bDir = bytes16(s, at(fDIR)), bIf1 = bytes16(s, at(fIF1)),
-            bIp1 = bytes16(s, at(fIP1)), bP1 = bytes16(s, at(fP1)), bIf2 = bytes16(s, at(fIF2)),
-            bIp2 = bytes16(s, at(fIP2)), bP2 = bytes16(s, at(fP2));
+  // two groups of blocks (fewer live registers at once): the header --
+  // Mmm ... | Mmm D YYYY | TAG-d-dddddd | DIR PROTO -- then the addresses
+  const B16 bM1 = bytes16(s, at(fM1)), bM2 = bytes16(s, at(fM2)), bTag = bytes16(s, at(fTAG)),
+            bDir = bytes16(s, at(fDIR));
   const uint32_t m2 = b16_pack3(bM2);
   const uint32_t ltag = len(fTAG), tag = b16_pack3(bTag);
   bool ok = b16_ulll(bM1) && b16_ulll(bM2);
@@ -875,6 +874,10 @@ RSA_HD bool tpl_finish(const S& s, Q slot, const rsa_parse_ifc* ifcs, uint32_t n
   const uint32_t proto = b16_pack3(bPr);
   const bool udp = proto == pack3('U', 'D', 'P');
   ok = ok && (udp || proto == pack3('T', 'C', 'P'));
+  if (!ok) return false;
+  // IF:IP/P (IP/P) to IF:IP/P
+  const B16 bIf1 = bytes16(s, at(fIF1)), bIp1 = bytes16(s, at(fIP1)), bP1 = bytes16(s, at(fP1)),
+            bIf2 = bytes16(s, at(fIF2)), bIp2 = bytes16(s, at(fIP2)), bP2 = bytes16(s, at(fP2));
   const uint32_t l1 = len(fIF1), l2 = len(fIF2);
   ok = ok && name_no_dash(s, at(fIF1), l1, bIf1) && name_no_dash(s, at(fIF2), l2, bIf2);   // '-' in a name
   uint32_t ip1 = 0, ip2 = 0;
@@ -922,6 +925,7 @@ RSA_HD bool tpl_finish(const S& s, Q slot, const rsa_parse_ifc* ifcs, uint32_t n
     const uint32_t ld = len(fD2);   // "Mmm D YYYY" / "Mmm DD YYYY"
     const uint32_t day = b16_num<2>(bM2, 4, ld);
     const uint32_t y = ld == 1 ? b16_num<4>(bM2, 6, 4) : b16_num<4>(bM2, 7, 4);
+    const B16 bHMS = bytes16(s, at(fHH));
     const uint32_t hh = b16_num<2>(bHMS, 0, 2), mm = b16_num<2>(bHMS, 3, 2), ss = b16_num<2>(bHMS, 6, 2);
     if (mo < 0 || y < RSA_TS_YEAR0 || y >= RSA_TS_YEAR0 + 128 || day > 31 || hh > 23 || mm > 59 || ss > 59)
       return false;
