@@ -10,7 +10,13 @@ MI355X_MICROARCH.md §HBM says for wide streaming reads), random 32-B reads
 2.0x and random 64-B reads 1.04x (one 64-B tally per read).  Each kernel is
 converted with the factor of its dominant read pattern: the streaming
 kernels (k_classify, k_count, k_part_hist, k_part_scatter, the scans) x2,
-k_reduce (segment reads plus random 64-B slot read-modify-writes) x1.
+k_reduce (segment reads plus random 64-B slot read-modify-writes) x1.  The
+cap kernels read streaming since round 4: k_cap_scatter(_lds) walks the used
+list and k_reduce's used-ordered key copy in order (16 B per entry, no slot
+gathers; the per-rule bound and segment tables are L2-resident) and
+k_cap_select reads its segments in order, so both take x2; before round 4
+k_cap_scatter gathered 64-B slots (random 64-B reads, x1.04) and x2
+overstated it.
 WRITE_SIZE * 1024 is taken as is.  Usage: pmc_summary.py FETCH_CSV WRITE_CSV
 OUT_JSON LINES STEPS_TOTAL (STEPS_TOTAL = warmup + timed steps of the profiled
 bench run, + 1 untimed stats step when the run had one)."""
