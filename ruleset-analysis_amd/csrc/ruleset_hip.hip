@@ -2387,9 +2387,23 @@ __global__ __launch_bounds__(1024) void k_cap_scatter_lds(const Slot* S, const u
 #pragma unroll
   for (int k = 0; k < kCapPer; ++k) rank[k] = cc[k] != 0xFFFFFFFFu ? atomicAdd(&cnt[cc[k]], 1u) : 0u;
   __syncthreads();
-  for (uint32_t r = threadIdx.x; r < n_capped; r += blockDim.x) {
-    const uint32_t m = cnt[r];
-    if (m) cnt[r] = atomicAdd(&capped_fill[r], m);
+  // every rule's run reserved with one returning device atomic per (workgroup,
+  // rule); a thread's atomics are all issued before any result is used, so
+  // they overlap instead of paying one round trip each
+  {
+    constexpr int kRes = kCapLds / 1024;
+    uint32_t res[kRes];
+#pragma unroll
+    for (int q = 0; q < kRes; ++q) {
+      const uint32_t r = threadIdx.x + (uint32_t)q * 1024u;
+      const uint32_t m = r < n_capped ? cnt[r] : 0u;
+      res[q] = m ? atomicAdd(&capped_fill[r], m) : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < kRes; ++q) {
+      const uint32_t r = threadIdx.x + (uint32_t)q * 1024u;
+      if (r < n_capped) cnt[r] = res[q];
+    }
   }
   __syncthreads();
 #pragma unroll

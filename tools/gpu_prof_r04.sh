@@ -6,6 +6,7 @@ TAG=$1; shift
 export TMPDIR=/tmp
 for cfg in "$@"; do
   OUT=gpurun_out/$TAG/$cfg
+  mkdir -p "$OUT"
   timeout -k 10 1100 bash tools/profile_round.sh "$OUT" --config $cfg > "$OUT.log" 2>&1 || { tail -20 "$OUT.log"; exit 1; }
   lines=$(python3 -c "import sys; sys.argv=['x']; import bench; print(bench.CONFIGS['$cfg']['lines'])")
   f=$(find "$OUT/fetch" -name '*counter_collection.csv' | head -1)
