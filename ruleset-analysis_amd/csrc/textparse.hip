@@ -222,8 +222,8 @@ constexpr uint32_t kParseWG = 128, kStageBytes = 28672;
 #ifndef RSA_OK_FULLBITS
 #define RSA_OK_FULLBITS 0   // A/B builds: order-key window sorts over all 64 key bits, not only the bits that vary
 #endif
-#ifndef RSA_TP_PROF
-#define RSA_TP_PROF 0   // PROFILING builds only (results invalid): 1 template scan without tpl_finish, 2 no scan either
+#ifndef RSA_TPL_PROF
+#define RSA_TPL_PROF 0   // PROFILING builds only (results invalid): 1 template scan without tpl_finish, 2 no scan either
 #endif
 
 // A line the template pass defers (rsa_text::kLineDefer): its index is
@@ -369,9 +369,9 @@ __global__ __launch_bounds__(kParseWG) void k_parse(const uint8_t* __restrict__ 
     } else if (staged) {
       const rsa_text::WordLn s{sm, (uint32_t)(a - base), (uint32_t)len};
       uint32_t* slot = tslot + threadIdx.x * rsa_text::tpl::kSlotWords;
-      if (RSA_TP_PROF == 2) {
+      if (RSA_TPL_PROF == 2) {
         d = RSA_LINE_NOACL + (s[len > 1 ? 1 : 0] == 0xFFu);
-      } else if (RSA_TP_PROF == 1) {
+      } else if (RSA_TPL_PROF == 1) {
         d = RSA_LINE_NOACL + !rsa_text::tpl::scan(s, tprog, tcls, slot);
       } else if (!(rsa_text::tpl::scan(s, tprog, tcls, slot) &&
                    rsa_text::tpl_finish(s, slot, ifcs, n_ifcs, spells, n_spells, tup, ts, d))) {
@@ -466,7 +466,7 @@ __global__ __launch_bounds__(kParseWG) RSA_PARSE_WIN_ATTR void k_parse_win(const
     uint32_t B[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) B[k] = __builtin_amdgcn_alignbit(X[k + 1], X[k], r);
-    if (RSA_TP_PROF == 2) {
+    if (RSA_TPL_PROF == 2) {
       st.ok ^= B[0] ^ B[1] ^ B[2] ^ B[3];   // (the loads only)
     } else {
 #pragma unroll
@@ -482,7 +482,7 @@ __global__ __launch_bounds__(kParseWG) RSA_PARSE_WIN_ATTR void k_parse_win(const
   if (!have) return;
   rsa_tuple tup = {0u, 0u, 0, 0, 0, 0, 0};
   uint32_t ts = 0, d = rsa_text::kLineDefer;
-  if (RSA_TP_PROF) {
+  if (RSA_TPL_PROF) {
     d = RSA_LINE_NOACL + (st.ok == 7u);
   } else if (scannable && st.ok && tprog[st.seg] == kEndSeg) {
     const uint64_t nw = n_bytes >> 2;
@@ -505,6 +505,7 @@ __global__ __launch_bounds__(kParseWG) RSA_PARSE_WIN_ATTR void k_parse_win(const
 // backtracking restated), reading from HBM.  Persistent grid over the
 // device-side count.
 constexpr uint32_t kSlowGrid = 2048;
+constexpr uint32_t kSlowStride = 65;   // LDS words per lane row (256 B + 1 word: rows start in different banks)
 template <bool kReduce>
 __global__ __launch_bounds__(kParseWG) void k_parse_slow(const uint8_t* __restrict__ text,
                                                          const uint64_t* __restrict__ off, uint64_t n_lines,
@@ -514,6 +515,7 @@ __global__ __launch_bounds__(kParseWG) void k_parse_slow(const uint8_t* __restri
                                                          const unsigned int* __restrict__ slow_n,
                                                          rsa_tuple* __restrict__ tuples, uint32_t* __restrict__ ts_out,
                                                          uint32_t* __restrict__ disp) {
+  __shared__ uint32_t srow[kReduce ? 1 : kParseWG * kSlowStride];   // one padded row per lane
   const uint32_t ns = *slow_n;
   const uint64_t n_bytes = off[n_lines];
   const uint32_t* w32 = reinterpret_cast<const uint32_t*>(text);
@@ -536,6 +538,26 @@ __global__ __launch_bounds__(kParseWG) void k_parse_slow(const uint8_t* __restri
         const rsa_text::GWordLn q{w32, text, pa, n_bytes, (uint32_t)plen, ~0ull, 0u};
         if (rsa_text::same_key(s, q)) d |= RSA_RED_SAME_KEY;
       }
+    } else if (len + 3 <= 4u * (kSlowStride - 1)) {
+      // the line copied into the lane's LDS row first (its words are independent
+      // loads, all in flight together): the general parse then reads LDS, not a
+      // chain of dependent HBM reads, one per 4 bytes scanned
+      uint32_t* row = srow + threadIdx.x * kSlowStride;
+      const uint64_t w0 = a >> 2, nw = ((a & 3u) + len + 3) >> 2;
+      for (uint64_t k = 0; k < nw; ++k) {
+        const uint64_t q = w0 + k;
+        uint32_t x;
+        if (4 * q + 4 <= n_bytes) {
+          x = w32[q];
+        } else {
+          x = 0;
+          for (uint32_t t = 0; t < 4; ++t)
+            if (4 * q + t < n_bytes) x |= (uint32_t)text[4 * q + t] << (8 * t);
+        }
+        row[k] = x;
+      }
+      const rsa_text::WordLn ls{row, (uint32_t)(a & 3u), (uint32_t)len};
+      rsa_text::parse_line(ls, ifcs, n_ifcs, spells, n_spells, tup, ts, d);
     } else {
       rsa_text::parse_line(s, ifcs, n_ifcs, spells, n_spells, tup, ts, d);
     }

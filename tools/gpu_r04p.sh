@@ -4,6 +4,9 @@ set -o pipefail
 OUT=gpurun_out/${1:-r04p}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_textparse.py tests/test_multifile.py tests/test_reducer_stream.py -m gpu -x -q --timeout 300 --timeout-method thread \
+  > "$OUT/pytest.log" 2>&1 || { tail -40 "$OUT/pytest.log"; exit 1; }
+tail -2 "$OUT/pytest.log"
 for v in base pw5; do
   lib=""; [ $v = pw5 ] && lib=ruleset-analysis_amd/_build/var/libruleset_hip_pw5.so
   RSA_HIP_LIB=$lib timeout -k 10 300 python -u bench.py --text --lines 16000000 --no-cpu-baseline --steps 3 --warmup 1 \
