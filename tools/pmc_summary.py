@@ -46,13 +46,16 @@ def main():
     # every pass-1 launch of every slice: classification, deferred tails,
     # aggregation (record append, region histogram, region scatter, per-region
     # reduction) -- the kernels bracketed by the pass-1 HIP events
-    kinds = ('k_classify', 'k_tail', 'k_count<', 'k_count_flush', 'k_aggregate', 'k_part_hist', 'k_scan_blocks',
+    kinds = ('k_classify', 'k_tail', 'k_count<', 'k_count_flush', 'k_cnt_', 'k_aggregate', 'k_part_hist', 'k_scan_blocks',
              'k_scan_sums', 'k_scan_add', 'k_part_scatter', 'k_seg_starts', 'k_hot_plan', 'k_hot_combine<1>',
              'k_reduce<1>', 'k_cap_mark', 'k_cap_scatter', 'k_cap_select')
     # pass-1 launches only: the classifier instantiated with emission (the
     # classify-only launches of bench's untimed checks are excluded)
-    pick = lambda name: any(k in name for k in kinds) and not ('k_classify' in name and 'false>' in name) and \
-        not ('k_tail' in name and 'false>' in name)
+    # (k_classify<kImg, kEmit, kMode, kNarrow>: kEmit is the second argument)
+    import re
+    no_emit = lambda name: re.search(r'k_classify<[^,>]+, false', name) is not None or \
+        ('k_tail' in name and 'false>' in name)
+    pick = lambda name: any(k in name for k in kinds) and not no_emit(name)
     factor = lambda name: 1.0 if 'k_reduce' in name else 2.0
     read = 1024 * sum(v * factor(fn[d]) for d, v in f.items() if pick(fn[d])) / steps
     write = 1024 * sum(v for d, v in w.items() if pick(wn[d])) / steps
