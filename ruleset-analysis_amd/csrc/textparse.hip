@@ -914,18 +914,6 @@ __global__ void k_compact(const uint32_t* __restrict__ ids, const uint32_t* __re
 // second), so the global rounds stop early.
 constexpr uint32_t kSmallClass = 64;
 
-// <0, 0, >0: line a vs line b from byte `depth` (LC_ALL=C order: bytes, then length)
-__device__ __forceinline__ int cmp_lines(const uint8_t* __restrict__ text, uint64_t n_bytes, uint64_t a, uint32_t la,
-                                         uint64_t b, uint32_t lb, uint32_t depth) {
-  for (uint32_t p = depth;; p += 8) {
-    const uint32_t ra = la > p ? la - p : 0u, rb = lb > p ? lb - p : 0u;
-    if (!ra || !rb) return (int)(ra != 0) - (int)(rb != 0);
-    const uint64_t ka = line_chunk8(text, n_bytes, a + p, ra), kb = line_chunk8(text, n_bytes, b + p, rb);
-    if (ka != kb) return ka < kb ? -1 : 1;
-    if (ra <= 8 || rb <= 8) return (int)(ra > rb) - (int)(ra < rb);
-  }
-}
-
 // per element of act: 1 + index of its class's first element at class starts, else 0
 // (cmin non-null: the class's k_lcp minimum is reset to ~0 at its first element)
 __global__ void k_cls_first(const Act* __restrict__ act, uint32_t m, uint32_t* __restrict__ out,
@@ -947,17 +935,22 @@ __global__ void k_cls_size(const Act* __restrict__ act, const uint32_t* __restri
 
 // rank every element of a small class; keep[j] = 1 for the elements of large
 // classes.  keys[j]: the element's window key at its class's window start
-// (k_keys): members are compared by key, and only members with equal keys
-// that both go on past the window by their bytes from the window's end.
+// (k_keys).  A member's rank is the number of members with a smaller key plus
+// the members with an equal key and a smaller id -- exact when the equal keys
+// are equal strings (the window holds their ends).  Members whose equal window
+// goes on (a tie group) are not compared further here: the group becomes a
+// class of its own, starting at its position in the class, one window deeper
+// (its members written to tie[] at their rank, tkeep[] = 1, its depth to
+// tdep[start]); it joins the current round behind the large classes, where the
+// common-prefix pass skips the bytes its lines share.
 // The members' keys and ids are staged in LDS: a workgroup's elements
 // [b0, b0 + 256) have their small classes inside [b0 - 64, b0 + 320).
 constexpr uint32_t kFinThreads = 256, kFinSpan = kFinThreads + 2 * kSmallClass;
 __global__ __launch_bounds__(kFinThreads) void k_finish_small(
-    const uint8_t* __restrict__ text, uint64_t n_bytes, const uint64_t* __restrict__ off,
-    const uint32_t* __restrict__ lens, const Act* __restrict__ act, const uint64_t* __restrict__ keys,
-    const uint32_t* __restrict__ first1, const uint32_t* __restrict__ size, uint32_t m,
-    const uint32_t* __restrict__ cdep, const uint32_t* __restrict__ cmin, uint64_t base, uint64_t* __restrict__ order,
-    uint32_t* __restrict__ keep) {
+    const Act* __restrict__ act, const uint64_t* __restrict__ keys, const uint32_t* __restrict__ first1,
+    const uint32_t* __restrict__ size, uint32_t m, const uint32_t* __restrict__ cdep,
+    const uint32_t* __restrict__ cmin, uint64_t base, uint64_t* __restrict__ order, uint32_t* __restrict__ keep,
+    Act* __restrict__ tie, uint32_t* __restrict__ tkeep, uint32_t* __restrict__ tdep) {
   __shared__ uint64_t skey[kFinSpan];
   __shared__ uint32_t sid[kFinSpan];
   const int64_t lo = (int64_t)blockIdx.x * kFinThreads - (int64_t)kSmallClass;
@@ -974,31 +967,43 @@ __global__ __launch_bounds__(kFinThreads) void k_finish_small(
   const uint32_t cs = first1[j] - 1, cn = size[cs];
   if (cn > kSmallClass) {
     keep[j] = 1u;
+    tkeep[j] = 0u;
     return;
   }
   keep[j] = 0u;
   const Act x = act[j];
   const uint64_t kx = keys[j];
-  const bool deeper = (kx & 0xFFu) == 8u;   // 8: the line goes on past the 7-byte window
-  const uint32_t depth = cdep[x.gs] + cmin[x.gs] + 7u;
-  uint32_t rank = 0;
+  uint32_t lt = 0, eq_before = 0, eq = 0;
   for (uint32_t k = cs; k < cs + cn; ++k) {
     if (k == j) continue;
     const uint32_t q = (uint32_t)((int64_t)k - lo);   // inside the staged span
     const uint64_t ky = skey[q];
-    const uint32_t y = sid[q];
-    bool before;
-    if (ky != kx) {
-      before = ky < kx;
-    } else if (deeper) {   // equal windows, both longer: the bytes after the window
-      const int c = cmp_lines(text, n_bytes, off[y], lens[y], off[x.id], lens[x.id], depth);
-      before = c < 0 || (c == 0 && y < x.id);
-    } else {               // equal strings
-      before = y < x.id;
+    lt += ky < kx ? 1u : 0u;
+    if (ky == kx) {
+      ++eq;
+      eq_before += sid[q] < x.id ? 1u : 0u;
     }
-    rank += before ? 1u : 0u;
   }
-  order[x.id] = base + x.gs + rank;
+  const uint32_t slot = cs + lt + eq_before;   // the member's rank, as an index into the class's range
+  if (eq == 0 || (kx & 0xFFu) != 8u) {         // unique, or equal strings
+    order[x.id] = base + x.gs + lt + eq_before;
+    tkeep[slot] = 0u;
+  } else {                                     // a tie group past the window: its own class
+    const uint32_t g = x.gs + lt;
+    tie[slot] = Act{x.id, g};
+    tkeep[slot] = 1u;
+    tdep[g] = cdep[x.gs] + cmin[x.gs] + 7u;    // (the same value from every member)
+  }
+}
+
+// the tie groups' depth into cdep (after the finisher: their starts are no
+// other live class's start)
+__global__ void k_tie_dep(const Act* __restrict__ act, uint32_t m, const uint32_t* __restrict__ tdep,
+                          uint32_t* __restrict__ cdep) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const uint32_t g = act[j].gs;
+  cdep[g] = tdep[g];
 }
 
 // compaction of the kept elements (slot: exclusive scan of keep)
@@ -1010,8 +1015,10 @@ __global__ void k_compact_act(const Act* __restrict__ in, const uint32_t* __rest
   if (j >= m || !keep[j]) return;
   const uint32_t q = slot[j];
   out[q] = in[j];
-  kout[q] = kin[j];
-  vout[q] = vin[j];
+  if (kin) {
+    kout[q] = kin[j];
+    vout[q] = vin[j];
+  }
 }
 
 inline uint32_t blocks(uint64_t n, uint32_t t) { return (uint32_t)((n + t - 1) / t); }
@@ -1426,7 +1433,7 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
   const size_t H = rs_hist_len(N), SL = scan_sums_len(H > N ? H : N);
   // keysA/keysB/keysT u64, valsA/valsB/valsT u64, gs/ids/first/pos/bstart/keep/slot/lens u32,
   // act/act3 Act (and a spare), class depths cdep/cnext/cmin u32, radix histogram + scan sums, flag words
-  const size_t bytes = N * (8 * 6 + 4 * 8 + 8 * 3 + 4 * 3) + (H + SL) * 4 + 512;
+  const size_t bytes = N * (8 * 6 + 4 * 8 + 8 * 3 + 4 * 5) + (H + SL) * 4 + 512;
   Scratch S{c, st};
   TPCHK(c, hipMallocAsync(&S.base, bytes, st));
   char* p = static_cast<char*>(S.base);
@@ -1446,7 +1453,9 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
   uint32_t* lens = reinterpret_cast<uint32_t*>(p); p += N * 4;
   Act* act = reinterpret_cast<Act*>(p); p += N * 8;
   Act* act3 = reinterpret_cast<Act*>(p); p += N * 8;
-  p += N * 8;   // (spare)
+  Act* tie = reinterpret_cast<Act*>(p); p += N * 8;                // finisher tie groups, by rank
+  uint32_t* tkeep = reinterpret_cast<uint32_t*>(p); p += N * 4;   // ... their flags
+  uint32_t* tdep = reinterpret_cast<uint32_t*>(p); p += N * 4;    // ... their depth, by class start
   uint32_t* cdep = reinterpret_cast<uint32_t*>(p); p += N * 4;    // per class start: bytes its lines share
   uint32_t* cnext = reinterpret_cast<uint32_t*>(p); p += N * 4;   // ... of the classes the next round forms
   uint32_t* cmin = reinterpret_cast<uint32_t*>(p); p += N * 4;    // per class start: k_lcp's further common bytes
@@ -1524,17 +1533,36 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
     hipLaunchKernelGGL(k_keys, dim3(blocks(m, 256)), dim3(256), 0, st, d_text, d_off, lens, n_bytes, act, m, cdep,
                        cmin, (const uint64_t*)keysT, (const uint64_t*)valsT, keysB, valsB);
     hipLaunchKernelGGL(k_cls_size, dim3(blocks(m, 256)), dim3(256), 0, st, act, first, m, pos);
-    hipLaunchKernelGGL(k_finish_small, dim3(blocks(m, kFinThreads)), dim3(kFinThreads), 0, st, d_text, n_bytes, d_off,
-                       lens, act, keysB, first, pos, m, cdep, cmin, base, d_order, keep);
+    hipLaunchKernelGGL(k_finish_small, dim3(blocks(m, kFinThreads)), dim3(kFinThreads), 0, st, act, keysB, first, pos,
+                       m, cdep, cmin, base, d_order, keep, tie, tkeep, tdep);
     exscan(keep, slot, m);
     hipLaunchKernelGGL(k_compact_act, dim3(blocks(m, 256)), dim3(256), 0, st, act, keep, slot, m, act3, keysB, valsB,
                        keysA, valsA);
+    exscan(tkeep, bstart, m);
+    uint32_t nt = 0;
     {
-      uint32_t nm = 0;
+      uint32_t nm = 0, lastt = 0;
       TPCHK(c, hipMemcpyAsync(&nm, slot + m - 1, 4, hipMemcpyDeviceToHost, st));
       TPCHK(c, hipMemcpyAsync(&lastk, keep + m - 1, 4, hipMemcpyDeviceToHost, st));
+      TPCHK(c, hipMemcpyAsync(&nt, bstart + m - 1, 4, hipMemcpyDeviceToHost, st));
+      TPCHK(c, hipMemcpyAsync(&lastt, tkeep + m - 1, 4, hipMemcpyDeviceToHost, st));
       TPCHK(c, hipStreamSynchronize(st));
-      m = nm + lastk;
+      const uint32_t nb = nm + lastk;
+      nt += lastt;
+      // the tie groups behind the large classes (each group contiguous)
+      if (nt) {
+        hipLaunchKernelGGL(k_compact_act, dim3(blocks(m, 256)), dim3(256), 0, st, tie, tkeep, bstart, m, act3 + nb,
+                           (const uint64_t*)nullptr, (const uint64_t*)nullptr, (uint64_t*)nullptr, (uint64_t*)nullptr);
+        hipLaunchKernelGGL(k_tie_dep, dim3(blocks(nt, 256)), dim3(256), 0, st, act3 + nb, nt, tdep, cdep);
+        // their windows: the common-prefix pass and keys over the tie groups alone
+        hipLaunchKernelGGL(k_cls_first, dim3(blocks(nt, 256)), dim3(256), 0, st, act3 + nb, nt, bstart, cmin);
+        maxscan(bstart, first, nt);
+        hipLaunchKernelGGL(k_lcp, dim3(blocks(nt, 256)), dim3(256), 0, st, d_text, n_bytes, d_off, lens, act3 + nb,
+                           first, nt, cdep, cmin, keysT, valsT);
+        hipLaunchKernelGGL(k_keys, dim3(blocks(nt, 256)), dim3(256), 0, st, d_text, d_off, lens, n_bytes, act3 + nb,
+                           nt, cdep, cmin, (const uint64_t*)keysT, (const uint64_t*)valsT, keysA + nb, valsA + nb);
+      }
+      m = nb + nt;
       Act* sw = act;
       act = act3;
       act3 = sw;
