@@ -505,7 +505,6 @@ __global__ __launch_bounds__(kParseWG) RSA_PARSE_WIN_ATTR void k_parse_win(const
 // backtracking restated), reading from HBM.  Persistent grid over the
 // device-side count.
 constexpr uint32_t kSlowGrid = 2048;
-constexpr uint32_t kSlowStride = 65;   // LDS words per lane row (256 B + 1 word: rows start in different banks)
 template <bool kReduce>
 __global__ __launch_bounds__(kParseWG) void k_parse_slow(const uint8_t* __restrict__ text,
                                                          const uint64_t* __restrict__ off, uint64_t n_lines,
@@ -515,7 +514,6 @@ __global__ __launch_bounds__(kParseWG) void k_parse_slow(const uint8_t* __restri
                                                          const unsigned int* __restrict__ slow_n,
                                                          rsa_tuple* __restrict__ tuples, uint32_t* __restrict__ ts_out,
                                                          uint32_t* __restrict__ disp) {
-  __shared__ uint32_t srow[kReduce ? 1 : kParseWG * kSlowStride];   // one padded row per lane
   const uint32_t ns = *slow_n;
   const uint64_t n_bytes = off[n_lines];
   const uint32_t* w32 = reinterpret_cast<const uint32_t*>(text);
@@ -538,26 +536,6 @@ __global__ __launch_bounds__(kParseWG) void k_parse_slow(const uint8_t* __restri
         const rsa_text::GWordLn q{w32, text, pa, n_bytes, (uint32_t)plen, ~0ull, 0u};
         if (rsa_text::same_key(s, q)) d |= RSA_RED_SAME_KEY;
       }
-    } else if (len + 3 <= 4u * (kSlowStride - 1)) {
-      // the line copied into the lane's LDS row first (its words are independent
-      // loads, all in flight together): the general parse then reads LDS, not a
-      // chain of dependent HBM reads, one per 4 bytes scanned
-      uint32_t* row = srow + threadIdx.x * kSlowStride;
-      const uint64_t w0 = a >> 2, nw = ((a & 3u) + len + 3) >> 2;
-      for (uint64_t k = 0; k < nw; ++k) {
-        const uint64_t q = w0 + k;
-        uint32_t x;
-        if (4 * q + 4 <= n_bytes) {
-          x = w32[q];
-        } else {
-          x = 0;
-          for (uint32_t t = 0; t < 4; ++t)
-            if (4 * q + t < n_bytes) x |= (uint32_t)text[4 * q + t] << (8 * t);
-        }
-        row[k] = x;
-      }
-      const rsa_text::WordLn ls{row, (uint32_t)(a & 3u), (uint32_t)len};
-      rsa_text::parse_line(ls, ifcs, n_ifcs, spells, n_spells, tup, ts, d);
     } else {
       rsa_text::parse_line(s, ifcs, n_ifcs, spells, n_spells, tup, ts, d);
     }
