@@ -2422,7 +2422,10 @@ __global__ __launch_bounds__(1024) void k_cap_scatter_lds(const Slot* S, const u
 // digits from the highest set bit of (max - min) down, so the digits of keys
 // that share their top bits (time-ordered order keys) still spread over the
 // bins.  Per-wave LDS histograms keep bin contention inside a wave.
-constexpr int kSelThreads = 1024;
+// 256 threads per rule: segments are ~cap..2 cap keys, so a pass is a few
+// keys per thread and the passes are barrier-bound; four times the rules in
+// flight at once (eight workgroups per CU) instead of wider workgroups
+constexpr int kSelThreads = 256;
 __global__ __launch_bounds__(kSelThreads) void k_cap_select(const unsigned long long* keys,
                                                             const uint32_t* capped_start, const uint32_t* capped_fill,
                                                             const uint32_t* capped_gid, uint32_t cap,
@@ -3111,7 +3114,7 @@ int cap_select(rsa_ctx* c, unsigned long long* out, uint32_t* h_n_capped) {
                                                           c->d_cidx, c->d_capped_start, c->d_capped_cnt, ukey,
                                                           c->d_capped_prev, c->d_keys, c->sort_alloc, c->d_flags);
   HIPCHK(c, hipGetLastError());
-  const unsigned sel_grid = nr < (uint32_t)c->cu_count * 2 ? nr : (unsigned)c->cu_count * 2;
+  const unsigned sel_grid = nr < (uint32_t)c->cu_count * 8 ? nr : (unsigned)c->cu_count * 8;
   k_cap_select<<<sel_grid, kSelThreads, 0, c->stream>>>(c->d_keys, c->d_capped_start, c->d_capped_cnt, c->d_capped_gid,
                                                         c->cap, d_ncap, out);
   HIPCHK(c, hipGetLastError());
