@@ -720,11 +720,12 @@ def text_main(args):
         # split -> parse -> classify -> order keys within each rule (the reducer
         # only compares one rule's lines: pipeline.analyze_text) -> aggregate
         ev[0].record()
+        # one pass over the text: offsets and the line count (the offset
+        # buffer is sized for the lines the generator rendered)
         nl = ctypes.c_uint64(0)
-        ctx.call('rsa_text_count_lines', v(text), ctypes.c_uint64(len(data)), ctypes.byref(nl))
+        ctx.call('rsa_text_split', v(text), ctypes.c_uint64(len(data)), v(off), ctypes.c_uint64(n), ctypes.byref(nl))
         if nl.value != n:
             die('line count %d != %d' % (nl.value, n))
-        ctx.call('rsa_text_line_offsets', v(text), ctypes.c_uint64(len(data)), v(off), ctypes.c_uint64(n))
         ev[1].record()
         ctx.call('rsa_parse_text', v(text), v(off), ctypes.c_uint64(n), hp(ifcs), ctypes.c_uint32(len(ifcs)),
                  hp(spells), ctypes.c_uint32(len(spells)), v(tup), v(ts), v(disp))

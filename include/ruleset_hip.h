@@ -378,6 +378,12 @@ typedef struct rsa_parse_spell {
 int rsa_text_count_lines(rsa_ctx *ctx, const uint8_t *d_text, uint64_t n_bytes, uint64_t *h_n_lines);
 /* Line start offsets: d_off[0 .. n_lines] (d_off[n_lines] = n_bytes). */
 int rsa_text_line_offsets(rsa_ctx *ctx, const uint8_t *d_text, uint64_t n_bytes, uint64_t *d_off, uint64_t n_lines);
+/* Both in one pass over the text: *h_n_lines = number of lines; when it is
+ * <= max_lines, d_off[0 .. n_lines] as rsa_text_line_offsets writes them,
+ * else RSA_ERR_CAPACITY (d_off unspecified; retry with room for *h_n_lines + 1
+ * offsets). */
+int rsa_text_split(rsa_ctx *ctx, const uint8_t *d_text, uint64_t n_bytes, uint64_t *d_off, uint64_t max_lines,
+                   uint64_t *h_n_lines);
 /* Parse every line: d_tuples (zero unless CLASSIFY), d_ts (codes, 0 unless
  * hit+BUILT), d_disp (RSA_LINE_* | interface index << 8).  h_ifcs / h_spells are
  * host tables (n_ifcs <= 4096, n_spells <= 64). */

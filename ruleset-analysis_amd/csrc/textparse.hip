@@ -1280,28 +1280,65 @@ int rsa_text_count_lines(rsa_ctx* c, const uint8_t* d_text, uint64_t n, uint64_t
   return RSA_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// One pass over the text: line starts d_off[1 ..] for lines < max_lines + 1
+// (k_nl_offsets) and the line count (the last block's inclusive prefix, + 1
+// when the text does not end in '\n').  d_off[0] = 0; the caller sets
+// d_off[n_lines].
+int split_pass(rsa_ctx* c, const uint8_t* d_text, uint64_t n, uint64_t* d_off, uint64_t max_lines,
+               uint64_t* h_count) {
+  hipStream_t st = rsa_internal_stream(c);
+  *h_count = 0;
+  hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(1), 0, st, d_off, (uint64_t)0);
+  if (!n) return RSA_OK;
+  const uint64_t nb = (n + kSplitBlock - 1) / kSplitBlock;
+  if (nb > 0xFFFFFFFFull) return rsa_internal_fail(c, RSA_ERR_ARG, "text too large");
+  const int aligned = (reinterpret_cast<uintptr_t>(d_text) & 15u) == 0;
+  Scratch S{c, st};
+  TPCHK(c, hipMallocAsync(&S.base, nb * 8 + 64, st));
+  unsigned long long* state = static_cast<unsigned long long*>(S.base);   // per block: look-back word
+  unsigned int* ticket = reinterpret_cast<unsigned int*>(state + nb);     // [0] ticket, [1] error flag
+  TPCHK(c, hipMemsetAsync(S.base, 0, nb * 8 + 64, st));
+  hipLaunchKernelGGL(k_nl_offsets, dim3((uint32_t)nb), dim3(kSplitThreads), 0, st, d_text, n, aligned, d_off, max_lines,
+                     state, ticket);
+  TPCHK(c, hipGetLastError());
+  unsigned int err = 0;
+  unsigned long long last_state = 0;
+  uint8_t last = 0;
+  TPCHK(c, hipMemcpyAsync(&err, ticket + 1, 4, hipMemcpyDeviceToHost, st));
+  TPCHK(c, hipMemcpyAsync(&last_state, state + nb - 1, 8, hipMemcpyDeviceToHost, st));
+  TPCHK(c, hipMemcpyAsync(&last, d_text + n - 1, 1, hipMemcpyDeviceToHost, st));
+  TPCHK(c, hipStreamSynchronize(st));
+  if (err || !(last_state & kLbIncl)) return rsa_internal_fail(c, RSA_ERR_HIP, "text split: look-back did not resolve");
+  *h_count = (last_state & kLbVal) + (last != '\n' ? 1u : 0u);
+  return RSA_OK;
+}
+}  // namespace
+
+extern "C" {
+
 int rsa_text_line_offsets(rsa_ctx* c, const uint8_t* d_text, uint64_t n, uint64_t* d_off, uint64_t n_lines) {
   if (!c || !d_off || (n && !d_text)) return RSA_ERR_ARG;
-  hipStream_t st = rsa_internal_stream(c);
-  hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(1), 0, st, d_off, (uint64_t)0);
-  if (n) {
-    const uint64_t nb = (n + kSplitBlock - 1) / kSplitBlock;
-    if (nb > 0xFFFFFFFFull) return rsa_internal_fail(c, RSA_ERR_ARG, "text too large");
-    const int aligned = (reinterpret_cast<uintptr_t>(d_text) & 15u) == 0;
-    Scratch S{c, st};
-    TPCHK(c, hipMallocAsync(&S.base, nb * 8 + 64, st));
-    unsigned long long* state = static_cast<unsigned long long*>(S.base);   // per block: look-back word
-    unsigned int* ticket = reinterpret_cast<unsigned int*>(state + nb);     // [0] ticket, [1] error flag
-    TPCHK(c, hipMemsetAsync(S.base, 0, nb * 8 + 64, st));
-    hipLaunchKernelGGL(k_nl_offsets, dim3((uint32_t)nb), dim3(kSplitThreads), 0, st, d_text, n, aligned, d_off, n_lines,
-                       state, ticket);
-    TPCHK(c, hipGetLastError());
-    unsigned int err = 0;
-    TPCHK(c, hipMemcpyAsync(&err, ticket + 1, 4, hipMemcpyDeviceToHost, st));
-    TPCHK(c, hipStreamSynchronize(st));
-    if (err) return rsa_internal_fail(c, RSA_ERR_HIP, "rsa_text_line_offsets: look-back did not resolve");
-  }
-  hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(1), 0, st, d_off + n_lines, n);
+  uint64_t count = 0;
+  const int rc = split_pass(c, d_text, n, d_off, n_lines, &count);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(1), 0, rsa_internal_stream(c), d_off + n_lines, n);
+  TPCHK(c, hipGetLastError());
+  return RSA_OK;
+}
+
+int rsa_text_split(rsa_ctx* c, const uint8_t* d_text, uint64_t n, uint64_t* d_off, uint64_t max_lines,
+                   uint64_t* h_n_lines) {
+  if (!c || !d_off || !h_n_lines || (n && !d_text)) return RSA_ERR_ARG;
+  uint64_t count = 0;
+  const int rc = split_pass(c, d_text, n, d_off, max_lines, &count);
+  *h_n_lines = count;
+  if (rc) return rc;
+  if (count > max_lines)
+    return rsa_internal_fail(c, RSA_ERR_CAPACITY, "rsa_text_split: more lines than max_lines (*h_n_lines holds the count)");
+  hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(1), 0, rsa_internal_stream(c), d_off + count, n);
   TPCHK(c, hipGetLastError());
   return RSA_OK;
 }

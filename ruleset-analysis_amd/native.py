@@ -77,6 +77,7 @@ SYMBOLS = {
     'rsa_shadowed_ports': (I32, [P, P, U32, P, U32, P]),
     'rsa_text_count_lines': (I32, [P, P, U64, PU64]),
     'rsa_text_line_offsets': (I32, [P, P, U64, P, U64]),
+    'rsa_text_split': (I32, [P, P, U64, P, U64, PU64]),
     'rsa_parse_text': (I32, [P, P, P, U64, P, U32, P, U32, P, P, P]),
     'rsa_order_keys': (I32, [P, P, P, U64, U64, P]),
     'rsa_order_keys_grouped': (I32, [P, P, P, U64, P, U64, P]),

@@ -84,12 +84,8 @@ class ReducerStream(object):
         ctx = eng.ctx
         v = lambda t: ctypes.c_void_p(t.data_ptr())
         text = textparse._device_bytes(torch, data, eng.device)
-        nl = ctypes.c_uint64(0)
-        ctx.call('rsa_text_count_lines', v(text), ctypes.c_uint64(len(data)), ctypes.byref(nl))
-        n = int(nl.value)
         dev = eng.device
-        off = torch.empty(n + 1, dtype=torch.int64, device=dev)
-        ctx.call('rsa_text_line_offsets', v(text), ctypes.c_uint64(len(data)), v(off), ctypes.c_uint64(n))
+        off, n = textparse.split_lines_device(ctx, torch, text, len(data))
         tuples = torch.zeros((max(n, 1), 4), dtype=torch.int32, device=dev)[:n]
         ts = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)[:n]
         disp = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)[:n]

@@ -201,6 +201,29 @@ class ParsedText(object):
         return DeviceBatch(self.tuples, self.ts, self.order)
 
 
+def split_lines_device(ctx, torch, text, n_bytes, hint=None):
+    """Line start offsets of device text in one pass (``rsa_text_split``):
+    (off tensor of n + 1 int64, n).  The offset buffer is sized from ``hint``
+    (an expected line count) or one line per 48 bytes; when the text holds more
+    lines, the library reports the count and the split runs again into a buffer
+    of that size."""
+    from .native import NativeError, RSA_ERR_CAPACITY
+    v = lambda t: ctypes.c_void_p(t.data_ptr())
+    cap = int(hint) if hint is not None else n_bytes // 48 + 16
+    nl = ctypes.c_uint64(0)
+    for _ in range(2):
+        off = torch.empty(cap + 1, dtype=torch.int64, device=text.device)
+        try:
+            ctx.call('rsa_text_split', v(text), ctypes.c_uint64(n_bytes), v(off), ctypes.c_uint64(cap), ctypes.byref(nl))
+            n = int(nl.value)
+            return off[:n + 1], n
+        except NativeError as e:
+            if e.code != RSA_ERR_CAPACITY or int(nl.value) <= cap:
+                raise
+            cap = int(nl.value)
+    raise RuntimeError('rsa_text_split: line count changed between passes')
+
+
 def _device_bytes(torch, data, device):
     t = torch.empty(len(data), dtype=torch.uint8, device=device)
     if len(data):
@@ -233,11 +256,7 @@ def parse_text(engine, host, data, db, compiled, pspell=None, order_base=0, need
     dev = engine.device
     text = _device_bytes(torch, data, dev)
     v = lambda t: ctypes.c_void_p(t.data_ptr())
-    nl = ctypes.c_uint64(0)
-    ctx.call('rsa_text_count_lines', v(text), ctypes.c_uint64(len(data)), ctypes.byref(nl))
-    n = int(nl.value)
-    off = torch.empty(n + 1, dtype=torch.int64, device=dev)
-    ctx.call('rsa_text_line_offsets', v(text), ctypes.c_uint64(len(data)), v(off), ctypes.c_uint64(n))
+    off, n = split_lines_device(ctx, torch, text, len(data))
     ifcs, acl_names = interface_table(db, compiled, host)
     sp = spell_table(spells)
     tuples = torch.zeros((max(n, 1), 4), dtype=torch.int32, device=dev)[:n]

@@ -387,6 +387,36 @@ def test_gpu_order_keys_adversarial(engine):
 
 
 @pytest.mark.gpu
+def test_gpu_text_split_one_pass(engine):
+    """rsa_text_split: the offsets rsa_text_line_offsets writes and the count
+    rsa_text_count_lines returns, in one pass; too small a buffer reports the
+    count with RSA_ERR_CAPACITY (blocks of 64 KiB: the look-back crosses many)."""
+    import ctypes
+    import torch
+    from ruleset_analysis_amd.native import NativeError, RSA_ERR_CAPACITY
+    rng = random.Random(5)
+    for data in (b'', b'x', b'\n', b'a\nb', b'a\nb\n',
+                 b''.join(bytes(rng.randrange(32, 127) for _ in range(rng.randrange(0, 300))) + b'\n'
+                          for _ in range(20000)) + b'tail without newline'):
+        lines = data.split(b'\n')
+        n = len(lines) - (1 if data.endswith(b'\n') or not data else 0)
+        want = np.cumsum([0] + [len(l) + 1 for l in lines[:n]])
+        want[-1] = min(want[-1], len(data))
+        text = textparse._device_bytes(torch, data, engine.device) if data else torch.zeros(1, dtype=torch.uint8,
+                                                                                              device=engine.device)
+        off, got_n = textparse.split_lines_device(engine.ctx, torch, text, len(data), hint=max(n // 3, 1))
+        assert got_n == n
+        assert np.array_equal(off.cpu().numpy(), want), data[:40]
+        if n > 1:
+            buf = torch.empty(n, dtype=torch.int64, device=engine.device)
+            nl = ctypes.c_uint64(0)
+            with pytest.raises(NativeError) as e:
+                engine.ctx.call('rsa_text_split', ctypes.c_void_p(text.data_ptr()), ctypes.c_uint64(len(data)),
+                                ctypes.c_void_p(buf.data_ptr()), ctypes.c_uint64(n - 1), ctypes.byref(nl))
+            assert e.value.code == RSA_ERR_CAPACITY and nl.value == n
+
+
+@pytest.mark.gpu
 def test_gpu_parse_1m_lines_equals_generator(engine):
     dbj, info = synth.make_db(21, 2000, interfaces=('outside', 'partner'))
     db = acldb.load_json(dbj)
