@@ -671,24 +671,25 @@ __global__ void k_grp_settle(const uint32_t* __restrict__ keys, const uint32_t* 
   keep[j] = settled ? 0u : 1u;
 }
 
-struct Act {               // an unsettled line: its id and the position its group starts at
-  uint32_t id, gs;
+struct Act {               // an unsettled line: its text offset, id, the position its class starts at, length
+  uint64_t off;            // (offset and length travel with the element: the rounds read them in order
+  uint32_t id, gs, len;    //  instead of gathering them by line id)
 };
+static_assert(sizeof(Act) == 24, "Act layout");
 
 // the window of a class: its depth (bytes all its lines share, cdep) plus the
 // further common prefix k_lcp found (cmin), both indexed by the class start
 // (preH / preL: the line's 16 bytes from the class depth, big-endian, as k_lcp
 // read them: a window inside them needs no text read -- text reads by line
 // are one HBM transaction each, the staged bytes are coalesced)
-__global__ void k_keys(const uint8_t* __restrict__ text, const uint64_t* __restrict__ off,
-                       const uint32_t* __restrict__ lens, uint64_t n_bytes, const Act* __restrict__ act, uint32_t m,
+__global__ void k_keys(const uint8_t* __restrict__ text, uint64_t n_bytes, const Act* __restrict__ act, uint32_t m,
                        const uint32_t* __restrict__ cdep, const uint32_t* __restrict__ cmin,
                        const uint64_t* __restrict__ preH, const uint64_t* __restrict__ preL,
                        uint64_t* __restrict__ keys, uint64_t* __restrict__ vals) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= m) return;
   const Act x = act[j];
-  const uint32_t e = cmin[x.gs], len = lens[x.id];
+  const uint32_t e = cmin[x.gs], len = x.len;
   const uint64_t pos = (uint64_t)cdep[x.gs] + e;
   uint64_t key;
   if (e <= 9u) {
@@ -700,7 +701,7 @@ __global__ void k_keys(const uint8_t* __restrict__ text, const uint64_t* __restr
     if (rem && rem < 7) k &= ~0ull << (64u - 8u * rem);
     key = rem ? (k | (rem < 8 ? rem : 8u)) : 0ull;
   } else {
-    key = chunk_key(text, n_bytes, off[x.id], len, pos);
+    key = chunk_key(text, n_bytes, x.off, len, pos);
   }
   keys[j] = key;
   vals[j] = (uint64_t)x.gs << 32 | x.id;
@@ -715,8 +716,7 @@ __global__ void k_keys(const uint8_t* __restrict__ text, const uint64_t* __restr
 // bytes.  Capped at kLcpMax bytes per pass (the window then starts there).
 constexpr uint32_t kLcpMax = 4096;
 // (the line's first 16 bytes from the depth go to preH / preL for k_keys)
-__global__ void k_lcp(const uint8_t* __restrict__ text, uint64_t n_bytes, const uint64_t* __restrict__ off,
-                      const uint32_t* __restrict__ lens, const Act* __restrict__ act,
+__global__ void k_lcp(const uint8_t* __restrict__ text, uint64_t n_bytes, const Act* __restrict__ act,
                       const uint32_t* __restrict__ first1, uint32_t m, const uint32_t* __restrict__ cdep,
                       uint32_t* __restrict__ cmin, uint64_t* __restrict__ preH, uint64_t* __restrict__ preL) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -724,18 +724,19 @@ __global__ void k_lcp(const uint8_t* __restrict__ text, uint64_t n_bytes, const 
   if (j < m) {
     const Act x = act[j];
     gs = x.gs;
-    const uint32_t y = act[first1[j] - 1].id;
-    const uint32_t d = cdep[gs], la = lens[x.id], lb = lens[y];
+    const Act ya = act[first1[j] - 1];   // the class's first line
+    const uint32_t y = ya.id;
+    const uint32_t d = cdep[gs], la = x.len, lb = ya.len;
     const uint32_t ra = la > d ? la - d : 0u, rb = lb > d ? lb - d : 0u;
     const uint32_t lim = (ra < rb ? ra : rb) < kLcpMax ? (ra < rb ? ra : rb) : kLcpMax;
-    const uint64_t pa = off[x.id] + d;
+    const uint64_t pa = x.off + d;
     const uint64_t H = ra ? line_chunk8(text, n_bytes, pa, ra) : 0ull;
     const uint64_t L = ra > 8 ? line_chunk8(text, n_bytes, pa + 8, ra - 8) : 0ull;
     preH[j] = H;
     preL[j] = L;
     e = lim;
     if (y != x.id) {
-      const uint64_t pb = off[y] + d;
+      const uint64_t pb = ya.off + d;
       for (uint32_t p = 0; p < lim; p += 8) {
         const uint64_t ka = p == 0 ? H : p == 8 ? L : line_chunk8(text, n_bytes, pa + p, la - d - p),
                        kb = line_chunk8(text, n_bytes, pb + p, lb - d - p);
@@ -872,14 +873,28 @@ __global__ void k_settle(const uint64_t* __restrict__ keys, const uint32_t* __re
 // the kept elements into act; their new classes' depth into cnext[new start]:
 // the old class's window end (cdep + cmin of the old start gs_old, 0 when
 // gs_old is null) + adv (7: the window matched; 0: the group stage)
+// (in: the elements in this order, whose offset and length are taken; null:
+// gathered by line id from off / lens -- after a sort)
 __global__ void k_compact(const uint32_t* __restrict__ ids, const uint32_t* __restrict__ ngs1,
                           const uint32_t* __restrict__ keep, const uint32_t* __restrict__ slot, uint32_t m,
                           Act* __restrict__ out, const uint32_t* __restrict__ gs_old, const uint32_t* __restrict__ cdep,
-                          const uint32_t* __restrict__ cmin, uint32_t* __restrict__ cnext, uint32_t adv) {
+                          const uint32_t* __restrict__ cmin, uint32_t* __restrict__ cnext, uint32_t adv,
+                          const Act* __restrict__ in, const uint64_t* __restrict__ off,
+                          const uint32_t* __restrict__ lens) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= m || !keep[j]) return;
-  const uint32_t g = ngs1[j] - 1;
-  out[slot[j]] = Act{ids[j], g};
+  const uint32_t g = ngs1[j] - 1, id = ids[j];
+  uint64_t o;
+  uint32_t l;
+  if (in) {
+    const Act x = in[j];
+    o = x.off;
+    l = x.len;
+  } else {
+    o = off[id];
+    l = lens[id];
+  }
+  out[slot[j]] = Act{o, id, g, l};
   cnext[g] = (gs_old ? cdep[gs_old[j]] + cmin[gs_old[j]] : 0u) + adv;   // (the same value from every member)
 }
 
@@ -968,7 +983,7 @@ __global__ __launch_bounds__(kFinThreads) void k_finish_small(
     tkeep[slot] = 0u;
   } else {                                     // a tie group past the window: its own class
     const uint32_t g = x.gs + lt;
-    tie[slot] = Act{x.id, g};
+    tie[slot] = Act{x.off, x.id, g, x.len};
     tkeep[slot] = 1u;
     tdep[g] = cdep[x.gs] + cmin[x.gs] + 7u;    // (the same value from every member)
   }
@@ -1448,7 +1463,7 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
   const size_t H = rs_hist_len(N), SL = scan_sums_len(H > N ? H : N);
   // keysA/keysB/keysT u64, valsA/valsB/valsT u64, gs/ids/first/pos/bstart/keep/slot/lens u32,
   // act/act3 Act (and a spare), class depths cdep/cnext/cmin u32, radix histogram + scan sums, flag words
-  const size_t bytes = N * (8 * 6 + 4 * 8 + 8 * 3 + 4 * 5) + (H + SL) * 4 + 512;
+  const size_t bytes = N * (8 * 6 + 4 * 8 + sizeof(Act) * 3 + 4 * 5) + (H + SL) * 4 + 512;
   Scratch S{c, st};
   TPCHK(c, hipMallocAsync(&S.base, bytes, st));
   char* p = static_cast<char*>(S.base);
@@ -1466,9 +1481,9 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
   uint32_t* keep = reinterpret_cast<uint32_t*>(p); p += N * 4;
   uint32_t* slot = reinterpret_cast<uint32_t*>(p); p += N * 4;
   uint32_t* lens = reinterpret_cast<uint32_t*>(p); p += N * 4;
-  Act* act = reinterpret_cast<Act*>(p); p += N * 8;
-  Act* act3 = reinterpret_cast<Act*>(p); p += N * 8;
-  Act* tie = reinterpret_cast<Act*>(p); p += N * 8;                // finisher tie groups, by rank
+  Act* act = reinterpret_cast<Act*>(p); p += N * sizeof(Act);
+  Act* act3 = reinterpret_cast<Act*>(p); p += N * sizeof(Act);
+  Act* tie = reinterpret_cast<Act*>(p); p += N * sizeof(Act);       // finisher tie groups, by rank
   uint32_t* tkeep = reinterpret_cast<uint32_t*>(p); p += N * 4;   // ... their flags
   uint32_t* tdep = reinterpret_cast<uint32_t*>(p); p += N * 4;    // ... their depth, by class start
   uint32_t* cdep = reinterpret_cast<uint32_t*>(p); p += N * 4;    // per class start: bytes its lines share
@@ -1529,7 +1544,8 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
   }
   exscan(keep, slot, n);
   hipLaunchKernelGGL(k_compact, dim3(blocks(n, 256)), dim3(256), 0, st, idsB, first, keep, slot, n, act,
-                     (const uint32_t*)nullptr, (const uint32_t*)nullptr, (const uint32_t*)nullptr, cdep, adv0);
+                     (const uint32_t*)nullptr, (const uint32_t*)nullptr, (const uint32_t*)nullptr, cdep, adv0,
+                     (const Act*)nullptr, d_off, (const uint32_t*)lens);
   uint32_t m = 0, lastk = 0;
   TPCHK(c, hipMemcpyAsync(&m, slot + n - 1, 4, hipMemcpyDeviceToHost, st));
   TPCHK(c, hipMemcpyAsync(&lastk, keep + n - 1, 4, hipMemcpyDeviceToHost, st));
@@ -1543,10 +1559,10 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
     // (k_finish_small) and the others go on to the sort of their windows
     hipLaunchKernelGGL(k_cls_first, dim3(blocks(m, 256)), dim3(256), 0, st, act, m, bstart, cmin);
     maxscan(bstart, first, m);
-    hipLaunchKernelGGL(k_lcp, dim3(blocks(m, 256)), dim3(256), 0, st, d_text, n_bytes, d_off, lens, act, first, m,
-                       cdep, cmin, keysT, valsT);
-    hipLaunchKernelGGL(k_keys, dim3(blocks(m, 256)), dim3(256), 0, st, d_text, d_off, lens, n_bytes, act, m, cdep,
-                       cmin, (const uint64_t*)keysT, (const uint64_t*)valsT, keysB, valsB);
+    hipLaunchKernelGGL(k_lcp, dim3(blocks(m, 256)), dim3(256), 0, st, d_text, n_bytes, act, first, m, cdep, cmin,
+                       keysT, valsT);
+    hipLaunchKernelGGL(k_keys, dim3(blocks(m, 256)), dim3(256), 0, st, d_text, n_bytes, act, m, cdep, cmin,
+                       (const uint64_t*)keysT, (const uint64_t*)valsT, keysB, valsB);
     hipLaunchKernelGGL(k_cls_size, dim3(blocks(m, 256)), dim3(256), 0, st, act, first, m, pos);
     hipLaunchKernelGGL(k_finish_small, dim3(blocks(m, kFinThreads)), dim3(kFinThreads), 0, st, act, keysB, first, pos,
                        m, cdep, cmin, base, d_order, keep, tie, tkeep, tdep);
@@ -1572,10 +1588,10 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
         // their windows: the common-prefix pass and keys over the tie groups alone
         hipLaunchKernelGGL(k_cls_first, dim3(blocks(nt, 256)), dim3(256), 0, st, act3 + nb, nt, bstart, cmin);
         maxscan(bstart, first, nt);
-        hipLaunchKernelGGL(k_lcp, dim3(blocks(nt, 256)), dim3(256), 0, st, d_text, n_bytes, d_off, lens, act3 + nb,
-                           first, nt, cdep, cmin, keysT, valsT);
-        hipLaunchKernelGGL(k_keys, dim3(blocks(nt, 256)), dim3(256), 0, st, d_text, d_off, lens, n_bytes, act3 + nb,
-                           nt, cdep, cmin, (const uint64_t*)keysT, (const uint64_t*)valsT, keysA + nb, valsA + nb);
+        hipLaunchKernelGGL(k_lcp, dim3(blocks(nt, 256)), dim3(256), 0, st, d_text, n_bytes, act3 + nb, first, nt, cdep,
+                           cmin, keysT, valsT);
+        hipLaunchKernelGGL(k_keys, dim3(blocks(nt, 256)), dim3(256), 0, st, d_text, n_bytes, act3 + nb, nt, cdep, cmin,
+                           (const uint64_t*)keysT, (const uint64_t*)valsT, keysA + nb, valsA + nb);
       }
       m = nb + nt;
       Act* sw = act;
@@ -1598,7 +1614,8 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
       cnext = sw;
       continue;
     }
-    if (!h_live[3]) {
+    const bool sorted = h_live[3] != 0;
+    if (!sorted) {
       // every class already in key order: no sort
       hipLaunchKernelGGL(k_split_vals, dim3(blocks(m, 256)), dim3(256), 0, st, valsA, m, gs, ids);
     } else {
@@ -1622,8 +1639,16 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
                        keep);
     // slot (new group start + 1) is still needed by k_compact: scan the keep flags into `first`
     exscan(keep, first, m);
-    hipLaunchKernelGGL(k_compact, dim3(blocks(m, 256)), dim3(256), 0, st, ids, slot, keep, first, m, act,
-                       (const uint32_t*)gs, (const uint32_t*)cdep, (const uint32_t*)cmin, cnext, 7u);
+    // (unsorted: element j is act[j], its offset and length read in order;
+    // sorted: gathered by line id)
+    hipLaunchKernelGGL(k_compact, dim3(blocks(m, 256)), dim3(256), 0, st, ids, slot, keep, first, m, act3,
+                       (const uint32_t*)gs, (const uint32_t*)cdep, (const uint32_t*)cmin, cnext, 7u,
+                       sorted ? (const Act*)nullptr : (const Act*)act, d_off, (const uint32_t*)lens);
+    {
+      Act* swa = act;
+      act = act3;
+      act3 = swa;
+    }
     uint32_t* sw = cdep;
     cdep = cnext;
     cnext = sw;
