@@ -257,6 +257,7 @@ def parse_text(engine, host, data, db, compiled, pspell=None, order_base=0, need
     text = _device_bytes(torch, data, dev)
     v = lambda t: ctypes.c_void_p(t.data_ptr())
     off, n = split_lines_device(ctx, torch, text, len(data))
+    n_all = n       # (n may end at a line the mapper dies on, below)
     ifcs, acl_names = interface_table(db, compiled, host)
     sp = spell_table(spells)
     tuples = torch.zeros((max(n, 1), 4), dtype=torch.int32, device=dev)[:n]
@@ -321,7 +322,7 @@ def parse_text(engine, host, data, db, compiled, pspell=None, order_base=0, need
     P.nl = np.zeros(n, bool)
     if n:
         P.nl[:] = True
-        if not data.endswith(b'\n') and n == int(nl.value):
+        if not data.endswith(b'\n') and n == n_all:
             P.nl[-1] = False
     P.tuples, P.ts, P.order = tuples[:n], ts[:n], order[:n]
     if keep_text:
