@@ -517,7 +517,6 @@ __global__ __launch_bounds__(kParseWG) void k_parse_slow(const uint8_t* __restri
   const uint32_t ns = *slow_n;
   const uint64_t n_bytes = off[n_lines];
   const uint32_t* w32 = reinterpret_cast<const uint32_t*>(text);
-  const bool aligned16 = (reinterpret_cast<uintptr_t>(text) & 15u) == 0;
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < ns; j += gridDim.x * blockDim.x) {
     const uint64_t i = slow_idx[j];
     const uint64_t a = off[i], b = off[i + 1];
@@ -537,9 +536,6 @@ __global__ __launch_bounds__(kParseWG) void k_parse_slow(const uint8_t* __restri
         const rsa_text::GWordLn q{w32, text, pa, n_bytes, (uint32_t)plen, ~0ull, 0u};
         if (rsa_text::same_key(s, q)) d |= RSA_RED_SAME_KEY;
       }
-    } else if (aligned16) {
-      const rsa_text::GChunkLn c16{w32, text, a, n_bytes, (uint32_t)len, ~0ull, {0u, 0u, 0u, 0u}};
-      rsa_text::parse_line(c16, ifcs, n_ifcs, spells, n_spells, tup, ts, d);
     } else {
       rsa_text::parse_line(s, ifcs, n_ifcs, spells, n_spells, tup, ts, d);
     }
