@@ -456,7 +456,7 @@ __global__ __launch_bounds__(kParseWG) RSA_PARSE_WIN_ATTR void k_parse_win(const
   uint64_t ci = a >> 4;
   const uint32_t q = (uint32_t)(a >> 2) & 3u, r = ((uint32_t)a & 3u) * 8u;
   uint4 w0 = text_chunk(t16, text, ci, n_full, n_bytes), w1 = text_chunk(t16, text, ci + 1, n_full, n_bytes);
-  State st;
+  State st = start(tprog);
   for (uint32_t base = 0; base < nmax; base += 16) {
     const uint4 w2 = text_chunk(t16, text, ci + 2, n_full, n_bytes);   // the next round's second chunk
     const uint32_t W[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};

@@ -708,9 +708,22 @@ constexpr uint32_t pack3(char a, char b, char c) { return (uint32_t)(uint8_t)a <
 // combined with integer ops and bit selects (v_bfi): booleans would live in
 // scalar lane masks, and their and/or/select bookkeeping is scalar work that
 // the CU's one scalar unit serialises over its four SIMDs.
+#ifndef RSA_TPL_PREFETCH
+#define RSA_TPL_PREFETCH 1   // A/B builds: 0 reads prog[seg] on every byte
+#endif
+// d0 = prog[seg], d1 = prog[seg + 1]: the next descriptor is a select, and
+// the read of the one after it is issued a byte ahead of its use, so no LDS
+// read sits on the byte-to-byte dependence chain.
 struct State {
-  uint32_t seg = 0, cnt = 0, pos0 = 0, ok = 1;
+  uint32_t seg = 0, cnt = 0, pos0 = 0, ok = 1, d0 = 0, d1 = 0;
 };
+template <class P>
+RSA_HD State start(P prog) {
+  State st;
+  st.d0 = prog[0];
+  st.d1 = prog[1];
+  return st;
+}
 RSA_HD uint32_t lt01(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a - b) >> 63); }   // a < b
 RSA_HD uint32_t nz01(uint32_t a) { return a ? 1u : 0u; }
 RSA_HD uint32_t sel(uint32_t m01, uint32_t a, uint32_t b) {   // m01 ? a : b, as a bit select
@@ -719,7 +732,7 @@ RSA_HD uint32_t sel(uint32_t m01, uint32_t a, uint32_t b) {   // m01 ? a : b, as
 }
 template <class P, class C, class Q>
 RSA_HD void step(State& st, uint32_t i, uint32_t c, uint32_t act, P prog, C cls, Q slot) {
-  const uint32_t desc = prog[st.seg];
+  const uint32_t desc = RSA_TPL_PREFETCH ? st.d0 : prog[st.seg];
   const uint32_t lit = desc & 0xFFu, msk = (desc >> 8) & 0xFFu, mn = (desc >> 16) & 7u, mx = (desc >> 19) & 0xFFu,
                  fld = desc >> 27;
   const uint32_t is_run = nz01(msk);
@@ -731,9 +744,15 @@ RSA_HD void step(State& st, uint32_t i, uint32_t c, uint32_t act, P prog, C cls,
   const uint32_t step_ok = cont | (((lt01(cnt, mn) ^ 1u) | (is_run ^ 1u)) & (1u - nz01(c ^ lit)) &
                                    nz01(desc ^ kEndSeg));
   const uint32_t nok = st.ok & step_ok;
-  st.seg += act & nok & (cont ^ 1u) & lt01(st.seg + 1, kProgLen);
+  const uint32_t adv = act & nok & (cont ^ 1u) & lt01(st.seg + 1, kProgLen);
+  st.seg += adv;
   st.ok = sel(act, nok, st.ok);
   st.cnt = sel(act, (cnt + 1) & (0u - cont), cnt);
+  if (RSA_TPL_PREFETCH) {
+    st.d0 = sel(adv, st.d1, st.d0);
+    const uint32_t n1 = st.seg + 1;
+    st.d1 = prog[n1 < kProgLen ? n1 : kProgLen - 1];   // used a byte from now
+  }
 }
 
 // The scan of a whole line.  True: the line has the template form.  All
@@ -741,7 +760,7 @@ RSA_HD void step(State& st, uint32_t i, uint32_t c, uint32_t act, P prog, C cls,
 template <class S, class P, class C, class Q>
 RSA_HD bool scan(const S& s, P prog, C cls, Q slot) {
   if (s.n > 0xFFFFu) return false;
-  State st;
+  State st = start(prog);
   for (uint32_t i = 0; i < s.n; ++i) step(st, i, s[i], 1u, prog, cls, slot);
   return st.ok && prog[st.seg] == kEndSeg;
 }
