@@ -126,6 +126,8 @@ struct Agg {
   uint32_t* occ;                     // occupancy bitmap of the slots (one bit per slot)
   uint32_t rs_bits;                  // region = 2^rs_bits slots (linear probing wraps inside a region)
   uint32_t np_bits;                  // 2^np_bits regions; a key's region = top np_bits of its slot hash
+  uint32_t tent2;                    // pass 1's last slice: records of rules under a filter bound also go
+                                     // into the pass-2 fields (exact when the final threshold equals the bound)
 };
 
 __device__ __forceinline__ unsigned long long mix64(unsigned long long x) {
@@ -1957,6 +1959,11 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
             *reinterpret_cast<v4u*>(&sl->min_order) = nm;
             if (nmo < mo) A.ukey[sl->pad[0]] = nmo;   // the cap resolution's copy of the key
             c.x += e_cnt[e];
+            if (A.tent2 && A.filter[gid] != RSA_NO_THRESHOLD) {
+              c.y += e_cnt[e];
+              c.z = min(c.z, e_first[e]);
+              c.w = max(c.w, e_last[e]);
+            }
           } else {
             c.y += e_cnt[e];
             c.z = min(c.z, e_first[e]);
@@ -1985,6 +1992,11 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
                 *reinterpret_cast<v4u*>(&sl->min_order) = nm;
                 if (nmo < mo) A.ukey[sl->pad[0]] = nmo;
                 sl->count += e_cnt[e];
+                if (A.tent2 && A.filter[gid] != RSA_NO_THRESHOLD) {
+                  sl->count2 += e_cnt[e];
+                  sl->first2 = min(sl->first2, e_first[e]);
+                  sl->last2 = max(sl->last2, e_last[e]);
+                }
               } else {
                 sl->count2 += e_cnt[e];
                 sl->first2 = min(sl->first2, e_first[e]);
@@ -2030,9 +2042,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
           ns.first = e_first[e];
           ns.last = e_last[e];
           ns.count = e_cnt[e];
-          ns.count2 = 0;
-          ns.first2 = 0xFFFFFFFFu;
-          ns.last2 = 0;
+          const bool t2 = A.tent2 && A.filter[(uint32_t)(ns.kB >> 32)] != RSA_NO_THRESHOLD;
+          ns.count2 = t2 ? e_cnt[e] : 0u;
+          ns.first2 = t2 ? e_first[e] : 0xFFFFFFFFu;
+          ns.last2 = t2 ? e_last[e] : 0u;
           ns.pad[0] = (uint32_t)ui;
           ns.pad[1] = ns.pad[2] = ns.pad[3] = 0;
           A.slots[(uint32_t)new_slot[q]] = ns;
@@ -2246,6 +2259,32 @@ __global__ void k_table_init(Slot* S, unsigned long long cap) {
   const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
   for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += stride)
     slot_clear(S, i);
+}
+
+// [0]: some rule under a filter bound got a threshold other than the bound;
+// [1]: some rule without a bound is capped now.
+__global__ void k_tent_check(const unsigned long long* filter, const unsigned long long* thresh, uint32_t n_rules,
+                             uint32_t* out) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_rules) return;
+  const unsigned long long f = filter[g], t = thresh[g];
+  if (f != RSA_NO_THRESHOLD && t != f) atomicOr(&out[0], 1u);
+  if (f == RSA_NO_THRESHOLD && t != RSA_NO_THRESHOLD) atomicOr(&out[1], 1u);
+}
+
+// The pass-2 fields of every used slot back to empty (the last slice's
+// tentative counts are replayed by a full recount).
+__global__ void k_pass2_clear(Slot* S, const unsigned long long* used, const unsigned long long* n_p,
+                              unsigned long long cap) {
+  unsigned long long n = *n_p;
+  if (n > cap) n = cap;
+  const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+  for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    Slot* s = &S[(uint32_t)used[i]];
+    s->count2 = 0;
+    s->first2 = 0xFFFFFFFFu;
+    s->last2 = 0;
+  }
 }
 
 // Reset only the slots the last job used.
@@ -2850,6 +2889,9 @@ struct rsa_ctx {
   unsigned long long* d_packed = nullptr;   // k_count / k_aggregate packed counters (rules > kCnt)
   // hot-region split (k_hot_plan / k_hot_combine)
   uint32_t min_regions_log2 = 10;           // RSA_OPT_MIN_REGIONS_LOG2: >= 1024 k_reduce workgroups (4 per CU)
+  bool tent2_on = false;                    // the current pass-1 launch is the last slice after the filter steps
+  uint32_t late_seg = 0xFFFFFFFFu;          // its record segment (pass-2 fields of filtered rules hold its records)
+  uint32_t* d_chk = nullptr;                // [0] a filtered rule's threshold moved, [1] a rule capped only now
   int parse_mode = 2;                       // RSA_OPT_PARSE_MODE (textparse.hip): register-window reads
   bool region_import = true;                // RSA_OPT_REGION_IMPORT: rsa_import by region sort + k_reduce
   bool slots_clean = true;                  // no slot holds a key of an earlier job (k_import's CAS claims need it)
@@ -2992,6 +3034,7 @@ Agg agg_of(const rsa_ctx* c) {
   a.occ = c->d_occ;
   a.rs_bits = c->rs_bits;
   a.np_bits = c->np_bits;
+  a.tent2 = c->tent2_on ? 1u : 0u;
   return a;
 }
 
@@ -3492,7 +3535,18 @@ int run_pass1(rsa_ctx* c, int classify, const rsa_tuple* T, const uint32_t* TS, 
       next = next * 4;
     }
     c->tightened = true;
-    return launch(done, n - done);
+    // the last slice runs under the final filter bounds: its records of
+    // bounded rules also go into the pass-2 fields, so the recount only has
+    // to replay the earlier slices when the thresholds equal the bounds
+    const bool tent = c->rec_cache && c->n_segs + 1 < (uint32_t)kMaxSegs && n - done + done <= c->recs2_alloc;
+    if (tent) {
+      c->late_seg = c->n_segs;
+      c->tent2_on = true;
+    }
+    rc = launch(done, n - done);
+    c->tent2_on = false;
+    if (tent && (rc || !c->rec_cache || c->n_segs != c->late_seg + 1)) c->late_seg = 0xFFFFFFFFu - 1;   // (a reset is due)
+    return rc;
   }
   return launch(0, n);
 }
@@ -3559,7 +3613,7 @@ int rsa_ctx_destroy(rsa_ctx* c) {
                   c->d_slots, c->d_used, c->d_ukey, c->d_used_n, c->d_filter, c->d_packed, c->d_hot, c->d_hot_tasks, c->d_hot_base,
                   c->d_hot_fill, c->d_hot_ctl, c->d_hot_total, c->d_cnt_words, c->d_cnt_starts,
                   c->d_cnt_tasks, c->d_cnt_ctl, c->d_flags, c->d_cursor, c->d_cidx,
-                  c->d_capped_gid, c->d_capped_cnt, c->d_capped_start, c->d_capped_prev, c->d_keys};
+                  c->d_capped_gid, c->d_capped_cnt, c->d_capped_start, c->d_capped_prev, c->d_keys, c->d_chk};
   for (void* b : bufs) (void)hipFree(b);
   for (int k = 0; k < kMaxEvents; ++k)
     if (c->ev[k]) (void)hipEventDestroy(c->ev[k]);
@@ -3963,6 +4017,8 @@ int rsa_reset(rsa_ctx* c, uint64_t capacity, uint32_t cap) {
   HIPCHK(c, hipMemsetAsync(c->d_filter, 0xFF, (nr ? nr : 1) * sizeof(unsigned long long), c->stream));
   HIPCHK(c, hipMemsetAsync(c->d_packed, 0, (nr ? nr : 1) * sizeof(unsigned long long), c->stream));
   c->tightened = false;
+  c->late_seg = 0xFFFFFFFFu;
+  c->tent2_on = false;
   HIPCHK(c, hipMemsetAsync(c->d_flags, 0, 4 * sizeof(unsigned int), c->stream));
   c->table_ready = true;
   return RSA_OK;
@@ -4043,16 +4099,44 @@ int rsa_recount(rsa_ctx* c, const rsa_tuple* T, const uint32_t* TS, const uint64
   if (rc) return rc;
   if (n == 0) return RSA_OK;
   if (!T || !TS || !ORD) return fail(c, RSA_ERR_ARG, "null tuple/ts/order pointer");
-  if (c->rec_cache && c->cache_T == (const void*)T && c->cache_n == n && c->n_segs > 0) {
+  // pass 1's last slice put its records of bounded rules into the pass-2
+  // fields (Agg::tent2): exact when every bounded rule's threshold equals its
+  // bound and no rule was capped only at the end; then the recount replays the
+  // earlier slices only.  Otherwise those fields are cleared and everything
+  // is replayed.
+  uint32_t n_segs = c->n_segs;
+  const bool tent = c->late_seg != 0xFFFFFFFFu;
+  bool clear = tent;
+  const bool cached = c->rec_cache && c->cache_T == (const void*)T && c->cache_n == n && c->n_segs > 0;
+  if (tent && cached && c->late_seg + 1 == c->n_segs && c->n_rules) {
+    if (!c->d_chk) HIPCHK(c, hipMalloc(&c->d_chk, 2 * sizeof(uint32_t)));
+    HIPCHK(c, hipMemsetAsync(c->d_chk, 0, 2 * sizeof(uint32_t), c->stream));
+    k_tent_check<<<(c->n_rules + kBlock - 1) / kBlock, kBlock, 0, c->stream>>>(c->d_filter, c->d_thresh, c->n_rules,
+                                                                                 c->d_chk);
+    uint32_t h[2] = {1u, 1u};
+    HIPCHK(c, hipMemcpyAsync(h, c->d_chk, sizeof h, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (!h[0] && !h[1]) {
+      clear = false;
+      n_segs = c->late_seg;   // the last slice is already counted
+    }
+  }
+  if (clear) {
+    k_pass2_clear<<<c->cu_count * 8, kBlock, 0, c->stream>>>(c->d_slots, c->d_used, c->d_used_n, c->slot_alloc);
+    HIPCHK(c, hipGetLastError());
+  }
+  c->late_seg = 0xFFFFFFFFu;   // (a second recount replays everything)
+  if (cached) {
     // every occurrence with order <= P of a capped rule produced a pass-1
     // record (P <= the filter bound in force when its line was aggregated)
+    if (n_segs == 0) return RSA_OK;
     const unsigned long long* hb = nullptr;
     const uint32_t* hf = nullptr;
     const HRec* hr = nullptr;
-    int rc2 = hot_split<2>(c, 0, c->n_segs, n, &hb, &hf, &hr);
+    int rc2 = hot_split<2>(c, 0, n_segs, n, &hb, &hf, &hr);
     if (rc2) return rc2;
     k_reduce<2><<<1u << c->np_bits, 1024, 0, c->stream>>>(reinterpret_cast<const Rec*>(c->d_recs2), c->d_starts,
-                                                         c->n_segs, agg_of(c), hb, hf, hr);
+                                                         n_segs, agg_of(c), hb, hf, hr);
     HIPCHK(c, hipGetLastError());
     return RSA_OK;
   }
