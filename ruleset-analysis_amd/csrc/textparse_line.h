@@ -59,35 +59,6 @@ struct GWordLn {             // global 4-byte loads with a one-word cache (no st
   }
 };
 
-struct GChunkLn {            // global 16-byte loads with a one-chunk cache (the slow parse: one load per
-  const uint32_t* w32;       // 16 bytes scanned instead of one per 4); the buffer 16-B aligned; bytes of its
-  const uint8_t* b8;         // last, partial chunk are read one by one
-  uint64_t o;                // byte offset of the line
-  uint64_t nb;               // bytes in the buffer
-  uint32_t n;
-  mutable uint64_t ci;
-  mutable uint32_t cw[4];
-  RSA_HD uint32_t operator[](uint32_t i) const {
-    const uint64_t pos = o + i, q = pos >> 4;
-    if (q != ci) {
-      ci = q;
-      if (16 * q + 16 <= nb) {
-        for (uint32_t k = 0; k < 4; ++k) cw[k] = w32[4 * q + k];
-      } else {
-        for (uint32_t k = 0; k < 4; ++k) {
-          uint32_t x = 0;
-          for (uint32_t t = 0; t < 4; ++t)
-            if (16 * q + 4 * k + t < nb) x |= (uint32_t)b8[16 * q + 4 * k + t] << (8 * t);
-          cw[k] = x;
-        }
-      }
-    }
-    const uint32_t r = (uint32_t)(pos & 15u);
-    const uint32_t w = (r >> 2) == 0 ? cw[0] : (r >> 2) == 1 ? cw[1] : (r >> 2) == 2 ? cw[2] : cw[3];
-    return (w >> ((r & 3u) * 8u)) & 0xFFu;
-  }
-};
-
 struct GWordU {              // global 4-byte loads, one per byte read, no per-lane branch: the word of
   const uint32_t* w32;       // the buffer's last, partial bytes comes from `tail`
   uint64_t o;                // byte offset of the line

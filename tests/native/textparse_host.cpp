@@ -14,11 +14,7 @@ extern "C" void parse_lines_host(const uint8_t* text, const uint64_t* off, uint6
     const uint64_t a = off[i], b = off[i + 1];
     uint64_t len = b - a;
     if (len && text[b - 1] == '\n') --len;
-    if (word == 3) {   // the slow pass's 16-byte chunk accessor (text 16-B aligned)
-      const rsa_text::GChunkLn s{reinterpret_cast<const uint32_t*>(text), text, a, off[n], (uint32_t)len, ~0ull,
-                                 {0u, 0u, 0u, 0u}};
-      rsa_text::parse_line(s, ifcs, n_ifcs, spells, n_spells, tuples[i], ts[i], disp[i]);
-    } else if (word == 2) {   // the direct-HBM accessor (k_parse<..., true>)
+    if (word == 2) {   // the direct-HBM accessor (k_parse<..., true>)
       const rsa_text::GWordLn s{reinterpret_cast<const uint32_t*>(text), text, a, off[n], (uint32_t)len, ~0ull, 0u};
       rsa_text::parse_line(s, ifcs, n_ifcs, spells, n_spells, tuples[i], ts[i], disp[i]);
     } else if (word) {

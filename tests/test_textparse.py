@@ -202,7 +202,7 @@ def _device_stage_on_cpu(lib, host, lines, db, compiled, spells, word=1):
     return tup, ts, disp, names
 
 
-@pytest.mark.parametrize('seed,word', [(1, 1), (2, 1), (3, 0), (4, 2), (5, 3)])
+@pytest.mark.parametrize('seed,word', [(1, 1), (2, 1), (3, 0), (4, 2)])
 def test_device_line_parser_on_cpu_equals_host_parser(seed, word):
     """Every line the device parser decides itself (not RSA_LINE_HOST) gets
     exactly the host parser's disposition, tuple, list, spelling and
