@@ -1645,14 +1645,32 @@ __global__ __launch_bounds__(1024) void k_part_scatter(const Rec* __restrict__ r
   const unsigned long long end = beg + tile_len < n ? beg + tile_len : n;
   const unsigned long long wend = (end + kWin - 1) / kWin;
   const uint32_t lane = __lane_id(), nwv = blockDim.x >> 6;
-  for (unsigned long long w0 = beg / kWin + (threadIdx.x >> 6) * kPartW; w0 < wend; w0 += (unsigned long long)nwv * kPartW) {
-    const WinGroup g = win_group(wcnt, w0, wend);
-    for (uint32_t q = lane; q < g.tot; q += kWin) {
-      const unsigned long long j = win_slot(g, w0, q);
-      const uint32_t rg = regs[j];
-      const Rec r = recs[j];
-      out[atomicAdd(&cur[rg], 1u)] = r;
+  const unsigned long long wstep = (unsigned long long)nwv * kPartW;
+  unsigned long long w0 = beg / kWin + (threadIdx.x >> 6) * kPartW;
+  WinGroup g = w0 < wend ? win_group(wcnt, w0, wend) : WinGroup{0, 0, 0, 0};
+  for (; w0 < wend; w0 += wstep) {
+    // the next group's window counts are read before this group's records
+    // are moved (their latency hides behind the moves), and every lane moves
+    // two records per trip, both loads in flight together
+    const WinGroup gn = w0 + wstep < wend ? win_group(wcnt, w0 + wstep, wend) : WinGroup{0, 0, 0, 0};
+    for (uint32_t q = lane; q < g.tot; q += 2 * kWin) {
+      const bool two = q + kWin < g.tot;
+      const unsigned long long j0 = win_slot(g, w0, q);
+      const unsigned long long j1 = two ? win_slot(g, w0, q + kWin) : j0;
+      const uint32_t rg0 = regs[j0];
+      const Rec r0 = recs[j0];
+      uint32_t rg1 = 0;
+      Rec r1;
+      if (two) {
+        rg1 = regs[j1];
+        r1 = recs[j1];
+      }
+      const uint32_t p0 = atomicAdd(&cur[rg0], 1u);
+      const uint32_t p1 = two ? atomicAdd(&cur[rg1], 1u) : 0u;
+      out[p0] = r0;
+      if (two) out[p1] = r1;
     }
+    g = gn;
   }
 }
 
@@ -2328,21 +2346,18 @@ __global__ void k_cap_mark(const unsigned int* distinct, uint32_t n_rules, uint3
   }
 }
 
-// Scatter the capped rules' min_order keys into their segments.  Lanes of one
-// wave that share a rule take their positions from one atomic (hot rules would
-// otherwise serialise thousands of atomics on one counter).
-__global__ __launch_bounds__(kBlock) void k_cap_scatter(const Slot* S, const unsigned long long* used,
-                                                        const unsigned long long* n_used_p, const unsigned int* n_capped_p,
-                                                        uint32_t lds_max,
-                                                        const uint32_t* cidx, const uint32_t* capped_start,
-                                                        uint32_t* capped_fill, const unsigned long long* ukey,
-                                                        const unsigned long long* cprev, unsigned long long* keys,
-                                                        unsigned long long max_keys, unsigned int* flags) {
-  const unsigned int n_capped = *n_capped_p;
-  if (n_capped == 0 || n_capped <= lds_max) return;   // the LDS variant's case (workgroup-uniform)
-  const unsigned long long n_used = *n_used_p < max_keys ? *n_used_p : max_keys;   // (overflow: flagged elsewhere)
-  const unsigned long long stride = (unsigned long long)gridDim.x * kBlock;
-  for (unsigned long long base = (unsigned long long)blockIdx.x * kBlock; base < n_used; base += stride) {
+// Scatter the capped rules' min_order keys into their segments when the
+// capped rules do not fit the LDS counters below.  Lanes of one wave that share
+// a rule take their positions from one atomic (hot rules would otherwise
+// serialise thousands of atomics on one counter).
+__device__ __forceinline__ void cap_scatter_waves(const Slot* S, const unsigned long long* used,
+                                                  unsigned long long n_used, const uint32_t* cidx,
+                                                  const uint32_t* capped_start, uint32_t* capped_fill,
+                                                  const unsigned long long* ukey, const unsigned long long* cprev,
+                                                  unsigned long long* keys, unsigned long long max_keys,
+                                                  unsigned int* flags) {
+  const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+  for (unsigned long long base = (unsigned long long)blockIdx.x * blockDim.x; base < n_used; base += stride) {
     const unsigned long long i = base + threadIdx.x;
     uint32_t c = 0xFFFFFFFFu;
     unsigned long long key = 0;
@@ -2383,11 +2398,12 @@ __global__ __launch_bounds__(kBlock) void k_cap_scatter(const Slot* S, const uns
   }
 }
 
-// The same scatter when the capped rules fit an LDS counter array (n_capped <=
-// kCapLds): each workgroup takes a contiguous chunk of the used list, ranks its
-// entries per rule with LDS atomics, reserves every rule's run with one global
-// atomic per (workgroup, rule), then writes the keys.  Constant work per entry,
-// where the wave grouping above loops once per distinct rule in the wave.
+// The scatter when the capped rules fit an LDS counter array (n_capped <=
+// kCapLds; else the wave grouping above): each workgroup takes a contiguous
+// chunk of the used list, ranks its entries per rule with LDS atomics, reserves
+// every rule's run with one global atomic per (workgroup, rule), then writes the
+// keys.  Constant work per entry, where the wave grouping loops once per
+// distinct rule in the wave.
 constexpr int kCapLds = 16384;
 constexpr int kCapPer = 16;                 // entries per thread (1024 threads: a chunk of 16384)
 __global__ __launch_bounds__(1024) void k_cap_scatter_lds(const Slot* S, const unsigned long long* used,
@@ -2401,8 +2417,12 @@ __global__ __launch_bounds__(1024) void k_cap_scatter_lds(const Slot* S, const u
   // counts are read on the device (no host round trip): a persistent grid
   // walks the chunks of the used list
   const uint32_t n_capped = *n_capped_p;
-  if (n_capped == 0 || n_capped > lds_max) return;   // workgroup-uniform
+  if (n_capped == 0) return;   // workgroup-uniform
   const unsigned long long n_used = *n_used_p < max_keys ? *n_used_p : max_keys;   // (overflow: flagged elsewhere)
+  if (n_capped > lds_max) {
+    cap_scatter_waves(S, used, n_used, cidx, capped_start, capped_fill, ukey, cprev, keys, max_keys, flags);
+    return;
+  }
   const unsigned long long chunk = 1024ull * kCapPer;
   for (unsigned long long base = (unsigned long long)blockIdx.x * chunk; base < n_used; base += gridDim.x * chunk) {
   for (uint32_t r = threadIdx.x; r < n_capped; r += blockDim.x) cnt[r] = 0;
@@ -2465,6 +2485,7 @@ __global__ __launch_bounds__(1024) void k_cap_scatter_lds(const Slot* S, const u
 // keys per thread and the passes are barrier-bound; four times the rules in
 // flight at once (eight workgroups per CU) instead of wider workgroups
 constexpr int kSelThreads = 256;
+constexpr int kSelR = 16;   // register-resident keys per thread
 __global__ __launch_bounds__(kSelThreads) void k_cap_select(const unsigned long long* keys,
                                                             const uint32_t* capped_start, const uint32_t* capped_fill,
                                                             const uint32_t* capped_gid, uint32_t cap,
@@ -2480,9 +2501,24 @@ __global__ __launch_bounds__(kSelThreads) void k_cap_select(const unsigned long 
   const unsigned long long* seg = keys + capped_start[c];
   const uint32_t n = capped_fill[c];
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  // min / max
+  // min / max; the segment's first kSelR x kSelThreads keys stay in
+  // registers for the digit passes (segments are ~cap..a few x cap keys), the
+  // rest is read again per pass
   unsigned long long mn = ~0ull, mx = 0;
-  for (uint32_t j = threadIdx.x; j < n; j += kSelThreads) {
+  unsigned long long kv[kSelR];
+#pragma unroll
+  for (int r = 0; r < kSelR; ++r) {
+    const uint32_t j = threadIdx.x + (uint32_t)r * kSelThreads;
+    kv[r] = j < n ? seg[j] : 0ull;
+  }
+#pragma unroll
+  for (int r = 0; r < kSelR; ++r) {
+    if (threadIdx.x + (uint32_t)r * kSelThreads < n) {
+      mn = kv[r] < mn ? kv[r] : mn;
+      mx = kv[r] > mx ? kv[r] : mx;
+    }
+  }
+  for (uint32_t j = threadIdx.x + kSelR * kSelThreads; j < n; j += kSelThreads) {
     const unsigned long long k = seg[j];
     mn = k < mn ? k : mn;
     mx = k > mx ? k : mx;
@@ -2523,7 +2559,13 @@ __global__ __launch_bounds__(kSelThreads) void k_cap_select(const unsigned long 
     for (int q = threadIdx.x; q < kWaves * 256; q += kSelThreads) (&hist[0][0])[q] = 0;
     __syncthreads();
     const unsigned long long prefix = sh_prefix;
-    for (uint32_t j = threadIdx.x; j < n; j += kSelThreads) {
+#pragma unroll
+    for (int r = 0; r < kSelR; ++r) {
+      const unsigned long long v = kv[r] - mn;
+      if (threadIdx.x + (uint32_t)r * kSelThreads < n && (v & hi_mask) == prefix)
+        atomicAdd(&hist[w][(v >> shift) & 255u], 1u);
+    }
+    for (uint32_t j = threadIdx.x + kSelR * kSelThreads; j < n; j += kSelThreads) {
       const unsigned long long v = seg[j] - mn;
       if ((v & hi_mask) == prefix) atomicAdd(&hist[w][(v >> shift) & 255u], 1u);
     }
@@ -2600,7 +2642,8 @@ __global__ __launch_bounds__(1024) void k_emit(const Slot* S, const unsigned lon
                                                const unsigned long long* n_used_p, unsigned long long slot_cap,
                                                const unsigned long long* thresh, int mode, rsa_conn_record* out,
                                                unsigned long long max_out, unsigned long long* cursor,
-                                               uint32_t owner_world, uint32_t owner_rank) {
+                                               uint32_t owner_world, uint32_t owner_rank,
+                                               const unsigned long long* ukey) {
   __shared__ uint32_t sh[18];
   __shared__ unsigned long long sh_base;
   // the used-slot count is read on the device (persistent grid): no host
@@ -2617,7 +2660,19 @@ __global__ __launch_bounds__(1024) void k_emit(const Slot* S, const unsigned lon
       const unsigned long long i = base + (unsigned long long)k * blockDim.x + threadIdx.x;
       which[k] = -1;
       if (i < n_used) {
-        sl[k] = S[(uint32_t)used[i]];
+        const unsigned long long u = used[i];
+        const uint32_t gid = (uint32_t)(u >> 32);
+        // decided from the used list (rule id) and the key copy before the
+        // 64 B slot is gathered: entries of capped rules past the threshold
+        // and entries of other owners are never read
+        if (owner_world && (gid % owner_world == owner_rank) != (mode == 0)) {
+          continue;
+        }
+        if (ukey && (mode == 0 || mode == 3)) {
+          const unsigned long long P = thresh[gid];
+          if (P != RSA_NO_THRESHOLD && ukey[i] > P) continue;
+        }
+        sl[k] = S[(uint32_t)u];
         if (mode == 0) {
           const unsigned long long P = thresh[sl[k].kB >> 32];
           if (P == RSA_NO_THRESHOLD) which[k] = 0;
@@ -2630,7 +2685,6 @@ __global__ __launch_bounds__(1024) void k_emit(const Slot* S, const unsigned lon
         } else if (sl[k].count2 != 0) {
           which[k] = 1;
         }
-        if (owner_world && ((uint32_t)(sl[k].kB >> 32) % owner_world == owner_rank) != (mode == 0)) which[k] = -1;
       }
       c += which[k] >= 0 ? 1u : 0u;
     }
@@ -2891,6 +2945,7 @@ struct rsa_ctx {
   uint32_t min_regions_log2 = 10;           // RSA_OPT_MIN_REGIONS_LOG2: >= 1024 k_reduce workgroups (4 per CU)
   bool tent2_on = false;                    // the current pass-1 launch is the last slice after the filter steps
   uint32_t late_seg = 0xFFFFFFFFu;          // its record segment (pass-2 fields of filtered rules hold its records)
+  uint32_t tent_skip = 0;                   // jobs left without the tentative pass-2 fields (set when they missed)
   uint32_t* d_chk = nullptr;                // [0] a filtered rule's threshold moved, [1] a rule capped only now
   int parse_mode = 2;                       // RSA_OPT_PARSE_MODE (textparse.hip): register-window reads
   bool region_import = true;                // RSA_OPT_REGION_IMPORT: rsa_import by region sort + k_reduce
@@ -3147,20 +3202,34 @@ int cap_select(rsa_ctx* c, unsigned long long* out, uint32_t* h_n_capped) {
                                                                    c->d_capped_cnt, c->d_capped_prev, d_ncap,
                                                                    c->d_cursor, out);
   HIPCHK(c, hipGetLastError());
-  // both scatter variants are launched; each exits unless the device-side
-  // count of capped rules is its case (LDS counters for <= kCapLds rules)
+  // the scatter picks its variant from the device-side count of capped rules
+  // (LDS counters for <= kCapLds rules)
   const uint32_t lds_max = c->wave_cap_scatter ? 0u : (uint32_t)kCapLds;
   k_cap_scatter_lds<<<c->cu_count * 2, 1024, 0, c->stream>>>(c->d_slots, c->d_used, c->d_used_n, d_ncap, lds_max,
                                                              c->d_cidx, c->d_capped_start, c->d_capped_cnt, ukey,
                                                              c->d_capped_prev, c->d_keys, c->sort_alloc, c->d_flags);
-  k_cap_scatter<<<c->cu_count * 8, kBlock, 0, c->stream>>>(c->d_slots, c->d_used, c->d_used_n, d_ncap, lds_max,
-                                                          c->d_cidx, c->d_capped_start, c->d_capped_cnt, ukey,
-                                                          c->d_capped_prev, c->d_keys, c->sort_alloc, c->d_flags);
   HIPCHK(c, hipGetLastError());
   const unsigned sel_grid = nr < (uint32_t)c->cu_count * 8 ? nr : (unsigned)c->cu_count * 8;
   k_cap_select<<<sel_grid, kSelThreads, 0, c->stream>>>(c->d_keys, c->d_capped_start, c->d_capped_cnt, c->d_capped_gid,
                                                         c->cap, d_ncap, out);
   HIPCHK(c, hipGetLastError());
+  if (c->debug) {
+    // the selection's volume: capped rules, their entries, the keys scattered
+    unsigned int f[4];
+    unsigned long long tot = 0, used_n = 0;
+    HIPCHK(c, hipMemcpyAsync(f, c->d_flags, sizeof f, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&tot, c->d_cursor, sizeof tot, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&used_n, c->d_used_n, sizeof used_n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::vector<uint32_t> fill(f[2]);
+    if (f[2]) {
+      HIPCHK(c, hipMemcpy(fill.data(), c->d_capped_cnt, f[2] * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    }
+    unsigned long long sc = 0;
+    for (uint32_t v : fill) sc += v;
+    fprintf(stderr, "[rsa] cap select: %u capped rules, %llu of %llu used entries theirs, %llu keys scattered\n", f[2],
+            tot, used_n, sc);
+  }
   if (h_n_capped) {
     // one round trip: the capped-rule count (d_flags[2]) with the sticky
     // error flags, which also cover every launch before this selection
@@ -3383,20 +3452,23 @@ int count_by_block(rsa_ctx* c, const uint32_t* gh, uint64_t m) {
 // sort of the records by table region into d_recs2[a ..] (records <= lines,
 // so no record count is needed on the host) and the per-region LDS reduction
 // and merge (k_reduce).
+// With gh, the counters cover the words [gh_count, gh_count + m_count) (the
+// auto-tightening slices count once, all of the batch's lines with the last).
 int launch_aggregate(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsigned long long* o, const int32_t* g,
-                     const uint32_t* gh, uint64_t a, uint64_t m) {
+                     const uint32_t* gh, uint64_t a, uint64_t m, const uint32_t* gh_count, uint64_t m_count) {
   const Agg ag = agg_of(c);
   int rc = RSA_OK;
   if (gh) {
-    if (!(ag.skip & 1u)) {
-      const uint64_t units = (m + 3) / 4;
+    if (!(ag.skip & 1u) && m_count) {
+      const uint64_t units = (m_count + 3) / 4;
       if (c->n_rules <= (uint32_t)kCnt) {
-        k_count<kCnt><<<grid_for_threads(c, units, 1024, RSA_COUNT_PER_CU), 1024, 0, c->stream>>>(gh, m, c->n_rules, ag);
+        k_count<kCnt><<<grid_for_threads(c, units, 1024, RSA_COUNT_PER_CU), 1024, 0, c->stream>>>(gh_count, m_count,
+                                                                                                  c->n_rules, ag);
       } else if (c->count_sort && ((c->n_rules + kCntBlock - 1) >> kCntBits) <= (uint32_t)kMaxRegions) {
-        const int rc2 = count_by_block(c, gh, m);
+        const int rc2 = count_by_block(c, gh_count, m_count);
         if (rc2) return rc2;
       } else {
-        k_count<0><<<grid_for_threads(c, units, 1024, 8), 1024, 0, c->stream>>>(gh, m, c->n_rules, ag);
+        k_count<0><<<grid_for_threads(c, units, 1024, 8), 1024, 0, c->stream>>>(gh_count, m_count, c->n_rules, ag);
         k_count_flush<<<grid_for(c, c->n_rules, 8), kBlock, 0, c->stream>>>(c->d_packed, c->n_rules, c->d_matches,
                                                                             c->d_hits);
       }
@@ -3494,7 +3566,11 @@ int run_pass1(rsa_ctx* c, int classify, const rsa_tuple* T, const uint32_t* TS, 
     if (rc) return rc;
     gh = c->d_gh;
   }
-  auto launch = [&](uint64_t a, uint64_t m) -> int {
+  // count_from: the first line whose gid|hit word the launch counts (the
+  // tightening slices leave theirs to the last one: the per-rule counters do
+  // not feed the filter bounds, and each counting launch ends in a flush of
+  // every rule's counter from every workgroup)
+  auto launch = [&](uint64_t a, uint64_t m, uint64_t count_from) -> int {
     if (m == 0) return RSA_OK;
     if (c->ev_used + 3 > kMaxEvents) return fail(c, RSA_ERR_STATE, "too many pass-1 launches in one call");
     const uint4* t = reinterpret_cast<const uint4*>(T) + a;
@@ -3514,7 +3590,8 @@ int run_pass1(rsa_ctx* c, int classify, const rsa_tuple* T, const uint32_t* TS, 
       if (rc2) return rc2;
     }
     HIPCHK(c, hipEventRecord(c->ev[c->ev_used + 1], c->stream));
-    const int rc2 = launch_aggregate(c, t, TS + a, o, G ? G + a : nullptr, classify ? gh + a : nullptr, a, m);
+    const int rc2 = launch_aggregate(c, t, TS + a, o, G ? G + a : nullptr, classify ? gh + a : nullptr, a, m,
+                                     classify ? gh + count_from : nullptr, a + m - count_from);
     if (rc2) return rc2;
     HIPCHK(c, hipEventRecord(c->ev[c->ev_used + 2], c->stream));
     c->ev_used += 3;
@@ -3527,7 +3604,7 @@ int run_pass1(rsa_ctx* c, int classify, const rsa_tuple* T, const uint32_t* TS, 
     uint64_t next = n / c->filter_slice;
     if (next < (1ull << 20)) next = n < (1ull << 21) ? n / 2 : (1ull << 20);
     for (uint32_t step = 0; step < c->filter_steps && next < n; ++step) {
-      rc = launch(done, next - done);
+      rc = launch(done, next - done, next);
       if (rc) return rc;
       rc = cap_select(c, c->d_filter, nullptr);   // on the device: no host round trip
       if (rc) return rc;
@@ -3538,17 +3615,24 @@ int run_pass1(rsa_ctx* c, int classify, const rsa_tuple* T, const uint32_t* TS, 
     // the last slice runs under the final filter bounds: its records of
     // bounded rules also go into the pass-2 fields, so the recount only has
     // to replay the earlier slices when the thresholds equal the bounds
-    const bool tent = c->rec_cache && c->n_segs + 1 < (uint32_t)kMaxSegs && n - done + done <= c->recs2_alloc;
+    // (learned per context: after a job whose thresholds moved below the
+    // bounds, so that the tentative fields had to be cleared and replayed,
+    // the next kTentBackoff jobs do not fill them)
+    bool tent = c->rec_cache && c->n_segs + 1 < (uint32_t)kMaxSegs && n - done + done <= c->recs2_alloc;
+    if (tent && c->tent_skip) {
+      --c->tent_skip;
+      tent = false;
+    }
     if (tent) {
       c->late_seg = c->n_segs;
       c->tent2_on = true;
     }
-    rc = launch(done, n - done);
+    rc = launch(done, n - done, 0);
     c->tent2_on = false;
     if (tent && (rc || !c->rec_cache || c->n_segs != c->late_seg + 1)) c->late_seg = 0xFFFFFFFFu - 1;   // (a reset is due)
     return rc;
   }
-  return launch(0, n);
+  return launch(0, n, 0);
 }
 
 int emit_mode(rsa_ctx* c, int mode, rsa_conn_record* out, uint64_t max_out, uint64_t* h_n) {
@@ -3560,7 +3644,8 @@ int emit_mode(rsa_ctx* c, int mode, rsa_conn_record* out, uint64_t max_out, uint
   // persistent grid (two 1024-thread workgroups per CU) over the device-side
   // used count; one round trip for the emitted count and the error flags
   k_emit<<<c->cu_count * 2, 1024, 0, c->stream>>>(c->d_slots, c->d_used, c->d_used_n, c->slot_cap, c->d_thresh, mode,
-                                                  out, max_out, c->d_cursor, c->owner_world, c->owner_rank);
+                                                  out, max_out, c->d_cursor, c->owner_world, c->owner_rank,
+                                                  c->ukey_ok ? c->d_ukey : nullptr);
   HIPCHK(c, hipGetLastError());
   unsigned long long n = 0;
   unsigned int f[4];
@@ -4092,6 +4177,8 @@ int rsa_resolve_cap(rsa_ctx* c, uint32_t* h_n_capped) {
   return cap_select(c, c->d_thresh, h_n_capped);
 }
 
+constexpr uint32_t kTentBackoff = 8;
+
 int rsa_recount(rsa_ctx* c, const rsa_tuple* T, const uint32_t* TS, const uint64_t* ORD, const int32_t* G,
                 uint64_t n) {
   if (!c) return RSA_ERR_ARG;
@@ -4120,6 +4207,7 @@ int rsa_recount(rsa_ctx* c, const rsa_tuple* T, const uint32_t* TS, const uint64
       clear = false;
       n_segs = c->late_seg;   // the last slice is already counted
     }
+    c->tent_skip = clear ? kTentBackoff : 0u;
   }
   if (clear) {
     k_pass2_clear<<<c->cu_count * 8, kBlock, 0, c->stream>>>(c->d_slots, c->d_used, c->d_used_n, c->slot_alloc);

@@ -680,11 +680,15 @@ constexpr uint32_t pack3(char a, char b, char c) { return (uint32_t)(uint8_t)a <
 // scalar lane masks, and their and/or/select bookkeeping is scalar work that
 // the CU's one scalar unit serialises over its four SIMDs.
 #ifndef RSA_TPL_PREFETCH
-#define RSA_TPL_PREFETCH 1   // A/B builds: 0 reads prog[seg] on every byte
+#define RSA_TPL_PREFETCH 0   // A/B builds: 1 carries the next descriptors in registers
 #endif
-// d0 = prog[seg], d1 = prog[seg + 1]: the next descriptor is a select, and
-// the read of the one after it is issued a byte ahead of its use, so no LDS
-// read sits on the byte-to-byte dependence chain.
+// With RSA_TPL_PREFETCH, d0 = prog[seg], d1 = prog[seg + 1]: the next
+// descriptor is a select, and the read of the one after it is issued a byte
+// ahead of its use, so no LDS read sits on the byte-to-byte dependence chain.
+// Measured slower on gfx950 (16M-line text job: parse 6.41 vs 6.08 ms,
+// profiles/r04w_text16_*.json): the two extra live registers and the LDS read
+// per byte cost more than the latency they hide, so the default reads
+// prog[seg] on every byte.
 struct State {
   uint32_t seg = 0, cnt = 0, pos0 = 0, ok = 1, d0 = 0, d1 = 0;
 };
