@@ -486,12 +486,24 @@ def rank_main(args, rank, world, local):
     pass1_launch_ms = []
     pass1_launches = []
     last = {}
+    pending = {'pass1_times': False}
+
+    def read_pass1_times():
+        # a timed job's pass-1 event times, read at the start of the next step
+        # (or after the timed loop): that job ended in a host read, so its
+        # events are complete, and no extra host round trip sits in the step
+        if pending['pass1_times']:
+            pass1_launch_ms.append(eng.last_pass1_times())
+            pass1_launches.append(eng.last_pass1_launches())
+            pending['pass1_times'] = False
 
     def step(timed):
+        read_pass1_times()
         n_t, n_l = len(pass1_launch_ms), len(pass1_launches)
         try:
             r = job(timed)
         except (native.NativeError, ShardOverflow) as e:
+            pending['pass1_times'] = False
             # multi-GPU: the merge raises ShardOverflow on every rank together,
             # with the entries the fullest owner table needs (its shard's plus
             # the imported ones: the per-shard bound does not cover those)
@@ -514,12 +526,12 @@ def rank_main(args, rank, world, local):
     def job(timed):
         eng.reset(sizing['capacity'], cap)
         eng.pass1(batch, gbuf)
-        if timed:
-            pass1_launch_ms.append(eng.last_pass1_times())
-            pass1_launches.append(eng.last_pass1_launches())
+        pending['pass1_times'] = timed
         if dist is None:
-            if eng.resolve_cap():
-                eng.pass2(batch, gbuf)
+            # the capped-rule count stays on the device: the recount's kernels
+            # skip their work there when no rule is capped
+            eng.resolve_cap(sync=False)
+            eng.pass2(batch, gbuf)
             recs = eng.emit_device('final')
             last['recs'] = recs
             return recs.numel() // RECORD_DTYPE.itemsize
@@ -554,6 +566,7 @@ def rank_main(args, rank, world, local):
     for _ in range(args.steps):
         n_rec = step(True)
     torch.cuda.synchronize()
+    read_pass1_times()
     if phase_prof:
         eng.ctx.call('rsa_phase_prof', ph, ctypes.c_int(1))
         v = [int(x) for x in ph]

@@ -281,7 +281,9 @@ int rsa_last_pass1_launches(rsa_ctx *ctx, uint32_t *h_n);
 /* Resolve the cap (connlist-reducer.py:151): for every rule with
  * distinct >= cap, P = the order key of the line that inserted the cap-th
  * distinct connection, written to d_thresh.  *h_n_capped receives the number
- * of capped rules (0 means no recount pass is needed). */
+ * of capped rules (0 means no recount pass is needed).  h_n_capped may be
+ * NULL: no host round trip; the count stays on the device and a following
+ * rsa_recount of the cached batch skips its work there when it is 0. */
 int rsa_resolve_cap(rsa_ctx *ctx, uint32_t *h_n_capped);
 
 /* Pass 2 — recount occurrences with order <= P for capped rules, per batch.

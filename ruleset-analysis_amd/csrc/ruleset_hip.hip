@@ -1842,7 +1842,8 @@ template <int kPass>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2 ? RSA_RED2_WPE : 4, 8))) void k_reduce(const Rec* __restrict__ recs,
                                                  const unsigned long long* __restrict__ starts, uint32_t n_segs,
                                                  Agg A, const unsigned long long* __restrict__ hot_base,
-                                                 const uint32_t* __restrict__ hot_fill, const HRec* __restrict__ hot) {
+                                                 const uint32_t* __restrict__ hot_fill, const HRec* __restrict__ hot,
+                                                 const unsigned int* __restrict__ skip_zero) {
   __shared__ unsigned long long e_kA[kRedE<kPass>], e_kB[kRedE<kPass>], e_mo[kRedE<kPass>];
   __shared__ uint32_t e_first[kRedE<kPass>], e_last[kRedE<kPass>], e_cnt[kRedE<kPass>];
   __shared__ uint32_t occ[1u << (kRegionMaxBits - 5)];     // occupied before this flush
@@ -1850,6 +1851,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
   __shared__ uint32_t used;
   __shared__ uint32_t sh[18];
   __shared__ unsigned long long sh_base;
+  // skip_zero: the device-side count of capped rules (a recount after a cap
+  // resolution whose count the host did not read): none, nothing to recount
+  if (skip_zero && *skip_zero == 0) return;   // workgroup-uniform
   const uint32_t region = blockIdx.x;
   const uint32_t n_regions = 1u << A.np_bits;
   // a hot region's records were pre-combined by k_hot_combine: read those
@@ -2105,9 +2109,15 @@ struct HotTask {
 __global__ void k_hot_plan(const unsigned long long* __restrict__ starts, uint32_t n_segs, uint32_t n_regions,
                            HotTask* __restrict__ tasks, uint32_t max_tasks, uint32_t* __restrict__ ctl,
                            unsigned long long* __restrict__ hot_total, unsigned long long* __restrict__ hot_base,
-                           uint32_t* __restrict__ hot_fill, unsigned long long min_recs, uint32_t factor) {
+                           uint32_t* __restrict__ hot_fill, unsigned long long min_recs, uint32_t factor,
+                           const unsigned int* __restrict__ skip_zero) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n_regions) return;
+  if (skip_zero && *skip_zero == 0) {   // (see k_reduce)
+    hot_fill[r] = 0;
+    hot_base[r] = kEmpty;
+    return;
+  }
   unsigned long long all = 0, mine = 0;
   for (uint32_t sg = 0; sg < n_segs; ++sg) {
     const unsigned long long* st = starts + (size_t)sg * (n_regions + 1);
@@ -3395,7 +3405,7 @@ int hot_split(rsa_ctx* c, uint32_t seg0, uint32_t n_segs, unsigned long long rec
   k_hot_plan<<<(n_regions + 255) / 256, 256, 0, c->stream>>>(c->d_starts + (size_t)seg0 * (n_regions + 1), n_segs,
                                                              n_regions, tasks, (uint32_t)max_tasks, c->d_hot_ctl,
                                                              c->d_hot_total, c->d_hot_base, c->d_hot_fill, c->hot_min,
-                                                             c->hot_factor);
+                                                             c->hot_factor, kPass == 2 ? c->d_flags + 2 : nullptr);
   k_hot_combine<kPass><<<c->cu_count, 1024, 0, c->stream>>>(reinterpret_cast<const Rec*>(c->d_recs2), tasks,
                                                              c->d_hot_ctl, agg_of(c), c->d_hot_base, c->d_hot_fill,
                                                              static_cast<HRec*>(c->d_hot));
@@ -3524,7 +3534,8 @@ int launch_aggregate(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsig
   const HRec* hr = nullptr;
   rc = hot_split<1>(c, c->n_segs, 1, m, &hb, &hf, &hr);
   if (rc) return rc;
-  k_reduce<1><<<n_regions, 1024, 0, c->stream>>>(reinterpret_cast<const Rec*>(c->d_recs2), st, 1, ag, hb, hf, hr);
+  k_reduce<1><<<n_regions, 1024, 0, c->stream>>>(reinterpret_cast<const Rec*>(c->d_recs2), st, 1, ag, hb, hf, hr,
+                                                 nullptr);
   HIPCHK(c, hipGetLastError());
   if (c->rec_cache) ++c->n_segs;
   if (c->debug) {
@@ -4171,7 +4182,7 @@ int rsa_last_pass1_ms(rsa_ctx* c, float* h_ms) {
 }
 
 int rsa_resolve_cap(rsa_ctx* c, uint32_t* h_n_capped) {
-  if (!c || !h_n_capped) return RSA_ERR_ARG;
+  if (!c) return RSA_ERR_ARG;
   int rc = need_agg(c);
   if (rc) return rc;
   return cap_select(c, c->d_thresh, h_n_capped);
@@ -4223,8 +4234,10 @@ int rsa_recount(rsa_ctx* c, const rsa_tuple* T, const uint32_t* TS, const uint64
     const HRec* hr = nullptr;
     int rc2 = hot_split<2>(c, 0, n_segs, n, &hb, &hf, &hr);
     if (rc2) return rc2;
+    // (a resolution whose count the host did not read leaves it at d_flags[2]:
+    // the kernels skip their work on the device when no rule is capped)
     k_reduce<2><<<1u << c->np_bits, 1024, 0, c->stream>>>(reinterpret_cast<const Rec*>(c->d_recs2), c->d_starts,
-                                                         n_segs, agg_of(c), hb, hf, hr);
+                                                         n_segs, agg_of(c), hb, hf, hr, c->d_flags + 2);
     HIPCHK(c, hipGetLastError());
     return RSA_OK;
   }
@@ -4299,10 +4312,10 @@ int rsa_import(rsa_ctx* c, int which, const rsa_conn_record* in, uint64_t n) {
   k_imp_desc<<<(n_regions + 255) / 256, 256, 0, c->stream>>>(counts, cursor, n_regions, c->d_hot_base, c->d_hot_fill);
   if (which == 0)
     k_reduce<1><<<n_regions, 1024, 0, c->stream>>>(nullptr, c->d_starts, 0, ag, c->d_hot_base, c->d_hot_fill,
-                                                   static_cast<const HRec*>(c->d_hot));
+                                                   static_cast<const HRec*>(c->d_hot), nullptr);
   else
     k_reduce<2><<<n_regions, 1024, 0, c->stream>>>(nullptr, c->d_starts, 0, ag, c->d_hot_base, c->d_hot_fill,
-                                                   static_cast<const HRec*>(c->d_hot));
+                                                   static_cast<const HRec*>(c->d_hot), nullptr);
   HIPCHK(c, hipGetLastError());
   return RSA_OK;
 }

@@ -185,7 +185,14 @@ class Engine(object):
             self.ctx.call('rsa_classify', _ptr(b.tuples), _ptr(b.ts), _ptr(b.order), ctypes.c_uint64(b.n),
                           _ptr(gid_out))
 
-    def resolve_cap(self):
+    def resolve_cap(self, sync=True):
+        """The cap resolution; returns the number of capped rules.  With
+        sync=False the count stays on the device (None is returned): a
+        following pass2 then runs unconditionally and its kernels skip their
+        work on the device when no rule is capped -- one host round trip less."""
+        if not sync:
+            self.ctx.call('rsa_resolve_cap', None)
+            return None
         n = ctypes.c_uint32(0)
         self.ctx.call('rsa_resolve_cap', ctypes.byref(n))
         return int(n.value)
@@ -255,8 +262,10 @@ class Engine(object):
                        c['distinct'][:R].cpu().numpy().view(np.uint32), c['thresh'][:R].cpu().numpy().view(np.uint64),
                        host.copy(), cap)
 
-    def run(self, batches, cap, capacity, keep_gids=True):
-        """Full single-GPU job over device batches; returns Results."""
+    def run(self, batches, cap, capacity, keep_gids=True, sync_cap=True):
+        """Full single-GPU job over device batches; returns Results.  With
+        sync_cap=False the capped-rule count is not read back (resolve_cap
+        sync=False) and the recount always runs."""
         torch = self.torch
         self.reset(capacity, cap)
         gid_bufs = []
@@ -266,7 +275,8 @@ class Engine(object):
                 g = torch.empty(b.n, dtype=torch.int32, device=self.device)
             self.pass1(b, g)
             gid_bufs.append(g)
-        if self.resolve_cap():
+        n_capped = self.resolve_cap(sync=sync_cap)
+        if n_capped is None or n_capped > 0:
             for b, g in zip(batches, gid_bufs):
                 self.pass2(b, g)
         self.last_gids = gid_bufs

@@ -47,7 +47,7 @@ def test_golden_mapper_stream(engine, case):
 
 
 def _gpu_vs_oracle(engine, n_rules, n_lines, cap, seed, zipf=None, interfaces=('outside',), batches=1,
-                   shuffle=False, index=True, broad=True, prefix=0, kind=None, population=None):
+                   shuffle=False, index=True, broad=True, prefix=0, kind=None, population=None, sync_cap=True):
     dbj, info = synth.make_db(seed, n_rules, interfaces=interfaces, broad=broad)
     if population:
         tr = synth.make_traffic_population((dbj, info), n_lines, seed=seed + 1, s=zipf, population=population)
@@ -63,7 +63,7 @@ def _gpu_vs_oracle(engine, n_rules, n_lines, cap, seed, zipf=None, interfaces=('
     engine.load_compiled(compiled, index=index, prefix=prefix, kind=kind)
     cuts = np.linspace(0, n_lines, batches + 1).astype(int)
     bs = [DeviceBatch.from_numpy(tup[a:b], ts[a:b], order[a:b], engine.device) for a, b in zip(cuts[:-1], cuts[1:])]
-    res = engine.run(bs, cap, capacity=max(built_hit_count(tup), 1))
+    res = engine.run(bs, cap, capacity=max(built_hit_count(tup), 1), sync_cap=sync_cap)
     gids = np.concatenate([g.cpu().numpy() for g in engine.last_gids])
     R = coracle.OracleRules(dbj)
     cols, ots, oorder = coracle.inputs_from_traffic(R, tr)
@@ -127,6 +127,15 @@ def test_synth_parity_deferred_tail(engine, kind):
 def test_synth_parity_bucket_index(engine, kind):
     """The partial-key bucket index (RSA5, both forms) against the oracle."""
     _gpu_vs_oracle(engine, 3000, 300000, 40, seed=61, zipf=1.2, broad=False, kind=kind)
+
+
+@pytest.mark.parametrize('cap', [5, 1000000])
+def test_synth_parity_cap_count_on_device(engine, cap):
+    """rsa_resolve_cap without the host read (the count stays on the device)
+    and the recount run unconditionally: its kernels skip their work on the
+    device when no rule is capped.  Equal to the oracle with rules capped and
+    with none (bench.py's job takes this form)."""
+    _gpu_vs_oracle(engine, 2000, 300000, cap, seed=31, zipf=1.1, sync_cap=False)
 
 
 def test_synth_parity_wave_cap_scatter(engine):
