@@ -2229,11 +2229,23 @@ __global__ __launch_bounds__(1024) void k_hot_combine(const Rec* __restrict__ re
 
 // Segment starts of one pass-1 launch: starts[r] = base + offs[r * n_tiles],
 // starts[n_regions] = base + the record total (written by k_scan_sums).
+// (hot_ctl / hot_total / ncap / cursor, nullable: the counters the hot-region
+// plan and the next cap resolution accumulate into, zeroed here instead of
+// by four memset launches per pass-1 launch; every earlier reader of them
+// precedes this kernel in stream order)
 __global__ void k_seg_starts(const uint32_t* __restrict__ offs, uint32_t n_tiles, uint32_t n_regions,
-                             unsigned long long base, const uint32_t* __restrict__ total, unsigned long long* starts) {
+                             unsigned long long base, const uint32_t* __restrict__ total, unsigned long long* starts,
+                             uint32_t* hot_ctl, unsigned long long* hot_total, unsigned int* ncap,
+                             unsigned long long* cursor) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r < n_regions) starts[r] = base + offs[(size_t)r * n_tiles];
   if (r == n_regions) starts[r] = base + *total;
+  if (r == 0) {
+    if (hot_ctl) hot_ctl[0] = hot_ctl[1] = hot_ctl[2] = hot_ctl[3] = 0u;
+    if (hot_total) *hot_total = 0ull;
+    if (ncap) *ncap = 0u;
+    if (cursor) *cursor = 0ull;
+  }
 }
 
 // Pass 2: lines with order <= P of capped rules recount count/first/last into
@@ -2961,6 +2973,8 @@ struct rsa_ctx {
   bool region_import = true;                // RSA_OPT_REGION_IMPORT: rsa_import by region sort + k_reduce
   bool slots_clean = true;                  // no slot holds a key of an earlier job (k_import's CAS claims need it)
   bool hot_split = true;                    // RSA_OPT_HOT_SPLIT
+  bool hot_ctl_zeroed = false;              // d_hot_ctl / d_hot_total zeroed by the last k_seg_starts
+  bool cap_ctl_zeroed = false;              // d_flags[2] / d_cursor zeroed by the last k_seg_starts
   unsigned long long hot_min = kHotMinRecs; // RSA_OPT_HOT_MIN: a hot region holds more than max(hot_min,
   uint32_t hot_factor = kHotFactor;         //   hot_factor x the mean region) records
   void* d_hot = nullptr;                    // HRec[hot_alloc]
@@ -3193,8 +3207,11 @@ int cap_select(rsa_ctx* c, unsigned long long* out, uint32_t* h_n_capped) {
     c->sort_alloc = c->slot_cap;
   }
   unsigned int* d_ncap = c->d_flags + 2;
-  HIPCHK(c, hipMemsetAsync(d_ncap, 0, sizeof(unsigned int), c->stream));
-  HIPCHK(c, hipMemsetAsync(c->d_cursor, 0, sizeof(unsigned long long), c->stream));
+  if (!c->cap_ctl_zeroed) {   // (a pass-1 launch zeroes them in k_seg_starts)
+    HIPCHK(c, hipMemsetAsync(d_ncap, 0, sizeof(unsigned int), c->stream));
+    HIPCHK(c, hipMemsetAsync(c->d_cursor, 0, sizeof(unsigned long long), c->stream));
+  }
+  c->cap_ctl_zeroed = false;
   // the keys: read from the used-list-ordered copy k_reduce<1> keeps
   // (16 B per used entry, coalesced) unless an entry was claimed by the CAS
   // import; only keys at or below the rule's earlier selection (the job's last
@@ -3366,6 +3383,16 @@ int exclusive_scan(rsa_ctx* c, uint32_t* d, unsigned long long n, uint32_t** tot
   return RSA_OK;
 }
 
+int ensure_hot_ctl(rsa_ctx* c) {
+  if (!c->d_hot_base) {
+    HIPCHK(c, hipMalloc(&c->d_hot_base, kMaxRegions * sizeof(unsigned long long)));
+    HIPCHK(c, hipMalloc(&c->d_hot_fill, kMaxRegions * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(&c->d_hot_ctl, 4 * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(&c->d_hot_total, sizeof(unsigned long long)));
+  }
+  return RSA_OK;
+}
+
 // The hot-region split for the records of segments [seg0, seg0 + n_segs) of
 // d_starts (at most `records` records): plan, combine; returns the hot
 // descriptors for k_reduce in *base / *fill / *hot (nullptr: split off).
@@ -3375,14 +3402,12 @@ int hot_split(rsa_ctx* c, uint32_t seg0, uint32_t n_segs, unsigned long long rec
   *base = nullptr;
   *fill = nullptr;
   *hot = nullptr;
+  const bool zeroed = c->hot_ctl_zeroed;
+  c->hot_ctl_zeroed = false;
   if (!c->hot_split || records == 0) return RSA_OK;
   const uint32_t n_regions = 1u << c->np_bits;
-  if (!c->d_hot_base) {
-    HIPCHK(c, hipMalloc(&c->d_hot_base, kMaxRegions * sizeof(unsigned long long)));
-    HIPCHK(c, hipMalloc(&c->d_hot_fill, kMaxRegions * sizeof(uint32_t)));
-    HIPCHK(c, hipMalloc(&c->d_hot_ctl, 4 * sizeof(uint32_t)));
-    HIPCHK(c, hipMalloc(&c->d_hot_total, sizeof(unsigned long long)));
-  }
+  int rc0 = ensure_hot_ctl(c);
+  if (rc0) return rc0;
   const size_t max_tasks = records / kHotSlice + (size_t)n_segs * n_regions + 1;
   if (max_tasks > c->tasks_alloc || records > c->hot_alloc) HIPCHK(c, hipStreamSynchronize(c->stream));
   if (max_tasks > c->tasks_alloc) {
@@ -3399,8 +3424,10 @@ int hot_split(rsa_ctx* c, uint32_t seg0, uint32_t n_segs, unsigned long long rec
     HIPCHK(c, hipMalloc(&c->d_hot, records * sizeof(HRec)));
     c->hot_alloc = records;
   }
-  HIPCHK(c, hipMemsetAsync(c->d_hot_ctl, 0, 4 * sizeof(uint32_t), c->stream));
-  HIPCHK(c, hipMemsetAsync(c->d_hot_total, 0, sizeof(unsigned long long), c->stream));
+  if (!zeroed) {   // (pass 1 zeroes them in k_seg_starts)
+    HIPCHK(c, hipMemsetAsync(c->d_hot_ctl, 0, 4 * sizeof(uint32_t), c->stream));
+    HIPCHK(c, hipMemsetAsync(c->d_hot_total, 0, sizeof(unsigned long long), c->stream));
+  }
   HotTask* tasks = static_cast<HotTask*>(c->d_hot_tasks);
   k_hot_plan<<<(n_regions + 255) / 256, 256, 0, c->stream>>>(c->d_starts + (size_t)seg0 * (n_regions + 1), n_segs,
                                                              n_regions, tasks, (uint32_t)max_tasks, c->d_hot_ctl,
@@ -3447,7 +3474,7 @@ int count_by_block(rsa_ctx* c, const uint32_t* gh, uint64_t m) {
   if (rc) return rc;
   k_cnt_scatter<<<n_tiles, 1024, 0, c->stream>>>(gh, m, n_blocks, n_tiles, tile_len, c->d_hist, c->d_cnt_words);
   k_seg_starts<<<(n_blocks + 1 + 255) / 256, 256, 0, c->stream>>>(c->d_hist, n_tiles, n_blocks, 0, total,
-                                                                  c->d_cnt_starts);
+                                                                  c->d_cnt_starts, nullptr, nullptr, nullptr, nullptr);
   k_cnt_plan<<<1, 1024, 0, c->stream>>>(c->d_cnt_starts, n_blocks, kCntChunk, c->d_cnt_tasks, (uint32_t)max_tasks,
                                         c->d_cnt_ctl);
   k_cnt_reduce<<<(unsigned)max_tasks, 1024, 0, c->stream>>>(c->d_cnt_words, c->d_cnt_tasks, c->d_cnt_ctl, c->n_rules,
@@ -3528,7 +3555,13 @@ int launch_aggregate(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsig
                                                   sorted);
   HIPCHK(c, hipGetLastError());
   unsigned long long* st = c->d_starts + (size_t)c->n_segs * (n_regions + 1);
-  k_seg_starts<<<(n_regions + 1 + 255) / 256, 256, 0, c->stream>>>(c->d_hist, n_tiles, n_regions, seg_base, total, st);
+  rc = ensure_hot_ctl(c);
+  if (rc) return rc;
+  k_seg_starts<<<(n_regions + 1 + 255) / 256, 256, 0, c->stream>>>(c->d_hist, n_tiles, n_regions, seg_base, total, st,
+                                                                   c->d_hot_ctl, c->d_hot_total, c->d_flags + 2,
+                                                                   c->d_cursor);
+  c->hot_ctl_zeroed = true;
+  c->cap_ctl_zeroed = true;
   const unsigned long long* hb = nullptr;
   const uint32_t* hf = nullptr;
   const HRec* hr = nullptr;
