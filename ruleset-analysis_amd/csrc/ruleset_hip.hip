@@ -320,7 +320,7 @@ constexpr uint32_t kListWords = 20, kGroupWords = 20, kMaskWords = 4;
 #define RSA_CAP_FULLSCAN 0   // A/B builds: cap resolution gathers every capped entry's key from its slot
 #endif
 #ifndef RSA_PREFETCH_T
-#define RSA_PREFETCH_T 0   // A/B builds: load the next tuple one iteration ahead
+#define RSA_PREFETCH_T -1   // k_classify prefetch (kPf): -1 auto per variant; A/B builds: 0 none, 1 next tuple, 2 + order/ts
 #endif
 
 // Pruning stage of the index lookup for ONE lane (compile.py pht_lookup): each
@@ -1076,14 +1076,17 @@ struct Emit {
   uint32_t* wcnt;                       // records per 64-line window
 };
 
-// The record of one line, or false (need).
-__device__ __forceinline__ bool make_rec(uint32_t i, uint4 t, uint32_t gid, const Agg& A, const Emit& E, Rec& r) {
+// The record of one line, or false (need).  kPre: the line's order and
+// timestamp were loaded ahead (o_pre, ts_pre; RSA_PREFETCH_T 2).
+template <bool kPre = false>
+__device__ __forceinline__ bool make_rec(uint32_t i, uint4 t, uint32_t gid, const Agg& A, const Emit& E, Rec& r,
+                                         unsigned long long o_pre = 0, uint32_t ts_pre = 0) {
   const uint32_t flags = (t.w >> 16) & 0xFFu;
   bool need = gid != kNoGid && (flags & RSA_F_HIT) && (flags & RSA_F_BUILT) && A.cap > 0 && !(A.skip & 2u);
   if (!need) return false;
   // the three loads in flight together (one memory round trip, not two)
-  const unsigned long long o = E.ord[i];
-  const uint32_t ts = __builtin_nontemporal_load(&E.ts[i]);
+  const unsigned long long o = kPre ? o_pre : E.ord[i];
+  const uint32_t ts = kPre ? ts_pre : __builtin_nontemporal_load(&E.ts[i]);
   const unsigned long long f = A.filter[gid];
   r.ts = ts;
   if (o > f) return false;   // exact skip: capped with threshold <= filter < order
@@ -1095,14 +1098,15 @@ __device__ __forceinline__ bool make_rec(uint32_t i, uint4 t, uint32_t gid, cons
 
 // Emission for one wave of classified lines (wave-uniform call; lanes with
 // !in do nothing).  i = the lane's line, lines of a wave are i - lane .. + 63.
+template <bool kPre = false>
 __device__ __forceinline__ void emit_wave(uint32_t i, uint32_t n, bool in, uint4 t, uint32_t gid, const Agg& A,
-                                          const Emit& E) {
+                                          const Emit& E, unsigned long long o_pre = 0, uint32_t ts_pre = 0) {
   const uint32_t flags = (t.w >> 16) & 0xFFu;
   const bool matched = in && gid != kNoGid;
   const bool hit = matched && (flags & RSA_F_HIT);
   if (in) E.gh[i] = matched ? (gid | (hit ? 0x80000000u : 0u)) : 0xFFFFFFFFu;
   Rec r;
-  const bool need = in && make_rec(i, t, gid, A, E, r);
+  const bool need = in && make_rec<kPre>(i, t, gid, A, E, r, o_pre, ts_pre);
   const unsigned long long mask = __ballot(need);
   const uint32_t lane = __lane_id();
   const uint32_t w0 = i - lane;   // the window's first line (waves cover aligned 64-line windows)
@@ -1153,12 +1157,23 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kIm
   PhaseAcc ph = {};
   unsigned long long waves_seen = 0;
 #endif
-#if RSA_PREFETCH_T
-  // the next iteration's tuple is loaded before this iteration's stores, so
-  // waiting for it does not wait for them (vmcnt counts stores too)
-  uint4 t_next = blockIdx.x * blockDim.x + threadIdx.x < n32 ? T[blockIdx.x * blockDim.x + threadIdx.x]
-                                                             : make_uint4(0u, 0u, 0u, 0u);
-#endif
+  // Prefetch (kPf, RSA_PREFETCH_T): 1 = the next iteration's tuple, 2 = also
+  // its order and timestamp (the emission loads), loaded before this
+  // iteration's stores, so waiting for them does not wait for the stores
+  // (vmcnt counts stores too).  Default: 2 for the global-image variant (no LDS
+  // image; 53 VGPRs, room at 8 waves/SIMD), 0 for the LDS-image variants (at
+  // the 64-VGPR budget prefetching spills: 0.77 -> 1.03 / 1.17 ms per cfg3
+  // launch, profiles/r04ai_*).
+  constexpr int kPf = RSA_PREFETCH_T >= 0 ? RSA_PREFETCH_T : (kImg == 0 ? 2 : 0);
+  const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
+  uint4 t_next = make_uint4(0u, 0u, 0u, 0u);
+  unsigned long long o_next = 0ull;
+  uint32_t ts_next = 0u;
+  if (kPf >= 1 && i0 < n32) t_next = T[i0];
+  if (kPf >= 2 && kEmit && i0 < n32) {
+    o_next = E.ord[i0];
+    ts_next = __builtin_nontemporal_load(&E.ts[i0]);
+  }
   for (uint32_t base = blockIdx.x * blockDim.x; base < n32; base += stride) {
 #ifdef RSA_PHASE_PROF
     ph.last = __builtin_amdgcn_s_memtime();
@@ -1166,12 +1181,21 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kIm
 #endif
     const uint32_t i = base + threadIdx.x;
     const bool in = i < n32;
-#if RSA_PREFETCH_T
-    const uint4 t = t_next;
-    t_next = i + stride < n32 ? T[i + stride] : make_uint4(0u, 0u, 0u, 0u);
-#else
-    const uint4 t = in ? T[i] : make_uint4(0u, 0u, 0u, 0u);
-#endif
+    uint4 t;
+    unsigned long long o_cur = 0ull;
+    uint32_t ts_cur = 0u;
+    if (kPf >= 1) {
+      t = t_next;
+      t_next = i + stride < n32 ? T[i + stride] : make_uint4(0u, 0u, 0u, 0u);
+      if (kPf >= 2 && kEmit) {
+        o_cur = o_next;
+        ts_cur = ts_next;
+        o_next = i + stride < n32 ? E.ord[i + stride] : 0ull;
+        ts_next = i + stride < n32 ? __builtin_nontemporal_load(&E.ts[i + stride]) : 0u;
+      }
+    } else {
+      t = in ? T[i] : make_uint4(0u, 0u, 0u, 0u);
+    }
     const bool valid = in && (((t.w >> 16) & 0xFFu) & RSA_F_VALID);
     uint32_t gid;
     if (kImg > 0) {
@@ -1190,7 +1214,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kIm
       if (defer) tail[pos + __popcll(dm & ((1ull << __lane_id()) - 1ull))] = (uint32_t)i;
     }
     if (gout && in && !defer) gout[i] = (int32_t)gid;
-    if (kEmit) emit_wave(i, n32, in && !defer, t, gid, A, E);
+    if (kEmit) emit_wave<kPf >= 2>(i, n32, in && !defer, t, gid, A, E, o_cur, ts_cur);
     PH(7);
   }
 #ifdef RSA_PHASE_PROF
