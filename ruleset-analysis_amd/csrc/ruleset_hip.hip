@@ -1160,11 +1160,11 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kIm
   // Prefetch (kPf, RSA_PREFETCH_T): 1 = the next iteration's tuple, 2 = also
   // its order and timestamp (the emission loads), loaded before this
   // iteration's stores, so waiting for them does not wait for the stores
-  // (vmcnt counts stores too).  Default: 2 for the global-image variant (no LDS
-  // image; 53 VGPRs, room at 8 waves/SIMD), 0 for the LDS-image variants (at
-  // the 64-VGPR budget prefetching spills: 0.77 -> 1.03 / 1.17 ms per cfg3
-  // launch, profiles/r04ai_*).
-  constexpr int kPf = RSA_PREFETCH_T >= 0 ? RSA_PREFETCH_T : (kImg == 0 ? 2 : 0);
+  // (vmcnt counts stores too).  Default: 2 for the global-image variants and
+  // the bucket index (52-53 VGPRs, room at 8 waves/SIMD), 0 for the LDS-image
+  // pht variants (at the 64-VGPR budget prefetching spills: 0.77 -> 1.03 /
+  // 1.17 ms per cfg3 launch, profiles/r04ai_*).
+  constexpr int kPf = RSA_PREFETCH_T >= 0 ? RSA_PREFETCH_T : ((kImg == 0 || kMode == 2) ? 2 : 0);
   const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
   uint4 t_next = make_uint4(0u, 0u, 0u, 0u);
   unsigned long long o_next = 0ull;
@@ -2260,10 +2260,13 @@ __global__ __launch_bounds__(1024) void k_hot_combine(const Rec* __restrict__ re
 __global__ void k_seg_starts(const uint32_t* __restrict__ offs, uint32_t n_tiles, uint32_t n_regions,
                              unsigned long long base, const uint32_t* __restrict__ total, unsigned long long* starts,
                              uint32_t* hot_ctl, unsigned long long* hot_total, unsigned int* ncap,
-                             unsigned long long* cursor) {
+                             unsigned long long* cursor, unsigned long long* job_recs) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r < n_regions) starts[r] = base + offs[(size_t)r * n_tiles];
-  if (r == n_regions) starts[r] = base + *total;
+  if (r == n_regions) {
+    starts[r] = base + *total;
+    if (job_recs) *job_recs += *total;   // the job's pass-1 records (region policy of the next rsa_reset)
+  }
   if (r == 0) {
     if (hot_ctl) hot_ctl[0] = hot_ctl[1] = hot_ctl[2] = hot_ctl[3] = 0u;
     if (hot_total) *hot_total = 0ull;
@@ -2989,6 +2992,9 @@ struct rsa_ctx {
   unsigned long long* d_packed = nullptr;   // k_count / k_aggregate packed counters (rules > kCnt)
   // hot-region split (k_hot_plan / k_hot_combine)
   uint32_t min_regions_log2 = 10;           // RSA_OPT_MIN_REGIONS_LOG2: >= 1024 k_reduce workgroups (4 per CU)
+  uint32_t region_records = 49152;           // RSA_OPT_REGION_RECORDS: regions >= previous job's records / this
+  unsigned long long* d_job_recs = nullptr;  // pass-1 records of the current job (k_seg_starts accumulates)
+  bool job_recs_valid = false;               // d_job_recs holds a finished job's count
   bool tent2_on = false;                    // the current pass-1 launch is the last slice after the filter steps
   uint32_t late_seg = 0xFFFFFFFFu;          // its record segment (pass-2 fields of filtered rules hold its records)
   uint32_t tent_skip = 0;                   // jobs left without the tentative pass-2 fields (set when they missed)
@@ -3498,7 +3504,8 @@ int count_by_block(rsa_ctx* c, const uint32_t* gh, uint64_t m) {
   if (rc) return rc;
   k_cnt_scatter<<<n_tiles, 1024, 0, c->stream>>>(gh, m, n_blocks, n_tiles, tile_len, c->d_hist, c->d_cnt_words);
   k_seg_starts<<<(n_blocks + 1 + 255) / 256, 256, 0, c->stream>>>(c->d_hist, n_tiles, n_blocks, 0, total,
-                                                                  c->d_cnt_starts, nullptr, nullptr, nullptr, nullptr);
+                                                                  c->d_cnt_starts, nullptr, nullptr, nullptr, nullptr,
+                                                                  nullptr);
   k_cnt_plan<<<1, 1024, 0, c->stream>>>(c->d_cnt_starts, n_blocks, kCntChunk, c->d_cnt_tasks, (uint32_t)max_tasks,
                                         c->d_cnt_ctl);
   k_cnt_reduce<<<(unsigned)max_tasks, 1024, 0, c->stream>>>(c->d_cnt_words, c->d_cnt_tasks, c->d_cnt_ctl, c->n_rules,
@@ -3583,7 +3590,8 @@ int launch_aggregate(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsig
   if (rc) return rc;
   k_seg_starts<<<(n_regions + 1 + 255) / 256, 256, 0, c->stream>>>(c->d_hist, n_tiles, n_regions, seg_base, total, st,
                                                                    c->d_hot_ctl, c->d_hot_total, c->d_flags + 2,
-                                                                   c->d_cursor);
+                                                                   c->d_cursor, c->d_job_recs);
+  if (c->d_job_recs) c->job_recs_valid = true;
   c->hot_ctl_zeroed = true;
   c->cap_ctl_zeroed = true;
   const unsigned long long* hb = nullptr;
@@ -3765,7 +3773,7 @@ int rsa_ctx_destroy(rsa_ctx* c) {
                   c->d_img, c->d_resid,
                   c->d_slots, c->d_used, c->d_ukey, c->d_used_n, c->d_filter, c->d_packed, c->d_hot, c->d_hot_tasks, c->d_hot_base,
                   c->d_hot_fill, c->d_hot_ctl, c->d_hot_total, c->d_cnt_words, c->d_cnt_starts,
-                  c->d_cnt_tasks, c->d_cnt_ctl, c->d_flags, c->d_cursor, c->d_cidx,
+                  c->d_cnt_tasks, c->d_cnt_ctl, c->d_flags, c->d_cursor, c->d_job_recs, c->d_cidx,
                   c->d_capped_gid, c->d_capped_cnt, c->d_capped_start, c->d_capped_prev, c->d_keys, c->d_chk};
   for (void* b : bufs) (void)hipFree(b);
   for (int k = 0; k < kMaxEvents; ++k)
@@ -3822,6 +3830,10 @@ int rsa_set_option(rsa_ctx* c, int option, int64_t value) {
     case RSA_OPT_MIN_REGIONS_LOG2:
       if (value < 0 || value > 12) return fail(c, RSA_ERR_ARG, "RSA_OPT_MIN_REGIONS_LOG2 must be 0..12");
       c->min_regions_log2 = (uint32_t)value;
+      return RSA_OK;
+    case RSA_OPT_REGION_RECORDS:
+      if (value < 0 || value > 0xFFFFFFFFll) return fail(c, RSA_ERR_ARG, "RSA_OPT_REGION_RECORDS must be 0..2^32-1");
+      c->region_records = (uint32_t)value;
       return RSA_OK;
     case RSA_OPT_REGION_IMPORT:
       c->region_import = value != 0;
@@ -4112,11 +4124,27 @@ int rsa_reset(rsa_ctx* c, uint64_t capacity, uint32_t cap) {
     // (one k_reduce workgroup each: 1024 = four per CU, so a CU's workgroups
     // overlap their flushes; cfg2 7.43 -> 6.37 ms/step against 256) while
     // they keep >= 1024 slots
+    // and, when the previous job of this ctx classified many records, at least
+    // records / region_records of them (k_reduce<1> time grows with a region's
+    // records; cfg4/cfg5 at ~87M records: 11.04 -> 10.63 / 10.46 -> 9.68 ms per
+    // step at 4096 regions, while cfg3's 41M keep 1024: profiles/r04ak_*)
+    uint32_t want_np = c->min_regions_log2;
+    if (c->region_records && c->job_recs_valid) {
+      unsigned long long prev = 0;
+      HIPCHK(c, hipMemcpyAsync(&prev, c->d_job_recs, sizeof prev, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      uint32_t lg = 0;
+      while (lg < 12u && (1ull << lg) * c->region_records < prev) ++lg;
+      if (lg > want_np) want_np = lg;
+    }
     uint32_t rs = bits < (uint32_t)kRegionMaxBits ? bits : (uint32_t)kRegionMaxBits;
-    while (rs > 10 && bits - rs < c->min_regions_log2) --rs;
+    while (rs > 10 && bits - rs < want_np) --rs;
     c->rs_bits = rs;
     c->np_bits = bits - rs;
   }
+  if (!c->d_job_recs) HIPCHK(c, hipMalloc(&c->d_job_recs, sizeof(unsigned long long)));
+  HIPCHK(c, hipMemsetAsync(c->d_job_recs, 0, sizeof(unsigned long long), c->stream));
+  c->job_recs_valid = false;
   if (want > c->slot_alloc) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     hipFree(c->d_slots);

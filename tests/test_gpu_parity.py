@@ -47,7 +47,8 @@ def test_golden_mapper_stream(engine, case):
 
 
 def _gpu_vs_oracle(engine, n_rules, n_lines, cap, seed, zipf=None, interfaces=('outside',), batches=1,
-                   shuffle=False, index=True, broad=True, prefix=0, kind=None, population=None, sync_cap=True):
+                   shuffle=False, index=True, broad=True, prefix=0, kind=None, population=None, sync_cap=True,
+                   capacity=None):
     dbj, info = synth.make_db(seed, n_rules, interfaces=interfaces, broad=broad)
     if population:
         tr = synth.make_traffic_population((dbj, info), n_lines, seed=seed + 1, s=zipf, population=population)
@@ -63,7 +64,7 @@ def _gpu_vs_oracle(engine, n_rules, n_lines, cap, seed, zipf=None, interfaces=('
     engine.load_compiled(compiled, index=index, prefix=prefix, kind=kind)
     cuts = np.linspace(0, n_lines, batches + 1).astype(int)
     bs = [DeviceBatch.from_numpy(tup[a:b], ts[a:b], order[a:b], engine.device) for a, b in zip(cuts[:-1], cuts[1:])]
-    res = engine.run(bs, cap, capacity=max(built_hit_count(tup), 1), sync_cap=sync_cap)
+    res = engine.run(bs, cap, capacity=capacity or max(built_hit_count(tup), 1), sync_cap=sync_cap)
     gids = np.concatenate([g.cpu().numpy() for g in engine.last_gids])
     R = coracle.OracleRules(dbj)
     cols, ots, oorder = coracle.inputs_from_traffic(R, tr)
@@ -136,6 +137,21 @@ def test_synth_parity_cap_count_on_device(engine, cap):
     device when no rule is capped.  Equal to the oracle with rules capped and
     with none (bench.py's job takes this form)."""
     _gpu_vs_oracle(engine, 2000, 300000, cap, seed=31, zipf=1.1, sync_cap=False)
+
+
+def test_synth_parity_region_count_from_previous_job(engine):
+    """rsa_reset sizes the region count from the previous job's pass-1 record
+    count (RSA_OPT_REGION_RECORDS): with 64 records per region and a table of
+    2^23 slots, jobs after the first run at 4096 regions of 2048 slots instead
+    of 1024; every job stays equal to the oracle, and so does the policy off."""
+    engine.set_option(native.RSA_OPT_REGION_RECORDS, 64)
+    try:
+        for seed in (33, 35):
+            _gpu_vs_oracle(engine, 2000, 300000, 5, seed=seed, zipf=1.1, capacity=1 << 22)
+        engine.set_option(native.RSA_OPT_REGION_RECORDS, 0)
+        _gpu_vs_oracle(engine, 2000, 300000, 5, seed=37, zipf=1.1, capacity=1 << 22)
+    finally:
+        engine.set_option(native.RSA_OPT_REGION_RECORDS, 49152)
 
 
 def test_synth_parity_wave_cap_scatter(engine):
