@@ -1862,8 +1862,11 @@ static_assert(sizeof(HRec) == 40, "hot record layout");
 #ifndef RSA_RED2_WPE
 #define RSA_RED2_WPE 8   // pass 2: 64 VGPRs, two 1024-thread workgroups per CU (73 KiB LDS each)
 #endif
+#ifndef RSA_RED1_WPE
+#define RSA_RED1_WPE 4   // pass 1: one 1024-thread workgroup per CU (3072 LDS entries, 127 KiB)
+#endif
 template <int kPass>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2 ? RSA_RED2_WPE : 4, 8))) void k_reduce(const Rec* __restrict__ recs,
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2 ? RSA_RED2_WPE : RSA_RED1_WPE, 8))) void k_reduce(const Rec* __restrict__ recs,
                                                  const unsigned long long* __restrict__ starts, uint32_t n_segs,
                                                  Agg A, const unsigned long long* __restrict__ hot_base,
                                                  const uint32_t* __restrict__ hot_fill, const HRec* __restrict__ hot,
