@@ -1760,7 +1760,10 @@ __global__ __launch_bounds__(1024) void k_scan_add(uint32_t* __restrict__ a, uns
 #endif
 template <int kPass>
 constexpr int kRedE = kPass == 1 ? RSA_RED1 : 2048;
-constexpr int kRegionMaxBits = 16;          // region <= 65536 slots (bitmap copy 8 KiB)
+#ifndef RSA_REGION_MAX_BITS
+#define RSA_REGION_MAX_BITS 16
+#endif
+constexpr int kRegionMaxBits = RSA_REGION_MAX_BITS;   // region <= 2^16 slots (bitmap copy 8 KiB)
 
 // kPass 1: the pass-1 reduction above.  kPass 2: the cap recount
 // (connlist-reducer.py:151-176 after the dict froze) from the records pass 1
