@@ -193,6 +193,7 @@ typedef struct rsa_pht_list {    /* 80 B: one list (or one chained chunk of a li
 #define RSA_OPT_OWNER_RANK 20    /* this ctx's rank for RSA_OPT_OWNER_WORLD */
 #define RSA_OPT_MIN_REGIONS_LOG2 21 /* table regions: at least 2^v of them (one k_reduce workgroup each) while a region keeps >= 1024 slots (default 10); takes effect at rsa_reset */
 #define RSA_OPT_REGION_RECORDS 22 /* table regions: at least the previous job's pass-1 record count / v of them (rounded up to a power of two, at most 4096; 0 = off; default 49152): more k_reduce workgroups for record-heavy jobs; takes effect at rsa_reset */
+#define RSA_OPT_REDUCE_BIG 23 /* pass-1 merges of jobs with more than 1024 table regions through a 4096-entry LDS table (1, default) instead of 3072 (0); takes effect per pass-1 launch */
 #define RSA_OPT_COUNT_SORT 18    /* rule sets past the LDS counters (> 13312 rules): per-rule line/hit counters by a counting sort of the lines by rule block and LDS histograms (1, default) or one device atomic per line (0) */
 
 /* One distinct (rule, connection) aggregate, 40 B (connlist-reducer.py:162-176). */

@@ -1868,16 +1868,16 @@ static_assert(sizeof(HRec) == 40, "hot record layout");
 #ifndef RSA_RED1_WPE
 #define RSA_RED1_WPE 4   // pass 1: one 1024-thread workgroup per CU (3072 LDS entries, 127 KiB)
 #endif
-template <int kPass>
+template <int kPass, int kE = kRedE<kPass>, int kBits = kRegionMaxBits>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2 ? RSA_RED2_WPE : RSA_RED1_WPE, 8))) void k_reduce(const Rec* __restrict__ recs,
                                                  const unsigned long long* __restrict__ starts, uint32_t n_segs,
                                                  Agg A, const unsigned long long* __restrict__ hot_base,
                                                  const uint32_t* __restrict__ hot_fill, const HRec* __restrict__ hot,
                                                  const unsigned int* __restrict__ skip_zero) {
-  __shared__ unsigned long long e_kA[kRedE<kPass>], e_kB[kRedE<kPass>], e_mo[kRedE<kPass>];
-  __shared__ uint32_t e_first[kRedE<kPass>], e_last[kRedE<kPass>], e_cnt[kRedE<kPass>];
-  __shared__ uint32_t occ[1u << (kRegionMaxBits - 5)];     // occupied before this flush
-  __shared__ uint32_t claim[1u << (kRegionMaxBits - 5)];   // claimed during this flush
+  __shared__ unsigned long long e_kA[kE], e_kB[kE], e_mo[kE];
+  __shared__ uint32_t e_first[kE], e_last[kE], e_cnt[kE];
+  __shared__ uint32_t occ[1u << (kBits - 5)];     // occupied before this flush
+  __shared__ uint32_t claim[1u << (kBits - 5)];   // claimed during this flush
   __shared__ uint32_t used;
   __shared__ uint32_t sh[18];
   __shared__ unsigned long long sh_base;
@@ -1904,7 +1904,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
     occ[w] = gocc[w];
     claim[w] = 0;
   }
-  for (uint32_t e = threadIdx.x; e < kRedE<kPass>; e += blockDim.x) e_kB[e] = kEmpty;
+  for (uint32_t e = threadIdx.x; e < kE; e += blockDim.x) e_kB[e] = kEmpty;
   if (threadIdx.x == 0) used = 0;
   __syncthreads();
   uint32_t sg = 0;
@@ -1918,7 +1918,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
     }
     const bool last_round = pos >= end;
     if (!last_round) {
-      const uint32_t room = (3u * kRedE<kPass>) / 4 - used;
+      const uint32_t room = (3u * kE) / 4 - used;
       const unsigned long long take = end - pos < room ? end - pos : room;
       __syncthreads();   // every thread has read `used` before any insert changes it
       for (unsigned long long jb = 0; jb < take; jb += blockDim.x) {   // workgroup-uniform trip count
@@ -1949,7 +1949,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
             if (P == RSA_NO_THRESHOLD || mo > P) have = false;
           }
         }
-        lds_agg_insert<kRedE<kPass>, kPass == 1>(e_kA, e_kB, e_mo, e_first, e_last, e_cnt, used, have, kA, kB, mo,
+        lds_agg_insert<kE, kPass == 1>(e_kA, e_kB, e_mo, e_first, e_last, e_cnt, used, have, kA, kB, mo,
                                                  first, last, cnt);
       }
       pos += take;
@@ -1957,13 +1957,13 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
       bool more = pos < end;
       for (uint32_t q = sg + 1; q < n_segs && !more; ++q)
         more = starts[(size_t)q * (n_regions + 1) + region + 1] > starts[(size_t)q * (n_regions + 1) + region];
-      if (used + 512u <= (3u * kRedE<kPass>) / 4 && more) continue;   // workgroup-uniform: room for 512 more
+      if (used + 512u <= (3u * kE) / 4 && more) continue;   // workgroup-uniform: room for 512 more
     }
     if (used > 0) {   // workgroup-uniform (read after a barrier)
       // flush: merge every LDS entry into the region; new slots are appended to
       // the used list with ONE device atomic per flush (a per-wave append on
       // the single cursor word would serialise ~30 atomics per workgroup on it)
-      constexpr int kPer = kRedE<kPass> / 1024;
+      constexpr int kPer = kE / 1024;
       unsigned long long new_slot[kPer];   // statically indexed (a counter index would spill it)
       bool is_new[kPer];
       // the home slots of this thread's entries first, every load in flight
@@ -2999,6 +2999,7 @@ struct rsa_ctx {
   // hot-region split (k_hot_plan / k_hot_combine)
   uint32_t min_regions_log2 = 10;           // RSA_OPT_MIN_REGIONS_LOG2: >= 1024 k_reduce workgroups (4 per CU)
   uint32_t region_records = 49152;           // RSA_OPT_REGION_RECORDS: regions >= previous job's records / this
+  bool reduce_big = true;                    // RSA_OPT_REDUCE_BIG: 4096-entry k_reduce<1> above 1024 regions
   unsigned long long* d_job_recs = nullptr;  // pass-1 records of the current job (k_seg_starts accumulates)
   bool job_recs_valid = false;               // d_job_recs holds a finished job's count
   bool tent2_on = false;                    // the current pass-1 launch is the last slice after the filter steps
@@ -3605,8 +3606,17 @@ int launch_aggregate(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsig
   const HRec* hr = nullptr;
   rc = hot_split<1>(c, c->n_segs, 1, m, &hb, &hf, &hr);
   if (rc) return rc;
-  k_reduce<1><<<n_regions, 1024, 0, c->stream>>>(reinterpret_cast<const Rec*>(c->d_recs2), st, 1, ag, hb, hf, hr,
-                                                 nullptr);
+  // record-heavy jobs (the region policy chose more than 1024 regions) merge
+  // through a 4096-entry LDS table (regions of at most 2^15 slots, so both
+  // bitmaps fit: 156 KiB): cfg5 9.84 -> 9.61 ms/step, while cfg3's 1024
+  // regions keep 3072 entries (4096 there: 8.03 -> 8.17; profiles/r04ao_*)
+  if (c->np_bits > 10 && c->rs_bits <= 15 && c->reduce_big) {
+    k_reduce<1, 4096, 15><<<n_regions, 1024, 0, c->stream>>>(reinterpret_cast<const Rec*>(c->d_recs2), st, 1, ag, hb,
+                                                             hf, hr, nullptr);
+  } else {
+    k_reduce<1><<<n_regions, 1024, 0, c->stream>>>(reinterpret_cast<const Rec*>(c->d_recs2), st, 1, ag, hb, hf, hr,
+                                                   nullptr);
+  }
   HIPCHK(c, hipGetLastError());
   if (c->rec_cache) ++c->n_segs;
   if (c->debug) {
@@ -3836,6 +3846,9 @@ int rsa_set_option(rsa_ctx* c, int option, int64_t value) {
     case RSA_OPT_MIN_REGIONS_LOG2:
       if (value < 0 || value > 12) return fail(c, RSA_ERR_ARG, "RSA_OPT_MIN_REGIONS_LOG2 must be 0..12");
       c->min_regions_log2 = (uint32_t)value;
+      return RSA_OK;
+    case RSA_OPT_REDUCE_BIG:
+      c->reduce_big = value != 0;
       return RSA_OK;
     case RSA_OPT_REGION_RECORDS:
       if (value < 0 || value > 0xFFFFFFFFll) return fail(c, RSA_ERR_ARG, "RSA_OPT_REGION_RECORDS must be 0..2^32-1");

@@ -143,7 +143,8 @@ def test_synth_parity_region_count_from_previous_job(engine):
     """rsa_reset sizes the region count from the previous job's pass-1 record
     count (RSA_OPT_REGION_RECORDS): with 64 records per region and a table of
     2^23 slots, jobs after the first run at 4096 regions of 2048 slots instead
-    of 1024; every job stays equal to the oracle, and so does the policy off."""
+    of 1024 (and merge through the 4096-entry k_reduce<1>); every job stays
+    equal to the oracle, and so does the policy off."""
     engine.set_option(native.RSA_OPT_REGION_RECORDS, 64)
     try:
         for seed in (33, 35):
