@@ -284,8 +284,12 @@ int rsa_last_pass1_launches(rsa_ctx *ctx, uint32_t *h_n);
  * distinct >= cap, P = the order key of the line that inserted the cap-th
  * distinct connection, written to d_thresh.  *h_n_capped receives the number
  * of capped rules (0 means no recount pass is needed).  h_n_capped may be
- * NULL: no host round trip; the count stays on the device and a following
- * rsa_recount of the cached batch skips its work there when it is 0. */
+ * NULL: no host round trip; the count stays on the device and the next
+ * rsa_recount of the cached batch skips its work there when it is 0.  Only a
+ * NULL resolution arms that skip (a caller that reads the count may rewrite
+ * d_thresh before its recount, as the multi-GPU merge does with the global
+ * thresholds, so its recount never skips on the local count); the skip is
+ * consumed by that recount and disarmed by any other resolution or reset. */
 int rsa_resolve_cap(rsa_ctx *ctx, uint32_t *h_n_capped);
 
 /* Pass 2 — recount occurrences with order <= P for capped rules, per batch.

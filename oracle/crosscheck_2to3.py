@@ -75,7 +75,9 @@ db.close()
 '''
 
 
-def run_reference(work, db_json, log_text, host, cap):
+def prepare_reference(work, db_json, cap):
+    """Convert the reference scripts into ``work`` and build its
+    ``accesslists.db`` from ``db_json``, the cap set in its ``config.py``."""
     os.makedirs(work, exist_ok=True)
     for name in ('mapper.py', 'connlist-reducer.py', 'firewallrule.py', 'config.py'):
         _convert(os.path.join(REF, name), os.path.join(work, name))
@@ -101,21 +103,60 @@ def run_reference(work, db_json, log_text, host, cap):
         json.dump(db_json, f)
     with open(os.path.join(work, 'build_db.py'), 'w') as f:
         f.write(BUILD_DB)
-    env = dict(os.environ, PYTHONIOENCODING='latin-1', LC_ALL='C', PYTHONHASHSEED='0')
-    subprocess.run([sys.executable, 'build_db.py', 'db.json'], cwd=work, check=True, env=env)
-    with open(os.path.join(work, 'log.txt'), 'w', encoding='latin-1', newline='') as f:
-        f.write(log_text)
-    env['mapred_input_dir'] = '/logs/%s/part-0000' % host
-    m = subprocess.run([sys.executable, 'mapper.py'], cwd=work, env=env, stdin=open(os.path.join(work, 'log.txt'), 'rb'),
-                       stdout=subprocess.PIPE, stderr=subprocess.PIPE)
-    if m.returncode != 0:
-        raise RuntimeError('reference mapper failed: %s' % m.stderr.decode('latin-1')[-2000:])
-    s = subprocess.run(['sort'], input=m.stdout, stdout=subprocess.PIPE, env=env, check=True)
+    subprocess.run([sys.executable, 'build_db.py', 'db.json'], cwd=work, check=True, env=_env())
+
+
+def _env():
+    return dict(os.environ, PYTHONIOENCODING='latin-1', LC_ALL='C', PYTHONHASHSEED='0')
+
+
+def _last_exception(stderr):
+    """Name of the exception a Python traceback on stderr ends with (None: none)."""
+    lines = [l for l in stderr.decode('latin-1').splitlines() if l.strip()]
+    if not lines or not any(l.startswith('Traceback') for l in lines):
+        return None
+    return lines[-1].split(':', 1)[0].strip().rsplit('.', 1)[-1]
+
+
+def run_reference_job(work, inputs):
+    """The no-Hadoop job of SURVEY.md §3.1 under ``set -o pipefail`` in a work
+    dir prepared by prepare_reference: for each (host, log text) in turn the
+    converted mapper (host from ``mapred_input_dir``, mapper.py:107-112), its
+    stdout appended to the map output; the first mapper that exits non-zero
+    ends the map stage (a Hadoop job whose map task failed).  Then ``LC_ALL=C
+    sort | connlist-reducer.py``.  Returns a dict: map text, reducer stdout,
+    the exit status of each stage and the exception a stage died with."""
+    env = _env()
+    maps, m_rc, m_exc = [], 0, None
+    for k, (host, text) in enumerate(inputs):
+        path = os.path.join(work, 'log%d.txt' % k)
+        with open(path, 'w', encoding='latin-1', newline='') as f:
+            f.write(text)
+        env['mapred_input_dir'] = '/logs/%s/part-0000' % host
+        with open(path, 'rb') as fin:
+            m = subprocess.run([sys.executable, 'mapper.py'], cwd=work, env=env, stdin=fin, stdout=subprocess.PIPE,
+                               stderr=subprocess.PIPE)
+        maps.append(m.stdout)
+        if m.returncode != 0:
+            m_rc, m_exc = m.returncode, _last_exception(m.stderr) or 'SystemExit'
+            break
+    mapped = b''.join(maps)
+    s = subprocess.run(['sort'], input=mapped, stdout=subprocess.PIPE, env=env, check=True)
     r = subprocess.run([sys.executable, 'connlist-reducer.py'], cwd=work, env=env, input=s.stdout,
                        stdout=subprocess.PIPE, stderr=subprocess.PIPE)
-    if r.returncode != 0:
-        raise RuntimeError('reference reducer failed: %s' % r.stderr.decode('latin-1')[-2000:])
-    return m.stdout.decode('latin-1'), r.stdout.decode('latin-1')
+    return {'map': mapped.decode('latin-1'), 'reduce': r.stdout.decode('latin-1'), 'map_rc': m_rc,
+            'map_exc': m_exc, 'reduce_rc': r.returncode,
+            'reduce_exc': _last_exception(r.stderr) if r.returncode else None}
+
+
+def run_reference(work, db_json, log_text, host, cap):
+    prepare_reference(work, db_json, cap)
+    res = run_reference_job(work, [(host, log_text)])
+    if res['map_rc'] != 0:
+        raise RuntimeError('reference mapper failed: %s' % res['map_exc'])
+    if res['reduce_rc'] != 0:
+        raise RuntimeError('reference reducer failed: %s' % res['reduce_exc'])
+    return res['map'], res['reduce']
 
 
 def run_postprocess(work, hadoop_text):

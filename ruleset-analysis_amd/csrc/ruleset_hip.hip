@@ -3002,6 +3002,8 @@ struct rsa_ctx {
   bool reduce_big = true;                    // RSA_OPT_REDUCE_BIG: 4096-entry k_reduce<1> above 1024 regions
   unsigned long long* d_job_recs = nullptr;  // pass-1 records of the current job (k_seg_starts accumulates)
   bool job_recs_valid = false;               // d_job_recs holds a finished job's count
+  unsigned long long h_job_recs = 0;         // d_job_recs as read by the last emission (no extra sync)
+  bool h_job_recs_valid = false;
   bool tent2_on = false;                    // the current pass-1 launch is the last slice after the filter steps
   uint32_t late_seg = 0xFFFFFFFFu;          // its record segment (pass-2 fields of filtered rules hold its records)
   uint32_t tent_skip = 0;                   // jobs left without the tentative pass-2 fields (set when they missed)
@@ -3012,6 +3014,8 @@ struct rsa_ctx {
   bool hot_split = true;                    // RSA_OPT_HOT_SPLIT
   bool hot_ctl_zeroed = false;              // d_hot_ctl / d_hot_total zeroed by the last k_seg_starts
   bool cap_ctl_zeroed = false;              // d_flags[2] / d_cursor zeroed by the last k_seg_starts
+  bool ncap_on_device = false;              // d_flags[2] = capped rules of the last rsa_resolve_cap(ctx, NULL):
+                                            //   the next rsa_recount may skip on the device when it is 0
   unsigned long long hot_min = kHotMinRecs; // RSA_OPT_HOT_MIN: a hot region holds more than max(hot_min,
   uint32_t hot_factor = kHotFactor;         //   hot_factor x the mean region) records
   void* d_hot = nullptr;                    // HRec[hot_alloc]
@@ -3249,6 +3253,7 @@ int cap_select(rsa_ctx* c, unsigned long long* out, uint32_t* h_n_capped) {
     HIPCHK(c, hipMemsetAsync(c->d_cursor, 0, sizeof(unsigned long long), c->stream));
   }
   c->cap_ctl_zeroed = false;
+  c->ncap_on_device = false;
   // the keys: read from the used-list-ordered copy k_reduce<1> keeps
   // (16 B per used entry, coalesced) unless an entry was claimed by the CAS
   // import; only keys at or below the rule's earlier selection (the job's last
@@ -3435,7 +3440,8 @@ int ensure_hot_ctl(rsa_ctx* c) {
 // descriptors for k_reduce in *base / *fill / *hot (nullptr: split off).
 template <int kPass>
 int hot_split(rsa_ctx* c, uint32_t seg0, uint32_t n_segs, unsigned long long records,
-              const unsigned long long** base, const uint32_t** fill, const HRec** hot) {
+              const unsigned long long** base, const uint32_t** fill, const HRec** hot,
+              const unsigned int* skip_zero = nullptr) {
   *base = nullptr;
   *fill = nullptr;
   *hot = nullptr;
@@ -3469,7 +3475,7 @@ int hot_split(rsa_ctx* c, uint32_t seg0, uint32_t n_segs, unsigned long long rec
   k_hot_plan<<<(n_regions + 255) / 256, 256, 0, c->stream>>>(c->d_starts + (size_t)seg0 * (n_regions + 1), n_segs,
                                                              n_regions, tasks, (uint32_t)max_tasks, c->d_hot_ctl,
                                                              c->d_hot_total, c->d_hot_base, c->d_hot_fill, c->hot_min,
-                                                             c->hot_factor, kPass == 2 ? c->d_flags + 2 : nullptr);
+                                                             c->hot_factor, skip_zero);
   k_hot_combine<kPass><<<c->cu_count, 1024, 0, c->stream>>>(reinterpret_cast<const Rec*>(c->d_recs2), tasks,
                                                              c->d_hot_ctl, agg_of(c), c->d_hot_base, c->d_hot_fill,
                                                              static_cast<HRec*>(c->d_hot));
@@ -3733,6 +3739,7 @@ int emit_mode(rsa_ctx* c, int mode, rsa_conn_record* out, uint64_t max_out, uint
   if (rc) return rc;
   if (max_out && !out) return fail(c, RSA_ERR_ARG, "null output buffer");
   HIPCHK(c, hipMemsetAsync(c->d_cursor, 0, sizeof(unsigned long long), c->stream));
+  c->cap_ctl_zeroed = false;   // d_cursor is advanced below: the next cap_select zeroes it itself
   // persistent grid (two 1024-thread workgroups per CU) over the device-side
   // used count; one round trip for the emitted count and the error flags
   k_emit<<<c->cu_count * 2, 1024, 0, c->stream>>>(c->d_slots, c->d_used, c->d_used_n, c->slot_cap, c->d_thresh, mode,
@@ -3743,7 +3750,13 @@ int emit_mode(rsa_ctx* c, int mode, rsa_conn_record* out, uint64_t max_out, uint
   unsigned int f[4];
   HIPCHK(c, hipMemcpyAsync(&n, c->d_cursor, sizeof n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipMemcpyAsync(f, c->d_flags, sizeof f, hipMemcpyDeviceToHost, c->stream));
+  // the job's pass-1 record count rides along (the next rsa_reset sizes its
+  // regions from it without a round trip of its own)
+  const bool read_recs = c->job_recs_valid && c->d_job_recs;
+  if (read_recs)
+    HIPCHK(c, hipMemcpyAsync(&c->h_job_recs, c->d_job_recs, sizeof c->h_job_recs, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->h_job_recs_valid = read_recs;
   rc = flags_status(c, f);
   if (rc) return rc;
   *h_n = n;
@@ -4149,9 +4162,12 @@ int rsa_reset(rsa_ctx* c, uint64_t capacity, uint32_t cap) {
     // step at 4096 regions, while cfg3's 41M keep 1024: profiles/r04ak_*)
     uint32_t want_np = c->min_regions_log2;
     if (c->region_records && c->job_recs_valid) {
-      unsigned long long prev = 0;
-      HIPCHK(c, hipMemcpyAsync(&prev, c->d_job_recs, sizeof prev, hipMemcpyDeviceToHost, c->stream));
-      HIPCHK(c, hipStreamSynchronize(c->stream));
+      // the count as the job's emission read it, else one read here
+      unsigned long long prev = c->h_job_recs;
+      if (!c->h_job_recs_valid) {
+        HIPCHK(c, hipMemcpyAsync(&prev, c->d_job_recs, sizeof prev, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+      }
       uint32_t lg = 0;
       while (lg < 12u && (1ull << lg) * c->region_records < prev) ++lg;
       if (lg > want_np) want_np = lg;
@@ -4164,6 +4180,8 @@ int rsa_reset(rsa_ctx* c, uint64_t capacity, uint32_t cap) {
   if (!c->d_job_recs) HIPCHK(c, hipMalloc(&c->d_job_recs, sizeof(unsigned long long)));
   HIPCHK(c, hipMemsetAsync(c->d_job_recs, 0, sizeof(unsigned long long), c->stream));
   c->job_recs_valid = false;
+  c->h_job_recs_valid = false;
+  c->ncap_on_device = false;
   if (want > c->slot_alloc) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     hipFree(c->d_slots);
@@ -4289,7 +4307,13 @@ int rsa_resolve_cap(rsa_ctx* c, uint32_t* h_n_capped) {
   if (!c) return RSA_ERR_ARG;
   int rc = need_agg(c);
   if (rc) return rc;
-  return cap_select(c, c->d_thresh, h_n_capped);
+  rc = cap_select(c, c->d_thresh, h_n_capped);
+  // with no host count the recount reads it on the device (and returns at
+  // once when it is 0); a caller that read the count decides itself, and may
+  // rewrite the thresholds before the recount (the multi-GPU merge installs
+  // the global ones), so its recount never skips on the local count
+  c->ncap_on_device = rc == RSA_OK && h_n_capped == nullptr;
+  return rc;
 }
 
 constexpr uint32_t kTentBackoff = 8;
@@ -4336,12 +4360,14 @@ int rsa_recount(rsa_ctx* c, const rsa_tuple* T, const uint32_t* TS, const uint64
     const unsigned long long* hb = nullptr;
     const uint32_t* hf = nullptr;
     const HRec* hr = nullptr;
-    int rc2 = hot_split<2>(c, 0, n_segs, n, &hb, &hf, &hr);
+    const unsigned int* skip = c->ncap_on_device ? c->d_flags + 2 : nullptr;
+    c->ncap_on_device = false;
+    int rc2 = hot_split<2>(c, 0, n_segs, n, &hb, &hf, &hr, skip);
     if (rc2) return rc2;
     // (a resolution whose count the host did not read leaves it at d_flags[2]:
     // the kernels skip their work on the device when no rule is capped)
     k_reduce<2><<<1u << c->np_bits, 1024, 0, c->stream>>>(reinterpret_cast<const Rec*>(c->d_recs2), c->d_starts,
-                                                         n_segs, agg_of(c), hb, hf, hr, c->d_flags + 2);
+                                                         n_segs, agg_of(c), hb, hf, hr, skip);
     HIPCHK(c, hipGetLastError());
     return RSA_OK;
   }

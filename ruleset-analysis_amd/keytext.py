@@ -29,9 +29,10 @@ class KeyText(object):
         """Id of a key (a (proto, from, to, port) tuple of strings)."""
         k = self.ids.get(key)
         if k is None:
-            k = self.ids[key] = len(self.values)
-            if k > 0xFFFFFFFF:
+            k = len(self.values)
+            if k > 0xFFFFFFFF:   # checked before the key is stored: no dangling id
                 raise OverflowError('more than 2^32 distinct interned connection keys')
+            self.ids[key] = k
             self.values.append(key)
         return k
 

@@ -28,9 +28,9 @@ def _worker(rank, world, port, args, out_q):
     from ruleset_analysis_amd.dist import EngineBackend, merge
     from ruleset_analysis_amd.engine import DeviceBatch, Engine
     from ruleset_analysis_amd.pipeline import built_hit_count
-    seed, n_rules, n_lines, cap = args
+    seed, n_rules, n_lines, cap, zipf = args
     dbj, info = synth.make_db(seed, n_rules)
-    tr = synth.make_traffic((dbj, info), n_lines, seed=seed + 1, zipf=1.2)
+    tr = synth.make_traffic((dbj, info), n_lines, seed=seed + 1, zipf=zipf)
     compiled = CompiledRules(acldb.load_json(dbj))
     compiled.ensure_lists()
     tup, ts, order = synth.pack(tr, compiled)
@@ -49,12 +49,10 @@ def _worker(rank, world, port, args, out_q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('cap', [12, 1000])
-def test_two_ranks_one_gpu(cap):
+def _run_two_ranks(args):
     from test_dist_merge import _free_port
     import queue
     import time
-    args = (61, 700, 120000, cap)
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
@@ -73,11 +71,18 @@ def test_two_ranks_one_gpu(cap):
     for p in procs:
         p.join(timeout=300)
         assert p.exitcode == 0
-    recs, matches, hits, distinct, thresh = out
-    dbj, info = synth.make_db(61, 700)
-    tr = synth.make_traffic((dbj, info), 120000, seed=62, zipf=1.2)
+    return out
+
+
+def _oracle_inputs(seed, n_rules, n_lines, zipf):
+    dbj, info = synth.make_db(seed, n_rules)
+    tr = synth.make_traffic((dbj, info), n_lines, seed=seed + 1, zipf=zipf)
     R = coracle.OracleRules(dbj)
-    cols, ots, oorder = coracle.inputs_from_traffic(R, tr)
+    return (R,) + tuple(coracle.inputs_from_traffic(R, tr))
+
+
+def _check(out, R, cols, ots, oorder, cap):
+    recs, matches, hits, distinct, thresh = out
     ref = coracle.run(R, cols, ots, oorder, cap)
     assert np.array_equal(matches, ref['matches'])
     assert np.array_equal(hits, ref['hits'])
@@ -88,6 +93,37 @@ def test_two_ranks_one_gpu(cap):
     want = sorted(zip(*(rows[k].astype(int).tolist() for k in ('gid', 'pspell', 'for_ip', 'to_ip', 'to_port',
                                                                   'count', 'first', 'last'))))
     assert got == want
+    return ref
+
+
+@pytest.mark.parametrize('cap', [12, 1000])
+def test_two_ranks_one_gpu(cap):
+    args = (61, 700, 120000, cap, 1.2)
+    out = _run_two_ranks(args)
+    _check(out, *_oracle_inputs(61, 700, 120000, 1.2), cap)
+
+
+def test_two_ranks_capped_only_after_merge():
+    """Uniform traffic and a cap above every shard's own distinct count but
+    below the merged count of some rules: no rank caps a rule locally, so each
+    rank's own cap resolution finds nothing, yet the merge caps rules -- every
+    rank's recount must still run under the global thresholds (ADVICE r04:
+    a device-side 'nothing capped' skip keyed on the local count dropped the
+    non-owners' pass-2 sums)."""
+    seed, n_rules, n_lines = 67, 120, 60000
+    R, cols, ots, oorder = _oracle_inputs(seed, n_rules, n_lines, None)
+    cut = np.linspace(0, n_lines, 3).astype(int)
+    big = n_lines + 1   # no rule capped (the oracle sizes its per-rule table from the cap)
+    shard_max = 0
+    for a, b in zip(cut[:-1], cut[1:]):
+        sub = {k: v[a:b] for k, v in cols.items()}
+        shard_max = max(shard_max, int(coracle.run(R, sub, ots[a:b], oorder[a:b], big)['n_conns'].max()))
+    whole = coracle.run(R, cols, ots, oorder, big)['n_conns']
+    cap = shard_max + 1
+    assert (whole >= cap).sum() >= 1, 'workload does not cap any rule only after the merge'
+    out = _run_two_ranks((seed, n_rules, n_lines, cap, None))
+    ref = _check(out, R, cols, ots, oorder, cap)
+    assert (ref['n_conns'] >= cap).any()
 
 
 @pytest.mark.parametrize('backend', ['nccl', 'gloo'])

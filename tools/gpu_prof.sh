@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC/SQ profiles of the given configs (tools/profile_round.sh passes) and their summaries.
-# Usage: tools/gpu_prof_r04.sh TAG CFG [CFG...]; lines per GPU from bench.py's CONFIGS.
+# Usage: tools/gpu_prof.sh TAG CFG [CFG...]; lines per GPU from bench.py's CONFIGS.
 set -o pipefail
 TAG=$1; shift
 export TMPDIR=/tmp

@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round-4 record call: full -m gpu suite, smoke(), the default bench line
+# Record call: full -m gpu suite, smoke(), the default bench line
 # (cfg3 with cpu_baseline), the rocprofv3 kernel trace/stats of that same
 # command, and the cfg2/cfg4/cfg5 bench lines.
 set -o pipefail
-OUT=gpurun_out/${1:-r04_final}
+OUT=gpurun_out/${1:-record}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
