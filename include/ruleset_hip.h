@@ -327,12 +327,14 @@ int rsa_stats(rsa_ctx *ctx, uint64_t *h_out4, int reset);
  * -1.  Rules are given in list order; one port per side (the preprocessors'
  * expansion, SURVEY.md trap 3).  Host buffers in and out. */
 typedef struct rsa_shadow_rule {
-  uint32_t src_lo, src_span;  /* IPv4 network [lo, lo + span]                      */
+  uint32_t src_lo, src_span;  /* IPv4 network [lo, lo + span] (IPv6: interval code)  */
   uint32_t dst_lo, dst_span;
   int32_t sport, dport;       /* one port, -1 = NO_PORT, <= -2 a list (rsa_shadowed_ports) */
   uint16_t proto;             /* protocol id, 0 = 'ip'                              */
   uint8_t action;             /* 1 permit, 0 deny                                   */
-  uint8_t v4;                 /* 1: both addresses IPv4 (else never contains/contained) */
+  uint8_t v4;                 /* address family code: 1 both IPv4; 3/4/5 = 2 + (src IPv6) + 2 x (dst IPv6),
+                                 the IPv6 sides as containment-preserving interval codes; only rules of
+                                 one code compare; 0 never contains / is contained */
   uint32_t reserved;
 } rsa_shadow_rule;
 int rsa_shadowed(rsa_ctx *ctx, const rsa_shadow_rule *h_rules, uint32_t n, int32_t *h_cover);

@@ -75,6 +75,8 @@ class OracleRules(object):
         self.dst = np.array([r.dst.ip if r.dst._ipversion == 4 else 0 for r in rules], np.uint32)
         self.src_len = np.array([r.src.len() if r.src._ipversion == 4 else 0 for r in rules], np.uint64)
         self.dst_len = np.array([r.dst.len() if r.dst._ipversion == 4 else 0 for r in rules], np.uint64)
+        self.src6 = np.array([_words6(r.src) for r in rules], np.uint64).reshape(-1)
+        self.dst6 = np.array([_words6(r.dst) for r in rules], np.uint64).reshape(-1)
         ports, sp_off, sp_len, dp_off, dp_len = [], [], [], [], []
         for r in rules:
             sp_off.append(len(ports)); sp_len.append(len(r.sport)); ports.extend(r.sport)
@@ -110,6 +112,7 @@ class OracleRules(object):
         self.proto = np.array([self._pid(x) for p in parts for x in p['proto']], np.uint8)
         self.v4src = np.ones(n, np.uint8)
         self.v4dst = np.ones(n, np.uint8)
+        self.src6 = self.dst6 = np.zeros(4 * n + 4, np.uint64)
         self.src, self.dst = cat('src', np.uint32), cat('dst', np.uint32)
         self.src_len, self.dst_len = cat('src_len', np.uint64), cat('dst_len', np.uint64)
         ports = np.empty(2 * n, np.int32)
@@ -169,6 +172,16 @@ def classify(R, list_of, proto_of, src, dst, sport, dport):
     return gid, int(evals.value)
 
 
+def _words6(ip):
+    """An IPv6 network as (ip hi, ip lo, last hi, last lo) uint64 words; zeros
+    for an IPv4 one (the C oracle reads them only for IPv6 sides)."""
+    if ip._ipversion == 4:
+        return (0, 0, 0, 0)
+    a, b = int(ip.ip), int(ip.ip) + ip.len() - 1
+    m = (1 << 64) - 1
+    return (a >> 64, a & m, b >> 64, b & m)
+
+
 def shadow(R, host, acl):
     """preprosess_access_lists.py:508-521 for one ACL: per rule the first rule
     above it that contains it (list-local index) or -1."""
@@ -178,7 +191,8 @@ def shadow(R, host, acl):
     cover = np.empty(end - beg, np.int32)
     lib().rsa_oracle_shadow(ctypes.c_uint32(beg), ctypes.c_uint32(end), _p(R.action), _p(R.proto), _p(R.v4src),
                             _p(R.v4dst), _p(R.src), _p(R.dst), _p(R.src_len), _p(R.dst_len), _p(R.sp_off),
-                            _p(R.sp_len), _p(R.dp_off), _p(R.dp_len), _p(R.ports), _p(cover))
+                            _p(R.sp_len), _p(R.dp_off), _p(R.dp_len), _p(R.ports), _p(R.src6), _p(R.dst6),
+                            _p(cover))
     return cover
 
 

@@ -128,6 +128,7 @@ def cases():
     yield 'asa_groups', lambda: synth_asa.make_config(2, 300, n_net_groups=14, n_svc_groups=8)[0]
     yield 'asa_wide', lambda: synth_asa.make_config(3, 80, wide=True)[0]
     yield 'asa_edges', lambda: EDGES
+    yield 'asa_ipv6', lambda: IPV6
 
 
 EDGES = '''hostname edge-fw
@@ -168,6 +169,41 @@ access-list dmz_in extended deny ip any any
 access-group outside_in in interface outside
 access-group dmz_in in interface dmz
 access-group dmz_in out interface inside
+'''
+
+
+# IPv6 hosts and networks (firewallrule.py:80-93 stores any address IPy takes)
+# between IPv4 rules: they keep their ruleindex, never match an IPv4
+# connection, and shadow each other only within one address family
+IPV6 = '''hostname v6-fw
+object-group network V6HOSTS
+ network-object host 2001:db8::10
+ network-object 2001:db8:1::/48
+ network-object host 10.0.0.10
+object-group network V6WIDE
+ network-object 2001:db8::/32
+object-group service WEB tcp
+ port-object eq www
+ port-object eq https
+access-list outside_in remark v4 and v6 rules interleaved
+access-list outside_in extended permit tcp any host 10.0.0.10 eq www
+access-list outside_in extended permit tcp host 2001:db8::1 host 10.0.0.20 eq https
+access-list outside_in extended permit tcp object-group V6WIDE any object-group WEB
+access-list outside_in extended permit tcp object-group V6HOSTS any eq www
+access-list outside_in extended permit tcp host 2001:db8:1::5 any eq www
+access-list outside_in extended permit tcp any host 10.0.0.20 range 440 450
+access-list outside_in extended permit udp any host 2001:db8::53 eq domain
+access-list outside_in extended permit udp any host 2001:db8::53 eq domain
+access-list outside_in extended permit tcp 10.1.0.0 255.255.0.0 host 2001:db8::99 eq 22
+access-list outside_in extended permit tcp host 2001:db8::1 host 2001:db8::2 eq 22
+access-list outside_in extended permit tcp object-group V6WIDE object-group V6WIDE eq 22
+access-list outside_in extended permit udp any any eq domain
+access-list outside_in extended deny ip any any
+access-list inside_in extended permit ip host fe80::1 any
+access-list inside_in extended permit tcp 10.0.0.0 255.0.0.0 any eq www
+access-list inside_in extended deny ip any any
+access-group outside_in in interface outside
+access-group inside_in in interface inside
 '''
 
 

@@ -42,6 +42,7 @@ typedef struct {
   const uint64_t *src_len, *dst_len; /* IPy len(): addresses in the network */
   const uint32_t *sp_off, *sp_len, *dp_off, *dp_len;
   const int32_t *ports;
+  const uint64_t *src6, *dst6; /* IPv6 sides (v4* = 0): ip hi, ip lo, last hi, last lo per rule */
 } rules_t;
 
 static int contains(const rules_t *R, uint32_t g, uint32_t proto, uint32_t src, uint32_t dst, uint32_t sp,
@@ -67,7 +68,8 @@ void rsa_oracle_classify(uint64_t n, const int32_t *list_of, const uint32_t *pro
                          const uint64_t *dst_len, const uint32_t *sp_off, const uint32_t *sp_len,
                          const uint32_t *dp_off, const uint32_t *dp_len, const int32_t *ports, int32_t *gid_out,
                          uint64_t *evals_out) {
-  rules_t R = {action, proto, v4src, v4dst, rsrc, rdst, src_len, dst_len, sp_off, sp_len, dp_off, dp_len, ports};
+  rules_t R = {action, proto, v4src, v4dst, rsrc, rdst, src_len, dst_len, sp_off, sp_len, dp_off, dp_len, ports,
+               NULL, NULL};
   uint64_t evals = 0;
   /* lines are independent (one mapper call each): spread them over the host's
    * cores; each line is still the reference's sequential first-match scan */
@@ -206,14 +208,32 @@ done:
 /* preprosess_access_lists.py:508-521 over rules [beg, end): cover[k] = the first
  * j in [beg, beg + k) with rule (beg + k) in rule j (FirewallRule.__contains__,
  * firewallrule.py:128-174, rule vs rule), or -1.  A plain double loop. */
+typedef unsigned __int128 u128;
+static u128 w128(const uint64_t *a, int k) { return ((u128)a[k] << 64) | a[k + 1]; }
+
+/* IPv6 network b (rule i) inside network a (rule j): IPy's
+ * b.ip >= a.ip and b's last address <= a's last address */
+static int in6(const uint64_t *A, uint32_t j, uint32_t i) {
+  return w128(A, 4 * i) >= w128(A, 4 * j) && w128(A, 4 * i + 2) <= w128(A, 4 * j + 2);
+}
+
 static int rule_in_rule(const rules_t *R, uint32_t j, uint32_t i) {
   if (R->action[j] != R->action[i]) return 0;                   /* :146 */
   if (R->proto[j] != 0 && R->proto[j] != R->proto[i]) return 0; /* :150 */
-  if (!R->v4src[j] || !R->v4src[i] || !R->v4dst[j] || !R->v4dst[i]) return 0;
-  if (!((uint64_t)R->src[i] >= R->src[j] && (uint64_t)R->src[i] + R->src_len[i] <= (uint64_t)R->src[j] + R->src_len[j]))
-    return 0;                                                    /* :154 */
-  if (!((uint64_t)R->dst[i] >= R->dst[j] && (uint64_t)R->dst[i] + R->dst_len[i] <= (uint64_t)R->dst[j] + R->dst_len[j]))
-    return 0;                                                    /* :158 */
+  /* IPy: an address of another version is never contained */
+  if (R->v4src[j] != R->v4src[i] || R->v4dst[j] != R->v4dst[i]) return 0;
+  if (R->v4src[i]) {
+    if (!((uint64_t)R->src[i] >= R->src[j] && (uint64_t)R->src[i] + R->src_len[i] <= (uint64_t)R->src[j] + R->src_len[j]))
+      return 0;                                                  /* :154 */
+  } else if (!in6(R->src6, j, i)) {
+    return 0;
+  }
+  if (R->v4dst[i]) {
+    if (!((uint64_t)R->dst[i] >= R->dst[j] && (uint64_t)R->dst[i] + R->dst_len[i] <= (uint64_t)R->dst[j] + R->dst_len[j]))
+      return 0;                                                  /* :158 */
+  } else if (!in6(R->dst6, j, i)) {
+    return 0;
+  }
   const int32_t *sj = R->ports + R->sp_off[j], *si = R->ports + R->sp_off[i];
   if (!(R->sp_len[j] == 1 && sj[0] == -1))                      /* :162-165 */
     for (uint32_t q = 0; q < R->sp_len[i]; ++q)
@@ -228,8 +248,10 @@ static int rule_in_rule(const rules_t *R, uint32_t j, uint32_t i) {
 void rsa_oracle_shadow(uint32_t beg, uint32_t end, const uint8_t *action, const uint8_t *proto, const uint8_t *v4src,
                        const uint8_t *v4dst, const uint32_t *rsrc, const uint32_t *rdst, const uint64_t *src_len,
                        const uint64_t *dst_len, const uint32_t *sp_off, const uint32_t *sp_len, const uint32_t *dp_off,
-                       const uint32_t *dp_len, const int32_t *ports, int32_t *cover) {
-  rules_t R = {action, proto, v4src, v4dst, rsrc, rdst, src_len, dst_len, sp_off, sp_len, dp_off, dp_len, ports};
+                       const uint32_t *dp_len, const int32_t *ports, const uint64_t *src6, const uint64_t *dst6,
+                       int32_t *cover) {
+  rules_t R = {action, proto, v4src, v4dst, rsrc, rdst, src_len, dst_len, sp_off, sp_len, dp_off, dp_len, ports,
+               src6, dst6};
 #pragma omp parallel for schedule(dynamic, 16)
   for (int64_t k = 0; k < (int64_t)(end - beg); ++k) {
     const uint32_t i = beg + (uint32_t)k;

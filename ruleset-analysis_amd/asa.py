@@ -54,7 +54,7 @@ from .acldb import AclDB
 from .ipaddr import IP
 from .py2dict import iteration_order
 from .py2text import py2_int, py2_split, py2_strip
-from .rulecols import RuleColumns
+from .rulecols import FAM_DST6, FAM_SRC6, Nets6, RuleColumns
 
 __all__ = ['PORT_NAMES', 'ICMP_TYPES', 'parse_port_spec', 'parse_acl_entry', 'find_all_children', 'build_db']
 
@@ -209,17 +209,18 @@ def _descendants(lines, i, ind):
         j += 1
 
 
-def _addr(text, side):
-    """FirewallRule's address conversion (firewallrule.py:80-92) -> (ip, prefix length)."""
+def _addr(text, side, nets6):
+    """FirewallRule's address conversion (firewallrule.py:80-92) -> (value,
+    prefix length, IPv6?); an IPv6 network's value is its ``nets6`` id."""
     if text == 'any':
-        return 0, 0
+        return 0, 0, 0
     try:
         ip = IP(text)
     except ValueError as e:
         raise ValueError('argument "%s" must be a valid IP address or network. Error: %s' % (side, e))
     if ip._ipversion != 4:
-        raise NotImplementedError('IPv6 rules are not supported by the columnar rule store: %r' % text)
-    return int(ip.ip), int(ip._prefixlen)
+        return nets6(text), int(ip._prefixlen), 1
+    return int(ip.ip), int(ip._prefixlen), 0
 
 
 class _Acl(object):
@@ -230,6 +231,7 @@ class _Acl(object):
         self.n = 0
         self.proto_names = []
         self.originals, self.comments, self.comment_ids, self.rulenums = [], [], {}, []
+        self.nets6 = Nets6()
 
     def add(self, allow, protocol, original, src, dst, sport, dport, comments, rulenum):
         # nesting dport -> dst -> sport -> src (:256-276); an empty port list is NO_PORT
@@ -237,8 +239,8 @@ class _Acl(object):
             return 0                      # no FirewallRule is built (no validation either)
         dp = np.array(dport if dport else [NO_PORT], np.int64)
         sp = np.array(sport if sport else [NO_PORT], np.int64)
-        s = [_addr(a, 'src') for a in src]
-        d = [_addr(a, 'dst') for a in dst]
+        s = [_addr(a, 'src', self.nets6) for a in src]
+        d = [_addr(a, 'dst', self.nets6) for a in dst]
         if protocol not in self.proto_names:
             self.proto_names.append(protocol)
         pid = self.proto_names.index(protocol)
@@ -248,10 +250,12 @@ class _Acl(object):
         di = np.tile(np.repeat(np.arange(D), P * S), Q)
         pi = np.tile(np.repeat(np.arange(P), S), Q * D)
         si = np.tile(np.arange(S), Q * D * P)
-        s_ip = np.array([a for a, _ in s], np.uint32)
-        s_len = np.array([b for _, b in s], np.uint8)
-        d_ip = np.array([a for a, _ in d], np.uint32)
-        d_len = np.array([b for _, b in d], np.uint8)
+        s_ip = np.array([a for a, _, _ in s], np.uint32)
+        s_len = np.array([b for _, b, _ in s], np.uint8)
+        s_v6 = np.array([v for _, _, v in s], np.uint8)
+        d_ip = np.array([a for a, _, _ in d], np.uint32)
+        d_len = np.array([b for _, b, _ in d], np.uint8)
+        d_v6 = np.array([v for _, _, v in d], np.uint8)
         self.originals.append(original)
         key = id(comments)
         if key not in self.comment_ids:
@@ -264,18 +268,20 @@ class _Acl(object):
             'sport': sp[pi].astype(np.int32), 'dport': dp[qi].astype(np.int32),
             'orig': np.full(m, len(self.originals) - 1, np.int32),
             'comment': np.full(m, self.comment_ids[key], np.int32),
-            'rulenum': np.full(m, len(self.rulenums) - 1, np.int32)})
+            'rulenum': np.full(m, len(self.rulenums) - 1, np.int32),
+            'fam': s_v6[si] * FAM_SRC6 | d_v6[di] * FAM_DST6})
         self.n += m
         return m
 
     def build(self):
         cols = {}
         for k in ('action', 'proto', 'src', 'src_len', 'dst', 'dst_len', 'sport', 'dport', 'orig', 'comment',
-                  'rulenum'):
+                  'rulenum', 'fam'):
             cols[k] = np.concatenate([p[k] for p in self.parts]) if self.parts else np.zeros(0)
         return RuleColumns(cols['action'], cols['proto'], self.proto_names, cols['src'], cols['src_len'], cols['dst'],
                            cols['dst_len'], cols['sport'], cols['dport'], cols['orig'], self.originals or [''],
-                           cols['comment'], self.comments or [[]], cols['rulenum'], self.rulenums or [-1])
+                           cols['comment'], self.comments or [[]], cols['rulenum'], self.rulenums or [-1],
+                           fam=cols['fam'], nets6=self.nets6.texts)
 
 
 def _exit(log, *msgs):

@@ -2908,7 +2908,9 @@ __device__ __forceinline__ bool rule_contains(const rsa_shadow_rule& a, const rs
                                               const int32_t* __restrict__ ports) {
   if (a.action != b.action) return false;                         // :146
   if (a.proto != 0 && a.proto != b.proto) return false;           // :150
-  if (!a.v4 || !b.v4) return false;                               // IPy: another version is never contained
+  // family codes (1 both IPv4, 3..5 IPv6 sides in order-isomorphic
+  // interval codes): IPy never contains an address of another version
+  if (!a.v4 || a.v4 != b.v4) return false;
   const unsigned long long as = a.src_lo, bs = b.src_lo, ad = a.dst_lo, bd = b.dst_lo;
   if (bs < as || bs + b.src_span > as + a.src_span) return false;   // :154 other.src in self.src
   if (bd < ad || bd + b.dst_span > ad + a.dst_span) return false;   // :158

@@ -38,7 +38,7 @@ from .firewallrule import FirewallRule
 from .ipaddr import IP
 from .py2dict import iteration_order
 from .py2text import py2_int, py2_lower, py2_split, py2_strip
-from .rulecols import RuleColumns
+from .rulecols import FAM_DST6, FAM_SRC6, Nets6, RuleColumns
 
 __all__ = ['parse_config', 'build_db', 'expand_addr', 'expand_service']
 
@@ -174,6 +174,7 @@ class _AclBuilder(object):
         self.n = 0
         self.originals, self.comments, self.rulenums = [], [], []
         self.proto_names = []
+        self.nets6 = Nets6()
 
     def proto_id(self, name):
         if name not in self.proto_names:
@@ -202,16 +203,17 @@ class _AclBuilder(object):
         v = len(sv_proto)
         if v == 0:
             return
-        sa = [IP(s) for s in srcs]
-        da = [IP(d) for d in dsts]
-        for a in sa + da:
-            if a._ipversion != 4:
-                raise NotImplementedError('IPv6 address objects are not supported by the columnar rule store')
+        # an IPv6 subnet keeps its rules' positions; its value is a nets6 id
+        # (rulecols: it never matches an IPv4 connection)
+        sa = [(t, IP(t)) for t in srcs]
+        da = [(t, IP(t)) for t in dsts]
         S, D = len(sa), len(da)
-        s_ip = np.array([a.ip for a in sa], np.uint32)
-        s_len = np.array([a._prefixlen for a in sa], np.uint8)
-        d_ip = np.array([a.ip for a in da], np.uint32)
-        d_len = np.array([a._prefixlen for a in da], np.uint8)
+        s_ip = np.array([a.ip if a._ipversion == 4 else self.nets6(t) for t, a in sa], np.uint32)
+        s_len = np.array([a._prefixlen for _t, a in sa], np.uint8)
+        s_v6 = np.array([a._ipversion != 4 for _t, a in sa], np.uint8)
+        d_ip = np.array([a.ip if a._ipversion == 4 else self.nets6(t) for t, a in da], np.uint32)
+        d_len = np.array([a._prefixlen for _t, a in da], np.uint8)
+        d_v6 = np.array([a._ipversion != 4 for _t, a in da], np.uint8)
         si = np.repeat(np.arange(S), D * v)
         di = np.tile(np.repeat(np.arange(D), v), S)
         vi = np.tile(np.arange(v), S * D)
@@ -225,17 +227,19 @@ class _AclBuilder(object):
             'sport': sv_sport[vi].astype(np.int32), 'dport': sv_dport[vi].astype(np.int32),
             'orig': np.full(m, len(self.originals) - 1, np.int32),
             'comment': np.full(m, len(self.comments) - 1, np.int32),
-            'rulenum': np.full(m, len(self.rulenums) - 1, np.int32)})
+            'rulenum': np.full(m, len(self.rulenums) - 1, np.int32),
+            'fam': s_v6[si] * FAM_SRC6 | d_v6[di] * FAM_DST6})
         self.n += m
 
     def build(self):
         cols = {}
         for k in ('action', 'proto', 'src', 'src_len', 'dst', 'dst_len', 'sport', 'dport', 'orig', 'comment',
-                  'rulenum'):
+                  'rulenum', 'fam'):
             cols[k] = np.concatenate([p[k] for p in self.parts]) if self.parts else np.zeros(0)
         return RuleColumns(cols['action'], cols['proto'], self.proto_names, cols['src'], cols['src_len'], cols['dst'],
                            cols['dst_len'], cols['sport'], cols['dport'], cols['orig'], self.originals or [''],
-                           cols['comment'], self.comments or [[]], cols['rulenum'], self.rulenums or [-1])
+                           cols['comment'], self.comments or [[]], cols['rulenum'], self.rulenums or [-1],
+                           fam=cols['fam'], nets6=self.nets6.texts)
 
 
 def build_db(text, timestamp=0.0, firewalls=None, accesslists=None, log=None, resolve=socket.gethostbyname_ex):

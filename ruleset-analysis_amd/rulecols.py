@@ -11,21 +11,43 @@ it is a drop-in for the ``'rules'`` list of ``accesslists.db``
 have stored, with ``ruleindex = i``), and ``CompiledRules`` lowers it to
 candidate-list entries without touching Python objects (``lower``).
 
-Every stored rule has an IPv4 source and destination and one port (or
-``NO_PORT``) per side — the shape both preprocessors produce for tcp/udp/ip
-rules (SURVEY.md trap 3).
+Every stored rule has one port (or ``NO_PORT``) per side -- the shape both
+preprocessors produce for tcp/udp/ip rules (SURVEY.md trap 3) -- and an IPv4
+or IPv6 network per address side.  IPv6 sides are rare and are kept aside:
+``fam`` has bit 0 (source) / bit 1 (destination) set, the side's ``src``/
+``dst`` column holds an index into ``nets6`` (the address text the rule was
+built from) and its ``*_len`` the prefix length.  Such a rule keeps its list
+position (its ``ruleindex``) but never matches the IPv4 connections of a log:
+IPy answers False for an address of another version
+(``firewallrule.py:82,91,154,158``).
 """
 
 import numpy as np
 
 from .firewallrule import FirewallRule
 
-__all__ = ['RuleColumns']
+__all__ = ['RuleColumns', 'FAM_SRC6', 'FAM_DST6', 'Nets6']
+
+FAM_SRC6, FAM_DST6 = 1, 2
 
 
 def _dotted(v):
     v = int(v)
     return '%d.%d.%d.%d' % ((v >> 24) & 255, (v >> 16) & 255, (v >> 8) & 255, v & 255)
+
+
+class Nets6(object):
+    """Interned IPv6 address texts of one rule store (``RuleColumns.nets6``)."""
+
+    def __init__(self):
+        self.texts, self.ids = [], {}
+
+    def __call__(self, text):
+        k = self.ids.get(text)
+        if k is None:
+            k = self.ids[text] = len(self.texts)
+            self.texts.append(text)
+        return k
 
 
 class RuleColumns(object):
@@ -34,10 +56,11 @@ class RuleColumns(object):
     action bool; proto uint8 (index into ``proto_names``); src/dst uint32 network
     address and uint8 prefix length; sport/dport int32 (-1 = NO_PORT); orig,
     comment, rulenum int32 indices into ``originals``, ``comments``,
-    ``rulenums``."""
+    ``rulenums``; fam uint8 (FAM_SRC6 / FAM_DST6: that side is the IPv6
+    network ``nets6[src or dst]`` of prefix length ``*_len``)."""
 
     def __init__(self, action, proto, proto_names, src, src_len, dst, dst_len, sport, dport, orig, originals,
-                 comment=None, comments=None, rulenum=None, rulenums=None):
+                 comment=None, comments=None, rulenum=None, rulenums=None, fam=None, nets6=None):
         n = len(action)
         self.action = np.asarray(action, bool)
         self.proto = np.asarray(proto, np.uint8)
@@ -54,8 +77,10 @@ class RuleColumns(object):
         self.comments = [[]] if comments is None else list(comments)
         self.rulenum = np.zeros(n, np.int32) if rulenum is None else np.asarray(rulenum, np.int32)
         self.rulenums = [-1] if rulenums is None else list(rulenums)
+        self.fam = np.zeros(n, np.uint8) if fam is None else np.asarray(fam, np.uint8)
+        self.nets6 = [] if nets6 is None else list(nets6)
         for a in (self.proto, self.src, self.src_len, self.dst, self.dst_len, self.sport, self.dport, self.orig,
-                  self.comment, self.rulenum):
+                  self.comment, self.rulenum, self.fam):
             if len(a) != n:
                 raise ValueError('rule columns differ in length')
         self._cache = {}
@@ -77,8 +102,15 @@ class RuleColumns(object):
         r = self._cache.get(i)
         if r is None:
             sp, dp = int(self.sport[i]), int(self.dport[i])
-            src = 'any' if self.src_len[i] == 0 and self.src[i] == 0 else self._addr(self.src[i], self.src_len[i])
-            dst = 'any' if self.dst_len[i] == 0 and self.dst[i] == 0 else self._addr(self.dst[i], self.dst_len[i])
+            f = int(self.fam[i])
+            if f & FAM_SRC6:
+                src = self.nets6[int(self.src[i])]
+            else:
+                src = 'any' if self.src_len[i] == 0 and self.src[i] == 0 else self._addr(self.src[i], self.src_len[i])
+            if f & FAM_DST6:
+                dst = self.nets6[int(self.dst[i])]
+            else:
+                dst = 'any' if self.dst_len[i] == 0 and self.dst[i] == 0 else self._addr(self.dst[i], self.dst_len[i])
             r = FirewallRule(bool(self.action[i]), self.proto_names[self.proto[i]], self.originals[self.orig[i]], src,
                              dst, [sp], [dp], comments=self.comments[self.comment[i]],
                              rulenum=self.rulenums[self.rulenum[i]], ruleindex=i)
@@ -109,7 +141,8 @@ class RuleColumns(object):
             raise IndexError('candidate index out of range')
         names = self.proto_names
         ok_proto = np.array([nm == 'ip' or nm == proto for nm in names], bool)
-        keep = self.action[idx] & ok_proto[self.proto[idx]]
+        # an IPv6 side never contains the connection's IPv4 address
+        keep = self.action[idx] & ok_proto[self.proto[idx]] & (self.fam[idx] == 0)
         sp = self.sport[idx].astype(np.int64)
         dp = self.dport[idx].astype(np.int64)
         for col, v in ((sp, oor[0]), (dp, oor[1])):

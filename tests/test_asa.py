@@ -144,6 +144,8 @@ def _traffic_lines(db, host, n, seed):
         acl = sorted(ifc_of)[k % len(ifc_of)]
         rules = db.accesslists[host][acl]['rules']
         i = int(rng.integers(0, len(rules)))
+        while rules.fam[i]:               # IPv6 rules match no IPv4 connection: draw from the others
+            i = int(rng.integers(0, len(rules)))
         proto = rules.proto_names[rules.proto[i]]
         proto = proto if proto in ('tcp', 'udp') else 'tcp'
         sl, dl = int(rules.src_len[i]), int(rules.dst_len[i])
@@ -178,6 +180,49 @@ def test_gpu_fused_job_on_asa_db_equals_oracle(engine):
     got, _ = analyze_text([(info['hostname'], ''.join(lines).encode('latin-1'))], db, cap=20, engine=engine)
     assert got == want
     assert sum(1 for l in got if l.startswith('Total number of hits:')) > 20
+
+
+def test_ipv6_rules_keep_positions_and_never_match():
+    """asa_ipv6: IPv6 rules sit between IPv4 rules with their ruleindex and
+    are absent from every compiled candidate list (IPy never contains an IPv4
+    address in an IPv6 network)."""
+    from ruleset_analysis_amd.compile import CompiledRules
+    text, _sha, _summary, _shadow = _case('asa_ipv6')
+    db = asa.build_db(text)
+    rules = db.accesslists['v6-fw']['outside_in']['rules']
+    six = np.flatnonzero(rules.fam)
+    assert len(six) and six[0] == 1 and len(six) < len(rules)
+    assert str(rules[1].src) == '2001:db8::1' and rules[1].ruleindex == 1
+    comp = CompiledRules(db)
+    comp.ensure_lists()
+    gids = set()
+    for lst in comp._lists:
+        gids.update(int(g) for g in lst['gid'])
+    base = comp.base[('v6-fw', 'outside_in')]
+    assert not gids & {base + int(i) for i in six}
+    assert base + 0 in gids
+
+
+@pytest.mark.gpu
+def test_gpu_fused_job_on_ipv6_db_equals_oracle(engine):
+    """The fused job over the asa_ipv6 DB (IPv6 rules between IPv4 ones) gives
+    the oracle's report: gids past an IPv6 rule keep their ruleindex."""
+    from oracle.crosscheck_2to3 import oracle_db
+    from oracle import pipeline as op
+    from ruleset_analysis_amd import acldb
+    from ruleset_analysis_amd.pipeline import analyze_text
+    text, _sha, _summary, _shadow = _case('asa_ipv6')
+    db = asa.build_db(text)
+    lines = _traffic_lines(db, 'v6-fw', 5000, 9)
+    dbj = acldb.to_json_obj(db)
+    for hs in dbj['accesslists'].values():
+        for e in hs.values():
+            e['protocols'] = {p: [int(x) for x in v] for p, v in e['protocols'].items()}
+    acls, fws = oracle_db(json.loads(json.dumps(dbj)))
+    _m, _s, want, _b = op.run_pipeline(''.join(lines), 'v6-fw', acls, fws, cap=50)
+    got, _ = analyze_text([('v6-fw', ''.join(lines).encode('latin-1'))], db, cap=50, engine=engine)
+    assert got == want
+    assert sum(1 for l in got if l.startswith('Total number of hits:')) >= 4
 
 
 @pytest.mark.gpu

@@ -48,6 +48,43 @@ def test_shadow_table_columns_equal_objects():
     assert np.array_equal(cols['proto'] == 0, objs['proto'] == 0)
 
 
+def test_laminar_codes_keep_containment():
+    """IPv6 prefix networks -> 32-bit intervals: a contains b exactly when
+    a's interval holds b's (random nested and disjoint prefixes)."""
+    from ruleset_analysis_amd.shadow import laminar_codes
+    rng = np.random.default_rng(11)
+    nets = []
+    for _ in range(400):
+        plen = int(rng.integers(0, 129))
+        base = int(rng.integers(0, 4)) << 126 | int(rng.integers(0, 1 << 62)) << 64 | int(rng.integers(0, 1 << 63))
+        nets.append((base >> (128 - plen) << (128 - plen) if plen else 0, plen))
+    nets += [(0, 0), nets[3], (nets[5][0], 128)]
+    codes = laminar_codes(nets)
+    last = lambda t: t[0] + (1 << (128 - t[1])) - 1
+    for a in set(nets):
+        for b in set(nets):
+            inside = b[0] >= a[0] and last(b) <= last(a)
+            (la, sa), (lb, sb) = codes[a], codes[b]
+            assert inside == (lb >= la and lb + sb <= la + sa), (a, b)
+
+
+def test_shadow_table_ipv6_columns_equal_objects():
+    """asa_ipv6: the columnar rows (family codes, interval codes of the IPv6
+    sides) equal the rows of the materialised FirewallRule objects."""
+    import os
+    from conftest import ROOT
+    from ruleset_analysis_amd import asa
+    with open(os.path.join(ROOT, 'tests', 'golden_asa', 'asa_ipv6', 'config.txt')) as f:
+        db = asa.build_db(f.read())
+    for acl, e in db.accesslists['v6-fw'].items():
+        rules = e['rules']
+        cols = shadow_table(rules)
+        objs = shadow_table([rules[i] for i in range(len(rules))])
+        for f in ('src_lo', 'src_span', 'dst_lo', 'dst_span', 'sport', 'dport', 'action', 'v4'):
+            assert np.array_equal(cols[f], objs[f]), (acl, f)
+    assert set(shadow_table(db.accesslists['v6-fw']['outside_in']['rules'])['v4'].tolist()) == {1, 3, 4, 5}
+
+
 @pytest.mark.gpu
 def test_gpu_shadow_equals_oracle_asa(engine):
     dbj, info = synth.make_db(92, 10000, interfaces=('outside', 'partner'))
