@@ -654,12 +654,14 @@ def rank_main(args, rank, world, local):
         }
         if world == 1 and not args.no_cpu_baseline:
             res['cpu_baseline'] = cpu_baseline(wl)
-            # SURVEY.md 8d's config-1 job (single pipeline and the Hadoop-like
-            # variant), measured by --cpu-baseline-only on the GPU box's host and
-            # committed (it takes minutes, too long for every bench run)
-            c1 = read_profile('config1_cpu_baseline.json')
-            if c1 is not None:
-                c1['source'] = 'profiles/config1_cpu_baseline.json (bench.py --cpu-baseline-only)'
+            if not args.no_config1:
+                # SURVEY.md 8d's config-1 job (BASELINE config 1: 1M lines, 200
+                # rules; the single pipeline and the Hadoop-like variant), run
+                # here on this host as real processes (~30 s)
+                t = time.perf_counter()
+                c1 = reference_pipeline_baseline(n_lines=args.baseline_lines, procs=args.baseline_procs or None)
+                c1['source'] = 'measured in this bench run (bench.py reference_pipeline_baseline)'
+                c1['measure_s'] = time.perf_counter() - t
                 res['cpu_baseline']['config1'] = c1
         print(json.dumps(res), flush=True)
     if dist is not None:
@@ -897,6 +899,8 @@ def parse_args(argv=None):
     ap.add_argument('--dump', default='', help='TESTING: rank 0 writes the final result (npz) here')
     ap.add_argument('--no-check', action='store_true', help='skip the untimed full-size checks')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-config1', action='store_true',
+                    help='skip the config-1 CPU pipeline (1M lines) that the default line measures beside the GPU job')
     ap.add_argument('--cpu-baseline-only', action='store_true',
                     help='run only the SURVEY.md 8d CPU baseline (config 1 through the restated reference job)')
     ap.add_argument('--baseline-lines', type=int, default=1_000_000)

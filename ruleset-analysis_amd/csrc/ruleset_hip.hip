@@ -1657,10 +1657,28 @@ __global__ __launch_bounds__(1024) void k_part_hist(const uint16_t* __restrict__
   for (uint32_t r = threadIdx.x; r < n_regions; r += blockDim.x) hist[(size_t)r * n_tiles + tile] = hcount[r];
 }
 
+#ifndef RSA_SCATTER_PF
+#define RSA_SCATTER_PF 1   // k_part_scatter: the next trip's loads issued before this trip's stores
+#endif
+
+// A window group's counts with one 16-B load (wcnt is padded by kPartW words
+// and w0 is a multiple of kPartW): no per-window branches.
+__device__ __forceinline__ WinGroup win_group4(const uint32_t* __restrict__ wcnt, unsigned long long w0,
+                                               unsigned long long wend) {
+  const uint4 c = *reinterpret_cast<const uint4*>(wcnt + w0);
+  WinGroup g;
+  g.p1 = w0 < wend ? c.x : 0u;
+  g.p2 = g.p1 + (w0 + 1 < wend ? c.y : 0u);
+  g.p3 = g.p2 + (w0 + 2 < wend ? c.z : 0u);
+  g.tot = g.p3 + (w0 + 3 < wend ? c.w : 0u);
+  return g;
+}
+
 __global__ __launch_bounds__(1024) void k_part_scatter(const Rec* __restrict__ recs, const uint16_t* __restrict__ regs,
                                                        const uint32_t* __restrict__ wcnt, unsigned long long n,
                                                        uint32_t n_regions, uint32_t n_tiles, uint32_t tile_len,
-                                                       const uint32_t* __restrict__ offs, Rec* __restrict__ out) {
+                                                       const uint32_t* __restrict__ offs, Rec* __restrict__ out,
+                                                       Rec* __restrict__ junk) {
   __shared__ uint32_t cur[kMaxRegions];
   const uint32_t tile = blockIdx.x;
   for (uint32_t r = threadIdx.x; r < n_regions; r += blockDim.x) cur[r] = offs[(size_t)r * n_tiles + tile];
@@ -1671,6 +1689,68 @@ __global__ __launch_bounds__(1024) void k_part_scatter(const Rec* __restrict__ r
   const uint32_t lane = __lane_id(), nwv = blockDim.x >> 6;
   const unsigned long long wstep = (unsigned long long)nwv * kPartW;
   unsigned long long w0 = beg / kWin + (threadIdx.x >> 6) * kPartW;
+#if RSA_SCATTER_PF
+  // software pipeline over the wave's trips (a trip = two records per lane of
+  // one window group; a group holds <= 256 records, so <= 2 trips): the
+  // window counts are read a group ahead and the records a trip ahead, both
+  // before the current trip's scattered stores, so the waits for those loads
+  // do not include the stores' completion (vmcnt counts stores too, in issue
+  // order).  For that every load and store is unconditional: invalid lanes
+  // read the group's first slot and write a junk record of their own lane.
+  // The records travel as plain 16-B vectors (region = the record's last
+  // word: the 2-B region array is not read here).
+  const uint4* R4 = reinterpret_cast<const uint4*>(recs);
+  uint4* O4 = reinterpret_cast<uint4*>(out);
+  uint4* J4 = reinterpret_cast<uint4*>(junk) + 2 * lane;
+  const WinGroup zero = {0, 0, 0, 0};
+  const unsigned long long wlast = beg / kWin;   // an in-range group start for clamped loads
+  WinGroup g = w0 < wend ? win_group4(wcnt, w0, wend) : zero;
+  uint4 c1 = *reinterpret_cast<const uint4*>(wcnt + (w0 + wstep < wend ? w0 + wstep : wlast));
+  uint32_t qb = 0;
+  const unsigned long long wl = w0 < wend ? w0 : wlast;
+  bool v0 = lane < g.tot, v1 = lane + kWin < g.tot;
+  unsigned long long j0 = v0 ? win_slot(g, wl, lane) : wl * kWin;
+  unsigned long long j1 = v1 ? win_slot(g, wl, lane + kWin) : wl * kWin;
+  uint4 a0 = R4[2 * j0], b0 = R4[2 * j0 + 1], a1 = R4[2 * j1], b1 = R4[2 * j1 + 1];
+  while (w0 < wend) {
+    const bool adv = qb + 2 * kWin >= g.tot;   // wave-uniform: the next trip is the next window group's first
+    const unsigned long long nw0 = adv ? w0 + wstep : w0;
+    WinGroup ng = g;
+    if (adv) {
+      const unsigned long long w1 = w0 + wstep;
+      ng.p1 = w1 < wend ? c1.x : 0u;
+      ng.p2 = ng.p1 + (w1 + 1 < wend ? c1.y : 0u);
+      ng.p3 = ng.p2 + (w1 + 2 < wend ? c1.z : 0u);
+      ng.tot = ng.p3 + (w1 + 3 < wend ? c1.w : 0u);
+    }
+    const uint32_t nqb = adv ? 0u : qb + 2 * kWin;
+    // the counts of the group after nw0 (used next iteration)
+    const uint4 c2 = *reinterpret_cast<const uint4*>(wcnt + (nw0 + wstep < wend ? nw0 + wstep : wlast));
+    const unsigned long long nwl = nw0 < wend ? nw0 : wlast;
+    const bool nv0 = nqb + lane < ng.tot, nv1 = nqb + lane + kWin < ng.tot;
+    const unsigned long long nj0 = nv0 ? win_slot(ng, nwl, nqb + lane) : nwl * kWin;
+    const unsigned long long nj1 = nv1 ? win_slot(ng, nwl, nqb + lane + kWin) : nwl * kWin;
+    const uint4 na0 = R4[2 * nj0], nb0 = R4[2 * nj0 + 1], na1 = R4[2 * nj1], nb1 = R4[2 * nj1 + 1];
+    const uint32_t p0 = v0 ? atomicAdd(&cur[b0.w], 1u) : 0u;
+    const uint32_t p1 = v1 ? atomicAdd(&cur[b1.w], 1u) : 0u;
+    uint4* d0 = v0 ? O4 + 2 * (size_t)p0 : J4;
+    uint4* d1 = v1 ? O4 + 2 * (size_t)p1 : J4;
+    d0[0] = a0;
+    d0[1] = b0;
+    d1[0] = a1;
+    d1[1] = b1;
+    a0 = na0;
+    b0 = nb0;
+    a1 = na1;
+    b1 = nb1;
+    v0 = nv0;
+    v1 = nv1;
+    w0 = nw0;
+    g = ng;
+    c1 = c2;
+    qb = nqb;
+  }
+#else
   WinGroup g = w0 < wend ? win_group(wcnt, w0, wend) : WinGroup{0, 0, 0, 0};
   for (; w0 < wend; w0 += wstep) {
     // the next group's window counts are read before this group's records
@@ -1696,6 +1776,7 @@ __global__ __launch_bounds__(1024) void k_part_scatter(const Rec* __restrict__ r
     }
     g = gn;
   }
+#endif
 }
 
 // Exclusive scan of n uint32 (three launches: per-block scan + block sums,
@@ -1784,12 +1865,18 @@ __device__ __forceinline__ unsigned long long readlane64(unsigned long long v, i
 // region, so lanes sharing the key of one of the wave's first live lanes are
 // combined with wave reductions and enter the table as ONE insert (LDS atomics
 // on one address serialise over the lanes).  Wave-uniform call.
+#ifndef RSA_USED_WAVE
+#define RSA_USED_WAVE 1   // k_reduce / k_hot_combine: one LDS add of the wave's new entries
+#endif
+// Returns true for the lane that created a new table entry (the caller counts
+// them into `used` with one LDS atomic per wave: a per-lane add on that one
+// word serialises over the wave's new keys).
 template <int kE, bool kMinOrder>
-__device__ __forceinline__ void lds_agg_insert(unsigned long long (&e_kA)[kE], unsigned long long (&e_kB)[kE],
-                                               unsigned long long (&e_mo)[kE], uint32_t (&e_first)[kE],
-                                               uint32_t (&e_last)[kE], uint32_t (&e_cnt)[kE], uint32_t& used,
-                                               bool have, unsigned long long kA, unsigned long long kB,
-                                               unsigned long long mo, uint32_t first, uint32_t last, uint32_t cnt) {
+__device__ __forceinline__ bool lds_agg_insert_lane(unsigned long long (&e_kA)[kE], unsigned long long (&e_kB)[kE],
+                                                    unsigned long long (&e_mo)[kE], uint32_t (&e_first)[kE],
+                                                    uint32_t (&e_last)[kE], uint32_t (&e_cnt)[kE], bool have,
+                                                    unsigned long long kA, unsigned long long kB, unsigned long long mo,
+                                                    uint32_t first, uint32_t last, uint32_t cnt) {
   unsigned long long pending = __ballot(have);
   for (int att = 0; att < kHotTries && pending; ++att) {
     const int l0 = __builtin_ctzll(pending);
@@ -1820,7 +1907,7 @@ __device__ __forceinline__ void lds_agg_insert(unsigned long long (&e_kA)[kE], u
       }
     }
   }
-  if (!have) return;
+  if (!have) return false;
   const uint32_t h = (uint32_t)mix64(kA ^ (kB * 0x9e3779b97f4a7c15ull));
   uint32_t e = (kE & (kE - 1)) == 0 ? (h & (kE - 1)) : __umulhi(h, (uint32_t)kE);
   while (true) {
@@ -1834,8 +1921,7 @@ __device__ __forceinline__ void lds_agg_insert(unsigned long long (&e_kA)[kE], u
         e_cnt[e] = cnt;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         atomicExch(&e_kB[e], kB);
-        atomicAdd(&used, 1u);
-        return;
+        return true;
       }
       continue;
     }
@@ -1845,10 +1931,26 @@ __device__ __forceinline__ void lds_agg_insert(unsigned long long (&e_kA)[kE], u
       atomicMin(&e_first[e], first);
       atomicMax(&e_last[e], last);
       if (kMinOrder) atomicMin(&e_mo[e], mo);
-      return;
+      return false;
     }
     e = e + 1 == (uint32_t)kE ? 0u : e + 1;
   }
+}
+
+template <int kE, bool kMinOrder>
+__device__ __forceinline__ void lds_agg_insert(unsigned long long (&e_kA)[kE], unsigned long long (&e_kB)[kE],
+                                               unsigned long long (&e_mo)[kE], uint32_t (&e_first)[kE],
+                                               uint32_t (&e_last)[kE], uint32_t (&e_cnt)[kE], uint32_t& used,
+                                               bool have, unsigned long long kA, unsigned long long kB,
+                                               unsigned long long mo, uint32_t first, uint32_t last, uint32_t cnt) {
+  const bool fresh = lds_agg_insert_lane<kE, kMinOrder>(e_kA, e_kB, e_mo, e_first, e_last, e_cnt, have, kA, kB, mo,
+                                                        first, last, cnt);
+#if RSA_USED_WAVE
+  const unsigned long long fm = __ballot(fresh);
+  if (fm && (int)__lane_id() == __builtin_ctzll(fm)) atomicAdd(&used, (uint32_t)__popcll(fm));
+#else
+  if (fresh) atomicAdd(&used, 1u);
+#endif
 }
 
 // A hot region's pre-combined records (k_hot_combine): one per key and
@@ -3056,6 +3158,7 @@ struct rsa_ctx {
   // on-chip shuffle of pass 1b: records, their region-sorted copy, histograms
   void* d_recs = nullptr;
   void* d_recs2 = nullptr;
+  void* d_junk = nullptr;               // 64 records: the sink of k_part_scatter's invalid lanes
   unsigned long long recs_alloc = 0;
   unsigned long long recs2_alloc = 0;
   uint16_t* d_regs = nullptr;          // region of each record (the histogram pass reads only these)
@@ -3493,7 +3596,7 @@ int prepare_records(rsa_ctx* c, uint64_t m) {
   const uint64_t mw = (m + kWin - 1) / kWin * kWin;
   int rc = ensure_buf(c, reinterpret_cast<Rec**>(&c->d_recs), &c->recs_alloc, mw);
   if (!rc) rc = ensure_buf(c, &c->d_regs, &c->regs_alloc, mw);
-  if (!rc) rc = ensure_buf(c, &c->d_wcnt, &c->wcnt_alloc, mw / kWin);
+  if (!rc) rc = ensure_buf(c, &c->d_wcnt, &c->wcnt_alloc, mw / kWin + kPartW);   // (padded: win_group4)
   return rc;
 }
 
@@ -3598,7 +3701,7 @@ int launch_aggregate(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsig
   rc = exclusive_scan(c, c->d_hist, hl, &total);
   if (rc) return rc;
   k_part_scatter<<<n_tiles, 1024, 0, c->stream>>>(recs, c->d_regs, c->d_wcnt, m, n_regions, n_tiles, tile_len, c->d_hist,
-                                                  sorted);
+                                                  sorted, static_cast<Rec*>(c->d_junk));
   HIPCHK(c, hipGetLastError());
   unsigned long long* st = c->d_starts + (size_t)c->n_segs * (n_regions + 1);
   rc = ensure_hot_ctl(c);
@@ -3785,6 +3888,7 @@ int rsa_ctx_create(int device, rsa_ctx** out) {
     c->cu_count = prop.multiProcessorCount;
   if (hipMalloc(&c->d_flags, 4 * sizeof(unsigned int)) != hipSuccess ||
       hipMalloc(&c->d_cursor, sizeof(unsigned long long)) != hipSuccess ||
+      hipMalloc(&c->d_junk, 64 * sizeof(Rec)) != hipSuccess ||
       hipMalloc(&c->d_used_n, sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(c->d_flags, 0, 4 * sizeof(unsigned int)) != hipSuccess ||
       hipMemset(c->d_used_n, 0, sizeof(unsigned long long)) != hipSuccess) {
@@ -3799,7 +3903,7 @@ int rsa_ctx_destroy(rsa_ctx* c) {
   if (!c) return RSA_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->d_tail, c->d_tail_n, c->d_gscratch, c->d_gh, c->d_stats, c->d_recs, c->d_recs2, c->d_regs, c->d_wcnt, c->d_nrecs, c->d_starts, c->d_hist,
+  void* bufs[] = {c->d_tail, c->d_tail_n, c->d_gscratch, c->d_gh, c->d_stats, c->d_recs, c->d_recs2, c->d_junk, c->d_regs, c->d_wcnt, c->d_nrecs, c->d_starts, c->d_hist,
                   c->d_scan_sums, c->d_occ, c->d_entries, c->d_off,
                   c->d_img, c->d_resid,
                   c->d_slots, c->d_used, c->d_ukey, c->d_used_n, c->d_filter, c->d_packed, c->d_hot, c->d_hot_tasks, c->d_hot_base,
