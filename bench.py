@@ -452,7 +452,8 @@ def rank_main(args, rank, world, local):
     from ruleset_analysis_amd import native
     from ruleset_analysis_amd.dist import EngineBackend, ShardOverflow, merge
     from ruleset_analysis_amd.engine import Engine
-    eng = Engine(local)
+    # --share-gpu (diagnosis: several ranks on one card, gloo): rank -> card rank % cards
+    eng = Engine(local % max(torch.cuda.device_count(), 1) if args.share_gpu else local)
     eng.load_compiled(compiled, index=not args.no_index, prefix=args.prefix, kind=args.index)
     if args.filter_slice:
         eng.set_option(native.RSA_OPT_FILTER_SLICE, args.filter_slice)
@@ -899,6 +900,8 @@ def parse_args(argv=None):
     ap.add_argument('--dump', default='', help='TESTING: rank 0 writes the final result (npz) here')
     ap.add_argument('--no-check', action='store_true', help='skip the untimed full-size checks')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--share-gpu', action='store_true',
+                    help='DIAGNOSIS ONLY: let --gpus exceed the visible cards, ranks sharing them (gloo)')
     ap.add_argument('--no-config1', action='store_true',
                     help='skip the config-1 CPU pipeline (1M lines) that the default line measures beside the GPU job')
     ap.add_argument('--cpu-baseline-only', action='store_true',
@@ -944,8 +947,10 @@ def main():
     if not args.cpu_model:
         import torch
         n_dev = torch.cuda.device_count()   # counts devices without initialising the GPU
-        if world > n_dev:
+        if world > n_dev and not args.share_gpu:
             die('--gpus %d but %d GPU(s) visible' % (world, n_dev))
+        if args.share_gpu and args.backend != 'gloo':
+            die('--share-gpu runs the ranks over gloo (--backend gloo)')
     if world == 1:
         if args.force_dist:
             os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(_free_port()), RANK='0', WORLD_SIZE='1',

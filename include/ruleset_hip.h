@@ -312,6 +312,17 @@ int rsa_emit(rsa_ctx *ctx, rsa_conn_record *d_out, uint64_t max_records, uint64_
  * combine into the pass-2 fields of existing keys). */
 int rsa_table_size(rsa_ctx *ctx, uint64_t *h_n);
 int rsa_export(rsa_ctx *ctx, int which, rsa_conn_record *d_out, uint64_t max_records, uint64_t *h_n);
+/* The same export routed to the owners (the keyed shuffle of
+ * runAnalysis.sh:12,42-56: rules partitioned gid % world, the reducer
+ * partitioning): the records of owner r form segment r of d_out (segments in
+ * owner order, each unordered inside), d_counts[r] (DEVICE, world uint64)
+ * receives its size.  No host round trip: the caller exchanges the device
+ * counts and reads send and receive sizes together.  Requires
+ * RSA_OPT_OWNER_WORLD == world (1..256); this rank's own segment is empty.
+ * Records past max_records are dropped while d_counts keep the true sizes
+ * (the caller compares their sum with its capacity). */
+int rsa_export_routed(rsa_ctx *ctx, int which, uint32_t world, rsa_conn_record *d_out, uint64_t max_records,
+                      uint64_t *d_counts);
 int rsa_import(rsa_ctx *ctx, int which, const rsa_conn_record *d_in, uint64_t n);
 
 /* Profiling counters (collected while RSA_OPT_STATS is on): h_out[0] lines

@@ -2795,6 +2795,38 @@ __device__ __forceinline__ rsa_conn_record make_record(const Slot& s, int which)
 // workgroup iteration reserves the output rows (a per-wave append on the one
 // cursor word serialises there).
 constexpr int kEmitU = 4;
+
+// The emission decision for used-list entry i (k_emit and the routed export):
+// which = -1 (not emitted), 0 (pass-1 aggregates) or 1 (pass-2); the slot is
+// gathered into *sl only for emitted entries.
+__device__ __forceinline__ int emit_select(const Slot* S, const unsigned long long* used,
+                                           const unsigned long long* thresh, int mode, uint32_t owner_world,
+                                           uint32_t owner_rank, const unsigned long long* ukey, unsigned long long i,
+                                           Slot* sl) {
+  const unsigned long long u = used[i];
+  const uint32_t gid = (uint32_t)(u >> 32);
+  // decided from the used list (rule id) and the key copy before the 64 B
+  // slot is gathered: entries of capped rules past the threshold and entries
+  // of other owners are never read
+  if (owner_world && (gid % owner_world == owner_rank) != (mode == 0)) return -1;
+  if (ukey && (mode == 0 || mode == 3)) {
+    const unsigned long long P = thresh[gid];
+    if (P != RSA_NO_THRESHOLD && ukey[i] > P) return -1;
+  }
+  *sl = S[(uint32_t)u];
+  if (mode == 0) {
+    const unsigned long long P = thresh[sl->kB >> 32];
+    if (P == RSA_NO_THRESHOLD) return 0;
+    return sl->min_order <= P ? 1 : -1;
+  }
+  if (mode == 1) return 0;
+  if (mode == 3) {
+    const unsigned long long P = thresh[sl->kB >> 32];
+    return (P == RSA_NO_THRESHOLD || sl->min_order <= P) ? 0 : -1;
+  }
+  return sl->count2 != 0 ? 1 : -1;
+}
+
 __global__ __launch_bounds__(1024) void k_emit(const Slot* S, const unsigned long long* used,
                                                const unsigned long long* n_used_p, unsigned long long slot_cap,
                                                const unsigned long long* thresh, int mode, rsa_conn_record* out,
@@ -2815,34 +2847,7 @@ __global__ __launch_bounds__(1024) void k_emit(const Slot* S, const unsigned lon
 #pragma unroll
     for (int k = 0; k < kEmitU; ++k) {
       const unsigned long long i = base + (unsigned long long)k * blockDim.x + threadIdx.x;
-      which[k] = -1;
-      if (i < n_used) {
-        const unsigned long long u = used[i];
-        const uint32_t gid = (uint32_t)(u >> 32);
-        // decided from the used list (rule id) and the key copy before the
-        // 64 B slot is gathered: entries of capped rules past the threshold
-        // and entries of other owners are never read
-        if (owner_world && (gid % owner_world == owner_rank) != (mode == 0)) {
-          continue;
-        }
-        if (ukey && (mode == 0 || mode == 3)) {
-          const unsigned long long P = thresh[gid];
-          if (P != RSA_NO_THRESHOLD && ukey[i] > P) continue;
-        }
-        sl[k] = S[(uint32_t)u];
-        if (mode == 0) {
-          const unsigned long long P = thresh[sl[k].kB >> 32];
-          if (P == RSA_NO_THRESHOLD) which[k] = 0;
-          else if (sl[k].min_order <= P) which[k] = 1;
-        } else if (mode == 1) {
-          which[k] = 0;
-        } else if (mode == 3) {
-          const unsigned long long P = thresh[sl[k].kB >> 32];
-          if (P == RSA_NO_THRESHOLD || sl[k].min_order <= P) which[k] = 0;
-        } else if (sl[k].count2 != 0) {
-          which[k] = 1;
-        }
-      }
+      which[k] = i < n_used ? emit_select(S, used, thresh, mode, owner_world, owner_rank, ukey, i, &sl[k]) : -1;
       c += which[k] >= 0 ? 1u : 0u;
     }
     uint32_t total;
@@ -2857,6 +2862,69 @@ __global__ __launch_bounds__(1024) void k_emit(const Slot* S, const unsigned lon
       if (pos < max_out) out[pos] = make_record(sl[k], which[k]);
       ++pos;
     }
+  }
+}
+
+// ---- Routed export (multi-GPU merge, the keyed shuffle of runAnalysis.sh:44):
+// the exported records grouped by owner rank gid % world, segment r at the sum
+// of the counts of the owners before it.  Pass 1 (kRoute = false) counts per
+// owner into counts[world] (device); pass 2 computes the segment bases from
+// those counts (each workgroup, world <= kRouteMax) and writes every record at
+// base[owner] + a per-(workgroup, owner) range reserved with one device atomic.
+// The two passes take the same decisions (the table does not change between
+// them).  Records past max_out are dropped; counts hold the true sizes.
+constexpr int kRouteMax = 256;
+template <bool kRoute>
+__global__ __launch_bounds__(1024) void k_emit_route(const Slot* S, const unsigned long long* used,
+                                                     const unsigned long long* n_used_p, unsigned long long slot_cap,
+                                                     const unsigned long long* thresh, int mode, uint32_t world,
+                                                     uint32_t owner_rank, const unsigned long long* ukey,
+                                                     unsigned long long* counts, unsigned long long* cursors,
+                                                     rsa_conn_record* out, unsigned long long max_out) {
+  __shared__ uint32_t cnt[kRouteMax];             // per owner: this group's records (of this iteration, kRoute)
+  __shared__ unsigned long long seg[kRouteMax];   // kRoute: segment base of each owner
+  __shared__ unsigned long long at[kRouteMax];    // kRoute: this iteration's first row of each owner
+  const unsigned long long n_used = *n_used_p < slot_cap ? *n_used_p : slot_cap;
+  const unsigned long long span = (unsigned long long)blockDim.x * kEmitU;
+  for (uint32_t o = threadIdx.x; o < world; o += blockDim.x) {
+    cnt[o] = 0;
+    if (kRoute) {
+      unsigned long long b = 0;
+      for (uint32_t q = 0; q < o; ++q) b += counts[q];
+      seg[o] = b;
+    }
+  }
+  __syncthreads();
+  for (unsigned long long base = (unsigned long long)blockIdx.x * span; base < n_used;
+       base += (unsigned long long)gridDim.x * span) {
+    int which[kEmitU];
+    Slot sl[kEmitU];
+    uint32_t rank[kEmitU];
+#pragma unroll
+    for (int k = 0; k < kEmitU; ++k) {
+      const unsigned long long i = base + (unsigned long long)k * blockDim.x + threadIdx.x;
+      which[k] = i < n_used ? emit_select(S, used, thresh, mode, world, owner_rank, ukey, i, &sl[k]) : -1;
+      rank[k] = which[k] >= 0 ? atomicAdd(&cnt[(uint32_t)(sl[k].kB >> 32) % world], 1u) : 0u;
+    }
+    if (!kRoute) continue;
+    __syncthreads();
+    for (uint32_t o = threadIdx.x; o < world; o += blockDim.x) {
+      const uint32_t c = cnt[o];
+      at[o] = seg[o] + (c ? atomicAdd(&cursors[o], (unsigned long long)c) : 0ull);
+      cnt[o] = 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kEmitU; ++k) {
+      if (which[k] < 0) continue;
+      const unsigned long long pos = at[(uint32_t)(sl[k].kB >> 32) % world] + rank[k];
+      if (pos < max_out) out[pos] = make_record(sl[k], which[k]);
+    }
+  }
+  if (!kRoute) {
+    __syncthreads();
+    for (uint32_t o = threadIdx.x; o < world; o += blockDim.x)
+      if (cnt[o]) atomicAdd(&counts[o], (unsigned long long)cnt[o]);
   }
 }
 
@@ -3159,6 +3227,7 @@ struct rsa_ctx {
   void* d_recs = nullptr;
   void* d_recs2 = nullptr;
   void* d_junk = nullptr;               // 64 records: the sink of k_part_scatter's invalid lanes
+  unsigned long long* d_route_cur = nullptr;   // rsa_export_routed: per-owner cursors
   unsigned long long recs_alloc = 0;
   unsigned long long recs2_alloc = 0;
   uint16_t* d_regs = nullptr;          // region of each record (the histogram pass reads only these)
@@ -3903,7 +3972,7 @@ int rsa_ctx_destroy(rsa_ctx* c) {
   if (!c) return RSA_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->d_tail, c->d_tail_n, c->d_gscratch, c->d_gh, c->d_stats, c->d_recs, c->d_recs2, c->d_junk, c->d_regs, c->d_wcnt, c->d_nrecs, c->d_starts, c->d_hist,
+  void* bufs[] = {c->d_tail, c->d_tail_n, c->d_gscratch, c->d_gh, c->d_stats, c->d_recs, c->d_recs2, c->d_junk, c->d_route_cur, c->d_regs, c->d_wcnt, c->d_nrecs, c->d_starts, c->d_hist,
                   c->d_scan_sums, c->d_occ, c->d_entries, c->d_off,
                   c->d_img, c->d_resid,
                   c->d_slots, c->d_used, c->d_ukey, c->d_used_n, c->d_filter, c->d_packed, c->d_hot, c->d_hot_tasks, c->d_hot_base,
@@ -4499,6 +4568,34 @@ int rsa_emit(rsa_ctx* c, rsa_conn_record* out, uint64_t max_out, uint64_t* h_n) 
 int rsa_export(rsa_ctx* c, int which, rsa_conn_record* out, uint64_t max_out, uint64_t* h_n) {
   if (which < 0 || which > 2) return fail(c, RSA_ERR_ARG, "which must be 0, 1 or 2");
   return emit_mode(c, which == 2 ? 3 : which ? 2 : 1, out, max_out, h_n);
+}
+
+int rsa_export_routed(rsa_ctx* c, int which, uint32_t world, rsa_conn_record* out, uint64_t max_out,
+                      uint64_t* d_counts) {
+  if (!c) return RSA_ERR_ARG;
+  if (which < 0 || which > 2) return fail(c, RSA_ERR_ARG, "which must be 0, 1 or 2");
+  if (world == 0 || world > (uint32_t)kRouteMax) return fail(c, RSA_ERR_ARG, "world must be 1..%d", kRouteMax);
+  if (!d_counts) return fail(c, RSA_ERR_ARG, "null counts pointer");
+  if (max_out && !out) return fail(c, RSA_ERR_ARG, "null output buffer");
+  int rc = need_agg(c);
+  if (rc) return rc;
+  if (c->owner_world != world) return fail(c, RSA_ERR_STATE, "RSA_OPT_OWNER_WORLD must equal world");
+  const int mode = which == 2 ? 3 : which ? 2 : 1;
+  unsigned long long* counts = reinterpret_cast<unsigned long long*>(d_counts);
+  // counts[world] (caller's) and the route cursors[world] (ctx scratch)
+  if (!c->d_route_cur) HIPCHK(c, hipMalloc(&c->d_route_cur, kRouteMax * sizeof(unsigned long long)));
+  HIPCHK(c, hipMemsetAsync(counts, 0, world * sizeof(unsigned long long), c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_route_cur, 0, world * sizeof(unsigned long long), c->stream));
+  const unsigned long long* uk = c->ukey_ok ? c->d_ukey : nullptr;
+  k_emit_route<false><<<c->cu_count * 2, 1024, 0, c->stream>>>(c->d_slots, c->d_used, c->d_used_n, c->slot_cap,
+                                                              c->d_thresh, mode, world, c->owner_rank, uk, counts,
+                                                              c->d_route_cur, out, max_out);
+  k_emit_route<true><<<c->cu_count * 2, 1024, 0, c->stream>>>(c->d_slots, c->d_used, c->d_used_n, c->slot_cap,
+                                                             c->d_thresh, mode, world, c->owner_rank, uk, counts,
+                                                             c->d_route_cur, out, max_out);
+  HIPCHK(c, hipGetLastError());
+  c->cap_ctl_zeroed = false;
+  return RSA_OK;
 }
 
 int rsa_import(rsa_ctx* c, int which, const rsa_conn_record* in, uint64_t n) {

@@ -6,7 +6,11 @@ on the GPU box, ``gloo`` in the CPU tests).  Every rank classifies and
 aggregates its own contiguous shard of the log (pass 1, rule tables
 replicated).  Rank r owns the rules with ``gid % world == r`` (the reducer
 partitioning), and its pass-1 table doubles as the merged table of those
-rules: their entries stay where pass 1 put them.  Then:
+rules: their entries stay where pass 1 put them.  Exports come out of the
+library already grouped by owner, with their per-owner counts on the device
+(``rsa_export_routed``), so each exchange is one all_to_all of the counts,
+one host read of the send and receive sizes, and one all_to_all of the rows.
+Then:
 
 1. ``all_reduce(SUM)`` of the per-rule line and hit counters;
 2. each rank resolves its shard's own cap thresholds and sends the entries of
@@ -23,14 +27,14 @@ rules: their entries stay where pass 1 put them.  Then:
 
 At world 1 nothing moves: the merge is the single-GPU job.  The order keys
 are global, so the cap logic is shard-agnostic.  Records are 40-byte
-``rsa_conn_record`` rows moved as uint8 tensors; routing uses torch index ops.
+``rsa_conn_record`` rows moved as uint8 tensors.
 """
 
 import numpy as np
 
 from .compile import RECORD_DTYPE
 
-__all__ = ['merge', 'merged_to_host', 'EngineBackend', 'route_records', 'ShardOverflow']
+__all__ = ['merge', 'merged_to_host', 'EngineBackend', 'Exported', 'route_records', 'ShardOverflow']
 
 REC = RECORD_DTYPE.itemsize
 NO_THRESHOLD = -1   # 0xFFFF_FFFF_FFFF_FFFF viewed as int64
@@ -136,35 +140,46 @@ class ShardOverflow(RuntimeError):
         self.needed = int(needed)
 
 
-def route_records(buf, world, dist, group=None, flag=0):
-    """all_to_all of record bytes to owner rank gid % world; returns received
-    bytes.  ``flag`` (this rank's error flag) rides along with the counts: if
-    any rank sent a non-zero flag, every rank returns None instead."""
+class Exported(object):
+    """One rank's export of a merge phase, already grouped by owner rank (gid %
+    world): ``buf`` uint8 rows (40 B each) with owner r's records forming
+    segment r, ``counts`` int64 [world] (device) the segment sizes, ``capacity``
+    the rows ``buf`` holds; ``again(n)`` exports once more into n rows (the
+    library drops rows past the capacity and reports the true counts) and
+    returns (buf, counts, capacity)."""
+
+    def __init__(self, buf, counts, capacity, again=None):
+        self.buf, self.counts, self.capacity, self.again = buf, counts, int(capacity), again
+
+    @classmethod
+    def empty(cls, world, device):
+        import torch
+        return cls(torch.zeros(0, dtype=torch.uint8, device=device), torch.zeros(world, dtype=torch.int64,
+                                                                                  device=device), 0)
+
+
+def route_records(exp, world, dist, group=None, flag=0):
+    """all_to_all of an owner-grouped export (``Exported``) to the owners;
+    returns the received bytes.  The per-owner counts go first, with ``flag``
+    (this rank's error flag) riding along, and the phase's ONE host read takes
+    the send and receive sizes together; if any rank sent a non-zero flag,
+    every rank returns None instead."""
     import torch
-    if world == 1:       # every record is already at its owner
-        return None if flag else buf
-    n = buf.numel() // REC
-    rows = buf.view(-1, REC)
-    gid = rows[:, 8:12].contiguous().view(torch.int32).view(-1).to(torch.int64) if n else \
-        torch.zeros(0, dtype=torch.int64, device=buf.device)
-    owner = gid % world
-    # owner ids as the narrowest key type: the stable device sort is then one
-    # radix pass over 8-bit keys instead of eight over int64
-    okey = owner.to(torch.uint8 if world <= 256 else torch.int32)
-    perm = torch.argsort(okey, stable=True)
-    send = rows[perm].contiguous().view(-1)
-    counts = torch.bincount(owner, minlength=world).to(torch.int64)
-    # (count, flag) per destination, one all_to_all and one host read for both
+    counts = exp.counts.to(torch.int64)
     send_c = torch.stack([counts, torch.full_like(counts, int(flag))], 1).reshape(-1)
     recv_c = torch.empty_like(send_c)
     _all_to_all(recv_c, send_c, dist, group)
-    h = torch.cat([counts, recv_c]).cpu().tolist()
+    h = [int(x) for x in torch.cat([counts, recv_c]).cpu().tolist()]
     if any(h[world + 2 * r + 1] for r in range(world)):
         return None
-    sc = [int(c) * REC for c in h[:world]]
-    rc = [int(h[world + 2 * r]) * REC for r in range(world)]
+    total = sum(h[:world])
+    buf = exp.buf
+    if total > exp.capacity:      # the export dropped rows past its buffer: again at the exact size
+        buf, _counts, _cap = exp.again(total)
+    sc = [c * REC for c in h[:world]]
+    rc = [h[world + 2 * r] * REC for r in range(world)]
     out = torch.empty(sum(rc), dtype=torch.uint8, device=buf.device)
-    _all_to_all(out, send, dist, group, rc, sc)
+    _all_to_all(out, buf[:total * REC], dist, group, rc, sc)
     return out
 
 
@@ -207,7 +222,7 @@ def merge(backend, dist, world, rank, group=None, to_host=True):
         except Exception as e:  # noqa: BLE001 - a table overflow must not strand the other ranks
             if not _overflow(e):
                 raise
-            exported = torch.zeros(0, dtype=torch.uint8, device=dev)
+            exported = Exported.empty(world, dev)
             failed = 1
         tr('export1', dev)
         if multi:
@@ -319,15 +334,18 @@ class EngineBackend(object):
         self.eng.set_option(native.RSA_OPT_OWNER_RANK, rank)
 
     def export(self, which):
-        """Entries of rules owned elsewhere: which 0 = the pass-1 aggregates
-        that can still reach the report (after the shard's own cap
-        resolution), 1 = the pass-2 sums.  A single rank owns every rule:
-        nothing to scan for."""
+        """Entries of rules owned elsewhere, grouped by owner (``Exported``):
+        which 0 = the pass-1 aggregates that can still reach the report (after
+        the shard's own cap resolution), 1 = the pass-2 sums.  A single rank
+        owns every rule: nothing to scan for."""
         if which == 0:
             self.capped = self.eng.resolve_cap()
+        dev = self.eng.device
         if self.world == 1:
-            return self.eng.torch.zeros(0, dtype=self.eng.torch.uint8, device=self.eng.device)
-        return self.eng.emit_device('pass1_kept' if which == 0 else 'pass2')
+            return Exported.empty(1, dev)
+        mode = 'pass1_kept' if which == 0 else 'pass2'
+        buf, counts, cap = self.eng.export_routed(mode, self.world)
+        return Exported(buf, counts, cap, lambda n: self.eng.export_routed(mode, self.world, capacity=n))
 
     def import_records(self, buf, which):
         self.eng.import_records(buf, which)

@@ -76,6 +76,7 @@ class Engine(object):
         torch.cuda.set_device(self.device)
         self.ctx = native.Ctx(device)
         self._emit_buf, self._emit_cap = None, 0   # emission buffer kept between calls (emit_device)
+        self._route_buf, self._route_cap, self._route_counts = None, 0, None   # export_routed's buffers
         self.stream = torch.cuda.current_stream(self.device)
         self.ctx.call('rsa_set_stream', ctypes.c_void_p(self.stream.cuda_stream))
         self.n_rules = 0
@@ -239,6 +240,26 @@ class Engine(object):
         # the buffer is reused by the next emission: callers that keep records
         # across calls clone them
         return buf[: int(n.value) * RECORD_DTYPE.itemsize]
+
+    def export_routed(self, mode, world, capacity=None):
+        """rsa_export_routed: the exported records grouped by owner rank (gid %
+        world) into a device buffer the engine keeps, and their per-owner
+        counts as a device int64 tensor [world]; no host round trip.  Returns
+        (buf, counts, capacity in records): records past the capacity are
+        dropped, so a caller whose counts sum past it exports again with
+        capacity=that sum."""
+        torch = self.torch
+        which = {'pass1': 0, 'pass2': 1, 'pass1_kept': 2}[mode]
+        size = int(capacity or self._emit_cap or self.table_size())
+        size = max(size, 1)
+        if self._route_buf is None or self._route_cap < size:
+            self._route_buf = torch.empty(size * RECORD_DTYPE.itemsize, dtype=torch.uint8, device=self.device)
+            self._route_cap = size
+        if self._route_counts is None or self._route_counts.numel() != world:
+            self._route_counts = torch.zeros(world, dtype=torch.int64, device=self.device)
+        self.ctx.call('rsa_export_routed', ctypes.c_int(which), ctypes.c_uint32(world), _ptr(self._route_buf),
+                      ctypes.c_uint64(self._route_cap), _ptr(self._route_counts))
+        return self._route_buf, self._route_counts, self._route_cap
 
     def _emit_buffer(self, size):
         size = max(int(size), 1)

@@ -73,6 +73,7 @@ SYMBOLS = {
     'rsa_table_size': (I32, [P, PU64]),
     'rsa_stats': (I32, [P, PU64, I32]),
     'rsa_export': (I32, [P, I32, P, U64, PU64]),
+    'rsa_export_routed': (I32, [P, I32, U32, P, U64, P]),
     'rsa_import': (I32, [P, I32, P, U64]),
     'rsa_shadowed': (I32, [P, P, U32, P]),
     'rsa_shadowed_ports': (I32, [P, P, U32, P, U32, P]),

@@ -176,8 +176,20 @@ class NumpyBackend(object):
             self.exported_all = sum(1 for (g, *_) in self.local.t if foreign(g))
             recs = self.local.records(3, self._thresh_np(), keep=foreign)
             self.exported_kept = recs.numel() // RECORD_DTYPE.itemsize
-            return recs
-        return self.local.records(1, keep=foreign)
+            return self._grouped(recs)
+        return self._grouped(self.local.records(1, keep=foreign))
+
+    def _grouped(self, recs):
+        """The model of rsa_export_routed: rows grouped by owner gid % world
+        and the per-owner counts."""
+        from ruleset_analysis_amd.dist import Exported
+        world = max(self.world, 1)
+        rows = recs.numpy().view(RECORD_DTYPE)
+        owner = rows['gid'].astype(np.int64) % world
+        order = np.argsort(owner, kind='stable')
+        buf = torch.from_numpy(rows[order].view(np.uint8).reshape(-1).copy())
+        counts = torch.from_numpy(np.bincount(owner, minlength=world).astype(np.int64))
+        return Exported(buf, counts, len(rows))
 
     def import_records(self, buf, which):
         for r in buf.numpy().view(RECORD_DTYPE):

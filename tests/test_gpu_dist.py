@@ -49,14 +49,14 @@ def _worker(rank, world, port, args, out_q):
     dist.destroy_process_group()
 
 
-def _run_two_ranks(args):
+def _run_two_ranks(args, world=2):
     from test_dist_merge import _free_port
     import queue
     import time
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, args, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, args, q)) for r in range(world)]
     for p in procs:
         p.start()
     out, deadline = None, time.time() + 400
@@ -101,6 +101,16 @@ def test_two_ranks_one_gpu(cap):
     args = (61, 700, 120000, cap, 1.2)
     out = _run_two_ranks(args)
     _check(out, *_oracle_inputs(61, 700, 120000, 1.2), cap)
+
+
+def test_four_ranks_one_gpu():
+    """Four ranks sharing the box's GPU, each with its own HIP table, cap 12
+    engaged (Zipf traffic): the owner-routed exports (rsa_export_routed), the
+    owners' imports and the global thresholds give the C oracle's result."""
+    args = (71, 700, 160000, 12, 1.2)
+    out = _run_two_ranks(args, world=4)
+    ref = _check(out, *_oracle_inputs(71, 700, 160000, 1.2), 12)
+    assert (ref['n_conns'] >= 12).sum() > 20
 
 
 def test_two_ranks_capped_only_after_merge():
