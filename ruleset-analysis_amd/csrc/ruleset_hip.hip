@@ -1076,6 +1076,61 @@ struct Emit {
   uint32_t* wcnt;                       // records per 64-line window
 };
 
+// k_classify's emission arguments, passed FIRST (kernarg offset 0) and read
+// from the kernarg segment where they are used (classify_emit_args): held in
+// SGPRs across the lookup they spilled to VGPR lanes (55 SGPRs, ~25 v_readlane
+// restores per emission); re-read they cost two scalar loads per iteration.
+struct EmitPack {
+  unsigned long long gh, ts, ord, recs, regs, wcnt, filter;   // device addresses (global memory)
+  uint32_t cap, skip, np_bits, pad;
+};
+
+template <typename T>
+__device__ __forceinline__ T* global_ptr(unsigned long long a) {
+  // an integer -> global (address space 1) pointer -> generic pointer: the
+  // address space stays known, so accesses through it are global_*, not flat_*
+  typedef __attribute__((address_space(1))) T gT;
+  return (T*)(gT*)a;
+}
+
+#ifndef RSA_EMIT_KERNARG
+#define RSA_EMIT_KERNARG 1
+#endif
+
+// The emission's Agg fields and Emit pointers, loaded from the kernarg segment
+// at this point of the loop (the empty asm makes the pointer opaque per
+// iteration, so the loads are not hoisted into long-lived SGPRs).
+__device__ __forceinline__ void classify_emit_args(const EmitPack& ep_arg, Agg& A, Emit& E) {
+#if RSA_EMIT_KERNARG
+  typedef __attribute__((address_space(4))) const EmitPack cEmitPack;
+  cEmitPack* ep = (cEmitPack*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(ep));
+  EmitPack p;   // field by field (an address-space-qualified aggregate does not copy-construct)
+  p.gh = ep->gh;
+  p.ts = ep->ts;
+  p.ord = ep->ord;
+  p.recs = ep->recs;
+  p.regs = ep->regs;
+  p.wcnt = ep->wcnt;
+  p.filter = ep->filter;
+  p.cap = ep->cap;
+  p.skip = ep->skip;
+  p.np_bits = ep->np_bits;
+#else
+  const EmitPack& p = ep_arg;
+#endif
+  E.gh = global_ptr<uint32_t>(p.gh);
+  E.ts = global_ptr<const uint32_t>(p.ts);
+  E.ord = global_ptr<const unsigned long long>(p.ord);
+  E.recs = global_ptr<Rec>(p.recs);
+  E.regs = global_ptr<uint16_t>(p.regs);
+  E.wcnt = global_ptr<uint32_t>(p.wcnt);
+  A.filter = global_ptr<const unsigned long long>(p.filter);
+  A.cap = p.cap;
+  A.skip = p.skip;
+  A.np_bits = p.np_bits;
+}
+
 // The record of one line, or false (need).  kPre: the line's order and
 // timestamp were loaded ahead (o_pre, ts_pre; RSA_PREFETCH_T 2).
 template <bool kPre = false>
@@ -1139,8 +1194,10 @@ __device__ __forceinline__ void emit_one(uint32_t i, uint4 t, uint32_t gid, cons
 // (k_tail scans and emits them exactly).
 template <int kImg, bool kEmit, int kMode, bool kNarrow>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kImgSmallMax ? 4 : 8, 8))) void k_classify(
-    const uint4* __restrict__ T, unsigned long long n, int32_t* __restrict__ gout, Rules R, unsigned int* flags,
-    uint32_t* tail, unsigned long long* tail_n, Agg A, Emit E) {
+    EmitPack EP, const uint4* __restrict__ T, unsigned long long n, int32_t* __restrict__ gout, Rules R,
+    unsigned int* flags, uint32_t* tail, unsigned long long* tail_n) {
+  Agg A = {};
+  Emit E = {};
   __shared__ __attribute__((aligned(16))) uint32_t lds_img[kImg > 0 ? kImg : 4];
   __shared__ uint32_t lds_task[kMode == 1 ? 1024 : 64];   // 64 words per wave (index_lookup_wave)
   lds_w32* scr = (lds_w32*)lds_task + (kMode == 1 ? (threadIdx.x & ~63u) : 0u);
@@ -1171,6 +1228,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kIm
   uint32_t ts_next = 0u;
   if (kPf >= 1 && i0 < n32) t_next = T[i0];
   if (kPf >= 2 && kEmit && i0 < n32) {
+    classify_emit_args(EP, A, E);
     o_next = E.ord[i0];
     ts_next = __builtin_nontemporal_load(&E.ts[i0]);
   }
@@ -1188,6 +1246,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kIm
       t = t_next;
       t_next = i + stride < n32 ? T[i + stride] : make_uint4(0u, 0u, 0u, 0u);
       if (kPf >= 2 && kEmit) {
+        classify_emit_args(EP, A, E);
         o_cur = o_next;
         ts_cur = ts_next;
         o_next = i + stride < n32 ? E.ord[i + stride] : 0ull;
@@ -1214,7 +1273,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kIm
       if (defer) tail[pos + __popcll(dm & ((1ull << __lane_id()) - 1ull))] = (uint32_t)i;
     }
     if (gout && in && !defer) gout[i] = (int32_t)gid;
-    if (kEmit) emit_wave<kPf >= 2>(i, n32, in && !defer, t, gid, A, E, o_cur, ts_cur);
+    if (kEmit) {
+      classify_emit_args(EP, A, E);
+      emit_wave<kPf >= 2>(i, n32, in && !defer, t, gid, A, E, o_cur, ts_cur);
+    }
     PH(7);
   }
 #ifdef RSA_PHASE_PROF
@@ -3529,15 +3591,26 @@ constexpr int kImgLarge = 38912;   // 152 KiB: one workgroup per CU
 template <bool kEmit, int kMode, bool kNarrow>
 void launch_classify_img(rsa_ctx* c, const uint4* t, uint64_t m, int32_t* go, const Rules& r, const Agg& ag,
                          const Emit& e) {
+  EmitPack ep = {};
+  ep.gh = reinterpret_cast<unsigned long long>(e.gh);
+  ep.ts = reinterpret_cast<unsigned long long>(e.ts);
+  ep.ord = reinterpret_cast<unsigned long long>(e.ord);
+  ep.recs = reinterpret_cast<unsigned long long>(e.recs);
+  ep.regs = reinterpret_cast<unsigned long long>(e.regs);
+  ep.wcnt = reinterpret_cast<unsigned long long>(e.wcnt);
+  ep.filter = reinterpret_cast<unsigned long long>(ag.filter);
+  ep.cap = ag.cap;
+  ep.skip = ag.skip;
+  ep.np_bits = ag.np_bits;
   if (c->indexed && c->img_words <= (uint32_t)kImgSmall && !RSA_FORCE_LARGE) {
     k_classify<kImgSmall, kEmit, kMode, kNarrow><<<grid_for_threads(c, m, 1024, 2), 1024, 0, c->stream>>>(
-        t, m, go, r, c->d_flags, c->d_tail, c->d_tail_n, ag, e);
+        ep, t, m, go, r, c->d_flags, c->d_tail, c->d_tail_n);
   } else if (c->indexed && c->img_words <= (uint32_t)kImgLarge) {
     k_classify<kImgLarge, kEmit, kMode, kNarrow><<<grid_for_threads(c, m, 1024, 1), 1024, 0, c->stream>>>(
-        t, m, go, r, c->d_flags, c->d_tail, c->d_tail_n, ag, e);
+        ep, t, m, go, r, c->d_flags, c->d_tail, c->d_tail_n);
   } else {
     k_classify<0, kEmit, kMode, kNarrow><<<grid_for_threads(c, m, 1024, 2), 1024, 0, c->stream>>>(
-        t, m, go, r, c->d_flags, c->d_tail, c->d_tail_n, ag, e);
+        ep, t, m, go, r, c->d_flags, c->d_tail, c->d_tail_n);
   }
 }
 
