@@ -176,7 +176,8 @@ typedef struct rsa_pht_list {    /* 80 B: one list (or one chained chunk of a li
 #define RSA_OPT_AUTO_FILTER 1 /* split a large first batch to derive the exact per-rule insert filter (default 1) */
 #define RSA_OPT_USE_INDEX 2   /* classify with the loaded index (1) or the linear lists (0)                  */
 #define RSA_OPT_FILTER_SLICE 5 /* auto filter: first 1/N (>= 1M lines) of a large batch builds the bound (default 256)       */
-#define RSA_OPT_FILTER_STEPS 7 /* auto filter: bound refinements, each after 4x the previous lines (default 3)  */
+#define RSA_OPT_FILTER_STEPS 7 /* auto filter: bound refinements, each after RSA_OPT_FILTER_GROWTH x the previous lines (default 3) */
+#define RSA_OPT_FILTER_GROWTH 24 /* auto filter: lines of each bound refinement's slice over the previous ones (default 4) */
 #define RSA_OPT_FORCE_DEFER 8  /* TESTING: every index candidate goes to the exact deferred-line path        */
 #define RSA_OPT_PROFILE_SKIP 3 /* PROFILING ONLY, results invalid: bit0 skips counters, bit1 skips the table, bit2 skips table updates */
 #define RSA_OPT_PRECHECK 9     /* pre-check monotone slot fields with a plain load before their atomics (default 1)       */

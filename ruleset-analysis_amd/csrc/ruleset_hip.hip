@@ -3278,7 +3278,8 @@ struct rsa_ctx {
   bool stats_on = false;
   unsigned long long* d_stats = nullptr;   // 4 counters (RSA_OPT_STATS)
   uint32_t filter_slice = 256;
-  uint32_t filter_steps = 3;          // auto filter: bound refinements (each after 4x the previous lines)
+  uint32_t filter_steps = 3;          // auto filter: bound refinements (each after filter_growth x the previous lines)
+  uint32_t filter_growth = 4;         // RSA_OPT_FILTER_GROWTH
   uint32_t* d_tail = nullptr;         // deferred line indices
   unsigned long long* d_tail_n = nullptr;
   unsigned long long tail_alloc = 0;
@@ -3954,7 +3955,7 @@ int run_pass1(rsa_ctx* c, int classify, const rsa_tuple* T, const uint32_t* TS, 
       rc = cap_select(c, c->d_filter, nullptr);   // on the device: no host round trip
       if (rc) return rc;
       done = next;
-      next = next * 4;
+      next = next * c->filter_growth;
     }
     c->tightened = true;
     // the last slice runs under the final filter bounds: its records of
@@ -4092,6 +4093,10 @@ int rsa_set_option(rsa_ctx* c, int option, int64_t value) {
     case RSA_OPT_FILTER_STEPS:
       if (value < 1 || value > 8) return fail(c, RSA_ERR_ARG, "filter steps must be in [1, 8]");
       c->filter_steps = (uint32_t)value;
+      return RSA_OK;
+    case RSA_OPT_FILTER_GROWTH:
+      if (value < 2 || value > 64) return fail(c, RSA_ERR_ARG, "filter growth must be in [2, 64]");
+      c->filter_growth = (uint32_t)value;
       return RSA_OK;
     case RSA_OPT_PROFILE_SKIP:
       c->profile_skip = (uint32_t)value;
