@@ -1069,6 +1069,7 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t* sh, uint3
 constexpr uint32_t kWin = 64;
 struct Emit {
   uint32_t* gh;                         // gid | hit << 31, 0xFFFFFFFF: no rule
+  uint16_t* gh16;                       // instead of gh when the rules fit 15 bits: gid | hit << 15, 0xFFFF
   const uint32_t* ts;
   const unsigned long long* ord;
   Rec* recs;                            // window-compacted records
@@ -1081,7 +1082,7 @@ struct Emit {
 // SGPRs across the lookup they spilled to VGPR lanes (55 SGPRs, ~25 v_readlane
 // restores per emission); re-read they cost two scalar loads per iteration.
 struct EmitPack {
-  unsigned long long gh, ts, ord, recs, regs, wcnt, filter;   // device addresses (global memory)
+  unsigned long long gh, gh16, ts, ord, recs, regs, wcnt, filter;   // device addresses (global memory)
   uint32_t cap, skip, np_bits, pad;
 };
 
@@ -1107,6 +1108,7 @@ __device__ __forceinline__ void classify_emit_args(const EmitPack& ep_arg, Agg& 
   asm volatile("" : "+s"(ep));
   EmitPack p;   // field by field (an address-space-qualified aggregate does not copy-construct)
   p.gh = ep->gh;
+  p.gh16 = ep->gh16;
   p.ts = ep->ts;
   p.ord = ep->ord;
   p.recs = ep->recs;
@@ -1120,6 +1122,7 @@ __device__ __forceinline__ void classify_emit_args(const EmitPack& ep_arg, Agg& 
   const EmitPack& p = ep_arg;
 #endif
   E.gh = global_ptr<uint32_t>(p.gh);
+  E.gh16 = p.gh16 ? global_ptr<uint16_t>(p.gh16) : nullptr;
   E.ts = global_ptr<const uint32_t>(p.ts);
   E.ord = global_ptr<const unsigned long long>(p.ord);
   E.recs = global_ptr<Rec>(p.recs);
@@ -1159,7 +1162,12 @@ __device__ __forceinline__ void emit_wave(uint32_t i, uint32_t n, bool in, uint4
   const uint32_t flags = (t.w >> 16) & 0xFFu;
   const bool matched = in && gid != kNoGid;
   const bool hit = matched && (flags & RSA_F_HIT);
-  if (in) E.gh[i] = matched ? (gid | (hit ? 0x80000000u : 0u)) : 0xFFFFFFFFu;
+  if (in) {
+    if (E.gh16)
+      E.gh16[i] = (uint16_t)(matched ? (gid | (hit ? 0x8000u : 0u)) : 0xFFFFu);
+    else
+      E.gh[i] = matched ? (gid | (hit ? 0x80000000u : 0u)) : 0xFFFFFFFFu;
+  }
   Rec r;
   const bool need = in && make_rec<kPre>(i, t, gid, A, E, r, o_pre, ts_pre);
   const unsigned long long mask = __ballot(need);
@@ -1178,7 +1186,10 @@ __device__ __forceinline__ void emit_one(uint32_t i, uint4 t, uint32_t gid, cons
   const uint32_t flags = (t.w >> 16) & 0xFFu;
   const bool matched = gid != kNoGid;
   const bool hit = matched && (flags & RSA_F_HIT);
-  E.gh[i] = matched ? (gid | (hit ? 0x80000000u : 0u)) : 0xFFFFFFFFu;
+  if (E.gh16)
+    E.gh16[i] = (uint16_t)(matched ? (gid | (hit ? 0x8000u : 0u)) : 0xFFFFu);
+  else
+    E.gh[i] = matched ? (gid | (hit ? 0x80000000u : 0u)) : 0xFFFFFFFFu;
   Rec r;
   if (!make_rec(i, t, gid, A, E, r)) return;
   const uint32_t w = i / kWin;
@@ -1380,6 +1391,51 @@ __global__ __launch_bounds__(1024) void k_count(const uint32_t* __restrict__ gh,
       if (m) atomicAdd(&A.matches[r], (unsigned long long)m);
       if (hh) atomicAdd(&A.hits[r], (unsigned long long)hh);
     }
+  }
+}
+
+// The same LDS histogram over 16-bit words (gid | hit << 15, 0xFFFF = no rule;
+// rule sets that fit 15 bits): eight words per 16-B load, half the bytes.
+template <int kLds>
+__global__ __launch_bounds__(1024) void k_count16(const uint16_t* __restrict__ gh, unsigned long long n,
+                                                  uint32_t n_rules, Agg A) {
+  __shared__ uint32_t cnt[2 * kLds];
+  for (uint32_t r = threadIdx.x; r < 2u * kLds; r += blockDim.x) cnt[r] = 0;
+  __syncthreads();
+  const unsigned long long n8 = n / 8;   // whole 16-B groups (gh is 16-B aligned: the batch's word 0)
+  const uint4* g4 = reinterpret_cast<const uint4*>(gh);
+  const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+  for (unsigned long long q = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; q < n8 + 1; q += stride) {
+    uint32_t w[4];
+    if (q < n8) {
+      const uint4 v = g4[q];
+      w[0] = v.x;
+      w[1] = v.y;
+      w[2] = v.z;
+      w[3] = v.w;
+    } else {   // the tail words (< 8)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const unsigned long long i = q * 8 + 2 * k;
+        const uint32_t lo = i < n ? gh[i] : 0xFFFFu, hi = i + 1 < n ? gh[i + 1] : 0xFFFFu;
+        w[k] = lo | (hi << 16);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t x = (w[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+      if (x != 0xFFFFu) {
+        const uint32_t g = x & 0x7FFFu;
+        atomicAdd(&cnt[g], 1u);
+        if (x >> 15) atomicAdd(&cnt[kLds + g], 1u);
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t r = threadIdx.x; r < n_rules; r += blockDim.x) {
+    const uint32_t m = cnt[r], hh = cnt[kLds + r];
+    if (m) atomicAdd(&A.matches[r], (unsigned long long)m);
+    if (hh) atomicAdd(&A.hits[r], (unsigned long long)hh);
   }
 }
 
@@ -3327,6 +3383,11 @@ struct rsa_ctx {
   unsigned long long sort_alloc = 0;
   // pass-1 kernel timing (HIP events on the ctx stream)
   hipEvent_t ev[48] = {};             // per pass-1 launch: start, classified, aggregated
+  hipStream_t count_stream = nullptr; // per-rule counting overlapped with the record merge (RSA_OPT_COUNT_STREAM)
+  hipEvent_t ev_count[2] = {};        // fork / join of that stream
+  bool count_pending = false;
+  bool count_stream_on = true;        // RSA_OPT_COUNT_STREAM
+  bool gh16 = true;                   // RSA_OPT_COUNTER_WORDS16: 16-bit gid|hit words when the rules fit
   int ev_used = 0;
   bool debug = false;                 // RSA_DEBUG=1 in the environment: per-launch counts on stderr
 };
@@ -3579,6 +3640,11 @@ constexpr int kMaxEvents = 48;
 int ensure_events(rsa_ctx* c) {
   for (int k = 0; k < kMaxEvents; ++k)
     if (!c->ev[k]) HIPCHK(c, hipEventCreate(&c->ev[k]));
+  if (c->count_stream_on && !c->count_stream) {
+    HIPCHK(c, hipStreamCreateWithFlags(&c->count_stream, hipStreamNonBlocking));
+    for (int k = 0; k < 2; ++k)
+      if (!c->ev_count[k]) HIPCHK(c, hipEventCreateWithFlags(&c->ev_count[k], hipEventDisableTiming));
+  }
   return RSA_OK;
 }
 
@@ -3594,6 +3660,7 @@ void launch_classify_img(rsa_ctx* c, const uint4* t, uint64_t m, int32_t* go, co
                          const Emit& e) {
   EmitPack ep = {};
   ep.gh = reinterpret_cast<unsigned long long>(e.gh);
+  ep.gh16 = reinterpret_cast<unsigned long long>(e.gh16);
   ep.ts = reinterpret_cast<unsigned long long>(e.ts);
   ep.ord = reinterpret_cast<unsigned long long>(e.ord);
   ep.recs = reinterpret_cast<unsigned long long>(e.recs);
@@ -3784,13 +3851,30 @@ int count_by_block(rsa_ctx* c, const uint32_t* gh, uint64_t m) {
 // With gh, the counters cover the words [gh_count, gh_count + m_count) (the
 // auto-tightening slices count once, all of the batch's lines with the last).
 int launch_aggregate(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsigned long long* o, const int32_t* g,
-                     const uint32_t* gh, uint64_t a, uint64_t m, const uint32_t* gh_count, uint64_t m_count) {
+                     const uint32_t* gh, uint64_t a, uint64_t m, const uint32_t* gh_count, uint64_t m_count,
+                     const uint16_t* gh16_count = nullptr) {
   const Agg ag = agg_of(c);
   int rc = RSA_OK;
-  if (gh) {
+  if (gh || gh16_count) {
     if (!(ag.skip & 1u) && m_count) {
       const uint64_t units = (m_count + 3) / 4;
-      if (c->n_rules <= (uint32_t)kCnt) {
+      if (gh16_count) {
+        // 16-bit words (rules <= kCnt): counted on the side stream, overlapping
+        // the record sort and merge below (the counters are read only after
+        // the job; the main stream waits for them at the end of this launch)
+        if (reinterpret_cast<uintptr_t>(gh16_count) & 15u) return fail(c, RSA_ERR_STATE, "misaligned counter words");
+        hipStream_t cs = c->count_stream ? c->count_stream : c->stream;
+        if (c->count_stream) {
+          HIPCHK(c, hipEventRecord(c->ev_count[0], c->stream));
+          HIPCHK(c, hipStreamWaitEvent(cs, c->ev_count[0], 0));
+        }
+        k_count16<kCnt><<<grid_for_threads(c, (m_count + 7) / 8 + 1, 1024, RSA_COUNT_PER_CU), 1024, 0, cs>>>(
+            gh16_count, m_count, c->n_rules, ag);
+        if (c->count_stream) {
+          HIPCHK(c, hipEventRecord(c->ev_count[1], cs));
+          c->count_pending = true;
+        }
+      } else if (c->n_rules <= (uint32_t)kCnt) {
         k_count<kCnt><<<grid_for_threads(c, units, 1024, RSA_COUNT_PER_CU), 1024, 0, c->stream>>>(gh_count, m_count,
                                                                                                   c->n_rules, ag);
       } else if (c->count_sort && ((c->n_rules + kCntBlock - 1) >> kCntBits) <= (uint32_t)kMaxRegions) {
@@ -3819,7 +3903,13 @@ int launch_aggregate(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsig
     }
   }
   HIPCHK(c, hipGetLastError());
-  if (ag.cap == 0 || (ag.skip & 2u)) return RSA_OK;   // no table this job
+  if (ag.cap == 0 || (ag.skip & 2u)) {   // no table this job
+    if (c->count_pending) {
+      HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_count[1], 0));
+      c->count_pending = false;
+    }
+    return RSA_OK;
+  }
   const Rec* recs = reinterpret_cast<const Rec*>(c->d_recs);
   // region-sorted records: at the launch's line offset while this job's
   // records are kept for the recount (rsa_recount), else from 0
@@ -3879,6 +3969,10 @@ int launch_aggregate(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsig
     HIPCHK(c, hipStreamSynchronize(c->stream));
     fprintf(stderr, "[rsa] pass-1 launch: %llu lines -> %u records\n", (unsigned long long)m, nr);
   }
+  if (c->count_pending) {   // the side stream's counters join the ctx stream
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_count[1], 0));
+    c->count_pending = false;
+  }
   return RSA_OK;
 }
 
@@ -3907,6 +4001,9 @@ int run_pass1(rsa_ctx* c, int classify, const rsa_tuple* T, const uint32_t* TS, 
     c->rec_cache = false;
   }
   uint32_t* gh = nullptr;
+  // 16-bit counter words when every gid fits 15 bits and the LDS histogram
+  // takes the rules (half the bytes written by k_classify and read by the count)
+  const bool narrow = classify && c->gh16 && c->n_rules <= (uint32_t)kCnt && c->n_rules < 0x7FFFu;
   if (classify) {
     rc = ensure_buf(c, &c->d_gh, &c->gh_alloc, n);
     if (rc) return rc;
@@ -3926,7 +4023,8 @@ int run_pass1(rsa_ctx* c, int classify, const rsa_tuple* T, const uint32_t* TS, 
       int rc2 = prepare_records(c, m);
       if (rc2) return rc2;
       Emit e;
-      e.gh = gh + a;
+      e.gh = narrow ? nullptr : gh + a;
+      e.gh16 = narrow ? reinterpret_cast<uint16_t*>(gh) + a : nullptr;
       e.ts = TS + a;
       e.ord = o;
       e.recs = reinterpret_cast<Rec*>(c->d_recs);
@@ -3936,8 +4034,9 @@ int run_pass1(rsa_ctx* c, int classify, const rsa_tuple* T, const uint32_t* TS, 
       if (rc2) return rc2;
     }
     HIPCHK(c, hipEventRecord(c->ev[c->ev_used + 1], c->stream));
-    const int rc2 = launch_aggregate(c, t, TS + a, o, G ? G + a : nullptr, classify ? gh + a : nullptr, a, m,
-                                     classify ? gh + count_from : nullptr, a + m - count_from);
+    const int rc2 = launch_aggregate(c, t, TS + a, o, G ? G + a : nullptr, classify && !narrow ? gh + a : nullptr, a,
+                                     m, classify && !narrow ? gh + count_from : nullptr, a + m - count_from,
+                                     classify && narrow ? reinterpret_cast<uint16_t*>(gh) + count_from : nullptr);
     if (rc2) return rc2;
     HIPCHK(c, hipEventRecord(c->ev[c->ev_used + 2], c->stream));
     c->ev_used += 3;
@@ -4056,6 +4155,9 @@ int rsa_ctx_destroy(rsa_ctx* c) {
   for (void* b : bufs) (void)hipFree(b);
   for (int k = 0; k < kMaxEvents; ++k)
     if (c->ev[k]) (void)hipEventDestroy(c->ev[k]);
+  for (int k = 0; k < 2; ++k)
+    if (c->ev_count[k]) (void)hipEventDestroy(c->ev_count[k]);
+  if (c->count_stream) (void)hipStreamDestroy(c->count_stream);
   delete c;
   return RSA_OK;
 }
@@ -4115,6 +4217,17 @@ int rsa_set_option(rsa_ctx* c, int option, int64_t value) {
       return RSA_OK;
     case RSA_OPT_REDUCE_BIG:
       c->reduce_big = value != 0;
+      return RSA_OK;
+    case RSA_OPT_COUNT_STREAM:
+      c->count_stream_on = value != 0;
+      if (!c->count_stream_on && c->count_stream) {
+        HIPCHK(c, hipStreamSynchronize(c->count_stream));
+        HIPCHK(c, hipStreamDestroy(c->count_stream));
+        c->count_stream = nullptr;
+      }
+      return RSA_OK;
+    case RSA_OPT_COUNTER_WORDS16:
+      c->gh16 = value != 0;
       return RSA_OK;
     case RSA_OPT_REGION_RECORDS:
       if (value < 0 || value > 0xFFFFFFFFll) return fail(c, RSA_ERR_ARG, "RSA_OPT_REGION_RECORDS must be 0..2^32-1");
