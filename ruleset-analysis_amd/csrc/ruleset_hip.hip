@@ -3334,8 +3334,12 @@ struct rsa_ctx {
   bool stats_on = false;
   unsigned long long* d_stats = nullptr;   // 4 counters (RSA_OPT_STATS)
   uint32_t filter_slice = 256;
-  uint32_t filter_steps = 3;          // auto filter: bound refinements (each after filter_growth x the previous lines)
-  uint32_t filter_growth = 4;         // RSA_OPT_FILTER_GROWTH
+  // auto filter: bound refinements (each after filter_growth x the previous
+  // lines).  1M then 16M lines: cfg3 7.91 -> 7.80, cfg5 9.55 -> 9.30 ms/step
+  // against 1M / 4M / 16M (profiles/r05j_*); the bound of the long last slice
+  // must come from ~16M lines (from 9M: 14.8 ms/step; 36M: 9.5)
+  uint32_t filter_steps = 2;
+  uint32_t filter_growth = 16;        // RSA_OPT_FILTER_GROWTH
   uint32_t* d_tail = nullptr;         // deferred line indices
   unsigned long long* d_tail_n = nullptr;
   unsigned long long tail_alloc = 0;
@@ -3386,7 +3390,7 @@ struct rsa_ctx {
   hipStream_t count_stream = nullptr; // per-rule counting overlapped with the record merge (RSA_OPT_COUNT_STREAM)
   hipEvent_t ev_count[2] = {};        // fork / join of that stream
   bool count_pending = false;
-  bool count_stream_on = true;        // RSA_OPT_COUNT_STREAM
+  bool count_stream_on = false;       // RSA_OPT_COUNT_STREAM (measured neutral at cfg3: 7.87 vs 7.91 ms/step)
   bool gh16 = true;                   // RSA_OPT_COUNTER_WORDS16: 16-bit gid|hit words when the rules fit
   int ev_used = 0;
   bool debug = false;                 // RSA_DEBUG=1 in the environment: per-launch counts on stderr
