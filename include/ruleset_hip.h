@@ -176,8 +176,8 @@ typedef struct rsa_pht_list {    /* 80 B: one list (or one chained chunk of a li
 #define RSA_OPT_AUTO_FILTER 1 /* split a large first batch to derive the exact per-rule insert filter (default 1) */
 #define RSA_OPT_USE_INDEX 2   /* classify with the loaded index (1) or the linear lists (0)                  */
 #define RSA_OPT_FILTER_SLICE 5 /* auto filter: first 1/N (>= 1M lines) of a large batch builds the bound (default 256)       */
-#define RSA_OPT_FILTER_STEPS 7 /* auto filter: bound refinements, each after RSA_OPT_FILTER_GROWTH x the previous lines (default 2) */
-#define RSA_OPT_FILTER_GROWTH 24 /* auto filter: lines of each bound refinement's slice over the previous ones (default 16) */
+#define RSA_OPT_FILTER_STEPS 7 /* auto filter: bound refinements, each after RSA_OPT_FILTER_GROWTH x the previous lines (default 3) */
+#define RSA_OPT_FILTER_GROWTH 24 /* auto filter: lines of each bound refinement's slice over the previous ones (default 4) */
 #define RSA_OPT_COUNT_STREAM 25 /* per-rule line/hit counting on a second HIP stream, overlapping the record merge (default 0) */
 #define RSA_OPT_COUNTER_WORDS16 26 /* 16-bit gid|hit words between classification and counting when every gid fits 15 bits and the LDS histogram holds the rules (1, default) */
 #define RSA_OPT_FORCE_DEFER 8  /* TESTING: every index candidate goes to the exact deferred-line path        */

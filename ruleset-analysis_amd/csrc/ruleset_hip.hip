@@ -3335,11 +3335,12 @@ struct rsa_ctx {
   unsigned long long* d_stats = nullptr;   // 4 counters (RSA_OPT_STATS)
   uint32_t filter_slice = 256;
   // auto filter: bound refinements (each after filter_growth x the previous
-  // lines).  1M then 16M lines: cfg3 7.91 -> 7.80, cfg5 9.55 -> 9.30 ms/step
-  // against 1M / 4M / 16M (profiles/r05j_*); the bound of the long last slice
-  // must come from ~16M lines (from 9M: 14.8 ms/step; 36M: 9.5)
-  uint32_t filter_steps = 2;
-  uint32_t filter_growth = 16;        // RSA_OPT_FILTER_GROWTH
+  // lines): 1M / 4M / 16M.  1M then 16M lines measured cfg3 7.91 -> 7.80 and
+  // cfg5 9.55 -> 9.30 but cfg2 5.65 -> 6.84 ms/step (profiles/r05j_*, r05k_*);
+  // the bound of the long last slice must come from ~16M lines (from 9M:
+  // 14.8 ms/step at cfg3; from 36M: 9.5)
+  uint32_t filter_steps = 3;
+  uint32_t filter_growth = 4;         // RSA_OPT_FILTER_GROWTH
   uint32_t* d_tail = nullptr;         // deferred line indices
   unsigned long long* d_tail_n = nullptr;
   unsigned long long tail_alloc = 0;

@@ -210,8 +210,8 @@ def test_synth_parity_10k_rules(engine):
 def test_synth_parity_tightened_filter(engine):
     # > 4M lines in one batch: the library aggregates the first 1M lines (the
     # default slice is 1/256 of the batch, at least 1M), derives the per-rule
-    # filter (refined after 16M lines in a longer batch) and skips the table
-    # for lines beyond it
+    # filter, refines it after 4M lines (and 16M in a longer batch) and skips
+    # the table for lines beyond it
     res, ref = _gpu_vs_oracle(engine, 800, 5_000_000, 40, seed=16, zipf=1.2)
     assert (ref['n_conns'] >= 40).sum() > 0           # the cap is engaged
 
@@ -220,10 +220,10 @@ def test_synth_parity_tightened_filter_shuffled(engine):
     _gpu_vs_oracle(engine, 800, 5_000_000, 40, seed=17, zipf=1.2, shuffle=True)
 
 
-@pytest.mark.parametrize('steps,slice_,growth', [(1, 256, 16), (3, 256, 4), (4, 256, 4), (3, 16, 4), (2, 256, 2)])
+@pytest.mark.parametrize('steps,slice_,growth', [(1, 256, 4), (2, 256, 16), (4, 256, 4), (3, 16, 4), (2, 256, 2)])
 def test_synth_parity_filter_schedule(engine, steps, slice_, growth):
-    """Other filter schedules: 1, 3 or 4 refinements growing 4x, a 1/16 first
-    slice, growth 2 (the default is 2 refinements, 1M then 16M lines)."""
+    """Other filter schedules: 1, 2 or 4 refinements, a 1/16 first slice,
+    growth 2 and 16 (the default: 3 refinements growing 4x)."""
     from ruleset_analysis_amd import native
     engine.set_option(native.RSA_OPT_FILTER_STEPS, steps)
     engine.set_option(native.RSA_OPT_FILTER_SLICE, slice_)
@@ -232,9 +232,9 @@ def test_synth_parity_filter_schedule(engine, steps, slice_, growth):
         _gpu_vs_oracle(engine, 1500, 5_000_000, 40, seed=24, zipf=1.1, broad=False,
                        interfaces=('outside', 'partner'))
     finally:
-        engine.set_option(native.RSA_OPT_FILTER_STEPS, 2)
+        engine.set_option(native.RSA_OPT_FILTER_STEPS, 3)
         engine.set_option(native.RSA_OPT_FILTER_SLICE, 256)
-        engine.set_option(native.RSA_OPT_FILTER_GROWTH, 16)
+        engine.set_option(native.RSA_OPT_FILTER_GROWTH, 4)
 
 
 def test_capacity_above_table_limit_is_clamped(engine):
