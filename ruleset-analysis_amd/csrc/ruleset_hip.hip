@@ -2561,8 +2561,8 @@ __global__ void k_tent_check(const unsigned long long* filter, const unsigned lo
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= n_rules) return;
   const unsigned long long f = filter[g], t = thresh[g];
-  if (f != RSA_NO_THRESHOLD && t != f) atomicOr(&out[0], 1u);
-  if (f == RSA_NO_THRESHOLD && t != RSA_NO_THRESHOLD) atomicOr(&out[1], 1u);
+  if (f != RSA_NO_THRESHOLD && t != f) atomicAdd(&out[0], 1u);   // counts (RSA_DEBUG prints them)
+  if (f == RSA_NO_THRESHOLD && t != RSA_NO_THRESHOLD) atomicAdd(&out[1], 1u);
 }
 
 // The pass-2 fields of every used slot back to empty (the last slice's
@@ -4713,6 +4713,7 @@ int rsa_recount(rsa_ctx* c, const rsa_tuple* T, const uint32_t* TS, const uint64
     uint32_t h[2] = {1u, 1u};
     HIPCHK(c, hipMemcpyAsync(h, c->d_chk, sizeof h, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->debug) fprintf(stderr, "[rsa] recount: %u bounded rules moved below their bound, %u capped only now\n", h[0], h[1]);
     if (!h[0] && !h[1]) {
       clear = false;
       n_segs = c->late_seg;   // the last slice is already counted
