@@ -128,6 +128,8 @@ struct Agg {
   uint32_t np_bits;                  // 2^np_bits regions; a key's region = top np_bits of its slot hash
   uint32_t tent2;                    // pass 1's last slice: records of rules under a filter bound also go
                                      // into the pass-2 fields (exact when the final threshold equals the bound)
+  const uint8_t* replay;             // pass 2 (selective recount): per rule, 1 = its records of segment
+  uint32_t late_seg;                 //   late_seg are replayed (0xFFFFFFFF: every segment is replayed)
 };
 
 __device__ __forceinline__ unsigned long long mix64(unsigned long long x) {
@@ -2167,6 +2169,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
           if (kPass == 2 && have) {   // (hot records of pass 2 were filtered when combined)
             const unsigned long long P = A.thresh[kB >> 32];
             if (P == RSA_NO_THRESHOLD || mo > P) have = false;
+            // selective recount: the last slice's records of rules whose
+            // pass-2 fields it already filled exactly are not replayed
+            if (sg == A.late_seg && !A.replay[kB >> 32]) have = false;
           }
         }
         lds_agg_insert<kE, kPass == 1>(e_kA, e_kB, e_mo, e_first, e_last, e_cnt, used, have, kA, kB, mo,
@@ -2395,7 +2400,7 @@ __global__ void k_hot_plan(const unsigned long long* __restrict__ starts, uint32
   for (uint32_t sg = 0; sg < n_segs; ++sg) {
     const unsigned long long* st = starts + (size_t)sg * (n_regions + 1);
     for (unsigned long long b = st[r]; b < st[r + 1]; b += kHotSlice)
-      tasks[t++] = HotTask{b, min(b + kHotSlice, st[r + 1]), r, 0u};
+      tasks[t++] = HotTask{b, min(b + kHotSlice, st[r + 1]), r, sg};
   }
 }
 
@@ -2437,6 +2442,7 @@ __global__ __launch_bounds__(1024) void k_hot_combine(const Rec* __restrict__ re
           if (kPass == 2 && have) {
             const unsigned long long P = A.thresh[r.kB >> 32];
             if (P == RSA_NO_THRESHOLD || r.order > P) have = false;
+            if (T.pad == A.late_seg && !A.replay[r.kB >> 32]) have = false;   // (selective recount)
           }
           lds_agg_insert<kE, kPass == 1>(e_kA, e_kB, e_mo, e_first, e_last, e_cnt, used, have, r.kA, r.kB, r.order,
                                          r.ts, r.ts, 1u);
@@ -2557,23 +2563,29 @@ __global__ void k_table_init(Slot* S, unsigned long long cap) {
 // [0]: some rule under a filter bound got a threshold other than the bound;
 // [1]: some rule without a bound is capped now.
 __global__ void k_tent_check(const unsigned long long* filter, const unsigned long long* thresh, uint32_t n_rules,
-                             uint32_t* out) {
+                             uint32_t* out, uint8_t* replay) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= n_rules) return;
   const unsigned long long f = filter[g], t = thresh[g];
-  if (f != RSA_NO_THRESHOLD && t != f) atomicAdd(&out[0], 1u);   // counts (RSA_DEBUG prints them)
-  if (f == RSA_NO_THRESHOLD && t != RSA_NO_THRESHOLD) atomicAdd(&out[1], 1u);
+  const bool moved = f != RSA_NO_THRESHOLD && t != f, now = f == RSA_NO_THRESHOLD && t != RSA_NO_THRESHOLD;
+  if (moved) atomicAdd(&out[0], 1u);   // counts (RSA_DEBUG prints them)
+  if (now) atomicAdd(&out[1], 1u);
+  // the rules whose last-slice pass-2 fields are not exact: their entries are
+  // cleared and all their records replayed (the others' late records are not)
+  if (replay) replay[g] = (moved || now) ? 1u : 0u;
 }
 
 // The pass-2 fields of every used slot back to empty (the last slice's
 // tentative counts are replayed by a full recount).
 __global__ void k_pass2_clear(Slot* S, const unsigned long long* used, const unsigned long long* n_p,
-                              unsigned long long cap) {
+                              unsigned long long cap, const uint8_t* replay = nullptr) {
   unsigned long long n = *n_p;
   if (n > cap) n = cap;
   const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
   for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    Slot* s = &S[(uint32_t)used[i]];
+    const unsigned long long u = used[i];
+    if (replay && !replay[(uint32_t)(u >> 32)]) continue;   // (selective: only the replayed rules' entries)
+    Slot* s = &S[(uint32_t)u];
     s->count2 = 0;
     s->first2 = 0xFFFFFFFFu;
     s->last2 = 0;
@@ -3297,6 +3309,10 @@ struct rsa_ctx {
   bool tent2_on = false;                    // the current pass-1 launch is the last slice after the filter steps
   uint32_t late_seg = 0xFFFFFFFFu;          // its record segment (pass-2 fields of filtered rules hold its records)
   uint32_t tent_skip = 0;                   // jobs left without the tentative pass-2 fields (set when they missed)
+  bool recount_selective = true;            // RSA_OPT_RECOUNT_SELECTIVE
+  uint8_t* d_replay = nullptr;              // per rule: replay its late-slice records (k_tent_check)
+  uint32_t replay_alloc = 0;
+  uint32_t replay_seg = 0xFFFFFFFFu;        // the segment the recount filters by d_replay (0xFFFFFFFF: none)
   uint32_t* d_chk = nullptr;                // [0] a filtered rule's threshold moved, [1] a rule capped only now
   int parse_mode = 2;                       // RSA_OPT_PARSE_MODE (textparse.hip): register-window reads
   bool region_import = true;                // RSA_OPT_REGION_IMPORT: rsa_import by region sort + k_reduce
@@ -3458,6 +3474,8 @@ Agg agg_of(const rsa_ctx* c) {
   a.rs_bits = c->rs_bits;
   a.np_bits = c->np_bits;
   a.tent2 = c->tent2_on ? 1u : 0u;
+  a.replay = c->d_replay;
+  a.late_seg = c->replay_seg;
   return a;
 }
 
@@ -4156,7 +4174,7 @@ int rsa_ctx_destroy(rsa_ctx* c) {
                   c->d_slots, c->d_used, c->d_ukey, c->d_used_n, c->d_filter, c->d_packed, c->d_hot, c->d_hot_tasks, c->d_hot_base,
                   c->d_hot_fill, c->d_hot_ctl, c->d_hot_total, c->d_cnt_words, c->d_cnt_starts,
                   c->d_cnt_tasks, c->d_cnt_ctl, c->d_flags, c->d_cursor, c->d_job_recs, c->d_cidx,
-                  c->d_capped_gid, c->d_capped_cnt, c->d_capped_start, c->d_capped_prev, c->d_keys, c->d_chk};
+                  c->d_capped_gid, c->d_capped_cnt, c->d_capped_start, c->d_capped_prev, c->d_keys, c->d_chk, c->d_replay};
   for (void* b : bufs) (void)hipFree(b);
   for (int k = 0; k < kMaxEvents; ++k)
     if (c->ev[k]) (void)hipEventDestroy(c->ev[k]);
@@ -4233,6 +4251,9 @@ int rsa_set_option(rsa_ctx* c, int option, int64_t value) {
       return RSA_OK;
     case RSA_OPT_COUNTER_WORDS16:
       c->gh16 = value != 0;
+      return RSA_OK;
+    case RSA_OPT_RECOUNT_SELECTIVE:
+      c->recount_selective = value != 0;
       return RSA_OK;
     case RSA_OPT_REGION_RECORDS:
       if (value < 0 || value > 0xFFFFFFFFll) return fail(c, RSA_ERR_ARG, "RSA_OPT_REGION_RECORDS must be 0..2^32-1");
@@ -4704,12 +4725,21 @@ int rsa_recount(rsa_ctx* c, const rsa_tuple* T, const uint32_t* TS, const uint64
   uint32_t n_segs = c->n_segs;
   const bool tent = c->late_seg != 0xFFFFFFFFu;
   bool clear = tent;
+  bool selective = false;
   const bool cached = c->rec_cache && c->cache_T == (const void*)T && c->cache_n == n && c->n_segs > 0;
   if (tent && cached && c->late_seg + 1 == c->n_segs && c->n_rules) {
     if (!c->d_chk) HIPCHK(c, hipMalloc(&c->d_chk, 2 * sizeof(uint32_t)));
+    if (c->recount_selective && c->replay_alloc < c->n_rules) {
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      hipFree(c->d_replay);
+      c->d_replay = nullptr;
+      c->replay_alloc = 0;
+      HIPCHK(c, hipMalloc(&c->d_replay, c->n_rules));
+      c->replay_alloc = c->n_rules;
+    }
     HIPCHK(c, hipMemsetAsync(c->d_chk, 0, 2 * sizeof(uint32_t), c->stream));
-    k_tent_check<<<(c->n_rules + kBlock - 1) / kBlock, kBlock, 0, c->stream>>>(c->d_filter, c->d_thresh, c->n_rules,
-                                                                                 c->d_chk);
+    k_tent_check<<<(c->n_rules + kBlock - 1) / kBlock, kBlock, 0, c->stream>>>(
+        c->d_filter, c->d_thresh, c->n_rules, c->d_chk, c->recount_selective ? c->d_replay : nullptr);
     uint32_t h[2] = {1u, 1u};
     HIPCHK(c, hipMemcpyAsync(h, c->d_chk, sizeof h, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -4717,13 +4747,20 @@ int rsa_recount(rsa_ctx* c, const rsa_tuple* T, const uint32_t* TS, const uint64
     if (!h[0] && !h[1]) {
       clear = false;
       n_segs = c->late_seg;   // the last slice is already counted
+    } else if (c->recount_selective) {
+      // only the rules whose bound moved or that were capped only now are
+      // cleared and replayed from the last slice; the others keep its exact
+      // pass-2 fields (no backoff: the next jobs keep the tentative fields)
+      selective = true;
     }
-    c->tent_skip = clear ? kTentBackoff : 0u;
+    c->tent_skip = clear && !selective ? kTentBackoff : 0u;
   }
   if (clear) {
-    k_pass2_clear<<<c->cu_count * 8, kBlock, 0, c->stream>>>(c->d_slots, c->d_used, c->d_used_n, c->slot_alloc);
+    k_pass2_clear<<<c->cu_count * 8, kBlock, 0, c->stream>>>(c->d_slots, c->d_used, c->d_used_n, c->slot_alloc,
+                                                            selective ? c->d_replay : nullptr);
     HIPCHK(c, hipGetLastError());
   }
+  c->replay_seg = selective ? c->late_seg : 0xFFFFFFFFu;
   c->late_seg = 0xFFFFFFFFu;   // (a second recount replays everything)
   if (cached) {
     // every occurrence with order <= P of a capped rule produced a pass-1
@@ -4741,8 +4778,10 @@ int rsa_recount(rsa_ctx* c, const rsa_tuple* T, const uint32_t* TS, const uint64
     k_reduce<2><<<1u << c->np_bits, 1024, 0, c->stream>>>(reinterpret_cast<const Rec*>(c->d_recs2), c->d_starts,
                                                          n_segs, agg_of(c), hb, hf, hr, skip);
     HIPCHK(c, hipGetLastError());
+    c->replay_seg = 0xFFFFFFFFu;
     return RSA_OK;
   }
+  c->replay_seg = 0xFFFFFFFFu;   // (the uncached recount replays every line)
   if (!G) {
     // re-classify into scratch gids
     if (!c->rules_loaded) return fail(c, RSA_ERR_STATE, "no rules loaded (recount without gids re-classifies)");
