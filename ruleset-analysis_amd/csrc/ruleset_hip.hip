@@ -3309,7 +3309,12 @@ struct rsa_ctx {
   bool tent2_on = false;                    // the current pass-1 launch is the last slice after the filter steps
   uint32_t late_seg = 0xFFFFFFFFu;          // its record segment (pass-2 fields of filtered rules hold its records)
   uint32_t tent_skip = 0;                   // jobs left without the tentative pass-2 fields (set when they missed)
-  bool recount_selective = true;            // RSA_OPT_RECOUNT_SELECTIVE
+  // RSA_OPT_RECOUNT_SELECTIVE: measured slower (cfg3 8.08 vs 8.00-8.04,
+  // cfg5 9.76 vs 9.60 ms/step, profiles/r05m_*): at cfg3 no bound moves and
+  // 173 rules are capped only in the last slice, so the recount still reads
+  // every record while every job pays the tentative fields, a host read and
+  // the selective clear
+  bool recount_selective = false;
   uint8_t* d_replay = nullptr;              // per rule: replay its late-slice records (k_tent_check)
   uint32_t replay_alloc = 0;
   uint32_t replay_seg = 0xFFFFFFFFu;        // the segment the recount filters by d_replay (0xFFFFFFFF: none)

@@ -269,7 +269,7 @@ def test_recount_after_moved_bounds_repeated_jobs(engine, selective):
                           int(r['count']), int(r['first']), int(r['last'])) for r in res.records)
             assert got == want
     finally:
-        engine.set_option(native.RSA_OPT_RECOUNT_SELECTIVE, 1)
+        engine.set_option(native.RSA_OPT_RECOUNT_SELECTIVE, 0)
     assert (ref['n_conns'] >= 40).sum() > 10
 
 
