@@ -676,23 +676,54 @@ constexpr int kBktMaxTables = 8;   // bucketindex.py MAX_TABLES
 // lane with more hit tables or candidates, or two tag-matching slots in one
 // table (an 11-bit tag collision), takes the serial form.  Typically one
 // global load per matched line, none for an unmatched one.
+// Image reads of the global (HBM) image are L2 round trips on the lane's
+// dependent chain, so that variant reads what it needs of a record or table
+// descriptor together, up front (kGlb); the LDS image re-reads words where
+// they are used (registers are its limit: 64 VGPRs at 8 waves per SIMD).
+// A/B switches (profiles/r05/ab_summary.txt, r05n; cfg4 ms per k_classify
+// launch): the first hit table's min_gid / entry_base kept from its probe
+// 0.912 -> 0.905 (default on); the list record's words read up front as well
+// costs the emission's order/timestamp prefetch its registers: 0.968 (1) and
+// 0.985 (2) with the prefetch off, 1.105 (2) with it on and VGPRs spilled.
+#ifndef RSA_GLB_REC
+#define RSA_GLB_REC 0    // global image: the list record's words read once, up front (2: also the residual range and continuation)
+#endif
+#ifndef RSA_GLB_DESC
+#define RSA_GLB_DESC 1   // global image: the first hit table's min_gid / entry_base kept from its probe
+#endif
 template <typename P32>
-__device__ __forceinline__ uint32_t bucket_lookup(const Rules& R, P32 img, uint32_t lw, uint32_t src, uint32_t dst,
-                                                  uint32_t ports, uint32_t best) {
+constexpr bool kGlobalImg = false;
+template <>
+constexpr bool kGlobalImg<const uint32_t*> = true;
+
+// toff / nt: the record's table descriptors and their count (words 0 and 1 of
+// the list record at lw).
+template <typename P32>
+__device__ __forceinline__ uint32_t bucket_lookup(const Rules& R, P32 img, uint32_t lw, uint32_t toff, uint32_t nt,
+                                                  uint32_t src, uint32_t dst, uint32_t ports, uint32_t best) {
 #if !RSA_BKT_PHASED
   return bucket_lookup_serial(R, img, lw, src, dst, ports, best);
 #else
-  const uint32_t toff = img[lw], nt = img[lw + 1];
+  constexpr bool kGlb = kGlobalImg<P32> && RSA_GLB_DESC;
   uint32_t h0 = 0u, h1 = 0u, h2 = 0u, h3 = 0u;   // hit slot words, in table order
   uint32_t tj = 0u;                              // their tables, 4 bits each (hit k at bits 4k)
   uint32_t nh = 0u;
+  // (global image) the first hit table's min_gid / entry_base, kept from the
+  // descriptor read of the probe (no second dependent read in (B') for the
+  // common single hit)
+  uint32_t g0 = 0u, e0 = 0u;
   bool slow = false;
 #pragma unroll
   for (int j = 0; j < kBktMaxTables; ++j) {
     if ((uint32_t)j < nt) {
       const uint32_t tw = toff + kBktTableWords * j;
       const v4u a = rd4(img, tw);
-      const uint32_t nb = img[tw + 4];
+      v4u d = {0u, 0u, 0u, 0u};   // n_buckets, filter_off, min_gid, entry_base
+      if (kGlb)
+        d = rd4(img, tw + 4);
+      else
+        d.x = img[tw + 4];
+      const uint32_t nb = d.x;
       const uint32_t h = bkt_hash(src & a.x, dst & a.y, ports & a.z, kBktSeedKey);
       const uint32_t b1 = umul24(h & 0xFFFFu, nb) >> 16;
       const uint32_t b2 = umul24(h >> 16, nb) >> 16;
@@ -712,6 +743,10 @@ __device__ __forceinline__ uint32_t bucket_lookup(const Rules& R, P32 img, uint3
         h1 = nh == 1u ? f : h1;
         h2 = nh == 2u ? f : h2;
         h3 = nh == 3u ? f : h3;
+        if (kGlb) {
+          g0 = nh == 0u ? d.z : g0;
+          e0 = nh == 0u ? d.w : e0;
+        }
         tj |= (uint32_t)j << (4 * (nh & 7u));
         ++nh;
       }
@@ -727,8 +762,14 @@ __device__ __forceinline__ uint32_t bucket_lookup(const Rules& R, P32 img, uint3
       const uint32_t ja = (tj >> (4 * p)) & 0xFu;
       const bool two = p + 1 < nh;
       const uint32_t jb = two ? (tj >> (4 * p + 4)) & 0xFu : ja;
-      const v2u ma = rd2(img, toff + kBktTableWords * ja + 6);   // min_gid, entry_base
-      const v2u mb = rd2(img, toff + kBktTableWords * jb + 6);
+      v2u ma, mb;   // min_gid, entry_base
+      if (kGlb && p == 0) {
+        ma = v2u{g0, e0};
+        mb = two ? rd2(img, toff + kBktTableWords * jb + 6) : ma;
+      } else {
+        ma = rd2(img, toff + kBktTableWords * ja + 6);
+        mb = rd2(img, toff + kBktTableWords * jb + 6);
+      }
       const uint32_t ea = ma.y + (wa & 0xFFFFu), eb = mb.y + ((two ? wb : wa) & 0xFFFFu);
       const v4u aa = R.residg[2 * (size_t)ea], ca = R.residg[2 * (size_t)ea + 1];
       const v4u ab = R.residg[2 * (size_t)eb], cb = R.residg[2 * (size_t)eb + 1];
@@ -817,10 +858,26 @@ __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Ru
     return active ? best : kNoGid;
   }
   // list record fields (include/ruleset_hip.h rsa_pht_list) are read from the
-  // image where they are used: lw = the lane's current record
+  // image where they are used: lw = the lane's current record.  The global
+  // image's words are read together, once per record (kGlb: rc0 = words 0-1,
+  // rc1 = 4-5, rc4 = 16-17, the prefix length and after_min at once; records
+  // are 4-word aligned)
+  constexpr bool kGlb = kGlobalImg<P32> && RSA_GLB_REC;
   uint32_t lw = R.list_off + kListWords * (active ? list : 0u);
+  v2u rc0 = {0u, 0u}, rc1 = rc0, rc4 = rc0;
+  uint32_t rc_pre = 0u, rc_min = 0u;
+  constexpr bool kGlb2 = kGlb && RSA_GLB_REC >= 2;   // the residual range and continuation too
+  if (kGlb) {
+    rc0 = rd2(img, lw);
+    rc_pre = img[lw + 6];
+    rc_min = img[lw + 15];
+  }
+  if (kGlb2) {
+    rc1 = rd2(img, lw + 4);
+    rc4 = rd2(img, lw + 16);
+  }
   // 1. prefix scans
-  const uint32_t pre_n = active ? img[lw + 6] : 0u;
+  const uint32_t pre_n = active ? (kGlb ? rc_pre : img[lw + 6]) : 0u;
   PH(0);
   unsigned long long pending = __ballot(active && pre_n != 0);
   while (pending) {
@@ -836,11 +893,11 @@ __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Ru
   // 2. per record of the lane's chain: the index (per lane), then the residual
   // scan (waterfall over the records present); the next chunk only while the
   // lane's best exceeds its smallest gid
-  bool go = active && best > img[lw + 15];
+  bool go = active && best > (kGlb ? rc_min : img[lw + 15]);
   bool deferred = false;
   PH(1);
   while (__ballot(go)) {
-    const bool ix = go && img[lw + 1] != 0;
+    const bool ix = go && (kGlb ? rc0.y : img[lw + 1]) != 0;
     uint32_t c = kNoGid;
     if (kMode == 2) {
       // partial-key bucket index: exact, never deferred
@@ -848,7 +905,7 @@ __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Ru
         if (R.force_defer) {
           c = kDefer;
         } else {
-          c = bucket_lookup(R, img, lw, t.x, t.y, t.z, best);
+          c = bucket_lookup(R, img, lw, kGlb ? rc0.x : img[lw], kGlb ? rc0.y : img[lw + 1], t.x, t.y, t.z, best);
         }
       }
     } else if (kMode == 1) {
@@ -864,7 +921,7 @@ __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Ru
         best = min(best, c);
       }
     }
-    const uint32_t rb = go ? img[lw + 4] : 0u, re = go ? img[lw + 5] : 0u;
+    const uint32_t rb = go ? (kGlb2 ? rc1.x : img[lw + 4]) : 0u, re = go ? (kGlb2 ? rc1.y : img[lw + 5]) : 0u;
     const bool want = go && rb < re;
     pending = __ballot(want);
     while (pending) {
@@ -877,9 +934,14 @@ __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Ru
       if (mine) best = b;
     }
     if (go) {
-      const uint32_t next = img[lw + 16];
-      go = next != RSA_PHT_NONE && best > img[lw + 17];
+      const uint32_t next = kGlb2 ? rc4.x : img[lw + 16];
+      go = next != RSA_PHT_NONE && best > (kGlb2 ? rc4.y : img[lw + 17]);
       if (go) lw = R.list_off + kListWords * next;
+      if (kGlb && go) rc0 = rd2(img, lw);   // the continuation record's words
+      if (kGlb2 && go) {
+        rc1 = rd2(img, lw + 4);
+        rc4 = rd2(img, lw + 16);
+      }
     }
     PH(6);
   }
@@ -1973,7 +2035,11 @@ constexpr int kRegionMaxBits = RSA_REGION_MAX_BITS;   // region <= 2^16 slots (b
 // region's records may lie in several segments (one per pass-1 launch):
 // starts[s * (n_regions + 1) + r] .. starts[s * (n_regions + 1) + r + 1].
 constexpr int kMaxSegs = 16;
-constexpr int kHotTries = 2, kHotMin = 8;
+#ifndef RSA_HOT_TRIES
+#define RSA_HOT_TRIES 1   // lds_agg_insert_lane: wave-combining tries for keys shared by >= kHotMin lanes
+                          // (r05o: 2 -> 1 cfg5 9.63 -> 9.45 ms/step, cfg3 within noise; 0: cfg5 10.28)
+#endif
+constexpr int kHotTries = RSA_HOT_TRIES, kHotMin = 8;
 __device__ __forceinline__ unsigned long long readlane64(unsigned long long v, int l) {
   return ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) |
          __builtin_amdgcn_readlane((uint32_t)v, l);
