@@ -558,7 +558,7 @@ def rank_main(args, rank, world, local):
     phase_prof = os.environ.get('RSA_PHASE_PROF') == '1'   # PROFILING: a -DRSA_PHASE_PROF library variant
     if phase_prof:
         import ctypes
-        ph = (ctypes.c_uint64 * 9)()
+        ph = (ctypes.c_uint64 * 13)()
         eng.ctx.call('rsa_phase_prof', ph, ctypes.c_int(1))
     if dist is not None:
         dist.barrier()
@@ -574,6 +574,9 @@ def rank_main(args, rank, world, local):
         names = ['tuple+list', 'prefix', 'pruning', 'group0', 'tasks', 'verify', 'resid+chain', 'emit']
         log('phase_prof cycles/wave-iteration: ' + json.dumps(
             {nm: round(v[k] / max(v[8], 1), 1) for k, nm in enumerate(names)}) + ' iterations %d' % v[8])
+        log('phase_prof k_reduce<1> cycles/workgroup: ' + json.dumps(
+            {nm: round(v[9 + k] / max(v[12], 1), 1) for k, nm in enumerate(('setup', 'insert', 'flush'))}) +
+            ' workgroups %d' % v[12])
     if dist is not None:
         dist.barrier()
     dt = time.perf_counter() - t0

@@ -299,7 +299,9 @@ __device__ __forceinline__ uint32_t pht_probe(P32 img, uint32_t H, v4u b) {
 struct PhaseAcc {
   unsigned long long last, acc[8];
 };
-__device__ unsigned long long g_phase[9];
+// [0..7] classifier phases, [8] its wave iterations; [9..11] k_reduce<1>
+// workgroup cycles in setup, record inserts and flushes, [12] its workgroups
+__device__ unsigned long long g_phase[13];
 #define RSA_PH_PARAM , PhaseAcc& ph
 #define RSA_PH_ARG , ph
 #define PH(k)                                                      \
@@ -2150,6 +2152,11 @@ static_assert(sizeof(HRec) == 40, "hot record layout");
 #ifndef RSA_COUNT_PER_CU
 #define RSA_COUNT_PER_CU 1   // k_count workgroups per CU (one is resident: 104 KiB LDS); fewer workgroups, fewer histogram-flush atomics
 #endif
+#ifndef RSA_RED_PF
+#define RSA_RED_PF 0   // A/B builds: k_reduce loads the next block step's record one step ahead (across rounds and
+                       // flushes); measured slower (r05r: cfg3 7.98 -> 8.04, cfg5 9.46 -> 9.58, cfg4 10.62 -> 10.69
+                       // ms/step): the inserts wait on LDS atomics and barriers, not on the record loads
+#endif
 #ifndef RSA_RED2_WPE
 #define RSA_RED2_WPE 8   // pass 2: 64 VGPRs, two 1024-thread workgroups per CU (73 KiB LDS each)
 #endif
@@ -2172,6 +2179,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
   // skip_zero: the device-side count of capped rules (a recount after a cap
   // resolution whose count the host did not read): none, nothing to recount
   if (skip_zero && *skip_zero == 0) return;   // workgroup-uniform
+#ifdef RSA_PHASE_PROF
+  const unsigned long long rp_t0 = __builtin_amdgcn_s_memtime();
+#endif
   const uint32_t region = blockIdx.x;
   const uint32_t n_regions = 1u << A.np_bits;
   // a hot region's records were pre-combined by k_hot_combine: read those
@@ -2195,9 +2205,31 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
   for (uint32_t e = threadIdx.x; e < kE; e += blockDim.x) e_kB[e] = kEmpty;
   if (threadIdx.x == 0) used = 0;
   __syncthreads();
+#ifdef RSA_PHASE_PROF
+  // PROFILING BUILD ONLY: wave 0's wall cycles per phase (the phases end at
+  // workgroup barriers, so one wave's clock is the workgroup's)
+  unsigned long long rp_t = __builtin_amdgcn_s_memtime(), rp_acc[3] = {0ull, 0ull, 0ull};
+  rp_acc[0] = rp_t - rp_t0;
+#define RP(k)                                                     \
+  do {                                                            \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();   \
+    rp_acc[k] += t_ - rp_t;                                       \
+    rp_t = t_;                                                    \
+  } while (0)
+#else
+#define RP(k) \
+  do {        \
+  } while (0)
+#endif
   uint32_t sg = 0;
   unsigned long long pos = is_hot ? hot_base[region] : starts[region];
   unsigned long long end = is_hot ? pos + total_recs : starts[region + 1];
+  // (RSA_RED_PF) this thread's record of the next block step -- or of the
+  // next round's first, loaded before the round-end barrier and the flush --
+  // read one step ahead: pf_at = its index in recs (kEmpty: none)
+  const uint4* R4 = reinterpret_cast<const uint4*>(recs);
+  uint4 pf0 = {0u, 0u, 0u, 0u}, pf1 = pf0;
+  unsigned long long pf_at = kEmpty;
   while (true) {
     while (pos >= end && sg + 1 < n_segs) {   // workgroup-uniform: next segment
       ++sg;
@@ -2224,6 +2256,28 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
             last = hr.last;
             cnt = hr.cnt;
           }
+        } else if (RSA_RED_PF) {
+          uint4 a = pf0, b = pf1;
+          const bool hit = pf_at == pos + j;
+          if (have && !hit) {
+            a = R4[2 * (pos + j)];
+            b = R4[2 * (pos + j) + 1];
+          }
+          // the next step's (or next round's first block's) record, in flight
+          // during this step's inserts
+          const unsigned long long nj = (jb + blockDim.x < take ? pos + jb + blockDim.x : pos + take) + threadIdx.x;
+          pf_at = kEmpty;
+          if (nj < end) {
+            pf0 = R4[2 * nj];
+            pf1 = R4[2 * nj + 1];
+            pf_at = nj;
+          }
+          if (have) {
+            kA = ((unsigned long long)a.y << 32) | a.x;
+            kB = ((unsigned long long)a.w << 32) | a.z;
+            mo = ((unsigned long long)b.y << 32) | b.x;
+            first = last = b.z;
+          }
         } else {
           if (have) {
             const Rec r = recs[pos + j];
@@ -2232,13 +2286,13 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
             mo = r.order;
             first = last = r.ts;
           }
-          if (kPass == 2 && have) {   // (hot records of pass 2 were filtered when combined)
-            const unsigned long long P = A.thresh[kB >> 32];
-            if (P == RSA_NO_THRESHOLD || mo > P) have = false;
-            // selective recount: the last slice's records of rules whose
-            // pass-2 fields it already filled exactly are not replayed
-            if (sg == A.late_seg && !A.replay[kB >> 32]) have = false;
-          }
+        }
+        if (kPass == 2 && !is_hot && have) {   // (hot records of pass 2 were filtered when combined)
+          const unsigned long long P = A.thresh[kB >> 32];
+          if (P == RSA_NO_THRESHOLD || mo > P) have = false;
+          // selective recount: the last slice's records of rules whose
+          // pass-2 fields it already filled exactly are not replayed
+          if (sg == A.late_seg && !A.replay[kB >> 32]) have = false;
         }
         lds_agg_insert<kE, kPass == 1>(e_kA, e_kB, e_mo, e_first, e_last, e_cnt, used, have, kA, kB, mo,
                                                  first, last, cnt);
@@ -2248,6 +2302,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
       bool more = pos < end;
       for (uint32_t q = sg + 1; q < n_segs && !more; ++q)
         more = starts[(size_t)q * (n_regions + 1) + region + 1] > starts[(size_t)q * (n_regions + 1) + region];
+      RP(1);
       if (used + 512u <= (3u * kE) / 4 && more) continue;   // workgroup-uniform: room for 512 more
     }
     if (used > 0) {   // workgroup-uniform (read after a barrier)
@@ -2404,11 +2459,19 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
       }
       if (threadIdx.x == 0) used = 0;
       __syncthreads();
+      RP(2);
     }
     if (last_round) break;
   }
   if (kPass == 1)
     for (uint32_t w = threadIdx.x; w < words; w += blockDim.x) gocc[w] = occ[w];
+#ifdef RSA_PHASE_PROF
+  if (kPass == 1 && threadIdx.x == 0) {
+    for (int k = 0; k < 3; ++k) atomicAdd(&g_phase[9 + k], rp_acc[k]);
+    atomicAdd(&g_phase[12], 1ull);
+  }
+#endif
+#undef RP
 }
 
 // ---- hot regions (skewed traffic: a few connections on most lines, BASELINE
@@ -5007,13 +5070,14 @@ int rsa_shadowed_ports(rsa_ctx* c, const rsa_shadow_rule* h_rules, uint32_t n, c
 
 #ifdef RSA_PHASE_PROF
 // PROFILING BUILD ONLY: the classifier's phase cycles (see PhaseAcc): out[0..7]
-// summed wave cycles per phase, out[8] wave iterations.
+// summed wave cycles per phase, out[8] wave iterations; out[9..12] k_reduce<1>'s
+// (g_phase).
 int rsa_phase_prof(rsa_ctx* c, uint64_t* h_out, int reset) {
   if (!c || !h_out) return RSA_ERR_ARG;
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  HIPCHK(c, hipMemcpyFromSymbol(h_out, HIP_SYMBOL(g_phase), 9 * sizeof(uint64_t)));
+  HIPCHK(c, hipMemcpyFromSymbol(h_out, HIP_SYMBOL(g_phase), 13 * sizeof(uint64_t)));
   if (reset) {
-    const uint64_t z[9] = {};
+    const uint64_t z[13] = {};
     HIPCHK(c, hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof z));
   }
   return RSA_OK;
