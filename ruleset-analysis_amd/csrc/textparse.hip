@@ -504,9 +504,25 @@ __global__ __launch_bounds__(kParseWG) RSA_PARSE_WIN_ATTR void k_parse_win(const
 // The deferred lines, densely packed: the general parse (the regexes'
 // backtracking restated), reading from HBM.  Persistent grid over the
 // device-side count.
-constexpr uint32_t kSlowGrid = 2048;
+// k_parse_slow's lanes each walk their lines through dependent 4-byte loads,
+// so more resident waves hide more of that latency: at 6 waves per SIMD (80
+// VGPRs) and 3072 workgroups the parse step of a 30M-line job takes 10.41-10.52
+// ms against 10.84 at the compiler's 102 VGPRs (4 waves, 2048 workgroups); 8
+// waves (64 VGPRs) gains nothing (tools/ab_text.sh, profiles/r05/ab_summary.txt r05s)
+#ifndef RSA_SLOW_WAVES
+#define RSA_SLOW_WAVES 6   // minimum waves per SIMD for k_parse_slow (register cap; 0 = compiler's choice)
+#endif
+#ifndef RSA_SLOW_GRID
+#define RSA_SLOW_GRID 3072
+#endif
+#if RSA_SLOW_WAVES
+#define RSA_SLOW_ATTR __attribute__((amdgpu_waves_per_eu(RSA_SLOW_WAVES, 8)))
+#else
+#define RSA_SLOW_ATTR
+#endif
+constexpr uint32_t kSlowGrid = RSA_SLOW_GRID;
 template <bool kReduce>
-__global__ __launch_bounds__(kParseWG) void k_parse_slow(const uint8_t* __restrict__ text,
+__global__ __launch_bounds__(kParseWG) RSA_SLOW_ATTR void k_parse_slow(const uint8_t* __restrict__ text,
                                                          const uint64_t* __restrict__ off, uint64_t n_lines,
                                                          const rsa_parse_ifc* __restrict__ ifcs, uint32_t n_ifcs,
                                                          const rsa_parse_spell* __restrict__ spells, uint32_t n_spells,
