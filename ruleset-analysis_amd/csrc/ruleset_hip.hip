@@ -381,6 +381,9 @@ __device__ __forceinline__ unsigned long long prune_side(P32 img, uint32_t moff,
   return acc;
 }
 
+#ifndef RSA_PRUNE_U
+#define RSA_PRUNE_U 4   // pruning masks per batch (all their LDS reads in flight together)
+#endif
 // lw: the lane's list record {group_off, n_groups, mask_off, n_masks}, {…,
 // bm_off}, {src_any, dst_any}, n_src_masks at word 18.
 template <bool kNarrow, typename P32>
@@ -392,8 +395,8 @@ __device__ __forceinline__ unsigned long long index_candidates(P32 img, uint32_t
   const uint32_t bm_off = img[lw + 7];
   const uint32_t nm = h0.w, ns = img[lw + 18];   // the first ns records are the src tables
   if (kNarrow) {
-    S |= prune_side<true, 4>(img, h0.z, 0u, ns, src, kSaltS, bm_off);
-    D |= prune_side<true, 4>(img, h0.z, ns, nm, dst, kSaltD, bm_off);
+    S |= prune_side<true, RSA_PRUNE_U>(img, h0.z, 0u, ns, src, kSaltS, bm_off);
+    D |= prune_side<true, RSA_PRUNE_U>(img, h0.z, ns, nm, dst, kSaltD, bm_off);
   } else {   // (rare: a list with more than 255 distinct group bitmaps) one mask at a time
     S |= prune_side<false, 1>(img, h0.z, 0u, ns, src, kSaltS, bm_off);
     D |= prune_side<false, 1>(img, h0.z, ns, nm, dst, kSaltD, bm_off);
