@@ -179,6 +179,7 @@ typedef struct rsa_pht_list {    /* 80 B: one list (or one chained chunk of a li
 #define RSA_OPT_FILTER_STEPS 7 /* auto filter: bound refinements, each after RSA_OPT_FILTER_GROWTH x the previous lines (default 3) */
 #define RSA_OPT_FILTER_GROWTH 24 /* auto filter: lines of each bound refinement's slice over the previous ones (default 4) */
 #define RSA_OPT_COUNT_STREAM 25 /* per-rule line/hit counting on a second HIP stream, overlapping the record merge (default 0) */
+#define RSA_OPT_CLASSIFY_PAIR 28 /* the global-memory bucket index (lists too large for LDS) classifies two lines per lane (1, default) or one (0) */
 #define RSA_OPT_RECOUNT_SELECTIVE 27 /* recount after a job whose thresholds moved below some bounds: only those rules' last-slice records are replayed (1) instead of every record with a backoff (0, default) */
 #define RSA_OPT_COUNTER_WORDS16 26 /* 16-bit gid|hit words between classification and counting when every gid fits 15 bits and the LDS histogram holds the rules (1, default) */
 #define RSA_OPT_FORCE_DEFER 8  /* TESTING: every index candidate goes to the exact deferred-line path        */

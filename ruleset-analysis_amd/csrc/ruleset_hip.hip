@@ -1128,6 +1128,204 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t* sh, uint3
   return before + x - v;
 }
 
+// ---- two lines per lane: the global bucket image (BASELINE config 4) ------
+// The global-image classifier is latency bound (VALU busy 0.16): a lane's
+// chain -- list record, table descriptors, bucket slots, bucket rows, the
+// rule's filter bound -- is a series of dependent L2/HBM round trips, and
+// occupancy is already at 8 waves per SIMD.  k_classify_pair gives each lane
+// two lines and runs their chains side by side: the probes of both lines'
+// tables are issued together (addresses selected, not branched, so the loads
+// share one basic block), then both lines' first bucket rows, then both
+// filter bounds before either line's stores.  Same answers as classify_wave
+// (the minimum gid over the same candidate rows; the early exits only skip
+// rows whose first gid cannot beat the lane's best).
+
+// The prefix scan of classify_wave for the lanes with `active` (waterfall over
+// the lists present).
+__device__ __forceinline__ void prefix_scan_wave(const Rules& R, uint32_t list, bool active, uint32_t pre_n, uint4 t,
+                                                 uint32_t& best) {
+  unsigned long long pending = __ballot(active && pre_n != 0);
+  while (pending) {
+    const int leader = __builtin_ctzll(pending);
+    const uint32_t L = __builtin_amdgcn_readlane(list, leader);
+    const bool mine = active && list == L;
+    pending &= ~__ballot(mine);
+    const uint32_t beg = R.off[L];
+    const uint32_t pre = __builtin_amdgcn_readlane(pre_n, leader);
+    const uint32_t b = scan_list(R.e, beg, beg + pre, mine, kNoGid, t.x, t.y, t.z);
+    if (mine) best = b;
+  }
+}
+
+// The residual scan of record lw for the lanes with `go` (waterfall over the
+// records present).
+template <typename P32>
+__device__ __forceinline__ void resid_scan_wave(const Rules& R, P32 img, bool go, uint32_t lw, uint4 t, uint32_t& best) {
+  const uint32_t rb = go ? img[lw + 4] : 0u, re = go ? img[lw + 5] : 0u;
+  const bool want = go && rb < re;
+  unsigned long long pending = __ballot(want);
+  while (pending) {
+    const int leader = __builtin_ctzll(pending);
+    const uint32_t Q = __builtin_amdgcn_readlane(lw, leader);
+    const bool mine = want && lw == Q;
+    pending &= ~__ballot(mine);
+    const uint32_t b = scan_list(R.resid, __builtin_amdgcn_readlane(rb, leader), __builtin_amdgcn_readlane(re, leader),
+                                 mine, best, t.x, t.y, t.z);
+    if (mine) best = b;
+  }
+}
+
+// One lane's tag-matching bucket slots (bucket_lookup's phase A state).
+struct BktHits {
+  uint32_t h0, h1, h2, h3;   // hit slot words, in table order
+  uint32_t tj;               // their tables, 4 bits each
+  uint32_t nh;
+  uint32_t g0, e0;           // the first hit table's min_gid / entry_base
+  uint32_t slow;             // two matching slots in one table: the serial form
+};
+
+// Table j of the record whose descriptors start at toff, for a lane with
+// `on`; a lane without (no table j, or no lookup) reads the image header
+// instead (word 0.., one bucket at word 0) and records nothing, so every lane
+// issues the same loads.
+__device__ __forceinline__ void bkt_probe_j(const uint32_t* img, uint32_t toff, bool on, uint32_t j, uint32_t src,
+                                            uint32_t dst, uint32_t ports, BktHits& H) {
+  const uint32_t tw = on ? toff + kBktTableWords * j : 0u;
+  const v4u a = rd4(img, tw);
+  const v4u d = rd4(img, tw + 4);   // n_buckets, filter_off, min_gid, entry_base
+  const uint32_t nb = on ? d.x : 1u;
+  const uint32_t h = bkt_hash(src & a.x, dst & a.y, ports & a.z, kBktSeedKey);
+  const uint32_t b1 = umul24(h & 0xFFFFu, nb) >> 16;
+  const uint32_t b2 = umul24(h >> 16, nb) >> 16;
+  const uint32_t tag = ((h >> 16) ^ h) & kBktTagMask;
+  const uint32_t bo = on ? a.w : 0u;
+  const v2u s1 = rd2(img, bo + 2 * b1), s2 = rd2(img, bo + 2 * b2);
+  const uint32_t sl[4] = {s1.x, s1.y, s2.x, s2.y};
+  uint32_t f = 0u, slow = 0u;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t w = sl[q];
+    const bool m = on && ((w >> 16) & kBktLenMask) != 0u && (w >> 21) == tag && !(q >= 2 && b2 == b1);
+    slow |= (m && f != 0u) ? 1u : 0u;
+    f = (m && f == 0u) ? w : f;
+  }
+  H.slow |= slow;
+  if (f) {
+    H.h0 = H.nh == 0u ? f : H.h0;
+    H.h1 = H.nh == 1u ? f : H.h1;
+    H.h2 = H.nh == 2u ? f : H.h2;
+    H.h3 = H.nh == 3u ? f : H.h3;
+    H.g0 = H.nh == 0u ? d.z : H.g0;
+    H.e0 = H.nh == 0u ? d.w : H.e0;
+    H.tj |= j << (4 * (H.nh & 7u));
+    ++H.nh;
+  }
+}
+
+// Hit k's bucket rows for one lane (bucket_lookup's (B') for one hit): the
+// first row loaded by the caller (ra, rc), the rest of the bucket scanned.
+__device__ __forceinline__ uint32_t bkt_rows(const Rules& R, v2u ge, uint32_t w, v4u ra, v4u rc, uint32_t src,
+                                             uint32_t dst, uint32_t ports, uint32_t best) {
+  if (best > ge.x) {
+    if (rc.z < best && entry_match(ra, rc, src, dst, ports)) best = min(best, entry_gid(rc, ports));
+    const uint32_t len = (w >> 16) & kBktLenMask;
+    const uint32_t e = ge.y + (w & 0xFFFFu);
+    if (len > 1u) best = scan_bucket(R.residg, e + 1, e + len, best, src, dst, ports);
+  }
+  return best;
+}
+
+__device__ __forceinline__ uint32_t hit_word(const BktHits& H, uint32_t k) {
+  return k == 0u ? H.h0 : k == 1u ? H.h1 : k == 2u ? H.h2 : H.h3;
+}
+
+// Both lines' bucket lookups (no row filters; the global image).  ia / ib:
+// the lanes whose line looks the record up; returns their new bests.
+__device__ __forceinline__ void bucket_lookup_pair(const Rules& R, const uint32_t* img, uint32_t lwa, bool ia, uint4 ta,
+                                                   uint32_t& besta, uint32_t lwb, bool ib, uint4 tb, uint32_t& bestb) {
+  const uint32_t toffa = img[lwa], nta = ia ? img[lwa + 1] : 0u;
+  const uint32_t toffb = img[lwb], ntb = ib ? img[lwb + 1] : 0u;
+  BktHits A = {}, B = {};
+#pragma unroll
+  for (uint32_t j = 0; j < (uint32_t)kBktMaxTables; ++j) {
+    const bool pa = j < nta, pb = j < ntb;
+    if (!__ballot(pa || pb)) break;   // wave-uniform: no lane has a table j
+    bkt_probe_j(img, toffa, pa, j, ta.x, ta.y, ta.z, A);
+    bkt_probe_j(img, toffb, pb, j, tb.x, tb.y, tb.z, B);
+  }
+  // (rare) two matching slots in one table, or more than four hit tables
+  const bool sa = ia && (A.slow || A.nh > 4u), sb = ib && (B.slow || B.nh > 4u);
+  if (sa) besta = bucket_lookup_serial(R, img, lwa, ta.x, ta.y, ta.z, besta);
+  if (sb) bestb = bucket_lookup_serial(R, img, lwb, tb.x, tb.y, tb.z, bestb);
+  const uint32_t na = (ia && !sa) ? A.nh : 0u, nb = (ib && !sb) ? B.nh : 0u;
+  for (uint32_t k = 0; __ballot(k < na || k < nb); ++k) {
+    const bool oa = k < na, ob = k < nb;
+    const uint32_t wa = hit_word(A, k), wb = hit_word(B, k);
+    v2u ga = {A.g0, A.e0}, gb = {B.g0, B.e0};
+    if (k > 0u) {   // (a second hit table: its min_gid / entry_base)
+      ga = oa ? rd2(img, toffa + kBktTableWords * ((A.tj >> (4 * k)) & 0xFu) + 6) : ga;
+      gb = ob ? rd2(img, toffb + kBktTableWords * ((B.tj >> (4 * k)) & 0xFu) + 6) : gb;
+    }
+    // both first rows in flight together (a lane without a hit reads row 0)
+    const uint32_t ea = oa ? ga.y + (wa & 0xFFFFu) : 0u, eb = ob ? gb.y + (wb & 0xFFFFu) : 0u;
+    const v4u aa = R.residg[2 * (size_t)ea], ca = R.residg[2 * (size_t)ea + 1];
+    const v4u ab = R.residg[2 * (size_t)eb], cb = R.residg[2 * (size_t)eb + 1];
+    if (oa) besta = bkt_rows(R, ga, wa, aa, ca, ta.x, ta.y, ta.z, besta);
+    if (ob) bestb = bkt_rows(R, gb, wb, ab, cb, tb.x, tb.y, tb.z, bestb);
+  }
+}
+
+// classify_wave<false, 2, false> for two lines per lane (global bucket image,
+// no row filters).
+__device__ __forceinline__ void classify_pair_bkt(uint4 ta, bool aa, uint4 tb, bool ab, const Rules& R,
+                                                  const uint32_t* img, unsigned int* flags, uint32_t& ga,
+                                                  uint32_t& gb) {
+  const uint32_t la = ta.w & 0xFFFFu, lb = tb.w & 0xFFFFu;
+  if (aa && la >= R.n_lists) {
+    atomicOr(&flags[1], 1u);
+    aa = false;
+  }
+  if (ab && lb >= R.n_lists) {
+    atomicOr(&flags[1], 1u);
+    ab = false;
+  }
+  uint32_t besta = kNoGid, bestb = kNoGid;
+  uint32_t lwa = R.list_off + kListWords * (aa ? la : 0u), lwb = R.list_off + kListWords * (ab ? lb : 0u);
+  const uint32_t prea = aa ? img[lwa + 6] : 0u, preb = ab ? img[lwb + 6] : 0u;
+  const uint32_t mina = img[lwa + 15], minb = img[lwb + 15];
+  prefix_scan_wave(R, la, aa, prea, ta, besta);
+  prefix_scan_wave(R, lb, ab, preb, tb, bestb);
+  bool goa = aa && besta > mina, gob = ab && bestb > minb;
+  bool defa = false, defb = false;
+  while (__ballot(goa || gob)) {
+    const bool ixa = goa && img[lwa + 1] != 0, ixb = gob && img[lwb + 1] != 0;
+    if (!(R.prof & 1)) {
+      if (R.force_defer) {
+        defa = defa || ixa;
+        defb = defb || ixb;
+      } else {
+        bucket_lookup_pair(R, img, lwa, ixa, ta, besta, lwb, ixb, tb, bestb);
+      }
+    }
+    if (ixa && defa) goa = false;
+    if (ixb && defb) gob = false;
+    resid_scan_wave(R, img, goa, lwa, ta, besta);
+    resid_scan_wave(R, img, gob, lwb, tb, bestb);
+    if (goa) {
+      const uint32_t next = img[lwa + 16];
+      goa = next != RSA_PHT_NONE && besta > img[lwa + 17];
+      if (goa) lwa = R.list_off + kListWords * next;
+    }
+    if (gob) {
+      const uint32_t next = img[lwb + 16];
+      gob = next != RSA_PHT_NONE && bestb > img[lwb + 17];
+      if (gob) lwb = R.list_off + kListWords * next;
+    }
+  }
+  ga = defa ? kDefer : (aa ? besta : kNoGid);
+  gb = defb ? kDefer : (ab ? bestb : kNoGid);
+}
+
 // Where pass 1 puts its per-line results (k_classify / k_tail with kEmit),
 // without appends to shared cursors (no atomics or workgroup barriers in the
 // classifier): the line's gid|hit word for the per-rule counters (k_count);
@@ -1205,16 +1403,19 @@ __device__ __forceinline__ void classify_emit_args(const EmitPack& ep_arg, Agg& 
 
 // The record of one line, or false (need).  kPre: the line's order and
 // timestamp were loaded ahead (o_pre, ts_pre; RSA_PREFETCH_T 2).
-template <bool kPre = false>
+// kPreF: the rule's filter bound was loaded ahead too (f_pre; k_classify_pair
+// loads both lines' bounds before either line's stores)
+template <bool kPre = false, bool kPreF = false>
 __device__ __forceinline__ bool make_rec(uint32_t i, uint4 t, uint32_t gid, const Agg& A, const Emit& E, Rec& r,
-                                         unsigned long long o_pre = 0, uint32_t ts_pre = 0) {
+                                         unsigned long long o_pre = 0, uint32_t ts_pre = 0,
+                                         unsigned long long f_pre = 0) {
   const uint32_t flags = (t.w >> 16) & 0xFFu;
   bool need = gid != kNoGid && (flags & RSA_F_HIT) && (flags & RSA_F_BUILT) && A.cap > 0 && !(A.skip & 2u);
   if (!need) return false;
   // the three loads in flight together (one memory round trip, not two)
   const unsigned long long o = kPre ? o_pre : E.ord[i];
   const uint32_t ts = kPre ? ts_pre : __builtin_nontemporal_load(&E.ts[i]);
-  const unsigned long long f = A.filter[gid];
+  const unsigned long long f = kPreF ? f_pre : A.filter[gid];
   r.ts = ts;
   if (o > f) return false;   // exact skip: capped with threshold <= filter < order
   conn_key(t, gid, r.kA, r.kB);
@@ -1225,9 +1426,10 @@ __device__ __forceinline__ bool make_rec(uint32_t i, uint4 t, uint32_t gid, cons
 
 // Emission for one wave of classified lines (wave-uniform call; lanes with
 // !in do nothing).  i = the lane's line, lines of a wave are i - lane .. + 63.
-template <bool kPre = false>
+template <bool kPre = false, bool kPreF = false>
 __device__ __forceinline__ void emit_wave(uint32_t i, uint32_t n, bool in, uint4 t, uint32_t gid, const Agg& A,
-                                          const Emit& E, unsigned long long o_pre = 0, uint32_t ts_pre = 0) {
+                                          const Emit& E, unsigned long long o_pre = 0, uint32_t ts_pre = 0,
+                                          unsigned long long f_pre = 0) {
   const uint32_t flags = (t.w >> 16) & 0xFFu;
   const bool matched = in && gid != kNoGid;
   const bool hit = matched && (flags & RSA_F_HIT);
@@ -1238,7 +1440,7 @@ __device__ __forceinline__ void emit_wave(uint32_t i, uint32_t n, bool in, uint4
       E.gh[i] = matched ? (gid | (hit ? 0x80000000u : 0u)) : 0xFFFFFFFFu;
   }
   Rec r;
-  const bool need = in && make_rec<kPre>(i, t, gid, A, E, r, o_pre, ts_pre);
+  const bool need = in && make_rec<kPre, kPreF>(i, t, gid, A, E, r, o_pre, ts_pre, f_pre);
   const unsigned long long mask = __ballot(need);
   const uint32_t lane = __lane_id();
   const uint32_t w0 = i - lane;   // the window's first line (waves cover aligned 64-line windows)
@@ -1365,6 +1567,78 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kIm
     atomicAdd(&g_phase[8], waves_seen);
   }
 #endif
+}
+
+// Pass 1a for the global bucket image, two lines per lane (lines i and i +
+// stride of each iteration; see classify_pair_bkt).  The tuples of the next
+// iteration and the emission's order / timestamp loads are issued ahead, as
+// in k_classify's global variants.
+// (256-thread workgroups: no LDS and no barriers, so a CU holds as many as
+// its registers allow -- six at the 80-VGPR cap, 24 waves)
+#ifndef RSA_PAIR_WAVES
+#define RSA_PAIR_WAVES 6   // minimum waves per SIMD (register cap: 80 VGPRs)
+#endif
+constexpr int kPairThreads = 256;
+template <bool kEmit>
+__global__ __launch_bounds__(kPairThreads) __attribute__((amdgpu_waves_per_eu(RSA_PAIR_WAVES, 8))) void k_classify_pair(
+    EmitPack EP, const uint4* __restrict__ T, unsigned long long n, int32_t* __restrict__ gout, Rules R,
+    unsigned int* flags, uint32_t* tail, unsigned long long* tail_n) {
+  Agg A = {};
+  Emit E = {};
+  const uint32_t n32 = (uint32_t)n;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  const uint32_t* img = R.img;
+  for (uint32_t base = blockIdx.x * blockDim.x; base < n32; base += 2 * stride) {
+    const uint32_t i0 = base + threadIdx.x, i1 = i0 + stride;
+    const bool in0 = i0 < n32, in1 = i1 < n32;
+    const uint4 t0 = in0 ? T[i0] : make_uint4(0u, 0u, 0u, 0u);
+    const uint4 t1 = in1 ? T[i1] : make_uint4(0u, 0u, 0u, 0u);
+    unsigned long long o0 = 0ull, o1 = 0ull;
+    uint32_t s0 = 0u, s1 = 0u;
+    if (kEmit) {
+      classify_emit_args(EP, A, E);
+      if (in0) {
+        o0 = E.ord[i0];
+        s0 = __builtin_nontemporal_load(&E.ts[i0]);
+      }
+      if (in1) {
+        o1 = E.ord[i1];
+        s1 = __builtin_nontemporal_load(&E.ts[i1]);
+      }
+    }
+    const bool v0 = in0 && (((t0.w >> 16) & 0xFFu) & RSA_F_VALID);
+    const bool v1 = in1 && (((t1.w >> 16) & 0xFFu) & RSA_F_VALID);
+    uint32_t g0, g1;
+    classify_pair_bkt(t0, v0, t1, v1, R, img, flags, g0, g1);
+    const bool d0 = g0 == kDefer, d1 = g1 == kDefer;
+    const unsigned long long dm0 = __ballot(d0), dm1 = __ballot(d1);
+    if (dm0 | dm1) {   // (testing only: R.force_defer) one device atomic per wave
+      const int leader = __builtin_ctzll(dm0 | dm1);
+      unsigned long long pos = 0;
+      if ((int)__lane_id() == leader)
+        pos = atomicAdd(tail_n, (unsigned long long)(__popcll(dm0) + __popcll(dm1)));
+      pos = ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(pos >> 32), leader) << 32) |
+            __builtin_amdgcn_readlane((uint32_t)pos, leader);
+      const unsigned long long below = (1ull << __lane_id()) - 1ull;
+      if (d0) tail[pos + __popcll(dm0 & below)] = i0;
+      if (d1) tail[pos + __popcll(dm0) + __popcll(dm1 & below)] = i1;
+    }
+    if (gout && in0 && !d0) gout[i0] = (int32_t)g0;
+    if (gout && in1 && !d1) gout[i1] = (int32_t)g1;
+    if (kEmit) {
+      classify_emit_args(EP, A, E);
+      // both rules' filter bounds before either line's stores (for the lines
+      // make_rec takes: a rule, hit and BUILT, the table on)
+      const bool tab = A.cap > 0 && !(A.skip & 2u);
+      const uint32_t hb = RSA_F_HIT | RSA_F_BUILT;
+      const bool r0 = tab && in0 && !d0 && g0 != kNoGid && (((t0.w >> 16) & hb) == hb);
+      const bool r1 = tab && in1 && !d1 && g1 != kNoGid && (((t1.w >> 16) & hb) == hb);
+      const unsigned long long f0 = r0 ? A.filter[g0] : 0ull;
+      const unsigned long long f1 = r1 ? A.filter[g1] : 0ull;
+      emit_wave<true, true>(i0, n32, in0 && !d0, t0, g0, A, E, o0, s0, f0);
+      emit_wave<true, true>(i1, n32, in1 && !d1, t1, g1, A, E, o1, s1, f1);
+    }
+  }
 }
 
 // Pass 1a, deferred lines: exact linear scan of their whole list (+ emission).
@@ -3447,6 +3721,7 @@ struct rsa_ctx {
   // every record while every job pays the tentative fields, a host read and
   // the selective clear
   bool recount_selective = false;
+  bool classify_pair = true;            // RSA_OPT_CLASSIFY_PAIR: the global bucket image classifies two lines per lane
   uint8_t* d_replay = nullptr;              // per rule: replay its late-slice records (k_tent_check)
   uint32_t replay_alloc = 0;
   uint32_t replay_seg = 0xFFFFFFFFu;        // the segment the recount filters by d_replay (0xFFFFFFFF: none)
@@ -3830,7 +4105,13 @@ void launch_classify_img(rsa_ctx* c, const uint4* t, uint64_t m, int32_t* go, co
   ep.cap = ag.cap;
   ep.skip = ag.skip;
   ep.np_bits = ag.np_bits;
-  if (c->indexed && c->img_words <= (uint32_t)kImgSmall && !RSA_FORCE_LARGE) {
+  if (kMode == 2 && c->classify_pair && c->indexed && !c->bkt_filters &&
+      !(c->img_words <= (uint32_t)kImgLarge)) {
+    // the global bucket image: two lines per lane
+    const unsigned long long lanes = (m + 1) / 2;
+    k_classify_pair<kEmit><<<grid_for_threads(c, lanes, kPairThreads, 4 * RSA_PAIR_WAVES / (kPairThreads / 64)),
+                             kPairThreads, 0, c->stream>>>(ep, t, m, go, r, c->d_flags, c->d_tail, c->d_tail_n);
+  } else if (c->indexed && c->img_words <= (uint32_t)kImgSmall && !RSA_FORCE_LARGE) {
     k_classify<kImgSmall, kEmit, kMode, kNarrow><<<grid_for_threads(c, m, 1024, 2), 1024, 0, c->stream>>>(
         ep, t, m, go, r, c->d_flags, c->d_tail, c->d_tail_n);
   } else if (c->indexed && c->img_words <= (uint32_t)kImgLarge) {
@@ -4388,6 +4669,9 @@ int rsa_set_option(rsa_ctx* c, int option, int64_t value) {
       return RSA_OK;
     case RSA_OPT_COUNTER_WORDS16:
       c->gh16 = value != 0;
+      return RSA_OK;
+    case RSA_OPT_CLASSIFY_PAIR:
+      c->classify_pair = value != 0;
       return RSA_OK;
     case RSA_OPT_RECOUNT_SELECTIVE:
       c->recount_selective = value != 0;

@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 from oracle import coracle
-from ruleset_analysis_amd import fortigate, synth, synth_fg
+from ruleset_analysis_amd import fortigate, native, synth, synth_fg
 from ruleset_analysis_amd.compile import CompiledRules
 from ruleset_analysis_amd.engine import DeviceBatch
 from ruleset_analysis_amd.pipeline import built_hit_count
@@ -65,6 +65,22 @@ def test_cfg4_parity_chained_index_capped(engine, cfg4, kind):
 def test_cfg4_parity_bucket_index(engine, cfg4, kind):
     text, info, db, comp, R = cfg4
     _job_vs_oracle(engine, text, info, comp, R, 12000, seed=44, cap=1000, kind=kind)
+
+
+@pytest.mark.parametrize('pair,defer,n', [(1, 0, 12001), (0, 0, 12001), (1, 1, 777), (1, 0, 63)])
+def test_cfg4_bucket_two_lines_per_lane(engine, cfg4, pair, defer, n):
+    """The global bucket image's two-lines-per-lane classifier (k_classify_pair,
+    RSA_OPT_CLASSIFY_PAIR) against the oracle: odd line counts (the second
+    line of the last lanes past the end), chained records, forced deferral
+    (every indexed line through k_tail), and the one-line classifier."""
+    text, info, db, comp, R = cfg4
+    engine.set_option(native.RSA_OPT_CLASSIFY_PAIR, pair)
+    engine.set_option(native.RSA_OPT_FORCE_DEFER, defer)
+    try:
+        _job_vs_oracle(engine, text, info, comp, R, n, seed=45 + n, cap=30, chunk=4096, kind='bucket')
+    finally:
+        engine.set_option(native.RSA_OPT_CLASSIFY_PAIR, 1)
+        engine.set_option(native.RSA_OPT_FORCE_DEFER, 0)
 
 
 def test_cfg4_parity_linear_scan(engine, cfg4):
