@@ -611,14 +611,29 @@ __device__ __forceinline__ uint64_t line_chunk8(const uint8_t* __restrict__ text
 }
 
 // round 0: every line's length without '\n' (kept for the later rounds) and its first key
+// A line that is not the last and does not end in '\n' (or is 4 GiB long):
+// its length cannot be taken from the next line's start (nl_bad, one atomic
+// per wave; k_compact then reads lens[] instead).
+__device__ __forceinline__ void note_nl(bool bad, uint32_t* __restrict__ nl_bad) {
+  const unsigned long long b = __ballot(bad);
+  if (b && (int)__lane_id() == __builtin_ctzll(b)) atomicOr(nl_bad, 1u);
+}
+
 __global__ void k_keys0(const uint8_t* __restrict__ text, const uint64_t* __restrict__ off, uint32_t n,
                         uint64_t n_bytes, uint32_t* __restrict__ lens, uint64_t* __restrict__ keys,
-                        uint32_t* __restrict__ ids) {
+                        uint32_t* __restrict__ ids, uint32_t* __restrict__ nl_bad) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t a = 0, b = 0, len = 0;
+  bool nl = true;
+  if (j < n) {
+    a = off[j];
+    b = off[j + 1];
+    len = b - a;
+    nl = len && text[b - 1] == '\n';
+    if (nl) --len;
+  }
+  note_nl(j + 1 < n && (!nl || len >= 0xFFFFFFFFull), nl_bad);
   if (j >= n) return;
-  const uint64_t a = off[j], b = off[j + 1];
-  uint64_t len = b - a;
-  if (len && text[b - 1] == '\n') --len;
   const uint32_t l32 = len < 0xFFFFFFFFull ? (uint32_t)len : 0xFFFFFFFFu;
   lens[j] = l32;
   keys[j] = chunk_key(text, n_bytes, a, l32, 0u);
@@ -630,12 +645,19 @@ __global__ void k_keys0(const uint8_t* __restrict__ text, const uint64_t* __rest
 // 0xFFFFFFFF) and its id.
 __global__ void k_grp0(const int32_t* __restrict__ group, const uint8_t* __restrict__ text,
                        const uint64_t* __restrict__ off, uint32_t n, uint32_t none, uint32_t* __restrict__ lens,
-                       uint32_t* __restrict__ keys, uint32_t* __restrict__ ids) {
+                       uint32_t* __restrict__ keys, uint32_t* __restrict__ ids, uint32_t* __restrict__ nl_bad) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t a = 0, b = 0, len = 0;
+  bool nl = true;
+  if (j < n) {
+    a = off[j];
+    b = off[j + 1];
+    len = b - a;
+    nl = len && text[b - 1] == '\n';
+    if (nl) --len;
+  }
+  note_nl(j + 1 < n && (!nl || len >= 0xFFFFFFFFull), nl_bad);
   if (j >= n) return;
-  const uint64_t a = off[j], b = off[j + 1];
-  uint64_t len = b - a;
-  if (len && text[b - 1] == '\n') --len;
   lens[j] = len < 0xFFFFFFFFull ? (uint32_t)len : 0xFFFFFFFFu;
   const int32_t g = group[j];
   keys[j] = g < 0 ? none : (uint32_t)g;
@@ -891,12 +913,15 @@ __global__ void k_settle(const uint64_t* __restrict__ keys, const uint32_t* __re
 // gs_old is null) + adv (7: the window matched; 0: the group stage)
 // (in: the elements in this order, whose offset and length are taken; null:
 // gathered by line id from off / lens -- after a sort)
+// (gathered by id: when every line but the last ends in '\n' -- *nl_bad == 0
+// -- the length comes from the next line's start, the same 64-B line as the
+// offset as a rule, so one random read instead of two)
 __global__ void k_compact(const uint32_t* __restrict__ ids, const uint32_t* __restrict__ ngs1,
                           const uint32_t* __restrict__ keep, const uint32_t* __restrict__ slot, uint32_t m,
                           Act* __restrict__ out, const uint32_t* __restrict__ gs_old, const uint32_t* __restrict__ cdep,
                           const uint32_t* __restrict__ cmin, uint32_t* __restrict__ cnext, uint32_t adv,
                           const Act* __restrict__ in, const uint64_t* __restrict__ off,
-                          const uint32_t* __restrict__ lens) {
+                          const uint32_t* __restrict__ lens, uint32_t n_lines, const uint32_t* __restrict__ nl_bad) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= m || !keep[j]) return;
   const uint32_t g = ngs1[j] - 1, id = ids[j];
@@ -906,6 +931,9 @@ __global__ void k_compact(const uint32_t* __restrict__ ids, const uint32_t* __re
     const Act x = in[j];
     o = x.off;
     l = x.len;
+  } else if (!*nl_bad && id + 1 < n_lines) {
+    o = off[id];
+    l = (uint32_t)(off[id + 1] - o - 1);
   } else {
     o = off[id];
     l = lens[id];
@@ -1519,6 +1547,8 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
     scan<OpMax, true, uint32_t, uint32_t>(st, in, out, m, sums);
   };
 
+  uint32_t* nl_bad = flags + 8;   // (set by k_grp0 / k_keys0: see note_nl)
+  TPCHK(c, hipMemsetAsync(nl_bad, 0, 4, st));
   uint64_t n_bytes = 0;
   TPCHK(c, hipMemcpyAsync(&n_bytes, d_off + n, 8, hipMemcpyDeviceToHost, st));
   TPCHK(c, hipStreamSynchronize(st));
@@ -1541,7 +1571,7 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
     uint32_t* gkB = reinterpret_cast<uint32_t*>(keysB);
     uint32_t* gkT = reinterpret_cast<uint32_t*>(keysT);
     hipLaunchKernelGGL(k_grp0, dim3(blocks(n, 256)), dim3(256), 0, st, d_group, d_text, d_off, n, gmax + 1, lens,
-                       gkA, idsA);
+                       gkA, idsA, nl_bad);
     radix_pairs<uint32_t, uint32_t>(st, gkA, gkB, idsA, idsB, n, 0, kbits, gkT, idsT, hist, sums);
     hipLaunchKernelGGL(k_grp_bounds, dim3(blocks(n, 256)), dim3(256), 0, st, gkB, n, bstart);
     maxscan(bstart, first, n);
@@ -1550,7 +1580,8 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
     adv0 = 0;
   } else {
     // round 0: all lines
-    hipLaunchKernelGGL(k_keys0, dim3(blocks(n, 256)), dim3(256), 0, st, d_text, d_off, n, n_bytes, lens, keysA, idsA);
+    hipLaunchKernelGGL(k_keys0, dim3(blocks(n, 256)), dim3(256), 0, st, d_text, d_off, n, n_bytes, lens, keysA, idsA,
+                       nl_bad);
     radix_pairs<uint64_t, uint32_t>(st, keysA, keysB, idsA, idsB, n, 0, 64, keysT, idsT, hist, sums);
     hipLaunchKernelGGL(k_bounds, dim3(blocks(n, 256)), dim3(256), 0, st, keysB, (const uint32_t*)nullptr,
                        (const uint32_t*)nullptr, n, pos, bstart);
@@ -1561,7 +1592,7 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
   exscan(keep, slot, n);
   hipLaunchKernelGGL(k_compact, dim3(blocks(n, 256)), dim3(256), 0, st, idsB, first, keep, slot, n, act,
                      (const uint32_t*)nullptr, (const uint32_t*)nullptr, (const uint32_t*)nullptr, cdep, adv0,
-                     (const Act*)nullptr, d_off, (const uint32_t*)lens);
+                     (const Act*)nullptr, d_off, (const uint32_t*)lens, n, (const uint32_t*)nl_bad);
   uint32_t m = 0, lastk = 0;
   TPCHK(c, hipMemcpyAsync(&m, slot + n - 1, 4, hipMemcpyDeviceToHost, st));
   TPCHK(c, hipMemcpyAsync(&lastk, keep + n - 1, 4, hipMemcpyDeviceToHost, st));
@@ -1659,7 +1690,8 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
     // sorted: gathered by line id)
     hipLaunchKernelGGL(k_compact, dim3(blocks(m, 256)), dim3(256), 0, st, ids, slot, keep, first, m, act3,
                        (const uint32_t*)gs, (const uint32_t*)cdep, (const uint32_t*)cmin, cnext, 7u,
-                       sorted ? (const Act*)nullptr : (const Act*)act, d_off, (const uint32_t*)lens);
+                       sorted ? (const Act*)nullptr : (const Act*)act, d_off, (const uint32_t*)lens, n,
+                       (const uint32_t*)nl_bad);
     {
       Act* swa = act;
       act = act3;
