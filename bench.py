@@ -431,8 +431,25 @@ def _free_port():
     return p
 
 
+class ResultOut(object):
+    """This process's real stdout, kept for the ONE result line.  Everything
+    else written to fd 1 -- RCCL's version banner at communicator init (seen
+    at world 1 with --force-dist), prints of the libraries -- goes to stderr
+    instead, so the driver reads exactly one JSON line from stdout."""
+
+    def __init__(self):
+        sys.stdout.flush()
+        self.fd = os.dup(1)
+        os.dup2(2, 1)
+
+    def line(self, obj):
+        sys.stdout.flush()
+        os.write(self.fd, (json.dumps(obj) + '\n').encode())
+
+
 def rank_main(args, rank, world, local):
     import torch
+    result_out = ResultOut()
     dist = None
     if world > 1 or args.force_dist:
         import torch.distributed as dist
@@ -447,7 +464,7 @@ def rank_main(args, rank, world, local):
     cap = wl.cap
     compiled = wl.compiled
     if args.cpu_model:
-        return _cpu_model_rank(args, wl, lines, cap, rank, world, dist)
+        return _cpu_model_rank(args, wl, lines, cap, rank, world, dist, result_out)
 
     from ruleset_analysis_amd import native
     from ruleset_analysis_amd.dist import EngineBackend, ShardOverflow, merge
@@ -667,7 +684,7 @@ def rank_main(args, rank, world, local):
                 c1['source'] = 'measured in this bench run (bench.py reference_pipeline_baseline)'
                 c1['measure_s'] = time.perf_counter() - t
                 res['cpu_baseline']['config1'] = c1
-        print(json.dumps(res), flush=True)
+        result_out.line(res)
     if dist is not None:
         dist.destroy_process_group()
     return 0
@@ -692,6 +709,7 @@ def text_main(args):
     touched (not timed)."""
     global _TEXT_WL
     import multiprocessing
+    result_out = ResultOut()
     wl = Workload(args.config, rules=args.rules, cap=args.cap)
     if wl.kind != 'asa':
         die('--text renders ASA log lines: use an ASA config')
@@ -836,7 +854,7 @@ def text_main(args):
                      'bytes': 'text bytes read + 32 B/line (off 8, tuple 16, ts 4, disp 4)'},
         'checks': checks,
     }
-    print(json.dumps(res), flush=True)
+    result_out.line(res)
     return 0
 
 
@@ -851,7 +869,7 @@ def _dump(path, last, eng, cap):
     np.savez(path, records=recs.view(np.uint8), matches=matches, hits=hits, distinct=distinct, thresh=thresh)
 
 
-def _cpu_model_rank(args, wl, lines, cap, rank, world, dist):
+def _cpu_model_rank(args, wl, lines, cap, rank, world, dist, result_out):
     """TESTING: one rank of the spawn + merge path with the CPU model of
     tests/cpu_model.py in place of the HIP library (no GPU)."""
     sys.path.insert(0, os.path.join(ROOT, 'tests'))
@@ -875,9 +893,9 @@ def _cpu_model_rank(args, wl, lines, cap, rank, world, dist):
             recs, matches, hits, distinct, thresh = out
             np.savez(args.dump, records=recs.view(np.uint8), matches=matches, hits=hits, distinct=distinct,
                      thresh=thresh)
-        print(json.dumps({'metric': 'TESTING cpu-model merge (not a measurement)', 'value': lines * world / dt,
-                          'unit': 'lines/s', 'n_gpus': world, 'steps': args.steps, 'cpu_model': True,
-                          'records': len(out[0])}), flush=True)
+        result_out.line({'metric': 'TESTING cpu-model merge (not a measurement)', 'value': lines * world / dt,
+                         'unit': 'lines/s', 'n_gpus': world, 'steps': args.steps, 'cpu_model': True,
+                         'records': len(out[0])})
     dist.destroy_process_group()
     return 0
 
