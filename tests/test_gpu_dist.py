@@ -28,7 +28,8 @@ def _worker(rank, world, port, args, out_q):
     from ruleset_analysis_amd.dist import EngineBackend, merge
     from ruleset_analysis_amd.engine import DeviceBatch, Engine
     from ruleset_analysis_amd.pipeline import built_hit_count
-    seed, n_rules, n_lines, cap, zipf = args
+    seed, n_rules, n_lines, cap, zipf = args[:5]
+    opts = args[5] if len(args) > 5 else {}
     dbj, info = synth.make_db(seed, n_rules)
     tr = synth.make_traffic((dbj, info), n_lines, seed=seed + 1, zipf=zipf)
     compiled = CompiledRules(acldb.load_json(dbj))
@@ -38,6 +39,9 @@ def _worker(rank, world, port, args, out_q):
     a, b = cut[rank], cut[rank + 1]
     local = Engine(0)
     local.load_compiled(compiled)
+    from ruleset_analysis_amd import native
+    for k, v in opts.items():
+        local.set_option(getattr(native, k), v)
     batch = DeviceBatch.from_numpy(tup[a:b], ts[a:b], order[a:b], local.device)
     local.reset(max(built_hit_count(tup[a:b]), 1), cap)
     g = torch.empty(batch.n, dtype=torch.int32, device=local.device)
@@ -111,6 +115,15 @@ def test_four_ranks_one_gpu():
     out = _run_two_ranks(args, world=4)
     ref = _check(out, *_oracle_inputs(71, 700, 160000, 1.2), 12)
     assert (ref['n_conns'] >= 12).sum() > 20
+
+
+def test_two_ranks_atomic_import():
+    """RSA_OPT_REGION_IMPORT=0: the owners merge the received entries with the
+    per-record atomic import (CAS claims on empty keys).  A fresh table is
+    written with empty keys only for this path (the region paths never read a
+    slot they did not claim), so the option is set before the reset."""
+    out = _run_two_ranks((61, 700, 120000, 12, 1.2, {'RSA_OPT_REGION_IMPORT': 0}))
+    _check(out, *_oracle_inputs(61, 700, 120000, 1.2), 12)
 
 
 def test_two_ranks_capped_only_after_merge():
