@@ -332,10 +332,14 @@ def valu_busy(sq, kernel_prefix):
     SQ_INSTS_VALU / (SIMDs x per-XCD active cycles, GRBM_GUI_ACTIVE / 8)."""
     if not sq:
         return None
+    # the kernel of that name that ran longest (the emitting classifier, not the
+    # classify-only launches of the untimed checks; k_classify_pair for cfg4)
+    best = None
     for name, c in sq.items():
         if name.startswith(kernel_prefix) and c.get('GRBM_GUI_ACTIVE'):
-            return 2.0 * c['SQ_INSTS_VALU'] / (N_SIMD * c['GRBM_GUI_ACTIVE'] / 8.0)
-    return None
+            if best is None or c['GRBM_GUI_ACTIVE'] > best['GRBM_GUI_ACTIVE']:
+                best = c
+    return None if best is None else 2.0 * best['SQ_INSTS_VALU'] / (N_SIMD * best['GRBM_GUI_ACTIVE'] / 8.0)
 
 
 def record_checksum(recs_u8):

@@ -55,7 +55,7 @@ def main():
     # (k_classify<kImg, kEmit, kMode, kNarrow>: kEmit is the second argument)
     import re
     no_emit = lambda name: re.search(r'k_classify<[^,>]+, false', name) is not None or \
-        ('k_tail' in name and 'false>' in name)
+        ('k_tail' in name and 'false>' in name) or 'k_classify_pair<false>' in name
     pick = lambda name: any(k in name for k in kinds) and not no_emit(name)
     factor = lambda name: 1.0 if 'k_reduce' in name else 2.0
     read = 1024 * sum(v * factor(fn[d]) for d, v in f.items() if pick(fn[d])) / steps
