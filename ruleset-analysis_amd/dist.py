@@ -34,7 +34,8 @@ import numpy as np
 
 from .compile import RECORD_DTYPE
 
-__all__ = ['merge', 'merged_to_host', 'EngineBackend', 'Exported', 'route_records', 'ShardOverflow']
+__all__ = ['merge', 'gather_rows', 'OwnerRows', 'merged_to_host', 'EngineBackend', 'Exported', 'route_records',
+           'ShardOverflow']
 
 REC = RECORD_DTYPE.itemsize
 NO_THRESHOLD = -1   # 0xFFFF_FFFF_FFFF_FFFF viewed as int64
@@ -187,12 +188,38 @@ def _overflow(e):
     return getattr(e, 'code', None) == ShardOverflow.code
 
 
-def merge(backend, dist, world, rank, group=None, to_host=True):
+class OwnerRows(object):
+    """merge(..., gather=False): this rank's own rules' final rows -- the
+    counterpart of one Hadoop reducer's part file (runAnalysis.sh:42-56 runs
+    NUM_REDUCERS reducers whose outputs stay separate files of the job's
+    -output directory) -- with the merged counters and every rank's row bytes.
+    gather_rows() collects them on rank 0 as merge() would have."""
+
+    def __init__(self, final, sizes, matches, hits, distinct, thresh):
+        self.final, self.sizes = final, sizes
+        self.matches, self.hits, self.distinct, self.thresh = matches, hits, distinct, thresh
+
+
+def gather_rows(part, dist, world, rank, group=None, to_host=True):
+    """The owners' rows of merge(..., gather=False) on rank 0: merge()'s result
+    there, None elsewhere."""
+    import torch
+    parts = _gather0(part.final, part.sizes, rank, world, dist, group) if world > 1 else [part.final]
+    if rank != 0:
+        return None
+    recs = parts[0] if world == 1 else torch.cat(parts)
+    out = (recs, part.matches, part.hits, part.distinct, part.thresh)
+    return merged_to_host(out) if to_host else out
+
+
+def merge(backend, dist, world, rank, group=None, to_host=True, gather=True):
     """Run the protocol; returns (records, matches, hits, distinct, thresh) on
     rank 0 and None elsewhere: numpy arrays (records as RECORD_DTYPE rows), or
     with to_host=False the device tensors as they stand in rank 0's HBM
     (records as uint8 rows; see merged_to_host), which is where the
-    single-GPU job leaves its result too.
+    single-GPU job leaves its result too.  gather=False: every rank returns
+    its OwnerRows instead (the rows stay with their owners, as the
+    reference's reducer outputs do; gather_rows collects them).
 
     One host read per phase: the route counts (with the overflow flag), the
     thresholds (with the import overflow need), the pass-2 route counts, and
@@ -283,9 +310,12 @@ def merge(backend, dist, world, rank, group=None, to_host=True):
         tr('emit', dev)
     finally:
         backend.set_owner(0, 0)
+    sizes = [int(s) for s in dsz[n_rules:].cpu().tolist()] if multi else [final.numel()]
+    if not gather:
+        tr('end', dev)
+        return OwnerRows(final, sizes, c['matches'], c['hits'], distinct, thresh)
     # the owners' rows to rank 0
     if multi:
-        sizes = [int(s) for s in dsz[n_rules:].cpu().tolist()]
         parts = _gather0(final, sizes, rank, world, dist, group)
     else:
         parts = [final]
