@@ -614,6 +614,8 @@ def rank_main(args, rank, world, local):
     if dist is not None:
         # (untimed) the last job's owner rows to rank 0
         last['merged'] = gather_rows(last['part'], dist, world, rank, to_host=False)
+        if last['merged'] is not None:   # rank 0: every owner's rows
+            n_rec = last['merged'][0].numel() // RECORD_DTYPE.itemsize
     if args.dump and rank == 0:
         _dump(args.dump, last, eng, cap)
     checks = None
