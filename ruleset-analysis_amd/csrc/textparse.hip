@@ -1111,21 +1111,40 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_tiles(const Tin* __restri
                                                              uint64_t n, Tout* __restrict__ sums) {
   __shared__ Tout sh[16];
   const uint64_t beg = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanPer;
+  // 32-bit elements of a full, 16-B aligned group: one 16-B load and store
+  // per thread (coalesced), else element by element
+  constexpr bool kVec = sizeof(Tin) == 4 && sizeof(Tout) == 4 && kScanPer == 4;
+  const bool vec = kVec && beg + kScanPer <= n && ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15u) == 0;
   Tout v[kScanPer];
   Tout c = Op::template id<Tout>();
+  if (vec) {
+    const uint4 q = *reinterpret_cast<const uint4*>(in + beg);
+    v[0] = (Tout)q.x;
+    v[1] = (Tout)q.y;
+    v[2] = (Tout)q.z;
+    v[3] = (Tout)q.w;
+  } else {
 #pragma unroll
-  for (uint32_t k = 0; k < kScanPer; ++k) {
-    v[k] = beg + k < n ? (Tout)in[beg + k] : Op::template id<Tout>();
-    c = Op::f(c, v[k]);
+    for (uint32_t k = 0; k < kScanPer; ++k) v[k] = beg + k < n ? (Tout)in[beg + k] : Op::template id<Tout>();
   }
+#pragma unroll
+  for (uint32_t k = 0; k < kScanPer; ++k) c = Op::f(c, v[k]);
   Tout ex, inc, total;
   wg_scan<Op>(c, sh, ex, inc, total);
   Tout run = ex;
+  Tout o[kScanPer];
 #pragma unroll
   for (uint32_t k = 0; k < kScanPer; ++k) {
     const Tout nx = Op::f(run, v[k]);
-    if (beg + k < n) out[beg + k] = kIncl ? nx : run;
+    o[k] = kIncl ? nx : run;
     run = nx;
+  }
+  if (vec) {
+    *reinterpret_cast<uint4*>(out + beg) = uint4{(uint32_t)o[0], (uint32_t)o[1], (uint32_t)o[2], (uint32_t)o[3]};
+  } else {
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer; ++k)
+      if (beg + k < n) out[beg + k] = o[k];
   }
   if (threadIdx.x == 0) sums[blockIdx.x] = total;
 }
@@ -1153,6 +1172,16 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_tiles_add(Tout* __restric
                                                                  const Tout* __restrict__ sums) {
   const uint64_t beg = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanPer;
   const Tout add = sums[blockIdx.x];
+  constexpr bool kVec = sizeof(Tout) == 4 && kScanPer == 4;
+  if (kVec && beg + kScanPer <= n && (reinterpret_cast<uintptr_t>(out) & 15u) == 0) {
+    uint4 q = *reinterpret_cast<const uint4*>(out + beg);
+    q.x = (uint32_t)Op::f(add, (Tout)q.x);
+    q.y = (uint32_t)Op::f(add, (Tout)q.y);
+    q.z = (uint32_t)Op::f(add, (Tout)q.z);
+    q.w = (uint32_t)Op::f(add, (Tout)q.w);
+    *reinterpret_cast<uint4*>(out + beg) = q;
+    return;
+  }
 #pragma unroll
   for (uint32_t k = 0; k < kScanPer; ++k)
     if (beg + k < n) out[beg + k] = Op::f(add, out[beg + k]);
