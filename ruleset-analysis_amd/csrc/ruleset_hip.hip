@@ -1633,8 +1633,11 @@ __global__ __launch_bounds__(kPairThreads) __attribute__((amdgpu_waves_per_eu(RS
       const uint32_t hb = RSA_F_HIT | RSA_F_BUILT;
       const bool r0 = tab && in0 && !d0 && g0 != kNoGid && (((t0.w >> 16) & hb) == hb);
       const bool r1 = tab && in1 && !d1 && g1 != kNoGid && (((t1.w >> 16) & hb) == hb);
-      const unsigned long long f0 = r0 ? A.filter[g0] : 0ull;
-      const unsigned long long f1 = r1 ? A.filter[g1] : 0ull;
+#ifndef RSA_ABL_NOFILTER
+#define RSA_ABL_NOFILTER 0   // PROFILING builds only (results invalid): no filter-bound loads
+#endif
+      const unsigned long long f0 = RSA_ABL_NOFILTER ? ~0ull : (r0 ? A.filter[g0] : 0ull);
+      const unsigned long long f1 = RSA_ABL_NOFILTER ? ~0ull : (r1 ? A.filter[g1] : 0ull);
       emit_wave<true, true>(i0, n32, in0 && !d0, t0, g0, A, E, o0, s0, f0);
       emit_wave<true, true>(i1, n32, in1 && !d1, t1, g1, A, E, o1, s1, f1);
     }
