@@ -1280,18 +1280,122 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const K* __restrict__
   }
 }
 
-// host: scan of n elements (sums: >= n / kScanTile + 2 elements of Tout; the
-// plus-scans leave the grand total in sums[n_tiles])
+// One-pass scan of 32-bit elements (decoupled look-back, as k_nl_offsets):
+// workgroups take the tiles in launch order (an atomic ticket), scan their
+// tile in registers, publish its aggregate, combine the predecessors' walking
+// back to the first published inclusive prefix, publish their own, and write
+// the tile once -- one read and one write of the data, where the three-pass
+// form (k_scan_tiles, k_scan_tile_sums, k_scan_tiles_add) read and wrote it
+// twice.  state: one look-back word per tile, then the ticket and a flag
+// (zeroed by the caller).
+template <typename Op, bool kIncl>
+__global__ __launch_bounds__(kScanThreads) void k_scan_lb(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                          uint64_t n, unsigned long long* __restrict__ state,
+                                                          unsigned int* __restrict__ ticket) {
+  __shared__ uint32_t sh[16];
+  __shared__ uint32_t sh_b, sh_prefix;
+  if (threadIdx.x == 0) sh_b = atomicAdd(&ticket[0], 1u);
+  __syncthreads();
+  const uint32_t b = sh_b;
+  const uint64_t beg = (uint64_t)b * kScanTile + (uint64_t)threadIdx.x * kScanPer;
+  const bool vec = beg + kScanPer <= n && ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15u) == 0;
+  uint32_t v[kScanPer];
+  if (vec) {
+    const uint4 q = *reinterpret_cast<const uint4*>(in + beg);
+    v[0] = q.x;
+    v[1] = q.y;
+    v[2] = q.z;
+    v[3] = q.w;
+  } else {
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer; ++k) v[k] = beg + k < n ? in[beg + k] : Op::template id<uint32_t>();
+  }
+  uint32_t c = Op::template id<uint32_t>();
+#pragma unroll
+  for (uint32_t k = 0; k < kScanPer; ++k) c = Op::f(c, v[k]);
+  uint32_t ex, inc, total;
+  wg_scan<Op>(c, sh, ex, inc, total);
+  if (threadIdx.x < 64) {
+    const uint32_t lane = threadIdx.x;
+    uint32_t run = Op::template id<uint32_t>();
+    if (b == 0) {
+      if (lane == 0) __hip_atomic_store(&state[0], kLbIncl | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      if (lane == 0) __hip_atomic_store(&state[b], kLbAgg | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int64_t top = (int64_t)b - 1;   // the window is tiles (top - 63, top]
+      uint32_t spins = 0;
+      while (true) {
+        const int64_t p = top - (int64_t)lane;
+        const unsigned long long w =
+            p >= 0 ? __hip_atomic_load(&state[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbIncl;
+        const unsigned long long incl = __ballot((w & kLbIncl) != 0);
+        const int stop = incl ? __builtin_ctzll(incl) : 64;   // lanes [0, stop) must be aggregates
+        const unsigned long long ready = __ballot((w & (kLbIncl | kLbAgg)) != 0);
+        const unsigned long long need = stop >= 64 ? ~0ull : ((2ull << stop) - 1ull);
+        if ((ready & need) != need) {   // someone in the window not published yet: look again
+          if (++spins > kLbSpinMax) {
+            if (lane == 0) atomicOr(&ticket[1], 1u);
+            break;
+          }
+          continue;
+        }
+        uint32_t x = ((int)lane <= stop && p >= 0) ? (uint32_t)(w & 0xFFFFFFFFull) : Op::template id<uint32_t>();
+        for (int o = 32; o > 0; o >>= 1) x = Op::f(x, (uint32_t)__shfl_xor((int)x, o));
+        run = Op::f(run, x);
+        if (stop < 64) break;
+        top -= 64;
+      }
+      if (lane == 0)
+        __hip_atomic_store(&state[b], kLbIncl | Op::f(run, total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) sh_prefix = run;
+  }
+  __syncthreads();
+  uint32_t r = Op::f(sh_prefix, ex);
+  uint32_t o[kScanPer];
+#pragma unroll
+  for (uint32_t k = 0; k < kScanPer; ++k) {
+    const uint32_t nx = Op::f(r, v[k]);
+    o[k] = kIncl ? nx : r;
+    r = nx;
+  }
+  if (vec) {
+    *reinterpret_cast<uint4*>(out + beg) = uint4{o[0], o[1], o[2], o[3]};
+  } else {
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer; ++k)
+      if (beg + k < n) out[beg + k] = o[k];
+  }
+}
+
+#ifndef RSA_SCAN_LB
+#define RSA_SCAN_LB 0   // A/B builds: 1 = the one-pass look-back scan, measured slower (order keys 8.54 -> 8.71 ms at
+                        // 30M lines, profiles/r05/ab_summary.txt r05lb: the tile-state clear and the in-order
+                        // look-back cost more than the second pass over the data)
+#endif
+
+// host: scan of n elements.  sums: scan_sums_len(n) words -- the three-pass
+// form's tile sums, or the one-pass form's look-back words (u64 per tile)
+// and ticket
 template <typename Op, bool kIncl, typename Tin, typename Tout>
 void scan(hipStream_t st, const Tin* in, Tout* out, uint64_t n, Tout* sums) {
   if (!n) return;
   const uint32_t nb = (uint32_t)((n + kScanTile - 1) / kScanTile);
+  if (RSA_SCAN_LB && sizeof(Tin) == 4 && sizeof(Tout) == 4 && (reinterpret_cast<uintptr_t>(sums) & 7u) == 0) {
+    unsigned long long* state = reinterpret_cast<unsigned long long*>(sums);   // (sums is 8-B aligned)
+    unsigned int* ticket = reinterpret_cast<unsigned int*>(state + nb);
+    (void)hipMemsetAsync(state, 0, (size_t)nb * 8 + 8, st);
+    hipLaunchKernelGGL((k_scan_lb<Op, kIncl>), dim3(nb), dim3(kScanThreads), 0, st,
+                       reinterpret_cast<const uint32_t*>(in), reinterpret_cast<uint32_t*>(out), n, state, ticket);
+    return;
+  }
   hipLaunchKernelGGL((k_scan_tiles<Op, kIncl, Tin, Tout>), dim3(nb), dim3(kScanThreads), 0, st, in, out, n, sums);
   hipLaunchKernelGGL((k_scan_tile_sums<Op, Tout>), dim3(1), dim3(kScanThreads), 0, st, sums, nb);
   hipLaunchKernelGGL((k_scan_tiles_add<Op, Tout>), dim3(nb), dim3(kScanThreads), 0, st, out, n, sums);
 }
 
-inline size_t scan_sums_len(uint64_t n) { return (size_t)((n + kScanTile - 1) / kScanTile) + 2; }
+// (u32 words: room for a u64 look-back word per tile plus the ticket)
+inline size_t scan_sums_len(uint64_t n) { return 2 * ((size_t)((n + kScanTile - 1) / kScanTile) + 2); }
 
 // scratch of radix_pairs for n elements: hist (256 per tile) and its scan sums
 inline size_t rs_hist_len(uint64_t n) { return (size_t)256 * ((n + kRsTile - 1) / kRsTile); }
