@@ -2433,7 +2433,7 @@ static_assert(sizeof(HRec) == 40, "hot record layout");
 #define RSA_COUNT_PER_CU 1   // k_count workgroups per CU (one is resident: 104 KiB LDS); fewer workgroups, fewer histogram-flush atomics
 #endif
 #ifndef RSA_RED_PF
-#define RSA_RED_PF 0   // A/B builds: k_reduce loads the next block step's record one step ahead (across rounds and
+#define RSA_RED_PF 0   // A/B builds (bit 0 pass 1, bit 1 pass 2; pass 2 alone: neutral, r05pf2): k_reduce loads the next block step's record one step ahead (across rounds and
                        // flushes); measured slower (r05r: cfg3 7.98 -> 8.04, cfg5 9.46 -> 9.58, cfg4 10.62 -> 10.69
                        // ms/step): the inserts wait on LDS atomics and barriers, not on the record loads
 #endif
@@ -2536,7 +2536,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
             last = hr.last;
             cnt = hr.cnt;
           }
-        } else if (RSA_RED_PF) {
+        } else if (RSA_RED_PF & kPass) {   // (bit 0: pass 1, bit 1: pass 2)
           uint4 a = pf0, b = pf1;
           const bool hit = pf_at == pos + j;
           if (have && !hit) {
