@@ -427,6 +427,93 @@ def full_size_checks(eng, batch, gbuf, n_rules, cap, recs_final, owner_rows=None
     return out
 
 
+def dist_full_size_checks(eng, batch, gbuf, n_rules, cap, last, step, dist, world, rank):
+    """The N = 1 full-size properties (full_size_checks) over the distributed
+    job's merged result, untimed, every rank taking part: the merged line and
+    hit counters equal the gid histograms of all shards (all_reduced), every
+    uncapped rule's row counts (on its owner) sum to its hit+BUILT lines of all
+    shards, each owner keeps only its own rules' rows, rank 0's gathered rows
+    are every owner's rows (checksum), the index gids equal a linear scan on
+    every shard, and a rerun of the whole job gives every owner the identical
+    rows.  Flags are AND-ed over the ranks; returned on rank 0 (None elsewhere)."""
+    import torch
+    from ruleset_analysis_amd.dist import _all_reduce
+    dev = gbuf.device
+    part = last['part']
+    flags = (batch.tuples[:, 3] >> 16) & 0xFF
+    g = gbuf.long()
+    ok = g >= 0
+    hitm = ok & ((flags & 2) != 0)
+    hb = hitm & ((flags & 4) != 0)
+    hist = torch.cat([torch.bincount(g[ok], minlength=n_rules)[:n_rules],
+                      torch.bincount(g[hitm], minlength=n_rules)[:n_rules],
+                      torch.bincount(g[hb], minlength=n_rules)[:n_rules],
+                      ok.sum().view(1)]).to(torch.int64)
+    _all_reduce(hist, dist, None)
+    m, h, need, n_cls = hist[:n_rules], hist[n_rules:2 * n_rules], hist[2 * n_rules:3 * n_rules], hist[-1]
+    out = {}
+    out['matches_eq_gid_histogram'] = bool(torch.equal(m, part.matches[:n_rules]))
+    out['hits_eq_gid_histogram'] = bool(torch.equal(h, part.hits[:n_rules]))
+    out['sum_matches_eq_classified_lines'] = int(part.matches[:n_rules].sum().item()) == int(n_cls.item())
+    rows = part.final.view(-1, 40)
+    rg = rows[:, 8:12].contiguous().view(torch.int32).view(-1).long()
+    rc = rows[:, 24:28].contiguous().view(torch.int32).view(-1).long()
+    got = torch.zeros(n_rules, dtype=torch.int64, device=dev).index_add_(0, rg, rc)
+    own = (torch.arange(n_rules, device=dev) % world) == rank
+    unc = own & (part.thresh[:n_rules] == -1)
+    if cap == 0:
+        unc = torch.zeros_like(unc)
+    out['owner_rows_only_own_rules'] = bool(((rg % world) == rank).all().item())
+    out['uncapped_count_sum_eq_hit_built_lines'] = bool(torch.equal(got[unc], need[unc]))
+    n_unc = torch.tensor([int(unc.sum().item())], dtype=torch.int64, device=dev)
+    _all_reduce(n_unc, dist, None)
+    out['uncapped_rules_checked'] = int(n_unc.item())
+    # rank 0's gathered rows = every owner's rows (the checksum is a sum over rows)
+    c_own = record_checksum(part.final)
+    cs = torch.tensor([c_own - (1 << 64) if c_own >= 1 << 63 else c_own], dtype=torch.int64, device=dev)
+    _all_reduce(cs, dist, None)
+    c_sum = int(cs.item()) & 0xFFFFFFFFFFFFFFFF
+    if rank == 0:
+        c_merged = record_checksum(last['merged'][0])
+        out['gathered_rows_eq_owner_rows'] = c_merged == c_sum
+        out['merged_record_checksum'] = '%016x' % c_merged
+    eng.use_index(False)
+    g2 = eng.classify_only(batch)
+    eng.use_index(True)
+    out['index_gids_eq_linear_scan'] = bool(torch.equal(g2, gbuf))
+    # a rerun of the whole distributed job: the identical rows on every owner
+    step(False)
+    out['rerun_identical_records'] = record_checksum(last['part'].final) == c_own
+    flags_ok = [k for k, v in out.items() if isinstance(v, bool)]
+    f = torch.tensor([int(out.get(k, True)) for k in flags_ok], dtype=torch.int64, device=dev)
+    _all_reduce(f, dist, None, op=dist.ReduceOp.MIN)
+    for k, v in zip(flags_ok, f.tolist()):
+        out[k] = bool(v)
+    out['ok'] = all(out[k] for k in flags_ok)
+    return out if rank == 0 else None
+
+
+def merge_exchange_summary(last, dist, world, eng):
+    """The rows the last timed job's merge moved (dist.merge stats), summed
+    and maxed over the ranks, in bytes of 40-B rows; projected per rank for
+    other world sizes in DESIGN.md section 6."""
+    import torch
+    from ruleset_analysis_amd.dist import _all_reduce
+    st = last.get('merge_stats') or {}
+    keys = ['route1_sent_rows', 'route1_recv_rows', 'route2_sent_rows', 'route2_recv_rows', 'owner_rows']
+    v = torch.tensor([int(st.get(k, 0)) for k in keys], dtype=torch.int64, device=eng.device)
+    vmax = v.clone()
+    _all_reduce(v, dist, None)
+    _all_reduce(vmax, dist, None, op=dist.ReduceOp.MAX)
+    rec = RECORD_DTYPE.itemsize
+    out = {'row_bytes': rec, 'allreduce_bytes_per_rank': int(st.get('allreduce_bytes', 0)),
+           'pass2_exchange': bool(st.get('pass2', False))}
+    for k, a, b in zip(keys, v.tolist(), vmax.tolist()):
+        out[k.replace('_rows', '_bytes') + '_total'] = a * rec
+        out[k.replace('_rows', '_bytes') + '_max_rank'] = b * rec
+    return out
+
+
 def _free_port():
     s = socket.socket()
     s.bind(('127.0.0.1', 0))
@@ -561,8 +648,10 @@ def rank_main(args, rank, world, local):
         # with NUM_REDUCERS reducer outputs, separate part files of its -output
         # directory (runAnalysis.sh:12,42-56) -- and are gathered to rank 0 for
         # the checks and --dump after the timed steps (gather_rows)
-        part = merge(EngineBackend(eng, [batch], [gbuf], cap), dist, world, rank, to_host=False, gather=False)
-        last['part'] = part
+        mstats = {}
+        part = merge(EngineBackend(eng, [batch], [gbuf], cap), dist, world, rank, to_host=False, gather=False,
+                     stats=mstats)
+        last['part'], last['merge_stats'] = part, mstats
         return part.final.numel() // RECORD_DTYPE.itemsize
 
     cold_ms = None
@@ -611,11 +700,27 @@ def rank_main(args, rank, world, local):
     classify_ms = float(np.mean([a for a, _b in pass1_launch_ms]))
     aggregate_ms = float(np.mean([b for _a, b in pass1_launch_ms]))
     pass1_ms = classify_ms + aggregate_ms
+    gather = None
     if dist is not None:
-        # (untimed) the last job's owner rows to rank 0
-        last['merged'] = gather_rows(last['part'], dist, world, rank, to_host=False)
+        # the last job's owner rows to rank 0, timed on its own
+        # beside the owner-rows step (barrier + synchronize on both sides, max
+        # over ranks): the reference's job also ends with separate reducer part
+        # files that `hadoop dfs -getmerge` pairs afterwards (README.md:35-38)
+        g_ms = []
+        for _ in range(max(1, min(args.steps, 5))):
+            dist.barrier()
+            torch.cuda.synchronize()
+            tg = time.perf_counter()
+            last['merged'] = gather_rows(last['part'], dist, world, rank, to_host=False)
+            torch.cuda.synchronize()
+            dist.barrier()
+            g_ms.append((time.perf_counter() - tg) * 1e3)
+        tg = torch.tensor([float(np.mean(g_ms))], dtype=torch.float64, device=eng.device)
+        dist.all_reduce(tg, op=dist.ReduceOp.MAX)
+        gather = {'gather_ms': float(tg.item()), 'repeats': len(g_ms)}
         if last['merged'] is not None:   # rank 0: every owner's rows
             n_rec = last['merged'][0].numel() // RECORD_DTYPE.itemsize
+        gather['bytes_to_rank0'] = int(last['merge_stats'].get('gather_rows_to_rank0', 0)) * RECORD_DTYPE.itemsize
     if args.dump and rank == 0:
         _dump(args.dump, last, eng, cap)
     checks = None
@@ -630,25 +735,20 @@ def rank_main(args, rank, world, local):
         checks['ok'] = checks['ok'] and checks['rerun_identical_records']
         log('checks: %s' % json.dumps(checks))
     elif not args.no_check:
-        # untimed checks of the distributed merge: the merged line counters
-        # cover every classified line of every shard; at world 1 the merged
-        # record set equals the single-GPU job's
-        n_cls = torch.tensor([int((gbuf >= 0).sum().item())], dtype=torch.int64, device=eng.device)
-        dist.all_reduce(n_cls)
+        # untimed checks of the distributed job at full size, the N = 1
+        # properties over the merged result (dist_full_size_checks)
+        checks = dist_full_size_checks(eng, batch, gbuf, compiled.n_rules, cap, last, step, dist, world, rank)
+        if world == 1 and rank == 0:
+            eng.reset(sizing['capacity'], cap)
+            eng.pass1(batch, gbuf)
+            if eng.resolve_cap():
+                eng.pass2(batch, gbuf)
+            checks['merged_eq_single_gpu_records'] = record_checksum(eng.emit_device('final')) == \
+                int(checks['merged_record_checksum'], 16)
+            checks['ok'] = checks['ok'] and checks['merged_eq_single_gpu_records']
         if rank == 0:
-            mrecs, mmatches = last['merged'][0], last['merged'][1]
-            c_merged = record_checksum(mrecs)
-            checks = {'merged_sum_matches_eq_classified_lines':
-                      int(mmatches[:compiled.n_rules].sum().item()) == int(n_cls.item()),
-                      'merged_record_checksum': '%016x' % c_merged}
-            if world == 1:
-                eng.reset(sizing['capacity'], cap)
-                eng.pass1(batch, gbuf)
-                if eng.resolve_cap():
-                    eng.pass2(batch, gbuf)
-                checks['merged_eq_single_gpu_records'] = record_checksum(eng.emit_device('final')) == c_merged
-            checks['ok'] = all(v for k, v in checks.items() if k != 'merged_record_checksum')
             log('checks: %s' % json.dumps(checks))
+    merge_exchange = merge_exchange_summary(last, dist, world, eng) if dist is not None else None
     sum_e = scan_work(compiled, batch, gbuf) if rank == 0 else 0
     if rank == 0:
         total_lines = lines * world * args.steps
@@ -685,6 +785,13 @@ def rank_main(args, rank, world, local):
                                         'scan-equivalent rate, not a utilisation'},
             'checks': checks,
         }
+        if dist is not None:
+            res['gather'] = dict(gather, ms_per_step_with_gather=dt / args.steps * 1e3 + gather['gather_ms'],
+                                 value_with_gather=total_lines / (dt + args.steps * gather['gather_ms'] * 1e-3),
+                                 definition='the owners\' final rows gathered to rank 0 (dist.gather_rows), timed '
+                                            'after the timed steps on its own; value/ms_per_step leave each owner\'s '
+                                            'rows in its HBM like the reference\'s reducer part files')
+            res['merge_exchange'] = merge_exchange
         if world == 1 and not args.no_cpu_baseline:
             res['cpu_baseline'] = cpu_baseline(wl)
             if not args.no_config1:

@@ -178,9 +178,7 @@ typedef struct rsa_pht_list {    /* 80 B: one list (or one chained chunk of a li
 #define RSA_OPT_FILTER_SLICE 5 /* auto filter: first 1/N (>= 1M lines) of a large batch builds the bound (default 256)       */
 #define RSA_OPT_FILTER_STEPS 7 /* auto filter: bound refinements, each after RSA_OPT_FILTER_GROWTH x the previous lines (default 3) */
 #define RSA_OPT_FILTER_GROWTH 24 /* auto filter: lines of each bound refinement's slice over the previous ones (default 4) */
-#define RSA_OPT_COUNT_STREAM 25 /* per-rule line/hit counting on a second HIP stream, overlapping the record merge (default 0) */
 #define RSA_OPT_CLASSIFY_PAIR 28 /* the global-memory bucket index (lists too large for LDS) classifies two lines per lane (1, default) or one (0) */
-#define RSA_OPT_RECOUNT_SELECTIVE 27 /* recount after a job whose thresholds moved below some bounds: only those rules' last-slice records are replayed (1) instead of every record with a backoff (0, default) */
 #define RSA_OPT_COUNTER_WORDS16 26 /* 16-bit gid|hit words between classification and counting when every gid fits 15 bits and the LDS histogram holds the rules (1, default) */
 #define RSA_OPT_FORCE_DEFER 8  /* TESTING: every index candidate goes to the exact deferred-line path        */
 #define RSA_OPT_PROFILE_SKIP 3 /* PROFILING ONLY, results invalid: bit0 skips counters, bit1 skips the table, bit2 skips table updates */
@@ -191,8 +189,8 @@ typedef struct rsa_pht_list {    /* 80 B: one list (or one chained chunk of a li
 #define RSA_OPT_STATS 10       /* PROFILING: count table work into the rsa_stats counters (default 0)                 */
 #define RSA_OPT_HOT_SPLIT 14   /* pre-combine regions holding > max(RSA_OPT_HOT_MIN, 4 x mean) records on all CUs (default 1) */
 #define RSA_OPT_HOT_MIN 15     /* hot-region minimum in records (default 65536; below it TESTING: any region above it is hot) */
-#define RSA_OPT_PARSE_MODE 16  /* text parse: 0 = each workgroup's lines staged in LDS, 1 = direct 4-byte HBM reads,
-                                  2 = register-window 16-byte HBM reads (default; text not 16-byte aligned: 0) */
+#define RSA_OPT_PARSE_STAGED 16 /* TESTING: the text parse stages each workgroup's lines in LDS (1) instead of register-window
+                                   16-byte HBM reads (0, default; text that is not 16-byte aligned is always staged) */
 #define RSA_OPT_REGION_IMPORT 17 /* rsa_import: records sorted by table region, merged per region in LDS (1, default) or device atomics per record (0) */
 #define RSA_OPT_OWNER_WORLD 19   /* multi-GPU merge (0 = off): the ctx's table also holds the merged entries of the rules it owns (gid % world == rank); rsa_export leaves those at home, rsa_emit returns only those */
 #define RSA_OPT_OWNER_RANK 20    /* this ctx's rank for RSA_OPT_OWNER_WORLD */

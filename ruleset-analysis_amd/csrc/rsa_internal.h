@@ -12,9 +12,9 @@ extern "C" {
 hipStream_t rsa_internal_stream(rsa_ctx* c);
 // Record `msg` as the ctx's last error and return `code`.
 int rsa_internal_fail(rsa_ctx* c, int code, const char* msg);
-// RSA_OPT_PARSE_MODE: 0 = lines staged in LDS per workgroup, 1 = direct HBM reads,
-// 2 = register-window reads (default).
-int rsa_internal_parse_mode(rsa_ctx* c);
+// RSA_OPT_PARSE_STAGED: the mapper-form parse stages each workgroup's lines in
+// LDS (k_parse) instead of the register-window reads (k_parse_win, default).
+int rsa_internal_parse_staged(rsa_ctx* c);
 }
 
 #endif

@@ -128,8 +128,6 @@ struct Agg {
   uint32_t np_bits;                  // 2^np_bits regions; a key's region = top np_bits of its slot hash
   uint32_t tent2;                    // pass 1's last slice: records of rules under a filter bound also go
                                      // into the pass-2 fields (exact when the final threshold equals the bound)
-  const uint8_t* replay;             // pass 2 (selective recount): per rule, 1 = its records of segment
-  uint32_t late_seg;                 //   late_seg are replayed (0xFFFFFFFF: every segment is replayed)
 };
 
 __device__ __forceinline__ unsigned long long mix64(unsigned long long x) {
@@ -2432,11 +2430,6 @@ static_assert(sizeof(HRec) == 40, "hot record layout");
 #ifndef RSA_COUNT_PER_CU
 #define RSA_COUNT_PER_CU 1   // k_count workgroups per CU (one is resident: 104 KiB LDS); fewer workgroups, fewer histogram-flush atomics
 #endif
-#ifndef RSA_RED_PF
-#define RSA_RED_PF 0   // A/B builds (bit 0 pass 1, bit 1 pass 2; pass 2 alone: neutral, r05pf2): k_reduce loads the next block step's record one step ahead (across rounds and
-                       // flushes); measured slower (r05r: cfg3 7.98 -> 8.04, cfg5 9.46 -> 9.58, cfg4 10.62 -> 10.69
-                       // ms/step): the inserts wait on LDS atomics and barriers, not on the record loads
-#endif
 #ifndef RSA_RED2_WPE
 #define RSA_RED2_WPE 8   // pass 2: 64 VGPRs, two 1024-thread workgroups per CU (73 KiB LDS each)
 #endif
@@ -2504,12 +2497,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
   uint32_t sg = 0;
   unsigned long long pos = is_hot ? hot_base[region] : starts[region];
   unsigned long long end = is_hot ? pos + total_recs : starts[region + 1];
-  // (RSA_RED_PF) this thread's record of the next block step -- or of the
-  // next round's first, loaded before the round-end barrier and the flush --
-  // read one step ahead: pf_at = its index in recs (kEmpty: none)
-  const uint4* R4 = reinterpret_cast<const uint4*>(recs);
-  uint4 pf0 = {0u, 0u, 0u, 0u}, pf1 = pf0;
-  unsigned long long pf_at = kEmpty;
   while (true) {
     while (pos >= end && sg + 1 < n_segs) {   // workgroup-uniform: next segment
       ++sg;
@@ -2536,28 +2523,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
             last = hr.last;
             cnt = hr.cnt;
           }
-        } else if (RSA_RED_PF & kPass) {   // (bit 0: pass 1, bit 1: pass 2)
-          uint4 a = pf0, b = pf1;
-          const bool hit = pf_at == pos + j;
-          if (have && !hit) {
-            a = R4[2 * (pos + j)];
-            b = R4[2 * (pos + j) + 1];
-          }
-          // the next step's (or next round's first block's) record, in flight
-          // during this step's inserts
-          const unsigned long long nj = (jb + blockDim.x < take ? pos + jb + blockDim.x : pos + take) + threadIdx.x;
-          pf_at = kEmpty;
-          if (nj < end) {
-            pf0 = R4[2 * nj];
-            pf1 = R4[2 * nj + 1];
-            pf_at = nj;
-          }
-          if (have) {
-            kA = ((unsigned long long)a.y << 32) | a.x;
-            kB = ((unsigned long long)a.w << 32) | a.z;
-            mo = ((unsigned long long)b.y << 32) | b.x;
-            first = last = b.z;
-          }
         } else {
           if (have) {
             const Rec r = recs[pos + j];
@@ -2570,9 +2535,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
         if (kPass == 2 && !is_hot && have) {   // (hot records of pass 2 were filtered when combined)
           const unsigned long long P = A.thresh[kB >> 32];
           if (P == RSA_NO_THRESHOLD || mo > P) have = false;
-          // selective recount: the last slice's records of rules whose
-          // pass-2 fields it already filled exactly are not replayed
-          if (sg == A.late_seg && !A.replay[kB >> 32]) have = false;
         }
         lds_agg_insert<kE, kPass == 1>(e_kA, e_kB, e_mo, e_first, e_last, e_cnt, used, have, kA, kB, mo,
                                                  first, last, cnt);
@@ -2851,7 +2813,6 @@ __global__ __launch_bounds__(1024) void k_hot_combine(const Rec* __restrict__ re
           if (kPass == 2 && have) {
             const unsigned long long P = A.thresh[r.kB >> 32];
             if (P == RSA_NO_THRESHOLD || r.order > P) have = false;
-            if (T.pad == A.late_seg && !A.replay[r.kB >> 32]) have = false;   // (selective recount)
           }
           lds_agg_insert<kE, kPass == 1>(e_kA, e_kB, e_mo, e_first, e_last, e_cnt, used, have, r.kA, r.kB, r.order,
                                          r.ts, r.ts, 1u);
@@ -2972,29 +2933,24 @@ __global__ void k_table_init(Slot* S, unsigned long long cap) {
 // [0]: some rule under a filter bound got a threshold other than the bound;
 // [1]: some rule without a bound is capped now.
 __global__ void k_tent_check(const unsigned long long* filter, const unsigned long long* thresh, uint32_t n_rules,
-                             uint32_t* out, uint8_t* replay) {
+                             uint32_t* out) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= n_rules) return;
   const unsigned long long f = filter[g], t = thresh[g];
   const bool moved = f != RSA_NO_THRESHOLD && t != f, now = f == RSA_NO_THRESHOLD && t != RSA_NO_THRESHOLD;
   if (moved) atomicAdd(&out[0], 1u);   // counts (RSA_DEBUG prints them)
   if (now) atomicAdd(&out[1], 1u);
-  // the rules whose last-slice pass-2 fields are not exact: their entries are
-  // cleared and all their records replayed (the others' late records are not)
-  if (replay) replay[g] = (moved || now) ? 1u : 0u;
 }
 
 // The pass-2 fields of every used slot back to empty (the last slice's
 // tentative counts are replayed by a full recount).
 __global__ void k_pass2_clear(Slot* S, const unsigned long long* used, const unsigned long long* n_p,
-                              unsigned long long cap, const uint8_t* replay = nullptr) {
+                              unsigned long long cap) {
   unsigned long long n = *n_p;
   if (n > cap) n = cap;
   const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
   for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const unsigned long long u = used[i];
-    if (replay && !replay[(uint32_t)(u >> 32)]) continue;   // (selective: only the replayed rules' entries)
-    Slot* s = &S[(uint32_t)u];
+    Slot* s = &S[(uint32_t)used[i]];
     s->count2 = 0;
     s->first2 = 0xFFFFFFFFu;
     s->last2 = 0;
@@ -3719,18 +3675,9 @@ struct rsa_ctx {
   bool tent2_on = false;                    // the current pass-1 launch is the last slice after the filter steps
   uint32_t late_seg = 0xFFFFFFFFu;          // its record segment (pass-2 fields of filtered rules hold its records)
   uint32_t tent_skip = 0;                   // jobs left without the tentative pass-2 fields (set when they missed)
-  // RSA_OPT_RECOUNT_SELECTIVE: measured slower (cfg3 8.08 vs 8.00-8.04,
-  // cfg5 9.76 vs 9.60 ms/step, profiles/r05m_*): at cfg3 no bound moves and
-  // 173 rules are capped only in the last slice, so the recount still reads
-  // every record while every job pays the tentative fields, a host read and
-  // the selective clear
-  bool recount_selective = false;
   bool classify_pair = true;            // RSA_OPT_CLASSIFY_PAIR: the global bucket image classifies two lines per lane
-  uint8_t* d_replay = nullptr;              // per rule: replay its late-slice records (k_tent_check)
-  uint32_t replay_alloc = 0;
-  uint32_t replay_seg = 0xFFFFFFFFu;        // the segment the recount filters by d_replay (0xFFFFFFFF: none)
   uint32_t* d_chk = nullptr;                // [0] a filtered rule's threshold moved, [1] a rule capped only now
-  int parse_mode = 2;                       // RSA_OPT_PARSE_MODE (textparse.hip): register-window reads
+  bool parse_staged = false;                // RSA_OPT_PARSE_STAGED (textparse.hip): LDS-staged lines, not register windows
   bool region_import = true;                // RSA_OPT_REGION_IMPORT: rsa_import by region sort + k_reduce
   bool slots_clean = true;                  // no slot holds a key of an earlier job (k_import's CAS claims need it)
   bool hot_split = true;                    // RSA_OPT_HOT_SPLIT
@@ -3820,10 +3767,6 @@ struct rsa_ctx {
   unsigned long long sort_alloc = 0;
   // pass-1 kernel timing (HIP events on the ctx stream)
   hipEvent_t ev[48] = {};             // per pass-1 launch: start, classified, aggregated
-  hipStream_t count_stream = nullptr; // per-rule counting overlapped with the record merge (RSA_OPT_COUNT_STREAM)
-  hipEvent_t ev_count[2] = {};        // fork / join of that stream
-  bool count_pending = false;
-  bool count_stream_on = false;       // RSA_OPT_COUNT_STREAM (measured neutral at cfg3: 7.87 vs 7.91 ms/step)
   bool gh16 = true;                   // RSA_OPT_COUNTER_WORDS16: 16-bit gid|hit words when the rules fit
   int ev_used = 0;
   bool debug = false;                 // RSA_DEBUG=1 in the environment: per-launch counts on stderr
@@ -3890,8 +3833,6 @@ Agg agg_of(const rsa_ctx* c) {
   a.rs_bits = c->rs_bits;
   a.np_bits = c->np_bits;
   a.tent2 = c->tent2_on ? 1u : 0u;
-  a.replay = c->d_replay;
-  a.late_seg = c->replay_seg;
   return a;
 }
 
@@ -4079,11 +4020,6 @@ constexpr int kMaxEvents = 48;
 int ensure_events(rsa_ctx* c) {
   for (int k = 0; k < kMaxEvents; ++k)
     if (!c->ev[k]) HIPCHK(c, hipEventCreate(&c->ev[k]));
-  if (c->count_stream_on && !c->count_stream) {
-    HIPCHK(c, hipStreamCreateWithFlags(&c->count_stream, hipStreamNonBlocking));
-    for (int k = 0; k < 2; ++k)
-      if (!c->ev_count[k]) HIPCHK(c, hipEventCreateWithFlags(&c->ev_count[k], hipEventDisableTiming));
-  }
   return RSA_OK;
 }
 
@@ -4304,21 +4240,10 @@ int launch_aggregate(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsig
     if (!(ag.skip & 1u) && m_count) {
       const uint64_t units = (m_count + 3) / 4;
       if (gh16_count) {
-        // 16-bit words (rules <= kCnt): counted on the side stream, overlapping
-        // the record sort and merge below (the counters are read only after
-        // the job; the main stream waits for them at the end of this launch)
+        // 16-bit words (rules <= kCnt)
         if (reinterpret_cast<uintptr_t>(gh16_count) & 15u) return fail(c, RSA_ERR_STATE, "misaligned counter words");
-        hipStream_t cs = c->count_stream ? c->count_stream : c->stream;
-        if (c->count_stream) {
-          HIPCHK(c, hipEventRecord(c->ev_count[0], c->stream));
-          HIPCHK(c, hipStreamWaitEvent(cs, c->ev_count[0], 0));
-        }
-        k_count16<kCnt><<<grid_for_threads(c, (m_count + 7) / 8 + 1, 1024, RSA_COUNT_PER_CU), 1024, 0, cs>>>(
+        k_count16<kCnt><<<grid_for_threads(c, (m_count + 7) / 8 + 1, 1024, RSA_COUNT_PER_CU), 1024, 0, c->stream>>>(
             gh16_count, m_count, c->n_rules, ag);
-        if (c->count_stream) {
-          HIPCHK(c, hipEventRecord(c->ev_count[1], cs));
-          c->count_pending = true;
-        }
       } else if (c->n_rules <= (uint32_t)kCnt) {
         k_count<kCnt><<<grid_for_threads(c, units, 1024, RSA_COUNT_PER_CU), 1024, 0, c->stream>>>(gh_count, m_count,
                                                                                                   c->n_rules, ag);
@@ -4348,13 +4273,7 @@ int launch_aggregate(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsig
     }
   }
   HIPCHK(c, hipGetLastError());
-  if (ag.cap == 0 || (ag.skip & 2u)) {   // no table this job
-    if (c->count_pending) {
-      HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_count[1], 0));
-      c->count_pending = false;
-    }
-    return RSA_OK;
-  }
+  if (ag.cap == 0 || (ag.skip & 2u)) return RSA_OK;   // no table this job
   const Rec* recs = reinterpret_cast<const Rec*>(c->d_recs);
   // region-sorted records: at the launch's line offset while this job's
   // records are kept for the recount (rsa_recount), else from 0
@@ -4413,10 +4332,6 @@ int launch_aggregate(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsig
     HIPCHK(c, hipMemcpyAsync(&nr, total, sizeof nr, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     fprintf(stderr, "[rsa] pass-1 launch: %llu lines -> %u records\n", (unsigned long long)m, nr);
-  }
-  if (c->count_pending) {   // the side stream's counters join the ctx stream
-    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_count[1], 0));
-    c->count_pending = false;
   }
   return RSA_OK;
 }
@@ -4596,13 +4511,10 @@ int rsa_ctx_destroy(rsa_ctx* c) {
                   c->d_slots, c->d_used, c->d_ukey, c->d_used_n, c->d_filter, c->d_packed, c->d_hot, c->d_hot_tasks, c->d_hot_base,
                   c->d_hot_fill, c->d_hot_ctl, c->d_hot_total, c->d_cnt_words, c->d_cnt_starts,
                   c->d_cnt_tasks, c->d_cnt_ctl, c->d_flags, c->d_cursor, c->d_job_recs, c->d_cidx,
-                  c->d_capped_gid, c->d_capped_cnt, c->d_capped_start, c->d_capped_prev, c->d_keys, c->d_chk, c->d_replay};
+                  c->d_capped_gid, c->d_capped_cnt, c->d_capped_start, c->d_capped_prev, c->d_keys, c->d_chk};
   for (void* b : bufs) (void)hipFree(b);
   for (int k = 0; k < kMaxEvents; ++k)
     if (c->ev[k]) (void)hipEventDestroy(c->ev[k]);
-  for (int k = 0; k < 2; ++k)
-    if (c->ev_count[k]) (void)hipEventDestroy(c->ev_count[k]);
-  if (c->count_stream) (void)hipStreamDestroy(c->count_stream);
   delete c;
   return RSA_OK;
 }
@@ -4651,10 +4563,8 @@ int rsa_set_option(rsa_ctx* c, int option, int64_t value) {
     case RSA_OPT_PRECHECK:
       c->precheck = value != 0;
       return RSA_OK;
-    case RSA_OPT_PARSE_MODE:
-      if (value < 0 || value > 2)
-        return fail(c, RSA_ERR_ARG, "parse mode must be 0 (LDS staged), 1 (direct) or 2 (register window)");
-      c->parse_mode = (int)value;
+    case RSA_OPT_PARSE_STAGED:
+      c->parse_staged = value != 0;
       return RSA_OK;
     case RSA_OPT_MIN_REGIONS_LOG2:
       if (value < 0 || value > 12) return fail(c, RSA_ERR_ARG, "RSA_OPT_MIN_REGIONS_LOG2 must be 0..12");
@@ -4663,22 +4573,11 @@ int rsa_set_option(rsa_ctx* c, int option, int64_t value) {
     case RSA_OPT_REDUCE_BIG:
       c->reduce_big = value != 0;
       return RSA_OK;
-    case RSA_OPT_COUNT_STREAM:
-      c->count_stream_on = value != 0;
-      if (!c->count_stream_on && c->count_stream) {
-        HIPCHK(c, hipStreamSynchronize(c->count_stream));
-        HIPCHK(c, hipStreamDestroy(c->count_stream));
-        c->count_stream = nullptr;
-      }
-      return RSA_OK;
     case RSA_OPT_COUNTER_WORDS16:
       c->gh16 = value != 0;
       return RSA_OK;
     case RSA_OPT_CLASSIFY_PAIR:
       c->classify_pair = value != 0;
-      return RSA_OK;
-    case RSA_OPT_RECOUNT_SELECTIVE:
-      c->recount_selective = value != 0;
       return RSA_OK;
     case RSA_OPT_REGION_RECORDS:
       if (value < 0 || value > 0xFFFFFFFFll) return fail(c, RSA_ERR_ARG, "RSA_OPT_REGION_RECORDS must be 0..2^32-1");
@@ -4724,7 +4623,7 @@ int rsa_set_option(rsa_ctx* c, int option, int64_t value) {
 
 hipStream_t rsa_internal_stream(rsa_ctx* c) { return c->stream; }
 int rsa_internal_fail(rsa_ctx* c, int code, const char* msg) { return fail(c, code, "%s", msg); }
-int rsa_internal_parse_mode(rsa_ctx* c) { return c->parse_mode; }
+int rsa_internal_parse_staged(rsa_ctx* c) { return c->parse_staged ? 1 : 0; }
 
 int rsa_sync(rsa_ctx* c) {
   if (!c) return RSA_ERR_ARG;
@@ -5166,21 +5065,12 @@ int rsa_recount(rsa_ctx* c, const rsa_tuple* T, const uint32_t* TS, const uint64
   uint32_t n_segs = c->n_segs;
   const bool tent = c->late_seg != 0xFFFFFFFFu;
   bool clear = tent;
-  bool selective = false;
   const bool cached = c->rec_cache && c->cache_T == (const void*)T && c->cache_n == n && c->n_segs > 0;
   if (tent && cached && c->late_seg + 1 == c->n_segs && c->n_rules) {
     if (!c->d_chk) HIPCHK(c, hipMalloc(&c->d_chk, 2 * sizeof(uint32_t)));
-    if (c->recount_selective && c->replay_alloc < c->n_rules) {
-      HIPCHK(c, hipStreamSynchronize(c->stream));
-      hipFree(c->d_replay);
-      c->d_replay = nullptr;
-      c->replay_alloc = 0;
-      HIPCHK(c, hipMalloc(&c->d_replay, c->n_rules));
-      c->replay_alloc = c->n_rules;
-    }
     HIPCHK(c, hipMemsetAsync(c->d_chk, 0, 2 * sizeof(uint32_t), c->stream));
     k_tent_check<<<(c->n_rules + kBlock - 1) / kBlock, kBlock, 0, c->stream>>>(
-        c->d_filter, c->d_thresh, c->n_rules, c->d_chk, c->recount_selective ? c->d_replay : nullptr);
+        c->d_filter, c->d_thresh, c->n_rules, c->d_chk);
     uint32_t h[2] = {1u, 1u};
     HIPCHK(c, hipMemcpyAsync(h, c->d_chk, sizeof h, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -5188,20 +5078,13 @@ int rsa_recount(rsa_ctx* c, const rsa_tuple* T, const uint32_t* TS, const uint64
     if (!h[0] && !h[1]) {
       clear = false;
       n_segs = c->late_seg;   // the last slice is already counted
-    } else if (c->recount_selective) {
-      // only the rules whose bound moved or that were capped only now are
-      // cleared and replayed from the last slice; the others keep its exact
-      // pass-2 fields (no backoff: the next jobs keep the tentative fields)
-      selective = true;
     }
-    c->tent_skip = clear && !selective ? kTentBackoff : 0u;
+    c->tent_skip = clear ? kTentBackoff : 0u;
   }
   if (clear) {
-    k_pass2_clear<<<c->cu_count * 8, kBlock, 0, c->stream>>>(c->d_slots, c->d_used, c->d_used_n, c->slot_alloc,
-                                                            selective ? c->d_replay : nullptr);
+    k_pass2_clear<<<c->cu_count * 8, kBlock, 0, c->stream>>>(c->d_slots, c->d_used, c->d_used_n, c->slot_alloc);
     HIPCHK(c, hipGetLastError());
   }
-  c->replay_seg = selective ? c->late_seg : 0xFFFFFFFFu;
   c->late_seg = 0xFFFFFFFFu;   // (a second recount replays everything)
   if (cached) {
     // every occurrence with order <= P of a capped rule produced a pass-1
@@ -5219,10 +5102,8 @@ int rsa_recount(rsa_ctx* c, const rsa_tuple* T, const uint32_t* TS, const uint64
     k_reduce<2><<<1u << c->np_bits, 1024, 0, c->stream>>>(reinterpret_cast<const Rec*>(c->d_recs2), c->d_starts,
                                                          n_segs, agg_of(c), hb, hf, hr, skip);
     HIPCHK(c, hipGetLastError());
-    c->replay_seg = 0xFFFFFFFFu;
     return RSA_OK;
   }
-  c->replay_seg = 0xFFFFFFFFu;   // (the uncached recount replays every line)
   if (!G) {
     // re-classify into scratch gids
     if (!c->rules_loaded) return fail(c, RSA_ERR_STATE, "no rules loaded (recount without gids re-classifies)");

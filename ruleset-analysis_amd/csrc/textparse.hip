@@ -219,9 +219,6 @@ __global__ void k_set_u64(uint64_t* p, uint64_t v) { *p = v; }
 // 28 KB of staged text + the scan's slots and tables: four workgroups per CU
 // (a workgroup whose lines average more than 224 B defers them to the slow pass)
 constexpr uint32_t kParseWG = 128, kStageBytes = 28672;
-#ifndef RSA_OK_FULLBITS
-#define RSA_OK_FULLBITS 0   // A/B builds: order-key window sorts over all 64 key bits, not only the bits that vary
-#endif
 #ifndef RSA_TPL_PROF
 #define RSA_TPL_PROF 0   // PROFILING builds only (results invalid): 1 template scan without tpl_finish, 2 no scan either
 #endif
@@ -241,23 +238,20 @@ __device__ __forceinline__ void defer_append(bool defer, uint64_t i, uint32_t* _
 }
 
 // kReduce: the reducer drop-in's lines (rsa_text::reduce_line, plus the
-// same-key flag against the previous line of the batch).
-// kDirect: no staging, every lane reads its line from HBM through 4-byte
-// loads (no LDS: occupancy bound by registers only).
-// Both parse the template form only (kDefer): other classified lines go to
-// the slow list for k_parse_slow.
-template <bool kReduce, bool kDirect>
+// same-key flag against the previous line of the batch).  The workgroup's
+// lines are staged in LDS; the mapper form runs here only for text that is not
+// 16-byte aligned (k_parse_win is the default).  Both parse the template form
+// only (kDefer): other classified lines go to the slow list for k_parse_slow.
+template <bool kReduce>
 __global__ __launch_bounds__(kParseWG) void k_parse(const uint8_t* __restrict__ text, const uint64_t* __restrict__ off,
                                                     uint64_t n_lines, const rsa_parse_ifc* __restrict__ ifcs,
                                                     uint32_t n_ifcs, const rsa_parse_spell* __restrict__ spells,
                                                     uint32_t n_spells, rsa_tuple* __restrict__ tuples,
                                                     uint32_t* __restrict__ ts_out, uint32_t* __restrict__ disp,
                                                     uint32_t* __restrict__ slow_idx, unsigned int* __restrict__ slow_n) {
-  __shared__ uint32_t sm[kDirect ? 1 : kStageBytes / 4 + 8];   // (+8: tpl_finish's 16-B field reads past a line)
-  // the template scan (rsa_text::tpl) over the staged lines; the direct mode
-  // keeps the per-lane template path (the scan's byte-per-step HBM loads were
-  // 2.3x slower there: profiles/r03y_text_parse_modes.txt)
-  constexpr bool kScan = !kReduce && !kDirect;
+  __shared__ uint32_t sm[kStageBytes / 4 + 8];   // (+8: tpl_finish's 16-B field reads past a line)
+  // the template scan (rsa_text::tpl) over the staged lines
+  constexpr bool kScan = !kReduce;
   __shared__ uint32_t tprog[kScan ? rsa_text::tpl::kProgLen : 1];
   __shared__ uint8_t tcls[kScan ? 256 : 1];
   __shared__ uint32_t tslot[kScan ? kParseWG * rsa_text::tpl::kSlotWords : 1];
@@ -269,52 +263,6 @@ __global__ __launch_bounds__(kParseWG) void k_parse(const uint8_t* __restrict__ 
   const uint64_t l0 = (uint64_t)blockIdx.x * kParseWG;
   const uint64_t l1 = l0 + kParseWG < n_lines ? l0 + kParseWG : n_lines;
   const uint64_t n_bytes = off[n_lines];
-  if (kDirect) {
-    if (kScan) __syncthreads();   // the scan tables (before any lane leaves)
-    const uint64_t i = l0 + threadIdx.x;
-    if (i >= l1) return;
-    const uint64_t a = off[i], b = off[i + 1];
-    uint64_t len = b - a;
-    if (len && text[b - 1] == '\n') --len;
-    rsa_tuple tup = {0u, 0u, 0, 0, 0, 0, 0};
-    uint32_t ts = 0, d = RSA_LINE_HOST;
-    if (kScan) {
-      d = rsa_text::kLineDefer;
-      if (len < 0xFFFFu) {
-        const uint64_t nw = n_bytes >> 2;
-        uint32_t tail = 0;
-        for (uint32_t k = 0; k < (uint32_t)(n_bytes & 3u); ++k) tail |= (uint32_t)text[4 * nw + k] << (8 * k);
-        const rsa_text::GWordU s{reinterpret_cast<const uint32_t*>(text), a, nw, tail, (uint32_t)len};
-        uint32_t* slot = tslot + threadIdx.x * rsa_text::tpl::kSlotWords;
-        if (!(rsa_text::tpl::scan(s, tprog, tcls, slot) &&
-              rsa_text::tpl_finish(s, slot, ifcs, n_ifcs, spells, n_spells, tup, ts, d))) {
-          tup = rsa_tuple{0u, 0u, 0, 0, 0, 0, 0};
-          ts = 0;
-          d = rsa_text::kLineDefer;
-        }
-      }
-    } else if (len < 0xFFFFFFFFull) {
-      const rsa_text::GWordLn s{reinterpret_cast<const uint32_t*>(text), text, a, n_bytes, (uint32_t)len, ~0ull, 0u};
-      if (kReduce) {
-        rsa_text::reduce_line<true>(s, spells, n_spells, tup, ts, d);
-        if (i > 0 && d != RSA_RED_NOISE && d != rsa_text::kLineDefer) {
-          const uint64_t pa = off[i - 1];
-          uint64_t plen = a - pa;
-          if (plen && text[a - 1] == '\n') --plen;
-          const rsa_text::GWordLn q{reinterpret_cast<const uint32_t*>(text), text, pa, n_bytes, (uint32_t)plen, ~0ull,
-                                    0u};
-          if (plen < 0xFFFFFFFFull && rsa_text::same_key(s, q)) d |= RSA_RED_SAME_KEY;
-        }
-      } else {
-        rsa_text::parse_line<true>(s, ifcs, n_ifcs, spells, n_spells, tup, ts, d);
-      }
-    }
-    defer_append(d == rsa_text::kLineDefer, i, slow_idx, slow_n);
-    tuples[i] = tup;
-    ts_out[i] = ts;
-    disp[i] = d;
-    return;
-  }
   const uint64_t base = off[l0] & ~3ull, span = off[l1] - base;
   const bool staged = span <= kStageBytes;   // workgroup-uniform
   if (staged) {
@@ -408,15 +356,7 @@ __device__ __forceinline__ uint4 text_chunk(const uint4* __restrict__ t16, const
   return uint4{w[0], w[1], w[2], w[3]};
 }
 
-#ifndef RSA_PARSE_WIN_WAVES
-#define RSA_PARSE_WIN_WAVES 0   // A/B builds: minimum waves per SIMD for k_parse_win (register cap; 0 = compiler's choice)
-#endif
-#if RSA_PARSE_WIN_WAVES
-#define RSA_PARSE_WIN_ATTR __attribute__((amdgpu_waves_per_eu(RSA_PARSE_WIN_WAVES, 8)))
-#else
-#define RSA_PARSE_WIN_ATTR
-#endif
-__global__ __launch_bounds__(kParseWG) RSA_PARSE_WIN_ATTR void k_parse_win(const uint8_t* __restrict__ text,
+__global__ __launch_bounds__(kParseWG) void k_parse_win(const uint8_t* __restrict__ text,
                                                        const uint64_t* __restrict__ off, uint64_t n_lines,
                                                        const rsa_parse_ifc* __restrict__ ifcs, uint32_t n_ifcs,
                                                        const rsa_parse_spell* __restrict__ spells, uint32_t n_spells,
@@ -1280,121 +1220,18 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(const K* __restrict__
   }
 }
 
-// One-pass scan of 32-bit elements (decoupled look-back, as k_nl_offsets):
-// workgroups take the tiles in launch order (an atomic ticket), scan their
-// tile in registers, publish its aggregate, combine the predecessors' walking
-// back to the first published inclusive prefix, publish their own, and write
-// the tile once -- one read and one write of the data, where the three-pass
-// form (k_scan_tiles, k_scan_tile_sums, k_scan_tiles_add) read and wrote it
-// twice.  state: one look-back word per tile, then the ticket and a flag
-// (zeroed by the caller).
-template <typename Op, bool kIncl>
-__global__ __launch_bounds__(kScanThreads) void k_scan_lb(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
-                                                          uint64_t n, unsigned long long* __restrict__ state,
-                                                          unsigned int* __restrict__ ticket) {
-  __shared__ uint32_t sh[16];
-  __shared__ uint32_t sh_b, sh_prefix;
-  if (threadIdx.x == 0) sh_b = atomicAdd(&ticket[0], 1u);
-  __syncthreads();
-  const uint32_t b = sh_b;
-  const uint64_t beg = (uint64_t)b * kScanTile + (uint64_t)threadIdx.x * kScanPer;
-  const bool vec = beg + kScanPer <= n && ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15u) == 0;
-  uint32_t v[kScanPer];
-  if (vec) {
-    const uint4 q = *reinterpret_cast<const uint4*>(in + beg);
-    v[0] = q.x;
-    v[1] = q.y;
-    v[2] = q.z;
-    v[3] = q.w;
-  } else {
-#pragma unroll
-    for (uint32_t k = 0; k < kScanPer; ++k) v[k] = beg + k < n ? in[beg + k] : Op::template id<uint32_t>();
-  }
-  uint32_t c = Op::template id<uint32_t>();
-#pragma unroll
-  for (uint32_t k = 0; k < kScanPer; ++k) c = Op::f(c, v[k]);
-  uint32_t ex, inc, total;
-  wg_scan<Op>(c, sh, ex, inc, total);
-  if (threadIdx.x < 64) {
-    const uint32_t lane = threadIdx.x;
-    uint32_t run = Op::template id<uint32_t>();
-    if (b == 0) {
-      if (lane == 0) __hip_atomic_store(&state[0], kLbIncl | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      if (lane == 0) __hip_atomic_store(&state[b], kLbAgg | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      int64_t top = (int64_t)b - 1;   // the window is tiles (top - 63, top]
-      uint32_t spins = 0;
-      while (true) {
-        const int64_t p = top - (int64_t)lane;
-        const unsigned long long w =
-            p >= 0 ? __hip_atomic_load(&state[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbIncl;
-        const unsigned long long incl = __ballot((w & kLbIncl) != 0);
-        const int stop = incl ? __builtin_ctzll(incl) : 64;   // lanes [0, stop) must be aggregates
-        const unsigned long long ready = __ballot((w & (kLbIncl | kLbAgg)) != 0);
-        const unsigned long long need = stop >= 64 ? ~0ull : ((2ull << stop) - 1ull);
-        if ((ready & need) != need) {   // someone in the window not published yet: look again
-          if (++spins > kLbSpinMax) {
-            if (lane == 0) atomicOr(&ticket[1], 1u);
-            break;
-          }
-          continue;
-        }
-        uint32_t x = ((int)lane <= stop && p >= 0) ? (uint32_t)(w & 0xFFFFFFFFull) : Op::template id<uint32_t>();
-        for (int o = 32; o > 0; o >>= 1) x = Op::f(x, (uint32_t)__shfl_xor((int)x, o));
-        run = Op::f(run, x);
-        if (stop < 64) break;
-        top -= 64;
-      }
-      if (lane == 0)
-        __hip_atomic_store(&state[b], kLbIncl | Op::f(run, total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (lane == 0) sh_prefix = run;
-  }
-  __syncthreads();
-  uint32_t r = Op::f(sh_prefix, ex);
-  uint32_t o[kScanPer];
-#pragma unroll
-  for (uint32_t k = 0; k < kScanPer; ++k) {
-    const uint32_t nx = Op::f(r, v[k]);
-    o[k] = kIncl ? nx : r;
-    r = nx;
-  }
-  if (vec) {
-    *reinterpret_cast<uint4*>(out + beg) = uint4{o[0], o[1], o[2], o[3]};
-  } else {
-#pragma unroll
-    for (uint32_t k = 0; k < kScanPer; ++k)
-      if (beg + k < n) out[beg + k] = o[k];
-  }
-}
 
-#ifndef RSA_SCAN_LB
-#define RSA_SCAN_LB 0   // A/B builds: 1 = the one-pass look-back scan, measured slower (order keys 8.54 -> 8.71 ms at
-                        // 30M lines, profiles/r05/ab_summary.txt r05lb: the tile-state clear and the in-order
-                        // look-back cost more than the second pass over the data)
-#endif
-
-// host: scan of n elements.  sums: scan_sums_len(n) words -- the three-pass
-// form's tile sums, or the one-pass form's look-back words (u64 per tile)
-// and ticket
+// host: scan of n elements (three passes: tile scans, a scan of the tile
+// sums, the sums added back).  sums: scan_sums_len(n) words
 template <typename Op, bool kIncl, typename Tin, typename Tout>
 void scan(hipStream_t st, const Tin* in, Tout* out, uint64_t n, Tout* sums) {
   if (!n) return;
   const uint32_t nb = (uint32_t)((n + kScanTile - 1) / kScanTile);
-  if (RSA_SCAN_LB && sizeof(Tin) == 4 && sizeof(Tout) == 4 && (reinterpret_cast<uintptr_t>(sums) & 7u) == 0) {
-    unsigned long long* state = reinterpret_cast<unsigned long long*>(sums);   // (sums is 8-B aligned)
-    unsigned int* ticket = reinterpret_cast<unsigned int*>(state + nb);
-    (void)hipMemsetAsync(state, 0, (size_t)nb * 8 + 8, st);
-    hipLaunchKernelGGL((k_scan_lb<Op, kIncl>), dim3(nb), dim3(kScanThreads), 0, st,
-                       reinterpret_cast<const uint32_t*>(in), reinterpret_cast<uint32_t*>(out), n, state, ticket);
-    return;
-  }
   hipLaunchKernelGGL((k_scan_tiles<Op, kIncl, Tin, Tout>), dim3(nb), dim3(kScanThreads), 0, st, in, out, n, sums);
   hipLaunchKernelGGL((k_scan_tile_sums<Op, Tout>), dim3(1), dim3(kScanThreads), 0, st, sums, nb);
   hipLaunchKernelGGL((k_scan_tiles_add<Op, Tout>), dim3(nb), dim3(kScanThreads), 0, st, out, n, sums);
 }
 
-// (u32 words: room for a u64 look-back word per tile plus the ticket)
 inline size_t scan_sums_len(uint64_t n) { return 2 * ((size_t)((n + kScanTile - 1) / kScanTile) + 2); }
 
 // scratch of radix_pairs for n elements: hist (256 per tile) and its scan sums
@@ -1565,15 +1402,13 @@ int rsa_parse_text(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_off, uin
   unsigned int* slow_n = static_cast<unsigned int*>(L.base);
   uint32_t* slow_idx = reinterpret_cast<uint32_t*>(static_cast<char*>(L.base) + 16);
   TPCHK(c, hipMemsetAsync(slow_n, 0, 4, st));
-  const int mode = rsa_internal_parse_mode(c);
-  if (mode == 2 && !(reinterpret_cast<uintptr_t>(d_text) & 15u))
+  // register-window reads need 16-byte aligned text; otherwise the lines are
+  // staged in LDS (RSA_OPT_PARSE_STAGED forces that form, for its tests)
+  if (!rsa_internal_parse_staged(c) && !(reinterpret_cast<uintptr_t>(d_text) & 15u))
     hipLaunchKernelGGL(k_parse_win, dim3((uint32_t)nb), dim3(kParseWG), 0, st, d_text, d_off, n_lines, d_ifcs, n_ifcs,
                        d_spells, n_spells, d_tuples, d_ts, d_disp, slow_idx, slow_n);
-  else if (mode == 1)
-    hipLaunchKernelGGL((k_parse<false, true>), dim3((uint32_t)nb), dim3(kParseWG), 0, st, d_text, d_off, n_lines, d_ifcs,
-                       n_ifcs, d_spells, n_spells, d_tuples, d_ts, d_disp, slow_idx, slow_n);
   else
-    hipLaunchKernelGGL((k_parse<false, false>), dim3((uint32_t)nb), dim3(kParseWG), 0, st, d_text, d_off, n_lines, d_ifcs,
+    hipLaunchKernelGGL((k_parse<false>), dim3((uint32_t)nb), dim3(kParseWG), 0, st, d_text, d_off, n_lines, d_ifcs,
                        n_ifcs, d_spells, n_spells, d_tuples, d_ts, d_disp, slow_idx, slow_n);
   hipLaunchKernelGGL((k_parse_slow<false>), dim3((uint32_t)(nb < kSlowGrid ? nb : kSlowGrid)), dim3(kParseWG), 0, st,
                      d_text, d_off, n_lines, d_ifcs, n_ifcs, d_spells, n_spells, slow_idx, slow_n, d_tuples, d_ts,
@@ -1608,12 +1443,8 @@ int rsa_parse_reduce(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_off, u
   unsigned int* slow_n = static_cast<unsigned int*>(L.base);
   uint32_t* slow_idx = reinterpret_cast<uint32_t*>(static_cast<char*>(L.base) + 16);
   TPCHK(c, hipMemsetAsync(slow_n, 0, 4, st));
-  if (rsa_internal_parse_mode(c) == 1)
-    hipLaunchKernelGGL((k_parse<true, true>), dim3((uint32_t)nb), dim3(kParseWG), 0, st, d_text, d_off, n_lines, nullptr,
-                       0u, d_spells, n_spells, d_tuples, d_ts, d_disp, slow_idx, slow_n);
-  else
-    hipLaunchKernelGGL((k_parse<true, false>), dim3((uint32_t)nb), dim3(kParseWG), 0, st, d_text, d_off, n_lines, nullptr,
-                       0u, d_spells, n_spells, d_tuples, d_ts, d_disp, slow_idx, slow_n);
+  hipLaunchKernelGGL((k_parse<true>), dim3((uint32_t)nb), dim3(kParseWG), 0, st, d_text, d_off, n_lines, nullptr, 0u,
+                     d_spells, n_spells, d_tuples, d_ts, d_disp, slow_idx, slow_n);
   hipLaunchKernelGGL((k_parse_slow<true>), dim3((uint32_t)(nb < kSlowGrid ? nb : kSlowGrid)), dim3(kParseWG), 0, st,
                      d_text, d_off, n_lines, nullptr, 0u, d_spells, n_spells, slow_idx, slow_n, d_tuples, d_ts, d_disp);
   TPCHK(c, hipGetLastError());
@@ -1799,7 +1630,7 @@ int rsa_order_keys_grouped(rsa_ctx* c, const uint8_t* d_text, const uint64_t* d_
       // every class already in key order: no sort
       hipLaunchKernelGGL(k_split_vals, dim3(blocks(m, 256)), dim3(256), 0, st, valsA, m, gs, ids);
     } else {
-      const uint64_t vary = RSA_OK_FULLBITS ? ~0ull : (uint64_t)h_live[2] << 32 | h_live[1];
+      const uint64_t vary = (uint64_t)h_live[2] << 32 | h_live[1];
       const unsigned b0 = vary ? (unsigned)__builtin_ctzll(vary) : 0u;
       const unsigned b1 = vary ? 64u - (unsigned)__builtin_clzll(vary) : 0u;
       // stable LSD: by the chunk key, then by the group start

@@ -159,12 +159,13 @@ class Exported(object):
                                                                                   device=device), 0)
 
 
-def route_records(exp, world, dist, group=None, flag=0):
+def route_records(exp, world, dist, group=None, flag=0, stats=None, phase='route'):
     """all_to_all of an owner-grouped export (``Exported``) to the owners;
     returns the received bytes.  The per-owner counts go first, with ``flag``
     (this rank's error flag) riding along, and the phase's ONE host read takes
     the send and receive sizes together; if any rank sent a non-zero flag,
-    every rank returns None instead."""
+    every rank returns None instead.  ``stats`` (a dict): the rows this rank
+    sent to other ranks, kept to itself and received, under ``phase``."""
     import torch
     counts = exp.counts.to(torch.int64)
     send_c = torch.stack([counts, torch.full_like(counts, int(flag))], 1).reshape(-1)
@@ -177,8 +178,15 @@ def route_records(exp, world, dist, group=None, flag=0):
     buf = exp.buf
     if total > exp.capacity:      # the export dropped rows past its buffer: again at the exact size
         buf, _counts, _cap = exp.again(total)
+        if stats is not None:
+            stats['reexports'] = stats.get('reexports', 0) + 1
     sc = [c * REC for c in h[:world]]
     rc = [h[world + 2 * r] * REC for r in range(world)]
+    if stats is not None:
+        rank = dist.get_rank(group)
+        stats[phase + '_sent_rows'] = total - h[rank]
+        stats[phase + '_self_rows'] = h[rank]
+        stats[phase + '_recv_rows'] = sum(rc) // REC - h[world + 2 * rank]
     out = torch.empty(sum(rc), dtype=torch.uint8, device=buf.device)
     _all_to_all(out, buf[:total * REC], dist, group, rc, sc)
     return out
@@ -212,7 +220,7 @@ def gather_rows(part, dist, world, rank, group=None, to_host=True):
     return merged_to_host(out) if to_host else out
 
 
-def merge(backend, dist, world, rank, group=None, to_host=True, gather=True):
+def merge(backend, dist, world, rank, group=None, to_host=True, gather=True, stats=None):
     """Run the protocol; returns (records, matches, hits, distinct, thresh) on
     rank 0 and None elsewhere: numpy arrays (records as RECORD_DTYPE rows), or
     with to_host=False the device tensors as they stand in rank 0's HBM
@@ -225,7 +233,9 @@ def merge(backend, dist, world, rank, group=None, to_host=True, gather=True):
     thresholds (with the import overflow need), the pass-2 route counts, and
     the gather sizes (riding on the distinct-count all_reduce).  At world 1
     there is no collective and no extra read: the shard's own cap resolution
-    says whether pass 2 runs, as in the single-GPU job."""
+    says whether pass 2 runs, as in the single-GPU job.  ``stats`` (a dict)
+    receives the rows each exchange moved (route_records) and the collective
+    bytes of the counter, threshold and size vectors."""
     import torch
     tr = _Trace(rank)
     c = backend.counters()
@@ -253,7 +263,7 @@ def merge(backend, dist, world, rank, group=None, to_host=True, gather=True):
             failed = 1
         tr('export1', dev)
         if multi:
-            recv = route_records(exported, world, dist, group, flag=failed)
+            recv = route_records(exported, world, dist, group, flag=failed, stats=stats, phase='route1')
             if recv is None:
                 raise ShardOverflow('distinct-connection table overflow on at least one rank')
             tr('route1', dev)
@@ -292,7 +302,7 @@ def merge(backend, dist, world, rank, group=None, to_host=True, gather=True):
                 backend.set_thresh(thresh)
             backend.recount()
             if multi:
-                recv2 = route_records(backend.export(1), world, dist, group)
+                recv2 = route_records(backend.export(1), world, dist, group, stats=stats, phase='route2')
                 if recv2.numel():
                     backend.import_records(recv2, 1)
             tr('pass2', dev)
@@ -311,6 +321,12 @@ def merge(backend, dist, world, rank, group=None, to_host=True, gather=True):
     finally:
         backend.set_owner(0, 0)
     sizes = [int(s) for s in dsz[n_rules:].cpu().tolist()] if multi else [final.numel()]
+    if stats is not None and multi:
+        # all_reduce payloads: line+hit counters, thresholds (+ flag), distinct counts + row sizes
+        stats['allreduce_bytes'] = 8 * (2 * n_rules + (n_rules + 1) + (n_rules + world))
+        stats['pass2'] = bool(capped_any)
+        stats['owner_rows'] = final.numel() // REC
+        stats['gather_rows_to_rank0'] = sum(sizes[1:]) // REC
     if not gather:
         tr('end', dev)
         return OwnerRows(final, sizes, c['matches'], c['hits'], distinct, thresh)

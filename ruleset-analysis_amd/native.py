@@ -37,10 +37,10 @@ RSA_OPT_STATS = 10
 RSA_OPT_WAVE_CAP_SCATTER = 11
 RSA_OPT_GROUP_TASKS = 12
 RSA_OPT_PROFILE_CLASSIFY = 13
-RSA_OPT_HOT_SPLIT, RSA_OPT_HOT_MIN, RSA_OPT_PARSE_MODE, RSA_OPT_REGION_IMPORT = 14, 15, 16, 17
+RSA_OPT_HOT_SPLIT, RSA_OPT_HOT_MIN, RSA_OPT_PARSE_STAGED, RSA_OPT_REGION_IMPORT = 14, 15, 16, 17
 RSA_OPT_COUNT_SORT, RSA_OPT_OWNER_WORLD, RSA_OPT_OWNER_RANK, RSA_OPT_MIN_REGIONS_LOG2 = 18, 19, 20, 21
 RSA_OPT_REGION_RECORDS, RSA_OPT_REDUCE_BIG, RSA_OPT_FILTER_GROWTH = 22, 23, 24
-RSA_OPT_COUNT_STREAM, RSA_OPT_COUNTER_WORDS16, RSA_OPT_RECOUNT_SELECTIVE, RSA_OPT_CLASSIFY_PAIR = 25, 26, 27, 28
+RSA_OPT_COUNTER_WORDS16, RSA_OPT_CLASSIFY_PAIR = 26, 28
 
 P = ctypes.c_void_p
 U32 = ctypes.c_uint32

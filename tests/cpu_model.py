@@ -179,17 +179,32 @@ class NumpyBackend(object):
             return self._grouped(recs)
         return self._grouped(self.local.records(1, keep=foreign))
 
+    route_cap = None   # TESTING: rows the first export buffer holds (None: all of them)
+
     def _grouped(self, recs):
         """The model of rsa_export_routed: rows grouped by owner gid % world
-        and the per-owner counts."""
+        and the per-owner counts.  With ``route_cap`` set, the buffer holds
+        only that many rows (the library drops the rows past its buffer and
+        still reports the true counts) and ``again(n)`` exports once more into
+        n rows."""
         from ruleset_analysis_amd.dist import Exported
         world = max(self.world, 1)
         rows = recs.numpy().view(RECORD_DTYPE)
         owner = rows['gid'].astype(np.int64) % world
         order = np.argsort(owner, kind='stable')
-        buf = torch.from_numpy(rows[order].view(np.uint8).reshape(-1).copy())
+        grouped = rows[order]
         counts = torch.from_numpy(np.bincount(owner, minlength=world).astype(np.int64))
-        return Exported(buf, counts, len(rows))
+
+        def export(n):
+            return torch.from_numpy(grouped[:n].view(np.uint8).reshape(-1).copy()), counts, n
+
+        def again(n):
+            self.reexports = getattr(self, 'reexports', 0) + 1
+            return export(n)
+
+        cap = len(rows) if self.route_cap is None else min(self.route_cap, len(rows))
+        buf, _c, _n = export(cap)
+        return Exported(buf, counts, cap, again)
 
     def import_records(self, buf, which):
         for r in buf.numpy().view(RECORD_DTYPE):

@@ -29,17 +29,20 @@ def _worker(rank, world, port, payload, out_q):
     from ruleset_analysis_amd.dist import gather_rows, merge
     n_rules, cap, cols = payload[:3]
     gather = payload[3] if len(payload) > 3 else True
+    route_cap = payload[4] if len(payload) > 4 else None
     n = len(cols[0])
     cut = np.linspace(0, n, world + 1).astype(int)
     shard = tuple(c[cut[rank]:cut[rank + 1]] for c in cols)
     be = NumpyBackend(n_rules, cap, shard)
+    be.route_cap = route_cap
+    stats = {}
     if gather:
-        out = merge(be, dist, world, rank)
+        out = merge(be, dist, world, rank, stats=stats)
     else:   # the owners keep their rows (bench.py's timed job); gathered afterwards
-        part = merge(be, dist, world, rank, gather=False)
+        part = merge(be, dist, world, rank, gather=False, stats=stats)
         out = gather_rows(part, dist, world, rank)
     if rank == 0:
-        out_q.put((out, be.exported_all, be.exported_kept))
+        out_q.put((out, be.exported_all, be.exported_kept, stats, getattr(be, 'reexports', 0)))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -52,15 +55,19 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize('cap,gather', [(15, True), (100000, True), (15, False)])
-def test_merge_world2_matches_oracle(cap, gather):
+@pytest.mark.parametrize('cap,gather,route_cap', [(15, True, None), (100000, True, None), (15, False, None),
+                                                  (15, True, 1), (15, False, 3)])
+def test_merge_world2_matches_oracle(cap, gather, route_cap):
+    """route_cap: every export first lands in a buffer of that many rows, so
+    both exchanges take the re-export path (Exported.again at the exact size,
+    ADVICE r05) and must still give the oracle's result."""
     dbj, info = synth.make_db(51, 300)
     tr = synth.make_traffic((dbj, info), 30000, seed=52, zipf=1.2)
     R = coracle.OracleRules(dbj)
     cols, ts, order = coracle.inputs_from_traffic(R, tr)
     ref = coracle.run(R, cols, ts, order, cap)
     payload = (R.n_rules, cap, (ref['gid'], cols['flags'], cols['pspell'], cols['src'], cols['dst'], cols['sport'],
-                                cols['dport'], ts, order), gather)
+                                cols['dport'], ts, order), gather, route_cap)
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
@@ -82,9 +89,14 @@ def test_merge_world2_matches_oracle(cap, gather):
     for p in procs:
         p.join(timeout=300)
         assert p.exitcode == 0
-    (recs, matches, hits, distinct, thresh), n_all, n_kept = out
+    (recs, matches, hits, distinct, thresh), n_all, n_kept, stats, reexports = out
     # the shard-side filter (export(0) = pass1_kept) engages when rules are capped
     assert (n_kept < n_all) if cap == 15 else (n_kept == n_all)
+    assert stats['route1_sent_rows'] > 0 and stats['route1_self_rows'] == 0
+    assert stats['pass2'] == (cap == 15) and ('route2_sent_rows' in stats) == (cap == 15)
+    if route_cap is not None:
+        # both exchanges overflowed their first buffer and exported again
+        assert reexports == 2 and stats['reexports'] == 2
     assert np.array_equal(matches, ref['matches'])
     assert np.array_equal(hits, ref['hits'])
     assert np.array_equal(thresh != NO, (ref['n_conns'] >= cap) & (cap > 0))

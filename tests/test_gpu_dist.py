@@ -29,7 +29,8 @@ def _worker(rank, world, port, args, out_q):
     from ruleset_analysis_amd.engine import DeviceBatch, Engine
     from ruleset_analysis_amd.pipeline import built_hit_count
     seed, n_rules, n_lines, cap, zipf = args[:5]
-    opts = args[5] if len(args) > 5 else {}
+    opts = dict(args[5]) if len(args) > 5 else {}
+    route_cap = opts.pop('route_cap', None)
     dbj, info = synth.make_db(seed, n_rules)
     tr = synth.make_traffic((dbj, info), n_lines, seed=seed + 1, zipf=zipf)
     compiled = CompiledRules(acldb.load_json(dbj))
@@ -46,7 +47,17 @@ def _worker(rank, world, port, args, out_q):
     local.reset(max(built_hit_count(tup[a:b]), 1), cap)
     g = torch.empty(batch.n, dtype=torch.int32, device=local.device)
     local.pass1(batch, g)
-    out = merge(EngineBackend(local, [batch], [g], cap), dist, world, rank)
+    if route_cap is not None:
+        # every export first lands in a buffer of route_cap rows: the library
+        # drops the rows past it and the exchange exports again at the exact
+        # size (dist.route_records -> Exported.again)
+        orig = local.export_routed
+        local.export_routed = lambda mode, world, capacity=None: orig(mode, world, capacity=capacity or route_cap)
+        local._route_buf, local._route_cap = None, 0
+    stats = {}
+    out = merge(EngineBackend(local, [batch], [g], cap), dist, world, rank, stats=stats)
+    if route_cap is not None:
+        assert stats.get('reexports', 0) >= 1, stats
     if rank == 0:
         out_q.put(out)
     dist.barrier()
@@ -126,6 +137,16 @@ def test_two_ranks_atomic_import():
     _check(out, *_oracle_inputs(61, 700, 120000, 1.2), 12)
 
 
+def test_two_ranks_export_overflow_reexport():
+    """The exports of both exchanges overflow a 1-row first buffer: the
+    library drops the rows past it and reports the true per-owner counts,
+    route_records exports again at the exact size (reallocating the engine's
+    route buffer after the counts were exchanged) -- the result must still be
+    the C oracle's."""
+    out = _run_two_ranks((61, 700, 120000, 12, 1.2, {'route_cap': 1}))
+    _check(out, *_oracle_inputs(61, 700, 120000, 1.2), 12)
+
+
 def test_two_ranks_capped_only_after_merge():
     """Uniform traffic and a cap above every shard's own distinct count but
     below the merged count of some rules: no rank caps a rule locally, so each
@@ -192,3 +213,28 @@ def test_bench_learned_capacity(tmp_path):
     assert line['config']['capacity_reruns'] == 0
     assert line['checks']['ok']
     check_dump_against_oracle(got, 1, rules, lines, cap)
+
+
+def test_bench_two_ranks_share_gpu_checks(tmp_path):
+    """bench.py's N = 2 job (two rank processes on the box's one GPU, gloo):
+    the full-size checks of the distributed job (the merged counters equal the
+    all-reduced gid histograms, uncapped row counts equal the hit+BUILT lines on
+    their owners, gathered rows = owner rows, index = linear scan, a rerun gives
+    identical rows) are green, the gather to rank 0 is timed (gather_ms) and the
+    exchange volume is reported -- and the dumped result equals the C oracle."""
+    from test_bench_spawn import check_dump_against_oracle, run_bench
+    rules, lines, cap = 800, 400000, 40
+    line, got = run_bench(tmp_path, ['--gpus', '2', '--share-gpu', '--backend', 'gloo', '--rules', str(rules),
+                                     '--lines', str(lines), '--cap', str(cap)], timeout=600)
+    assert line['n_gpus'] == 2
+    c = line['checks']
+    assert c['ok'], c
+    for k in ('matches_eq_gid_histogram', 'hits_eq_gid_histogram', 'uncapped_count_sum_eq_hit_built_lines',
+              'gathered_rows_eq_owner_rows', 'index_gids_eq_linear_scan', 'rerun_identical_records',
+              'owner_rows_only_own_rules'):
+        assert c[k] is True, k
+    assert c['uncapped_rules_checked'] > 0
+    assert line['gather']['gather_ms'] > 0 and line['gather']['bytes_to_rank0'] > 0
+    mx = line['merge_exchange']
+    assert mx['route1_sent_bytes_total'] > 0 and mx['route1_sent_bytes_total'] == mx['route1_recv_bytes_total']
+    check_dump_against_oracle(got, 2, rules, lines, cap)

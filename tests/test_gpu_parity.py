@@ -237,14 +237,11 @@ def test_synth_parity_filter_schedule(engine, steps, slice_, growth):
         engine.set_option(native.RSA_OPT_FILTER_GROWTH, 4)
 
 
-@pytest.mark.parametrize('selective', [1, 0])
-def test_recount_after_moved_bounds_repeated_jobs(engine, selective):
+def test_recount_after_moved_bounds_repeated_jobs(engine):
     """Shuffled 5M-line jobs (the last slice finds new connections below some
     rules' bounds, so thresholds move) run three times on one context: the
-    tentative pass-2 fields of the last slice, the per-rule replay of the moved
-    rules (RSA_OPT_RECOUNT_SELECTIVE=1) or the full replay with its backoff (0)
-    must give the oracle's result every time."""
-    from ruleset_analysis_amd import native
+    tentative pass-2 fields of the last slice and the full replay with its
+    backoff must give the oracle's result every time."""
     dbj, info = synth.make_db(29, 900)
     tr = synth.make_traffic((dbj, info), 5_000_000, seed=30, zipf=1.15)
     perm = np.random.default_rng(29).permutation(5_000_000)
@@ -260,16 +257,12 @@ def test_recount_after_moved_bounds_repeated_jobs(engine, selective):
     rows = ref['rows']
     want = sorted(zip(*(rows[k].astype(int).tolist() for k in ('gid', 'pspell', 'for_ip', 'to_ip', 'to_port', 'count',
                                                                   'first', 'last'))))
-    engine.set_option(native.RSA_OPT_RECOUNT_SELECTIVE, selective)
-    try:
-        for _ in range(3):
-            res = engine.run([b], 40, capacity=built_hit_count(tup))
-            assert np.array_equal(res.matches, ref['matches']) and np.array_equal(res.hits, ref['hits'])
-            got = sorted((int(r['gid']), int(r['pspell']), int(r['for_ip']), int(r['to_ip']), int(r['to_port']),
-                          int(r['count']), int(r['first']), int(r['last'])) for r in res.records)
-            assert got == want
-    finally:
-        engine.set_option(native.RSA_OPT_RECOUNT_SELECTIVE, 0)
+    for _ in range(3):
+        res = engine.run([b], 40, capacity=built_hit_count(tup))
+        assert np.array_equal(res.matches, ref['matches']) and np.array_equal(res.hits, ref['hits'])
+        got = sorted((int(r['gid']), int(r['pspell']), int(r['for_ip']), int(r['to_ip']), int(r['to_port']),
+                      int(r['count']), int(r['first']), int(r['last'])) for r in res.records)
+        assert got == want
     assert (ref['n_conns'] >= 40).sum() > 10
 
 

@@ -292,19 +292,19 @@ def test_gpu_parse_golden_equals_host(engine, case):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('seed,mode', [(1, 0), (2, 0), (1, 1), (1, 2), (2, 2)])
-def test_gpu_parse_fuzz_equals_host(engine, seed, mode):
-    """mode: RSA_OPT_PARSE_MODE (0 LDS-staged lines, 1 direct HBM reads,
-    2 register-window reads)."""
+@pytest.mark.parametrize('seed,staged', [(1, 1), (2, 1), (1, 0), (2, 0)])
+def test_gpu_parse_fuzz_equals_host(engine, seed, staged):
+    """staged: RSA_OPT_PARSE_STAGED (1 LDS-staged lines, the form unaligned
+    text takes; 0 register-window reads, the default)."""
     from ruleset_analysis_amd import native
     db, lines = _fuzz_lines(seed, 6000)
     good = [l for l in lines if _host_ok('fw1', l, db)]
     assert len(good) > 4000
-    engine.set_option(native.RSA_OPT_PARSE_MODE, mode)
+    engine.set_option(native.RSA_OPT_PARSE_STAGED, staged)
     try:
         got = _compare(engine, 'fw1', good, db)
     finally:
-        engine.set_option(native.RSA_OPT_PARSE_MODE, 2)
+        engine.set_option(native.RSA_OPT_PARSE_STAGED, 0)
     d = got.disposition
     # the fuzz reaches every outcome, and most lines stay on the device
     for k in (logparse.D_IGNORE, logparse.D_NOACL, logparse.D_MISSING, logparse.D_CLASSIFY):
