@@ -473,6 +473,7 @@ def dist_full_size_checks(eng, batch, gbuf, n_rules, cap, last, step, dist, worl
     cs = torch.tensor([c_own - (1 << 64) if c_own >= 1 << 63 else c_own], dtype=torch.int64, device=dev)
     _all_reduce(cs, dist, None)
     c_sum = int(cs.item()) & 0xFFFFFFFFFFFFFFFF
+    out['gathered_rows_eq_owner_rows'] = True   # (decided on rank 0, which holds the gathered rows)
     if rank == 0:
         c_merged = record_checksum(last['merged'][0])
         out['gathered_rows_eq_owner_rows'] = c_merged == c_sum
@@ -484,7 +485,7 @@ def dist_full_size_checks(eng, batch, gbuf, n_rules, cap, last, step, dist, worl
     # a rerun of the whole distributed job: the identical rows on every owner
     step(False)
     out['rerun_identical_records'] = record_checksum(last['part'].final) == c_own
-    flags_ok = [k for k, v in out.items() if isinstance(v, bool)]
+    flags_ok = sorted(k for k, v in out.items() if isinstance(v, bool))   # the same keys on every rank
     f = torch.tensor([int(out.get(k, True)) for k in flags_ok], dtype=torch.int64, device=dev)
     _all_reduce(f, dist, None, op=dist.ReduceOp.MIN)
     for k, v in zip(flags_ok, f.tolist()):
@@ -671,7 +672,7 @@ def rank_main(args, rank, world, local):
     phase_prof = os.environ.get('RSA_PHASE_PROF') == '1'   # PROFILING: a -DRSA_PHASE_PROF library variant
     if phase_prof:
         import ctypes
-        ph = (ctypes.c_uint64 * 13)()
+        ph = (ctypes.c_uint64 * 17)()
         eng.ctx.call('rsa_phase_prof', ph, ctypes.c_int(1))
     if dist is not None:
         dist.barrier()
@@ -689,7 +690,9 @@ def rank_main(args, rank, world, local):
             {nm: round(v[k] / max(v[8], 1), 1) for k, nm in enumerate(names)}) + ' iterations %d' % v[8])
         log('phase_prof k_reduce<1> cycles/workgroup: ' + json.dumps(
             {nm: round(v[9 + k] / max(v[12], 1), 1) for k, nm in enumerate(('setup', 'insert', 'flush'))}) +
-            ' workgroups %d' % v[12])
+            ' workgroups %d; inside: ' % v[12] + json.dumps(
+                {nm: round(v[13 + k] / max(v[12], 1), 1) for k, nm in enumerate(('record_load_wait', 'lds_insert',
+                                                                                 'flush_claims', 'flush_writes'))}))
     if dist is not None:
         dist.barrier()
     dt = time.perf_counter() - t0

@@ -298,8 +298,11 @@ struct PhaseAcc {
   unsigned long long last, acc[8];
 };
 // [0..7] classifier phases, [8] its wave iterations; [9..11] k_reduce<1>
-// workgroup cycles in setup, record inserts and flushes, [12] its workgroups
-__device__ unsigned long long g_phase[13];
+// workgroup cycles in setup, record inserts and flushes, [12] its workgroups;
+// [13..16] inside them: waiting for the record loads, LDS inserts, the flush
+// up to the claims, the flush's scan and slot writes
+constexpr int kPhaseWords = 17;
+__device__ unsigned long long g_phase[kPhaseWords];
 #define RSA_PH_PARAM , PhaseAcc& ph
 #define RSA_PH_ARG , ph
 #define PH(k)                                                      \
@@ -2320,6 +2323,14 @@ constexpr int kMaxSegs = 16;
                           // (r05o: 2 -> 1 cfg5 9.63 -> 9.45 ms/step, cfg3 within noise; 0: cfg5 10.28)
 #endif
 constexpr int kHotTries = RSA_HOT_TRIES, kHotMin = 8;
+#ifndef RSA_LDS_PAIR
+#define RSA_LDS_PAIR 1   // lds_agg_insert_lane: a probe reads kB and kA together; the creator publishes kB with a store
+#endif
+#ifndef RSA_RED_FILL
+#define RSA_RED_FILL 6   // k_reduce / k_hot_combine: the LDS table is flushed at RSA_RED_FILL / 8 of its entries
+#endif
+template <int kE>
+constexpr uint32_t kRedRoom = (uint32_t)(RSA_RED_FILL * kE) / 8u;
 __device__ __forceinline__ unsigned long long readlane64(unsigned long long v, int l) {
   return ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) |
          __builtin_amdgcn_readlane((uint32_t)v, l);
@@ -2377,7 +2388,16 @@ __device__ __forceinline__ bool lds_agg_insert_lane(unsigned long long (&e_kA)[k
   const uint32_t h = (uint32_t)mix64(kA ^ (kB * 0x9e3779b97f4a7c15ull));
   uint32_t e = (kE & (kE - 1)) == 0 ? (h & (kE - 1)) : __umulhi(h, (uint32_t)kE);
   while (true) {
+#if RSA_LDS_PAIR
+    // kB and kA read with both loads in flight (one LDS round trip): the LDS
+    // executes a wave's operations in issue order (volatile keeps that order),
+    // and a creator stores kA before it publishes kB, so a kA read issued
+    // after a kB read that sees the published key sees its final kA
+    const unsigned long long cur = *reinterpret_cast<volatile unsigned long long*>(&e_kB[e]);
+    const unsigned long long curA = *reinterpret_cast<volatile unsigned long long*>(&e_kA[e]);
+#else
     const unsigned long long cur = __hip_atomic_load(&e_kB[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
     if (cur == kEmpty) {
       if (atomicCAS(&e_kB[e], kEmpty, kBusy) == kEmpty) {
         e_kA[e] = kA;
@@ -2385,14 +2405,22 @@ __device__ __forceinline__ bool lds_agg_insert_lane(unsigned long long (&e_kA)[k
         e_first[e] = first;
         e_last[e] = last;
         e_cnt[e] = cnt;
+#if RSA_LDS_PAIR
+        __hip_atomic_store(&e_kB[e], kB, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         atomicExch(&e_kB[e], kB);
+#endif
         return true;
       }
       continue;
     }
     if (cur == kBusy) continue;
+#if RSA_LDS_PAIR
+    if (cur == kB && curA == kA) {
+#else
     if (cur == kB && __hip_atomic_load(&e_kA[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == kA) {
+#endif
       atomicAdd(&e_cnt[e], cnt);
       atomicMin(&e_first[e], first);
       atomicMax(&e_last[e], last);
@@ -2482,15 +2510,28 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
   // PROFILING BUILD ONLY: wave 0's wall cycles per phase (the phases end at
   // workgroup barriers, so one wave's clock is the workgroup's)
   unsigned long long rp_t = __builtin_amdgcn_s_memtime(), rp_acc[3] = {0ull, 0ull, 0ull};
+  unsigned long long rq_t = rp_t, rq_acc[4] = {0ull, 0ull, 0ull, 0ull};
   rp_acc[0] = rp_t - rp_t0;
 #define RP(k)                                                     \
   do {                                                            \
     const unsigned long long t_ = __builtin_amdgcn_s_memtime();   \
     rp_acc[k] += t_ - rp_t;                                       \
     rp_t = t_;                                                    \
+    rq_t = t_;                                                    \
+  } while (0)
+// sub-phases (the loads are waited for right after they are issued)
+#define RQ(k)                                                     \
+  do {                                                            \
+    if ((k) == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();   \
+    rq_acc[k] += t_ - rq_t;                                       \
+    rq_t = t_;                                                    \
   } while (0)
 #else
 #define RP(k) \
+  do {        \
+  } while (0)
+#define RQ(k) \
   do {        \
   } while (0)
 #endif
@@ -2505,7 +2546,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
     }
     const bool last_round = pos >= end;
     if (!last_round) {
-      const uint32_t room = (3u * kE) / 4 - used;
+      const uint32_t room = kRedRoom<kE> - used;
       const unsigned long long take = end - pos < room ? end - pos : room;
       __syncthreads();   // every thread has read `used` before any insert changes it
       for (unsigned long long jb = 0; jb < take; jb += blockDim.x) {   // workgroup-uniform trip count
@@ -2532,12 +2573,14 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
             first = last = r.ts;
           }
         }
+        RQ(0);
         if (kPass == 2 && !is_hot && have) {   // (hot records of pass 2 were filtered when combined)
           const unsigned long long P = A.thresh[kB >> 32];
           if (P == RSA_NO_THRESHOLD || mo > P) have = false;
         }
         lds_agg_insert<kE, kPass == 1>(e_kA, e_kB, e_mo, e_first, e_last, e_cnt, used, have, kA, kB, mo,
                                                  first, last, cnt);
+        RQ(1);
       }
       pos += take;
       __syncthreads();
@@ -2545,7 +2588,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
       for (uint32_t q = sg + 1; q < n_segs && !more; ++q)
         more = starts[(size_t)q * (n_regions + 1) + region + 1] > starts[(size_t)q * (n_regions + 1) + region];
       RP(1);
-      if (used + 512u <= (3u * kE) / 4 && more) continue;   // workgroup-uniform: room for 512 more
+      if (used + 512u <= kRedRoom<kE> && more) continue;   // workgroup-uniform: room for 512 more
     }
     if (used > 0) {   // workgroup-uniform (read after a barrier)
       // flush: merge every LDS entry into the region; new slots are appended to
@@ -2662,6 +2705,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
           new_slot[q] = ((unsigned long long)gid << 32) | (uint32_t)slot;
         }
       }
+      RQ(2);
       if (kPass == 1) {
         uint32_t total, n_new = 0;
 #pragma unroll
@@ -2701,6 +2745,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
       }
       if (threadIdx.x == 0) used = 0;
       __syncthreads();
+      RQ(3);
       RP(2);
     }
     if (last_round) break;
@@ -2711,9 +2756,11 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
   if (kPass == 1 && threadIdx.x == 0) {
     for (int k = 0; k < 3; ++k) atomicAdd(&g_phase[9 + k], rp_acc[k]);
     atomicAdd(&g_phase[12], 1ull);
+    for (int k = 0; k < 4; ++k) atomicAdd(&g_phase[13 + k], rq_acc[k]);
   }
 #endif
 #undef RP
+#undef RQ
 }
 
 // ---- hot regions (skewed traffic: a few connections on most lines, BASELINE
@@ -2802,7 +2849,7 @@ __global__ __launch_bounds__(1024) void k_hot_combine(const Rec* __restrict__ re
     unsigned long long pos = T.beg;
     while (pos < T.end || used > 0) {   // workgroup-uniform (read after a barrier)
       if (pos < T.end) {
-        const uint32_t room = (3u * kE) / 4 - used;
+        const uint32_t room = kRedRoom<kE> - used;
         const unsigned long long take = T.end - pos < room ? T.end - pos : room;
         __syncthreads();   // every thread has read `used` before any insert changes it
         for (unsigned long long jb = 0; jb < take; jb += blockDim.x) {
@@ -2819,7 +2866,7 @@ __global__ __launch_bounds__(1024) void k_hot_combine(const Rec* __restrict__ re
         }
         pos += take;
         __syncthreads();
-        if (pos < T.end && used + 1024u <= (3u * kE) / 4) continue;   // room for more of this slice
+        if (pos < T.end && used + 1024u <= kRedRoom<kE>) continue;   // room for more of this slice
       }
       // flush: the table's entries to the region's hot area
       constexpr int kPer = kE / 1024;
@@ -5258,14 +5305,14 @@ int rsa_shadowed_ports(rsa_ctx* c, const rsa_shadow_rule* h_rules, uint32_t n, c
 
 #ifdef RSA_PHASE_PROF
 // PROFILING BUILD ONLY: the classifier's phase cycles (see PhaseAcc): out[0..7]
-// summed wave cycles per phase, out[8] wave iterations; out[9..12] k_reduce<1>'s
+// summed wave cycles per phase, out[8] wave iterations; out[9..16] k_reduce<1>'s
 // (g_phase).
 int rsa_phase_prof(rsa_ctx* c, uint64_t* h_out, int reset) {
   if (!c || !h_out) return RSA_ERR_ARG;
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  HIPCHK(c, hipMemcpyFromSymbol(h_out, HIP_SYMBOL(g_phase), 13 * sizeof(uint64_t)));
+  HIPCHK(c, hipMemcpyFromSymbol(h_out, HIP_SYMBOL(g_phase), kPhaseWords * sizeof(uint64_t)));
   if (reset) {
-    const uint64_t z[13] = {};
+    const uint64_t z[kPhaseWords] = {};
     HIPCHK(c, hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof z));
   }
   return RSA_OK;
