@@ -146,17 +146,14 @@ typedef struct rsa_pht_group {   /* 80 B */
   rsa_pht_table table[4];    /* port classes any, dport, sport, sport+dport       */
 } rsa_pht_group;
 
-#define RSA_PHT_NARROW 0x80000000u   /* rsa_pht_mask.bucket_off: 16-bit slots */
+#define RSA_PHT_NARROW 0x80000000u   /* rsa_pht_mask.slot: 16-bit slots */
 typedef struct rsa_pht_mask {    /* 16 B: one pruning table (src tables first: rsa_pht_list.n_src_masks) */
   uint32_t mask;             /* address mask (non-zero)                           */
-  uint32_t bucket_off;       /* image word offset of the buckets | RSA_PHT_NARROW. A table is two-choice
-                                (compile.py prune_buckets): buckets of two slots, a key in one of the
-                                two buckets its hash picks, no two keys of a bucket with one tag.
-                                RSA_PHT_NARROW: uint16 slots tag8 << 8 | value, one word per bucket,
-                                values 1..255; else uint32 slots tag16 << 16 | value, two words per
-                                bucket (even offset); 0 = empty; value = bitmap index */
-  uint32_t n_buckets;        /* 1 .. 65536                                        */
-  uint32_t reserved;         /* 0                                                 */
+  uint32_t slot;             /* slot_off | RSA_PHT_NARROW: uint16 slots (H & 0xFF) << 8 | value,
+                                slot_off in uint16 units, values 1..255; else uint32
+                                slots (H & 0xFFFF) << 16 | value; 0 = empty (value 0) */
+  uint32_t disp_off;         /* first displacement, uint16 units                  */
+  uint32_t size;             /* n_slots | disp_mask << 17; slot value = bitmap index */
 } rsa_pht_mask;
 
 typedef struct rsa_pht_list {    /* 80 B: one list (or one chained chunk of a list) */

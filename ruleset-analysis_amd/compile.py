@@ -390,8 +390,7 @@ PHT_EMPTY = 0xFFFFFFFF
 PHT_NONE = 0xFFFF
 PHT_MAX_IDX = 0xFFFE
 PHT_MAX_SLOTS = 0x10000              # slot index * n_slots must fit the 24-bit multiplier
-MASK_NARROW = 0x80000000            # pruning record word 1: 16-bit slots (two per 32-bit bucket)
-PRUNE_LOAD = 0.85                   # pruning tables: keys per slot of the two-choice bucket tables
+MASK_NARROW = 0x80000000            # pruning record word 1: 16-bit slots (offset in uint16 units)
 HDR_ALL_NARROW = 0x2                # image word 5: every pruning table has 16-bit slots
 SALT_S, SALT_D, SALT_P = 0x9E3779B9, 0x7F4A7C15, 0x2545F491
 
@@ -431,72 +430,6 @@ def pht_slot(H, d, n_slots):
     step = ((H >> np.uint64(16)) | np.uint64(1)) & np.uint64(0xFFFF)
     x = (H + np.asarray(d, np.uint64) * step) & np.uint64(0xFFFF)
     return ((x * np.uint64(n_slots)) >> np.uint64(16)).astype(np.int64)
-
-
-def prune_buckets(H, nb, narrow):
-    """(b1, b2, tag) of pruning-key hashes H for a two-choice table of nb <=
-    65536 buckets (csrc: prune_side): each half of H picks a bucket by
-    multiply-shift (24-bit operands), the tag (8 bits for 16-bit slots, else
-    16) is the low part of the xor of both halves."""
-    H = np.asarray(H, np.uint32).astype(np.int64)
-    b1 = ((H & 0xFFFF) * nb) >> 16
-    b2 = ((H >> 16) * nb) >> 16
-    tag = ((H >> 16) ^ H) & (0xFF if narrow else 0xFFFF)
-    return b1, b2, tag
-
-
-def _prune_cuckoo(H, narrow, load=PRUNE_LOAD, kicks=500, seed=11):
-    """Two-choice bucketised cuckoo placement of distinct hashes H: buckets of
-    two slots, a key in one of its two candidate buckets, and no two keys of
-    one bucket sharing a tag (so a probe's tag match in a bucket is the key's
-    own slot when the key is in that bucket).  Returns (nb, slot per key)."""
-    n = len(H)
-    nb = max(1, int(np.ceil(n / (2 * load))))
-    rng = np.random.default_rng(seed)
-    while True:
-        if nb > 0x10000:
-            raise OverflowError('pruning table of %d keys does not fit 65536 buckets' % n)
-        b1, b2, tag = (x.tolist() for x in prune_buckets(H, nb, narrow))
-        slot = [-1] * (2 * nb)
-        where = [-1] * n
-        ok = True
-
-        def fits(k, b):
-            """A free slot of bucket b for key k (none if the bucket holds its tag)."""
-            o0, o1 = slot[2 * b], slot[2 * b + 1]
-            if (o0 >= 0 and tag[o0] == tag[k]) or (o1 >= 0 and tag[o1] == tag[k]):
-                return -1
-            return 2 * b if o0 < 0 else (2 * b + 1 if o1 < 0 else -1)
-
-        for k in range(n):
-            cur = k
-            for _kick in range(kicks):
-                s_ = fits(cur, b1[cur])
-                if s_ < 0:
-                    s_ = fits(cur, b2[cur])
-                if s_ >= 0:
-                    slot[s_] = cur
-                    where[cur] = s_
-                    cur = -1
-                    break
-                # evict: a slot of one of cur's buckets whose neighbour does not
-                # carry cur's tag takes cur, its key moves on
-                cand = [q for b in {b1[cur], b2[cur]} for q in (2 * b, 2 * b + 1)
-                        if slot[q ^ 1] < 0 or tag[slot[q ^ 1]] != tag[cur]]
-                if not cand:
-                    break
-                q = cand[int(rng.integers(len(cand)))]
-                victim = slot[q]
-                slot[q] = cur
-                where[cur] = q
-                where[victim] = -1
-                cur = victim
-            if cur >= 0:
-                ok = False
-                break
-        if ok and all(w >= 0 for w in where):
-            return nb, np.array(where, np.int64)
-        nb = nb + nb // 8 + 1
 
 
 def _prefix_mask(lo, span):
@@ -597,20 +530,31 @@ class _Image(object):
         soff, _ = self.alloc(slots)
         return (soff, 2 * doff, nslots, dmask)
 
-    def table_prune2(self, H, vals, narrow):
-        """Pruning table of distinct hashes H -> bitmap indices vals (>= 1):
-        two-choice buckets of two slots (_prune_cuckoo).  narrow: 16-bit slots
-        tag8 << 8 | value8, one 32-bit word per bucket; else 32-bit slots
-        tag16 << 16 | value16, two words per bucket.  0 = empty.  Returns
-        (bucket word offset, n_buckets)."""
-        nb, where = _prune_cuckoo(H, narrow)
-        _b1, _b2, tag = prune_buckets(H, nb, narrow)
-        sh = 8 if narrow else 16
-        words = (tag.astype(np.uint32) << np.uint32(sh)) | np.asarray(vals, np.uint32)
-        slots = np.zeros(2 * nb, dtype=np.uint16 if narrow else np.uint32)
-        slots[where] = words
-        off, _ = self.alloc(slots.view(np.uint32), align=1 if narrow else 2)
-        return off, nb
+    def table16(self, H, vals):
+        """Pruning CHD table with 16-bit slots (8-bit tag << 8 | 8-bit value,
+        values 1..255; 0 = empty, which reads as value 0 = the empty bitmap);
+        offsets in uint16 units of the image."""
+        nslots, dmask, disp, slot_of = _chd(H)
+        dwords = np.zeros(((dmask + 2) // 2) * 2, dtype=np.uint16)
+        dwords[:dmask + 1] = disp
+        doff, _ = self.alloc(dwords.view(np.uint32))
+        slots = np.zeros(nslots + (nslots & 1), dtype=np.uint16)
+        slots[slot_of] = ((H.astype(np.uint32) & np.uint32(0xFF)) << np.uint32(8)).astype(np.uint16) | \
+            np.asarray(vals, np.uint16)
+        soff, _ = self.alloc(slots.view(np.uint32))
+        return (2 * soff, 2 * doff, nslots, dmask)
+
+    def table_prune(self, H, vals):
+        """Pruning CHD table with 32-bit slots (16-bit tag << 16 | value, 0 =
+        empty = value 0, the empty bitmap)."""
+        nslots, dmask, disp, slot_of = _chd(H)
+        dwords = np.zeros(((dmask + 2) // 2) * 2, dtype=np.uint16)
+        dwords[:dmask + 1] = disp
+        doff, _ = self.alloc(dwords.view(np.uint32))
+        slots = np.zeros(nslots, dtype=np.uint32)
+        slots[slot_of] = ((H.astype(np.uint32) & np.uint32(0xFFFF)) << np.uint32(16)) | np.asarray(vals, np.uint32)
+        soff, _ = self.alloc(slots)
+        return (soff, 2 * doff, nslots, dmask)
 
     def build(self):
         return np.concatenate(self.chunks)
@@ -732,11 +676,11 @@ def _index_record(img, rec, e, pre, min_entries, max_groups):
             H = np.array(list(merged.keys()), dtype=np.uint32)
             vals = np.array([bm_index[b] for b in merged.values()], dtype=np.uint32)
             r = mrec[PHT_MASK_WORDS * q: PHT_MASK_WORDS * (q + 1)]
-            boff, nb = img.table_prune2(H, vals, narrow)
+            soff, doff, nslots, dmask = img.table16(H, vals) if narrow else img.table_prune(H, vals)
             r[0] = m
-            r[1] = boff | (MASK_NARROW if narrow else 0)
-            r[2] = nb
-            r[3] = 0
+            r[1] = soff | (MASK_NARROW if narrow else 0)
+            r[2] = doff
+            r[3] = nslots | (dmask << 17)
         rec[0:4] = (goff, len(groups), moff, len(tables))
         rec[18] = sum(1 for _m, side, _mg in tables if side == 0)   # src tables come first
         rec[7] = bm_off
@@ -821,26 +765,19 @@ def _probe(image, H, t):
     return (w & 0xFFFF) if (w >> 16) == (H & 0xFFFF) else PHT_NONE
 
 
-def _prune_probe(image, H, boff, nb, narrow):
-    """One pruning-table probe (csrc: prune_side): per candidate bucket the
-    value of its first slot whose tag matches (0, the empty bitmap, if none);
-    the caller ORs both buckets' bitmaps."""
-    b1, b2, tag = (int(x) for x in prune_buckets(np.uint32(H), nb, narrow))
-    sh, vm = (8, 0xFF) if narrow else (16, 0xFFFF)
-    out = []
-    for b in (b1, b2):
-        if narrow:
-            w = int(image[boff + b])
-            sl = (w & 0xFFFF, w >> 16)
-        else:
-            sl = (int(image[boff + 2 * b]), int(image[boff + 2 * b + 1]))
-        v = 0
-        for x in sl:
-            if (x >> sh) == tag and (x & vm):
-                v = x & vm
-                break
-        out.append(v)
-    return out
+def _prune_probe(image, H, t, narrow):
+    """One pruning-table probe (csrc: prune_side): the bitmap index of the
+    slot, 0 (the empty bitmap) on an empty slot or a tag mismatch."""
+    slot_off, disp_off, n_slots, disp_mask = (int(v) for v in t)
+    H = int(H)
+    h16 = image.view(np.uint16)
+    d = int(h16[disp_off + ((H >> 16) & disp_mask)])
+    slot = int(pht_slot(H, d, n_slots))
+    if narrow:
+        w = int(h16[slot_off + slot])
+        return (w & 0xFF) if (w >> 8) == (H & 0xFF) else 0
+    w = int(image[slot_off + slot])
+    return (w & 0xFFFF) if (w >> 16) == (H & 0xFFFF) else 0
 
 
 def _match(x, src, dst, ports):
@@ -886,10 +823,9 @@ def pht_lookup(index, ent, off, L, src, dst, ports):
                 mr = [int(v) for v in image[moff + PHT_MASK_WORDS * q: moff + PHT_MASK_WORDS * (q + 1)]]
                 side = 0 if q < n_src else 1
                 key = (dst if side else src) & mr[0]
-                bits = 0
-                for v in _prune_probe(image, field_hash(key, side), mr[1] & ~MASK_NARROW, mr[2],
-                                      bool(mr[1] & MASK_NARROW)):
-                    bits |= int(image[r[7] + 2 * v]) | (int(image[r[7] + 2 * v + 1]) << 32)
+                t = (mr[1] & ~MASK_NARROW, mr[2], mr[3] & 0x1FFFF, mr[3] >> 17)
+                v = _prune_probe(image, field_hash(key, side), t, bool(mr[1] & MASK_NARROW))
+                bits = int(image[r[7] + 2 * v]) | (int(image[r[7] + 2 * v + 1]) << 32)
                 if side:
                     D |= bits
                 else:

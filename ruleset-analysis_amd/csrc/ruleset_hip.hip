@@ -331,62 +331,52 @@ constexpr uint32_t kListWords = 20, kGroupWords = 20, kMaskWords = 4;
 // Pruning stage of the index lookup for ONE lane (compile.py pht_lookup): each
 // src/dst mask table maps the masked address to a bitmap of the groups holding
 // a rule on that prefix; the candidate groups are those in both the src and
-// the dst bitmap.  A pruning table is two-choice: buckets of two slots, each
-// key in one of the buckets its hash H picks (b1 from H's low half, b2 from its
-// high half, compile.py prune_buckets), and no bucket holds two keys with the
-// same tag.  A slot holds tag << 8 | value (16-bit slots, one 32-bit word per
-// bucket) or tag << 16 | value (32-bit slots, two words per bucket); value
-// indexes the record's uint64 bitmaps, where bitmap 0 is empty.  A probe reads
-// BOTH buckets at once (no displacement level), takes in each the value of its
-// first slot whose tag matches (0 if none) and ORs both bitmaps: a key in the
-// table finds its own value in its bucket, anything else only adds groups.
+// the dst bitmap.  A pruning slot holds tag << 8 | value (16-bit slots, tag =
+// H & 0xFF) or tag << 16 | value (32-bit, tag = H & 0xFFFF); value indexes
+// the record's uint64 bitmaps, where bitmap 0 is empty: an empty slot (0) or
+// a tag mismatch reads bitmap 0, so every probe ORs a bitmap in, branch-free.
 // The src tables come first (n_src_masks), then the dst tables: each side is
 // its own loop with its address and salt fixed, kU masks per iteration phase
 // by phase (all reads of a phase in flight before the first is waited for; a
 // short last batch repeats its last mask: OR is idempotent).  kNarrow: every
 // table of the image has 16-bit slots (image word 5 bit 1, wave-uniform), so
 // the slot width is not decided per table.
-__device__ __forceinline__ uint32_t prune_pick(uint32_t s0, uint32_t s1, uint32_t tag, uint32_t sh) {
-  const uint32_t vm = (1u << sh) - 1u;
-  const uint32_t v0 = (s0 >> sh) == tag ? (s0 & vm) : 0u;
-  const uint32_t v1 = (s1 >> sh) == tag ? (s1 & vm) : 0u;
-  return v0 ? v0 : v1;
-}
-
 template <bool kNarrow, int kPruneU, typename P32>
 __device__ __forceinline__ unsigned long long prune_side(P32 img, uint32_t moff, uint32_t k0, uint32_t k1, uint32_t key,
                                                          uint32_t salt, uint32_t bm_off) {
   unsigned long long acc = 0ull;
   for (uint32_t k = k0; k < k1; k += kPruneU) {
     v4u m[kPruneU];
-    uint32_t H[kPruneU];
-    v2u w[kPruneU];   // narrow: bucket b1's word, bucket b2's word; wide: the matched values (after the picks)
+    uint32_t H[kPruneU], w[kPruneU];
 #pragma unroll
     for (int u = 0; u < kPruneU; ++u) m[u] = rd4(img, moff + kMaskWords * min(k + u, k1 - 1));
 #pragma unroll
     for (int u = 0; u < kPruneU; ++u) {
       H[u] = fmix32((key & m[u].x) ^ salt);
-      const uint32_t b1 = umul24(H[u] & 0xFFFFu, m[u].z) >> 16, b2 = umul24(H[u] >> 16, m[u].z) >> 16;
-      const uint32_t boff = m[u].y & 0x7FFFFFFFu;
-      if (kNarrow || (m[u].y >> 31)) {
-        w[u].x = img[boff + b1];
-        w[u].y = img[boff + b2];
-      } else {   // 32-bit slots: both buckets' slot pairs, picked at once
-        const uint32_t tag = ((H[u] >> 16) ^ H[u]) & 0xFFFFu;
-        const v2u p1 = rd2(img, boff + 2 * b1), p2 = rd2(img, boff + 2 * b2);
-        w[u].x = prune_pick(p1.x, p1.y, tag, 16u);
-        w[u].y = prune_pick(p2.x, p2.y, tag, 16u);
+      w[u] = rd16(img, m[u].z + ((H[u] >> 16) & (m[u].w >> 17)));   // displacement
+    }
+#pragma unroll
+    for (int u = 0; u < kPruneU; ++u) {
+      const uint32_t hidx = (m[u].y & 0x7FFFFFFFu) + pht_slot(H[u], w[u], m[u].w & 0x1FFFFu);
+      if (kNarrow) {
+        w[u] = rd16(img, hidx);
+      } else {
+        const uint32_t narrow = m[u].y >> 31;
+        const uint32_t w32 = img[hidx >> narrow];
+        w[u] = narrow ? (w32 >> ((hidx & 1u) << 4)) & 0xFFFFu : w32;
       }
     }
 #pragma unroll
     for (int u = 0; u < kPruneU; ++u) {
-      if (kNarrow || (m[u].y >> 31)) {
-        const uint32_t tag = ((H[u] >> 16) ^ H[u]) & 0xFFu;
-        w[u].x = prune_pick(w[u].x & 0xFFFFu, w[u].x >> 16, tag, 8u);
-        w[u].y = prune_pick(w[u].y & 0xFFFFu, w[u].y >> 16, tag, 8u);
+      uint32_t v;
+      if (kNarrow) {
+        v = (w[u] >> 8) == (H[u] & 0xFFu) ? (w[u] & 0xFFu) : 0u;
+      } else {
+        const uint32_t sh = (m[u].y >> 31) ? 8u : 16u, fm = (1u << sh) - 1u;
+        v = (w[u] >> sh) == (H[u] & fm) ? (w[u] & fm) : 0u;
       }
-      const v2u b1 = rd2(img, bm_off + 2 * w[u].x), b2 = rd2(img, bm_off + 2 * w[u].y);   // bm_off is even
-      acc |= ((unsigned long long)(b1.y | b2.y) << 32) | (b1.x | b2.x);
+      const v2u bb = rd2(img, bm_off + 2 * v);   // bm_off is even (compile.py: alloc align=2)
+      acc |= ((unsigned long long)bb.y << 32) | bb.x;
     }
   }
   return acc;
@@ -2333,14 +2323,10 @@ constexpr int kMaxSegs = 16;
                           // (r05o: 2 -> 1 cfg5 9.63 -> 9.45 ms/step, cfg3 within noise; 0: cfg5 10.28)
 #endif
 constexpr int kHotTries = RSA_HOT_TRIES, kHotMin = 8;
-#ifndef RSA_LDS_PAIR
-#define RSA_LDS_PAIR 1   // lds_agg_insert_lane: a probe reads kB and kA together; the creator publishes kB with a store
-#endif
-#ifndef RSA_RED_FILL
-#define RSA_RED_FILL 6   // k_reduce / k_hot_combine: the LDS table is flushed at RSA_RED_FILL / 8 of its entries
-#endif
+// k_reduce / k_hot_combine flush the LDS table at 3/4 of its entries (5/8
+// and 7/8 measured slower: profiles/r06/ab_kreduce.txt)
 template <int kE>
-constexpr uint32_t kRedRoom = (uint32_t)(RSA_RED_FILL * kE) / 8u;
+constexpr uint32_t kRedRoom = (uint32_t)(3 * kE) / 4u;
 __device__ __forceinline__ unsigned long long readlane64(unsigned long long v, int l) {
   return ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) |
          __builtin_amdgcn_readlane((uint32_t)v, l);
@@ -2398,16 +2384,13 @@ __device__ __forceinline__ bool lds_agg_insert_lane(unsigned long long (&e_kA)[k
   const uint32_t h = (uint32_t)mix64(kA ^ (kB * 0x9e3779b97f4a7c15ull));
   uint32_t e = (kE & (kE - 1)) == 0 ? (h & (kE - 1)) : __umulhi(h, (uint32_t)kE);
   while (true) {
-#if RSA_LDS_PAIR
     // kB and kA read with both loads in flight (one LDS round trip): the LDS
     // executes a wave's operations in issue order (volatile keeps that order),
     // and a creator stores kA before it publishes kB, so a kA read issued
     // after a kB read that sees the published key sees its final kA
+    // (profiles/r06/ab_kreduce.txt: aggregation 3.29 -> 3.26 ms/step at cfg3)
     const unsigned long long cur = *reinterpret_cast<volatile unsigned long long*>(&e_kB[e]);
     const unsigned long long curA = *reinterpret_cast<volatile unsigned long long*>(&e_kA[e]);
-#else
-    const unsigned long long cur = __hip_atomic_load(&e_kB[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
     if (cur == kEmpty) {
       if (atomicCAS(&e_kB[e], kEmpty, kBusy) == kEmpty) {
         e_kA[e] = kA;
@@ -2415,22 +2398,13 @@ __device__ __forceinline__ bool lds_agg_insert_lane(unsigned long long (&e_kA)[k
         e_first[e] = first;
         e_last[e] = last;
         e_cnt[e] = cnt;
-#if RSA_LDS_PAIR
         __hip_atomic_store(&e_kB[e], kB, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-#else
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        atomicExch(&e_kB[e], kB);
-#endif
         return true;
       }
       continue;
     }
     if (cur == kBusy) continue;
-#if RSA_LDS_PAIR
     if (cur == kB && curA == kA) {
-#else
-    if (cur == kB && __hip_atomic_load(&e_kA[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == kA) {
-#endif
       atomicAdd(&e_cnt[e], cnt);
       atomicMin(&e_first[e], first);
       atomicMax(&e_last[e], last);
@@ -4726,8 +4700,21 @@ int rsa_load_rules(rsa_ctx* c, const rsa_rule_entry* h_entries, uint32_t n_entri
 
 namespace {
 
-// A CHD table (a group's port-class table) inside the image whose slot
-// values are all < `limit`; `empty`: the empty slot word.
+// A 16-bit-slot pruning table inside the image whose slot values are all <
+// `limit` (the record's bitmap count; an empty slot is 0, bitmap 0).
+bool table16_ok(const uint32_t* img, uint32_t words, const rsa_pht_table& t, uint32_t limit) {
+  if (t.n_slots == 0 || t.n_slots > 0x10000u || (uint64_t)t.slot_off + t.n_slots > 2ull * words || (t.disp_mask & (t.disp_mask + 1)) != 0 ||
+      (uint64_t)t.disp_off + t.disp_mask + 1 > 2ull * words || limit == 0 || limit > 0x100u)
+    return false;
+  const uint16_t* h = reinterpret_cast<const uint16_t*>(img);
+  for (uint32_t q = 0; q < t.n_slots; ++q)
+    if ((h[t.slot_off + q] & 0xFFu) >= limit) return false;
+  return true;
+}
+
+// A CHD table inside the image whose slot values are all < `limit`; `empty`:
+// the empty slot word (0xFFFFFFFF in the group tables, 0 in the pruning
+// tables, whose value 0 is a valid index: bitmap 0).
 bool table_ok(const uint32_t* img, uint32_t words, const rsa_pht_table& t, uint32_t limit,
               uint32_t empty = 0xFFFFFFFFu) {
   if (t.n_slots == 0 || t.n_slots > 0x10000u || (uint64_t)t.slot_off + t.n_slots > words || (t.disp_mask & (t.disp_mask + 1)) != 0 ||
@@ -4830,20 +4817,12 @@ int rsa_load_index(rsa_ctx* c, const uint32_t* img, uint32_t words, const rsa_ru
         for (uint32_t m = 0; m < h.n_masks; ++m) {
           rsa_pht_mask M;
           memcpy(&M, img + h.mask_off + (size_t)mw * m, sizeof M);
-          const bool narrow = (M.bucket_off & RSA_PHT_NARROW) != 0;
-          const uint32_t boff = M.bucket_off & ~RSA_PHT_NARROW;
-          if (!narrow && (img[5] & 2u))
+          const rsa_pht_table T = {M.slot & ~RSA_PHT_NARROW, M.disp_off, M.size & 0x1FFFFu, M.size >> 17};
+          if (!(M.slot & RSA_PHT_NARROW) && (img[5] & 2u))
             return fail(c, RSA_ERR_ARG, "list %u mask %u: 32-bit slots in an image flagged all-narrow", l, m);
-          const uint64_t bw = narrow ? 1u : 2u;   // words per bucket
-          if (M.n_buckets == 0 || M.n_buckets > 0x10000u || (!narrow && boff % 2) ||
-              (uint64_t)boff + bw * M.n_buckets > words)
-            return fail(c, RSA_ERR_ARG, "list %u mask %u: pruning buckets outside the image", l, m);
-          for (uint64_t q = 0; q < bw * M.n_buckets; ++q) {
-            const uint32_t x = img[boff + q];
-            const uint32_t v0 = narrow ? x & 0xFFu : x & 0xFFFFu, v1 = narrow ? (x >> 16) & 0xFFu : 0u;
-            if (v0 >= h.n_bitmaps || v1 >= h.n_bitmaps)
-              return fail(c, RSA_ERR_ARG, "list %u mask %u: pruning value past the bitmaps", l, m);
-          }
+          if ((M.slot & RSA_PHT_NARROW) ? !table16_ok(img, words, T, h.n_bitmaps)
+                                        : !table_ok(img, words, T, h.n_bitmaps, 0u))
+            return fail(c, RSA_ERR_ARG, "list %u mask %u: table outside the image or bitmap out of range", l, m);
         }
       }
       at = h.entry_beg + h.entry_len;
