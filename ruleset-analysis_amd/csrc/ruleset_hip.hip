@@ -2122,9 +2122,7 @@ __global__ __launch_bounds__(1024) void k_part_hist(const uint16_t* __restrict__
   for (uint32_t r = threadIdx.x; r < n_regions; r += blockDim.x) hist[(size_t)r * n_tiles + tile] = hcount[r];
 }
 
-#ifndef RSA_SCATTER_PF
-#define RSA_SCATTER_PF 1   // k_part_scatter: the next trip's loads issued before this trip's stores
-#endif
+
 
 // A window group's counts with one 16-B load (wcnt is padded by kPartW words
 // and w0 is a multiple of kPartW): no per-window branches.
@@ -2154,7 +2152,6 @@ __global__ __launch_bounds__(1024) void k_part_scatter(const Rec* __restrict__ r
   const uint32_t lane = __lane_id(), nwv = blockDim.x >> 6;
   const unsigned long long wstep = (unsigned long long)nwv * kPartW;
   unsigned long long w0 = beg / kWin + (threadIdx.x >> 6) * kPartW;
-#if RSA_SCATTER_PF
   // software pipeline over the wave's trips (a trip = two records per lane of
   // one window group; a group holds <= 256 records, so <= 2 trips): the
   // window counts are read a group ahead and the records a trip ahead, both
@@ -2215,33 +2212,6 @@ __global__ __launch_bounds__(1024) void k_part_scatter(const Rec* __restrict__ r
     c1 = c2;
     qb = nqb;
   }
-#else
-  WinGroup g = w0 < wend ? win_group(wcnt, w0, wend) : WinGroup{0, 0, 0, 0};
-  for (; w0 < wend; w0 += wstep) {
-    // the next group's window counts are read before this group's records
-    // are moved (their latency hides behind the moves), and every lane moves
-    // two records per trip, both loads in flight together
-    const WinGroup gn = w0 + wstep < wend ? win_group(wcnt, w0 + wstep, wend) : WinGroup{0, 0, 0, 0};
-    for (uint32_t q = lane; q < g.tot; q += 2 * kWin) {
-      const bool two = q + kWin < g.tot;
-      const unsigned long long j0 = win_slot(g, w0, q);
-      const unsigned long long j1 = two ? win_slot(g, w0, q + kWin) : j0;
-      const uint32_t rg0 = regs[j0];
-      const Rec r0 = recs[j0];
-      uint32_t rg1 = 0;
-      Rec r1;
-      if (two) {
-        rg1 = regs[j1];
-        r1 = recs[j1];
-      }
-      const uint32_t p0 = atomicAdd(&cur[rg0], 1u);
-      const uint32_t p1 = two ? atomicAdd(&cur[rg1], 1u) : 0u;
-      out[p0] = r0;
-      if (two) out[p1] = r1;
-    }
-    g = gn;
-  }
-#endif
 }
 
 // Exclusive scan of n uint32 (three launches: per-block scan + block sums,
