@@ -321,12 +321,6 @@ __device__ unsigned long long g_phase[kPhaseWords];
 
 constexpr int kAttempts = 4;   // compile.py PHT_ATTEMPTS
 constexpr uint32_t kListWords = 20, kGroupWords = 20, kMaskWords = 4;
-#ifndef RSA_CAP_FULLSCAN
-#define RSA_CAP_FULLSCAN 0   // A/B builds: cap resolution gathers every capped entry's key from its slot
-#endif
-#ifndef RSA_PREFETCH_T
-#define RSA_PREFETCH_T -1   // k_classify prefetch (kPf): -1 auto per variant; A/B builds: 0 none, 1 next tuple, 2 + order/ts
-#endif
 
 // Pruning stage of the index lookup for ONE lane (compile.py pht_lookup): each
 // src/dst mask table maps the masked address to a bitmap of the groups holding
@@ -666,9 +660,6 @@ __device__ __forceinline__ uint32_t bucket_lookup_serial(const Rules& R, P32 img
   return best;
 }
 
-#ifndef RSA_BKT_PHASED
-#define RSA_BKT_PHASED 1
-#endif
 constexpr int kBktMaxTables = 8;   // bucketindex.py MAX_TABLES
 
 
@@ -686,17 +677,9 @@ constexpr int kBktMaxTables = 8;   // bucketindex.py MAX_TABLES
 // dependent chain, so that variant reads what it needs of a record or table
 // descriptor together, up front (kGlb); the LDS image re-reads words where
 // they are used (registers are its limit: 64 VGPRs at 8 waves per SIMD).
-// A/B switches (profiles/r05/ab_summary.txt, r05n; cfg4 ms per k_classify
-// launch): the first hit table's min_gid / entry_base kept from its probe
-// 0.912 -> 0.905 (default on); the list record's words read up front as well
-// costs the emission's order/timestamp prefetch its registers: 0.968 (1) and
-// 0.985 (2) with the prefetch off, 1.105 (2) with it on and VGPRs spilled.
-#ifndef RSA_GLB_REC
-#define RSA_GLB_REC 0    // global image: the list record's words read once, up front (2: also the residual range and continuation)
-#endif
-#ifndef RSA_GLB_DESC
-#define RSA_GLB_DESC 1   // global image: the first hit table's min_gid / entry_base kept from its probe
-#endif
+// The first hit table's min_gid / entry_base are kept from the descriptor read
+// of its probe (cfg4 0.912 -> 0.905 ms per k_classify launch,
+// profiles/r05/ab_summary.txt r05n).
 template <typename P32>
 constexpr bool kGlobalImg = false;
 template <>
@@ -707,10 +690,7 @@ constexpr bool kGlobalImg<const uint32_t*> = true;
 template <typename P32>
 __device__ __forceinline__ uint32_t bucket_lookup(const Rules& R, P32 img, uint32_t lw, uint32_t toff, uint32_t nt,
                                                   uint32_t src, uint32_t dst, uint32_t ports, uint32_t best) {
-#if !RSA_BKT_PHASED
-  return bucket_lookup_serial(R, img, lw, src, dst, ports, best);
-#else
-  constexpr bool kGlb = kGlobalImg<P32> && RSA_GLB_DESC;
+  constexpr bool kGlb = kGlobalImg<P32>;
   uint32_t h0 = 0u, h1 = 0u, h2 = 0u, h3 = 0u;   // hit slot words, in table order
   uint32_t tj = 0u;                              // their tables, 4 bits each (hit k at bits 4k)
   uint32_t nh = 0u;
@@ -832,7 +812,6 @@ __device__ __forceinline__ uint32_t bucket_lookup(const Rules& R, P32 img, uint3
     }
   }
   return best;
-#endif
 }
 
 // First-match classification of one wave of tuples.  Linear scans (the whole
@@ -864,26 +843,13 @@ __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Ru
     return active ? best : kNoGid;
   }
   // list record fields (include/ruleset_hip.h rsa_pht_list) are read from the
-  // image where they are used: lw = the lane's current record.  The global
-  // image's words are read together, once per record (kGlb: rc0 = words 0-1,
-  // rc1 = 4-5, rc4 = 16-17, the prefix length and after_min at once; records
-  // are 4-word aligned)
-  constexpr bool kGlb = kGlobalImg<P32> && RSA_GLB_REC;
+  // image where they are used: lw = the lane's current record.  (Reading the
+  // global image's record words once, up front, costs the emission's
+  // order/timestamp prefetch its registers: cfg4 0.905 -> 0.968-1.105 ms per
+  // launch, profiles/r05/ab_summary.txt r05n.)
   uint32_t lw = R.list_off + kListWords * (active ? list : 0u);
-  v2u rc0 = {0u, 0u}, rc1 = rc0, rc4 = rc0;
-  uint32_t rc_pre = 0u, rc_min = 0u;
-  constexpr bool kGlb2 = kGlb && RSA_GLB_REC >= 2;   // the residual range and continuation too
-  if (kGlb) {
-    rc0 = rd2(img, lw);
-    rc_pre = img[lw + 6];
-    rc_min = img[lw + 15];
-  }
-  if (kGlb2) {
-    rc1 = rd2(img, lw + 4);
-    rc4 = rd2(img, lw + 16);
-  }
   // 1. prefix scans
-  const uint32_t pre_n = active ? (kGlb ? rc_pre : img[lw + 6]) : 0u;
+  const uint32_t pre_n = active ? img[lw + 6] : 0u;
   PH(0);
   unsigned long long pending = __ballot(active && pre_n != 0);
   while (pending) {
@@ -899,11 +865,11 @@ __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Ru
   // 2. per record of the lane's chain: the index (per lane), then the residual
   // scan (waterfall over the records present); the next chunk only while the
   // lane's best exceeds its smallest gid
-  bool go = active && best > (kGlb ? rc_min : img[lw + 15]);
+  bool go = active && best > img[lw + 15];
   bool deferred = false;
   PH(1);
   while (__ballot(go)) {
-    const bool ix = go && (kGlb ? rc0.y : img[lw + 1]) != 0;
+    const bool ix = go && img[lw + 1] != 0;
     uint32_t c = kNoGid;
     if (kMode == 2) {
       // partial-key bucket index: exact, never deferred
@@ -911,7 +877,7 @@ __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Ru
         if (R.force_defer) {
           c = kDefer;
         } else {
-          c = bucket_lookup(R, img, lw, kGlb ? rc0.x : img[lw], kGlb ? rc0.y : img[lw + 1], t.x, t.y, t.z, best);
+          c = bucket_lookup(R, img, lw, img[lw], img[lw + 1], t.x, t.y, t.z, best);
         }
       }
     } else if (kMode == 1) {
@@ -927,7 +893,7 @@ __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Ru
         best = min(best, c);
       }
     }
-    const uint32_t rb = go ? (kGlb2 ? rc1.x : img[lw + 4]) : 0u, re = go ? (kGlb2 ? rc1.y : img[lw + 5]) : 0u;
+    const uint32_t rb = go ? img[lw + 4] : 0u, re = go ? img[lw + 5] : 0u;
     const bool want = go && rb < re;
     pending = __ballot(want);
     while (pending) {
@@ -940,14 +906,9 @@ __device__ __forceinline__ uint32_t classify_wave(uint4 t, bool active, const Ru
       if (mine) best = b;
     }
     if (go) {
-      const uint32_t next = kGlb2 ? rc4.x : img[lw + 16];
-      go = next != RSA_PHT_NONE && best > (kGlb2 ? rc4.y : img[lw + 17]);
+      const uint32_t next = img[lw + 16];
+      go = next != RSA_PHT_NONE && best > img[lw + 17];
       if (go) lw = R.list_off + kListWords * next;
-      if (kGlb && go) rc0 = rd2(img, lw);   // the continuation record's words
-      if (kGlb2 && go) {
-        rc1 = rd2(img, lw + 4);
-        rc4 = rd2(img, lw + 16);
-      }
     }
     PH(6);
   }
@@ -1362,15 +1323,11 @@ __device__ __forceinline__ T* global_ptr(unsigned long long a) {
   return (T*)(gT*)a;
 }
 
-#ifndef RSA_EMIT_KERNARG
-#define RSA_EMIT_KERNARG 1
-#endif
 
 // The emission's Agg fields and Emit pointers, loaded from the kernarg segment
 // at this point of the loop (the empty asm makes the pointer opaque per
 // iteration, so the loads are not hoisted into long-lived SGPRs).
 __device__ __forceinline__ void classify_emit_args(const EmitPack& ep_arg, Agg& A, Emit& E) {
-#if RSA_EMIT_KERNARG
   typedef __attribute__((address_space(4))) const EmitPack cEmitPack;
   cEmitPack* ep = (cEmitPack*)__builtin_amdgcn_kernarg_segment_ptr();
   asm volatile("" : "+s"(ep));
@@ -1386,9 +1343,6 @@ __device__ __forceinline__ void classify_emit_args(const EmitPack& ep_arg, Agg& 
   p.cap = ep->cap;
   p.skip = ep->skip;
   p.np_bits = ep->np_bits;
-#else
-  const EmitPack& p = ep_arg;
-#endif
   E.gh = global_ptr<uint32_t>(p.gh);
   E.gh16 = p.gh16 ? global_ptr<uint16_t>(p.gh16) : nullptr;
   E.ts = global_ptr<const uint32_t>(p.ts);
@@ -1403,7 +1357,7 @@ __device__ __forceinline__ void classify_emit_args(const EmitPack& ep_arg, Agg& 
 }
 
 // The record of one line, or false (need).  kPre: the line's order and
-// timestamp were loaded ahead (o_pre, ts_pre; RSA_PREFETCH_T 2).
+// timestamp were loaded ahead (o_pre, ts_pre; kPf 2).
 // kPreF: the rule's filter bound was loaded ahead too (f_pre; k_classify_pair
 // loads both lines' bounds before either line's stores)
 template <bool kPre = false, bool kPreF = false>
@@ -1497,14 +1451,14 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kImg > kIm
   PhaseAcc ph = {};
   unsigned long long waves_seen = 0;
 #endif
-  // Prefetch (kPf, RSA_PREFETCH_T): 1 = the next iteration's tuple, 2 = also
+  // Prefetch (kPf): 1 = the next iteration's tuple, 2 = also
   // its order and timestamp (the emission loads), loaded before this
   // iteration's stores, so waiting for them does not wait for the stores
   // (vmcnt counts stores too).  Default: 2 for the global-image variants and
   // the bucket index (52-53 VGPRs, room at 8 waves/SIMD), 0 for the LDS-image
   // pht variants (at the 64-VGPR budget prefetching spills: 0.77 -> 1.03 /
   // 1.17 ms per cfg3 launch, profiles/r04ai_*).
-  constexpr int kPf = RSA_PREFETCH_T >= 0 ? RSA_PREFETCH_T : ((kImg == 0 || kMode == 2) ? 2 : 0);
+  constexpr int kPf = (kImg == 0 || kMode == 2) ? 2 : 0;
   const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
   uint4 t_next = make_uint4(0u, 0u, 0u, 0u);
   unsigned long long o_next = 0ull;
@@ -2308,9 +2262,6 @@ __device__ __forceinline__ unsigned long long readlane64(unsigned long long v, i
 // region, so lanes sharing the key of one of the wave's first live lanes are
 // combined with wave reductions and enter the table as ONE insert (LDS atomics
 // on one address serialise over the lanes).  Wave-uniform call.
-#ifndef RSA_USED_WAVE
-#define RSA_USED_WAVE 1   // k_reduce / k_hot_combine: one LDS add of the wave's new entries
-#endif
 // Returns true for the lane that created a new table entry (the caller counts
 // them into `used` with one LDS atomic per wave: a per-lane add on that one
 // word serialises over the wave's new keys).
@@ -2393,12 +2344,8 @@ __device__ __forceinline__ void lds_agg_insert(unsigned long long (&e_kA)[kE], u
                                                unsigned long long mo, uint32_t first, uint32_t last, uint32_t cnt) {
   const bool fresh = lds_agg_insert_lane<kE, kMinOrder>(e_kA, e_kB, e_mo, e_first, e_last, e_cnt, have, kA, kB, mo,
                                                         first, last, cnt);
-#if RSA_USED_WAVE
   const unsigned long long fm = __ballot(fresh);
   if (fm && (int)__lane_id() == __builtin_ctzll(fm)) atomicAdd(&used, (uint32_t)__popcll(fm));
-#else
-  if (fresh) atomicAdd(&used, 1u);
-#endif
 }
 
 // A hot region's pre-combined records (k_hot_combine): one per key and
@@ -3937,14 +3884,8 @@ int cap_select(rsa_ctx* c, unsigned long long* out, uint32_t* h_n_capped) {
   // (16 B per used entry, coalesced) unless an entry was claimed by the CAS
   // import; only keys at or below the rule's earlier selection (the job's last
   // filter slice) are scattered and selected over
-#if RSA_CAP_FULLSCAN   // A/B build switch: slot gathers, every key of a capped rule
-  const unsigned long long* ukey = nullptr;
-  const unsigned long long* prev = out;
-  HIPCHK(c, hipMemsetAsync(out, 0xFF, nr * sizeof(unsigned long long), c->stream));
-#else
   const unsigned long long* ukey = c->ukey_ok ? c->d_ukey : nullptr;
   const unsigned long long* prev = c->d_filter;
-#endif
   k_cap_mark<<<(nr + kBlock - 1) / kBlock, kBlock, 0, c->stream>>>(c->d_distinct, nr, c->cap, prev, c->d_cidx,
                                                                    c->d_capped_gid, c->d_capped_start,
                                                                    c->d_capped_cnt, c->d_capped_prev, d_ncap,
@@ -4028,9 +3969,6 @@ int ensure_events(rsa_ctx* c) {
 constexpr int kImgSmall = kImgSmallMax;   // 76 KiB: two 1024-thread workgroups per CU (32 waves)
 constexpr int kImgLarge = 38912;   // 152 KiB: one workgroup per CU
 
-#ifndef RSA_FORCE_LARGE
-#define RSA_FORCE_LARGE 0   // A/B builds: every indexed launch takes the one-workgroup-per-CU image variant
-#endif
 template <bool kEmit, int kMode, bool kNarrow>
 void launch_classify_img(rsa_ctx* c, const uint4* t, uint64_t m, int32_t* go, const Rules& r, const Agg& ag,
                          const Emit& e) {
@@ -4052,7 +3990,7 @@ void launch_classify_img(rsa_ctx* c, const uint4* t, uint64_t m, int32_t* go, co
     const unsigned long long lanes = (m + 1) / 2;
     k_classify_pair<kEmit><<<grid_for_threads(c, lanes, kPairThreads, 4 * RSA_PAIR_WAVES / (kPairThreads / 64)),
                              kPairThreads, 0, c->stream>>>(ep, t, m, go, r, c->d_flags, c->d_tail, c->d_tail_n);
-  } else if (c->indexed && c->img_words <= (uint32_t)kImgSmall && !RSA_FORCE_LARGE) {
+  } else if (c->indexed && c->img_words <= (uint32_t)kImgSmall) {
     k_classify<kImgSmall, kEmit, kMode, kNarrow><<<grid_for_threads(c, m, 1024, 2), 1024, 0, c->stream>>>(
         ep, t, m, go, r, c->d_flags, c->d_tail, c->d_tail_n);
   } else if (c->indexed && c->img_words <= (uint32_t)kImgLarge) {

@@ -679,25 +679,15 @@ constexpr uint32_t pack3(char a, char b, char c) { return (uint32_t)(uint8_t)a <
 // combined with integer ops and bit selects (v_bfi): booleans would live in
 // scalar lane masks, and their and/or/select bookkeeping is scalar work that
 // the CU's one scalar unit serialises over its four SIMDs.
-#ifndef RSA_TPL_PREFETCH
-#define RSA_TPL_PREFETCH 0   // A/B builds: 1 carries the next descriptors in registers
-#endif
-// With RSA_TPL_PREFETCH, d0 = prog[seg], d1 = prog[seg + 1]: the next
-// descriptor is a select, and the read of the one after it is issued a byte
-// ahead of its use, so no LDS read sits on the byte-to-byte dependence chain.
-// Measured slower on gfx950 (16M-line text job: parse 6.41 vs 6.08 ms,
-// profiles/r04w_text16_*.json): the two extra live registers and the LDS read
-// per byte cost more than the latency they hide, so the default reads
-// prog[seg] on every byte.
+// The descriptor prog[seg] is read on every byte: carrying the next ones in
+// registers (no LDS read on the byte-to-byte chain) measured slower on gfx950
+// (16M-line text job: parse 6.41 vs 6.08 ms, profiles/r04w_text16_*.json).
 struct State {
-  uint32_t seg = 0, cnt = 0, pos0 = 0, ok = 1, d0 = 0, d1 = 0;
+  uint32_t seg = 0, cnt = 0, pos0 = 0, ok = 1;
 };
 template <class P>
-RSA_HD State start(P prog) {
-  State st;
-  st.d0 = prog[0];
-  st.d1 = prog[1];
-  return st;
+RSA_HD State start(P) {
+  return State{};
 }
 RSA_HD uint32_t lt01(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a - b) >> 63); }   // a < b
 RSA_HD uint32_t nz01(uint32_t a) { return a ? 1u : 0u; }
@@ -707,7 +697,7 @@ RSA_HD uint32_t sel(uint32_t m01, uint32_t a, uint32_t b) {   // m01 ? a : b, as
 }
 template <class P, class C, class Q>
 RSA_HD void step(State& st, uint32_t i, uint32_t c, uint32_t act, P prog, C cls, Q slot) {
-  const uint32_t desc = RSA_TPL_PREFETCH ? st.d0 : prog[st.seg];
+  const uint32_t desc = prog[st.seg];
   const uint32_t lit = desc & 0xFFu, msk = (desc >> 8) & 0xFFu, mn = (desc >> 16) & 7u, mx = (desc >> 19) & 0xFFu,
                  fld = desc >> 27;
   const uint32_t is_run = nz01(msk);
@@ -723,11 +713,6 @@ RSA_HD void step(State& st, uint32_t i, uint32_t c, uint32_t act, P prog, C cls,
   st.seg += adv;
   st.ok = sel(act, nok, st.ok);
   st.cnt = sel(act, (cnt + 1) & (0u - cont), cnt);
-  if (RSA_TPL_PREFETCH) {
-    st.d0 = sel(adv, st.d1, st.d0);
-    const uint32_t n1 = st.seg + 1;
-    st.d1 = prog[n1 < kProgLen ? n1 : kProgLen - 1];   // used a byte from now
-  }
 }
 
 // The scan of a whole line.  True: the line has the template form.  All
