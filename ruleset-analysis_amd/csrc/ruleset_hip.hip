@@ -2620,20 +2620,15 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
           if (!is_new[q]) continue;
           const uint32_t e = threadIdx.x + q * blockDim.x;
           const unsigned long long ui = sh_base + off + k++;
-          Slot ns;
-          ns.kA = e_kA[e];
-          ns.kB = e_kB[e];
-          ns.min_order = e_mo[e];
-          ns.first = e_first[e];
-          ns.last = e_last[e];
-          ns.count = e_cnt[e];
-          const bool t2 = A.tent2 && A.filter[(uint32_t)(ns.kB >> 32)] != RSA_NO_THRESHOLD;
-          ns.count2 = t2 ? e_cnt[e] : 0u;
-          ns.first2 = t2 ? e_first[e] : 0xFFFFFFFFu;
-          ns.last2 = t2 ? e_last[e] : 0u;
-          ns.pad[0] = (uint32_t)ui;
-          ns.pad[1] = ns.pad[2] = ns.pad[3] = 0;
-          A.slots[(uint32_t)new_slot[q]] = ns;
+          // the whole 64-B slot as four 16-B stores (Slot layout)
+          const unsigned long long kA = e_kA[e], kB = e_kB[e], mo = e_mo[e];
+          const uint32_t fi = e_first[e], la = e_last[e], cn = e_cnt[e];
+          const bool t2 = A.tent2 && A.filter[(uint32_t)(kB >> 32)] != RSA_NO_THRESHOLD;
+          v4u* sw = reinterpret_cast<v4u*>(&A.slots[(uint32_t)new_slot[q]]);
+          sw[0] = v4u{(uint32_t)kA, (uint32_t)(kA >> 32), (uint32_t)kB, (uint32_t)(kB >> 32)};
+          sw[1] = v4u{(uint32_t)mo, (uint32_t)(mo >> 32), fi, la};
+          sw[2] = v4u{cn, t2 ? cn : 0u, t2 ? fi : 0xFFFFFFFFu, t2 ? la : 0u};
+          sw[3] = v4u{(uint32_t)ui, 0u, 0u, 0u};
           A.used[ui] = new_slot[q];
           A.ukey[ui] = e_mo[e];
           e_kB[e] = kEmpty;
