@@ -201,17 +201,21 @@ def _hadoop_partition(key, n):
     return (h & 0x7FFFFFFF) % n
 
 
-def reference_pipeline_baseline(n_lines=1_000_000, rules=200, seed=1, procs=None, reducers=4):
+def reference_pipeline_baseline(n_lines=1_000_000, rules=200, seed=1, procs=None, reducers=4, broad=True,
+                                single=True):
     """SURVEY.md §8d CPU baseline, BASELINE config 1: a 200-rule ACL and 1M
     synthetic ASA log lines through the reference's job restated in Python
     (oracle.cli: mapper.py / connlist-reducer.py as Unix filters), run as real
     processes on this host:
 
-    (1) ``mapper | LC_ALL=C sort | reducer`` (SURVEY.md §3.1, one process each);
+    (1) ``mapper | LC_ALL=C sort | reducer`` (SURVEY.md §3.1, one process each;
+        skipped with single=False);
     (2) Hadoop-like: ``procs`` mappers over contiguous splits, map output
         partitioned by Hadoop's key hash into ``reducers`` parts
         (runAnalysis.sh:12,44), ``LC_ALL=C sort --parallel``, one reducer per part.
-    """
+
+    ``rules``/``seed``/``broad`` pick the synth.make_db workload (the bench's
+    own configuration for the same-workload baseline)."""
     import shutil
     import subprocess
     import tempfile
@@ -219,7 +223,7 @@ def reference_pipeline_baseline(n_lines=1_000_000, rules=200, seed=1, procs=None
     # GPU gets 16 of the host's CPUs (OMP_NUM_THREADS=16 there), although
     # os.cpu_count() shows the whole machine
     procs = procs or int(os.environ.get('OMP_NUM_THREADS') or len(os.sched_getaffinity(0)) or 1)
-    dbj, info = synth.make_db(seed, rules)
+    dbj, info = synth.make_db(seed, rules, broad=broad)
     tr = synth.make_traffic((dbj, info), n_lines, seed=seed + 100)
     text = ''.join(l + '\n' for l in synth.render_lines(tr))
     work = tempfile.mkdtemp(prefix='rsa_cpu_baseline_')
@@ -231,10 +235,12 @@ def reference_pipeline_baseline(n_lines=1_000_000, rules=200, seed=1, procs=None
         env = dict(os.environ, LC_ALL='C', mapred_input_dir='/logs/fw1/part-00000', PYTHONPATH=ROOT,
                    OMP_NUM_THREADS='1')
         py = sys.executable
-        t = time.perf_counter()
-        subprocess.run('%s -m oracle.cli map db.json < log.txt | LC_ALL=C sort | %s -m oracle.cli reduce db.json 1000 '
-                       '> report.txt' % (py, py), shell=True, cwd=work, env=env, check=True)
-        t_single = time.perf_counter() - t
+        t_single = None
+        if single:
+            t = time.perf_counter()
+            subprocess.run('%s -m oracle.cli map db.json < log.txt | LC_ALL=C sort | %s -m oracle.cli reduce db.json '
+                           '1000 > report.txt' % (py, py), shell=True, cwd=work, env=env, check=True)
+            t_single = time.perf_counter() - t
         # Hadoop-like job
         lines = text.splitlines(True)
         cuts = np.linspace(0, len(lines), procs + 1).astype(int)
@@ -265,19 +271,22 @@ def reference_pipeline_baseline(n_lines=1_000_000, rules=200, seed=1, procs=None
                 raise RuntimeError('reducer failed')
         t_hadoop = time.perf_counter() - t
         hits = lambda txt: sum(int(l.split(': ')[1]) for l in txt.splitlines() if l.startswith('Total number of hits'))
-        with open(os.path.join(work, 'report.txt'), encoding='latin-1') as f:
-            h1 = hits(f.read())
         h2 = 0
         for r in range(reducers):
             with open(os.path.join(work, 'red%d.txt' % r), encoding='latin-1') as f:
                 h2 += hits(f.read())
-        if h1 != h2:
-            raise RuntimeError('the partitioned job disagrees with the single pipeline (%d vs %d hits)' % (h1, h2))
+        h1 = h2
+        if single:
+            with open(os.path.join(work, 'report.txt'), encoding='latin-1') as f:
+                h1 = hits(f.read())
+            if h1 != h2:
+                raise RuntimeError('the partitioned job disagrees with the single pipeline (%d vs %d hits)' % (h1, h2))
     finally:
         shutil.rmtree(work, ignore_errors=True)
-    return {'config': 'BASELINE config 1: %d-rule ACL, %d synthetic ASA lines, seed %d' % (rules, n_lines, seed),
-            'single': {'value': n_lines / t_single, 'unit': 'lines/s', 'wall_s': t_single, 'cores': 1,
-                       'kind': 'port', 'pipeline': 'oracle.cli map | LC_ALL=C sort | oracle.cli reduce'},
+    return {'config': '%d-rule ACL, %d synthetic ASA lines, seed %d' % (rules, n_lines, seed),
+            'single': None if t_single is None else {
+                'value': n_lines / t_single, 'unit': 'lines/s', 'wall_s': t_single, 'cores': 1, 'kind': 'port',
+                'pipeline': 'oracle.cli map | LC_ALL=C sort | oracle.cli reduce'},
             'hadoop_like': {'value': n_lines / t_hadoop, 'unit': 'lines/s', 'wall_s': t_hadoop, 'cores': procs,
                             'kind': 'port', 'pipeline': '%d mappers, Hadoop HashPartitioner to %d parts, '
                                                         'sort --parallel, %d reducers' % (procs, reducers, reducers)},
@@ -797,6 +806,25 @@ def rank_main(args, rank, world, local):
             res['merge_exchange'] = merge_exchange
         if world == 1 and not args.no_cpu_baseline:
             res['cpu_baseline'] = cpu_baseline(wl)
+            spec = CONFIGS[args.config]
+            if wl.kind == 'asa' and not spec.get('zipf') and len(spec['ifcs']) == 1 and args.baseline_same_lines:
+                # the same workload through the restated reference JOB on the
+                # host's cores, Hadoop-like (mappers over splits, key-hash
+                # partition to 4 reducers, sort): the headline CPU baseline,
+                # the single-core sample beside it
+                t = time.perf_counter()
+                par = reference_pipeline_baseline(n_lines=args.baseline_same_lines, rules=wl.rules, seed=wl.seed,
+                                                  broad=spec['broad'], single=False,
+                                                  procs=args.baseline_procs or None)
+                hl = par['hadoop_like']
+                one = res['cpu_baseline']
+                res['cpu_baseline'] = {
+                    'value': hl['value'], 'unit': 'lines/s', 'cores': hl['cores'], 'kind': 'port',
+                    'host_cpus': os.cpu_count(),
+                    'sample': '%d lines of the same %d-rule workload (synth seed %d, %s) through the restated '
+                              'reference job as real processes: %s; wall %.1f s' % (
+                                  args.baseline_same_lines, wl.rules, wl.seed, wl.data, hl['pipeline'], hl['wall_s']),
+                    'single_core': one, 'measure_s': time.perf_counter() - t}
             if not args.no_config1:
                 # SURVEY.md 8d's config-1 job (BASELINE config 1: 1M lines, 200
                 # rules; the single pipeline and the Hadoop-like variant), run
@@ -1051,6 +1079,9 @@ def parse_args(argv=None):
                     help='run only the SURVEY.md 8d CPU baseline (config 1 through the restated reference job)')
     ap.add_argument('--baseline-lines', type=int, default=1_000_000)
     ap.add_argument('--baseline-procs', type=int, default=0)
+    ap.add_argument('--baseline-same-lines', type=int, default=160_000,
+                    help='lines of the headline CPU baseline (the bench workload through the Hadoop-like restated '
+                         'reference job on the host cores; 0 = only the single-core sample)')
     ap.add_argument('--filter-slice', type=int, default=0, help='override RSA_OPT_FILTER_SLICE')
     ap.add_argument('--opt', action='append', default=[], help='NAME=VALUE library option (e.g. FILTER_STEPS=3)')
     ap.add_argument('--no-index', action='store_true', help='classify with the plain linear scan')
