@@ -660,7 +660,7 @@ def rank_main(args, rank, world, local):
         # the checks and --dump after the timed steps (gather_rows)
         mstats = {}
         part = merge(EngineBackend(eng, [batch], [gbuf], cap), dist, world, rank, to_host=False, gather=False,
-                     stats=mstats)
+                     stats=mstats, impl=args.merge_impl, force_exchange=world == 1 and args.merge_impl == 'lib')
         last['part'], last['merge_stats'] = part, mstats
         return part.final.numel() // RECORD_DTYPE.itemsize
 
@@ -779,6 +779,9 @@ def rank_main(args, rank, world, local):
                        'rules': compiled.n_rules, 'entries': len(ent), 'lines_per_gpu': lines, 'cap': cap,
                        'parallelism': 'dp%d' % world, 'index': 'none' if args.no_index else getattr(eng, 'index_kind', args.index),
                        'backend': args.backend if dist is not None else 'none', 'records': n_rec,
+                       'merge': ('rsa_merge_rccl' if args.backend == 'nccl' else 'rsa_merge (host-buffer transport)')
+                                if dist is not None and args.merge_impl == 'lib' else
+                                ('dist.merge (Python protocol)' if dist is not None else 'none'),
                        'table_capacity': sizing['capacity'], 'capacity_bound': bound,
                        'capacity_reruns': sizing['reruns'],
                        'cold_job_ms': cold_ms,
@@ -1066,7 +1069,11 @@ def parse_args(argv=None):
     ap.add_argument('--rules', type=int, default=0, help='override the expanded rule count')
     ap.add_argument('--cap', type=int, default=None, help='override the per-rule connection cap')
     ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'])
-    ap.add_argument('--force-dist', action='store_true', help='run the distributed merge even with one rank')
+    ap.add_argument('--force-dist', action='store_true',
+                    help='run the distributed merge even with one rank (every collective runs: '
+                         'RSA_MERGE_ALWAYS_EXCHANGE)')
+    ap.add_argument('--merge-impl', default='lib', choices=['lib', 'python'],
+                    help='the merge inside the library (rsa_merge, default) or the Python protocol of dist.py')
     ap.add_argument('--cpu-model', action='store_true', help='TESTING: CPU model instead of the HIP library')
     ap.add_argument('--dump', default='', help='TESTING: rank 0 writes the final result (npz) here')
     ap.add_argument('--no-check', action='store_true', help='skip the untimed full-size checks')

@@ -180,6 +180,7 @@ typedef struct rsa_pht_list {    /* 80 B: one list (or one chained chunk of a li
 #define RSA_OPT_FILTER_GROWTH 24 /* auto filter: lines of each bound refinement's slice over the previous ones (default 4) */
 #define RSA_OPT_CLASSIFY_PAIR 28 /* the global-memory bucket index (lists too large for LDS) classifies two lines per lane (1, default) or one (0) */
 #define RSA_OPT_COUNTER_WORDS16 26 /* 16-bit gid|hit words between classification and counting when every gid fits 15 bits and the LDS histogram holds the rules (1, default) */
+#define RSA_OPT_ROUTE_ROWS 29 /* TESTING: rsa_merge starts every routed export in a buffer of this many rows (0, default: the rows the last merge needed) -- forces the re-export path */
 #define RSA_OPT_FORCE_DEFER 8  /* TESTING: every index candidate goes to the exact deferred-line path        */
 #define RSA_OPT_PROFILE_SKIP 3 /* PROFILING ONLY, results invalid: bit0 skips counters, bit1 skips the table, bit2 skips table updates */
 #define RSA_OPT_PRECHECK 9     /* pre-check monotone slot fields with a plain load before their atomics (default 1)       */
@@ -327,6 +328,103 @@ int rsa_export(rsa_ctx *ctx, int which, rsa_conn_record *d_out, uint64_t max_rec
 int rsa_export_routed(rsa_ctx *ctx, int which, uint32_t world, rsa_conn_record *d_out, uint64_t max_records,
                       uint64_t *d_counts);
 int rsa_import(rsa_ctx *ctx, int which, const rsa_conn_record *d_in, uint64_t n);
+
+/* The whole multi-GPU merge behind one call (the reference's
+ * keyed shuffle into NUM_REDUCERS reducers and `hadoop dfs -getmerge`,
+ * runAnalysis.sh:12,42-56, README.md:35-38).  Every rank has run pass 1 over
+ * its own shard on its own ctx (rsa_reset, rsa_classify / rsa_aggregate_gids);
+ * rank r owns the rules with gid % world == r.  rsa_merge then runs, on every
+ * rank together:
+ *   1. SUM all_reduce of the line and hit counters;
+ *   2. this shard's cap resolution, and the routed export (rsa_export_routed,
+ *      which=2) of the entries other ranks own that can still reach the
+ *      report; an all_to_allv of the per-owner counts (with an overflow flag)
+ *      and ONE host read of send and receive sizes, then an all_to_allv of the
+ *      40-B rows; the owners import them (which=0) and resolve their caps;
+ *   3. MAX all_reduce of the owners' thresholds (-1 = none) with the import
+ *      overflow need: every rank holds every rule's P in d_thresh;
+ *   4. if any rule is capped: the pass-2 recount over h_batches, a routed
+ *      export (which=1), the exchange, the owners' import (which=1);
+ *   5. rsa_emit of the owned rules' final rows into a ctx buffer, and a SUM
+ *      all_reduce of the owned distinct counts (d_distinct) with every rank's
+ *      row count;
+ *   6. flags & RSA_MERGE_GATHER: the owners' rows to rank 0 (rsa_gather).
+ * Afterwards d_matches/d_hits/d_thresh/d_distinct hold the merged counters on
+ * every rank.  A distinct-connection table overflow on any rank (pass 1 or the
+ * import) returns RSA_ERR_CAPACITY on EVERY rank, with h_info->needed = the
+ * entries the fullest table must hold (0 if unknown): rerun the job with
+ * rsa_reset at that capacity.  At world 1 no collective runs (the merge is the
+ * single-GPU job: resolve, recount if capped, emit) unless flags has
+ * RSA_MERGE_ALWAYS_EXCHANGE: then every step runs over the transport anyway
+ * (self exchanges; a one-GPU check of a transport, results unchanged).
+ *
+ * The collectives go through a transport: rsa_merge_rccl binds an RCCL
+ * communicator (the path over xGMI); any other collective library (MPI, a
+ * host-side TCP group) fills rsa_transport itself.  host_buffers != 0: the
+ * callbacks receive pinned HOST buffers (the library stages device data
+ * through them) -- a CPU-only collective; else device pointers on `stream`
+ * (the ctx stream).  Callbacks return 0 on success. */
+typedef struct rsa_transport {
+  void *self;
+  int32_t world, rank;
+  int32_t host_buffers;
+  /* in place over n int64: op 0 = sum, 1 = max */
+  int (*all_reduce_i64)(void *self, int64_t *buf, uint64_t n, int op, void *stream);
+  /* rows to every rank: h_send_bytes[r] bytes, the r-th consecutive segment of
+   * send, go to rank r; the h_recv_bytes[r] bytes from rank r land at recv +
+   * sum(h_recv_bytes[0..r)).  h_*_bytes are host arrays of world entries. */
+  int (*all_to_allv)(void *self, const void *send, const uint64_t *h_send_bytes, void *recv,
+                     const uint64_t *h_recv_bytes, void *stream);
+} rsa_transport;
+
+typedef struct rsa_shard_batch {   /* one pass-1 batch of this rank's shard (for the pass-2 recount) */
+  const rsa_tuple *d_tuples;
+  const uint32_t *d_ts;
+  const uint64_t *d_order;
+  const int32_t *d_gid;            /* pass 1's d_gid_out, or NULL to re-classify */
+  uint64_t n;
+} rsa_shard_batch;
+
+#define RSA_MERGE_GATHER 1
+#define RSA_MERGE_ALWAYS_EXCHANGE 2
+
+typedef struct rsa_merge_info {
+  const rsa_conn_record *d_rows;   /* after the gather: on rank 0 every owner's rows in rank order (NULL
+                                      elsewhere); else this rank's own rules' rows.  A ctx buffer, valid
+                                      until the ctx's next merge or destroy (rsa_merge_rows copies it) */
+  uint64_t n_rows;
+  uint64_t owner_rows;             /* this rank's own rules' final rows */
+  uint64_t gather_rows;            /* rows the gather moves to rank 0 from the other ranks */
+  uint64_t route1_sent, route1_self, route1_recv;   /* pass-1 exchange rows (self: kept at home) */
+  uint64_t route2_sent, route2_self, route2_recv;   /* pass-2 exchange rows */
+  uint64_t allreduce_bytes;        /* payload of the counter, threshold and size all_reduces */
+  uint64_t needed;                 /* RSA_ERR_CAPACITY: entries the fullest table must hold (0: unknown) */
+  uint32_t reexports;              /* exports repeated because the route buffer was too small */
+  uint32_t pass2;                  /* 1 if some rule was capped (the recount ran) */
+} rsa_merge_info;
+
+int rsa_merge(rsa_ctx *ctx, const rsa_transport *t, const rsa_shard_batch *h_batches, uint32_t n_batches,
+              int flags, rsa_merge_info *h_info);
+/* The owners' rows of the last rsa_merge to rank 0 (every rank calls it; the
+ * sizes are known from the merge, no extra collective): h_info->d_rows /
+ * n_rows become rank 0's gathered rows (NULL / 0 elsewhere). */
+int rsa_gather(rsa_ctx *ctx, const rsa_transport *t, rsa_merge_info *h_info);
+/* Copy rows of the last merge into d_out (device, max_records rows): which 0 =
+ * this rank's own rules' rows, 1 = the last gather's rows (rank 0).  *h_n
+ * receives the count; RSA_ERR_CAPACITY if it exceeds max_records. */
+int rsa_merge_rows(rsa_ctx *ctx, int which, rsa_conn_record *d_out, uint64_t max_records, uint64_t *h_n);
+
+/* RCCL (over xGMI) as the transport.  The library resolves RCCL at run time
+ * (the librccl already loaded in the process, else librccl.so.1).  Rank 0
+ * makes a unique id, the caller broadcasts its 128 bytes by any means, every
+ * rank creates its communicator on the ctx's device; one communicator serves
+ * any number of merges. */
+int rsa_rccl_unique_id(uint8_t h_id[128]);
+int rsa_rccl_comm_create(rsa_ctx *ctx, int32_t world, int32_t rank, const uint8_t h_id[128], void **comm);
+int rsa_rccl_comm_destroy(void *comm);
+int rsa_merge_rccl(rsa_ctx *ctx, void *comm, const rsa_shard_batch *h_batches, uint32_t n_batches, int flags,
+                   rsa_merge_info *h_info);
+int rsa_gather_rccl(rsa_ctx *ctx, void *comm, rsa_merge_info *h_info);
 
 /* Profiling counters (collected while RSA_OPT_STATS is on): h_out[0] lines
  * combined into the table, [1] probes beyond a line's home slot, [2] probes that

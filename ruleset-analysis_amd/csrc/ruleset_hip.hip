@@ -3591,6 +3591,8 @@ struct rsa_ctx {
   unsigned long long* d_hits = nullptr;
   unsigned int* d_distinct = nullptr;
   unsigned long long* d_thresh = nullptr;
+  void* merge_state = nullptr;   // merge.hip (rsa_merge's buffers)
+  uint64_t route_rows = 0;       // RSA_OPT_ROUTE_ROWS (testing)
   // library-owned table
   Slot* d_slots = nullptr;
   unsigned long long slot_cap = 0;    // power of two in use
@@ -4447,6 +4449,7 @@ int rsa_ctx_destroy(rsa_ctx* c) {
                   c->d_cnt_tasks, c->d_cnt_ctl, c->d_flags, c->d_cursor, c->d_job_recs, c->d_cidx,
                   c->d_capped_gid, c->d_capped_cnt, c->d_capped_start, c->d_capped_prev, c->d_keys, c->d_chk};
   for (void* b : bufs) (void)hipFree(b);
+  if (c->merge_state) rsa_internal_merge_free(c->merge_state);
   for (int k = 0; k < kMaxEvents; ++k)
     if (c->ev[k]) (void)hipEventDestroy(c->ev[k]);
   delete c;
@@ -4513,6 +4516,10 @@ int rsa_set_option(rsa_ctx* c, int option, int64_t value) {
     case RSA_OPT_CLASSIFY_PAIR:
       c->classify_pair = value != 0;
       return RSA_OK;
+    case RSA_OPT_ROUTE_ROWS:
+      if (value < 0) return fail(c, RSA_ERR_ARG, "RSA_OPT_ROUTE_ROWS must be >= 0");
+      c->route_rows = (uint64_t)value;
+      return RSA_OK;
     case RSA_OPT_REGION_RECORDS:
       if (value < 0 || value > 0xFFFFFFFFll) return fail(c, RSA_ERR_ARG, "RSA_OPT_REGION_RECORDS must be 0..2^32-1");
       c->region_records = (uint32_t)value;
@@ -4558,6 +4565,17 @@ int rsa_set_option(rsa_ctx* c, int option, int64_t value) {
 hipStream_t rsa_internal_stream(rsa_ctx* c) { return c->stream; }
 int rsa_internal_fail(rsa_ctx* c, int code, const char* msg) { return fail(c, code, "%s", msg); }
 int rsa_internal_parse_staged(rsa_ctx* c) { return c->parse_staged ? 1 : 0; }
+int rsa_internal_device(rsa_ctx* c) { return c->device; }
+void rsa_internal_counters(rsa_ctx* c, unsigned long long** m, unsigned long long** h, unsigned int** d,
+                           unsigned long long** t, uint32_t* n_rules) {
+  *m = c->d_matches;
+  *h = c->d_hits;
+  *d = c->d_distinct;
+  *t = c->d_thresh;
+  *n_rules = c->n_rules;
+}
+void** rsa_internal_merge_slot(rsa_ctx* c) { return &c->merge_state; }
+uint64_t rsa_internal_route_rows(rsa_ctx* c) { return c->route_rows; }
 
 int rsa_sync(rsa_ctx* c) {
   if (!c) return RSA_ERR_ARG;

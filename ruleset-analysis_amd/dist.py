@@ -28,7 +28,19 @@ Then:
 At world 1 nothing moves: the merge is the single-GPU job.  The order keys
 are global, so the cap logic is shard-agnostic.  Records are 40-byte
 ``rsa_conn_record`` rows moved as uint8 tensors.
+
+On the GPU (``EngineBackend``) the whole sequence runs inside the library,
+behind one C-ABI call (``rsa_merge`` in ``csrc/merge.hip``): over RCCL
+(``rsa_merge_rccl``, the library's own communicator on the ctx's device) when
+the group's backend is ``nccl``, else over this group through host-buffer
+callbacks (``rsa_transport.host_buffers``; gloo, several ranks sharing one
+GPU).  Python only creates the communicator and copies the resulting rows into
+a torch tensor.  The Python protocol below (``merge(..., impl='python')``) is
+the same sequence step for step: the model the CPU tests run over numpy
+backends (tests/cpu_model.py), and a GPU cross-check of the library's.
 """
+
+import ctypes
 
 import numpy as np
 
@@ -196,6 +208,155 @@ def _overflow(e):
     return getattr(e, 'code', None) == ShardOverflow.code
 
 
+class _HostTransport(object):
+    """rsa_transport over a torch.distributed group with host buffers: the
+    library stages device data through pinned host memory and these callbacks
+    run the group's collectives on CPU tensors viewing that memory (gloo)."""
+
+    def __init__(self, dist, group, world, rank):
+        from . import native
+        self.dist, self.group, self.world = dist, group, world
+        self.error = None
+        self._ar = native.ALL_REDUCE_FN(self._all_reduce)
+        self._a2a = native.ALL_TO_ALLV_FN(self._all_to_allv)
+        self.t = native.Transport(None, world, rank, 1, self._ar, self._a2a)
+
+    def _all_reduce(self, _self, buf, n, op, _stream):
+        try:
+            import torch
+            t = torch.from_numpy(np.ctypeslib.as_array(buf, shape=(n,))) if n else torch.zeros(0, dtype=torch.int64)
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX if op else self.dist.ReduceOp.SUM, group=self.group)
+            return 0
+        except BaseException as e:  # noqa: BLE001 - reported by merge() after the call returns
+            self.error = e
+            return 1
+
+    def _all_to_allv(self, _self, send, sb, recv, rb, _stream):
+        try:
+            import torch
+            sbl = [int(sb[r]) for r in range(self.world)]
+            rbl = [int(rb[r]) for r in range(self.world)]
+
+            def view(addr, n):
+                if not n:
+                    return torch.zeros(0, dtype=torch.uint8)
+                return torch.from_numpy(np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(addr)))
+            self.dist.all_to_all_single(view(recv, sum(rbl)), view(send, sum(sbl)), rbl, sbl, group=self.group)
+            return 0
+        except BaseException as e:  # noqa: BLE001
+            self.error = e
+            return 1
+
+
+def rccl_comm(eng, dist, group, world, rank):
+    """The library's RCCL communicator for this engine and group (created once,
+    collectively: rank 0's unique id is broadcast over the group)."""
+    import torch
+    from . import native
+    key = (id(group), world, rank)
+    have = getattr(eng, '_rccl_comm', None)
+    if have is not None and have[0] == key:
+        return have[1]
+    lib = native.load()
+    uid = (ctypes.c_uint8 * 128)()
+    if rank == 0:
+        rc = lib.rsa_rccl_unique_id(uid)
+        if rc:
+            raise native.NativeError(rc, 'rsa_rccl_unique_id failed (RCCL not found?)')
+    t = torch.tensor(list(bytes(uid)), dtype=torch.uint8, device=eng.device)
+    dist.broadcast(t, 0, group=group)
+    uid = (ctypes.c_uint8 * 128)(*t.cpu().tolist())
+    comm = ctypes.c_void_p()
+    eng.ctx.call('rsa_rccl_comm_create', ctypes.c_int32(world), ctypes.c_int32(rank), uid, ctypes.byref(comm))
+    eng._rccl_comm = (key, comm)
+    return comm
+
+
+class _LibMerge(object):
+    """One rank's side of rsa_merge / rsa_gather (the library's protocol)."""
+
+    def __init__(self, eng, dist, group, world, rank, force_exchange=False):
+        from . import native
+        self.native, self.eng, self.world, self.rank = native, eng, world, rank
+        self.flags = native.RSA_MERGE_ALWAYS_EXCHANGE if force_exchange else 0
+        self.rccl = None
+        self.host = None
+        if dist is not None and world >= 1 and (world > 1 or force_exchange):
+            if not _host_staged(dist, group):
+                self.rccl = rccl_comm(eng, dist, group, world, rank)
+            else:
+                self.host = _HostTransport(dist, group, world, rank)
+        if self.host is None:
+            # world 1 without a group, or RCCL: the struct is only read for world/rank
+            self.t = native.Transport(None, world, rank, 1, native.ALL_REDUCE_FN(), native.ALL_TO_ALLV_FN())
+        else:
+            self.t = self.host.t
+
+    def _check(self, rc, what, info=None):
+        err = self.host.error if self.host is not None else None
+        if self.host is not None:
+            self.host.error = None
+        if err is not None:
+            raise err
+        if rc == self.native.RSA_ERR_CAPACITY:
+            msg = self.eng.ctx.lib.rsa_last_error(self.eng.ctx.h)
+            raise ShardOverflow('%s: %s' % (what, msg.decode() if msg else ''),
+                                needed=int(info.needed) if info is not None else 0)
+        self.eng.ctx.check(rc, what)
+
+    def merge(self, batches, gather, stats=None):
+        from .engine import _ptr
+        n = self.native
+        arr = (n.ShardBatch * max(len(batches), 1))()
+        for i, (b, g) in enumerate(batches):
+            gid = b.gids if b.gids is not None else g
+            arr[i] = n.ShardBatch(_ptr(b.tuples).value, _ptr(b.ts).value, _ptr(b.order).value, _ptr(gid).value, b.n)
+        info = n.MergeInfo()
+        flags = self.flags | (n.RSA_MERGE_GATHER if gather else 0)
+        lib, h = self.eng.ctx.lib, self.eng.ctx.h
+        if self.rccl is not None:
+            rc = lib.rsa_merge_rccl(h, self.rccl, arr, len(batches), flags, ctypes.byref(info))
+        else:
+            rc = lib.rsa_merge(h, ctypes.byref(self.t), arr, len(batches), flags, ctypes.byref(info))
+        self._check(rc, 'rsa_merge', info)
+        if stats is not None:
+            for ph in ('route1', 'route2'):
+                if ph == 'route1' or info.pass2:
+                    for k in ('sent', 'self', 'recv'):
+                        stats['%s_%s_rows' % (ph, k)] = int(getattr(info, '%s_%s' % (ph, k)))
+            stats['reexports'] = int(info.reexports)
+            if self.world > 1 or self.flags:
+                stats['allreduce_bytes'] = int(info.allreduce_bytes)
+                stats['pass2'] = bool(info.pass2)
+                stats['owner_rows'] = int(info.owner_rows)
+                stats['gather_rows_to_rank0'] = int(info.gather_rows)
+        return info
+
+    def gather(self):
+        info = self.native.MergeInfo()
+        lib, h = self.eng.ctx.lib, self.eng.ctx.h
+        if self.rccl is not None:
+            rc = lib.rsa_gather_rccl(h, self.rccl, ctypes.byref(info))
+        else:
+            rc = lib.rsa_gather(h, ctypes.byref(self.t), ctypes.byref(info))
+        self._check(rc, 'rsa_gather')
+        return info
+
+    def rows(self, which):
+        """The last merge's own rows (0) or gathered rows (1) as a uint8 tensor."""
+        import torch
+        from .engine import _ptr
+        nr = ctypes.c_uint64(0)
+        lib, h = self.eng.ctx.lib, self.eng.ctx.h
+        rc = lib.rsa_merge_rows(h, which, None, 0, ctypes.byref(nr))
+        if rc not in (self.native.RSA_OK, self.native.RSA_ERR_CAPACITY):
+            self.eng.ctx.check(rc, 'rsa_merge_rows')
+        out = torch.empty(int(nr.value) * REC, dtype=torch.uint8, device=self.eng.device)
+        if nr.value:
+            self.eng.ctx.call('rsa_merge_rows', which, _ptr(out), nr, ctypes.byref(nr))
+        return out
+
+
 class OwnerRows(object):
     """merge(..., gather=False): this rank's own rules' final rows -- the
     counterpart of one Hadoop reducer's part file (runAnalysis.sh:42-56 runs
@@ -203,15 +364,23 @@ class OwnerRows(object):
     -output directory) -- with the merged counters and every rank's row bytes.
     gather_rows() collects them on rank 0 as merge() would have."""
 
-    def __init__(self, final, sizes, matches, hits, distinct, thresh):
+    def __init__(self, final, sizes, matches, hits, distinct, thresh, lib=None):
         self.final, self.sizes = final, sizes
         self.matches, self.hits, self.distinct, self.thresh = matches, hits, distinct, thresh
+        self.lib = lib     # _LibMerge of the library's protocol: it gathers (rsa_gather)
 
 
 def gather_rows(part, dist, world, rank, group=None, to_host=True):
     """The owners' rows of merge(..., gather=False) on rank 0: merge()'s result
     there, None elsewhere."""
     import torch
+    if part.lib is not None:
+        part.lib.gather()
+        if rank != 0:
+            return None
+        recs = part.lib.rows(1)
+        out = (recs, part.matches, part.hits, part.distinct, part.thresh)
+        return merged_to_host(out) if to_host else out
     parts = _gather0(part.final, part.sizes, rank, world, dist, group) if world > 1 else [part.final]
     if rank != 0:
         return None
@@ -220,7 +389,8 @@ def gather_rows(part, dist, world, rank, group=None, to_host=True):
     return merged_to_host(out) if to_host else out
 
 
-def merge(backend, dist, world, rank, group=None, to_host=True, gather=True, stats=None):
+def merge(backend, dist, world, rank, group=None, to_host=True, gather=True, stats=None, impl=None,
+          force_exchange=False):
     """Run the protocol; returns (records, matches, hits, distinct, thresh) on
     rank 0 and None elsewhere: numpy arrays (records as RECORD_DTYPE rows), or
     with to_host=False the device tensors as they stand in rank 0's HBM
@@ -235,7 +405,16 @@ def merge(backend, dist, world, rank, group=None, to_host=True, gather=True, sta
     there is no collective and no extra read: the shard's own cap resolution
     says whether pass 2 runs, as in the single-GPU job.  ``stats`` (a dict)
     receives the rows each exchange moved (route_records) and the collective
-    bytes of the counter, threshold and size vectors."""
+    bytes of the counter, threshold and size vectors.
+
+    impl: 'lib' (the default for an EngineBackend) runs the protocol inside
+    the library (rsa_merge); 'python' runs it here (the default for the CPU
+    model backends).  force_exchange (lib): every collective runs even at
+    world 1 (RSA_MERGE_ALWAYS_EXCHANGE, a one-GPU check of the transport)."""
+    if impl is None:
+        impl = 'lib' if isinstance(backend, EngineBackend) else 'python'
+    if impl == 'lib':
+        return _merge_lib(backend, dist, world, rank, group, to_host, gather, stats, force_exchange)
     import torch
     tr = _Trace(rank)
     c = backend.counters()
@@ -344,6 +523,25 @@ def merge(backend, dist, world, rank, group=None, to_host=True, gather=True, sta
     if to_host:
         out = merged_to_host(out)
     tr('end', dev)
+    return out
+
+
+def _merge_lib(backend, dist, world, rank, group, to_host, gather, stats, force_exchange):
+    """merge() through rsa_merge: the library runs the whole sequence; the
+    counters it merged stay in the engine's bound tensors."""
+    eng = backend.eng
+    lm = _LibMerge(eng, dist, group, world, rank, force_exchange=force_exchange)
+    tr = _Trace(rank)
+    tr('start', eng.device)
+    lm.merge(list(zip(backend.batches, backend.gid_bufs)), gather=False, stats=stats)
+    tr('merge', eng.device)
+    c = eng.counters
+    part = OwnerRows(lm.rows(0), None, c['matches'], c['hits'], c['distinct'], c['thresh'], lib=lm)
+    if not gather:
+        tr('end', eng.device)
+        return part
+    out = gather_rows(part, dist, world, rank, group, to_host=to_host)
+    tr('end', eng.device)
     return out
 
 

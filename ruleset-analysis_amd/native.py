@@ -9,7 +9,8 @@ is no fallback: if the library or a symbol is missing, ``load()`` raises
 import ctypes
 import os
 
-__all__ = ['load', 'lib_path', 'NativeUnavailable', 'NativeError', 'SYMBOLS', 'Ctx']
+__all__ = ['load', 'lib_path', 'NativeUnavailable', 'NativeError', 'SYMBOLS', 'Ctx', 'Transport', 'ShardBatch',
+           'MergeInfo']
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _BUILD = os.path.join(_HERE, '_build')
@@ -41,6 +42,7 @@ RSA_OPT_HOT_SPLIT, RSA_OPT_HOT_MIN, RSA_OPT_PARSE_STAGED, RSA_OPT_REGION_IMPORT 
 RSA_OPT_COUNT_SORT, RSA_OPT_OWNER_WORLD, RSA_OPT_OWNER_RANK, RSA_OPT_MIN_REGIONS_LOG2 = 18, 19, 20, 21
 RSA_OPT_REGION_RECORDS, RSA_OPT_REDUCE_BIG, RSA_OPT_FILTER_GROWTH = 22, 23, 24
 RSA_OPT_COUNTER_WORDS16, RSA_OPT_CLASSIFY_PAIR = 26, 28
+RSA_OPT_ROUTE_ROWS = 29
 
 P = ctypes.c_void_p
 U32 = ctypes.c_uint32
@@ -48,6 +50,29 @@ U64 = ctypes.c_uint64
 I32 = ctypes.c_int
 PU32 = ctypes.POINTER(ctypes.c_uint32)
 PU64 = ctypes.POINTER(ctypes.c_uint64)
+
+RSA_MERGE_GATHER, RSA_MERGE_ALWAYS_EXCHANGE = 1, 2
+
+# rsa_transport callbacks: all_reduce_i64(self, buf, n, op, stream), all_to_allv(self, send, send_bytes, recv,
+# recv_bytes, stream)
+ALL_REDUCE_FN = ctypes.CFUNCTYPE(I32, P, ctypes.POINTER(ctypes.c_int64), U64, I32, P)
+ALL_TO_ALLV_FN = ctypes.CFUNCTYPE(I32, P, P, PU64, P, PU64, P)
+
+
+class Transport(ctypes.Structure):
+    _fields_ = [('self', P), ('world', ctypes.c_int32), ('rank', ctypes.c_int32), ('host_buffers', ctypes.c_int32),
+                ('all_reduce_i64', ALL_REDUCE_FN), ('all_to_allv', ALL_TO_ALLV_FN)]
+
+
+class ShardBatch(ctypes.Structure):
+    _fields_ = [('d_tuples', P), ('d_ts', P), ('d_order', P), ('d_gid', P), ('n', U64)]
+
+
+class MergeInfo(ctypes.Structure):
+    _fields_ = [('d_rows', P), ('n_rows', U64), ('owner_rows', U64), ('gather_rows', U64),
+                ('route1_sent', U64), ('route1_self', U64), ('route1_recv', U64),
+                ('route2_sent', U64), ('route2_self', U64), ('route2_recv', U64),
+                ('allreduce_bytes', U64), ('needed', U64), ('reexports', U32), ('pass2', U32)]
 
 # name -> (restype, argtypes); exactly the functions declared in include/ruleset_hip.h
 SYMBOLS = {
@@ -76,6 +101,14 @@ SYMBOLS = {
     'rsa_export': (I32, [P, I32, P, U64, PU64]),
     'rsa_export_routed': (I32, [P, I32, U32, P, U64, P]),
     'rsa_import': (I32, [P, I32, P, U64]),
+    'rsa_merge': (I32, [P, ctypes.POINTER(Transport), P, U32, I32, ctypes.POINTER(MergeInfo)]),
+    'rsa_gather': (I32, [P, ctypes.POINTER(Transport), ctypes.POINTER(MergeInfo)]),
+    'rsa_merge_rows': (I32, [P, I32, P, U64, PU64]),
+    'rsa_rccl_unique_id': (I32, [P]),
+    'rsa_rccl_comm_create': (I32, [P, ctypes.c_int32, ctypes.c_int32, P, ctypes.POINTER(P)]),
+    'rsa_rccl_comm_destroy': (I32, [P]),
+    'rsa_merge_rccl': (I32, [P, P, P, U32, I32, ctypes.POINTER(MergeInfo)]),
+    'rsa_gather_rccl': (I32, [P, P, ctypes.POINTER(MergeInfo)]),
     'rsa_shadowed': (I32, [P, P, U32, P]),
     'rsa_shadowed_ports': (I32, [P, P, U32, P, U32, P]),
     'rsa_text_count_lines': (I32, [P, P, U64, PU64]),

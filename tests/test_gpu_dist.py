@@ -1,7 +1,9 @@
 """The multi-GPU merge with the real HIP tables: two ranks on the box's one
 GPU (gloo, tensors staged through host memory; the bench uses RCCL), each
 classifying and aggregating its half of the log; rank 0's merged result must
-equal the C oracle over the whole log."""
+equal the C oracle over the whole log.  The merge runs inside the library
+(rsa_merge, csrc/merge.hip; impl 'lib', the product path) and, as a cross-check,
+as the Python protocol of dist.py over the same engines (impl 'python')."""
 import os
 
 import numpy as np
@@ -23,14 +25,21 @@ def _worker(rank, world, port, args, out_q):
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
-    dist.init_process_group('gloo', rank=rank, world_size=world)
+    opts = dict(args[5]) if len(args) > 5 else {}
+    backend = opts.pop('backend', 'gloo')
+    if backend == 'nccl':
+        torch.cuda.set_device(0)
+        dist.init_process_group('nccl', rank=rank, world_size=world, device_id=torch.device('cuda', 0))
+    else:
+        dist.init_process_group('gloo', rank=rank, world_size=world)
     from ruleset_analysis_amd.compile import CompiledRules
     from ruleset_analysis_amd.dist import EngineBackend, merge
     from ruleset_analysis_amd.engine import DeviceBatch, Engine
     from ruleset_analysis_amd.pipeline import built_hit_count
     seed, n_rules, n_lines, cap, zipf = args[:5]
-    opts = dict(args[5]) if len(args) > 5 else {}
     route_cap = opts.pop('route_cap', None)
+    impl = opts.pop('impl', 'lib')
+    force = opts.pop('force_exchange', False)
     dbj, info = synth.make_db(seed, n_rules)
     tr = synth.make_traffic((dbj, info), n_lines, seed=seed + 1, zipf=zipf)
     compiled = CompiledRules(acldb.load_json(dbj))
@@ -50,12 +59,24 @@ def _worker(rank, world, port, args, out_q):
     if route_cap is not None:
         # every export first lands in a buffer of route_cap rows: the library
         # drops the rows past it and the exchange exports again at the exact
-        # size (dist.route_records -> Exported.again)
-        orig = local.export_routed
-        local.export_routed = lambda mode, world, capacity=None: orig(mode, world, capacity=capacity or route_cap)
-        local._route_buf, local._route_cap = None, 0
+        # size (rsa_merge: RSA_OPT_ROUTE_ROWS; the Python protocol:
+        # dist.route_records -> Exported.again)
+        if impl == 'lib':
+            local.set_option(native.RSA_OPT_ROUTE_ROWS, route_cap)
+        else:
+            orig = local.export_routed
+            local.export_routed = lambda mode, world, capacity=None: orig(mode, world, capacity=capacity or route_cap)
+            local._route_buf, local._route_cap = None, 0
     stats = {}
-    out = merge(EngineBackend(local, [batch], [g], cap), dist, world, rank, stats=stats)
+    out = merge(EngineBackend(local, [batch], [g], cap), dist, world, rank, stats=stats, impl=impl,
+                force_exchange=force)
+    if force:
+        # the same job on the single-GPU path: the forced exchange must not change it
+        single = local.run([batch], cap, max(built_hit_count(tup[a:b]), 1))
+        assert np.array_equal(single.matches, out[1]) and np.array_equal(single.hits, out[2])
+        key = lambda r: sorted(map(tuple, r.view(np.uint8).reshape(len(r), -1).tolist()))  # noqa: E731
+        assert key(single.records) == key(out[0])
+        assert stats['allreduce_bytes'] > 0, stats
     if route_cap is not None:
         assert stats.get('reexports', 0) >= 1, stats
     if rank == 0:
@@ -111,11 +132,24 @@ def _check(out, R, cols, ots, oorder, cap):
     return ref
 
 
-@pytest.mark.parametrize('cap', [12, 1000])
-def test_two_ranks_one_gpu(cap):
-    args = (61, 700, 120000, cap, 1.2)
+@pytest.mark.parametrize('cap,impl', [(12, 'lib'), (1000, 'lib'), (12, 'python')])
+def test_two_ranks_one_gpu(cap, impl):
+    args = (61, 700, 120000, cap, 1.2, {'impl': impl})
     out = _run_two_ranks(args)
     _check(out, *_oracle_inputs(61, 700, 120000, 1.2), cap)
+
+
+@pytest.mark.parametrize('backend', ['nccl', 'gloo'])
+def test_one_rank_forced_exchange(backend):
+    """rsa_merge with RSA_MERGE_ALWAYS_EXCHANGE at world 1: every collective
+    runs over the transport anyway -- over RCCL (rsa_merge_rccl: the library's
+    own communicator, all_reduce and grouped send/recv to itself, the gathered
+    rows included) or the host-buffer callbacks (gloo).  The result must equal
+    the single-GPU job and the C oracle (the box has one GPU: RCCL refuses two
+    ranks on one device, so this is where the RCCL transport runs here)."""
+    args = (61, 700, 120000, 12, 1.2, {'backend': backend, 'force_exchange': True})
+    out = _run_two_ranks(args, world=1)
+    _check(out, *_oracle_inputs(61, 700, 120000, 1.2), 12)
 
 
 def test_four_ranks_one_gpu():
@@ -137,13 +171,14 @@ def test_two_ranks_atomic_import():
     _check(out, *_oracle_inputs(61, 700, 120000, 1.2), 12)
 
 
-def test_two_ranks_export_overflow_reexport():
+@pytest.mark.parametrize('impl', ['lib', 'python'])
+def test_two_ranks_export_overflow_reexport(impl):
     """The exports of both exchanges overflow a 1-row first buffer: the
-    library drops the rows past it and reports the true per-owner counts,
-    route_records exports again at the exact size (reallocating the engine's
-    route buffer after the counts were exchanged) -- the result must still be
-    the C oracle's."""
-    out = _run_two_ranks((61, 700, 120000, 12, 1.2, {'route_cap': 1}))
+    library drops the rows past it and reports the true per-owner counts, the
+    exchange exports again at the exact size (reallocating the route buffer
+    after the counts were exchanged) -- the result must still be the C
+    oracle's."""
+    out = _run_two_ranks((61, 700, 120000, 12, 1.2, {'route_cap': 1, 'impl': impl}))
     _check(out, *_oracle_inputs(61, 700, 120000, 1.2), 12)
 
 

@@ -62,10 +62,35 @@ def test_header_constants_equal_binding():
     with open(os.path.join(ROOT, 'include', 'ruleset_hip.h')) as f:
         text = f.read()
     defs = {m.group(1): int(m.group(2), 0) for m in
-            re.finditer(r'^#define\s+(RSA_(?:OPT|ERR|LINE|F|RED)_[A-Z0-9_]+)\s+\(?(-?(?:0x)?[0-9A-Fa-f]+)u?\)?', text,
+            re.finditer(r'^#define\s+(RSA_(?:OPT|ERR|LINE|F|RED|MERGE)_[A-Z0-9_]+)\s+\(?(-?(?:0x)?[0-9A-Fa-f]+)u?\)?', text,
                         re.M)}
     bound = {k: getattr(native, k) for k in dir(native) if k in defs}
     assert len(bound) >= 20
     for k, v in bound.items():
         assert v == defs[k], k
-    assert {'RSA_OPT_COUNT_SORT', 'RSA_OPT_OWNER_WORLD', 'RSA_OPT_OWNER_RANK'} <= set(bound)
+    assert {'RSA_OPT_COUNT_SORT', 'RSA_OPT_OWNER_WORLD', 'RSA_OPT_OWNER_RANK', 'RSA_MERGE_GATHER',
+            'RSA_MERGE_ALWAYS_EXCHANGE'} <= set(bound)
+
+
+def test_merge_struct_layouts_equal_header(tmp_path):
+    """The ctypes mirrors of rsa_transport, rsa_shard_batch and rsa_merge_info
+    have the header's sizes and field offsets (gcc on the header itself)."""
+    import subprocess
+    structs = [('rsa_transport', native.Transport), ('rsa_shard_batch', native.ShardBatch),
+               ('rsa_merge_info', native.MergeInfo)]
+    lines = ['#include <stddef.h>', '#include <stdio.h>', '#include "ruleset_hip.h"', 'int main(void) {']
+    for cname, cls in structs:
+        lines.append('printf("%%zu\\n", sizeof(%s));' % cname)
+        for f, _t in cls._fields_:
+            lines.append('printf("%%zu\\n", offsetof(%s, %s));' % (cname, f))
+    lines.append('return 0; }')
+    src = tmp_path / 'layout.c'
+    src.write_text('\n'.join(lines) + '\n')
+    exe = tmp_path / 'layout'
+    subprocess.run(['gcc', '-I', os.path.join(ROOT, 'include'), '-o', str(exe), str(src)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    want = []
+    for _cname, cls in structs:
+        want.append(ctypes.sizeof(cls))
+        want.extend(getattr(cls, f).offset for f, _t in cls._fields_)
+    assert got == want
