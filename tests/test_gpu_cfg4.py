@@ -83,6 +83,35 @@ def test_cfg4_bucket_two_lines_per_lane(engine, cfg4, pair, defer, n):
         engine.set_option(native.RSA_OPT_FORCE_DEFER, 0)
 
 
+def test_cfg4_sampled_lines_at_4m(engine, cfg4):
+    """4M lines of config 4 through the fused job (bucket index, cap 1000):
+    the first match of 16K lines drawn uniformly from the whole batch equals
+    the C oracle's scan of the expanded rules (a line's first match does not
+    depend on the others), and the per-rule line and hit counters equal the
+    histograms of the job's own gids (every line)."""
+    text, info, db, comp, R = cfg4
+    n = 4_000_000
+    tr = synth_fg.make_traffic(info, n, seed=46)
+    tup, ts, order = synth.pack(tr, comp)
+    engine.load_compiled(comp)
+    b = DeviceBatch.from_numpy(tup, ts, order, engine.device)
+    res = engine.run([b], 1000, capacity=max(built_hit_count(tup), 1))
+    gids = engine.last_gids[0].cpu().numpy()
+    pick = np.sort(np.random.default_rng(7).choice(n, 16384, replace=False))
+    sub = {k: (np.asarray(v)[pick] if isinstance(v, np.ndarray) and len(v) == n else v) for k, v in tr.items()}
+    cols, _ts, _order = coracle.inputs_from_traffic(R, sub)
+    g_ref, _evals = coracle.classify(R, cols['list'], cols['proto'], cols['src'], cols['dst'], cols['sport'],
+                                     cols['dport'])
+    assert np.array_equal(gids[pick], g_ref)
+    ok = gids >= 0
+    hit = ok & ((tup['flags'] & 2) != 0)
+    assert np.array_equal(res.matches[:comp.n_rules].astype(np.int64),
+                          np.bincount(gids[ok], minlength=comp.n_rules)[:comp.n_rules])
+    assert np.array_equal(res.hits[:comp.n_rules].astype(np.int64),
+                          np.bincount(gids[hit], minlength=comp.n_rules)[:comp.n_rules])
+    assert (g_ref >= 0).mean() > 0.3
+
+
 def test_cfg4_parity_linear_scan(engine, cfg4):
     text, info, db, comp, R = cfg4
     _job_vs_oracle(engine, text, info, comp, R, 6000, seed=43, cap=1000, index=False)
