@@ -397,7 +397,8 @@ def test_gpu_text_split_one_pass(engine):
     rng = random.Random(5)
     for data in (b'', b'x', b'\n', b'a\nb', b'a\nb\n',
                  b''.join(bytes(rng.randrange(32, 127) for _ in range(rng.randrange(0, 300))) + b'\n'
-                          for _ in range(20000)) + b'tail without newline'):
+                          for _ in range(20000)) + b'tail without newline',
+                 b'\n' * (3 * 65536 + 77)):   # every byte a line end: each 16-KiB round's count at its maximum
         lines = data.split(b'\n')
         n = len(lines) - (1 if data.endswith(b'\n') or not data else 0)
         want = np.cumsum([0] + [len(l) + 1 for l in lines[:n]])
