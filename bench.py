@@ -681,7 +681,7 @@ def rank_main(args, rank, world, local):
     phase_prof = os.environ.get('RSA_PHASE_PROF') == '1'   # PROFILING: a -DRSA_PHASE_PROF library variant
     if phase_prof:
         import ctypes
-        ph = (ctypes.c_uint64 * 17)()
+        ph = (ctypes.c_uint64 * 25)()
         eng.ctx.call('rsa_phase_prof', ph, ctypes.c_int(1))
     if dist is not None:
         dist.barrier()
@@ -697,11 +697,12 @@ def rank_main(args, rank, world, local):
         names = ['tuple+list', 'prefix', 'pruning', 'group0', 'tasks', 'verify', 'resid+chain', 'emit']
         log('phase_prof cycles/wave-iteration: ' + json.dumps(
             {nm: round(v[k] / max(v[8], 1), 1) for k, nm in enumerate(names)}) + ' iterations %d' % v[8])
-        log('phase_prof k_reduce<1> cycles/workgroup: ' + json.dumps(
-            {nm: round(v[9 + k] / max(v[12], 1), 1) for k, nm in enumerate(('setup', 'insert', 'flush'))}) +
-            ' workgroups %d; inside: ' % v[12] + json.dumps(
-                {nm: round(v[13 + k] / max(v[12], 1), 1) for k, nm in enumerate(('record_load_wait', 'lds_insert',
-                                                                                 'flush_claims', 'flush_writes'))}))
+        for name, b in (('k_reduce<1>', 9), ('k_reduce<2>', 17)):
+            log('phase_prof %s cycles/workgroup: ' % name + json.dumps(
+                {nm: round(v[b + k] / max(v[b + 3], 1), 1) for k, nm in enumerate(('setup', 'insert', 'flush'))}) +
+                ' workgroups %d; inside: ' % v[b + 3] + json.dumps(
+                    {nm: round(v[b + 4 + k] / max(v[b + 3], 1), 1) for k, nm in
+                     enumerate(('record_load_wait', 'lds_insert', 'flush_claims', 'flush_writes'))}))
     if dist is not None:
         dist.barrier()
     dt = time.perf_counter() - t0

@@ -300,8 +300,9 @@ struct PhaseAcc {
 // [0..7] classifier phases, [8] its wave iterations; [9..11] k_reduce<1>
 // workgroup cycles in setup, record inserts and flushes, [12] its workgroups;
 // [13..16] inside them: waiting for the record loads, LDS inserts, the flush
-// up to the claims, the flush's scan and slot writes
-constexpr int kPhaseWords = 17;
+// up to the claims, the flush's scan and slot writes; [17..24] the same for
+// k_reduce<2> (the recount)
+constexpr int kPhaseWords = 25;
 __device__ unsigned long long g_phase[kPhaseWords];
 #define RSA_PH_PARAM , PhaseAcc& ph
 #define RSA_PH_ARG , ph
@@ -2649,10 +2650,11 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(kPass == 2
   if (kPass == 1)
     for (uint32_t w = threadIdx.x; w < words; w += blockDim.x) gocc[w] = occ[w];
 #ifdef RSA_PHASE_PROF
-  if (kPass == 1 && threadIdx.x == 0) {
-    for (int k = 0; k < 3; ++k) atomicAdd(&g_phase[9 + k], rp_acc[k]);
-    atomicAdd(&g_phase[12], 1ull);
-    for (int k = 0; k < 4; ++k) atomicAdd(&g_phase[13 + k], rq_acc[k]);
+  if (threadIdx.x == 0) {
+    constexpr int b = kPass == 1 ? 9 : 17;
+    for (int k = 0; k < 3; ++k) atomicAdd(&g_phase[b + k], rp_acc[k]);
+    atomicAdd(&g_phase[b + 3], 1ull);
+    for (int k = 0; k < 4; ++k) atomicAdd(&g_phase[b + 4 + k], rq_acc[k]);
   }
 #endif
 #undef RP
