@@ -248,6 +248,28 @@ class _HostTransport(object):
             return 1
 
 
+class _LoopbackTransport(object):
+    """World 1 without a process group (merge(..., dist=None,
+    force_exchange=True)): every collective over the library's pinned host
+    buffers is an identity -- the all_reduce leaves the vector, the
+    all_to_allv copies this rank's one segment to itself."""
+
+    def __init__(self):
+        from . import native
+        self.error = None
+        self._ar = native.ALL_REDUCE_FN(lambda _s, _buf, _n, _op, _st: 0)
+        self._a2a = native.ALL_TO_ALLV_FN(self._copy)
+        self.t = native.Transport(None, 1, 0, 1, self._ar, self._a2a)
+
+    def _copy(self, _self, send, sb, recv, rb, _stream):
+        n = int(sb[0])
+        if n != int(rb[0]):
+            return 1
+        if n:
+            ctypes.memmove(recv, send, n)
+        return 0
+
+
 def rccl_comm(eng, dist, group, world, rank):
     """The library's RCCL communicator for this engine and group (created once,
     collectively: rank 0's unique id is broadcast over the group)."""
@@ -286,6 +308,8 @@ class _LibMerge(object):
                 self.rccl = rccl_comm(eng, dist, group, world, rank)
             else:
                 self.host = _HostTransport(dist, group, world, rank)
+        elif dist is None and world == 1 and force_exchange:
+            self.host = _LoopbackTransport()
         if self.host is None:
             # world 1 without a group, or RCCL: the struct is only read for world/rank
             self.t = native.Transport(None, world, rank, 1, native.ALL_REDUCE_FN(), native.ALL_TO_ALLV_FN())

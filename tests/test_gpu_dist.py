@@ -273,3 +273,30 @@ def test_bench_two_ranks_share_gpu_checks(tmp_path):
     mx = line['merge_exchange']
     assert mx['route1_sent_bytes_total'] > 0 and mx['route1_sent_bytes_total'] == mx['route1_recv_bytes_total']
     check_dump_against_oracle(got, 2, rules, lines, cap)
+
+
+def test_loopback_forced_exchange_in_process(engine):
+    """rsa_merge at world 1 without a process group: every collective forced
+    through the loopback transport (identity all_reduce, self copy) -- the
+    records, counters and capped set equal the C oracle's."""
+    from ruleset_analysis_amd.compile import CompiledRules
+    from ruleset_analysis_amd.dist import EngineBackend, merge
+    from ruleset_analysis_amd.engine import DeviceBatch
+    from ruleset_analysis_amd.pipeline import built_hit_count
+    import torch
+    seed, n_rules, n_lines, cap = 63, 600, 90000, 15
+    dbj, info = synth.make_db(seed, n_rules)
+    tr = synth.make_traffic((dbj, info), n_lines, seed=seed + 1, zipf=1.2)
+    compiled = CompiledRules(acldb.load_json(dbj))
+    compiled.ensure_lists()
+    tup, ts, order = synth.pack(tr, compiled)
+    engine.load_compiled(compiled)
+    b = DeviceBatch.from_numpy(tup, ts, order, engine.device)
+    g = torch.empty(b.n, dtype=torch.int32, device=engine.device)
+    for _ in range(2):   # twice: the second merge reuses the library's buffers
+        engine.reset(max(built_hit_count(tup), 1), cap)
+        engine.pass1(b, g)
+        stats = {}
+        out = merge(EngineBackend(engine, [b], [g], cap), None, 1, 0, force_exchange=True, stats=stats)
+        ref = _check(out, *_oracle_inputs(seed, n_rules, n_lines, 1.2), cap)
+        assert stats['allreduce_bytes'] > 0 and stats['pass2'] == bool((ref['n_conns'] >= cap).any())
