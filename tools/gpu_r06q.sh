@@ -1,0 +1,13 @@
+#!/bin/bash
+# Cap scatter with one reservation per 4-chunk span (re-read pass): GPU parity
+# tests, then a same-box A/B against the per-chunk form (HEAD) and span 1.
+set -o pipefail
+OUT=gpurun_out/${1:-r06q}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_sampled.py tests/test_gpu_cfg4.py -x -q --timeout 600 --timeout-method thread > "$OUT/parity.log" 2>&1 || { tail -40 "$OUT/parity.log"; exit 1; }
+tail -2 "$OUT/parity.log"
+V=ruleset-analysis_amd/_build
+bash tools/ab_bench.sh "$OUT/cfg3" $V/libruleset_hip.so $V/var/libruleset_hip_capold.so $V/var/libruleset_hip_capsuper1.so || exit 1
+bash tools/ab_bench.sh "$OUT/cfg5" $V/libruleset_hip.so $V/var/libruleset_hip_capold.so -- --config cfg5 || exit 1
+echo done
