@@ -300,3 +300,64 @@ def test_loopback_forced_exchange_in_process(engine):
         out = merge(EngineBackend(engine, [b], [g], cap), None, 1, 0, force_exchange=True, stats=stats)
         ref = _check(out, *_oracle_inputs(seed, n_rules, n_lines, 1.2), cap)
         assert stats['allreduce_bytes'] > 0 and stats['pass2'] == bool((ref['n_conns'] >= cap).any())
+
+
+def test_three_ranks_one_gpu_uneven_owners():
+    """Three ranks sharing the GPU (owners gid % 3: uneven rule shares and
+    shard sizes from a 3-way split) through rsa_merge, cap engaged."""
+    args = (73, 701, 150001, 12, 1.2)
+    out = _run_two_ranks(args, world=3)
+    _check(out, *_oracle_inputs(73, 701, 150001, 1.2), 12)
+
+
+def test_merge_abi_errors(engine):
+    """The merge entry points' error behaviour through the C ABI: a transport
+    with an out-of-range world or rank, missing callbacks at world 2, unknown
+    flags, rsa_gather / rsa_merge_rows before any merge, and rows that do not
+    fit the caller's buffer (RSA_ERR_CAPACITY with the count)."""
+    import ctypes
+    import torch
+    from ruleset_analysis_amd import native
+    from ruleset_analysis_amd.compile import CompiledRules
+    from ruleset_analysis_amd.engine import DeviceBatch
+    from ruleset_analysis_amd.pipeline import built_hit_count
+    lib, h = engine.ctx.lib, engine.ctx.h
+    dbj, info = synth.make_db(5, 200)
+    tr = synth.make_traffic((dbj, info), 20000, seed=6)
+    compiled = CompiledRules(acldb.load_json(dbj))
+    compiled.ensure_lists()
+    tup, ts, order = synth.pack(tr, compiled)
+    engine.load_compiled(compiled)
+    b = DeviceBatch.from_numpy(tup, ts, order, engine.device)
+    g = torch.empty(b.n, dtype=torch.int32, device=engine.device)
+    engine.reset(max(built_hit_count(tup), 1), 10)
+    engine.pass1(b, g)
+    info_ = native.MergeInfo()
+    nores = native.ALL_REDUCE_FN(), native.ALL_TO_ALLV_FN()
+    rows = ctypes.c_uint64(0)
+    # a fresh context: nothing merged yet
+    fresh = native.Ctx(0)
+    assert lib.rsa_merge_rows(fresh.h, 0, None, 0, ctypes.byref(rows)) == native.RSA_ERR_STATE
+    t1 = native.Transport(None, 1, 0, 1, *nores)
+    assert lib.rsa_gather(fresh.h, ctypes.byref(t1), ctypes.byref(info_)) == native.RSA_ERR_STATE
+    fresh.close()
+    for world, rank in ((0, 0), (2, 2), (257, 0), (2, -1)):
+        t = native.Transport(None, world, rank, 1, *nores)
+        assert lib.rsa_merge(h, ctypes.byref(t), None, 0, 0, ctypes.byref(info_)) == native.RSA_ERR_ARG
+    t2 = native.Transport(None, 2, 0, 1, *nores)
+    assert lib.rsa_merge(h, ctypes.byref(t2), None, 0, 0, ctypes.byref(info_)) == native.RSA_ERR_ARG
+    assert lib.rsa_merge(h, ctypes.byref(t1), None, 0, 8, ctypes.byref(info_)) == native.RSA_ERR_ARG
+    # world 1 without collectives: the single-GPU job; its rows through rsa_merge_rows
+    sb = native.ShardBatch(b.tuples.data_ptr(), b.ts.data_ptr(), b.order.data_ptr(), g.data_ptr(), b.n)
+    assert lib.rsa_merge(h, ctypes.byref(t1), ctypes.byref(sb), 1, native.RSA_MERGE_GATHER,
+                         ctypes.byref(info_)) == 0
+    n = int(info_.n_rows)
+    assert n > 1 and info_.owner_rows == n and info_.gather_rows == 0
+    small = torch.empty((n - 1) * 40, dtype=torch.uint8, device=engine.device)
+    assert lib.rsa_merge_rows(h, 1, ctypes.c_void_p(small.data_ptr()), n - 1, ctypes.byref(rows)) == \
+        native.RSA_ERR_CAPACITY and rows.value == n
+    full = torch.empty(n * 40, dtype=torch.uint8, device=engine.device)
+    assert lib.rsa_merge_rows(h, 0, ctypes.c_void_p(full.data_ptr()), n, ctypes.byref(rows)) == 0
+    res = engine.run([b], 10, capacity=max(built_hit_count(tup), 1))
+    got = sorted(map(bytes, full.cpu().numpy().reshape(n, 40)))
+    assert got == sorted(map(bytes, res.records.view(np.uint8).reshape(-1, 40)))
