@@ -48,6 +48,21 @@ def _worker(rank, world, port, payload, out_q):
 
 
 def _free_port():
+    """A free port for a rendezvous store, drawn below the kernel's ephemeral
+    range (32768-60999): a port bind(0) hands out can be taken again by a
+    client socket of an earlier process group before the store binds it."""
+    import random
+    rng = random.Random()
+    for _ in range(200):
+        p = rng.randrange(20000, 32000)
+        s = socket.socket()
+        try:
+            s.bind(('127.0.0.1', p))
+        except OSError:
+            continue
+        finally:
+            s.close()
+        return p
     s = socket.socket()
     s.bind(('127.0.0.1', 0))
     p = s.getsockname()[1]
