@@ -2018,6 +2018,9 @@ __global__ __launch_bounds__(1024) void k_aggregate(const uint4* __restrict__ T,
 // tile]) so that its exclusive scan gives every (region, tile) run its output
 // offset.
 constexpr uint32_t kPartTileMin = 8192, kPartTileMax = 262144, kPartTilesWant = 384;
+#ifndef RSA_PART_TILES_CU
+#define RSA_PART_TILES_CU 1   // region sort tiles: two per CU (else the power-of-two tiles for >= 384 workgroups)
+#endif
 
 // Both partition kernels walk their tile as groups of kPartW windows per wave:
 // the group's window counts are wave-uniform (scalar) loads, and the live
@@ -4224,8 +4227,16 @@ int launch_aggregate(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsig
   }
   Rec* sorted = reinterpret_cast<Rec*>(c->d_recs2) + seg_base;
   const uint32_t n_regions = 1u << c->np_bits;
+#if RSA_PART_TILES_CU
+  // tiles: two per CU (every CU holds two 1024-thread scatter workgroups), in
+  // multiples of kPartTileMin lines, at most kPartTileMax
+  const unsigned long long want = (unsigned long long)c->cu_count * 2;
+  unsigned long long tl = ((m + want - 1) / want + kPartTileMin - 1) / kPartTileMin * kPartTileMin;
+  const uint32_t tile_len = (uint32_t)(tl < kPartTileMin ? kPartTileMin : tl > kPartTileMax ? kPartTileMax : tl);
+#else
   uint32_t tile_len = kPartTileMin;
   while (tile_len < kPartTileMax && (unsigned long long)tile_len * 2 * kPartTilesWant <= m) tile_len <<= 1;
+#endif
   const uint32_t n_tiles = (uint32_t)((m + tile_len - 1) / tile_len);
   const unsigned long long hl = (unsigned long long)n_regions * n_tiles;
   rc = ensure_buf(c, &c->d_hist, &c->hist_alloc, hl);
