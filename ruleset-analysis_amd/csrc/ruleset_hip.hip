@@ -2017,9 +2017,13 @@ __global__ __launch_bounds__(1024) void k_aggregate(const uint4* __restrict__ T,
 // runs per region stay ~10 records); the histogram matrix is region-major (hist[region * n_tiles +
 // tile]) so that its exclusive scan gives every (region, tile) run its output
 // offset.
-constexpr uint32_t kPartTileMin = 8192, kPartTileMax = 262144, kPartTilesWant = 384;
+constexpr uint32_t kPartTileMin = 8192, kPartTileMax = 262144;
+[[maybe_unused]] constexpr uint32_t kPartTilesWant = 384;   // (RSA_PART_TILES_CU=0: the power-of-two tiles)
 #ifndef RSA_PART_TILES_CU
-#define RSA_PART_TILES_CU 1   // region sort tiles: two per CU (else the power-of-two tiles for >= 384 workgroups)
+#define RSA_PART_TILES_CU 1   // region sort tiles: RSA_PART_TPC per CU (else the power-of-two tiles for >= 384 workgroups)
+#endif
+#ifndef RSA_PART_TPC
+#define RSA_PART_TPC 2        // tiles per CU (the scatter holds two 1024-thread workgroups per CU)
 #endif
 
 // Both partition kernels walk their tile as groups of kPartW windows per wave:
@@ -4132,12 +4136,29 @@ int prepare_records(rsa_ctx* c, uint64_t m) {
   return rc;
 }
 
+// Tile length (lines) of the tiled counting sorts (the region sort of the
+// records, the rule-block sort of the counter words) over m lines: the tiles
+// are dealt to the CUs evenly -- RSA_PART_TPC workgroups per CU, in multiples
+// of kPartTileMin lines, at most kPartTileMax (power-of-two tiles for >= 384
+// workgroups left a third of the CUs with one scatter workgroup more than the
+// rest: -0.2 to -0.3 ms/step, profiles/r06/ab_part_tiles_per_cu.txt)
+uint32_t part_tile_len(const rsa_ctx* c, uint64_t m) {
+#if RSA_PART_TILES_CU
+  const unsigned long long want = (unsigned long long)c->cu_count * RSA_PART_TPC;
+  const unsigned long long tl = ((m + want - 1) / want + kPartTileMin - 1) / kPartTileMin * kPartTileMin;
+  return (uint32_t)(tl < kPartTileMin ? kPartTileMin : tl > kPartTileMax ? kPartTileMax : tl);
+#else
+  uint32_t tile_len = kPartTileMin;
+  while (tile_len < kPartTileMax && (unsigned long long)tile_len * 2 * kPartTilesWant <= m) tile_len <<= 1;
+  return tile_len;
+#endif
+}
+
 // Per-rule counters of m gid|hit words by rule block (rule sets > kCnt, at
 // most kMaxRegions blocks): see k_cnt_hist.
 int count_by_block(rsa_ctx* c, const uint32_t* gh, uint64_t m) {
   const uint32_t n_blocks = (c->n_rules + kCntBlock - 1) >> kCntBits;
-  uint32_t tile_len = kPartTileMin;
-  while (tile_len < kPartTileMax && (unsigned long long)tile_len * 2 * kPartTilesWant <= m) tile_len <<= 1;
+  const uint32_t tile_len = part_tile_len(c, m);
   const uint32_t n_tiles = (uint32_t)((m + tile_len - 1) / tile_len);
   const unsigned long long hl = (unsigned long long)n_blocks * n_tiles;
   const unsigned long long max_tasks = m / kCntChunk + n_blocks + 1;
@@ -4227,16 +4248,7 @@ int launch_aggregate(rsa_ctx* c, const uint4* t, const uint32_t* ts, const unsig
   }
   Rec* sorted = reinterpret_cast<Rec*>(c->d_recs2) + seg_base;
   const uint32_t n_regions = 1u << c->np_bits;
-#if RSA_PART_TILES_CU
-  // tiles: two per CU (every CU holds two 1024-thread scatter workgroups), in
-  // multiples of kPartTileMin lines, at most kPartTileMax
-  const unsigned long long want = (unsigned long long)c->cu_count * 2;
-  unsigned long long tl = ((m + want - 1) / want + kPartTileMin - 1) / kPartTileMin * kPartTileMin;
-  const uint32_t tile_len = (uint32_t)(tl < kPartTileMin ? kPartTileMin : tl > kPartTileMax ? kPartTileMax : tl);
-#else
-  uint32_t tile_len = kPartTileMin;
-  while (tile_len < kPartTileMax && (unsigned long long)tile_len * 2 * kPartTilesWant <= m) tile_len <<= 1;
-#endif
+  const uint32_t tile_len = part_tile_len(c, m);
   const uint32_t n_tiles = (uint32_t)((m + tile_len - 1) / tile_len);
   const unsigned long long hl = (unsigned long long)n_regions * n_tiles;
   rc = ensure_buf(c, &c->d_hist, &c->hist_alloc, hl);
